@@ -1,0 +1,128 @@
+"""ctypes mirror of `include/brax_amd.h` (structs only, no library loading).
+
+`make_desc` / `make_reset_desc` turn the compiler's numpy descriptor into the
+C structs; the returned keep-alive list must outlive every call that reads the
+struct (create copies it to the device, so only the create call needs it).
+"""
+import ctypes as C
+
+import numpy as np
+
+i32p = C.POINTER(C.c_int32)
+f64p = C.POINTER(C.c_double)
+f32p = C.POINTER(C.c_float)
+
+_DESC_FIELDS = [
+    ('n_bodies', C.c_int32), ('n_joints', C.c_int32), ('n_actuators', C.c_int32),
+    ('n_rows', C.c_int32), ('n_groups', C.c_int32),
+    ('substeps', C.c_int32), ('action_size', C.c_int32), ('num_joint_dof', C.c_int32),
+    ('dt', C.c_double), ('h', C.c_double), ('gravity', C.c_double * 3),
+    ('velocity_damping', C.c_double), ('angular_damping', C.c_double),
+    ('body_mass', f64p), ('body_inv_inertia', f64p), ('pos_mask', f64p),
+    ('rot_mask', f64p), ('quat_mask', f64p),
+    ('joint_type', i32p), ('joint_dof', i32p), ('joint_free_dofs', i32p),
+    ('joint_body_p', i32p), ('joint_body_c', i32p), ('joint_group', i32p),
+    ('joint_off_p', f64p), ('joint_off_c', f64p), ('joint_axis_p', f64p),
+    ('joint_axis_c', f64p), ('joint_limit', f64p), ('joint_damping', f64p),
+    ('joint_scale_pos', f64p), ('joint_scale_ang', f64p),
+    ('act_type', i32p), ('act_joint', i32p), ('act_index', i32p),
+    ('act_group', i32p), ('act_strength', f64p),
+    ('col_oneway', i32p), ('col_fn', i32p), ('col_scale', f64p),
+    ('col_velocity_threshold', f64p), ('col_baumgarte_erp', f64p),
+    ('row_group', i32p), ('row_body_a', i32p), ('row_body_b', i32p),
+    ('row_a_pos', f64p), ('row_a_end', f64p), ('row_a_radius', f64p),
+    ('row_b_pos', f64p), ('row_b_end', f64p), ('row_b_radius', f64p),
+    ('row_friction', f64p), ('row_elasticity', f64p),
+]
+
+
+class BxDesc(C.Structure):
+  _fields_ = _DESC_FIELDS
+
+
+class BxResetDesc(C.Structure):
+  _fields_ = [
+      ('n_fk', C.c_int32), ('fk_body_p', i32p), ('fk_body_c', i32p),
+      ('fk_dof_index', i32p), ('fk_rot', f64p), ('fk_ref', f64p),
+      ('fk_off_p', f64p), ('fk_off_c', f64p), ('base_qp', f64p),
+      ('n_zpts', C.c_int32), ('zpt_body', i32p), ('zpt_local', f64p),
+      ('zpt_radius', f64p), ('body_zero_cand', i32p), ('body_root_group', i32p),
+      ('n_root_groups', C.c_int32),
+  ]
+
+
+class BxField(C.Structure):
+  _fields_ = [('ptr', C.c_void_p), ('env_stride', C.c_int64),
+              ('body_stride', C.c_int64)]
+
+
+class BxQP(C.Structure):
+  _fields_ = [('pos', BxField), ('rot', BxField), ('vel', BxField),
+              ('ang', BxField)]
+
+
+class BxInfo(C.Structure):
+  _fields_ = [('contact_vel', BxField), ('contact_ang', BxField),
+              ('actuator_vel', BxField), ('actuator_ang', BxField),
+              ('contact_pos', C.c_void_p), ('contact_normal', C.c_void_p),
+              ('contact_penetration', C.c_void_p)]
+
+
+class BxEnvState(C.Structure):
+  _fields_ = [('qp', BxQP), ('obs', C.c_void_p), ('reward', C.c_void_p),
+              ('done', C.c_void_p), ('metrics', C.c_void_p),
+              ('steps', C.c_void_p), ('truncation', C.c_void_p)]
+
+
+class BxEnvParams(C.Structure):
+  _fields_ = [('kind', C.c_int32), ('obs_size', C.c_int32),
+              ('n_metrics', C.c_int32), ('episode_length', C.c_int32),
+              ('action_repeat', C.c_int32), ('auto_reset', C.c_int32),
+              ('first_qp', BxQP), ('first_obs', C.c_void_p)]
+
+
+def _arr(x, dtype):
+  a = np.ascontiguousarray(np.asarray(x, dtype=dtype))
+  if a.size == 0:
+    a = np.zeros(1, dtype)
+  return a
+
+
+def make_desc(d):
+  """numpy descriptor dict -> (BxDesc, keepalive)."""
+  keep = []
+  s = BxDesc()
+  s.n_bodies = int(d['n_bodies'])
+  s.n_joints = len(d['joint_type'])
+  s.n_actuators = len(d['act_type'])
+  s.n_rows = len(d['row_group'])
+  s.n_groups = len(d['col_oneway'])
+  s.substeps = int(d['substeps'])
+  s.action_size = int(d.get('action_size', 0))
+  s.num_joint_dof = int(d.get('num_joint_dof', 0))
+  s.dt = float(d['dt'])
+  s.h = float(d['h'])
+  for k in range(3):
+    s.gravity[k] = float(d['gravity'][k])
+  s.velocity_damping = float(d['velocity_damping'])
+  s.angular_damping = float(d['angular_damping'])
+  for name, ctype in _DESC_FIELDS:
+    if ctype is i32p or ctype is f64p:
+      a = _arr(d[name], np.int32 if ctype is i32p else np.float64)
+      keep.append(a)
+      setattr(s, name, a.ctypes.data_as(ctype))
+  return s, keep
+
+
+def make_reset_desc(r):
+  keep = []
+  s = BxResetDesc()
+  s.n_fk = len(r['fk_body_p'])
+  s.n_zpts = len(r['zpt_body'])
+  s.n_root_groups = int(r['n_root_groups'])
+  for name, ctype in BxResetDesc._fields_:
+    if ctype is i32p or ctype is f64p:
+      a = _arr(r[name], np.int32 if ctype is i32p else np.float64)
+      keep.append(a)
+      setattr(s, name, a.ctypes.data_as(ctype))
+  return s, keep

@@ -1,0 +1,577 @@
+"""System compiler: `brax.Config` -> flat constant arrays (the descriptor).
+
+Host-side, once per System, float64 numpy (the reference builds these in
+Python double from fp32 proto fields and lets `jit` cast them to fp32). The
+ordering rules and quirks are the reference's, restated:
+
+  validate_config      `brax/physics/base.py:156-254`
+  Body                 `brax/physics/bodies.py:38-44`   (stores INVERSE inertia)
+  colliders.get        `brax/physics/colliders.py:891-1023`
+  Collidable/Capsule*  `brax/physics/geometry.py:78-99,242-288`
+  joints.get / Joint   `brax/physics/joints.py:418-474,36-77`
+  actuators.get        `brax/physics/actuators.py:115-164`
+  Euler.__init__       `brax/physics/integrators.py:32-48`
+  Collider.__init__    `brax/physics/colliders.py:95-114`
+
+The descriptor keys match `oracle/gen_golden.py:dump_desc`, so the reference's
+own compiled arrays pin this compiler (tests/test_compiler.py).
+"""
+import copy
+import warnings
+
+import numpy as np
+
+from brax_amd import config as cfgmod
+
+# joint kinds (descriptor `joint_type`)
+REVOLUTE, SPHERICAL = 1, 3
+# actuator kinds (descriptor `act_type`)
+TORQUE, ANGLE = 0, 1
+# contact functions (descriptor `col_fn`)
+CAPSULE_PLANE, CAPSULE_CAPSULE = 0, 1
+# force kinds
+THRUSTER, TWISTER = 0, 1
+
+
+# --------------------------------------------------------------------------
+# float64 math helpers (same formulas as `brax/math.py:25-77`)
+# --------------------------------------------------------------------------
+
+def vec(v):
+  return np.array([v.x, v.y, v.z], np.float64)
+
+
+def euler_to_quat(v):
+  """x-y'-z'' intrinsic Tait-Bryan, degrees -> wxyz (`math.py:68-77`)."""
+  c1, c2, c3 = np.cos(v * np.pi / 360)
+  s1, s2, s3 = np.sin(v * np.pi / 360)
+  w = c1 * c2 * c3 - s1 * s2 * s3
+  x = s1 * c2 * c3 + c1 * s2 * s3
+  y = c1 * s2 * c3 - s1 * c2 * s3
+  z = c1 * c2 * s3 + s1 * s2 * c3
+  return np.array([w, x, y, z])
+
+
+def rotate(vv, q):
+  """Rotates vector vv by unit quaternion q (`math.py:25-40`)."""
+  s, u = q[0], q[1:]
+  r = 2 * (np.dot(u, vv) * u) + (s * s - np.dot(u, u)) * vv
+  return r + 2 * s * np.cross(u, vv)
+
+
+# --------------------------------------------------------------------------
+# validate_config
+# --------------------------------------------------------------------------
+
+def validate_config(config):
+  """Normalises a config like `base.py:156-254` (returns a deep copy)."""
+  config = copy.deepcopy(config)
+  if config.dt <= 0:
+    raise ValueError('config.dt must be positive')
+  if config.substeps == 0:
+    config.substeps = 1
+  config.solver_scale_collide = config.solver_scale_collide or 1.0
+
+  def find_dupes(objs):
+    names = set()
+    for obj in objs:
+      if obj.name in names:
+        raise RuntimeError(f'duplicate name in config: {obj.name}')
+      names.add(obj.name)
+
+  find_dupes(config.bodies)
+  find_dupes(config.joints)
+  find_dupes(config.actuators)
+  find_dupes(config.mesh_geometries)
+
+  if config.dynamics_mode == 'legacy_spring':
+    if any(j.stiffness == 0 for j in config.joints):
+      raise ValueError(
+          'joint.stiffness must be >0 when dynamics_mode == legacy_spring')
+  elif config.dynamics_mode == 'pbd':
+    if any(j.stiffness != 0 for j in config.joints):
+      raise ValueError('joint.stiffness is invalid when dynamics_mode == pbd')
+    if config.baumgarte_erp:
+      raise ValueError('baumgarte_erp is invalid when dynamics_mode == pbd')
+  elif any(j.stiffness != 0 for j in config.joints):
+    config.dynamics_mode = 'legacy_spring'
+    warnings.warn('dynamics_mode not specified, but joint.stiffness >0. '
+                  'Setting dynamics_mode="legacy_spring".')
+  else:
+    config.dynamics_mode = 'pbd'
+    warnings.warn('dynamics_mode not specified, defaulting to "pbd".')
+
+  allvec = cfgmod.Message('Vector3', x=1.0, y=1.0, z=1.0)
+  frozen = config.frozen
+  if frozen.all:
+    frozen.position.CopyFrom(allvec)
+    frozen.rotation.CopyFrom(allvec)
+  if all([frozen.position.x, frozen.position.y, frozen.position.z,
+          frozen.rotation.x, frozen.rotation.y, frozen.rotation.z]):
+    config.frozen.all = True
+  for b in config.bodies:
+    inertia = b.inertia
+    if inertia.x == 0 and inertia.y == 0 and inertia.z == 0:
+      b.inertia.x, b.inertia.y, b.inertia.z = 1, 1, 1
+    b.frozen.position.x = b.frozen.position.x or frozen.position.x
+    b.frozen.position.y = b.frozen.position.y or frozen.position.y
+    b.frozen.position.z = b.frozen.position.z or frozen.position.z
+    b.frozen.rotation.x = b.frozen.rotation.x or frozen.rotation.x
+    b.frozen.rotation.y = b.frozen.rotation.y or frozen.rotation.y
+    b.frozen.rotation.z = b.frozen.rotation.z or frozen.rotation.z
+    if b.frozen.all:
+      b.frozen.position.CopyFrom(allvec)
+      b.frozen.rotation.CopyFrom(allvec)
+    if all([b.frozen.position.x, b.frozen.position.y, b.frozen.position.z,
+            b.frozen.rotation.x, b.frozen.rotation.y, b.frozen.rotation.z]):
+      b.frozen.all = True
+    for c in b.colliders:
+      if not c.HasField('material'):
+        c.material.friction = config.friction
+        c.material.elasticity = config.elasticity
+  frozen.all = all(b.frozen.all for b in config.bodies)
+  return config
+
+
+# --------------------------------------------------------------------------
+# pieces
+# --------------------------------------------------------------------------
+
+def _bodies(config):
+  inv_inertia = 1. / np.array([vec(b.inertia) for b in config.bodies])
+  mass = np.array([b.mass for b in config.bodies], np.float64)
+  index = {b.name: i for i, b in enumerate(config.bodies)}
+  return mass, inv_inertia, index
+
+
+def _integrator(config):
+  pos_mask = 1. * np.logical_not(
+      np.array([vec(b.frozen.position) for b in config.bodies]))
+  rot_mask = 1. * np.logical_not(
+      np.array([vec(b.frozen.rotation) for b in config.bodies]))
+  quat_mask = 1. * np.logical_not(
+      np.array([[0.] + list(vec(b.frozen.rotation)) for b in config.bodies]))
+  return pos_mask, rot_mask, quat_mask
+
+
+def _capsule_axis(col):
+  return rotate(np.array([0., 0., 1.]), euler_to_quat(vec(col.rotation)))
+
+
+def _colliders(config, index):
+  """Collider groups and flattened contact rows (`colliders.py:891-1023`)."""
+  # only the capsule/sphere/plane subset of `collider_pairs` is on the path
+  # (SURVEY §2); other supported-by-reference types raise.
+  pair_types = [('box', 'plane'), ('box', 'heightMap'), ('capsule', 'box'),
+                ('capsule', 'plane'), ('capsule', 'capsule'),
+                ('capsule', 'mesh'), ('capsule', 'clipped_plane'),
+                ('mesh', 'plane'), ('box', 'box')]
+  supported = {('capsule', 'plane'): CAPSULE_PLANE,
+               ('capsule', 'capsule'): CAPSULE_CAPSULE}
+  cols = []
+  for b in config.bodies:
+    for c_idx, c in enumerate(b.colliders):
+      if c.no_contact:
+        continue
+      if c.WhichOneof('type') == 'sphere':
+        nc = cfgmod.Message('Collider')
+        nc.CopyFrom(c)
+        nc.capsule.radius = c.sphere.radius
+        nc.capsule.length = 2 * c.sphere.radius
+        nc.capsule.end = 1
+        c = nc
+      cols.append((c, b, c_idx))
+
+  include = {(ci.first, ci.second) for ci in config.collide_include}
+  # NB: a generator, consumed by the first membership test (App. A.1)
+  parents = ((j.parent, j.child) for j in config.joints)
+  groups = []
+  for (type_a, type_b) in pair_types:
+    cols_a = [x for x in cols if x[0].WhichOneof('type') == type_a]
+    cols_b = [x for x in cols if x[0].WhichOneof('type') == type_b]
+    cols_a = [x for x in cols_a if not x[1].frozen.all]
+    cols_ab = []
+    pair_count = {}
+    for ca, ba, ca_idx in cols_a:
+      for cb, bb, cb_idx in cols_b:
+        included = (ba.name, bb.name) in include or (bb.name, ba.name) in include
+        if ((ba.name, ca_idx, bb.name, cb_idx) in pair_count or
+            (bb.name, cb_idx, ba.name, ca_idx) in pair_count):
+          continue
+        if ba.name == bb.name:
+          continue
+        if ba.frozen.all and bb.frozen.all:
+          continue
+        # `A or B and not included` binds as `A or (B and not included)`
+        if (ba.name, bb.name) in parents or (bb.name, ba.name) in parents and not included:
+          continue
+        if ca.no_contact or cb.no_contact:
+          continue
+        if not include or included:
+          cols_ab.append((ca, ca_idx, ba, cb, cb_idx, bb))
+          pair_count[(ba.name, ca_idx, bb.name, cb_idx)] = 1
+          pair_count[(bb.name, cb_idx, ba.name, ca_idx)] = 1
+    for b_is_frozen in (True, False):
+      flt = [x for x in cols_ab if x[-1].frozen.all == b_is_frozen]
+      if not flt:
+        continue
+      if (type_a, type_b) not in supported:
+        raise NotImplementedError(
+            f'collider pair {type_a}/{type_b} is outside the MI355X path')
+      if (config.collider_cutoff and len(flt) > config.collider_cutoff and
+          (type_a, type_b) == ('capsule', 'capsule')):
+        raise NotImplementedError('NearNeighbors culling (collider_cutoff) is '
+                                  'not implemented yet (SURVEY §8(f).2)')
+      groups.append(dict(oneway=b_is_frozen, fn=supported[(type_a, type_b)],
+                         pairs=flt))
+
+  h = config.dt / config.substeps
+  g_norm = np.linalg.norm(vec(config.gravity))
+  out = dict(col_oneway=[], col_fn=[], col_scale=[], col_velocity_threshold=[],
+             col_baumgarte_erp=[])
+  rows = {k: [] for k in ('group', 'body_a', 'body_b', 'a_pos', 'a_end',
+                          'a_radius', 'b_pos', 'b_end', 'b_radius', 'friction',
+                          'elasticity')}
+  for gi, g in enumerate(groups):
+    out['col_oneway'].append(1 if g['oneway'] else 0)
+    out['col_fn'].append(g['fn'])
+    out['col_scale'].append(config.solver_scale_collide)
+    out['col_velocity_threshold'].append(g_norm * h * 4.0)
+    out['col_baumgarte_erp'].append(config.baumgarte_erp * config.substeps / config.dt)
+    if g['fn'] == CAPSULE_PLANE:
+      # CapsuleEnd (`geometry.py:261-288`): 1 or 2 ends; mixed -> pad by dup
+      ends_l = []
+      for ca, _, _, _, _, _ in g['pairs']:
+        axis = _capsule_axis(ca)
+        seg = ca.capsule.length * 0.5 - ca.capsule.radius
+        ends_l.append([vec(ca.position) + e * axis * seg
+                       for e in ([ca.capsule.end] if ca.capsule.end else [-1, 1])])
+      if len({len(e) for e in ends_l}) != 1:
+        for e in ends_l:
+          if len(e) == 1:
+            e.append(e[0])
+    for pi, (ca, _, ba, cb, _, bb) in enumerate(g['pairs']):
+      fa = ca.material.friction * cb.material.friction
+      ea = ca.material.elasticity * cb.material.elasticity
+      if g['fn'] == CAPSULE_PLANE:
+        ends = ends_l[pi]
+        b_end, b_rad = np.zeros(3), 0.
+      else:
+        ends = [_capsule_axis(ca) * (ca.capsule.length * 0.5 - ca.capsule.radius)]
+        b_end = _capsule_axis(cb) * (cb.capsule.length * 0.5 - cb.capsule.radius)
+        b_rad = cb.capsule.radius
+      for e in ends:
+        rows['group'].append(gi)
+        rows['body_a'].append(index[ba.name])
+        rows['body_b'].append(index[bb.name])
+        rows['a_pos'].append(vec(ca.position))
+        rows['a_end'].append(e)
+        rows['a_radius'].append(ca.capsule.radius)
+        rows['b_pos'].append(vec(cb.position))
+        rows['b_end'].append(b_end)
+        rows['b_radius'].append(b_rad)
+        rows['friction'].append(fa)
+        rows['elasticity'].append(ea)
+  d = {}
+  d['col_oneway'] = np.asarray(out['col_oneway'], np.int32)
+  d['col_fn'] = np.asarray(out['col_fn'], np.int32)
+  for k in ('col_scale', 'col_velocity_threshold', 'col_baumgarte_erp'):
+    d[k] = np.asarray(out[k], np.float64)
+  for k, v in rows.items():
+    if k in ('group', 'body_a', 'body_b'):
+      d['row_' + k] = np.asarray(v, np.int32)
+    elif k.endswith(('pos', 'end')):
+      d['row_' + k] = np.asarray(v, np.float64).reshape(-1, 3)
+    else:
+      d['row_' + k] = np.asarray(v, np.float64)
+  return d
+
+
+def _joints(config, mass, inv_inertia, index):
+  """Joint groups (`joints.py:418-474`). MUTATES config.joints (App. A.2)."""
+  if config.dynamics_mode != 'pbd':
+    raise NotImplementedError('legacy_spring dynamics are outside the MI355X '
+                              'path (SURVEY §2, spring_joints.py)')
+  groups = {}
+  dofs = {len(j.angle_limit) for j in config.joints}
+  sphericalize = len(dofs) > 1
+  sphericalize |= 2 in dofs
+  for joint in config.joints:
+    dof = len(joint.angle_limit)
+    free = dof
+    while sphericalize and dof < 3:
+      joint.angle_limit.add()
+      dof += 1
+    groups.setdefault(dof, {'joint': [], 'free_dofs': []})
+    groups[dof]['joint'].append(joint)
+    groups[dof]['free_dofs'].append(free)
+  groups = sorted(groups.items(), key=lambda kv: kv[0])
+  scale_pos = config.solver_scale_pos or .6
+  scale_ang = config.solver_scale_ang or .2
+  J = {k: [] for k in ('type', 'dof', 'free_dofs', 'body_p', 'body_c', 'off_p',
+                       'off_c', 'axis_p', 'axis_c', 'limit', 'damping',
+                       'scale_pos', 'scale_ang', 'group')}
+  meta = []  # per group: (dof, names, free_dofs or None)
+  for gi, (dof, v) in enumerate(groups):
+    if dof not in (1, 2, 3):
+      raise RuntimeError(f'invalid number of joint limits: {dof}')
+    jtype = REVOLUTE if dof == 1 else SPHERICAL
+    free = v['free_dofs'] if dof == 3 else None
+    meta.append((dof, [j.name for j in v['joint']], free))
+    for k, j in enumerate(v['joint']):
+      J['type'].append(jtype)
+      J['dof'].append(dof)
+      J['free_dofs'].append(free[k] if free is not None else -1)
+      J['body_p'].append(index[j.parent])
+      J['body_c'].append(index[j.child])
+      J['off_p'].append(vec(j.parent_offset))
+      J['off_c'].append(vec(j.child_offset))
+      axis_c = np.array([rotate(e, euler_to_quat(vec(j.rotation)))
+                         for e in np.eye(3)])
+      ref = euler_to_quat(vec(j.reference_rotation))
+      J['axis_c'].append(axis_c)
+      J['axis_p'].append(np.array([rotate(a, ref) for a in axis_c]))
+      lim = np.zeros((3, 2))
+      lim[:dof] = np.array([[i.min, i.max] for i in j.angle_limit]) / 180.0 * np.pi
+      J['limit'].append(lim)
+      J['damping'].append(j.angular_damping)
+      J['scale_pos'].append(scale_pos)
+      J['scale_ang'].append(scale_ang)
+      J['group'].append(gi)
+  d = {}
+  for k in ('type', 'dof', 'free_dofs', 'body_p', 'body_c', 'group'):
+    d['joint_' + k] = np.asarray(J[k], np.int32)
+  d['joint_off_p'] = np.asarray(J['off_p'], np.float64).reshape(-1, 3)
+  d['joint_off_c'] = np.asarray(J['off_c'], np.float64).reshape(-1, 3)
+  d['joint_axis_p'] = np.asarray(J['axis_p'], np.float64).reshape(-1, 3, 3)
+  d['joint_axis_c'] = np.asarray(J['axis_c'], np.float64).reshape(-1, 3, 3)
+  d['joint_limit'] = np.asarray(J['limit'], np.float64).reshape(-1, 3, 2)
+  for k in ('damping', 'scale_pos', 'scale_ang'):
+    d['joint_' + k] = np.asarray(J[k], np.float64)
+  return d, meta
+
+
+def _actuators(config, jmeta):
+  """Actuator groups (`actuators.py:115-164`)."""
+  groups = {}
+  current = 0
+  gbase = np.cumsum([0] + [len(m[1]) for m in jmeta])
+  for actuator in config.actuators:
+    gi = [i for i, m in enumerate(jmeta) if actuator.joint in m[1]]
+    if not gi:
+      raise RuntimeError(f'joint not found: {actuator.joint}')
+    gi = gi[0]
+    dof, names, free = jmeta[gi]
+    jidx = names.index(actuator.joint)
+    if free is not None:
+      fd = free[jidx]
+      act_index = tuple(i if i - current < fd else -1
+                        for i in range(current, current + dof))
+      current += fd
+    else:
+      act_index = tuple(range(current, current + dof))
+      current += dof
+    kind = actuator.WhichOneof('type')
+    if kind not in ('torque', 'angle'):
+      raise RuntimeError(f'unknown actuator type: {kind}')
+    key = (kind, dof, gi)
+    groups.setdefault(key, []).append((actuator, act_index, gbase[gi] + jidx))
+  groups = sorted(groups.items(), key=lambda kv: kv[0][:2])
+  A = {k: [] for k in ('type', 'joint', 'strength', 'index', 'group')}
+  for g, ((kind, dof, _), items) in enumerate(groups):
+    for act, idx, jglob in items:
+      A['type'].append(TORQUE if kind == 'torque' else ANGLE)
+      A['joint'].append(jglob)
+      A['strength'].append(act.strength)
+      ii = -np.ones(3, np.int64)
+      ii[:dof] = idx
+      A['index'].append(ii)
+      A['group'].append(g)
+  d = {'act_type': np.asarray(A['type'], np.int32),
+       'act_joint': np.asarray(A['joint'], np.int32),
+       'act_strength': np.asarray(A['strength'], np.float64),
+       'act_index': np.asarray(A['index'], np.int32).reshape(-1, 3),
+       'act_group': np.asarray(A['group'], np.int32)}
+  return d, current
+
+
+def _forces(config, index, act_offset):
+  """Thruster/Twister groups (`forces.py:110-138`): act tail after joints."""
+  F = {'type': [], 'body': [], 'strength': [], 'index': []}
+  groups = {}
+  for f in config.forces:
+    kind = f.WhichOneof('type')
+    groups.setdefault(kind, []).append(f)
+  cur = act_offset
+  for kind in sorted(groups):
+    for f in groups[kind]:
+      F['type'].append(THRUSTER if kind == 'thruster' else TWISTER)
+      F['body'].append(index[f.body])
+      F['strength'].append(f.strength)
+      F['index'].append([cur, cur + 1, cur + 2])
+      cur += 3
+  return {'force_type': np.asarray(F['type'], np.int32),
+          'force_body': np.asarray(F['body'], np.int32),
+          'force_strength': np.asarray(F['strength'], np.float64),
+          'force_index': np.asarray(F['index'], np.int32).reshape(-1, 3)}, cur - act_offset
+
+
+def compile_system(config):
+  """Returns (validated config, descriptor dict, metadata dict)."""
+  config = validate_config(config)
+  num_joint_dof = sum(len(j.angle_limit) for j in config.joints)
+  mass, inv_inertia, index = _bodies(config)
+  d = {}
+  d['n_bodies'] = np.int32(len(config.bodies))
+  d['body_mass'] = mass
+  d['body_inv_inertia'] = inv_inertia
+  d['pos_mask'], d['rot_mask'], d['quat_mask'] = _integrator(config)
+  d['h'] = np.float64(config.dt / config.substeps)
+  d['dt'] = np.float64(config.dt)
+  d['substeps'] = np.int32(config.substeps)
+  d['gravity'] = vec(config.gravity)
+  d['velocity_damping'] = np.float64(config.velocity_damping)
+  d['angular_damping'] = np.float64(config.angular_damping)
+  d.update(_colliders(config, index))
+  jd, jmeta = _joints(config, mass, inv_inertia, index)
+  d.update(jd)
+  ad, _ = _actuators(config, jmeta)
+  d.update(ad)
+  fd, n_force_dof = _forces(config, index, num_joint_dof)
+  d.update(fd)
+  if len(fd['force_type']):
+    raise NotImplementedError('Thruster/Twister forces are not on the kernel '
+                              'path yet (SURVEY §8 a26)')
+  d['num_joint_dof'] = np.int32(num_joint_dof)
+  d['action_size'] = np.int32(num_joint_dof + n_force_dof)
+  meta = dict(num_joint_dof=num_joint_dof, num_forces_dof=n_force_dof,
+              body_index=index, joint_groups=jmeta,
+              action_size=num_joint_dof + n_force_dof)
+  return config, d, meta
+
+
+# --------------------------------------------------------------------------
+# reset (System.default_angle / default_qp / bodies.min_z)
+# --------------------------------------------------------------------------
+
+def default_angle(config, default_index=0):
+  """`System.default_angle` (system.py:86-110), float64."""
+  if not config.joints:
+    return np.zeros(0)
+  dofs = {j.name: sum([l.min != 0 or l.max != 0 for l in j.angle_limit])
+          for j in config.joints}
+  angles = {}
+  if default_index < len(config.defaults):
+    for ja in config.defaults[default_index].angles:
+      angles[ja.name] = vec(ja.angle)[:dofs[ja.name]] * np.pi / 180
+  for joint in config.joints:
+    if joint.name not in angles:
+      dof = dofs[joint.name]
+      angles[joint.name] = np.array(
+          [(l.min + l.max) * np.pi / 360 for l in joint.angle_limit][:dof])
+  return np.concatenate([angles[j.name] for j in config.joints])
+
+
+_BOX_CORNERS = np.array([[x, y, z] for x in (-1, 1) for y in (-1, 1)
+                         for z in (-1, 1)], np.float64)
+
+
+def compile_reset(config, index, default_index=0):
+  """Reset descriptor for `System.default_qp` (system.py:112-242).
+
+  `config` must be the validated config AFTER joints.get padded it (the
+  reference's System.config is that same mutated object)."""
+  N = len(config.bodies)
+  base = np.zeros((N, 13))
+  base[:, 3] = 1.0
+  default = None
+  if default_index < len(config.defaults):
+    default = config.defaults[default_index]
+    for dqp in default.qps:
+      i = index[dqp.name]
+      base[i, 0:3] = vec(dqp.pos)
+      base[i, 3:7] = euler_to_quat(vec(dqp.rot))
+      base[i, 7:10] = vec(dqp.vel)
+      base[i, 10:13] = vec(dqp.ang)
+  joint_idxs = []
+  for j in config.joints:
+    beg = joint_idxs[-1][1][1] if joint_idxs else 0
+    dof = sum([l.min != 0 or l.max != 0 for l in j.angle_limit])
+    joint_idxs.append((j, (beg, beg + dof)))
+  lineage = {j.child: j.parent for j in config.joints}
+  depth = {}
+  for child, parent in lineage.items():
+    depth[child] = 1
+    while parent in lineage:
+      parent = lineage[parent]
+      depth[child] += 1
+  joint_idxs = sorted(joint_idxs, key=lambda x: depth.get(x[0].parent, 0))
+  joints = [j for j, _ in joint_idxs]
+  r = {k: [] for k in ('fk_body_p', 'fk_body_c', 'fk_dof_index', 'fk_rot',
+                       'fk_ref', 'fk_off_p', 'fk_off_c')}
+  for j, (beg, end) in joint_idxs:
+    r['fk_body_p'].append(index[j.parent])
+    r['fk_body_c'].append(index[j.child])
+    ix = list(range(beg, end)) + [-1] * (3 - (end - beg))
+    r['fk_dof_index'].append(ix[:3])
+    r['fk_rot'].append(euler_to_quat(vec(j.rotation)))
+    r['fk_ref'].append(euler_to_quat(vec(j.reference_rotation)))
+    r['fk_off_p'].append(vec(j.parent_offset))
+    r['fk_off_c'].append(vec(j.child_offset))
+  out = {
+      'fk_body_p': np.asarray(r['fk_body_p'], np.int32),
+      'fk_body_c': np.asarray(r['fk_body_c'], np.int32),
+      'fk_dof_index': np.asarray(r['fk_dof_index'], np.int32).reshape(-1, 3),
+      'fk_rot': np.asarray(r['fk_rot'], np.float64).reshape(-1, 4),
+      'fk_ref': np.asarray(r['fk_ref'], np.float64).reshape(-1, 4),
+      'fk_off_p': np.asarray(r['fk_off_p'], np.float64).reshape(-1, 3),
+      'fk_off_c': np.asarray(r['fk_off_c'], np.float64).reshape(-1, 3),
+      'base_qp': base,
+  }
+  # root trees lifted above the plane (system.py:213-240)
+  fixed = {j.child for j in joints}
+  if default:
+    fixed |= {q.name for q in default.qps}
+  root_idx = {b.name: [i] for i, b in enumerate(config.bodies)
+              if b.name not in fixed}
+  for j in joints:
+    parent = j.parent
+    while parent in lineage:
+      parent = lineage[parent]
+    if parent in root_idx:
+      root_idx[parent].append(index[j.child])
+  group = -np.ones(N, np.int32)
+  for gi, members in enumerate(root_idx.values()):
+    for b in members:
+      group[b] = gi
+  out['body_root_group'] = group
+  out['n_root_groups'] = np.int32(len(root_idx))
+  # bodies.min_z candidates (bodies.py:62-98)
+  zb, zl, zr = [], [], []
+  zero = np.zeros(N, np.int32)
+  for bi, b in enumerate(config.bodies):
+    if not b.colliders:
+      zero[bi] = 1
+    for col in b.colliders:
+      kind = col.WhichOneof('type')
+      if kind == 'sphere':
+        zb.append(bi); zl.append(vec(col.position)); zr.append(col.sphere.radius)
+      elif kind == 'capsule':
+        axis = rotate(np.array([0., 0., 1.]), euler_to_quat(vec(col.rotation)))
+        length = col.capsule.length / 2 - col.capsule.radius
+        for e in (-1, 1):
+          zb.append(bi)
+          zl.append(vec(col.position) + e * axis * length)
+          zr.append(col.capsule.radius)
+      elif kind == 'box':
+        q = euler_to_quat(vec(col.rotation))
+        for corner in _BOX_CORNERS:
+          c = rotate(corner * vec(col.box.halfsize), q) + vec(col.position)
+          zb.append(bi); zl.append(c); zr.append(0.0)
+      else:
+        zero[bi] = 1
+  out['zpt_body'] = np.asarray(zb, np.int32)
+  out['zpt_local'] = np.asarray(zl, np.float64).reshape(-1, 3)
+  out['zpt_radius'] = np.asarray(zr, np.float64)
+  out['body_zero_cand'] = zero
+  return out

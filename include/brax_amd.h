@@ -1,0 +1,225 @@
+/*
+ * brax_amd — C ABI of the MI355X-native PBD rigid-body stepper.
+ *
+ * This is the drop-in boundary for the reference's hot path:
+ * what `brax.System.step`, `brax.System.default_qp/info` and the
+ * `Env.step/reset` + Episode/AutoReset wrapper stack compute under `jax.jit`
+ * is exported here as stream-ordered C calls on caller-owned device buffers.
+ *
+ *   reference interface                                  replaced by
+ *   brax.System(config)          system.py:53-84         bx_system_create
+ *   System.step(qp, act)         system.py:244-325       bx_system_step
+ *   System.default_qp(a, v)      system.py:112-242       bx_system_default_qp
+ *   System.info(qp)              system.py:249-252,327-340  bx_system_info
+ *   Env.step + EpisodeWrapper + AutoResetWrapper
+ *     ant.py:222-255, wrappers.py:105-148                bx_env_step
+ *   Env.reset                    ant.py:198-220          bx_env_reset
+ *
+ * Conventions
+ *   - Every array argument is a raw device pointer (HBM) owned by the caller.
+ *     Sizes are explicit (n_envs, strides in elements); no torch types.
+ *   - fp32 throughout on the device (what jit computes; `config.proto` floats
+ *     are fp32). The descriptor is float64/int32 host memory, copied at create.
+ *   - All calls enqueue on `stream` (a hipStream_t; NULL = default stream) and
+ *     return immediately. Not re-entrant per handle.
+ *   - Return 0 on success, non-zero on error; `bx_last_error()` returns a
+ *     thread-local message. Descriptor errors surface at create time.
+ */
+#ifndef BRAX_AMD_H_
+#define BRAX_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BX_ABI_VERSION 1
+
+/* joint kinds, actuator kinds, contact functions (descriptor enums) */
+enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_SPHERICAL = 3 };
+enum { BX_ACT_TORQUE = 0, BX_ACT_ANGLE = 1 };
+enum { BX_COL_CAPSULE_PLANE = 0, BX_COL_CAPSULE_CAPSULE = 1 };
+/* env layer kinds (obs / reward programs) */
+enum { BX_ENV_NONE = 0, BX_ENV_ANT = 1, BX_ENV_HUMANOID = 2, BX_ENV_HALFCHEETAH = 3 };
+
+/*
+ * System descriptor: the compiled constant arrays of `brax.System`
+ * (bodies.py:38-44, joints.py:36-77, actuators.py:28-35, colliders.py:95-114,
+ * geometry.py:78-99,242-288, integrators.py:32-48). Built on the host by
+ * brax_amd/compiler.py. Shapes in brackets; row-major; J = n_joints etc.
+ */
+typedef struct bx_desc {
+  int32_t n_bodies, n_joints, n_actuators, n_rows, n_groups;
+  int32_t substeps, action_size, num_joint_dof;
+  double dt, h;
+  double gravity[3];
+  double velocity_damping, angular_damping;
+  /* bodies */
+  const double* body_mass;         /* [N] */
+  const double* body_inv_inertia;  /* [N,3]  (inverse, body-frame diagonal) */
+  const double* pos_mask;          /* [N,3] */
+  const double* rot_mask;          /* [N,3] */
+  const double* quat_mask;         /* [N,4] */
+  /* joints, in application order (grouped by dof like joints.get) */
+  const int32_t* joint_type;       /* [J] BX_JOINT_* */
+  const int32_t* joint_dof;        /* [J] 1..3 (limit rows in use) */
+  const int32_t* joint_free_dofs;  /* [J] -1 for revolute groups */
+  const int32_t* joint_body_p;     /* [J] */
+  const int32_t* joint_body_c;     /* [J] */
+  const int32_t* joint_group;      /* [J] */
+  const double* joint_off_p;       /* [J,3] */
+  const double* joint_off_c;       /* [J,3] */
+  const double* joint_axis_p;      /* [J,3,3] */
+  const double* joint_axis_c;      /* [J,3,3] */
+  const double* joint_limit;       /* [J,3,2] radians */
+  const double* joint_damping;     /* [J] */
+  const double* joint_scale_pos;   /* [J] */
+  const double* joint_scale_ang;   /* [J] */
+  /* actuators, in application order (sorted by type, dof) */
+  const int32_t* act_type;         /* [K] BX_ACT_* */
+  const int32_t* act_joint;        /* [K] index into joints */
+  const int32_t* act_index;        /* [K,3] action index, -1 = masked */
+  const int32_t* act_group;        /* [K] */
+  const double* act_strength;      /* [K] */
+  /* collider groups and flattened contact rows */
+  const int32_t* col_oneway;       /* [G] 1 = OneWayCollider */
+  const int32_t* col_fn;           /* [G] BX_COL_* */
+  const double* col_scale;         /* [G] solver_scale_collide */
+  const double* col_velocity_threshold; /* [G] */
+  const double* col_baumgarte_erp; /* [G] */
+  const int32_t* row_group;        /* [R] */
+  const int32_t* row_body_a;       /* [R] */
+  const int32_t* row_body_b;       /* [R] */
+  const double* row_a_pos;         /* [R,3] collidable offset of a */
+  const double* row_a_end;         /* [R,3] capsule end (plane: end point in body a) */
+  const double* row_a_radius;      /* [R] */
+  const double* row_b_pos;         /* [R,3] */
+  const double* row_b_end;         /* [R,3] */
+  const double* row_b_radius;      /* [R] */
+  const double* row_friction;      /* [R] friction_a * friction_b */
+  const double* row_elasticity;    /* [R] */
+} bx_desc;
+
+/*
+ * Reset descriptor (`System.default_qp`, system.py:112-242; bodies.min_z
+ * bodies.py:62-98): joint-tree forward kinematics in depth order, then lift
+ * every free root tree so its lowest collider touches z = 0.
+ */
+typedef struct bx_reset_desc {
+  int32_t n_fk;                    /* joints in depth order */
+  const int32_t* fk_body_p;        /* [n_fk] */
+  const int32_t* fk_body_c;        /* [n_fk] */
+  const int32_t* fk_dof_index;     /* [n_fk,3] index into joint angle vector, -1 = 0 */
+  const double* fk_rot;            /* [n_fk,4] euler_to_quat(rotation) */
+  const double* fk_ref;            /* [n_fk,4] euler_to_quat(reference_rotation) */
+  const double* fk_off_p;          /* [n_fk,3] */
+  const double* fk_off_c;          /* [n_fk,3] */
+  const double* base_qp;           /* [N,13] config default qps (else identity) */
+  int32_t n_zpts;                  /* min_z candidate points */
+  const int32_t* zpt_body;         /* [n_zpts] */
+  const double* zpt_local;         /* [n_zpts,3] point in body frame */
+  const double* zpt_radius;        /* [n_zpts] */
+  const int32_t* body_zero_cand;   /* [N] 1: min_z also sees 0.0 (plane/none) */
+  const int32_t* body_root_group;  /* [N] lift group, -1 = not lifted */
+  int32_t n_root_groups;
+} bx_reset_desc;
+
+/* A strided view of one fp32 QP field: element (env e, body b, k) lives at
+ * ptr[e*env_stride + b*body_stride + k]. Lets the caller pass the reference's
+ * (B,N,3)/(B,N,4) arrays or the packed (B,N,16) layout without copies. */
+typedef struct bx_field {
+  float* ptr;
+  int64_t env_stride;
+  int64_t body_stride;
+} bx_field;
+
+typedef struct bx_qp {
+  bx_field pos, rot, vel, ang;     /* rot is wxyz */
+} bx_qp;
+
+/* Optional Info outputs of System.step (base.py:136-153); NULL ptr = skip. */
+typedef struct bx_info {
+  bx_field contact_vel, contact_ang;     /* (B,N,3) accumulated contact P */
+  bx_field actuator_vel, actuator_ang;  /* (B,N,3) */
+  float* contact_pos;                   /* (B,R,3) contiguous */
+  float* contact_normal;                /* (B,R,3) */
+  float* contact_penetration;           /* (B,R)   */
+} bx_info;
+
+/* Env-layer state of one batch (ant.py:198-255, wrappers.py:83-148).
+ * obs (B,O), reward/done/steps/truncation (B,), metrics (B,M); contiguous. */
+typedef struct bx_env_state {
+  bx_qp qp;
+  float* obs;
+  float* reward;
+  float* done;
+  float* metrics;
+  float* steps;
+  float* truncation;
+} bx_env_state;
+
+typedef struct bx_env_params {
+  int32_t kind;             /* BX_ENV_* */
+  int32_t obs_size;
+  int32_t n_metrics;
+  int32_t episode_length;   /* <= 0: no EpisodeWrapper */
+  int32_t action_repeat;    /* EpisodeWrapper action_repeat (>= 1) */
+  int32_t auto_reset;       /* AutoResetWrapper present */
+  /* AutoReset targets (first_qp / first_obs); required when auto_reset */
+  bx_qp first_qp;
+  const float* first_obs;
+} bx_env_params;
+
+typedef struct bx_system bx_system;
+
+int bx_abi_version(void);
+const char* bx_last_error(void);
+int bx_device_count(int* count);
+
+int bx_system_create(const bx_desc* desc, const bx_reset_desc* reset,
+                     int device, bx_system** out);
+int bx_system_destroy(bx_system* sys);
+
+/* Physics only: B independent System.step calls (system.py:244-325).
+ * act: (B, action_size) with row stride act_stride. qp_in and qp_out may not
+ * alias. info may be NULL. */
+int bx_system_step(bx_system* sys, int64_t n_envs, const bx_qp* qp_in,
+                   const float* act, int64_t act_stride, const bx_qp* qp_out,
+                   const bx_info* info, void* stream);
+
+/* Env layer fused with physics: for each env, EpisodeWrapper-repeat
+ * action_repeat times (System.step + obs/reward/done/metrics), then the
+ * episode counters and the AutoReset select. in/out may not alias. */
+int bx_env_step(bx_system* sys, const bx_env_params* env, int64_t n_envs,
+                const bx_env_state* in, const float* act, int64_t act_stride,
+                const bx_env_state* out, void* stream);
+
+/* Batched System.default_qp from per-env joint angles/velocities
+ * (B, num_joint_dof) contiguous (system.py:112-242). */
+int bx_system_default_qp(bx_system* sys, int64_t n_envs,
+                         const float* joint_angle, const float* joint_velocity,
+                         const bx_qp* qp_out, void* stream);
+
+/* Batched reset-time Info (`_pbd_info`, system.py:327-340: Collider.apply). */
+int bx_system_info(bx_system* sys, int64_t n_envs, const bx_qp* qp,
+                   const bx_info* info, void* stream);
+
+/* Env observation of a state (Env._get_obs with the reset-time Info). */
+int bx_env_observe(bx_system* sys, const bx_env_params* env, int64_t n_envs,
+                   const bx_qp* qp, const float* act, int64_t act_stride,
+                   float* obs, void* stream);
+
+/* Counter-based uniform [lo,hi) fill keyed by (seed, global index); used for
+ * reset noise and synthetic actions (the JAX threefry stream is parity
+ * unpinned). */
+int bx_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
+               float lo, float hi, void* stream);
+
+/* Multi-rank episodic exchange is done over RCCL by the host (torch.distributed);
+ * no collective lives in this library. */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BRAX_AMD_H_ */

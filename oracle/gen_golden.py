@@ -1,0 +1,408 @@
+"""Golden-vector generator — TEST INFRASTRUCTURE ONLY, never shipped.
+
+Drives the reference's own numpy backend (`/root/reference/brax/jumpy.py:16-48`
+dispatches every op to numpy when no jax array is present) through the test-only
+stubs in `oracle/refstub/` and writes small `.npz` fixtures to `tests/golden/`:
+
+  desc_<env>.npz   the reference System's compiled constant arrays
+                   (`bodies.py:38-44`, `joints.py:418-474`, `actuators.py:115-164`,
+                   `colliders.py:891-1023`, `integrators.py:32-48`), in the
+                   descriptor layout of `brax_amd/system.py`.
+  traj_<env>.npz   seeded reset states + random-action rollouts of the unwrapped
+                   env (`Ant.step` `ant.py:222-255`, `Humanoid.step`
+                   `humanoid.py:246-280`) or of `System.step` (`system.py:244-325`).
+  wrap_ant.npz     an Episode+AutoReset wrapped rollout (`wrappers.py:83-148`).
+  kat.npz          known answers from the reference's own tests/functions.
+
+The reference computes in float64 here. The JAX PRNG is not
+available, so reset noise is numpy `default_rng` (`jumpy.py:408-460`) and is
+recorded explicitly: parity is defined on explicit states, never on seeds.
+
+Refuses to run when /root/reference is absent, so nothing reference-derived can
+run on the GPU box.
+"""
+import argparse
+import importlib
+import os
+import sys
+import time
+
+import numpy as np
+
+REF = '/root/reference'
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(os.path.dirname(HERE), 'tests', 'golden')
+
+
+def _setup():
+  if not os.path.isdir(os.path.join(REF, 'brax')):
+    raise SystemExit('gen_golden: /root/reference is absent; refusing to run')
+  sys.path[:0] = [os.path.join(HERE, 'refstub'), REF]
+  import warnings
+  warnings.simplefilter('ignore')
+
+
+# ---------------------------------------------------------------------------
+# descriptor dump (reference objects -> flat arrays)
+# ---------------------------------------------------------------------------
+
+def dump_desc(sys_):
+  """Flattens a reference brax.System into the brax_amd descriptor layout."""
+  from brax.physics import joints as rj
+  from brax.physics import actuators as ra
+  from brax.physics import colliders as rc
+  from brax.physics import geometry as rg
+  d = {}
+  body = sys_.body
+  integ = sys_.integrator
+  cfg = sys_.config
+  d['n_bodies'] = np.int32(sys_.num_bodies)
+  d['body_mass'] = np.asarray(body.mass, np.float64)
+  d['body_inv_inertia'] = np.asarray(body.inertia, np.float64)
+  d['pos_mask'] = np.asarray(integ.pos_mask, np.float64)
+  d['rot_mask'] = np.asarray(integ.rot_mask, np.float64)
+  d['quat_mask'] = np.asarray(integ.quat_mask, np.float64)
+  d['h'] = np.float64(integ.dt)
+  d['dt'] = np.float64(cfg.dt)
+  d['substeps'] = np.int32(cfg.substeps)
+  d['gravity'] = np.asarray(integ.gravity, np.float64)
+  d['velocity_damping'] = np.float64(integ.velocity_damping)
+  d['angular_damping'] = np.float64(integ.angular_damping)
+
+  jt, jd, jfree, jbp, jbc, joffp, joffc, jaxp, jaxc, jlim, jdamp = ([] for _ in range(11))
+  jsp, jsa, jgrp = [], [], []
+  joint_base = []
+  for g, j in enumerate(sys_.joints):
+    if not isinstance(j, (rj.Revolute, rj.Spherical)):
+      raise RuntimeError('unsupported joint type %r' % type(j))
+    n = len(j.body_p.idx)
+    joint_base.append(len(jt))
+    for k in range(n):
+      jt.append(1 if isinstance(j, rj.Revolute) else 3)
+      jd.append(j.dof)
+      jfree.append(j.free_dofs[k] if j.free_dofs is not None else -1)
+      jbp.append(j.body_p.idx[k])
+      jbc.append(j.body_c.idx[k])
+      joffp.append(j.off_p[k])
+      joffc.append(j.off_c[k])
+      jaxp.append(j.axis_p[k])
+      jaxc.append(j.axis_c[k])
+      lim = np.zeros((3, 2))
+      lim[:j.dof] = j.limit[k]
+      jlim.append(lim)
+      jdamp.append(j.angular_damping[k])
+      jsp.append(j.scale_pos[k])
+      jsa.append(j.scale_ang[k])
+      jgrp.append(g)
+  d['joint_type'] = np.asarray(jt, np.int32)
+  d['joint_dof'] = np.asarray(jd, np.int32)
+  d['joint_free_dofs'] = np.asarray(jfree, np.int32)
+  d['joint_body_p'] = np.asarray(jbp, np.int32)
+  d['joint_body_c'] = np.asarray(jbc, np.int32)
+  d['joint_off_p'] = np.asarray(joffp, np.float64).reshape(-1, 3)
+  d['joint_off_c'] = np.asarray(joffc, np.float64).reshape(-1, 3)
+  d['joint_axis_p'] = np.asarray(jaxp, np.float64).reshape(-1, 3, 3)
+  d['joint_axis_c'] = np.asarray(jaxc, np.float64).reshape(-1, 3, 3)
+  d['joint_limit'] = np.asarray(jlim, np.float64).reshape(-1, 3, 2)
+  d['joint_damping'] = np.asarray(jdamp, np.float64)
+  d['joint_scale_pos'] = np.asarray(jsp, np.float64)
+  d['joint_scale_ang'] = np.asarray(jsa, np.float64)
+  d['joint_group'] = np.asarray(jgrp, np.int32)
+
+  at, aj, astr, aidx, agrp = [], [], [], [], []
+  for g, a in enumerate(sys_.actuators):
+    # locate the joint group this actuator's joints came from
+    for k in range(len(a.strength)):
+      at.append(0 if isinstance(a, ra.Torque) else 1)
+      # global joint index: match by (parent, child) body indices
+      bp, bc = a.joint.body_p.idx[k], a.joint.body_c.idx[k]
+      cand = [i for i in range(len(jt)) if jbp[i] == bp and jbc[i] == bc]
+      aj.append(cand[0])
+      astr.append(a.strength[k])
+      idx = -np.ones(3, np.int64)
+      idx[:a.act_index.shape[1]] = a.act_index[k]
+      aidx.append(idx)
+      agrp.append(g)
+  d['act_type'] = np.asarray(at, np.int32)
+  d['act_joint'] = np.asarray(aj, np.int32)
+  d['act_strength'] = np.asarray(astr, np.float64)
+  d['act_index'] = np.asarray(aidx, np.int32).reshape(-1, 3)
+  d['act_group'] = np.asarray(agrp, np.int32)
+
+  goneway, gfn, gscale, gthr, gerp = [], [], [], [], []
+  rows = {k: [] for k in ('group', 'body_a', 'body_b', 'a_pos', 'a_end', 'a_radius',
+                          'b_pos', 'b_end', 'b_radius', 'friction', 'elasticity')}
+  for g, c in enumerate(sys_.colliders):
+    ca, cb = c.cull.get()
+    goneway.append(1 if isinstance(c, rc.OneWayCollider) else 0)
+    fn = c.contact_fn.__name__
+    gfn.append({'capsule_plane': 0, 'capsule_capsule': 1}[fn])
+    gscale.append(c.collide_scale)
+    gthr.append(c.velocity_threshold)
+    gerp.append(c.baumgarte_erp)
+    P = len(ca.body.idx)
+    for p in range(P):
+      ends = [ca.end[p]] if fn == 'capsule_capsule' else list(ca.end[p])
+      for e in ends:
+        rows['group'].append(g)
+        rows['body_a'].append(ca.body.idx[p])
+        rows['body_b'].append(cb.body.idx[p])
+        rows['a_pos'].append(ca.pos[p])
+        rows['a_end'].append(e)
+        rows['a_radius'].append(ca.radius[p])
+        rows['b_pos'].append(cb.pos[p])
+        rows['b_end'].append(cb.end[p] if fn == 'capsule_capsule' else np.zeros(3))
+        rows['b_radius'].append(cb.radius[p] if fn == 'capsule_capsule' else 0.)
+        rows['friction'].append(ca.friction[p] * cb.friction[p])
+        rows['elasticity'].append(ca.elasticity[p] * cb.elasticity[p])
+  d['col_oneway'] = np.asarray(goneway, np.int32)
+  d['col_fn'] = np.asarray(gfn, np.int32)
+  d['col_scale'] = np.asarray(gscale, np.float64)
+  d['col_velocity_threshold'] = np.asarray(gthr, np.float64)
+  d['col_baumgarte_erp'] = np.asarray(gerp, np.float64)
+  ints = ('group', 'body_a', 'body_b')
+  for k, v in rows.items():
+    if k in ints:
+      d['row_' + k] = np.asarray(v, np.int32)
+    else:
+      arr = np.asarray(v, np.float64)
+      d['row_' + k] = arr.reshape(-1, 3) if k.endswith(('pos', 'end')) else arr
+  return d
+
+
+def qp_pack(qp):
+  """QP -> (..., N, 13) float64: pos, rot(wxyz), vel, ang."""
+  return np.concatenate([np.asarray(qp.pos), np.asarray(qp.rot),
+                         np.asarray(qp.vel), np.asarray(qp.ang)], axis=-1)
+
+
+def qp_unpack(a):
+  from brax.physics.base import QP
+  a = np.asarray(a, np.float64)
+  return QP(pos=a[..., 0:3].copy(), rot=a[..., 3:7].copy(), vel=a[..., 7:10].copy(),
+            ang=a[..., 10:13].copy())
+
+
+# ---------------------------------------------------------------------------
+# trajectories
+# ---------------------------------------------------------------------------
+
+def env_traj(env, name, n_envs, n_steps, act_seed_base=10_000):
+  """Unwrapped env: reset from seeds 0..B-1, then T random-action steps."""
+  A = env.action_size
+  out = {k: [] for k in ('qp', 'obs', 'reward', 'done', 'metrics', 'info_contact',
+                         'info_actuator', 'contact_pos', 'contact_normal',
+                         'contact_penetration')}
+  qpos_l, qvel_l = [], []
+  states = []
+  from brax import jumpy as jp
+  for s in range(n_envs):
+    rng = np.array([s, 0], np.uint32)
+    # re-derive the reset noise exactly as Env.reset does (`ant.py:198-203`)
+    _, r1, r2 = jp.random_split(rng, 3)
+    qpos_l.append(env.sys.default_angle() + env._noise(r1))
+    qvel_l.append(env._noise(r2))
+    states.append(env.reset(rng))
+  acts = np.stack([np.random.default_rng(act_seed_base + t).uniform(-1, 1, (n_envs, A))
+                   for t in range(n_steps)])
+  metric_keys = sorted(states[0].metrics.keys())
+
+  def rec(sts, sys_infos):
+    out['qp'].append(np.stack([qp_pack(s.qp) for s in sts]))
+    out['obs'].append(np.stack([np.asarray(s.obs) for s in sts]))
+
+  rec(states, None)
+  reset_obs = out['obs'][0]
+  t0 = time.time()
+  for t in range(n_steps):
+    new = []
+    infos = []
+    for b, s in enumerate(states):
+      # capture the Info of the System.step that Env.step makes
+      captured = []
+      orig = env.sys.step
+      def spy(qp, act, _orig=orig):
+        r = _orig(qp, act)
+        captured.append(r[1])
+        return r
+      env.sys.step = spy
+      try:
+        new.append(env.step(s, acts[t, b]))
+      finally:
+        del env.sys.step
+      infos.append(captured[0])
+    states = new
+    rec(states, infos)
+    out['reward'].append(np.array([float(s.reward) for s in states]))
+    out['done'].append(np.array([float(s.done) for s in states]))
+    out['metrics'].append(np.array([[float(s.metrics[k]) for k in metric_keys]
+                                    for s in states]))
+    out['info_contact'].append(np.stack([np.concatenate(
+        [i.contact.vel, i.contact.ang], -1) for i in infos]))
+    out['info_actuator'].append(np.stack([np.concatenate(
+        [i.actuator.vel, i.actuator.ang], -1) for i in infos]))
+    out['contact_pos'].append(np.stack([i.contact_pos for i in infos]))
+    out['contact_normal'].append(np.stack([i.contact_normal for i in infos]))
+    out['contact_penetration'].append(np.stack([i.contact_penetration for i in infos]))
+    print(f'  {name}: step {t + 1}/{n_steps}  ({time.time() - t0:.1f}s)', flush=True)
+  res = {k: np.stack(v) for k, v in out.items() if v}
+  res['action'] = acts
+  res['reset_qpos'] = np.stack(qpos_l)
+  res['reset_qvel'] = np.stack(qvel_l)
+  res['reset_obs'] = reset_obs
+  res['metric_keys'] = np.array(metric_keys)
+  return res
+
+
+def sys_traj(sys_, name, qp0, n_envs, n_steps, act_scale, A, seed_base=20_000):
+  """Physics-only System.step rollout from a fixed state."""
+  out = {k: [] for k in ('qp', 'info_contact', 'info_actuator', 'contact_penetration')}
+  acts = np.stack([np.random.default_rng(seed_base + t).uniform(-1, 1, (n_envs, A))
+                   * act_scale for t in range(n_steps)])
+  qps = [qp0 for _ in range(n_envs)]
+  out['qp'].append(np.stack([qp_pack(q) for q in qps]))
+  t0 = time.time()
+  for t in range(n_steps):
+    res = [sys_.step(q, acts[t, b]) for b, q in enumerate(qps)]
+    qps = [r[0] for r in res]
+    out['qp'].append(np.stack([qp_pack(q) for q in qps]))
+    out['info_contact'].append(np.stack([np.concatenate(
+        [r[1].contact.vel, r[1].contact.ang], -1) for r in res]))
+    out['info_actuator'].append(np.stack([np.concatenate(
+        [r[1].actuator.vel, r[1].actuator.ang], -1) for r in res]))
+    out['contact_penetration'].append(np.stack([r[1].contact_penetration for r in res]))
+    print(f'  {name}: step {t + 1}/{n_steps}  ({time.time() - t0:.1f}s)', flush=True)
+  r = {k: np.stack(v) for k, v in out.items()}
+  r['action'] = acts
+  return r
+
+
+def ant_mountain_sys(count):
+  """Ant Mountain scene, as built in `notebooks/multiagent.ipynb` cell 3."""
+  from brax import envs
+  import brax
+  config = envs.create('ant').sys.config
+  repeat = count - 1
+  for lst in (config.bodies, config.joints, config.actuators):
+    for obj in list(lst):
+      if obj.name == 'Ground':
+        continue
+      for i in range(repeat):
+        new_obj = lst.add()
+        new_obj.CopyFrom(obj)
+        for attr in ('name', 'joint', 'parent', 'child'):
+          if hasattr(new_obj, attr):
+            setattr(new_obj, attr, f'{getattr(new_obj, attr)}_{i}')
+  default = config.defaults.add()
+  for i in range(repeat):
+    qp = default.qps.add(name=f'$ Torso_{i}')
+    qp.pos.x = np.sin(i * np.pi / 2)
+    qp.pos.y = np.cos(i * np.pi / 2)
+    qp.pos.z = (i + 1) * 2
+  del config.collide_include[:]
+  config.collider_cutoff = 0
+  return brax.System(config)
+
+
+def wrapped_ant(n_envs=8, n_steps=6, episode_length=3):
+  """Episode + AutoReset wrapped Ant (`envs/__init__.py:74-92`)."""
+  from brax import envs
+  env = envs.create('ant', episode_length=episode_length, auto_reset=True,
+                    batch_size=n_envs)
+  st = env.reset(np.array([7, 0], np.uint32))
+  out = {k: [] for k in ('qp', 'obs', 'reward', 'done', 'steps', 'truncation')}
+  out['first_qp'] = qp_pack(st.info['first_qp'])
+  out['first_obs'] = np.asarray(st.info['first_obs'])
+  def rec(s):
+    out['qp'].append(qp_pack(s.qp))
+    out['obs'].append(np.asarray(s.obs))
+    out['reward'].append(np.asarray(s.reward, np.float64))
+    out['done'].append(np.asarray(s.done, np.float64))
+    out['steps'].append(np.asarray(s.info['steps'], np.float64))
+    out['truncation'].append(np.asarray(s.info['truncation'], np.float64))
+  rec(st)
+  acts = np.stack([np.random.default_rng(30_000 + t).uniform(-1, 1, (n_envs, 8))
+                   for t in range(n_steps)])
+  # force an unhealthy env to exercise done-driven auto-reset: lift env 0's ant
+  for t in range(n_steps):
+    st = env.step(st, acts[t])
+    rec(st)
+  r = {k: (np.stack(v) if isinstance(v, list) else v) for k, v in out.items()}
+  r['action'] = acts
+  r['episode_length'] = np.int32(episode_length)
+  return r
+
+
+def kats():
+  """Known answers: the reference's own geometry/math functions."""
+  from brax import math as bm
+  from brax.physics import geometry as g
+  k = {}
+  rng = np.random.default_rng(123)
+  segs = rng.normal(size=(64, 4, 3))
+  # the reference's own test inputs (`geometry_test.py:217-272`)
+  segs[0] = [[0., 0., -1.], [0., 0., 1.], [1., 2., -1.], [-1., -2., 1.]]
+  a_best, b_best = [], []
+  for s in segs:
+    a, b = g.closest_segment_to_segment_points(*s)
+    a_best.append(a)
+    b_best.append(b)
+  k['seg_in'] = segs
+  k['seg_a'] = np.array(a_best)
+  k['seg_b'] = np.array(b_best)
+  v = rng.normal(size=(32, 3))
+  q = rng.normal(size=(32, 4))
+  q /= np.linalg.norm(q, axis=-1, keepdims=True)
+  k['rot_v'], k['rot_q'] = v, q
+  k['rot_out'] = np.array([bm.rotate(a, b) for a, b in zip(v, q)])
+  e = rng.uniform(-180, 180, size=(32, 3))
+  k['euler_in'] = e
+  k['euler_quat'] = np.array([bm.euler_to_quat(x) for x in e])
+  return k
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument('--only', default='')
+  args = ap.parse_args()
+  _setup()
+  os.makedirs(OUT, exist_ok=True)
+  from brax import envs
+  from brax.envs import ant as ant_mod
+  only = set(args.only.split(',')) if args.only else None
+
+  def want(n):
+    return only is None or n in only
+
+  def save(name, d):
+    path = os.path.join(OUT, name + '.npz')
+    np.savez_compressed(path, **d)
+    print('wrote', path, os.path.getsize(path), 'bytes', flush=True)
+
+  if want('kat'):
+    save('kat', kats())
+  if want('ant'):
+    env = ant_mod.Ant(use_contact_forces=True)
+    save('desc_ant', dump_desc(env.sys))
+    save('traj_ant', env_traj(env, 'ant', 64, 8))
+  if want('humanoid'):
+    env = importlib.import_module('brax.envs.humanoid').Humanoid()
+    save('desc_humanoid', dump_desc(env.sys))
+    save('traj_humanoid', env_traj(env, 'humanoid', 16, 4))
+  if want('halfcheetah'):
+    env = envs.get_environment('halfcheetah')
+    save('desc_halfcheetah', dump_desc(env.sys))
+    save('traj_halfcheetah', env_traj(env, 'halfcheetah', 16, 4))
+  if want('wrap'):
+    save('wrap_ant', wrapped_ant())
+  for n in (1, 2, 4):
+    if want(f'mountain{n}'):
+      s = ant_mountain_sys(n)
+      save(f'desc_mountain{n}', dump_desc(s))
+      B, T = {1: (4, 4), 2: (2, 3), 4: (1, 2)}[n]
+      save(f'traj_mountain{n}', sys_traj(s, f'mountain{n}', s.default_qp(), B, T,
+                                         1.0, 8 * n))
+
+
+if __name__ == '__main__':
+  main()

@@ -1,0 +1,138 @@
+"""ctypes front-end of the C restatement (oracle/pbd_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, `__graft_entry__.smoke()` and
+bench.py's cpu_baseline leg — never by the `brax_amd` product package.
+
+    o = Oracle(desc, reset_desc, dtype=np.float64)
+    qp1, info = o.system_step(qp0, act)          # qp (B,N,13) pos|rot|vel|ang
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from brax_amd import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, '_build', 'liboracle.so')
+
+ENV_KIND = {'none': 0, 'ant': 1, 'humanoid': 2, 'halfcheetah': 3}
+
+
+def build():
+  subprocess.run(['make', '-s', '-C', HERE], check=True)
+
+
+def _load():
+  if not os.path.exists(LIB):
+    build()
+  lib = C.CDLL(LIB)
+  return lib
+
+
+_LIB = None
+
+
+def lib():
+  global _LIB
+  if _LIB is None:
+    _LIB = _load()
+  return _LIB
+
+
+def _p(a):
+  return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Oracle:
+  """C restatement at float64 (checker) or float32 (CPU baseline)."""
+
+  def __init__(self, desc, reset_desc=None, dtype=np.float64, safe_guard=True):
+    self.dtype = np.dtype(dtype)
+    self.suf = '_f64' if self.dtype == np.float64 else '_f32'
+    self.desc = dict(desc)
+    self.cdesc, self._keep = abi.make_desc(self.desc)
+    self.N = int(desc['n_bodies'])
+    self.R = len(desc['row_group'])
+    self.A = int(desc.get('action_size', 0))
+    if reset_desc is not None:
+      self.creset, self._keep_r = abi.make_reset_desc(reset_desc)
+    else:
+      self.creset = None
+    self._fn('oracle_set_safe_norm_guard')(C.c_int(1 if safe_guard else 0))
+
+  def _fn(self, name):
+    return getattr(lib(), name + self.suf)
+
+  def _a(self, x):
+    return np.ascontiguousarray(np.asarray(x, self.dtype))
+
+  def set_threads(self, n):
+    self._fn('oracle_set_threads')(C.c_int(n))
+
+  def max_threads(self):
+    return int(self._fn('oracle_max_threads')())
+
+  def system_step(self, qp, act):
+    qp = self._a(qp)
+    B = qp.shape[0]
+    act = self._a(act).reshape(B, -1)
+    assert act.shape[1] == self.A, (act.shape, self.A)
+    out = np.empty_like(qp)
+    ic = np.empty((B, self.N, 6), self.dtype)
+    ia = np.empty((B, self.N, 6), self.dtype)
+    cp = np.empty((B, self.R, 3), self.dtype)
+    cn = np.empty((B, self.R, 3), self.dtype)
+    pen = np.empty((B, self.R), self.dtype)
+    self._fn('oracle_system_step')(C.byref(self.cdesc), C.c_int64(B), _p(qp), _p(act),
+                                   _p(out), _p(ic), _p(ia), _p(cp), _p(cn), _p(pen))
+    return out, dict(contact=ic, actuator=ia, contact_pos=cp, contact_normal=cn,
+                     contact_penetration=pen)
+
+  def system_info(self, qp):
+    qp = self._a(qp)
+    B = qp.shape[0]
+    ic = np.empty((B, self.N, 6), self.dtype)
+    self._fn('oracle_system_info')(C.byref(self.cdesc), C.c_int64(B), _p(qp), _p(ic))
+    return ic
+
+  def env_obs(self, kind, qp, info_contact, act, obs_size):
+    qp = self._a(qp)
+    B = qp.shape[0]
+    ic = self._a(info_contact)
+    act = self._a(act).reshape(B, -1)
+    obs = np.empty((B, obs_size), self.dtype)
+    rc = self._fn('oracle_env_obs')(C.byref(self.cdesc), C.c_int(ENV_KIND[kind]),
+                                    C.c_int64(B), _p(qp), _p(ic), _p(act), _p(obs),
+                                    C.c_int(obs_size))
+    if rc:
+      raise ValueError('obs size mismatch')
+    return obs
+
+  def env_step(self, kind, qp, act, obs_size, n_metrics, done=None):
+    qp = self._a(qp)
+    B = qp.shape[0]
+    act = self._a(act).reshape(B, -1)
+    out = np.empty_like(qp)
+    obs = np.empty((B, obs_size), self.dtype)
+    rew = np.empty(B, self.dtype)
+    dn = self._a(np.zeros(B) if done is None else done).copy()
+    met = np.zeros((B, n_metrics), self.dtype)
+    rc = self._fn('oracle_env_step')(C.byref(self.cdesc), C.c_int(ENV_KIND[kind]),
+                                     C.c_int64(B), _p(qp), _p(act), _p(out), _p(obs),
+                                     C.c_int(obs_size), _p(rew), _p(dn), _p(met),
+                                     C.c_int(n_metrics))
+    if rc:
+      raise ValueError('obs size mismatch')
+    return out, obs, rew, dn, met
+
+  def default_qp(self, angles, vels):
+    assert self.creset is not None
+    angles = self._a(angles)
+    vels = self._a(vels)
+    B = angles.shape[0]
+    out = np.empty((B, self.N, 13), self.dtype)
+    self._fn('oracle_default_qp')(C.byref(self.cdesc), C.byref(self.creset),
+                                  C.c_int64(B), _p(angles), _p(vels), _p(out))
+    return out

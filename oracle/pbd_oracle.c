@@ -1,0 +1,1497 @@
+/*
+ * pbd_oracle.c — CPU RESTATEMENT OF THE REFERENCE, TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of the reference's position-based-dynamics step
+ * (`brax/physics/system.py:254-325`) and the Ant/Humanoid/HalfCheetah env
+ * layer, compiled twice: REAL=double (the checker, pinned to the reference's
+ * own float64 numpy execution by tests/golden/*.npz) and REAL=float (the CPU
+ * baseline timed by bench.py, OpenMP over envs). Only tests/, smoke() and
+ * bench.py's cpu_baseline leg may load it; the product path never does.
+ *
+ * Each function cites the reference file:line it restates. Array layout here
+ * is the oracle's own: qp (B,N,13) = pos, rot(wxyz), vel, ang.
+ */
+#define _USE_MATH_DEFINES
+#include <math.h>
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/brax_amd.h"
+
+#ifndef REAL
+#define REAL double
+#endif
+#ifndef SUF
+#define SUF _f64
+#endif
+#define CAT2(a, b) a##b
+#define CAT(a, b) CAT2(a, b)
+#define FN(name) CAT(name, SUF)
+
+typedef REAL R;
+
+/* 1: emulate jnp safe_norm's allclose(x, 0) zero guard (jumpy.py:183-189);
+ * 0: plain norm, as the numpy backend the goldens come from (jumpy.py:190). */
+static int g_safe_guard = 1;
+
+void FN(oracle_set_safe_norm_guard)(int on) { g_safe_guard = on; }
+void FN(oracle_set_threads)(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}
+int FN(oracle_max_threads)(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+/* ---------------------------------------------------------------- math --- */
+/* brax/math.py and the jumpy helpers it uses */
+
+static inline R dot3(const R* a, const R* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static inline void cross3(const R* a, const R* b, R* o) {
+  R x = a[1] * b[2] - a[2] * b[1];
+  R y = a[2] * b[0] - a[0] * b[2];
+  R z = a[0] * b[1] - a[1] * b[0];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+static inline R norm3(const R* a) { return (R)sqrt(dot3(a, a)); }
+/* jumpy.py:170-192 */
+static inline R safe_norm3(const R* a) {
+  if (g_safe_guard && fabs((double)a[0]) <= 1e-8 && fabs((double)a[1]) <= 1e-8 &&
+      fabs((double)a[2]) <= 1e-8)
+    return (R)0;
+  return norm3(a);
+}
+/* math.py:25-40 */
+static inline void rotate(const R* v, const R* q, R* o) {
+  R s = q[0];
+  const R* u = q + 1;
+  R uv = dot3(u, v), uu = dot3(u, u);
+  R c[3];
+  cross3(u, v, c);
+  R r0 = 2 * (uv * u[0]) + (s * s - uu) * v[0];
+  R r1 = 2 * (uv * u[1]) + (s * s - uu) * v[1];
+  R r2 = 2 * (uv * u[2]) + (s * s - uu) * v[2];
+  o[0] = r0 + 2 * s * c[0];
+  o[1] = r1 + 2 * s * c[1];
+  o[2] = r2 + 2 * s * c[2];
+}
+/* math.py:130-145 */
+static inline void quat_mul(const R* u, const R* v, R* o) {
+  R w = u[0] * v[0] - u[1] * v[1] - u[2] * v[2] - u[3] * v[3];
+  R x = u[0] * v[1] + u[1] * v[0] + u[2] * v[3] - u[3] * v[2];
+  R y = u[0] * v[2] - u[1] * v[3] + u[2] * v[0] + u[3] * v[1];
+  R z = u[0] * v[3] + u[1] * v[2] - u[2] * v[1] + u[3] * v[0];
+  o[0] = w; o[1] = x; o[2] = y; o[3] = z;
+}
+/* math.py:148-170 */
+static inline void vec_quat_mul(const R* u, const R* v, R* o) {
+  R w = -u[0] * v[1] - u[1] * v[2] - u[2] * v[3];
+  R x = u[0] * v[0] + u[1] * v[3] - u[2] * v[2];
+  R y = -u[0] * v[3] + u[1] * v[0] + u[2] * v[1];
+  R z = u[0] * v[2] - u[1] * v[1] + u[2] * v[0];
+  o[0] = w; o[1] = x; o[2] = y; o[3] = z;
+}
+/* math.py:173-187 */
+static inline void quat_rot_axis(const R* axis, R angle, R* o) {
+  R s = (R)sin(angle / 2), c = (R)cos(angle / 2);
+  o[0] = c; o[1] = axis[0] * s; o[2] = axis[1] * s; o[3] = axis[2] * s;
+}
+/* math.py:190-199 */
+static inline void quat_inv(const R* q, R* o) { o[0] = q[0]; o[1] = -q[1]; o[2] = -q[2]; o[3] = -q[3]; }
+/* math.py:116-127 */
+static inline R signed_angle(const R* axis, const R* ref_p, const R* ref_c) {
+  R c[3];
+  cross3(ref_p, ref_c, c);
+  return (R)atan2(dot3(c, axis), dot3(ref_p, ref_c));
+}
+static inline R clip(R x, R lo, R hi) { return x < lo ? lo : (x > hi ? hi : x); }
+static inline R sgn(R x) { return (R)((x > 0) - (x < 0)); }
+
+/* ----------------------------------------------------------- descriptor --- */
+/* the descriptor's float64 constants, cast once to REAL (jit casts the
+ * Python-double constants to fp32 the same way) */
+typedef struct {
+  const bx_desc* d;
+  int N, J, K, Rn, G, A;
+  R h, g[3], vdamp_exp, adamp_exp;
+  R *mass, *inv_mass, *I, *pos_mask, *rot_mask, *quat_mask;
+  R *joff_p, *joff_c, *jax_p, *jax_c, *jlim, *jdamp, *jsp, *jsa;
+  R *astr;
+  R *gscale, *gthr, *gerp;
+  R *ra_pos, *ra_end, *ra_rad, *rb_pos, *rb_end, *rb_rad, *rfric, *relas;
+} sysc;
+
+static R* cvt(const double* s, int n) {
+  R* o = (R*)malloc(sizeof(R) * (n > 0 ? n : 1));
+  for (int i = 0; i < n; i++) o[i] = (R)s[i];
+  return o;
+}
+
+static void sys_init(sysc* s, const bx_desc* d) {
+  s->d = d;
+  s->N = d->n_bodies; s->J = d->n_joints; s->K = d->n_actuators;
+  s->Rn = d->n_rows; s->G = d->n_groups; s->A = d->action_size;
+  s->h = (R)d->h;
+  for (int k = 0; k < 3; k++) s->g[k] = (R)d->gravity[k];
+  /* integrators.py:87,91: exp(damping * dt) of Python floats -> a constant */
+  s->vdamp_exp = (R)exp(d->velocity_damping * d->h);
+  s->adamp_exp = (R)exp(d->angular_damping * d->h);
+  int N = s->N, J = s->J, Rn = s->Rn;
+  s->mass = cvt(d->body_mass, N);
+  s->inv_mass = (R*)malloc(sizeof(R) * (N ? N : 1));
+  for (int i = 0; i < N; i++) s->inv_mass[i] = (R)(1.0 / d->body_mass[i]);
+  s->I = cvt(d->body_inv_inertia, 3 * N);
+  s->pos_mask = cvt(d->pos_mask, 3 * N);
+  s->rot_mask = cvt(d->rot_mask, 3 * N);
+  s->quat_mask = cvt(d->quat_mask, 4 * N);
+  s->joff_p = cvt(d->joint_off_p, 3 * J);
+  s->joff_c = cvt(d->joint_off_c, 3 * J);
+  s->jax_p = cvt(d->joint_axis_p, 9 * J);
+  s->jax_c = cvt(d->joint_axis_c, 9 * J);
+  s->jlim = cvt(d->joint_limit, 6 * J);
+  s->jdamp = cvt(d->joint_damping, J);
+  s->jsp = cvt(d->joint_scale_pos, J);
+  s->jsa = cvt(d->joint_scale_ang, J);
+  s->astr = cvt(d->act_strength, s->K);
+  s->gscale = cvt(d->col_scale, s->G);
+  s->gthr = cvt(d->col_velocity_threshold, s->G);
+  s->gerp = cvt(d->col_baumgarte_erp, s->G);
+  s->ra_pos = cvt(d->row_a_pos, 3 * Rn);
+  s->ra_end = cvt(d->row_a_end, 3 * Rn);
+  s->ra_rad = cvt(d->row_a_radius, Rn);
+  s->rb_pos = cvt(d->row_b_pos, 3 * Rn);
+  s->rb_end = cvt(d->row_b_end, 3 * Rn);
+  s->rb_rad = cvt(d->row_b_radius, Rn);
+  s->rfric = cvt(d->row_friction, Rn);
+  s->relas = cvt(d->row_elasticity, Rn);
+}
+
+static void sys_free(sysc* s) {
+  R** p[] = {&s->mass, &s->inv_mass, &s->I, &s->pos_mask, &s->rot_mask, &s->quat_mask,
+             &s->joff_p, &s->joff_c, &s->jax_p, &s->jax_c, &s->jlim, &s->jdamp,
+             &s->jsp, &s->jsa, &s->astr, &s->gscale, &s->gthr, &s->gerp,
+             &s->ra_pos, &s->ra_end, &s->ra_rad, &s->rb_pos, &s->rb_end,
+             &s->rb_rad, &s->rfric, &s->relas};
+  for (size_t i = 0; i < sizeof(p) / sizeof(p[0]); i++) free(*p[i]);
+}
+
+/* ------------------------------------------------------------ state ------ */
+typedef struct { R pos[3], rot[4], vel[3], ang[3]; } body_t;
+
+/* workspace per env */
+typedef struct {
+  body_t *qp, *qprev, *qrb;
+  R *dp_a, *dp_j, *acc;          /* (N,3) angular */
+  R *dq_pos, *dq_rot;            /* (N,3),(N,4) */
+  R *dp_vel, *dp_ang;            /* (N,3) */
+  R *cnt;                        /* (N) */
+  R *gpos, *grot, *gvel, *gang;  /* per-group scratch (N,3/4) */
+  R *c_pos, *c_norm, *c_pen, *c_vel, *dlam; /* contact rows */
+  R *info_c, *info_a;            /* (N,6) accumulators */
+} work_t;
+
+static void work_alloc(work_t* w, int N, int Rn) {
+  int n = N > 0 ? N : 1, r = Rn > 0 ? Rn : 1;
+  w->qp = calloc(n, sizeof(body_t)); w->qprev = calloc(n, sizeof(body_t));
+  w->qrb = calloc(n, sizeof(body_t));
+  w->dp_a = calloc(3 * n, sizeof(R)); w->dp_j = calloc(3 * n, sizeof(R));
+  w->acc = calloc(3 * n, sizeof(R));
+  w->dq_pos = calloc(3 * n, sizeof(R)); w->dq_rot = calloc(4 * n, sizeof(R));
+  w->dp_vel = calloc(3 * n, sizeof(R)); w->dp_ang = calloc(3 * n, sizeof(R));
+  w->cnt = calloc(n, sizeof(R));
+  w->gpos = calloc(3 * n, sizeof(R)); w->grot = calloc(4 * n, sizeof(R));
+  w->gvel = calloc(3 * n, sizeof(R)); w->gang = calloc(3 * n, sizeof(R));
+  w->c_pos = calloc(3 * r, sizeof(R)); w->c_norm = calloc(3 * r, sizeof(R));
+  w->c_pen = calloc(r, sizeof(R)); w->c_vel = calloc(3 * r, sizeof(R));
+  w->dlam = calloc(r, sizeof(R));
+  w->info_c = calloc(6 * n, sizeof(R)); w->info_a = calloc(6 * n, sizeof(R));
+}
+static void work_free(work_t* w) {
+  void* p[] = {w->qp, w->qprev, w->qrb, w->dp_a, w->dp_j, w->acc, w->dq_pos, w->dq_rot,
+               w->dp_vel, w->dp_ang, w->cnt, w->gpos, w->grot, w->gvel, w->gang,
+               w->c_pos, w->c_norm, w->c_pen, w->c_vel, w->dlam, w->info_c, w->info_a};
+  for (size_t i = 0; i < sizeof(p) / sizeof(p[0]); i++) free(p[i]);
+}
+
+static void load_qp(body_t* qp, const R* src, int N) {
+  for (int b = 0; b < N; b++) {
+    const R* s = src + 13 * b;
+    memcpy(qp[b].pos, s, 3 * sizeof(R)); memcpy(qp[b].rot, s + 3, 4 * sizeof(R));
+    memcpy(qp[b].vel, s + 7, 3 * sizeof(R)); memcpy(qp[b].ang, s + 10, 3 * sizeof(R));
+  }
+}
+static void store_qp(const body_t* qp, R* dst, int N) {
+  for (int b = 0; b < N; b++) {
+    R* s = dst + 13 * b;
+    memcpy(s, qp[b].pos, 3 * sizeof(R)); memcpy(s + 3, qp[b].rot, 4 * sizeof(R));
+    memcpy(s + 7, qp[b].vel, 3 * sizeof(R)); memcpy(s + 10, qp[b].ang, 3 * sizeof(R));
+  }
+}
+
+/* -------------------------------------------------------------- joints --- */
+
+/* Revolute.axis_angle (joints.py:311-319) / Spherical.axis_angle (:388-415) */
+static int axis_angle(const sysc* s, int j, const body_t* p, const body_t* c,
+                      R axes[3][3], R ang[3]) {
+  const R* axp = s->jax_p + 9 * j;
+  const R* axc = s->jax_c + 9 * j;
+  if (s->d->joint_type[j] == BX_JOINT_REVOLUTE) {
+    R ref_p[3], ref_c[3];
+    rotate(axp, p->rot, axes[0]);
+    rotate(axp + 6, p->rot, ref_p);
+    rotate(axc + 6, c->rot, ref_c);
+    ang[0] = signed_angle(axes[0], ref_p, ref_c);
+    return 1;
+  }
+  R a1p[3], a2p[3], a1c[3], a2c[3], a3c[3];
+  rotate(axp, p->rot, a1p);
+  rotate(axp + 3, p->rot, a2p);
+  rotate(axc, c->rot, a1c);
+  rotate(axc + 3, c->rot, a2c);
+  rotate(axc + 6, c->rot, a3c);
+  R lon[3];
+  cross3(a3c, a1p, lon);
+  R ln = (R)1e-10 + safe_norm3(lon);
+  for (int k = 0; k < 3; k++) lon[k] /= ln;
+  R psi = signed_angle(a1p, a2p, lon);
+  R d11 = dot3(a1p, a1c), d12 = dot3(a1p, a2c);
+  R xz[3];
+  for (int k = 0; k < 3; k++) xz[k] = d11 * a1c[k] + d12 * a2c[k];
+  R xn = (R)1e-10 + safe_norm3(xz);
+  for (int k = 0; k < 3; k++) xz[k] /= xn;
+  R cb = dot3(xz, a1p);
+  R theta = (R)acos(clip(cb, -1, 1)) * sgn(dot3(a1p, a3c));
+  R ycn[3] = {-a3c[0], -a3c[1], -a3c[2]};
+  R phi = signed_angle(ycn, a2c, lon);
+  memcpy(axes[0], a1p, sizeof(a1p));
+  memcpy(axes[1], a2c, sizeof(a2c));
+  memcpy(axes[2], a3c, sizeof(a3c));
+  ang[0] = psi; ang[1] = theta; ang[2] = phi;
+  return 3;
+}
+
+/* Joint.apply_angle_update (joints.py:130-152); accumulates into dq (7 per side) */
+static void angle_update(const sysc* s, int j, const body_t* p, const body_t* c,
+                         const R* dq, R* out_p, R* out_c) {
+  int bp = s->d->joint_body_p[j], bc = s->d->joint_body_c[j];
+  const R* Ip = s->I + 3 * bp;
+  const R* Ic = s->I + 3 * bc;
+  R th = safe_norm3(dq);
+  R n[3];
+  for (int k = 0; k < 3; k++) n[k] = dq[k] / (th + (R)1e-6);
+  R w1 = n[0] * (Ip[0] * n[0]) + n[1] * (Ip[1] * n[1]) + n[2] * (Ip[2] * n[2]);
+  R w2 = n[0] * (Ic[0] * n[0]) + n[1] * (Ic[1] * n[1]) + n[2] * (Ic[2] * n[2]);
+  R dl = -th / (w1 + w2 + (R)1e-6);
+  R pv[3] = {-dl * n[0], -dl * n[1], -dl * n[2]};
+  R t[3], q[4];
+  R sa = s->jsa[j];
+  for (int k = 0; k < 3; k++) t[k] = Ip[k] * pv[k];
+  vec_quat_mul(t, p->rot, q);
+  for (int k = 0; k < 4; k++) out_p[3 + k] += sa * ((R)0.5 * q[k]);
+  for (int k = 0; k < 3; k++) t[k] = Ic[k] * pv[k];
+  vec_quat_mul(t, c->rot, q);
+  for (int k = 0; k < 4; k++) out_c[3 + k] += sa * ((R)-0.5 * q[k]);
+  /* dq pos is scale_ang * zeros: adds exact zeros */
+}
+
+/* Joint.apply_position_update (joints.py:154-195) */
+static void position_update(const sysc* s, int j, const body_t* p, const body_t* c,
+                            const R* pos_p_w, const R* pos_c_w, R* out_p, R* out_c) {
+  int bp = s->d->joint_body_p[j], bc = s->d->joint_body_c[j];
+  const R* Ip = s->I + 3 * bp;
+  const R* Ic = s->I + 3 * bc;
+  R dx[3], rp[3], rc[3];
+  for (int k = 0; k < 3; k++) {
+    dx[k] = pos_p_w[k] - pos_c_w[k];
+    rp[k] = pos_p_w[k] - p->pos[k];
+    rc[k] = pos_c_w[k] - c->pos[k];
+  }
+  R cc = safe_norm3(dx);
+  R n[3];
+  for (int k = 0; k < 3; k++) n[k] = dx[k] / (cc + (R)1e-6);
+  R cr1[3], cr2[3];
+  cross3(rp, n, cr1);
+  cross3(rc, n, cr2);
+  R w1 = (R)1 / s->mass[bp] +
+         (cr1[0] * (Ip[0] * cr1[0]) + cr1[1] * (Ip[1] * cr1[1]) + cr1[2] * (Ip[2] * cr1[2]));
+  R w2 = (R)1 / s->mass[bc] +
+         (cr2[0] * (Ic[0] * cr2[0]) + cr2[1] * (Ic[1] * cr2[1]) + cr2[2] * (Ic[2] * cr2[2]));
+  R dl = -cc / (w1 + w2 + (R)1e-6);
+  R pv[3] = {dl * n[0], dl * n[1], dl * n[2]};
+  R sp = s->jsp[j];
+  R t[3], u[3], q[4];
+  cross3(rp, pv, t);
+  for (int k = 0; k < 3; k++) u[k] = Ip[k] * t[k];
+  vec_quat_mul(u, p->rot, q);
+  for (int k = 0; k < 3; k++) out_p[k] += sp * (pv[k] / s->mass[bp]);
+  for (int k = 0; k < 4; k++) out_p[3 + k] += sp * ((R)0.5 * q[k]);
+  cross3(rc, pv, t);
+  for (int k = 0; k < 3; k++) u[k] = Ic[k] * t[k];
+  vec_quat_mul(u, c->rot, q);
+  for (int k = 0; k < 3; k++) out_c[k] += sp * (-pv[k] / s->mass[bc]);
+  for (int k = 0; k < 4; k++) out_c[3 + k] += sp * ((R)-0.5 * q[k]);
+}
+
+/* Revolute.apply_reduced (joints.py:270-309), Spherical (:332-386).
+ * out_p/out_c: 7 (pos3, rot4) zero-initialised */
+static void joint_apply_one(const sysc* s, int j, const body_t* qp, R* out_p, R* out_c) {
+  const bx_desc* d = s->d;
+  const body_t* p = &qp[d->joint_body_p[j]];
+  const body_t* c = &qp[d->joint_body_c[j]];
+  const R* axp = s->jax_p + 9 * j;
+  const R* axc = s->jax_c + 9 * j;
+  const R* lim = s->jlim + 6 * j;
+  R pw[3], cw[3];
+  rotate(s->joff_p + 3 * j, p->rot, pw);
+  rotate(s->joff_c + 3 * j, c->rot, cw);
+  for (int k = 0; k < 3; k++) { pw[k] += p->pos[k]; cw[k] += c->pos[k]; }
+  position_update(s, j, p, c, pw, cw, out_p, out_c);
+  if (d->joint_type[j] == BX_JOINT_REVOLUTE) {
+    R axis[3], ref_p[3], ref_c[3], axis_c[3];
+    rotate(axp, p->rot, axis);
+    rotate(axp + 6, p->rot, ref_p);
+    rotate(axc + 6, c->rot, ref_c);
+    R psi = signed_angle(axis, ref_p, ref_c);
+    rotate(axc, c->rot, axis_c);
+    R dq1[3], dq2[3], fix[4], n1[3];
+    cross3(axis, axis_c, dq1);
+    R ph = clip(psi, lim[0], lim[1]);
+    quat_rot_axis(axis, ph, fix);
+    rotate(ref_p, fix, n1);
+    cross3(n1, ref_c, dq2);
+    /* v_apply over [dq_1, dq_2], summed then added (joints.py:299-307) */
+    R ap[2][7] = {{0}}, ac[2][7] = {{0}};
+    angle_update(s, j, p, c, dq1, ap[0], ac[0]);
+    angle_update(s, j, p, c, dq2, ap[1], ac[1]);
+    for (int k = 0; k < 7; k++) {
+      out_p[k] += ap[0][k] + ap[1][k];
+      out_c[k] += ac[0][k] + ac[1][k];
+    }
+    return;
+  }
+  /* Spherical */
+  R a1p[3], a2p[3], a1c[3], a2c[3], a3c[3];
+  rotate(axp, p->rot, a1p);
+  rotate(axp + 3, p->rot, a2p);
+  rotate(axc, c->rot, a1c);
+  rotate(axc + 3, c->rot, a2c);
+  rotate(axc + 6, c->rot, a3c);
+  R lon[3];
+  cross3(a3c, a1p, lon);
+  R ln = (R)1e-6 + safe_norm3(lon);
+  for (int k = 0; k < 3; k++) lon[k] /= ln;
+  R d11 = dot3(a1p, a1c), d12 = dot3(a1p, a2c);
+  R xz[3];
+  for (int k = 0; k < 3; k++) xz[k] = d11 * a1c[k] + d12 * a2c[k];
+  R xn = (R)1e-6 + safe_norm3(xz);
+  for (int k = 0; k < 3; k++) xz[k] /= xn;
+  R a2n[3];
+  cross3(xz, a1p, a2n);
+  R an = (R)1e-6 + safe_norm3(a2n);
+  for (int k = 0; k < 3; k++) a2n[k] /= an;
+  R sg = sgn(dot3(a1p, a3c));
+  R nvec[3][3], n1v[3][3], n2v[3][3];
+  for (int k = 0; k < 3; k++) {
+    nvec[0][k] = a1p[k]; n1v[0][k] = a2p[k]; n2v[0][k] = lon[k];
+    nvec[1][k] = -a2n[k] * sg; n1v[1][k] = a1p[k]; n2v[1][k] = xz[k];
+    nvec[2][k] = -(-a3c[k]); n1v[2][k] = lon[k]; n2v[2][k] = a2c[k];
+  }
+  R acc_p[7] = {0}, acc_c[7] = {0};
+  for (int l = 0; l < 3; l++) {
+    /* limit_angle (joints.py:343-355) */
+    R ph = signed_angle(nvec[l], n1v[l], n2v[l]);
+    R lo = lim[2 * l], hi = lim[2 * l + 1];
+    R mask = ph < lo ? (R)1 : (R)0;
+    mask = ph > hi ? (R)1 : mask;
+    ph = clip(ph, lo, hi);
+    R fix[4], n1[3], dq[3];
+    quat_rot_axis(nvec[l], ph, fix);
+    rotate(n1v[l], fix, n1);
+    cross3(n1, n2v[l], dq);
+    for (int k = 0; k < 3; k++) dq[k] *= mask;
+    R ap[7] = {0}, ac[7] = {0};
+    angle_update(s, j, p, c, dq, ap, ac);
+    for (int k = 0; k < 7; k++) { acc_p[k] += ap[k]; acc_c[k] += ac[k]; }
+  }
+  for (int k = 0; k < 7; k++) { out_p[k] += acc_p[k]; out_c[k] += acc_c[k]; }
+}
+
+/* Joint.apply (joints.py:79-100), summed over joint groups (system.py:272) */
+static void joints_apply(const sysc* s, work_t* w) {
+  int N = s->N, J = s->J;
+  memset(w->dq_pos, 0, sizeof(R) * 3 * N);
+  memset(w->dq_rot, 0, sizeof(R) * 4 * N);
+  int j0 = 0;
+  while (j0 < J) {
+    int g = s->d->joint_group[j0], j1 = j0;
+    while (j1 < J && s->d->joint_group[j1] == g) j1++;
+    memset(w->gpos, 0, sizeof(R) * 3 * N);
+    memset(w->grot, 0, sizeof(R) * 4 * N);
+    R (*op)[7] = calloc(j1 - j0, sizeof(R[7]));
+    R (*oc)[7] = calloc(j1 - j0, sizeof(R[7]));
+    for (int j = j0; j < j1; j++) joint_apply_one(s, j, w->qp, op[j - j0], oc[j - j0]);
+    /* segment_sum over concat(parents, children) */
+    for (int j = j0; j < j1; j++) {
+      int b = s->d->joint_body_p[j];
+      for (int k = 0; k < 3; k++) w->gpos[3 * b + k] += op[j - j0][k];
+      for (int k = 0; k < 4; k++) w->grot[4 * b + k] += op[j - j0][3 + k];
+    }
+    for (int j = j0; j < j1; j++) {
+      int b = s->d->joint_body_c[j];
+      for (int k = 0; k < 3; k++) w->gpos[3 * b + k] += oc[j - j0][k];
+      for (int k = 0; k < 4; k++) w->grot[4 * b + k] += oc[j - j0][3 + k];
+    }
+    for (int i = 0; i < 3 * N; i++) w->dq_pos[i] += w->gpos[i];
+    for (int i = 0; i < 4 * N; i++) w->dq_rot[i] += w->grot[i];
+    free(op); free(oc);
+    j0 = j1;
+  }
+}
+
+/* Joint.damp (joints.py:103-128), per group, summed into dp_j */
+static void joints_damp(const sysc* s, work_t* w) {
+  int N = s->N, J = s->J;
+  memset(w->dp_j, 0, sizeof(R) * 3 * N);
+  int j0 = 0;
+  while (j0 < J) {
+    int g = s->d->joint_group[j0], j1 = j0;
+    while (j1 < J && s->d->joint_group[j1] == g) j1++;
+    memset(w->gang, 0, sizeof(R) * 3 * N);
+    for (int pass = 0; pass < 2; pass++) {
+      for (int j = j0; j < j1; j++) {
+        int bp = s->d->joint_body_p[j], bc = s->d->joint_body_c[j];
+        R tq[3];
+        for (int k = 0; k < 3; k++)
+          tq[k] = (R)-1 * s->jdamp[j] * (w->qp[bp].ang[k] - w->qp[bc].ang[k]);
+        if (pass == 0)
+          for (int k = 0; k < 3; k++) w->gang[3 * bp + k] += s->I[3 * bp + k] * tq[k];
+        else
+          for (int k = 0; k < 3; k++) w->gang[3 * bc + k] += -s->I[3 * bc + k] * tq[k];
+      }
+    }
+    for (int i = 0; i < 3 * N; i++) w->dp_j[i] += w->gang[i];
+    j0 = j1;
+  }
+}
+
+/* Actuator.apply + Torque/Angle.apply_reduced (actuators.py:52-112) */
+static void actuators_apply(const sysc* s, work_t* w, const R* act) {
+  int N = s->N, K = s->K;
+  memset(w->dp_a, 0, sizeof(R) * 3 * N);
+  int k0 = 0;
+  while (k0 < K) {
+    int g = s->d->act_group[k0], k1 = k0;
+    while (k1 < K && s->d->act_group[k1] == g) k1++;
+    memset(w->gang, 0, sizeof(R) * 3 * N);
+    R (*tp)[3] = calloc(k1 - k0, sizeof(R[3]));
+    R (*tc)[3] = calloc(k1 - k0, sizeof(R[3]));
+    for (int a = k0; a < k1; a++) {
+      int j = s->d->act_joint[a];
+      int bp = s->d->joint_body_p[j], bc = s->d->joint_body_c[j];
+      R axes[3][3], ang[3];
+      int dof = axis_angle(s, j, &w->qp[bp], &w->qp[bc], axes, ang);
+      const int32_t* idx = s->d->act_index + 3 * a;
+      const R* lim = s->jlim + 6 * j;
+      R tq[3] = {0, 0, 0};
+      for (int l = 0; l < dof; l++) {
+        /* jp.take(act, act_index) * act_mask; take clips -1 to 0 */
+        int ai = idx[l] < 0 ? 0 : idx[l];
+        R a_l = act[ai] * (idx[l] >= 0 ? (R)1 : (R)0);
+        R t;
+        if (s->d->act_type[a] == BX_ACT_TORQUE) {
+          t = a_l * s->astr[a] * (R)-1;
+          if (ang[l] < lim[2 * l]) t = 0;
+          if (ang[l] > lim[2 * l + 1]) t = 0;
+        } else {
+          R target = clip(a_l * (R)M_PI / (R)180, lim[2 * l], lim[2 * l + 1]);
+          t = (target - ang[l]) * s->astr[a];
+        }
+        for (int k = 0; k < 3; k++) tq[k] += axes[l][k] * t;
+      }
+      R sgn_p = s->d->act_type[a] == BX_ACT_TORQUE ? (R)1 : (R)-1;
+      for (int k = 0; k < 3; k++) {
+        tp[a - k0][k] = sgn_p * s->I[3 * bp + k] * tq[k];
+        tc[a - k0][k] = -sgn_p * s->I[3 * bc + k] * tq[k];
+      }
+    }
+    for (int a = k0; a < k1; a++) {
+      int b = s->d->joint_body_p[s->d->act_joint[a]];
+      for (int k = 0; k < 3; k++) w->gang[3 * b + k] += tp[a - k0][k];
+    }
+    for (int a = k0; a < k1; a++) {
+      int b = s->d->joint_body_c[s->d->act_joint[a]];
+      for (int k = 0; k < 3; k++) w->gang[3 * b + k] += tc[a - k0][k];
+    }
+    for (int i = 0; i < 3 * N; i++) w->dp_a[i] += w->gang[i];
+    free(tp); free(tc);
+    k0 = k1;
+  }
+}
+
+/* ---------------------------------------------------------- integrator --- */
+
+/* Euler.update acc (integrators.py:85-93); acc = dp_a + dp_f + dp_j (ang) */
+static void update_acc(const sysc* s, work_t* w) {
+  for (int b = 0; b < s->N; b++) {
+    body_t* q = &w->qp[b];
+    for (int k = 0; k < 3; k++) {
+      R v = s->vdamp_exp * q->vel[k];
+      v += ((R)0 + s->g[k]) * s->h;
+      v *= s->pos_mask[3 * b + k];
+      R acc = (w->dp_a[3 * b + k] + (R)0) + w->dp_j[3 * b + k];
+      R a = s->adamp_exp * q->ang[k];
+      a += acc * s->h;
+      a *= s->rot_mask[3 * b + k];
+      q->vel[k] = v;
+      q->ang[k] = a;
+    }
+  }
+}
+
+/* Euler.kinetic (integrators.py:50-68) */
+static void kinetic(const sysc* s, work_t* w) {
+  for (int b = 0; b < s->N; b++) {
+    body_t* q = &w->qp[b];
+    for (int k = 0; k < 3; k++) q->pos[k] = q->pos[k] + q->vel[k] * s->h * s->pos_mask[3 * b + k];
+    R hq[4] = {0, q->ang[0] * s->rot_mask[3 * b], q->ang[1] * s->rot_mask[3 * b + 1],
+               q->ang[2] * s->rot_mask[3 * b + 2]};
+    for (int k = 0; k < 4; k++) hq[k] = hq[k] * (R)0.5 * s->h;
+    R m[4];
+    quat_mul(hq, q->rot, m);
+    R r[4];
+    for (int k = 0; k < 4; k++) r[k] = q->rot[k] + m[k];
+    R n = (R)sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3]);
+    for (int k = 0; k < 4; k++) q->rot[k] = r[k] / n;
+  }
+}
+
+/* Euler.update pos (integrators.py:102-110) */
+static void update_pos(const sysc* s, work_t* w) {
+  for (int b = 0; b < s->N; b++) {
+    body_t* q = &w->qp[b];
+    for (int k = 0; k < 3; k++) q->pos[k] = q->pos[k] + w->dq_pos[3 * b + k] * s->pos_mask[3 * b + k];
+    for (int k = 0; k < 4; k++) q->rot[k] = q->rot[k] + w->dq_rot[4 * b + k] * s->quat_mask[4 * b + k];
+  }
+}
+
+/* Euler.update vel (integrators.py:96-100) */
+static void update_vel(const sysc* s, work_t* w) {
+  for (int b = 0; b < s->N; b++) {
+    body_t* q = &w->qp[b];
+    for (int k = 0; k < 3; k++) {
+      q->vel[k] = (q->vel[k] + w->dp_vel[3 * b + k]) * s->pos_mask[3 * b + k];
+      q->ang[k] = (q->ang[k] + w->dp_ang[3 * b + k]) * s->rot_mask[3 * b + k];
+    }
+  }
+}
+
+/* Euler.velocity_projection (integrators.py:122-146) */
+static void velocity_projection(const sysc* s, work_t* w, const body_t* prev) {
+  for (int b = 0; b < s->N; b++) {
+    body_t* q = &w->qp[b];
+    const body_t* p = &prev[b];
+    R n = (R)sqrt(q->rot[0] * q->rot[0] + q->rot[1] * q->rot[1] + q->rot[2] * q->rot[2] +
+                  q->rot[3] * q->rot[3]);
+    R nr[4];
+    for (int k = 0; k < 4; k++) nr[k] = q->rot[k] / n;
+    for (int k = 0; k < 3; k++) q->vel[k] = ((q->pos[k] - p->pos[k]) / s->h) * s->pos_mask[3 * b + k];
+    R inv[4], dq[4];
+    quat_inv(p->rot, inv);
+    quat_mul(nr, inv, dq);
+    R scale = dq[0] >= 0 ? (R)1 : (R)-1;
+    for (int k = 0; k < 3; k++) {
+      R a = (R)2 * dq[1 + k] / s->h;
+      R sc = scale * s->rot_mask[3 * b + k];
+      q->ang[k] = sc * a * s->rot_mask[3 * b + k];
+    }
+    memcpy(q->rot, nr, sizeof(nr));
+  }
+}
+
+/* ----------------------------------------------------------- colliders --- */
+
+/* capsule_plane (colliders.py:744-759) / capsule_capsule (:805-819) */
+static void contact_row(const sysc* s, int r, const body_t* qp, R* pos, R* vel, R* nrm, R* pen) {
+  const bx_desc* d = s->d;
+  int g = d->row_group[r];
+  const body_t* a = &qp[d->row_body_a[r]];
+  const body_t* b = &qp[d->row_body_b[r]];
+  if (d->col_fn[g] == BX_COL_CAPSULE_PLANE) {
+    R e[3], z[3] = {0, 0, 1};
+    rotate(s->ra_end + 3 * r, a->rot, e);
+    for (int k = 0; k < 3; k++) e[k] += a->pos[k];
+    rotate(z, b->rot, nrm);
+    for (int k = 0; k < 3; k++) pos[k] = e[k] - nrm[k] * s->ra_rad[r];
+    R rel[3], c[3];
+    for (int k = 0; k < 3; k++) rel[k] = pos[k] - a->pos[k];
+    cross3(a->ang, rel, c);
+    for (int k = 0; k < 3; k++) vel[k] = a->vel[k] + c[k];
+    R dpb[3];
+    for (int k = 0; k < 3; k++) dpb[k] = b->pos[k] - pos[k];
+    *pen = dot3(dpb, nrm);
+    return;
+  }
+  /* _endpoints (colliders.py:660-664) */
+  R pa[3], ea[3], pb[3], eb[3];
+  rotate(s->ra_pos + 3 * r, a->rot, pa);
+  rotate(s->ra_end + 3 * r, a->rot, ea);
+  rotate(s->rb_pos + 3 * r, b->rot, pb);
+  rotate(s->rb_end + 3 * r, b->rot, eb);
+  R a0[3], a1[3], b0[3], b1[3];
+  for (int k = 0; k < 3; k++) {
+    pa[k] += a->pos[k]; pb[k] += b->pos[k];
+    a0[k] = pa[k] + ea[k]; a1[k] = pa[k] - ea[k];
+    b0[k] = pb[k] + eb[k]; b1[k] = pb[k] - eb[k];
+  }
+  /* _closest_segment_to_segment_points (geometry.py:394-451) */
+  R da[3], db[3];
+  for (int k = 0; k < 3; k++) { da[k] = a1[k] - a0[k]; db[k] = b1[k] - b0[k]; }
+  R la = safe_norm3(da);
+  la += (R)1e-6 * (R)(la == 0);
+  for (int k = 0; k < 3; k++) da[k] /= la;
+  R hla = la * (R)0.5;
+  R lb = safe_norm3(db);
+  lb += (R)1e-6 * (R)(lb == 0);
+  for (int k = 0; k < 3; k++) db[k] /= lb;
+  R hlb = lb * (R)0.5;
+  R am[3], bm[3], tr[3];
+  for (int k = 0; k < 3; k++) {
+    am[k] = a0[k] + da[k] * hla;
+    bm[k] = b0[k] + db[k] * hlb;
+    tr[k] = am[k] - bm[k];
+  }
+  R dadb = dot3(da, db), datr = dot3(da, tr), dbtr = dot3(db, tr);
+  R den = 1 - dadb * dadb;
+  R ota = (-datr + dadb * dbtr) / (den + (R)1e-6);
+  R otb = dbtr + ota * dadb;
+  R ta = clip(ota, -hla, hla), tb = clip(otb, -hlb, hlb);
+  R ba[3], bb[3];
+  for (int k = 0; k < 3; k++) { ba[k] = am[k] + da[k] * ta; bb[k] = bm[k] + db[k] * tb; }
+  /* closest_segment_point_and_dist (geometry.py:360-374) */
+  R na[3], nb[3], d1, d2;
+  {
+    R ab[3], t[3];
+    for (int k = 0; k < 3; k++) { ab[k] = a1[k] - a0[k]; t[k] = bb[k] - a0[k]; }
+    R tt = dot3(t, ab) / (dot3(ab, ab) + (R)1e-6);
+    tt = clip(tt, 0, 1);
+    for (int k = 0; k < 3; k++) na[k] = a0[k] + tt * ab[k];
+    R v[3];
+    for (int k = 0; k < 3; k++) v[k] = bb[k] - na[k];
+    d1 = dot3(v, v);
+  }
+  {
+    R ab[3], t[3];
+    for (int k = 0; k < 3; k++) { ab[k] = b1[k] - b0[k]; t[k] = ba[k] - b0[k]; }
+    R tt = dot3(t, ab) / (dot3(ab, ab) + (R)1e-6);
+    tt = clip(tt, 0, 1);
+    for (int k = 0; k < 3; k++) nb[k] = b0[k] + tt * ab[k];
+    R v[3];
+    for (int k = 0; k < 3; k++) v[k] = ba[k] - nb[k];
+    d2 = dot3(v, v);
+  }
+  if (d1 < d2) { memcpy(ba, na, sizeof(na)); } else { memcpy(bb, nb, sizeof(nb)); }
+  R pv[3];
+  for (int k = 0; k < 3; k++) pv[k] = ba[k] - bb[k];
+  R dist = safe_norm3(pv);
+  for (int k = 0; k < 3; k++) nrm[k] = pv[k] / ((R)1e-6 + dist);
+  *pen = s->ra_rad[r] + s->rb_rad[r] - dist;
+  for (int k = 0; k < 3; k++) pos[k] = (ba[k] + bb[k]) / 2;
+  R ra[3], rb[3], ca[3], cb[3];
+  for (int k = 0; k < 3; k++) { ra[k] = pos[k] - a->pos[k]; rb[k] = pos[k] - b->pos[k]; }
+  cross3(a->ang, ra, ca);
+  cross3(b->ang, rb, cb);
+  for (int k = 0; k < 3; k++) vel[k] = (a->vel[k] + ca[k]) - (b->vel[k] + cb[k]);
+}
+
+static inline R quad_I(const R* I, const R* v) {
+  return v[0] * (I[0] * v[0]) + v[1] * (I[1] * v[1]) + v[2] * (I[2] * v[2]);
+}
+
+/* One/TwoWay._position_contact (colliders.py:306-377, :495-580).
+ * oa/ob: (pos3, rot4) outputs; returns dlambda. */
+static R position_contact(const sysc* s, int r, const body_t* qp, const body_t* qprev,
+                          const R* cpos, const R* n, R cpen, R* oa, R* ob) {
+  const bx_desc* d = s->d;
+  int g = d->row_group[r];
+  int ia = d->row_body_a[r], ib = d->row_body_b[r];
+  const body_t* a = &qp[ia];
+  const body_t* b = &qp[ib];
+  const body_t* ao = &qprev[ia];
+  const body_t* bo = &qprev[ib];
+  const R* Ia = s->I + 3 * ia;
+  const R* Ib = s->I + 3 * ib;
+  R ma = s->mass[ia], mb = s->mass[ib];
+  R sc = s->gscale[g];
+  R t[3], u[3], q[4];
+  for (int k = 0; k < 7; k++) { oa[k] = 0; ob[k] = 0; }
+  if (d->col_oneway[g]) {
+    R fr = s->rfric[r];
+    R pp[3], pc[3], dx[3];
+    for (int k = 0; k < 3; k++) {
+      pp[k] = cpos[k];
+      pc[k] = cpos[k] + n[k] * cpen;
+      dx[k] = pp[k] - pc[k];
+      pp[k] = pp[k] - a->pos[k];
+      pc[k] = pc[k] - b->pos[k];
+    }
+    R c = dot3(dx, n);
+    R cr1[3];
+    cross3(pp, n, cr1);
+    R w1 = (R)1 / ma + quad_I(Ia, cr1);
+    R dl = -c / (w1 + (R)1e-6);
+    R cm = c < 0 ? (R)1 : (R)0;
+    R pv[3];
+    for (int k = 0; k < 3; k++) pv[k] = dl * n[k] * cm;
+    cross3(pp, pv, t);
+    for (int k = 0; k < 3; k++) u[k] = Ia[k] * t[k];
+    vec_quat_mul(u, a->rot, q);
+    for (int k = 0; k < 3; k++) oa[k] = sc * (pv[k] / ma);
+    for (int k = 0; k < 4; k++) oa[3 + k] = sc * ((R)0.5 * q[k]);
+    /* static friction */
+    R qi[4], r1[3], rr[3], p1bar[3];
+    quat_inv(a->rot, qi);
+    for (int k = 0; k < 3; k++) rr[k] = cpos[k] - a->pos[k];
+    rotate(rr, qi, r1);
+    rotate(r1, ao->rot, p1bar);
+    R dp[3];
+    for (int k = 0; k < 3; k++) { p1bar[k] += ao->pos[k]; dp[k] = cpos[k] - p1bar[k]; }
+    R dpn = dot3(dp, n);
+    R dt_[3];
+    for (int k = 0; k < 3; k++) dt_[k] = dp[k] - dpn * n[k];
+    R c2 = safe_norm3(dt_);
+    R n2[3];
+    for (int k = 0; k < 3; k++) n2[k] = dt_[k] / (c2 + (R)1e-6);
+    cross3(pp, n2, cr1);
+    w1 = (R)1 / ma + quad_I(Ia, cr1);
+    R dlt = -c2 / (w1 + (R)0);
+    R sm = fabs((double)dlt) < fabs((double)(fr * dl)) ? (R)1 : (R)0;
+    for (int k = 0; k < 3; k++) pv[k] = dlt * n2[k] * sm * cm;
+    cross3(pp, pv, t);
+    for (int k = 0; k < 3; k++) u[k] = Ia[k] * t[k];
+    vec_quat_mul(u, a->rot, q);
+    for (int k = 0; k < 3; k++) oa[k] = oa[k] + sc * (pv[k] / ma);
+    for (int k = 0; k < 4; k++) oa[3 + k] = oa[3 + k] + sc * ((R)0.5 * q[k]);
+    return dl * cm;
+  }
+  /* TwoWay */
+  R pp[3], pc[3];
+  for (int k = 0; k < 3; k++) {
+    pp[k] = cpos[k] - n[k] * cpen / 2;
+    pc[k] = cpos[k] + n[k] * cpen / 2;
+    pp[k] -= a->pos[k];
+    pc[k] -= b->pos[k];
+  }
+  R c = -cpen;
+  R cr1[3], cr2[3];
+  cross3(pp, n, cr1);
+  cross3(pc, n, cr2);
+  R w1 = (R)1 / ma + quad_I(Ia, cr1);
+  R w2 = (R)1 / mb + quad_I(Ib, cr2);
+  R dl = -c / (w1 + w2 + (R)1e-6);
+  R cm = c < 0 ? (R)1 : (R)0;
+  R pv[3];
+  for (int k = 0; k < 3; k++) pv[k] = dl * n[k] * cm;
+  cross3(pp, pv, t);
+  for (int k = 0; k < 3; k++) u[k] = Ia[k] * t[k];
+  vec_quat_mul(u, a->rot, q);
+  for (int k = 0; k < 3; k++) oa[k] = sc * (pv[k] / ma);
+  for (int k = 0; k < 4; k++) oa[3 + k] = sc * ((R)0.5 * q[k]);
+  cross3(pc, pv, t);
+  for (int k = 0; k < 3; k++) u[k] = Ib[k] * t[k];
+  vec_quat_mul(u, b->rot, q);
+  for (int k = 0; k < 3; k++) ob[k] = sc * (-pv[k] / mb);
+  for (int k = 0; k < 4; k++) ob[3 + k] = sc * ((R)-0.5 * q[k]);
+  /* static friction */
+  R qi[4], rr[3], r1[3], r2[3], p1bar[3], p2bar[3];
+  quat_inv(a->rot, qi);
+  for (int k = 0; k < 3; k++) rr[k] = cpos[k] - a->pos[k];
+  rotate(rr, qi, r1);
+  quat_inv(b->rot, qi);
+  for (int k = 0; k < 3; k++) rr[k] = cpos[k] - b->pos[k];
+  rotate(rr, qi, r2);
+  rotate(r1, ao->rot, p1bar);
+  rotate(r2, bo->rot, p2bar);
+  R dp[3];
+  for (int k = 0; k < 3; k++) {
+    p1bar[k] += ao->pos[k];
+    p2bar[k] += bo->pos[k];
+    dp[k] = (cpos[k] - p1bar[k]) - (cpos[k] - p2bar[k]);
+  }
+  R dpn = dot3(dp, n);
+  R dt_[3];
+  for (int k = 0; k < 3; k++) dt_[k] = dp[k] - dpn * n[k];
+  for (int k = 0; k < 3; k++) { pp[k] = cpos[k] - a->pos[k]; pc[k] = cpos[k] - b->pos[k]; }
+  R c2 = safe_norm3(dt_);
+  R n2[3];
+  for (int k = 0; k < 3; k++) n2[k] = dt_[k] / (c2 + (R)1e-6);
+  cross3(pp, n2, cr1);
+  cross3(pc, n2, cr2);
+  w1 = (R)1 / ma + quad_I(Ia, cr1);
+  w2 = (R)1 / mb + quad_I(Ib, cr2);
+  R dlt = -c2 / (w1 + w2);
+  R sm = fabs((double)dlt) < fabs((double)dl) ? (R)1 : (R)0;
+  for (int k = 0; k < 3; k++) pv[k] = dlt * n2[k] * sm * cm;
+  cross3(pp, pv, t);
+  for (int k = 0; k < 3; k++) u[k] = Ia[k] * t[k];
+  vec_quat_mul(u, a->rot, q);
+  for (int k = 0; k < 3; k++) oa[k] = oa[k] + sc * (pv[k] / ma);
+  for (int k = 0; k < 4; k++) oa[3 + k] = oa[3 + k] + sc * ((R)0.5 * q[k]);
+  R mp[3] = {-pv[0], -pv[1], -pv[2]};
+  cross3(pc, mp, t);
+  for (int k = 0; k < 3; k++) u[k] = Ib[k] * t[k];
+  vec_quat_mul(u, b->rot, q);
+  for (int k = 0; k < 3; k++) ob[k] = ob[k] + sc * (-pv[k] / mb);
+  for (int k = 0; k < 4; k++) ob[3 + k] = ob[3 + k] + sc * ((R)0.5 * q[k]);
+  return dl;
+}
+
+/* One/TwoWay._velocity_contact (colliders.py:379-442, :584-658).
+ * qo = qp_right_before (the `qp_prev` argument of velocity_apply). */
+static void velocity_contact(const sysc* s, int r, const body_t* qp, const body_t* qo,
+                             const R* cpos, const R* n, R cpen, R dlam, R* oa, R* ob) {
+  const bx_desc* d = s->d;
+  int g = d->row_group[r];
+  int ia = d->row_body_a[r], ib = d->row_body_b[r];
+  const body_t* a = &qp[ia];
+  const body_t* b = &qp[ib];
+  const body_t* ao = &qo[ia];
+  const body_t* bo = &qo[ib];
+  const R* Ia = s->I + 3 * ia;
+  const R* Ib = s->I + 3 * ib;
+  R ma = s->mass[ia], mb = s->mass[ib];
+  R fr = s->rfric[r], el = s->relas[r];
+  R h = s->h;
+  int one = d->col_oneway[g];
+  for (int k = 0; k < 6; k++) { oa[k] = 0; ob[k] = 0; }
+  R ra[3], rb[3], ca[3], cb[3], rv[3];
+  for (int k = 0; k < 3; k++) { ra[k] = cpos[k] - a->pos[k]; rb[k] = cpos[k] - b->pos[k]; }
+  cross3(a->ang, ra, ca);
+  cross3(b->ang, rb, cb);
+  for (int k = 0; k < 3; k++)
+    rv[k] = one ? a->vel[k] + ca[k] : (a->vel[k] + ca[k]) - (b->vel[k] + cb[k]);
+  R vn = dot3(rv, n);
+  R vt[3];
+  for (int k = 0; k < 3; k++) vt[k] = rv[k] - n[k] * vn;
+  R vtn = safe_norm3(vt);
+  R vtd[3];
+  for (int k = 0; k < 3; k++) vtd[k] = vt[k] / ((R)1e-6 + vtn);
+  R lim = fr * (R)fabs((double)dlam) / ((R)2 * h);
+  R mag = lim < vtn ? lim : vtn; /* jp.amin over [lim, vtn] */
+  R dvel[3];
+  for (int k = 0; k < 3; k++) dvel[k] = -vtd[k] * mag;
+  R pdyn[3];
+  if (one) {
+    R aw[3];
+    cross3(ra, vtd, aw);
+    R w = (R)1 / ma + dot3(aw, aw);
+    for (int k = 0; k < 3; k++) pdyn[k] = dvel[k] / (w + (R)1e-6);
+  } else {
+    R a1[3], a2[3];
+    cross3(ra, vtd, a1);
+    cross3(rb, vtd, a2);
+    R w1 = (R)1 / ma + quad_I(Ia, a1);
+    R w2 = (R)1 / mb + quad_I(Ib, a2);
+    for (int k = 0; k < 3; k++) pdyn[k] = dvel[k] / (w1 + w2 + (R)1e-6);
+  }
+  /* restitution */
+  R rao[3], rbo[3], cao[3], cbo[3], rvo[3];
+  for (int k = 0; k < 3; k++) { rao[k] = cpos[k] - ao->pos[k]; rbo[k] = cpos[k] - bo->pos[k]; }
+  cross3(ao->ang, rao, cao);
+  cross3(bo->ang, rbo, cbo);
+  for (int k = 0; k < 3; k++)
+    rvo[k] = one ? ao->vel[k] + cao[k] : (ao->vel[k] + cao[k]) - (bo->vel[k] + cbo[k]);
+  R vno = dot3(rvo, n);
+  R ev = el * vno;
+  R mn = ev < 0 ? ev : (R)0;
+  R dvr[3];
+  for (int k = 0; k < 3; k++) dvr[k] = n[k] * (-vn - mn);
+  R pp[3], pc[3];
+  for (int k = 0; k < 3; k++) {
+    pp[k] = cpos[k] - a->pos[k];
+    pc[k] = (cpos[k] + n[k] * cpen) - b->pos[k];
+  }
+  R c = safe_norm3(dvr);
+  R n2[3];
+  for (int k = 0; k < 3; k++) n2[k] = dvr[k] / (c + (R)1e-6);
+  R cr1[3], cr2[3];
+  cross3(pp, n2, cr1);
+  R w1 = (R)1 / ma + quad_I(Ia, cr1);
+  R dlr;
+  if (one) {
+    dlr = c / (w1 + (R)1e-6);
+  } else {
+    cross3(pc, n2, cr2);
+    R w2 = (R)1 / mb + quad_I(Ib, cr2);
+    dlr = c / (w1 + w2 + (R)1e-6);
+  }
+  R sm = cpen > 0 ? (R)1 : (R)0;
+  R sink = one ? (vno <= -s->gthr[g] ? (R)1 : (R)0) : (vno <= 0 ? (R)1 : (R)0);
+  R pv[3];
+  for (int k = 0; k < 3; k++) pv[k] = (dlr * n2[k] * sink + pdyn[k]) * sm;
+  R t[3];
+  for (int k = 0; k < 3; k++) { oa[k] = pv[k] / ma; t[k] = Ia[k] * ra[k]; }
+  cross3(t, pv, oa + 3);
+  if (!one) {
+    R mp[3] = {-pv[0], -pv[1], -pv[2]};
+    for (int k = 0; k < 3; k++) { ob[k] = -pv[k] / mb; t[k] = Ib[k] * rb[k]; }
+    cross3(t, mp, ob + 3);
+  }
+}
+
+/* One/TwoWay._contact (colliders.py:267-304, :449-493): impulse model used by
+ * System.info at reset. oa/ob: (vel3, ang3). */
+static void impulse_contact(const sysc* s, int r, const body_t* qp, const R* cpos,
+                            const R* cvel, const R* n, R cpen, R* oa, R* ob) {
+  const bx_desc* d = s->d;
+  int g = d->row_group[r];
+  int ia = d->row_body_a[r], ib = d->row_body_b[r];
+  const body_t* a = &qp[ia];
+  const body_t* b = &qp[ib];
+  const R* Ia = s->I + 3 * ia;
+  const R* Ib = s->I + 3 * ib;
+  R ma = s->mass[ia], mb = s->mass[ib];
+  R fr = s->rfric[r], el = s->relas[r];
+  int one = d->col_oneway[g];
+  R rpa[3], rpb[3];
+  for (int k = 0; k < 3; k++) { rpa[k] = cpos[k] - a->pos[k]; rpb[k] = cpos[k] - b->pos[k]; }
+  R bv = s->gerp[g] * cpen;
+  R nv = dot3(n, cvel);
+  R c1[3], t1[3], x1[3];
+  cross3(rpa, n, c1);
+  for (int k = 0; k < 3; k++) t1[k] = Ia[k] * c1[k];
+  cross3(t1, rpa, x1);
+  R ang;
+  R denom;
+  if (one) {
+    ang = dot3(n, x1);
+    denom = (R)1 / ma + ang;
+  } else {
+    R c2[3], t2[3], x2[3], sx[3];
+    cross3(rpb, n, c2);
+    for (int k = 0; k < 3; k++) t2[k] = Ib[k] * c2[k];
+    cross3(t2, rpb, x2);
+    for (int k = 0; k < 3; k++) sx[k] = x1[k] + x2[k];
+    ang = dot3(n, sx);
+    denom = (R)1 / ma + (R)1 / mb + ang;
+  }
+  R imp = ((R)-1 * ((R)1 + el) * nv + bv) / denom;
+  R vd[3];
+  for (int k = 0; k < 3; k++) vd[k] = cvel[k] - nv * n[k];
+  R vdn = safe_norm3(vd);
+  R impd = vdn / denom;
+  R fi = fr * imp;
+  impd = impd < fi ? impd : fi;
+  R dird[3];
+  for (int k = 0; k < 3; k++) dird[k] = vd[k] / ((R)1e-6 + vdn);
+  R an = (cpen > 0 && nv < 0 && imp > 0) ? (R)1 : (R)0;
+  R ad = an * (vdn > (R)0.01 ? (R)1 : (R)0);
+  /* Body.impulse (bodies.py:46-59): dvel = J/m, dang = I * cross(pos - qp.pos, J) */
+  R J[3], Jd[3], cx[3], cxd[3];
+  for (int k = 0; k < 3; k++) { J[k] = imp * n[k]; Jd[k] = -impd * dird[k]; }
+  cross3(rpa, J, cx);
+  cross3(rpa, Jd, cxd);
+  for (int k = 0; k < 3; k++) {
+    oa[k] = (J[k] / ma) * an + (Jd[k] / ma) * ad;
+    oa[3 + k] = (Ia[k] * cx[k]) * an + (Ia[k] * cxd[k]) * ad;
+  }
+  if (!one) {
+    for (int k = 0; k < 3; k++) { J[k] = -imp * n[k]; Jd[k] = impd * dird[k]; }
+    cross3(rpb, J, cx);
+    cross3(rpb, Jd, cxd);
+    for (int k = 0; k < 3; k++) {
+      ob[k] = (J[k] / mb) * an + (Jd[k] / mb) * ad;
+      ob[3 + k] = (Ib[k] * cx[k]) * an + (Ib[k] * cxd[k]) * ad;
+    }
+  } else {
+    for (int k = 0; k < 6; k++) ob[k] = 0;
+  }
+}
+
+/* segment-sum rows of one collider group into w->g*, with the any()-count and
+ * the (eps + count) normalisation (colliders.py:141-153, :179-196, :221-240).
+ * width 7 -> (pos, rot) targets; width 6 -> (vel, ang). */
+static void group_reduce(const sysc* s, work_t* w, int g, int width, R eps,
+                         const R* rows_a, const R* rows_b, R* out_lin, R* out_rot) {
+  const bx_desc* d = s->d;
+  int N = s->N, Rn = s->Rn;
+  int rw = width == 7 ? 4 : 3;
+  memset(w->cnt, 0, sizeof(R) * N);
+  memset(w->gpos, 0, sizeof(R) * 3 * N);
+  memset(w->grot, 0, sizeof(R) * 4 * N);
+  for (int side = 0; side < 2; side++) {
+    if (side == 1 && d->col_oneway[g]) break;
+    const R* rows = side == 0 ? rows_a : rows_b;
+    for (int r = 0; r < Rn; r++) {
+      if (d->row_group[r] != g) continue;
+      int b = side == 0 ? d->row_body_a[r] : d->row_body_b[r];
+      const R* v = rows + width * r;
+      int any = v[0] != 0 || v[1] != 0 || v[2] != 0;
+      w->cnt[b] += any ? (R)1 : (R)0;
+      for (int k = 0; k < 3; k++) w->gpos[3 * b + k] += v[k];
+      for (int k = 0; k < rw; k++) w->grot[4 * b + k] += v[3 + k];
+    }
+  }
+  for (int b = 0; b < N; b++) {
+    R c = eps + w->cnt[b];
+    for (int k = 0; k < 3; k++) out_lin[3 * b + k] += w->gpos[3 * b + k] / c;
+    for (int k = 0; k < rw; k++) out_rot[rw * b + k] += w->grot[4 * b + k] / c;
+  }
+}
+
+/* --------------------------------------------------------------- step ---- */
+
+static void one_substep(const sysc* s, work_t* w, const R* act) {
+  actuators_apply(s, w, act);
+  joints_damp(s, w);
+  update_acc(s, w);
+  kinetic(s, w);
+  joints_apply(s, w);
+  update_pos(s, w);
+}
+
+/* System._pbd_step (system.py:254-325) for one env */
+static void pbd_step_env(const sysc* s, work_t* w, const R* act, R* rows_a, R* rows_b) {
+  int N = s->N, Rn = s->Rn;
+  memset(w->info_c, 0, sizeof(R) * 6 * N);
+  memset(w->info_a, 0, sizeof(R) * 6 * N);
+  for (int it = 0; it < s->d->substeps / 2; it++) {
+    memcpy(w->qprev, w->qp, sizeof(body_t) * N);
+    one_substep(s, w, act);
+    velocity_projection(s, w, w->qprev);
+    memcpy(w->qprev, w->qp, sizeof(body_t) * N);
+    one_substep(s, w, act);
+    /* Collider.position_apply (colliders.py:198-240) */
+    for (int r = 0; r < Rn; r++)
+      contact_row(s, r, w->qp, w->c_pos + 3 * r, w->c_vel + 3 * r, w->c_norm + 3 * r, &w->c_pen[r]);
+    for (int r = 0; r < Rn; r++)
+      w->dlam[r] = position_contact(s, r, w->qp, w->qprev, w->c_pos + 3 * r, w->c_norm + 3 * r,
+                                    w->c_pen[r], rows_a + 7 * r, rows_b + 7 * r);
+    memset(w->dq_pos, 0, sizeof(R) * 3 * N);
+    memset(w->dq_rot, 0, sizeof(R) * 4 * N);
+    for (int g = 0; g < s->G; g++) group_reduce(s, w, g, 7, (R)1e-6, rows_a, rows_b, w->dq_pos, w->dq_rot);
+    update_pos(s, w);
+    memcpy(w->qrb, w->qp, sizeof(body_t) * N);
+    velocity_projection(s, w, w->qprev);
+    /* Collider.velocity_apply (colliders.py:155-196); rows at stride 6 */
+    for (int r = 0; r < Rn; r++)
+      velocity_contact(s, r, w->qp, w->qrb, w->c_pos + 3 * r, w->c_norm + 3 * r, w->c_pen[r],
+                       w->dlam[r], rows_a + 6 * r, rows_b + 6 * r);
+    memset(w->dp_vel, 0, sizeof(R) * 3 * N);
+    memset(w->dp_ang, 0, sizeof(R) * 3 * N);
+    for (int g = 0; g < s->G; g++) group_reduce(s, w, g, 6, (R)1e-6, rows_a, rows_b, w->dp_vel, w->dp_ang);
+    update_vel(s, w);
+    for (int b = 0; b < N; b++)
+      for (int k = 0; k < 3; k++) {
+        w->info_c[6 * b + k] += w->dp_vel[3 * b + k];
+        w->info_c[6 * b + 3 + k] += w->dp_ang[3 * b + k];
+        w->info_a[6 * b + 3 + k] += w->dp_a[3 * b + k];
+      }
+  }
+}
+
+int FN(oracle_system_step)(const bx_desc* d, int64_t B, const R* qp_in, const R* act,
+                           R* qp_out, R* info_contact, R* info_actuator, R* cpos,
+                           R* cnorm, R* cpen) {
+  sysc s;
+  sys_init(&s, d);
+  int N = s.N, Rn = s.Rn, A = s.A;
+#pragma omp parallel
+  {
+    work_t w;
+    work_alloc(&w, N, Rn);
+    R* ra = calloc(7 * (Rn > 0 ? Rn : 1), sizeof(R));
+    R* rb = calloc(7 * (Rn > 0 ? Rn : 1), sizeof(R));
+#pragma omp for schedule(static)
+    for (int64_t e = 0; e < B; e++) {
+      load_qp(w.qp, qp_in + e * 13 * N, N);
+      pbd_step_env(&s, &w, act + e * A, ra, rb);
+      store_qp(w.qp, qp_out + e * 13 * N, N);
+      if (info_contact) memcpy(info_contact + e * 6 * N, w.info_c, sizeof(R) * 6 * N);
+      if (info_actuator) memcpy(info_actuator + e * 6 * N, w.info_a, sizeof(R) * 6 * N);
+      if (cpos) memcpy(cpos + e * 3 * Rn, w.c_pos, sizeof(R) * 3 * Rn);
+      if (cnorm) memcpy(cnorm + e * 3 * Rn, w.c_norm, sizeof(R) * 3 * Rn);
+      if (cpen) memcpy(cpen + e * Rn, w.c_pen, sizeof(R) * Rn);
+    }
+    free(ra); free(rb);
+    work_free(&w);
+  }
+  sys_free(&s);
+  return 0;
+}
+
+/* System._pbd_info contact part (system.py:327-340; Collider.apply
+ * colliders.py:116-153) for one env: info_c (N,6) */
+static void pbd_info_env(const sysc* s, work_t* w, R* rows_a, R* rows_b) {
+  int N = s->N, Rn = s->Rn;
+  for (int r = 0; r < Rn; r++)
+    contact_row(s, r, w->qp, w->c_pos + 3 * r, w->c_vel + 3 * r, w->c_norm + 3 * r, &w->c_pen[r]);
+  for (int r = 0; r < Rn; r++)
+    impulse_contact(s, r, w->qp, w->c_pos + 3 * r, w->c_vel + 3 * r, w->c_norm + 3 * r,
+                    w->c_pen[r], rows_a + 6 * r, rows_b + 6 * r);
+  memset(w->dp_vel, 0, sizeof(R) * 3 * N);
+  memset(w->dp_ang, 0, sizeof(R) * 3 * N);
+  for (int g = 0; g < s->G; g++) group_reduce(s, w, g, 6, (R)1e-8, rows_a, rows_b, w->dp_vel, w->dp_ang);
+  for (int b = 0; b < N; b++)
+    for (int k = 0; k < 3; k++) {
+      w->info_c[6 * b + k] = w->dp_vel[3 * b + k];
+      w->info_c[6 * b + 3 + k] = w->dp_ang[3 * b + k];
+    }
+}
+
+int FN(oracle_system_info)(const bx_desc* d, int64_t B, const R* qp, R* info_contact) {
+  sysc s;
+  sys_init(&s, d);
+  int N = s.N, Rn = s.Rn;
+#pragma omp parallel
+  {
+    work_t w;
+    work_alloc(&w, N, Rn);
+    R* ra = calloc(7 * (Rn > 0 ? Rn : 1), sizeof(R));
+    R* rb = calloc(7 * (Rn > 0 ? Rn : 1), sizeof(R));
+#pragma omp for schedule(static)
+    for (int64_t e = 0; e < B; e++) {
+      load_qp(w.qp, qp + e * 13 * N, N);
+      pbd_info_env(&s, &w, ra, rb);
+      memcpy(info_contact + e * 6 * N, w.info_c, sizeof(R) * 6 * N);
+    }
+    free(ra); free(rb);
+    work_free(&w);
+  }
+  sys_free(&s);
+  return 0;
+}
+
+/* ---------------------------------------------------------------- env ---- */
+
+/* Joint.angle_vel (joints.py:197-226) for all joints, free-dof gathered.
+ * Returns the count written to angles/vels. */
+static int angle_vel(const sysc* s, const body_t* qp, R* angles, R* vels) {
+  int n = 0;
+  for (int j = 0; j < s->J; j++) {
+    int bp = s->d->joint_body_p[j], bc = s->d->joint_body_c[j];
+    R axes[3][3], ang[3];
+    int dof = axis_angle(s, j, &qp[bp], &qp[bc], axes, ang);
+    int fd = s->d->joint_free_dofs[j];
+    int use = fd >= 0 ? fd : dof;
+    for (int l = 0; l < use; l++) {
+      R dv[3];
+      for (int k = 0; k < 3; k++) dv[k] = qp[bp].ang[k] - qp[bc].ang[k];
+      angles[n] = ang[l];
+      vels[n] = dot3(dv, axes[l]);
+      n++;
+    }
+  }
+  return n;
+}
+
+static R clip1(R x) { return clip(x, -1, 1); }
+
+/* Ant._get_obs (ant.py:257-282), use_contact_forces=True -> 87 */
+static int obs_ant(const sysc* s, const body_t* qp, const R* info_c, R* obs) {
+  int n = 0, N = s->N;
+  R ang[64], vel[64];
+  int nd = angle_vel(s, qp, ang, vel);
+  obs[n++] = qp[0].pos[2];
+  for (int k = 0; k < 4; k++) obs[n++] = qp[0].rot[k];
+  for (int i = 0; i < nd; i++) obs[n++] = ang[i];
+  for (int k = 0; k < 3; k++) obs[n++] = qp[0].vel[k];
+  for (int k = 0; k < 3; k++) obs[n++] = qp[0].ang[k];
+  for (int i = 0; i < nd; i++) obs[n++] = vel[i];
+  for (int b = 0; b < N; b++)
+    for (int k = 0; k < 3; k++) obs[n++] = clip1(info_c[6 * b + k]);
+  for (int b = 0; b < N; b++)
+    for (int k = 0; k < 3; k++) obs[n++] = clip1(info_c[6 * b + 3 + k]);
+  return n;
+}
+
+/* Halfcheetah._get_obs (half_cheetah.py:200-214) -> 18 */
+static int obs_halfcheetah(const sysc* s, const body_t* qp, R* obs) {
+  int n = 0;
+  R ang[64], vel[64];
+  int nd = angle_vel(s, qp, ang, vel);
+  obs[n++] = qp[0].pos[2];
+  obs[n++] = qp[0].rot[0];
+  obs[n++] = qp[0].rot[2];
+  for (int i = 0; i < nd; i++) obs[n++] = ang[i];
+  obs[n++] = qp[0].vel[0];
+  obs[n++] = qp[0].vel[2];
+  obs[n++] = qp[0].ang[1];
+  for (int i = 0; i < nd; i++) obs[n++] = vel[i];
+  return n;
+}
+
+/* Humanoid._center_of_mass (humanoid.py:336-338): bodies [:-1] */
+static void humanoid_com(const sysc* s, const body_t* qp, R* com) {
+  R m = 0;
+  R acc[3] = {0, 0, 0};
+  for (int b = 0; b < s->N - 1; b++) {
+    for (int k = 0; k < 3; k++) acc[k] += s->mass[b] * qp[b].pos[k];
+    m += s->mass[b];
+  }
+  for (int k = 0; k < 3; k++) com[k] = acc[k] / m;
+}
+
+/* Humanoid._get_obs (humanoid.py:282-334) -> 240 */
+static int obs_humanoid(const sysc* s, const body_t* qp, const R* act, R* obs) {
+  int n = 0, N = s->N;
+  R ang[64], vel[64];
+  int nd = angle_vel(s, qp, ang, vel);
+  obs[n++] = qp[0].pos[2];
+  for (int k = 0; k < 4; k++) obs[n++] = qp[0].rot[k];
+  for (int i = 0; i < nd; i++) obs[n++] = ang[i];
+  for (int k = 0; k < 3; k++) obs[n++] = qp[0].vel[k];
+  for (int k = 0; k < 3; k++) obs[n++] = qp[0].ang[k];
+  for (int i = 0; i < nd; i++) obs[n++] = vel[i];
+  R com[3];
+  humanoid_com(s, qp, com);
+  R msum = 0;
+  for (int b = 0; b < N - 1; b++) msum += s->mass[b];
+  /* cinert: (N-1) x 3x3 */
+  for (int b = 0; b < N - 1; b++) {
+    R dd[3];
+    for (int k = 0; k < 3; k++) dd[k] = qp[b].pos[k] - com[k];
+    R nn = norm3(dd);
+    R n2 = nn * nn;
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) {
+        R v = s->mass[b] * (R)(r == c) * n2;
+        v += (r == c ? s->I[3 * b + r] : (R)0) - dd[r] * dd[c];
+        obs[n++] = v;
+      }
+  }
+  /* cvel: com_vel (N-1)x3 then com_ang (N-1)x3 */
+  for (int b = 0; b < N - 1; b++)
+    for (int k = 0; k < 3; k++) obs[n++] = s->mass[b] * qp[b].vel[k] / msum;
+  for (int b = 0; b < N - 1; b++) {
+    R dd[3], cr[3];
+    for (int k = 0; k < 3; k++) dd[k] = qp[b].pos[k] - com[k];
+    cross3(dd, qp[b].vel, cr);
+    R nn = norm3(dd);
+    for (int k = 0; k < 3; k++) obs[n++] = cr[k] / ((R)1e-7 + nn * nn);
+  }
+  /* qfrc_actuator: take(action, act_index) unmasked (-1 -> clip -> 0) */
+  for (int a = 0; a < s->K; a++) {
+    int j = s->d->act_joint[a];
+    int dof = s->d->joint_dof[j];
+    for (int l = 0; l < dof; l++) {
+      int ai = s->d->act_index[3 * a + l];
+      if (ai < 0) ai = 0;
+      obs[n++] = act[ai] * s->astr[a];
+    }
+  }
+  return n;
+}
+
+int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const R* info_c,
+                       const R* act, R* obs, int obs_size) {
+  sysc s;
+  sys_init(&s, d);
+  int N = s.N;
+  int rc = 0;
+#pragma omp parallel
+  {
+    body_t* q = calloc(N, sizeof(body_t));
+#pragma omp for schedule(static)
+    for (int64_t e = 0; e < B; e++) {
+      load_qp(q, qp + e * 13 * N, N);
+      int n = 0;
+      if (kind == BX_ENV_ANT) n = obs_ant(&s, q, info_c + e * 6 * N, obs + e * obs_size);
+      else if (kind == BX_ENV_HALFCHEETAH) n = obs_halfcheetah(&s, q, obs + e * obs_size);
+      else if (kind == BX_ENV_HUMANOID) n = obs_humanoid(&s, q, act + e * s.A, obs + e * obs_size);
+      if (n != obs_size) rc = -1;
+    }
+    free(q);
+  }
+  sys_free(&s);
+  return rc;
+}
+
+/* Env.step of the unwrapped env (ant.py:222-255, humanoid.py:246-280,
+ * half_cheetah.py:178-197). done_io is read (HalfCheetah keeps it) and written. */
+int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, const R* act,
+                        R* qp_out, R* obs, int obs_size, R* reward, R* done_io,
+                        R* metrics, int n_metrics) {
+  sysc s;
+  sys_init(&s, d);
+  int N = s.N, Rn = s.Rn, A = s.A;
+  int rc = 0;
+#pragma omp parallel
+  {
+    work_t w;
+    work_alloc(&w, N, Rn);
+    R* ra = calloc(7 * (Rn > 0 ? Rn : 1), sizeof(R));
+    R* rb = calloc(7 * (Rn > 0 ? Rn : 1), sizeof(R));
+    body_t* q0 = calloc(N, sizeof(body_t));
+#pragma omp for schedule(static)
+    for (int64_t e = 0; e < B; e++) {
+      const R* a = act + e * A;
+      load_qp(w.qp, qp_in + e * 13 * N, N);
+      memcpy(q0, w.qp, sizeof(body_t) * N);
+      pbd_step_env(&s, &w, a, ra, rb);
+      store_qp(w.qp, qp_out + e * 13 * N, N);
+      R* o = obs + e * obs_size;
+      R* m = metrics + e * n_metrics;
+      R dt = (R)d->dt;
+      R sq = 0;
+      for (int i = 0; i < A; i++) sq += a[i] * a[i];
+      int n = 0;
+      if (kind == BX_ENV_ANT) {
+        n = obs_ant(&s, w.qp, w.info_c, o);
+        R vel[3];
+        for (int k = 0; k < 3; k++) vel[k] = (w.qp[0].pos[k] - q0[0].pos[k]) / dt;
+        R fwd = vel[0];
+        R z = w.qp[0].pos[2];
+        R healthy = z < (R)0.2 ? (R)0 : (R)1;
+        healthy = z > (R)1.0 ? (R)0 : healthy;
+        R ctrl = (R)0.5 * sq;
+        R csum = 0;
+        for (int b = 0; b < N; b++)
+          for (int k = 0; k < 3; k++) { R c = clip1(w.info_c[6 * b + k]); csum += c * c; }
+        R ccost = (R)5e-4 * csum;
+        reward[e] = fwd + (R)1 - ctrl - ccost;
+        done_io[e] = (R)1 - healthy;
+        /* metric keys sorted: distance_from_origin, forward_reward,
+         * reward_contact, reward_ctrl, reward_forward, reward_survive,
+         * x_position, x_velocity, y_position, y_velocity */
+        m[0] = norm3(w.qp[0].pos); m[1] = fwd; m[2] = -ccost; m[3] = -ctrl;
+        m[4] = fwd; m[5] = 1; m[6] = w.qp[0].pos[0]; m[7] = vel[0];
+        m[8] = w.qp[0].pos[1]; m[9] = vel[1];
+      } else if (kind == BX_ENV_HALFCHEETAH) {
+        n = obs_halfcheetah(&s, w.qp, o);
+        R v0 = (w.qp[0].pos[0] - q0[0].pos[0]) / dt;
+        R fwd = (R)1.0 * v0;
+        R ctrl = (R)0.1 * sq;
+        reward[e] = fwd - ctrl;
+        /* done unchanged; metrics sorted: reward_ctrl, reward_run, x_position, x_velocity */
+        m[0] = -ctrl; m[1] = fwd; m[2] = w.qp[0].pos[0]; m[3] = v0;
+      } else if (kind == BX_ENV_HUMANOID) {
+        n = obs_humanoid(&s, w.qp, a, o);
+        R cb[3], ca[3], v[3];
+        humanoid_com(&s, q0, cb);
+        humanoid_com(&s, w.qp, ca);
+        for (int k = 0; k < 3; k++) v[k] = (ca[k] - cb[k]) / dt;
+        R fwd = (R)1.25 * v[0];
+        R z = w.qp[0].pos[2];
+        R healthy = z < (R)0.8 ? (R)0 : (R)1;
+        healthy = z > (R)2.1 ? (R)0 : healthy;
+        R ctrl = (R)0.1 * sq;
+        reward[e] = fwd + (R)5.0 - ctrl;
+        done_io[e] = (R)1 - healthy;
+        /* sorted: distance_from_origin, forward_reward, reward_alive,
+         * reward_linvel, reward_quadctrl, x_position, x_velocity,
+         * y_position, y_velocity */
+        m[0] = norm3(ca); m[1] = fwd; m[2] = 5; m[3] = fwd; m[4] = -ctrl;
+        m[5] = ca[0]; m[6] = v[0]; m[7] = ca[1]; m[8] = v[1];
+      }
+      if (n != obs_size) rc = -1;
+    }
+    free(q0); free(ra); free(rb);
+    work_free(&w);
+  }
+  sys_free(&s);
+  return rc;
+}
+
+/* -------------------------------------------------------------- reset ---- */
+
+/* System.default_qp (system.py:112-242) for B envs from explicit joint angles
+ * and velocities (B, num_joint_dof). */
+int FN(oracle_default_qp)(const bx_desc* d, const bx_reset_desc* rd, int64_t B,
+                          const R* angles, const R* vels, R* qp_out) {
+  int N = d->n_bodies, D = d->num_joint_dof;
+#pragma omp parallel
+  {
+    body_t* q = calloc(N > 0 ? N : 1, sizeof(body_t));
+    R* zmin = malloc(sizeof(R) * (rd->n_root_groups > 0 ? rd->n_root_groups : 1));
+#pragma omp for schedule(static)
+    for (int64_t e = 0; e < B; e++) {
+      const R* ja = angles + e * D;
+      const R* jv = vels + e * D;
+      for (int b = 0; b < N; b++) {
+        const double* s = rd->base_qp + 13 * b;
+        for (int k = 0; k < 3; k++) { q[b].pos[k] = (R)s[k]; q[b].vel[k] = (R)s[7 + k]; q[b].ang[k] = (R)s[10 + k]; }
+        for (int k = 0; k < 4; k++) q[b].rot[k] = (R)s[3 + k];
+      }
+      for (int f = 0; f < rd->n_fk; f++) {
+        R ang3[3], vel3[3];
+        for (int l = 0; l < 3; l++) {
+          int ix = rd->fk_dof_index[3 * f + l];
+          ang3[l] = ix >= 0 ? ja[ix] : (R)0;
+          vel3[l] = ix >= 0 ? jv[ix] : (R)0;
+        }
+        R jr[4], ref[4];
+        for (int k = 0; k < 4; k++) { jr[k] = (R)rd->fk_rot[4 * f + k]; ref[k] = (R)rd->fk_ref[4 * f + k]; }
+        /* local_rot_ang (system.py:178-188) */
+        R axes[3][3];
+        for (int l = 0; l < 3; l++) {
+          R e3[3] = {0, 0, 0};
+          e3[l] = 1;
+          rotate(e3, jr, axes[l]);
+        }
+        R lang[3];
+        for (int k = 0; k < 3; k++) lang[k] = axes[0][k] * vel3[0] + axes[1][k] * vel3[1] + axes[2][k] * vel3[2];
+        R rot[4];
+        memcpy(rot, ref, sizeof(rot));
+        for (int l = 0; l < 3; l++) {
+          R ax[3], nr[4], t[4];
+          rotate(axes[l], rot, ax);
+          quat_rot_axis(ax, ang3[l], nr);
+          quat_mul(nr, rot, t);
+          memcpy(rot, t, sizeof(rot));
+        }
+        /* set_qp (system.py:197-209) */
+        int bp = rd->fk_body_p[f], bc = rd->fk_body_c[f];
+        R wr[4], oc[3], lp[3], wp[3], wa[3], offp[3], offc[3];
+        for (int k = 0; k < 3; k++) { offp[k] = (R)rd->fk_off_p[3 * f + k]; offc[k] = (R)rd->fk_off_c[3 * f + k]; }
+        quat_mul(q[bp].rot, rot, wr);
+        rotate(offc, rot, oc);
+        for (int k = 0; k < 3; k++) lp[k] = offp[k] - oc[k];
+        rotate(lp, q[bp].rot, wp);
+        rotate(lang, q[bp].rot, wa);
+        for (int k = 0; k < 3; k++) { q[bc].pos[k] = q[bp].pos[k] + wp[k]; q[bc].ang[k] = wa[k]; }
+        memcpy(q[bc].rot, wr, sizeof(wr));
+      }
+      /* bodies.min_z per root group, then lift (system.py:213-240) */
+      for (int gi = 0; gi < rd->n_root_groups; gi++) zmin[gi] = (R)INFINITY;
+      for (int b = 0; b < N; b++) {
+        int gi = rd->body_root_group[b];
+        if (gi < 0) continue;
+        R bz = (R)INFINITY;
+        for (int p = 0; p < rd->n_zpts; p++) {
+          if (rd->zpt_body[p] != b) continue;
+          R loc[3], wz[3];
+          for (int k = 0; k < 3; k++) loc[k] = (R)rd->zpt_local[3 * p + k];
+          rotate(loc, q[b].rot, wz);
+          R z = q[b].pos[2] + wz[2] - (R)rd->zpt_radius[p];
+          bz = z < bz ? z : bz;
+        }
+        if (rd->body_zero_cand[b]) bz = bz < 0 ? bz : (R)0;
+        zmin[gi] = bz < zmin[gi] ? bz : zmin[gi];
+      }
+      for (int b = 0; b < N; b++) {
+        int gi = rd->body_root_group[b];
+        if (gi < 0) continue;
+        q[b].pos[2] = q[b].pos[2] - zmin[gi] * (R)1;
+        q[b].pos[0] = q[b].pos[0] - zmin[gi] * (R)0;
+        q[b].pos[1] = q[b].pos[1] - zmin[gi] * (R)0;
+      }
+      store_qp(q, qp_out + e * 13 * N, N);
+    }
+    free(q); free(zmin);
+  }
+  return 0;
+}
