@@ -1,0 +1,193 @@
+"""Benchmark: env-steps/sec of Ant at 4096 envs per GPU (BASELINE.json).
+
+One step = one `Env.step` of `envs.create('ant', batch_size=B,
+episode_length=1000, auto_reset=True)`, i.e. ONE fused kernel launch doing
+10 PBD substeps + observation + reward + Episode/AutoReset, on synthetic
+U[-1,1] actions drawn on the device each step. Inputs are resident in HBM.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+    torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU)
+
+Multi-GPU: every rank owns B envs (weak scaling, env ids offset by rank) and
+the only collective is an RCCL all-gather of the per-env (reward, done) pair
+each step. Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Algorithmic HBM bytes per Ant env-step: QP in 520 + QP out
+# 520 + action 32 + obs 348 + reward/done 8 = 1,428 B.
+ANT_BYTES_PER_ENV_STEP = 1428
+# Counted flops per Ant Env.step (reference numpy path).
+ANT_FLOPS_PER_ENV_STEP = 87382
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8 TB/s HBM3E
+FP32_VALU_PEAK_TFLOPS = 157.3
+
+
+def _dist():
+  ws = int(os.environ.get('WORLD_SIZE', '1'))
+  if ws > 1:
+    import torch.distributed as dist
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    return dist, dist.get_rank(), ws, local
+  return None, 0, 1, 0
+
+
+def cpu_baseline(batch, min_seconds=10.0, max_steps=200):
+  """The oracle's float32 C restatement (OpenMP over envs) on this host's
+  cores, on a bounded sample of the same workload."""
+  from oracle.oracle import Oracle
+  from tests.helpers import compiled
+  _, d, rd, _ = compiled('ant')
+  o = Oracle(d, rd, np.float32)
+  threads = o.max_threads()
+  rng = np.random.default_rng(0)
+  B = batch
+  T = np.load(os.path.join(ROOT, 'tests', 'golden', 'traj_ant.npz'))
+  qp = np.repeat(T['qp'][0], (B + 63) // 64, axis=0)[:B].astype(np.float32)
+  o.env_step('ant', qp[:64], rng.uniform(-1, 1, (64, 8)), 87, 10)  # warm
+  t0 = time.perf_counter()
+  steps = 0
+  while steps < max_steps and (time.perf_counter() - t0) < min_seconds:
+    act = rng.uniform(-1, 1, (B, 8)).astype(np.float32)
+    qp, _, _, _, _ = o.env_step('ant', qp, act, 87, 10)
+    steps += 1
+  dt = time.perf_counter() - t0
+  return {'value': B * steps / dt, 'unit': 'env-steps/s', 'cores': threads, 'kind': 'port',
+          'sample': f'Ant, {B} envs x {steps} env-steps ({dt:.1f} s), float32 C '
+                    f'restatement (oracle/pbd_oracle.c), {threads} OpenMP threads, '
+                    f'{platform.processor() or platform.machine()}'}
+
+
+def _traffic():
+  """HBM bytes per launch from the committed PMC profile, if present."""
+  p = os.path.join(ROOT, 'profiles', 'traffic.json')
+  if os.path.exists(p):
+    with open(p) as f:
+      return json.load(f)
+  return None
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument('--gpus', type=int, default=1)
+  ap.add_argument('--steps', type=int, default=1000)
+  ap.add_argument('--warmup', type=int, default=50)
+  ap.add_argument('--batch', type=int, default=4096)
+  ap.add_argument('--no-cpu-baseline', action='store_true')
+  args = ap.parse_args()
+
+  dist, rank, world, local = _dist()
+  dev = torch.device('cuda', local)
+  torch.cuda.set_device(dev)
+  from brax_amd import _native, envs
+  import ctypes as C
+
+  B = args.batch
+  env = envs.create('ant', batch_size=B, episode_length=1000, auto_reset=True, device=dev)
+  state = env.reset(np.array([rank, 0x5EED], np.uint32))
+  acts = torch.empty((2, B, 8), dtype=torch.float32, device=dev)
+  lib = _native.lib()
+  gathered = (torch.empty((world, 2, B), dtype=torch.float32, device=dev)
+              if world > 1 else None)
+
+  def one_step(st, k, ev=None):
+    a = acts[k & 1]
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _native.check(lib.bx_uniform(C.c_void_p(a.data_ptr()), a.numel(), 1 + rank,
+                                 k * a.numel(), -1.0, 1.0, stream))
+    if ev is not None:
+      ev[0].record()
+    st = env.step(st, a)
+    if ev is not None:
+      ev[1].record()
+    if dist is not None:
+      rd = torch.stack([st.reward, st.done])
+      dist.all_gather_into_tensor(gathered, rd)
+    return st
+
+  for k in range(args.warmup):
+    state = one_step(state, k)
+  torch.cuda.synchronize()
+  if dist is not None:
+    dist.barrier()
+  torch.cuda.synchronize()
+  events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for _ in range(args.steps)]
+  t0 = time.perf_counter()
+  for k in range(args.steps):
+    state = one_step(state, args.warmup + k, events[k])
+  torch.cuda.synchronize()
+  if dist is not None:
+    dist.barrier()
+  torch.cuda.synchronize()
+  elapsed = time.perf_counter() - t0
+  kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+  if dist is not None:
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+  total = B * world * args.steps
+  value = total / elapsed
+  if rank != 0:
+    dist.destroy_process_group()
+    return
+  bytes_per_launch = ANT_BYTES_PER_ENV_STEP * B
+  achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+  tr = _traffic()
+  traffic = None
+  if tr and tr.get('batch') == B:
+    traffic = tr.get('hbm_bytes_per_launch')
+  out = {
+      'metric': 'env-steps/sec (Ant, 4096 envs/GPU)',
+      'value': value,
+      'unit': 'env-steps/s',
+      'n_gpus': world,
+      'steps': args.steps,
+      'warmup': args.warmup,
+      'ms_per_step': elapsed * 1e3 / args.steps,
+      'higher_is_better': True,
+      'scaling': 'weak',
+      'vs_baseline': None,
+      'dtype': 'f32',
+      'data': 'synthetic: U[-1,1] actions drawn on device each step; reset from the '
+              'Ant config with device-RNG joint noise',
+      'config': {'workload': 'Ant-v1 Env.step (10 PBD substeps + obs/reward + '
+                             'Episode/AutoReset), envs.create(ant)',
+                 'envs_per_gpu': B, 'episode_length': 1000, 'substeps': 10,
+                 'parallelism': f'env-shard x{world}'},
+      'roofline': {'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
+                   'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
+                   'traffic': traffic,
+                   'kernel': 'bx::env_step_kernel<16>', 'kernel_ms': kern_ms,
+                   'bytes_per_launch': bytes_per_launch,
+                   'note': 'fused env-step is VALU/latency-bound (AI ~61 flop/B, '
+                           'SURVEY 8(d)); compute view below',
+                   'valu_tflops': ANT_FLOPS_PER_ENV_STEP * B / (kern_ms * 1e-3) / 1e12,
+                   'valu_peak_tflops': FP32_VALU_PEAK_TFLOPS},
+  }
+  if world == 1 and not args.no_cpu_baseline:
+    out['cpu_baseline'] = cpu_baseline(B)
+  else:
+    out['cpu_baseline'] = None
+  print(json.dumps(out), flush=True)
+  if dist is not None:
+    dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+  main()

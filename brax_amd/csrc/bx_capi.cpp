@@ -1,0 +1,443 @@
+// bx_capi.cpp — the C ABI (include/brax_amd.h): descriptor -> device blob,
+// argument validation, and stream-ordered kernel launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/brax_amd.h"
+#include "pbd_launch.h"
+#include "pbd_layout.h"
+
+using namespace bx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& m) {
+  g_err = m;
+  return 1;
+}
+
+#define HIP_OK(expr)                                                       \
+  do {                                                                     \
+    hipError_t _e = (expr);                                                \
+    if (_e != hipSuccess) return fail(std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+uint32_t fbits(double x) {
+  float f = (float)x;
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return u;
+}
+
+}  // namespace
+
+struct bx_system {
+  int device = 0;
+  BlobHdr hdr{};
+  std::vector<uint32_t> host;
+  uint32_t* blob = nullptr;
+  int L = 16;
+  size_t lds_env = 0;    // bytes per block for the per-env kernels
+  size_t lds_reset = 0;  // bytes per block for default_qp
+};
+
+namespace {
+
+struct Builder {
+  std::vector<uint32_t> w;
+  int alloc(int n) {
+    int o = (int)w.size();
+    w.resize(w.size() + (size_t)std::max(n, 0), 0u);
+    return o;
+  }
+  void f(int o, double x) { w[o] = fbits(x); }
+  void i(int o, int x) { w[o] = (uint32_t)x; }
+};
+
+int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
+  const int N = d->n_bodies, J = d->n_joints, K = d->n_actuators, R = d->n_rows, G = d->n_groups;
+  if (N <= 0) return fail("descriptor has no bodies");
+  if (d->substeps <= 0) return fail("substeps must be positive");
+  for (int j = 0; j < J; j++) {
+    if (d->joint_body_p[j] < 0 || d->joint_body_p[j] >= N || d->joint_body_c[j] < 0 ||
+        d->joint_body_c[j] >= N)
+      return fail("joint body index out of range");
+    if (d->joint_type[j] != BX_JOINT_REVOLUTE && d->joint_type[j] != BX_JOINT_SPHERICAL)
+      return fail("unsupported joint type");
+  }
+  for (int a = 0; a < K; a++) {
+    if (d->act_joint[a] < 0 || d->act_joint[a] >= J) return fail("actuator joint out of range");
+    for (int l = 0; l < 3; l++)
+      if (d->act_index[3 * a + l] >= d->action_size) return fail("actuator index out of range");
+  }
+  for (int x = 0; x < R; x++) {
+    if (d->row_body_a[x] < 0 || d->row_body_a[x] >= N || d->row_body_b[x] < 0 ||
+        d->row_body_b[x] >= N)
+      return fail("contact row body out of range");
+    if (d->row_group[x] < 0 || d->row_group[x] >= G) return fail("contact row group out of range");
+    int fn = d->col_fn[d->row_group[x]];
+    if (fn != BX_COL_CAPSULE_PLANE && fn != BX_COL_CAPSULE_CAPSULE)
+      return fail("unsupported contact function");
+  }
+  if (G >= 128) return fail("too many collider groups");
+  if (2 * R >= (1 << 24)) return fail("too many contact rows");
+
+  Builder B;
+  int o_hdr = B.alloc((int)(sizeof(BlobHdr) / 4));
+  (void)o_hdr;
+  BlobHdr H{};
+  H.N = N; H.J = J; H.K = K; H.R = R; H.G = G; H.A = d->action_size; H.substeps = d->substeps;
+  H.num_joint_dof = d->num_joint_dof;
+  H.h = (float)d->h;
+  H.dt = (float)d->dt;
+  // integrators.py:87,91 — exp(damping * dt) of Python doubles, one constant
+  H.vexp = (float)std::exp(d->velocity_damping * d->h);
+  H.aexp = (float)std::exp(d->angular_damping * d->h);
+  H.gx = (float)d->gravity[0]; H.gy = (float)d->gravity[1]; H.gz = (float)d->gravity[2];
+
+  H.o_body = B.alloc(N * BODY_STRIDE);
+  for (int b = 0; b < N; b++) {
+    int o = H.o_body + b * BODY_STRIDE;
+    B.f(o + BODY_MASS, d->body_mass[b]);
+    for (int k = 0; k < 3; k++) {
+      B.f(o + BODY_I + k, d->body_inv_inertia[3 * b + k]);
+      B.f(o + BODY_PM + k, d->pos_mask[3 * b + k]);
+      B.f(o + BODY_RM + k, d->rot_mask[3 * b + k]);
+    }
+    for (int k = 0; k < 4; k++) B.f(o + BODY_QM + k, d->quat_mask[4 * b + k]);
+  }
+  H.o_joint = B.alloc(J * JOINT_STRIDE);
+  int D = 0;
+  for (int j = 0; j < J; j++) {
+    int o = H.o_joint + j * JOINT_STRIDE;
+    int type = d->joint_type[j];
+    int nang = d->joint_free_dofs[j] >= 0 ? d->joint_free_dofs[j] : (type == BX_JOINT_REVOLUTE ? 1 : 3);
+    B.i(o + J_TYPE, type);
+    B.i(o + J_BP, d->joint_body_p[j]);
+    B.i(o + J_BC, d->joint_body_c[j]);
+    B.i(o + J_FREE, d->joint_free_dofs[j]);
+    B.i(o + J_DOF, d->joint_dof[j]);
+    B.i(o + J_ANGLE_OFF, D);
+    B.i(o + J_NANGLES, nang);
+    D += nang;
+    B.f(o + J_DAMP, d->joint_damping[j]);
+    B.f(o + J_SP, d->joint_scale_pos[j]);
+    B.f(o + J_SA, d->joint_scale_ang[j]);
+    for (int k = 0; k < 3; k++) {
+      B.f(o + J_OFFP + k, d->joint_off_p[3 * j + k]);
+      B.f(o + J_OFFC + k, d->joint_off_c[3 * j + k]);
+    }
+    for (int k = 0; k < 9; k++) {
+      B.f(o + J_AXP + k, d->joint_axis_p[9 * j + k]);
+      B.f(o + J_AXC + k, d->joint_axis_c[9 * j + k]);
+    }
+    for (int k = 0; k < 6; k++) B.f(o + J_LIM + k, d->joint_limit[6 * j + k]);
+  }
+  H.D = D;
+  H.o_act = B.alloc(K * ACT_STRIDE);
+  for (int a = 0; a < K; a++) {
+    int o = H.o_act + a * ACT_STRIDE;
+    B.i(o + A_TYPE, d->act_type[a]);
+    B.i(o + A_JOINT, d->act_joint[a]);
+    for (int k = 0; k < 3; k++) B.i(o + A_IDX + k, d->act_index[3 * a + k]);
+    B.f(o + A_STR, d->act_strength[a]);
+  }
+  H.o_row = B.alloc(R * ROW_STRIDE);
+  for (int x = 0; x < R; x++) {
+    int o = H.o_row + x * ROW_STRIDE;
+    int g = d->row_group[x];
+    B.i(o + R_GROUP, g);
+    B.i(o + R_A, d->row_body_a[x]);
+    B.i(o + R_B, d->row_body_b[x]);
+    B.i(o + R_FN, d->col_fn[g]);
+    B.i(o + R_ONEWAY, d->col_oneway[g]);
+    for (int k = 0; k < 3; k++) {
+      B.f(o + R_APOS + k, d->row_a_pos[3 * x + k]);
+      B.f(o + R_AEND + k, d->row_a_end[3 * x + k]);
+      B.f(o + R_BPOS + k, d->row_b_pos[3 * x + k]);
+      B.f(o + R_BEND + k, d->row_b_end[3 * x + k]);
+    }
+    B.f(o + R_ARAD, d->row_a_radius[x]);
+    B.f(o + R_BRAD, d->row_b_radius[x]);
+    B.f(o + R_FRIC, d->row_friction[x]);
+    B.f(o + R_ELAS, d->row_elasticity[x]);
+    B.f(o + R_SCALE, d->col_scale[g]);
+    B.f(o + R_THR, d->col_velocity_threshold[g]);
+    B.f(o + R_ERP, d->col_baumgarte_erp[g]);
+  }
+  // gather lists (the reference's segment_sum order: per group, parents then
+  // children / a-rows then b-rows)
+  std::vector<std::vector<int>> jl(N), al(N), cl(N);
+  for (int j0 = 0; j0 < J;) {
+    int g = d->joint_group[j0], j1 = j0;
+    while (j1 < J && d->joint_group[j1] == g) j1++;
+    for (int j = j0; j < j1; j++) jl[d->joint_body_p[j]].push_back(2 * j);
+    for (int j = j0; j < j1; j++) jl[d->joint_body_c[j]].push_back(2 * j + 1);
+    j0 = j1;
+  }
+  for (int a0 = 0; a0 < K;) {
+    int g = d->act_group[a0], a1 = a0;
+    while (a1 < K && d->act_group[a1] == g) a1++;
+    for (int a = a0; a < a1; a++) al[d->joint_body_p[d->act_joint[a]]].push_back(2 * a);
+    for (int a = a0; a < a1; a++) al[d->joint_body_c[d->act_joint[a]]].push_back(2 * a + 1);
+    a0 = a1;
+  }
+  for (int g = 0; g < G; g++) {
+    for (int x = 0; x < R; x++)
+      if (d->row_group[x] == g) cl[d->row_body_a[x]].push_back((2 * x) | (g << 24));
+    if (!d->col_oneway[g])
+      for (int x = 0; x < R; x++)
+        if (d->row_group[x] == g) cl[d->row_body_b[x]].push_back((2 * x + 1) | (g << 24));
+  }
+  auto put_lists = [&](std::vector<std::vector<int>>& L_, int& o_off, int& o_l) {
+    o_off = B.alloc(N + 1);
+    int tot = 0;
+    for (int b = 0; b < N; b++) tot += (int)L_[b].size();
+    o_l = B.alloc(tot);
+    int k = 0;
+    for (int b = 0; b < N; b++) {
+      B.i(o_off + b, k);
+      for (int v : L_[b]) B.i(o_l + k++, v);
+    }
+    B.i(o_off + N, k);
+  };
+  put_lists(jl, H.o_jl_off, H.o_jl);
+  put_lists(al, H.o_al_off, H.o_al);
+  put_lists(cl, H.o_cl_off, H.o_cl);
+
+  // reset tables
+  if (r) {
+    H.n_fk = r->n_fk;
+    H.n_root_groups = r->n_root_groups;
+    H.o_base = B.alloc(N * 13);
+    for (int k = 0; k < N * 13; k++) B.f(H.o_base + k, r->base_qp[k]);
+    H.o_fk = B.alloc(r->n_fk * FK_STRIDE);
+    for (int f = 0; f < r->n_fk; f++) {
+      int o = H.o_fk + f * FK_STRIDE;
+      if (r->fk_body_p[f] < 0 || r->fk_body_p[f] >= N || r->fk_body_c[f] < 0 || r->fk_body_c[f] >= N)
+        return fail("reset joint body out of range");
+      B.i(o + FK_BP, r->fk_body_p[f]);
+      B.i(o + FK_BC, r->fk_body_c[f]);
+      for (int l = 0; l < 3; l++) {
+        int ix = r->fk_dof_index[3 * f + l];
+        if (ix >= d->num_joint_dof) return fail("reset dof index out of range");
+        B.i(o + FK_IDX + l, ix);
+      }
+      for (int k = 0; k < 4; k++) {
+        B.f(o + FK_ROT + k, r->fk_rot[4 * f + k]);
+        B.f(o + FK_REF + k, r->fk_ref[4 * f + k]);
+      }
+      for (int k = 0; k < 3; k++) {
+        B.f(o + FK_OFFP + k, r->fk_off_p[3 * f + k]);
+        B.f(o + FK_OFFC + k, r->fk_off_c[3 * f + k]);
+      }
+    }
+    std::vector<std::vector<int>> zl(N);
+    for (int p = 0; p < r->n_zpts; p++) {
+      if (r->zpt_body[p] < 0 || r->zpt_body[p] >= N) return fail("min_z point body out of range");
+      zl[r->zpt_body[p]].push_back(p);
+    }
+    H.o_zoff = B.alloc(N + 1);
+    H.o_zpt = B.alloc(r->n_zpts * 4);
+    int k = 0;
+    for (int b = 0; b < N; b++) {
+      B.i(H.o_zoff + b, k);
+      for (int p : zl[b]) {
+        for (int q = 0; q < 3; q++) B.f(H.o_zpt + 4 * k + q, r->zpt_local[3 * p + q]);
+        B.f(H.o_zpt + 4 * k + 3, r->zpt_radius[p]);
+        k++;
+      }
+    }
+    B.i(H.o_zoff + N, k);
+    H.o_zero = B.alloc(N);
+    H.o_rgroup = B.alloc(N);
+    for (int b = 0; b < N; b++) {
+      B.i(H.o_zero + b, r->body_zero_cand[b]);
+      B.i(H.o_rgroup + b, r->body_root_group[b]);
+    }
+  }
+  H.total_words = (int)B.w.size();
+
+  // per-env LDS layout
+  int L = std::max({N, J, K, R, 1});
+  L = L <= 16 ? 16 : (L <= 32 ? 32 : 64);
+  H.L = L;
+  int off = 0;
+  auto carve = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
+  H.l_qp = carve(N * QP_STRIDE);
+  H.l_prev = carve(N * PREV_STRIDE);
+  H.l_rb = carve(N * RB_STRIDE);
+  H.l_jslot = carve(J * 16);
+  H.l_aslot = carve(K * 8);
+  H.l_rowd = carve(R * 8);
+  H.l_cslot = carve(R * 16);
+  H.l_acc = carve(N * ACC_STRIDE);
+  H.l_ang = carve(2 * D);
+  H.l_red = carve(64);
+  H.env_words = off;
+  std::memcpy(B.w.data(), &H, sizeof(BlobHdr));
+
+  S->hdr = H;
+  S->host = std::move(B.w);
+  S->L = L;
+  S->lds_env = (size_t)(64 / L) * H.env_words * 4;
+  S->lds_reset = (size_t)64 * N * 13 * 4;
+  if (S->lds_env > 160 * 1024) return fail("system too large for one workgroup's LDS");
+  if (r && S->lds_reset > 160 * 1024) return fail("system too large for the reset kernel's LDS");
+  return 0;
+}
+
+hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+bool field_ok(const bx_field& f) { return f.ptr != nullptr; }
+bool qp_ok(const bx_qp& q) {
+  return field_ok(q.pos) && field_ok(q.rot) && field_ok(q.vel) && field_ok(q.ang);
+}
+
+}  // namespace
+
+extern "C" {
+
+int bx_abi_version(void) { return BX_ABI_VERSION; }
+
+const char* bx_last_error(void) { return g_err.c_str(); }
+
+int bx_device_count(int* count) {
+  HIP_OK(hipGetDeviceCount(count));
+  return 0;
+}
+
+int bx_system_create(const bx_desc* desc, const bx_reset_desc* reset, int device, bx_system** out) {
+  if (!desc || !out) return fail("null argument");
+  bx_system* S = new bx_system();
+  S->device = device;
+  if (int rc = build_blob(desc, reset, S)) {
+    delete S;
+    return rc;
+  }
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc(&S->blob, S->host.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(S->blob, S->host.data(), S->host.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    std::string m = std::string("device setup: ") + hipGetErrorString(e);
+    if (S->blob) (void)hipFree(S->blob);
+    delete S;
+    return fail(m);
+  }
+  *out = S;
+  return 0;
+}
+
+int bx_system_destroy(bx_system* S) {
+  if (!S) return 0;
+  if (S->blob) {
+    (void)hipSetDevice(S->device);
+    HIP_OK(hipFree(S->blob));
+  }
+  delete S;
+  return 0;
+}
+
+int bx_system_lanes(bx_system* S) { return S ? S->L : 0; }
+
+int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* act,
+                   int64_t act_stride, const bx_qp* qout, const bx_info* info, void* stream) {
+  if (!S || !qin || !qout) return fail("null argument");
+  if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
+  if (!qp_ok(*qin) || !qp_ok(*qout)) return fail("null qp field");
+  if (S->hdr.A > 0 && !act) return fail("null action");
+  StepArgs a{};
+  a.blob = S->blob;
+  a.n_envs = n_envs;
+  a.qin = *qin;
+  a.qout = *qout;
+  a.act = act;
+  a.act_stride = act_stride;
+  if (info) a.info = *info;
+  HIP_OK(launch_system_step(S->L, n_envs, S->lds_env, as_stream(stream), a));
+  return 0;
+}
+
+int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx_env_state* in,
+                const float* act, int64_t act_stride, const bx_env_state* out, void* stream) {
+  if (!S || !env || !in || !out) return fail("null argument");
+  if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
+  if (!qp_ok(in->qp) || !qp_ok(out->qp)) return fail("null qp field");
+  if (!in->done || !out->done || !out->reward || !out->obs) return fail("null env buffer");
+  if (env->auto_reset && (!qp_ok(env->first_qp) || !env->first_obs))
+    return fail("auto_reset needs first_qp and first_obs");
+  if (env->episode_length > 0 && (!out->steps || !out->truncation))
+    return fail("episode wrapper needs steps and truncation buffers");
+  if (env->kind < BX_ENV_ANT || env->kind > BX_ENV_HALFCHEETAH) return fail("unknown env kind");
+  EnvArgs a{};
+  a.blob = S->blob;
+  a.n_envs = n_envs;
+  a.P = *env;
+  a.in = *in;
+  a.out = *out;
+  a.act = act;
+  a.act_stride = act_stride;
+  HIP_OK(launch_env_step(S->L, n_envs, S->lds_env, as_stream(stream), a));
+  return 0;
+}
+
+int bx_system_info(bx_system* S, int64_t n_envs, const bx_qp* qp, const bx_info* info, void* stream) {
+  if (!S || !qp || !info) return fail("null argument");
+  if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
+  InfoArgs a{};
+  a.blob = S->blob;
+  a.n_envs = n_envs;
+  a.q = *qp;
+  a.info = *info;
+  HIP_OK(launch_info_obs(S->L, n_envs, S->lds_env, as_stream(stream), a));
+  return 0;
+}
+
+int bx_env_observe(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx_qp* qp,
+                   const float* act, int64_t act_stride, float* obs, void* stream) {
+  if (!S || !env || !qp || !obs) return fail("null argument");
+  if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
+  InfoArgs a{};
+  a.blob = S->blob;
+  a.n_envs = n_envs;
+  a.q = *qp;
+  a.kind = env->kind;
+  a.obs_size = env->obs_size;
+  a.act = act;
+  a.act_stride = act_stride;
+  a.obs = obs;
+  HIP_OK(launch_info_obs(S->L, n_envs, S->lds_env, as_stream(stream), a));
+  return 0;
+}
+
+int bx_system_default_qp(bx_system* S, int64_t n_envs, const float* joint_angle,
+                         const float* joint_velocity, const bx_qp* qp_out, void* stream) {
+  if (!S || !qp_out) return fail("null argument");
+  if (S->hdr.o_base == 0) return fail("system was created without a reset descriptor");
+  if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
+  if (S->hdr.num_joint_dof > 0 && (!joint_angle || !joint_velocity)) return fail("null joint arrays");
+  ResetArgs a{};
+  a.blob = S->blob;
+  a.n_envs = n_envs;
+  a.angle = joint_angle;
+  a.vel = joint_velocity;
+  a.out = *qp_out;
+  HIP_OK(launch_default_qp(n_envs, S->lds_reset, as_stream(stream), a));
+  return 0;
+}
+
+int bx_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset, float lo, float hi, void* stream) {
+  if (n <= 0) return n == 0 ? 0 : fail("negative n");
+  if (!out) return fail("null output");
+  HIP_OK(launch_uniform(out, n, seed, offset, lo, hi, as_stream(stream)));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1337 @@
+// pbd_kernels.hip — MI355X (gfx950) kernels of the PBD env stepper.
+//
+// One fused launch runs a whole `Env.step` for a batch of environments:
+// `System._pbd_step` (brax/physics/system.py:254-325: actuators, joint damping,
+// Euler update/kinetic, PBD joint projection, capsule contacts, velocity
+// projection, contact velocity pass — `substeps` times) followed by the env
+// layer (obs/reward/done/metrics, ant.py:222-282) and the Episode/AutoReset
+// wrappers (wrappers.py:105-148).
+//
+// Work mapping: L lanes (16/32/64) of a 64-wide wavefront
+// own one environment; a workgroup is one wavefront holding 64/L envs. Every
+// per-item phase (bodies, joints, actuators, contact rows) spreads its items
+// over the env's L lanes; the env's state lives in LDS for the whole step and
+// item results are combined per body by deterministic gather lists (the
+// reference's `segment_sum`s), so the only HBM traffic is the QP in/out,
+// the action and the env-layer outputs.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pbd_launch.h"
+#include "pbd_layout.h"
+#include "pbd_math.h"
+
+namespace bx {
+
+// ---------------------------------------------------------------------------
+// constant-blob accessors (the descriptor lives in HBM, read-only, L2-resident)
+// ---------------------------------------------------------------------------
+struct Cst {
+  const uint32_t* __restrict__ w;
+  __device__ __forceinline__ int i(int off) const { return (int)w[off]; }
+  __device__ __forceinline__ float f(int off) const { return __uint_as_float(w[off]); }
+  __device__ __forceinline__ v3 f3(int off) const { return mk(f(off), f(off + 1), f(off + 2)); }
+};
+
+struct BodyC {
+  float mass;
+  v3 I, pm, rm;
+  q4 qm;
+};
+__device__ __forceinline__ BodyC load_body(const Cst& c, const BlobHdr& H, int b) {
+  int o = H.o_body + b * BODY_STRIDE;
+  BodyC r;
+  r.mass = c.f(o + BODY_MASS);
+  r.I = c.f3(o + BODY_I);
+  r.pm = c.f3(o + BODY_PM);
+  r.rm = c.f3(o + BODY_RM);
+  r.qm = q4{c.f(o + BODY_QM), c.f(o + BODY_QM + 1), c.f(o + BODY_QM + 2), c.f(o + BODY_QM + 3)};
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// LDS views of one env
+// ---------------------------------------------------------------------------
+struct Env {
+  float* qp;     // N x 16: pos 0..2, rot 3..6, vel 7..9, ang 10..12
+  float* prev;   // N x 8 : pos, rot   (qprev)
+  float* rb;     // N x 12: pos, vel, ang (qp_right_before)
+  float* jslot;  // J x 2 x 8
+  float* aslot;  // K x 2 x 4
+  float* rowd;   // R x 8 : cpos 3, normal 3, pen, dlambda
+  float* cslot;  // R x 2 x 8
+  float* acc;    // N x 12: info contact vel 3, ang 3, info actuator ang 3, dp_a 3
+  float* ang;    // 2 x D: joint angles, joint vels
+  float* red;    // 64 scratch
+};
+
+__device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+__device__ __forceinline__ void st3(float* p, v3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
+__device__ __forceinline__ q4 ld4(const float* p) { return q4{p[0], p[1], p[2], p[3]}; }
+__device__ __forceinline__ void st4(float* p, q4 q) { p[0] = q.w; p[1] = q.x; p[2] = q.y; p[3] = q.z; }
+
+struct QP {
+  v3 pos;
+  q4 rot;
+  v3 vel, ang;
+};
+__device__ __forceinline__ QP ldqp(const float* s) {
+  return QP{ld3(s), ld4(s + 3), ld3(s + 7), ld3(s + 10)};
+}
+__device__ __forceinline__ void stqp(float* s, const QP& q) {
+  st3(s, q.pos); st4(s + 3, q.rot); st3(s + 7, q.vel); st3(s + 10, q.ang);
+}
+
+// ---------------------------------------------------------------------------
+// joints (brax/physics/joints.py)
+// ---------------------------------------------------------------------------
+struct JointC {
+  int type, bp, bc, free, angle_off, n_angles;
+  float damping, sp, sa;
+  v3 off_p, off_c;
+  v3 axp[3], axc[3];
+  float lim[6];
+  float mp, mc;
+  v3 Ip, Ic;
+};
+__device__ __forceinline__ JointC load_joint(const Cst& c, const BlobHdr& H, int j) {
+  int o = H.o_joint + j * JOINT_STRIDE;
+  JointC r;
+  r.type = c.i(o + J_TYPE);
+  r.bp = c.i(o + J_BP);
+  r.bc = c.i(o + J_BC);
+  r.free = c.i(o + J_FREE);
+  r.angle_off = c.i(o + J_ANGLE_OFF);
+  r.n_angles = c.i(o + J_NANGLES);
+  r.damping = c.f(o + J_DAMP);
+  r.sp = c.f(o + J_SP);
+  r.sa = c.f(o + J_SA);
+  r.off_p = c.f3(o + J_OFFP);
+  r.off_c = c.f3(o + J_OFFC);
+  for (int k = 0; k < 3; k++) {
+    r.axp[k] = c.f3(o + J_AXP + 3 * k);
+    r.axc[k] = c.f3(o + J_AXC + 3 * k);
+  }
+  for (int k = 0; k < 6; k++) r.lim[k] = c.f(o + J_LIM + k);
+  int ob = H.o_body + r.bp * BODY_STRIDE, oc = H.o_body + r.bc * BODY_STRIDE;
+  r.mp = c.f(ob + BODY_MASS);
+  r.mc = c.f(oc + BODY_MASS);
+  r.Ip = c.f3(ob + BODY_I);
+  r.Ic = c.f3(oc + BODY_I);
+  return r;
+}
+
+// Joint.apply_angle_update (joints.py:130-152): adds rot parts into dqp/dqc
+__device__ __forceinline__ void angle_update(const JointC& J, const q4& rp, const q4& rc, v3 dq,
+                                             q4& dqp, q4& dqc) {
+  float th = safe_norm(dq);
+  v3 n = dq / (th + 1e-6f);
+  float w1 = dot(n, mul(J.Ip, n));
+  float w2 = dot(n, mul(J.Ic, n));
+  float dl = -th / (w1 + w2 + 1e-6f);
+  v3 p = -dl * n;
+  q4 a = J.sa * (0.5f * vec_quat_mul(mul(J.Ip, p), rp));
+  q4 b = J.sa * (-0.5f * vec_quat_mul(mul(J.Ic, p), rc));
+  dqp = dqp + a;
+  dqc = dqc + b;
+}
+
+// Revolute/Spherical.apply_reduced (joints.py:270-309, 332-386)
+__device__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, q4& dpr,
+                            v3& dcp, q4& dcr) {
+  // positional constraint: apply_position_update (joints.py:154-195)
+  v3 pw = p.pos + rotate(J.off_p, p.rot);
+  v3 cw = c.pos + rotate(J.off_c, c.rot);
+  v3 dx = pw - cw;
+  v3 rp = pw - p.pos, rc = cw - c.pos;
+  float cc = safe_norm(dx);
+  v3 n = dx / (cc + 1e-6f);
+  v3 cr1 = cross(rp, n), cr2 = cross(rc, n);
+  float w1 = 1.f / J.mp + dot(cr1, mul(J.Ip, cr1));
+  float w2 = 1.f / J.mc + dot(cr2, mul(J.Ic, cr2));
+  float dl = -cc / (w1 + w2 + 1e-6f);
+  v3 pv = dl * n;
+  dpp = J.sp * (pv / J.mp);
+  dpr = J.sp * (0.5f * vec_quat_mul(mul(J.Ip, cross(rp, pv)), p.rot));
+  dcp = J.sp * (-pv / J.mc);
+  dcr = J.sp * (-0.5f * vec_quat_mul(mul(J.Ic, cross(rc, pv)), c.rot));
+  q4 ap{0.f, 0.f, 0.f, 0.f}, ac{0.f, 0.f, 0.f, 0.f};
+  if (J.type == 1) {
+    v3 axis = rotate(J.axp[0], p.rot);
+    v3 ref_p = rotate(J.axp[2], p.rot);
+    v3 ref_c = rotate(J.axc[2], c.rot);
+    float psi = signed_angle(axis, ref_p, ref_c);
+    v3 axis_c = rotate(J.axc[0], c.rot);
+    v3 dq1 = cross(axis, axis_c);
+    float ph = clampf(psi, J.lim[0], J.lim[1]);
+    q4 fix = quat_rot_axis(axis, ph);
+    v3 n1 = rotate(ref_p, fix);
+    v3 dq2 = cross(n1, ref_c);
+    q4 a1p{0, 0, 0, 0}, a1c{0, 0, 0, 0}, a2p{0, 0, 0, 0}, a2c{0, 0, 0, 0};
+    angle_update(J, p.rot, c.rot, dq1, a1p, a1c);
+    angle_update(J, p.rot, c.rot, dq2, a2p, a2c);
+    ap = a1p + a2p;
+    ac = a1c + a2c;
+  } else {
+    v3 a1p = rotate(J.axp[0], p.rot), a2p = rotate(J.axp[1], p.rot);
+    v3 a1c = rotate(J.axc[0], c.rot), a2c = rotate(J.axc[1], c.rot), a3c = rotate(J.axc[2], c.rot);
+    v3 lon = cross(a3c, a1p);
+    lon = lon / (1e-6f + safe_norm(lon));
+    v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
+    xz = xz / (1e-6f + safe_norm(xz));
+    v3 a2n = cross(xz, a1p);
+    a2n = a2n / (1e-6f + safe_norm(a2n));
+    float sg = signf(dot(a1p, a3c));
+    v3 nv[3] = {a1p, -a2n * sg, a3c};
+    v3 n1v[3] = {a2p, a1p, lon};
+    v3 n2v[3] = {lon, xz, a2c};
+#pragma unroll
+    for (int l = 0; l < 3; l++) {
+      // limit_angle (joints.py:343-355)
+      float ph = signed_angle(nv[l], n1v[l], n2v[l]);
+      float lo = J.lim[2 * l], hi = J.lim[2 * l + 1];
+      float mask = ph < lo ? 1.f : 0.f;
+      mask = ph > hi ? 1.f : mask;
+      ph = clampf(ph, lo, hi);
+      q4 fix = quat_rot_axis(nv[l], ph);
+      v3 n1 = rotate(n1v[l], fix);
+      v3 dq = cross(n1, n2v[l]) * mask;
+      angle_update(J, p.rot, c.rot, dq, ap, ac);
+    }
+  }
+  dpr = dpr + ap;
+  dcr = dcr + ac;
+}
+
+// Revolute/Spherical.axis_angle (joints.py:311-319, 388-415); returns dof
+__device__ int axis_angle(const JointC& J, const QP& p, const QP& c, v3* axes, float* ang) {
+  if (J.type == 1) {
+    axes[0] = rotate(J.axp[0], p.rot);
+    v3 ref_p = rotate(J.axp[2], p.rot);
+    v3 ref_c = rotate(J.axc[2], c.rot);
+    ang[0] = signed_angle(axes[0], ref_p, ref_c);
+    return 1;
+  }
+  v3 a1p = rotate(J.axp[0], p.rot), a2p = rotate(J.axp[1], p.rot);
+  v3 a1c = rotate(J.axc[0], c.rot), a2c = rotate(J.axc[1], c.rot), a3c = rotate(J.axc[2], c.rot);
+  v3 lon = cross(a3c, a1p);
+  lon = lon / (1e-10f + safe_norm(lon));
+  float psi = signed_angle(a1p, a2p, lon);
+  v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
+  xz = xz / (1e-10f + safe_norm(xz));
+  float cb = dot(xz, a1p);
+  float theta = acosf(clampf(cb, -1.f, 1.f)) * signf(dot(a1p, a3c));
+  float phi = signed_angle(-a3c, a2c, lon);
+  axes[0] = a1p; axes[1] = a2c; axes[2] = a3c;
+  ang[0] = psi; ang[1] = theta; ang[2] = phi;
+  return 3;
+}
+
+// ---------------------------------------------------------------------------
+// actuators (brax/physics/actuators.py:52-112)
+// ---------------------------------------------------------------------------
+struct ActC {
+  int type, joint;
+  int idx[3];
+  float strength;
+};
+__device__ __forceinline__ ActC load_act(const Cst& c, const BlobHdr& H, int a) {
+  int o = H.o_act + a * ACT_STRIDE;
+  ActC r;
+  r.type = c.i(o + A_TYPE);
+  r.joint = c.i(o + A_JOINT);
+  for (int k = 0; k < 3; k++) r.idx[k] = c.i(o + A_IDX + k);
+  r.strength = c.f(o + A_STR);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// contacts (brax/physics/colliders.py)
+// ---------------------------------------------------------------------------
+struct RowC {
+  int group, a, b, fn, oneway;
+  v3 a_pos, a_end, b_pos, b_end;
+  float a_rad, b_rad, fric, elas, scale, thr, erp;
+  float ma, mb;
+  v3 Ia, Ib;
+};
+__device__ __forceinline__ RowC load_row(const Cst& c, const BlobHdr& H, int r) {
+  int o = H.o_row + r * ROW_STRIDE;
+  RowC x;
+  x.group = c.i(o + R_GROUP);
+  x.a = c.i(o + R_A);
+  x.b = c.i(o + R_B);
+  x.fn = c.i(o + R_FN);
+  x.oneway = c.i(o + R_ONEWAY);
+  x.a_pos = c.f3(o + R_APOS);
+  x.a_end = c.f3(o + R_AEND);
+  x.a_rad = c.f(o + R_ARAD);
+  x.b_pos = c.f3(o + R_BPOS);
+  x.b_end = c.f3(o + R_BEND);
+  x.b_rad = c.f(o + R_BRAD);
+  x.fric = c.f(o + R_FRIC);
+  x.elas = c.f(o + R_ELAS);
+  x.scale = c.f(o + R_SCALE);
+  x.thr = c.f(o + R_THR);
+  x.erp = c.f(o + R_ERP);
+  int oa = H.o_body + x.a * BODY_STRIDE, ob = H.o_body + x.b * BODY_STRIDE;
+  x.ma = c.f(oa + BODY_MASS);
+  x.mb = c.f(ob + BODY_MASS);
+  x.Ia = c.f3(oa + BODY_I);
+  x.Ib = c.f3(ob + BODY_I);
+  return x;
+}
+
+// capsule_plane (colliders.py:744-759) / capsule_capsule (:805-819)
+__device__ void contact_gen(const RowC& R, const QP& a, const QP& b, v3& pos, v3& vel, v3& n,
+                            float& pen) {
+  if (R.fn == 0) {
+    v3 e = a.pos + rotate(R.a_end, a.rot);
+    n = rotate(mk(0.f, 0.f, 1.f), b.rot);
+    pos = e - n * R.a_rad;
+    vel = a.vel + cross(a.ang, pos - a.pos);
+    pen = dot(b.pos - pos, n);
+    return;
+  }
+  v3 pa = a.pos + rotate(R.a_pos, a.rot), ea = rotate(R.a_end, a.rot);
+  v3 pb = b.pos + rotate(R.b_pos, b.rot), eb = rotate(R.b_end, b.rot);
+  v3 a0 = pa + ea, a1 = pa - ea, b0 = pb + eb, b1 = pb - eb;
+  // _closest_segment_to_segment_points (geometry.py:394-451)
+  v3 da = a1 - a0;
+  float la = safe_norm(da);
+  la += 1e-6f * (float)(la == 0.f);
+  da = da / la;
+  float hla = la * 0.5f;
+  v3 db = b1 - b0;
+  float lb = safe_norm(db);
+  lb += 1e-6f * (float)(lb == 0.f);
+  db = db / lb;
+  float hlb = lb * 0.5f;
+  v3 am = a0 + da * hla, bm = b0 + db * hlb;
+  v3 tr = am - bm;
+  float dadb = dot(da, db), datr = dot(da, tr), dbtr = dot(db, tr);
+  float den = 1.f - dadb * dadb;
+  float ota = (-datr + dadb * dbtr) / (den + 1e-6f);
+  float otb = dbtr + ota * dadb;
+  float ta = clampf(ota, -hla, hla), tb = clampf(otb, -hlb, hlb);
+  v3 ba = am + da * ta, bb = bm + db * tb;
+  v3 ab = a1 - a0;
+  float t1 = clampf(dot(bb - a0, ab) / (dot(ab, ab) + 1e-6f), 0.f, 1.f);
+  v3 na = a0 + t1 * ab;
+  v3 va = bb - na;
+  float d1 = dot(va, va);
+  v3 bbv = b1 - b0;
+  float t2 = clampf(dot(ba - b0, bbv) / (dot(bbv, bbv) + 1e-6f), 0.f, 1.f);
+  v3 nb = b0 + t2 * bbv;
+  v3 vb = ba - nb;
+  float d2 = dot(vb, vb);
+  if (d1 < d2) ba = na; else bb = nb;
+  v3 pv = ba - bb;
+  float dist = safe_norm(pv);
+  n = pv / (1e-6f + dist);
+  pen = R.a_rad + R.b_rad - dist;
+  pos = (ba + bb) / 2.f;
+  vel = (a.vel + cross(a.ang, pos - a.pos)) - (b.vel + cross(b.ang, pos - b.pos));
+}
+
+// One/TwoWay._position_contact (colliders.py:306-377, 495-580)
+__device__ float position_contact(const RowC& R, const QP& a, const QP& b, const v3& ao_pos,
+                                  const q4& ao_rot, const v3& bo_pos, const q4& bo_rot, v3 cpos,
+                                  v3 n, float cpen, v3& oap, q4& oar, v3& obp, q4& obr) {
+  float sc = R.scale;
+  if (R.oneway) {
+    v3 pp = cpos, pc = cpos + n * cpen;
+    v3 dx = pp - pc;
+    pp = pp - a.pos;
+    float c = dot(dx, n);
+    v3 cr1 = cross(pp, n);
+    float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
+    float dl = -c / (w1 + 1e-6f);
+    float cm = c < 0.f ? 1.f : 0.f;
+    v3 pv = dl * n * cm;
+    oap = sc * (pv / R.ma);
+    oar = sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
+    // static friction
+    v3 r1 = rotate(cpos - a.pos, quat_inv(a.rot));
+    v3 p1bar = ao_pos + rotate(r1, ao_rot);
+    v3 dp = cpos - p1bar;
+    v3 dt = dp - dot(dp, n) * n;
+    float c2 = safe_norm(dt);
+    v3 n2 = dt / (c2 + 1e-6f);
+    cr1 = cross(pp, n2);
+    w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
+    float dlt = -c2 / (w1 + 0.f);
+    float sm = fabsf(dlt) < fabsf(R.fric * dl) ? 1.f : 0.f;
+    pv = dlt * n2 * sm * cm;
+    oap = oap + sc * (pv / R.ma);
+    oar = oar + sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
+    obp = mk(0.f, 0.f, 0.f);
+    obr = q4{0.f, 0.f, 0.f, 0.f};
+    return dl * cm;
+  }
+  v3 pp = cpos - n * cpen / 2.f - a.pos;
+  v3 pc = cpos + n * cpen / 2.f - b.pos;
+  float c = -cpen;
+  v3 cr1 = cross(pp, n), cr2 = cross(pc, n);
+  float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
+  float w2 = 1.f / R.mb + dot(cr2, mul(R.Ib, cr2));
+  float dl = -c / (w1 + w2 + 1e-6f);
+  float cm = c < 0.f ? 1.f : 0.f;
+  v3 pv = dl * n * cm;
+  oap = sc * (pv / R.ma);
+  oar = sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
+  obp = sc * (-pv / R.mb);
+  obr = sc * (-0.5f * vec_quat_mul(mul(R.Ib, cross(pc, pv)), b.rot));
+  v3 r1 = rotate(cpos - a.pos, quat_inv(a.rot));
+  v3 r2 = rotate(cpos - b.pos, quat_inv(b.rot));
+  v3 p1bar = ao_pos + rotate(r1, ao_rot);
+  v3 p2bar = bo_pos + rotate(r2, bo_rot);
+  v3 dp = (cpos - p1bar) - (cpos - p2bar);
+  v3 dt = dp - dot(dp, n) * n;
+  pp = cpos - a.pos;
+  pc = cpos - b.pos;
+  float c2 = safe_norm(dt);
+  v3 n2 = dt / (c2 + 1e-6f);
+  cr1 = cross(pp, n2);
+  cr2 = cross(pc, n2);
+  w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
+  w2 = 1.f / R.mb + dot(cr2, mul(R.Ib, cr2));
+  float dlt = -c2 / (w1 + w2);
+  float sm = fabsf(dlt) < fabsf(dl) ? 1.f : 0.f;
+  pv = dlt * n2 * sm * cm;
+  oap = oap + sc * (pv / R.ma);
+  oar = oar + sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
+  obp = obp + sc * (-pv / R.mb);
+  obr = obr + sc * (0.5f * vec_quat_mul(mul(R.Ib, cross(pc, -pv)), b.rot));
+  return dl;
+}
+
+// One/TwoWay._velocity_contact (colliders.py:379-442, 584-658);
+// (aov, aoa, aop) = qp_right_before of body a (vel, ang, pos), same for b.
+__device__ void velocity_contact(const RowC& R, float h, const QP& a, const QP& b, v3 aop,
+                                 v3 aov, v3 aoa, v3 bop, v3 bov, v3 boa, v3 cpos, v3 n, float cpen,
+                                 float dlam, v3& oav, v3& oaa, v3& obv, v3& oba) {
+  v3 ra = cpos - a.pos, rb = cpos - b.pos;
+  v3 rv = R.oneway ? a.vel + cross(a.ang, ra)
+                   : (a.vel + cross(a.ang, ra)) - (b.vel + cross(b.ang, rb));
+  float vn = dot(rv, n);
+  v3 vt = rv - n * vn;
+  float vtn = safe_norm(vt);
+  v3 vtd = vt / (1e-6f + vtn);
+  float lim = R.fric * fabsf(dlam) / (2.f * h);
+  float mag = fminf(lim, vtn);
+  v3 dvel = -vtd * mag;
+  v3 pdyn;
+  if (R.oneway) {
+    v3 aw = cross(ra, vtd);
+    float w = 1.f / R.ma + dot(aw, aw);
+    pdyn = dvel / (w + 1e-6f);
+  } else {
+    v3 a1 = cross(ra, vtd), a2 = cross(rb, vtd);
+    float w1 = 1.f / R.ma + dot(a1, mul(R.Ia, a1));
+    float w2 = 1.f / R.mb + dot(a2, mul(R.Ib, a2));
+    pdyn = dvel / (w1 + w2 + 1e-6f);
+  }
+  v3 rvo = R.oneway ? aov + cross(aoa, cpos - aop)
+                    : (aov + cross(aoa, cpos - aop)) - (bov + cross(boa, cpos - bop));
+  float vno = dot(rvo, n);
+  float mn = fminf(R.elas * vno, 0.f);
+  v3 dvr = n * (-vn - mn);
+  v3 pp = cpos - a.pos;
+  v3 pc = (cpos + n * cpen) - b.pos;
+  float c = safe_norm(dvr);
+  v3 n2 = dvr / (c + 1e-6f);
+  v3 cr1 = cross(pp, n2);
+  float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
+  float dlr;
+  if (R.oneway) {
+    dlr = c / (w1 + 1e-6f);
+  } else {
+    v3 cr2 = cross(pc, n2);
+    float w2 = 1.f / R.mb + dot(cr2, mul(R.Ib, cr2));
+    dlr = c / (w1 + w2 + 1e-6f);
+  }
+  float sm = cpen > 0.f ? 1.f : 0.f;
+  float sink = R.oneway ? (vno <= -R.thr ? 1.f : 0.f) : (vno <= 0.f ? 1.f : 0.f);
+  v3 pv = (dlr * n2 * sink + pdyn) * sm;
+  oav = pv / R.ma;
+  oaa = cross(mul(R.Ia, ra), pv);
+  if (R.oneway) {
+    obv = mk(0.f, 0.f, 0.f);
+    oba = mk(0.f, 0.f, 0.f);
+  } else {
+    obv = -pv / R.mb;
+    oba = cross(mul(R.Ib, rb), -pv);
+  }
+}
+
+// One/TwoWay._contact (colliders.py:267-304, 449-493): the impulse model used
+// by System.info at reset.
+__device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos, v3 cvel, v3 n,
+                                float cpen, v3& oav, v3& oaa, v3& obv, v3& oba) {
+  v3 rpa = cpos - a.pos, rpb = cpos - b.pos;
+  float bv = R.erp * cpen;
+  float nv = dot(n, cvel);
+  v3 x1 = cross(mul(R.Ia, cross(rpa, n)), rpa);
+  float denom;
+  if (R.oneway) {
+    denom = 1.f / R.ma + dot(n, x1);
+  } else {
+    v3 x2 = cross(mul(R.Ib, cross(rpb, n)), rpb);
+    denom = 1.f / R.ma + 1.f / R.mb + dot(n, x1 + x2);
+  }
+  float imp = (-1.f * (1.f + R.elas) * nv + bv) / denom;
+  v3 vd = cvel - nv * n;
+  float vdn = safe_norm(vd);
+  float impd = fminf(vdn / denom, R.fric * imp);
+  v3 dird = vd / (1e-6f + vdn);
+  float an = (cpen > 0.f && nv < 0.f && imp > 0.f) ? 1.f : 0.f;
+  float ad = an * (vdn > 0.01f ? 1.f : 0.f);
+  v3 J = imp * n, Jd = -impd * dird;
+  oav = (J / R.ma) * an + (Jd / R.ma) * ad;
+  oaa = mul(R.Ia, cross(rpa, J)) * an + mul(R.Ia, cross(rpa, Jd)) * ad;
+  if (R.oneway) {
+    obv = mk(0.f, 0.f, 0.f);
+    oba = mk(0.f, 0.f, 0.f);
+  } else {
+    v3 Jb = -imp * n, Jdb = impd * dird;
+    obv = (Jb / R.mb) * an + (Jdb / R.mb) * ad;
+    oba = mul(R.Ib, cross(rpb, Jb)) * an + mul(R.Ib, cross(rpb, Jdb)) * ad;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// per-env LDS carving
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
+  Env E;
+  E.qp = base + H.l_qp;
+  E.prev = base + H.l_prev;
+  E.rb = base + H.l_rb;
+  E.jslot = base + H.l_jslot;
+  E.aslot = base + H.l_aslot;
+  E.rowd = base + H.l_rowd;
+  E.cslot = base + H.l_cslot;
+  E.acc = base + H.l_acc;
+  E.ang = base + H.l_ang;
+  E.red = base + H.l_red;
+  return E;
+}
+
+__device__ __forceinline__ void sync() { __syncthreads(); }
+
+// global <-> LDS QP through strided field views
+__device__ __forceinline__ void load_qp_global(const bx_qp& q, int64_t e, int b, float* s) {
+  const float* p = q.pos.ptr + e * q.pos.env_stride + b * q.pos.body_stride;
+  const float* r = q.rot.ptr + e * q.rot.env_stride + b * q.rot.body_stride;
+  const float* v = q.vel.ptr + e * q.vel.env_stride + b * q.vel.body_stride;
+  const float* a = q.ang.ptr + e * q.ang.env_stride + b * q.ang.body_stride;
+  s[0] = p[0]; s[1] = p[1]; s[2] = p[2];
+  s[3] = r[0]; s[4] = r[1]; s[5] = r[2]; s[6] = r[3];
+  s[7] = v[0]; s[8] = v[1]; s[9] = v[2];
+  s[10] = a[0]; s[11] = a[1]; s[12] = a[2];
+}
+__device__ __forceinline__ void store_qp_global(const bx_qp& q, int64_t e, int b, const float* s) {
+  float* p = q.pos.ptr + e * q.pos.env_stride + b * q.pos.body_stride;
+  float* r = q.rot.ptr + e * q.rot.env_stride + b * q.rot.body_stride;
+  float* v = q.vel.ptr + e * q.vel.env_stride + b * q.vel.body_stride;
+  float* a = q.ang.ptr + e * q.ang.env_stride + b * q.ang.body_stride;
+  p[0] = s[0]; p[1] = s[1]; p[2] = s[2];
+  r[0] = s[3]; r[1] = s[4]; r[2] = s[5]; r[3] = s[6];
+  v[0] = s[7]; v[1] = s[8]; v[2] = s[9];
+  a[0] = s[10]; a[1] = s[11]; a[2] = s[12];
+}
+
+// ---------------------------------------------------------------------------
+// the PBD step of one env (system.py:254-325), all L lanes of the env
+// ---------------------------------------------------------------------------
+template <int L>
+__device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
+                         const float* act) {
+  const int N = H.N, J = H.J, K = H.K, Rn = H.R;
+  const float h = H.h;
+  for (int b = lane; b < N; b += L) {
+    float* acc = E.acc + b * ACC_STRIDE;
+    for (int k = 0; k < 9; k++) acc[k] = 0.f;
+  }
+  for (int it = 0; it < H.substeps / 2; it++) {
+    for (int sub = 0; sub < 2; sub++) {
+      // qprev = qp
+      for (int b = lane; b < N; b += L) {
+        const float* s = E.qp + b * QP_STRIDE;
+        float* d = E.prev + b * PREV_STRIDE;
+        for (int k = 0; k < 7; k++) d[k] = s[k];
+      }
+      // actuators (actuators.py:52-112) and joint damping (joints.py:103-128)
+      for (int a = lane; a < K; a += L) {
+        ActC A = load_act(c, H, a);
+        JointC Jc = load_joint(c, H, A.joint);
+        QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), q = ldqp(E.qp + Jc.bc * QP_STRIDE);
+        v3 axes[3];
+        float ang[3];
+        int dof = axis_angle(Jc, p, q, axes, ang);
+        v3 tq = mk(0.f, 0.f, 0.f);
+        for (int l = 0; l < dof; l++) {
+          int ai = A.idx[l];
+          float al = valid ? act[ai < 0 ? 0 : ai] * (ai >= 0 ? 1.f : 0.f) : 0.f;
+          float t;
+          if (A.type == 0) {
+            t = al * A.strength * -1.f;
+            if (ang[l] < Jc.lim[2 * l]) t = 0.f;
+            if (ang[l] > Jc.lim[2 * l + 1]) t = 0.f;
+          } else {
+            float tgt = clampf(al * 3.14159265358979323846f / 180.f, Jc.lim[2 * l], Jc.lim[2 * l + 1]);
+            t = (tgt - ang[l]) * A.strength;
+          }
+          tq = tq + axes[l] * t;
+        }
+        float sgp = A.type == 0 ? 1.f : -1.f;
+        st3(E.aslot + (2 * a) * 4, sgp * mul(Jc.Ip, tq));
+        st3(E.aslot + (2 * a + 1) * 4, -sgp * mul(Jc.Ic, tq));
+      }
+      for (int j = lane; j < J; j += L) {
+        int o = H.o_joint + j * JOINT_STRIDE;
+        int bp = c.i(o + J_BP), bc = c.i(o + J_BC);
+        float damp = c.f(o + J_DAMP);
+        v3 Ip = c.f3(H.o_body + bp * BODY_STRIDE + BODY_I);
+        v3 Ic = c.f3(H.o_body + bc * BODY_STRIDE + BODY_I);
+        v3 tq = -1.f * damp * (ld3(E.qp + bp * QP_STRIDE + 10) - ld3(E.qp + bc * QP_STRIDE + 10));
+        st3(E.jslot + (2 * j) * 8, mul(Ip, tq));
+        st3(E.jslot + (2 * j + 1) * 8, -1.f * mul(Ic, tq));
+      }
+      sync();
+      // Euler.update(acc) + Euler.kinetic (integrators.py:50-93)
+      for (int b = lane; b < N; b += L) {
+        BodyC B = load_body(c, H, b);
+        v3 dpa = mk(0.f, 0.f, 0.f), dpj = mk(0.f, 0.f, 0.f);
+        for (int i = c.i(H.o_al_off + b), e = c.i(H.o_al_off + b + 1); i < e; i++)
+          dpa = dpa + ld3(E.aslot + c.i(H.o_al + i) * 4);
+        for (int i = c.i(H.o_jl_off + b), e = c.i(H.o_jl_off + b + 1); i < e; i++)
+          dpj = dpj + ld3(E.jslot + c.i(H.o_jl + i) * 8);
+        QP q = ldqp(E.qp + b * QP_STRIDE);
+        v3 vel = H.vexp * q.vel;
+        vel = vel + (mk(0.f, 0.f, 0.f) + mk(H.gx, H.gy, H.gz)) * h;
+        vel = mul(vel, B.pm);
+        v3 ang = H.aexp * q.ang;
+        ang = ang + ((dpa + mk(0.f, 0.f, 0.f)) + dpj) * h;
+        ang = mul(ang, B.rm);
+        q.vel = vel;
+        q.ang = ang;
+        q.pos = q.pos + mul(q.vel * h, B.pm);
+        v3 am = mul(q.ang, B.rm);
+        q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
+        q4 r = q.rot + quat_mul(hq, q.rot);
+        float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
+        q.rot = q4{r.w / rn, r.x / rn, r.y / rn, r.z / rn};
+        stqp(E.qp + b * QP_STRIDE, q);
+        if (sub == 1) st3(E.acc + b * ACC_STRIDE + ACC_DPA, dpa);
+      }
+      sync();
+      // Joint.apply (joints.py:79-100)
+      for (int j = lane; j < J; j += L) {
+        JointC Jc = load_joint(c, H, j);
+        QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), q = ldqp(E.qp + Jc.bc * QP_STRIDE);
+        v3 dpp, dcp;
+        q4 dpr, dcr;
+        joint_apply(Jc, p, q, dpp, dpr, dcp, dcr);
+        float* sp = E.jslot + (2 * j) * 8;
+        float* sc = E.jslot + (2 * j + 1) * 8;
+        st3(sp, dpp); st4(sp + 3, dpr);
+        st3(sc, dcp); st4(sc + 3, dcr);
+      }
+      sync();
+      // Euler.update(pos) (+ velocity_projection on the first substep)
+      for (int b = lane; b < N; b += L) {
+        BodyC B = load_body(c, H, b);
+        v3 dp = mk(0.f, 0.f, 0.f);
+        q4 dr{0.f, 0.f, 0.f, 0.f};
+        for (int i = c.i(H.o_jl_off + b), e = c.i(H.o_jl_off + b + 1); i < e; i++) {
+          const float* s = E.jslot + c.i(H.o_jl + i) * 8;
+          dp = dp + ld3(s);
+          dr = dr + ld4(s + 3);
+        }
+        float* s = E.qp + b * QP_STRIDE;
+        QP q = ldqp(s);
+        q.pos = q.pos + mul(dp, B.pm);
+        q.rot = q4{q.rot.w + dr.w * B.qm.w, q.rot.x + dr.x * B.qm.x, q.rot.y + dr.y * B.qm.y,
+                   q.rot.z + dr.z * B.qm.z};
+        if (sub == 0) {
+          // Euler.velocity_projection (integrators.py:122-146)
+          const float* pv = E.prev + b * PREV_STRIDE;
+          v3 ppos = ld3(pv);
+          q4 prot = ld4(pv + 3);
+          float rn = sqrtf(q.rot.w * q.rot.w + q.rot.x * q.rot.x + q.rot.y * q.rot.y + q.rot.z * q.rot.z);
+          q4 nr{q.rot.w / rn, q.rot.x / rn, q.rot.y / rn, q.rot.z / rn};
+          q.vel = mul((q.pos - ppos) / h, B.pm);
+          q4 dq = quat_mul(nr, quat_inv(prot));
+          v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
+          float scl = dq.w >= 0.f ? 1.f : -1.f;
+          q.ang = mul(mul(scl * B.rm, a), B.rm);
+          q.rot = nr;
+        }
+        stqp(s, q);
+      }
+      sync();
+    }
+    // ---- collisions on the second substep (system.py:288-313)
+    // Collider.position_apply (colliders.py:198-240)
+    for (int r = lane; r < Rn; r += L) {
+      RowC R = load_row(c, H, r);
+      QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+      v3 cpos, cvel, n;
+      float pen;
+      contact_gen(R, a, b, cpos, cvel, n, pen);
+      const float* pa = E.prev + R.a * PREV_STRIDE;
+      const float* pb = E.prev + R.b * PREV_STRIDE;
+      v3 oap, obp;
+      q4 oar, obr;
+      float dl = position_contact(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, n, pen,
+                                  oap, oar, obp, obr);
+      float* rd = E.rowd + r * 8;
+      st3(rd, cpos); st3(rd + 3, n); rd[6] = pen; rd[7] = dl;
+      float* sa = E.cslot + (2 * r) * 8;
+      float* sb = E.cslot + (2 * r + 1) * 8;
+      st3(sa, oap); st4(sa + 3, oar);
+      sa[7] = (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f;
+      st3(sb, obp); st4(sb + 3, obr);
+      sb[7] = (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f;
+    }
+    sync();
+    for (int b = lane; b < N; b += L) {
+      BodyC B = load_body(c, H, b);
+      v3 dp = mk(0.f, 0.f, 0.f);
+      q4 dr{0.f, 0.f, 0.f, 0.f};
+      int i = c.i(H.o_cl_off + b), e = c.i(H.o_cl_off + b + 1);
+      while (i < e) {
+        int g = c.i(H.o_cl + i) >> 24;
+        v3 gp = mk(0.f, 0.f, 0.f);
+        q4 gr{0.f, 0.f, 0.f, 0.f};
+        float cnt = 0.f;
+        for (; i < e && (c.i(H.o_cl + i) >> 24) == g; i++) {
+          const float* s = E.cslot + (c.i(H.o_cl + i) & 0xFFFFFF) * 8;
+          gp = gp + ld3(s);
+          gr = gr + ld4(s + 3);
+          cnt += s[7];
+        }
+        float d = 1e-6f + cnt;
+        dp = dp + gp / d;
+        dr = dr + q4{gr.w / d, gr.x / d, gr.y / d, gr.z / d};
+      }
+      float* s = E.qp + b * QP_STRIDE;
+      QP q = ldqp(s);
+      q.pos = q.pos + mul(dp, B.pm);
+      q.rot = q4{q.rot.w + dr.w * B.qm.w, q.rot.x + dr.x * B.qm.x, q.rot.y + dr.y * B.qm.y,
+                 q.rot.z + dr.z * B.qm.z};
+      // qp_right_before, then velocity_projection
+      float* rb = E.rb + b * RB_STRIDE;
+      st3(rb, q.pos); st3(rb + 3, q.vel); st3(rb + 6, q.ang);
+      const float* pv = E.prev + b * PREV_STRIDE;
+      v3 ppos = ld3(pv);
+      q4 prot = ld4(pv + 3);
+      float rn = sqrtf(q.rot.w * q.rot.w + q.rot.x * q.rot.x + q.rot.y * q.rot.y + q.rot.z * q.rot.z);
+      q4 nr{q.rot.w / rn, q.rot.x / rn, q.rot.y / rn, q.rot.z / rn};
+      q.vel = mul((q.pos - ppos) / h, B.pm);
+      q4 dq = quat_mul(nr, quat_inv(prot));
+      v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
+      float scl = dq.w >= 0.f ? 1.f : -1.f;
+      q.ang = mul(mul(scl * B.rm, a), B.rm);
+      q.rot = nr;
+      stqp(s, q);
+    }
+    sync();
+    // Collider.velocity_apply (colliders.py:155-196)
+    for (int r = lane; r < Rn; r += L) {
+      RowC R = load_row(c, H, r);
+      QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+      const float* ra = E.rb + R.a * RB_STRIDE;
+      const float* rbb = E.rb + R.b * RB_STRIDE;
+      const float* rd = E.rowd + r * 8;
+      v3 oav, oaa, obv, oba;
+      velocity_contact(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
+                       ld3(rbb + 6), ld3(rd), ld3(rd + 3), rd[6], rd[7], oav, oaa, obv, oba);
+      float* sa = E.cslot + (2 * r) * 8;
+      float* sb = E.cslot + (2 * r + 1) * 8;
+      st3(sa, oav); st3(sa + 3, oaa);
+      sa[7] = (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f;
+      st3(sb, obv); st3(sb + 3, oba);
+      sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
+    }
+    sync();
+    for (int b = lane; b < N; b += L) {
+      BodyC B = load_body(c, H, b);
+      v3 dv = mk(0.f, 0.f, 0.f), da = mk(0.f, 0.f, 0.f);
+      int i = c.i(H.o_cl_off + b), e = c.i(H.o_cl_off + b + 1);
+      while (i < e) {
+        int g = c.i(H.o_cl + i) >> 24;
+        v3 gv = mk(0.f, 0.f, 0.f), ga = mk(0.f, 0.f, 0.f);
+        float cnt = 0.f;
+        for (; i < e && (c.i(H.o_cl + i) >> 24) == g; i++) {
+          const float* s = E.cslot + (c.i(H.o_cl + i) & 0xFFFFFF) * 8;
+          gv = gv + ld3(s);
+          ga = ga + ld3(s + 3);
+          cnt += s[7];
+        }
+        float d = 1e-6f + cnt;
+        dv = dv + gv / d;
+        da = da + ga / d;
+      }
+      float* s = E.qp + b * QP_STRIDE;
+      v3 vel = mul(ld3(s + 7) + dv, B.pm);
+      v3 ang = mul(ld3(s + 10) + da, B.rm);
+      st3(s + 7, vel);
+      st3(s + 10, ang);
+      float* acc = E.acc + b * ACC_STRIDE;
+      st3(acc + ACC_ICV, ld3(acc + ACC_ICV) + dv);
+      st3(acc + ACC_ICA, ld3(acc + ACC_ICA) + da);
+      st3(acc + ACC_IAA, ld3(acc + ACC_IAA) + ld3(acc + ACC_DPA));
+    }
+    sync();
+  }
+}
+
+// System._pbd_info contact part (system.py:327-340 -> Collider.apply): info
+// contact (vel, ang) per body into acc[ACC_ICV], acc[ACC_ICA]
+template <int L>
+__device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane) {
+  const int N = H.N, Rn = H.R;
+  for (int r = lane; r < Rn; r += L) {
+    RowC R = load_row(c, H, r);
+    QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+    v3 cpos, cvel, n;
+    float pen;
+    contact_gen(R, a, b, cpos, cvel, n, pen);
+    v3 oav, oaa, obv, oba;
+    impulse_contact(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
+    float* sa = E.cslot + (2 * r) * 8;
+    float* sb = E.cslot + (2 * r + 1) * 8;
+    st3(sa, oav); st3(sa + 3, oaa);
+    sa[7] = (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f;
+    st3(sb, obv); st3(sb + 3, oba);
+    sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
+  }
+  sync();
+  for (int b = lane; b < N; b += L) {
+    v3 dv = mk(0.f, 0.f, 0.f), da = mk(0.f, 0.f, 0.f);
+    int i = c.i(H.o_cl_off + b), e = c.i(H.o_cl_off + b + 1);
+    while (i < e) {
+      int g = c.i(H.o_cl + i) >> 24;
+      v3 gv = mk(0.f, 0.f, 0.f), ga = mk(0.f, 0.f, 0.f);
+      float cnt = 0.f;
+      for (; i < e && (c.i(H.o_cl + i) >> 24) == g; i++) {
+        const float* s = E.cslot + (c.i(H.o_cl + i) & 0xFFFFFF) * 8;
+        gv = gv + ld3(s);
+        ga = ga + ld3(s + 3);
+        cnt += s[7];
+      }
+      float d = 1e-8f + cnt;
+      dv = dv + gv / d;
+      da = da + ga / d;
+    }
+    float* acc = E.acc + b * ACC_STRIDE;
+    st3(acc + ACC_ICV, dv);
+    st3(acc + ACC_ICA, da);
+  }
+  sync();
+}
+
+// ---------------------------------------------------------------------------
+// env layer (ant.py:222-282, half_cheetah.py:178-214, humanoid.py:246-338)
+// ---------------------------------------------------------------------------
+
+// joint angles and velocities into E.ang (Joint.angle_vel, joints.py:197-226)
+template <int L>
+__device__ void joint_angles(const Cst& c, const BlobHdr& H, const Env& E, int lane) {
+  for (int j = lane; j < H.J; j += L) {
+    JointC Jc = load_joint(c, H, j);
+    QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), q = ldqp(E.qp + Jc.bc * QP_STRIDE);
+    v3 axes[3];
+    float ang[3];
+    axis_angle(Jc, p, q, axes, ang);
+    v3 dv = p.ang - q.ang;
+    for (int l = 0; l < Jc.n_angles; l++) {
+      E.ang[Jc.angle_off + l] = ang[l];
+      E.ang[H.D + Jc.angle_off + l] = dot(dv, axes[l]);
+    }
+  }
+}
+
+__device__ __forceinline__ float clip1(float x) { return clampf(x, -1.f, 1.f); }
+
+// Humanoid center of mass over bodies [:-1] (humanoid.py:336-338) -> red[32..35]
+__device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3& com, float& msum) {
+  v3 acc = mk(0.f, 0.f, 0.f);
+  float m = 0.f;
+  for (int b = 0; b < H.N - 1; b++) {
+    float mb = c.f(H.o_body + b * BODY_STRIDE + BODY_MASS);
+    acc = acc + mb * ld3(qp + b * QP_STRIDE);
+    m += mb;
+  }
+  com = acc / m;
+  msum = m;
+}
+
+// observation element i of the env kind
+__device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind, int i,
+                          const float* act, bool valid) {
+  const int N = H.N, D = H.D;
+  const float* q0 = E.qp;
+  if (kind == BX_ENV_ANT) {
+    if (i == 0) return q0[2];
+    i -= 1;
+    if (i < 4) return q0[3 + i];
+    i -= 4;
+    if (i < D) return E.ang[i];
+    i -= D;
+    if (i < 3) return q0[7 + i];
+    i -= 3;
+    if (i < 3) return q0[10 + i];
+    i -= 3;
+    if (i < D) return E.ang[D + i];
+    i -= D;
+    if (i < 3 * N) return clip1(E.acc[(i / 3) * ACC_STRIDE + ACC_ICV + i % 3]);
+    i -= 3 * N;
+    return clip1(E.acc[(i / 3) * ACC_STRIDE + ACC_ICA + i % 3]);
+  }
+  if (kind == BX_ENV_HALFCHEETAH) {
+    if (i == 0) return q0[2];
+    if (i == 1) return q0[3];
+    if (i == 2) return q0[5];
+    i -= 3;
+    if (i < D) return E.ang[i];
+    i -= D;
+    if (i == 0) return q0[7];
+    if (i == 1) return q0[9];
+    if (i == 2) return q0[11];
+    i -= 3;
+    return E.ang[D + i];
+  }
+  // humanoid
+  if (i == 0) return q0[2];
+  i -= 1;
+  if (i < 4) return q0[3 + i];
+  i -= 4;
+  if (i < D) return E.ang[i];
+  i -= D;
+  if (i < 3) return q0[7 + i];
+  i -= 3;
+  if (i < 3) return q0[10 + i];
+  i -= 3;
+  if (i < D) return E.ang[D + i];
+  i -= D;
+  v3 com = ld3(E.red + 32);
+  float msum = E.red[35];
+  int M = N - 1;
+  if (i < 9 * M) {
+    int b = i / 9, rc = i % 9, r = rc / 3, cc = rc % 3;
+    float mb = c.f(H.o_body + b * BODY_STRIDE + BODY_MASS);
+    v3 d = ld3(E.qp + b * QP_STRIDE) - com;
+    float nn = norm(d);
+    float v = mb * (float)(r == cc) * (nn * nn);
+    float dr = r == 0 ? d.x : (r == 1 ? d.y : d.z);
+    float dc = cc == 0 ? d.x : (cc == 1 ? d.y : d.z);
+    float Ir = c.f(H.o_body + b * BODY_STRIDE + BODY_I + r);
+    v += (r == cc ? Ir : 0.f) - dr * dc;
+    return v;
+  }
+  i -= 9 * M;
+  if (i < 3 * M) {
+    int b = i / 3, k = i % 3;
+    float mb = c.f(H.o_body + b * BODY_STRIDE + BODY_MASS);
+    return mb * E.qp[b * QP_STRIDE + 7 + k] / msum;
+  }
+  i -= 3 * M;
+  if (i < 3 * M) {
+    int b = i / 3, k = i % 3;
+    v3 d = ld3(E.qp + b * QP_STRIDE) - com;
+    v3 cr = cross(d, ld3(E.qp + b * QP_STRIDE + 7));
+    float nn = norm(d);
+    float v = k == 0 ? cr.x : (k == 1 ? cr.y : cr.z);
+    return v / (1e-7f + nn * nn);
+  }
+  i -= 3 * M;
+  // qfrc_actuator: unmasked take (index -1 clips to 0), times strength
+  for (int a = 0; a < H.K; a++) {
+    ActC A = load_act(c, H, a);
+    int dof = c.i(H.o_joint + A.joint * JOINT_STRIDE + J_DOF);
+    if (i < dof) {
+      int ai = A.idx[i] < 0 ? 0 : A.idx[i];
+      return (valid ? act[ai] : 0.f) * A.strength;
+    }
+    i -= dof;
+  }
+  return 0.f;
+}
+
+template <int L>
+__device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int lane, int kind,
+                            int obs_size, const float* act, bool valid, float* obs_out) {
+  joint_angles<L>(c, H, E, lane);
+  if (kind == BX_ENV_HUMANOID && lane == 0) {
+    v3 com;
+    float msum;
+    humanoid_com(c, H, E.qp, com, msum);
+    st3(E.red + 32, com);
+    E.red[35] = msum;
+  }
+  sync();
+  if (valid)
+    for (int i = lane; i < obs_size; i += L) obs_out[i] = obs_elem(c, H, E, kind, i, act, valid);
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+
+
+
+template <int L>
+__global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
+  extern __shared__ float smem[];
+  Cst c{A.blob};
+  BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
+  const int lane = threadIdx.x % L;
+  const int le = threadIdx.x / L;
+  const int64_t e = (int64_t)blockIdx.x * (64 / L) + le;
+  const bool valid = e < A.n_envs;
+  Env E = carve(smem + le * H.env_words, H);
+  for (int b = lane; b < H.N; b += L) {
+    if (valid) {
+      load_qp_global(A.qin, e, b, E.qp + b * QP_STRIDE);
+    } else {
+      float* s = E.qp + b * QP_STRIDE;
+      for (int k = 0; k < 13; k++) s[k] = k == 3 ? 1.f : 0.f;
+    }
+  }
+  sync();
+  pbd_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr);
+  if (!valid) return;
+  for (int b = lane; b < H.N; b += L) {
+    store_qp_global(A.qout, e, b, E.qp + b * QP_STRIDE);
+    const float* acc = E.acc + b * ACC_STRIDE;
+    const bx_info& I = A.info;
+    if (I.contact_vel.ptr) {
+      float* p = I.contact_vel.ptr + e * I.contact_vel.env_stride + b * I.contact_vel.body_stride;
+      p[0] = acc[ACC_ICV]; p[1] = acc[ACC_ICV + 1]; p[2] = acc[ACC_ICV + 2];
+    }
+    if (I.contact_ang.ptr) {
+      float* p = I.contact_ang.ptr + e * I.contact_ang.env_stride + b * I.contact_ang.body_stride;
+      p[0] = acc[ACC_ICA]; p[1] = acc[ACC_ICA + 1]; p[2] = acc[ACC_ICA + 2];
+    }
+    if (I.actuator_vel.ptr) {
+      float* p = I.actuator_vel.ptr + e * I.actuator_vel.env_stride + b * I.actuator_vel.body_stride;
+      p[0] = 0.f; p[1] = 0.f; p[2] = 0.f;
+    }
+    if (I.actuator_ang.ptr) {
+      float* p = I.actuator_ang.ptr + e * I.actuator_ang.env_stride + b * I.actuator_ang.body_stride;
+      p[0] = acc[ACC_IAA]; p[1] = acc[ACC_IAA + 1]; p[2] = acc[ACC_IAA + 2];
+    }
+  }
+  for (int r = lane; r < H.R; r += L) {
+    const float* rd = E.rowd + r * 8;
+    if (A.info.contact_pos) st3(A.info.contact_pos + (e * H.R + r) * 3, ld3(rd));
+    if (A.info.contact_normal) st3(A.info.contact_normal + (e * H.R + r) * 3, ld3(rd + 3));
+    if (A.info.contact_penetration) A.info.contact_penetration[e * H.R + r] = rd[6];
+  }
+}
+
+
+
+// Env.step fused with EpisodeWrapper/AutoResetWrapper (wrappers.py:105-148)
+template <int L>
+__global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
+  extern __shared__ float smem[];
+  Cst c{A.blob};
+  BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
+  const int lane = threadIdx.x % L;
+  const int le = threadIdx.x / L;
+  const int64_t e = (int64_t)blockIdx.x * (64 / L) + le;
+  const bool valid = e < A.n_envs;
+  Env E = carve(smem + le * H.env_words, H);
+  const bx_env_params& P = A.P;
+  const int kind = P.kind;
+  const float* act = valid ? A.act + e * A.act_stride : nullptr;
+  for (int b = lane; b < H.N; b += L) {
+    if (valid) {
+      load_qp_global(A.in.qp, e, b, E.qp + b * QP_STRIDE);
+    } else {
+      float* s = E.qp + b * QP_STRIDE;
+      for (int k = 0; k < 13; k++) s[k] = k == 3 ? 1.f : 0.f;
+    }
+  }
+  sync();
+  // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
+  float done_in = valid ? A.in.done[e] : 0.f;
+  float steps = 0.f;
+  if (valid && A.in.steps) steps = (P.auto_reset && done_in != 0.f) ? 0.f : A.in.steps[e];
+  float done = P.auto_reset ? 0.f : done_in;
+  float reward_sum = 0.f;
+  const int reps = P.episode_length > 0 ? (P.action_repeat > 0 ? P.action_repeat : 1) : 1;
+  // action sum of squares (ctrl cost), shared by every repeat
+  float sq = 0.f;
+  if (valid && lane == 0)
+    for (int i = 0; i < H.A; i++) sq += act[i] * act[i];
+  for (int rep = 0; rep < reps; rep++) {
+    v3 pos0 = ld3(E.qp);  // torso position before the step
+    v3 com0 = mk(0.f, 0.f, 0.f);
+    float msum = 0.f;
+    if (kind == BX_ENV_HUMANOID) humanoid_com(c, H, E.qp, com0, msum);
+    sync();
+    pbd_step<L>(c, H, E, lane, valid, act);
+    env_observe<L>(c, H, E, lane, kind, P.obs_size, act, valid, valid ? A.out.obs + e * P.obs_size : nullptr);
+    // reward / done / metrics (lane 0 of the env)
+    if (lane == 0 && valid) {
+      const float dt = H.dt;
+      float* m = A.out.metrics ? A.out.metrics + e * P.n_metrics : nullptr;
+      v3 p1 = ld3(E.qp);
+      float reward = 0.f;
+      if (kind == BX_ENV_ANT) {
+        v3 vel = (p1 - pos0) / dt;
+        float fwd = vel.x;
+        float z = p1.z;
+        float healthy = z < P.coef[4] ? 0.f : 1.f;
+        healthy = z > P.coef[5] ? 0.f : healthy;
+        bool term = P.coef[6] != 0.f;
+        float hr = term ? P.coef[3] : P.coef[3] * healthy;
+        float ctrl = P.coef[1] * sq;
+        float cs = 0.f;
+        for (int b = 0; b < H.N; b++)
+          for (int k = 0; k < 3; k++) {
+            float cv = clip1(E.acc[b * ACC_STRIDE + ACC_ICV + k]);
+            cs += cv * cv;
+          }
+        float ccost = P.coef[2] * cs;
+        reward = fwd + hr - ctrl - ccost;
+        done = term ? 1.f - healthy : 0.f;
+        if (m) {
+          m[0] = norm(p1); m[1] = fwd; m[2] = -ccost; m[3] = -ctrl; m[4] = fwd;
+          m[5] = hr; m[6] = p1.x; m[7] = vel.x; m[8] = p1.y; m[9] = vel.y;
+        }
+      } else if (kind == BX_ENV_HALFCHEETAH) {
+        float v0 = (p1.x - pos0.x) / dt;
+        float fwd = P.coef[0] * v0;
+        float ctrl = P.coef[1] * sq;
+        reward = fwd - ctrl;
+        if (m) { m[0] = -ctrl; m[1] = fwd; m[2] = p1.x; m[3] = v0; }
+      } else if (kind == BX_ENV_HUMANOID) {
+        v3 com1 = ld3(E.red + 32);
+        v3 v = (com1 - com0) / dt;
+        float fwd = P.coef[0] * v.x;
+        float z = p1.z;
+        float healthy = z < P.coef[4] ? 0.f : 1.f;
+        healthy = z > P.coef[5] ? 0.f : healthy;
+        bool term = P.coef[6] != 0.f;
+        float hr = term ? P.coef[3] : P.coef[3] * healthy;
+        float ctrl = P.coef[1] * sq;
+        reward = fwd + hr - ctrl;
+        done = term ? 1.f - healthy : 0.f;
+        if (m) {
+          m[0] = norm(com1); m[1] = fwd; m[2] = hr; m[3] = fwd; m[4] = -ctrl;
+          m[5] = com1.x; m[6] = v.x; m[7] = com1.y; m[8] = v.y;
+        }
+      }
+      reward_sum = rep == 0 ? reward : reward_sum + reward;
+      E.red[0] = done;
+    }
+    sync();
+  }
+  if (!valid) return;
+  done = E.red[0];
+  float trunc = 0.f;
+  bool reset_now = false;
+  if (P.episode_length > 0) {
+    steps = steps + (float)reps;
+    float ep = (float)P.episode_length;
+    float d_inner = done;
+    done = steps >= ep ? 1.f : d_inner;
+    trunc = steps >= ep ? 1.f - d_inner : 0.f;
+  }
+  if (P.auto_reset) reset_now = done != 0.f;
+  if (lane == 0) {
+    A.out.reward[e] = reward_sum;
+    A.out.done[e] = done;
+    if (A.out.steps) A.out.steps[e] = steps;
+    if (A.out.truncation) A.out.truncation[e] = trunc;
+  }
+  if (reset_now) {
+    for (int b = lane; b < H.N; b += L) {
+      float tmp[13];
+      load_qp_global(P.first_qp, e, b, tmp);
+      store_qp_global(A.out.qp, e, b, tmp);
+    }
+    for (int i = lane; i < P.obs_size; i += L) A.out.obs[e * P.obs_size + i] = P.first_obs[e * P.obs_size + i];
+  } else {
+    for (int b = lane; b < H.N; b += L) store_qp_global(A.out.qp, e, b, E.qp + b * QP_STRIDE);
+  }
+}
+
+
+
+// System.info contact part + optional Env._get_obs of the same state (reset)
+template <int L>
+__global__ void __launch_bounds__(64) info_obs_kernel(InfoArgs A) {
+  extern __shared__ float smem[];
+  Cst c{A.blob};
+  BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
+  const int lane = threadIdx.x % L;
+  const int le = threadIdx.x / L;
+  const int64_t e = (int64_t)blockIdx.x * (64 / L) + le;
+  const bool valid = e < A.n_envs;
+  Env E = carve(smem + le * H.env_words, H);
+  if (valid) {
+    for (int b = lane; b < H.N; b += L) load_qp_global(A.q, e, b, E.qp + b * QP_STRIDE);
+  } else {
+    for (int b = lane; b < H.N; b += L) {
+      float* s = E.qp + b * QP_STRIDE;
+      for (int k = 0; k < 13; k++) s[k] = k == 3 ? 1.f : 0.f;
+    }
+  }
+  sync();
+  pbd_info<L>(c, H, E, lane);
+  if (valid) {
+    for (int b = lane; b < H.N; b += L) {
+      const float* acc = E.acc + b * ACC_STRIDE;
+      const bx_info& I = A.info;
+      if (I.contact_vel.ptr) {
+        float* p = I.contact_vel.ptr + e * I.contact_vel.env_stride + b * I.contact_vel.body_stride;
+        p[0] = acc[ACC_ICV]; p[1] = acc[ACC_ICV + 1]; p[2] = acc[ACC_ICV + 2];
+      }
+      if (I.contact_ang.ptr) {
+        float* p = I.contact_ang.ptr + e * I.contact_ang.env_stride + b * I.contact_ang.body_stride;
+        p[0] = acc[ACC_ICA]; p[1] = acc[ACC_ICA + 1]; p[2] = acc[ACC_ICA + 2];
+      }
+    }
+  }
+  if (A.obs) {
+    const float* act = valid && A.act ? A.act + e * A.act_stride : nullptr;
+    env_observe<L>(c, H, E, lane, A.kind, A.obs_size, act, valid && act != nullptr,
+                   valid ? A.obs + e * A.obs_size : nullptr);
+  }
+}
+
+// System.default_qp (system.py:112-242): one thread per env (reset path)
+
+
+__global__ void __launch_bounds__(64) default_qp_kernel(ResetArgs A) {
+  extern __shared__ float smem[];
+  Cst c{A.blob};
+  BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
+  const int64_t e = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (e >= A.n_envs) return;
+  float* q = smem + threadIdx.x * H.N * 13;  // per-thread scratch: N x 13
+  const int N = H.N, D = H.num_joint_dof;
+  for (int b = 0; b < N; b++)
+    for (int k = 0; k < 13; k++) q[b * 13 + k] = c.f(H.o_base + b * 13 + k);
+  const float* ja = A.angle + e * D;
+  const float* jv = A.vel + e * D;
+  for (int f = 0; f < H.n_fk; f++) {
+    int o = H.o_fk + f * FK_STRIDE;
+    float a3[3], v3_[3];
+    for (int l = 0; l < 3; l++) {
+      int ix = c.i(o + FK_IDX + l);
+      a3[l] = ix >= 0 ? ja[ix] : 0.f;
+      v3_[l] = ix >= 0 ? jv[ix] : 0.f;
+    }
+    q4 jr{c.f(o + FK_ROT), c.f(o + FK_ROT + 1), c.f(o + FK_ROT + 2), c.f(o + FK_ROT + 3)};
+    q4 rot{c.f(o + FK_REF), c.f(o + FK_REF + 1), c.f(o + FK_REF + 2), c.f(o + FK_REF + 3)};
+    v3 axes[3] = {rotate(mk(1.f, 0.f, 0.f), jr), rotate(mk(0.f, 1.f, 0.f), jr),
+                  rotate(mk(0.f, 0.f, 1.f), jr)};
+    v3 lang = axes[0] * v3_[0] + axes[1] * v3_[1] + axes[2] * v3_[2];
+    for (int l = 0; l < 3; l++) {
+      v3 ax = rotate(axes[l], rot);
+      rot = quat_mul(quat_rot_axis(ax, a3[l]), rot);
+    }
+    int bp = c.i(o + FK_BP), bc = c.i(o + FK_BC);
+    float* sp = q + bp * 13;
+    float* sc = q + bc * 13;
+    q4 prot = ld4(sp + 3);
+    q4 wr = quat_mul(prot, rot);
+    v3 lp = c.f3(o + FK_OFFP) - rotate(c.f3(o + FK_OFFC), rot);
+    v3 wp = ld3(sp) + rotate(lp, prot);
+    v3 wa = rotate(lang, prot);
+    st3(sc, wp);
+    st4(sc + 3, wr);
+    st3(sc + 10, wa);
+  }
+  // bodies.min_z per root group, then lift (system.py:213-240)
+  for (int g = 0; g < H.n_root_groups; g++) {
+    float zmin = __builtin_inff();
+    for (int b = 0; b < N; b++) {
+      if (c.i(H.o_rgroup + b) != g) continue;
+      float bz = __builtin_inff();
+      for (int p = c.i(H.o_zoff + b), pe = c.i(H.o_zoff + b + 1); p < pe; p++) {
+        int o = H.o_zpt + p * 4;
+        v3 w = rotate(c.f3(o), ld4(q + b * 13 + 3));
+        float z = q[b * 13 + 2] + w.z - c.f(o + 3);
+        bz = fminf(bz, z);
+      }
+      if (c.i(H.o_zero + b)) bz = fminf(bz, 0.f);
+      zmin = fminf(zmin, bz);
+    }
+    for (int b = 0; b < N; b++) {
+      if (c.i(H.o_rgroup + b) != g) continue;
+      q[b * 13 + 0] = q[b * 13 + 0] - zmin * 0.f;
+      q[b * 13 + 1] = q[b * 13 + 1] - zmin * 0.f;
+      q[b * 13 + 2] = q[b * 13 + 2] - zmin * 1.f;
+    }
+  }
+  for (int b = 0; b < N; b++) store_qp_global(A.out, e, b, q + b * 13);
+}
+
+// counter-based uniform fill: splitmix64 of (seed, index) -> [lo, hi)
+__global__ void uniform_kernel(float* out, int64_t n, uint64_t seed, uint64_t offset, float lo,
+                               float hi) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + (uint64_t)(i + offset) + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  float u = (float)(z >> 40) * (1.0f / 16777216.0f);
+  out[i] = lo + (hi - lo) * u;
+}
+
+}  // namespace bx
+
+// ---------------------------------------------------------------------------
+// launch helpers (host)
+// ---------------------------------------------------------------------------
+namespace bx {
+
+hipError_t launch_system_step(int L, int64_t n_envs, size_t lds, hipStream_t s, const StepArgs& a) {
+  int epb = 64 / L;
+  dim3 grid((unsigned)((n_envs + epb - 1) / epb));
+  if (L == 16) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(system_step_kernel<16>, grid, dim3(64), lds, s, a); }
+  else if (L == 32) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(system_step_kernel<32>, grid, dim3(64), lds, s, a); }
+  else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(system_step_kernel<64>, grid, dim3(64), lds, s, a); }
+  return hipGetLastError();
+}
+hipError_t launch_env_step(int L, int64_t n_envs, size_t lds, hipStream_t s, const EnvArgs& a) {
+  int epb = 64 / L;
+  dim3 grid((unsigned)((n_envs + epb - 1) / epb));
+  if (L == 16) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(env_step_kernel<16>, grid, dim3(64), lds, s, a); }
+  else if (L == 32) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(env_step_kernel<32>, grid, dim3(64), lds, s, a); }
+  else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(env_step_kernel<64>, grid, dim3(64), lds, s, a); }
+  return hipGetLastError();
+}
+hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a) {
+  int epb = 64 / L;
+  dim3 grid((unsigned)((n_envs + epb - 1) / epb));
+  if (L == 16) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<16>, grid, dim3(64), lds, s, a); }
+  else if (L == 32) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<32>, grid, dim3(64), lds, s, a); }
+  else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<64>, grid, dim3(64), lds, s, a); }
+  return hipGetLastError();
+}
+hipError_t launch_default_qp(int64_t n_envs, size_t lds, hipStream_t s, const ResetArgs& a) {
+  dim3 grid((unsigned)((n_envs + 63) / 64));
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)default_qp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(default_qp_kernel, grid, dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset, float lo, float hi,
+                          hipStream_t s) {
+  dim3 grid((unsigned)((n + 255) / 256));
+  hipLaunchKernelGGL(uniform_kernel, grid, dim3(256), 0, s, out, n, seed, offset, lo, hi);
+  return hipGetLastError();
+}
+
+}  // namespace bx

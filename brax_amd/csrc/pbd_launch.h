@@ -1,0 +1,51 @@
+// pbd_launch.h — host-side launch entry points of pbd_kernels.hip
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/brax_amd.h"
+
+namespace bx {
+
+struct StepArgs {
+  const uint32_t* blob;
+  int64_t n_envs;
+  bx_qp qin, qout;
+  const float* act;
+  int64_t act_stride;
+  bx_info info;
+};
+struct EnvArgs {
+  const uint32_t* blob;
+  int64_t n_envs;
+  bx_env_params P;
+  bx_env_state in, out;
+  const float* act;
+  int64_t act_stride;
+};
+struct InfoArgs {
+  const uint32_t* blob;
+  int64_t n_envs;
+  bx_qp q;
+  bx_info info;
+  int kind, obs_size;
+  const float* act;
+  int64_t act_stride;
+  float* obs;
+};
+struct ResetArgs {
+  const uint32_t* blob;
+  int64_t n_envs;
+  const float* angle;
+  const float* vel;
+  bx_qp out;
+};
+
+hipError_t launch_system_step(int L, int64_t n_envs, size_t lds, hipStream_t s, const StepArgs& a);
+hipError_t launch_env_step(int L, int64_t n_envs, size_t lds, hipStream_t s, const EnvArgs& a);
+hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a);
+hipError_t launch_default_qp(int64_t n_envs, size_t lds, hipStream_t s, const ResetArgs& a);
+hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset, float lo, float hi,
+                          hipStream_t s);
+
+}  // namespace bx

@@ -1,0 +1,55 @@
+// pbd_layout.h — device constant-blob and per-env LDS layout (host + device).
+//
+// The blob is one read-only array of 32-bit words in HBM (floats bit-cast):
+// a BlobHdr followed by fixed-stride records for bodies, joints, actuators,
+// contact rows, the per-body gather lists that replace the reference's
+// `segment_sum`s, and the reset (forward-kinematics) tables.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/brax_amd.h"
+
+namespace bx {
+
+// record strides (words) and field offsets
+enum {
+  BODY_STRIDE = 16,
+  BODY_MASS = 0, BODY_I = 2, BODY_PM = 5, BODY_RM = 8, BODY_QM = 11,
+};
+enum {
+  JOINT_STRIDE = 48,
+  J_TYPE = 0, J_BP = 1, J_BC = 2, J_FREE = 3, J_DOF = 4, J_ANGLE_OFF = 5, J_NANGLES = 6,
+  J_DAMP = 7, J_SP = 8, J_SA = 9, J_OFFP = 10, J_OFFC = 13, J_AXP = 16, J_AXC = 25, J_LIM = 34,
+};
+enum { ACT_STRIDE = 8, A_TYPE = 0, A_JOINT = 1, A_IDX = 2, A_STR = 5 };
+enum {
+  ROW_STRIDE = 32,
+  R_GROUP = 0, R_A = 1, R_B = 2, R_FN = 3, R_ONEWAY = 4, R_APOS = 5, R_AEND = 8, R_ARAD = 11,
+  R_BPOS = 12, R_BEND = 15, R_BRAD = 18, R_FRIC = 19, R_ELAS = 20, R_SCALE = 21, R_THR = 22,
+  R_ERP = 23,
+};
+enum {
+  FK_STRIDE = 24,
+  FK_BP = 0, FK_BC = 1, FK_IDX = 2, FK_ROT = 5, FK_REF = 9, FK_OFFP = 13, FK_OFFC = 16,
+};
+// per-env LDS record strides (floats)
+enum { QP_STRIDE = 16, PREV_STRIDE = 8, RB_STRIDE = 12, ACC_STRIDE = 12 };
+enum { ACC_ICV = 0, ACC_ICA = 3, ACC_IAA = 6, ACC_DPA = 9 };
+
+struct BlobHdr {
+  int32_t N, J, K, R, G, A, substeps, D;
+  int32_t num_joint_dof, n_fk, n_root_groups, L;
+  float h, vexp, aexp, dt;
+  float gx, gy, gz, pad0;
+  // word offsets into the blob
+  int32_t o_body, o_joint, o_act, o_row;
+  int32_t o_jl_off, o_jl, o_al_off, o_al, o_cl_off, o_cl;
+  int32_t o_base, o_fk, o_zoff, o_zpt, o_zero, o_rgroup;
+  int32_t total_words;
+  // per-env LDS layout (float offsets) and size
+  int32_t l_qp, l_prev, l_rb, l_jslot, l_aslot, l_rowd, l_cslot, l_acc, l_ang, l_red;
+  int32_t env_words;
+  int32_t pad1[3];
+};
+
+}  // namespace bx

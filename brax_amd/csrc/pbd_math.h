@@ -1,0 +1,81 @@
+// pbd_math.h — fp32 vector/quaternion primitives for the gfx950 kernels.
+//
+// Same formulas (and operand order) as the reference's `brax/math.py:25-204`
+// and the jumpy helpers it uses (`brax/jumpy.py:170-192`), evaluated in fp32
+// the way `jax.jit` evaluates them with x64 disabled.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace bx {
+
+struct v3 {
+  float x, y, z;
+};
+struct q4 {
+  float w, x, y, z;
+};
+
+__device__ __forceinline__ v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+__device__ __forceinline__ v3 operator+(v3 a, v3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ v3 operator-(v3 a, v3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ v3 operator-(v3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ v3 operator*(v3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ v3 operator*(float s, v3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ v3 operator/(v3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ v3 mul(v3 a, v3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ v3 cross(v3 a, v3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ float norm(v3 a) { return sqrtf(dot(a, a)); }
+
+// jnp safe_norm: 0 when every |x_i| <= 1e-8 (allclose(x, 0), jumpy.py:183-189)
+__device__ __forceinline__ float safe_norm(v3 a) {
+  bool z = fabsf(a.x) <= 1e-8f && fabsf(a.y) <= 1e-8f && fabsf(a.z) <= 1e-8f;
+  return z ? 0.f : norm(a);
+}
+
+__device__ __forceinline__ q4 operator+(q4 a, q4 b) {
+  return {a.w + b.w, a.x + b.x, a.y + b.y, a.z + b.z};
+}
+__device__ __forceinline__ q4 operator*(q4 a, float s) { return {a.w * s, a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ q4 operator*(float s, q4 a) { return {s * a.w, s * a.x, s * a.y, s * a.z}; }
+
+// math.py:25-40
+__device__ __forceinline__ v3 rotate(v3 v, q4 q) {
+  v3 u{q.x, q.y, q.z};
+  float s = q.w;
+  v3 r = 2.f * (dot(u, v) * u) + (s * s - dot(u, u)) * v;
+  return r + 2.f * s * cross(u, v);
+}
+// math.py:130-145
+__device__ __forceinline__ q4 quat_mul(q4 u, q4 v) {
+  return {u.w * v.w - u.x * v.x - u.y * v.y - u.z * v.z,
+          u.w * v.x + u.x * v.w + u.y * v.z - u.z * v.y,
+          u.w * v.y - u.x * v.z + u.y * v.w + u.z * v.x,
+          u.w * v.z + u.x * v.y - u.y * v.x + u.z * v.w};
+}
+// math.py:148-170
+__device__ __forceinline__ q4 vec_quat_mul(v3 u, q4 v) {
+  return {-u.x * v.x - u.y * v.y - u.z * v.z,
+          u.x * v.w + u.y * v.z - u.z * v.y,
+          -u.x * v.z + u.y * v.w + u.z * v.x,
+          u.x * v.y - u.y * v.x + u.z * v.w};
+}
+// math.py:173-187
+__device__ __forceinline__ q4 quat_rot_axis(v3 axis, float angle) {
+  float s, c;
+  sincosf(angle * 0.5f, &s, &c);
+  return {c, axis.x * s, axis.y * s, axis.z * s};
+}
+__device__ __forceinline__ q4 quat_inv(q4 q) { return {q.w, -q.x, -q.y, -q.z}; }
+// math.py:116-127
+__device__ __forceinline__ float signed_angle(v3 axis, v3 ref_p, v3 ref_c) {
+  return atan2f(dot(cross(ref_p, ref_c), axis), dot(ref_p, ref_c));
+}
+__device__ __forceinline__ float clampf(float x, float lo, float hi) {
+  return x < lo ? lo : (x > hi ? hi : x);
+}
+__device__ __forceinline__ float signf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
+
+}  // namespace bx

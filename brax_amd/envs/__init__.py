@@ -1,0 +1,48 @@
+"""Environment registry (`brax/envs/__init__.py:45-130`).
+
+    env = brax_amd.envs.create('ant', batch_size=4096)   # Episode/AutoReset fused
+    state = env.reset(rng)                                # batched State on HBM
+    state = env.step(state, action)                       # one kernel launch
+"""
+import functools
+from typing import Callable, Optional
+
+from brax_amd.envs import wrappers
+from brax_amd.envs.ant import Ant
+from brax_amd.envs.env import Env, PhysicsEnv, State, Wrapper
+from brax_amd.envs.half_cheetah import Halfcheetah
+from brax_amd.envs.humanoid import Humanoid
+
+_envs = {
+    'ant': functools.partial(Ant, use_contact_forces=True),
+    'halfcheetah': Halfcheetah,
+    'humanoid': Humanoid,
+}
+
+
+def get_environment(env_name, **kwargs) -> Env:
+  return _envs[env_name](**kwargs)
+
+
+def register_environment(env_name: str, env_class):
+  _envs[env_name] = env_class
+
+
+def create(env_name: str, episode_length: int = 1000, action_repeat: int = 1,
+           auto_reset: bool = True, batch_size: Optional[int] = None,
+           eval_metrics: bool = False, **kwargs) -> Env:
+  """Creates an Env (`envs/__init__.py:74-92`); same wrapper order."""
+  env = _envs[env_name](**kwargs)
+  if episode_length is not None:
+    env = wrappers.EpisodeWrapper(env, episode_length, action_repeat)
+  if batch_size:
+    env = wrappers.VectorWrapper(env, batch_size)
+  if auto_reset:
+    env = wrappers.AutoResetWrapper(env)
+  if eval_metrics:
+    raise NotImplementedError('EvalWrapper is not implemented yet')
+  return env
+
+
+def create_fn(env_name: str, **kwargs) -> Callable[..., Env]:
+  return functools.partial(create, env_name, **kwargs)

@@ -1,0 +1,244 @@
+"""`brax.envs.Env` / `State` / `Wrapper` (`brax/envs/env.py:28-102`) on MI355X.
+
+A `PhysicsEnv` (Ant, Humanoid, HalfCheetah) steps through ONE fused kernel
+launch (`bx_env_step`): System.step + observation + reward/done/metrics, plus
+the EpisodeWrapper counters and the AutoResetWrapper select when those
+wrappers sit directly above it (`wrappers.py` folds them into the launch).
+States are batched: every leaf has a leading env axis (B, ...).
+"""
+import abc
+import ctypes as C
+import dataclasses
+from typing import Any, Dict
+
+import numpy as np
+import torch
+
+from brax_amd import _native
+from brax_amd import abi
+from brax_amd.base import QP, packed_view
+from brax_amd.system import System, _stream, qp_struct
+
+
+@dataclasses.dataclass(frozen=True)
+class State:
+  """Environment state (`env.py:28-36`)."""
+  qp: QP
+  obs: Any
+  reward: Any
+  done: Any
+  metrics: Dict[str, Any] = dataclasses.field(default_factory=dict)
+  info: Dict[str, Any] = dataclasses.field(default_factory=dict)
+
+  def replace(self, **kw):
+    return dataclasses.replace(self, **kw)
+
+
+def key_to_seed(rng):
+  """A jax-style PRNG key (2,) uint32, or an int, -> 64-bit seed."""
+  if isinstance(rng, (int, np.integer)):
+    return int(rng) & 0xFFFFFFFFFFFFFFFF
+  a = np.asarray(rng.cpu() if isinstance(rng, torch.Tensor) else rng).astype(np.uint64).reshape(-1)
+  if a.size >= 2:
+    return (int(a[0]) << 32) | int(a[1])
+  return int(a[0])
+
+
+class Env(abc.ABC):
+  """API for driving a brax system (`env.py:39-71`)."""
+
+  def __init__(self, config, device=None):
+    if config is not None:
+      self.sys = System(config, device=device)
+
+  @abc.abstractmethod
+  def reset(self, rng) -> State:
+    """Resets the environment to an initial state."""
+
+  @abc.abstractmethod
+  def step(self, state: State, action) -> State:
+    """Run one timestep of the environment's dynamics."""
+
+  @property
+  def observation_size(self) -> int:
+    return self.unwrapped.obs_size
+
+  @property
+  def action_size(self) -> int:
+    return self.sys.num_joint_dof + self.sys.num_forces_dof
+
+  @property
+  def unwrapped(self) -> 'Env':
+    return self
+
+  # fused-chain protocol: wrappers pass their options down to the env
+  def _chain_step(self, state, action, opts):
+    if opts:
+      raise NotImplementedError
+    return self.step(state, action)
+
+
+class Wrapper(Env):
+  """Wraps the environment to allow modular transformations (`env.py:74-102`)."""
+
+  def __init__(self, env: Env):
+    super().__init__(config=None)
+    self.env = env
+
+  def reset(self, rng) -> State:
+    return self.env.reset(rng)
+
+  def step(self, state: State, action) -> State:
+    return self.env.step(state, action)
+
+  @property
+  def observation_size(self) -> int:
+    return self.env.observation_size
+
+  @property
+  def action_size(self) -> int:
+    return self.env.action_size
+
+  @property
+  def unwrapped(self) -> Env:
+    return self.env.unwrapped
+
+  def __getattr__(self, name):
+    if name == '__setstate__':
+      raise AttributeError(name)
+    return getattr(self.env, name)
+
+
+class PhysicsEnv(Env):
+  """An env whose step/obs/reward are one of the fused kernel's env kinds."""
+
+  kind = 0
+  metric_keys = ()
+
+  def __init__(self, config, batch_size=None, device=None, **kwargs):
+    super().__init__(config, device=device)
+    self.batch_size = batch_size
+    self.coef = np.zeros(8, np.float32)
+
+  # -------------------------------------------------------------- helpers
+  def _params(self, opts=None, first_qp=None, first_obs=None):
+    opts = opts or {}
+    p = abi.BxEnvParams()
+    p.kind = self.kind
+    p.obs_size = self.obs_size
+    p.n_metrics = len(self.metric_keys)
+    p.episode_length = int(opts.get('episode_length', 0) or 0)
+    p.action_repeat = int(opts.get('action_repeat', 1))
+    p.auto_reset = 1 if opts.get('auto_reset') else 0
+    for i in range(8):
+      p.coef[i] = float(self.coef[i])
+    if first_qp is not None:
+      p.first_qp = qp_struct(first_qp, True)
+      p.first_obs = first_obs.data_ptr()
+    return p
+
+  def _alloc(self, B):
+    dev = self.sys.device
+    qp = packed_view(torch.empty((B, self.sys.num_bodies, 16), dtype=torch.float32, device=dev))
+    obs = torch.empty((B, self.obs_size), dtype=torch.float32, device=dev)
+    # one buffer for the per-env scalars: reward, done, steps, truncation
+    scal = torch.zeros((4, B), dtype=torch.float32, device=dev)
+    met = torch.empty((B, max(len(self.metric_keys), 1)), dtype=torch.float32, device=dev)
+    return qp, obs, scal, met
+
+  def _metrics(self, met):
+    return {k: met[:, i] for i, k in enumerate(self.metric_keys)}
+
+  # -------------------------------------------------------------- reset
+  def _noise_scale(self):
+    return self.reset_noise_scale
+
+  def reset_batch(self, rng, batch_size):
+    """Batched `Env.reset` (e.g. `ant.py:198-220`).
+
+    Reset noise U[-s, s] comes from the device counter RNG keyed by `rng`
+    (parity with JAX threefry is unpinned); parity of the
+    reset itself is pinned through `reset_from`."""
+    s = float(self._noise_scale())
+    D = self.sys.num_joint_dof
+    dev = self.sys.device
+    noise = torch.empty((2, batch_size, D), dtype=torch.float32, device=dev)
+    if D and batch_size:
+      _native.check(_native.lib().bx_uniform(C.c_void_p(noise.data_ptr()), noise.numel(),
+                                             key_to_seed(rng), 0, -s, s, _stream()))
+    qpos = self.sys.default_angle().reshape(1, -1) + noise[0]
+    return self.reset_from(qpos, noise[1])
+
+  def reset_from(self, joint_angle, joint_velocity):
+    """Reset state from explicit joint angles/velocities (B, num_joint_dof)."""
+    qp = self.sys.default_qp(joint_angle=joint_angle, joint_velocity=joint_velocity)
+    B = qp.pos.shape[0]
+    obs = self.observe(qp, torch.zeros((B, self.action_size), dtype=torch.float32,
+                                       device=self.sys.device))
+    dev = self.sys.device
+    zeros = torch.zeros((B,), dtype=torch.float32, device=dev)
+    metrics = {k: torch.zeros((B,), dtype=torch.float32, device=dev) for k in self.metric_keys}
+    return State(qp=qp, obs=obs, reward=zeros, done=torch.zeros_like(zeros), metrics=metrics,
+                 info={})
+
+  def observe(self, qp, action):
+    """`_get_obs(qp, sys.info(qp), action)` as used by reset."""
+    B = qp.pos.shape[0]
+    obs = torch.empty((B, self.obs_size), dtype=torch.float32, device=self.sys.device)
+    p = self._params()
+    qs = qp_struct(qp, True)
+    act = torch.as_tensor(action, dtype=torch.float32, device=self.sys.device).contiguous()
+    _native.check(_native.lib().bx_env_observe(
+        self.sys._h, C.byref(p), B, C.byref(qs), C.c_void_p(act.data_ptr()),
+        act.shape[-1], C.c_void_p(obs.data_ptr()), _stream()))
+    return obs
+
+  def reset(self, rng) -> State:
+    return self.reset_batch(rng, self.batch_size or 1)
+
+  # -------------------------------------------------------------- step
+  def step(self, state: State, action) -> State:
+    return self._chain_step(state, action, {})
+
+  def _chain_step(self, state, action, opts):
+    B = state.qp.pos.shape[0]
+    act = torch.as_tensor(action, dtype=torch.float32, device=self.sys.device)
+    if act.dim() == 1:
+      act = act.reshape(1, -1).expand(B, -1)
+    if act.shape != (B, self.action_size):
+      raise ValueError(f'action shape {tuple(act.shape)} != {(B, self.action_size)}')
+    if act.stride(-1) != 1:
+      act = act.contiguous()
+    auto = bool(opts.get('auto_reset'))
+    first_qp = state.info.get('first_qp') if auto else None
+    first_obs = state.info.get('first_obs') if auto else None
+    if auto and (first_qp is None or first_obs is None):
+      raise ValueError('AutoResetWrapper state lacks first_qp / first_obs')
+    p = self._params(opts, first_qp, first_obs)
+    qp, obs, scal, met = self._alloc(B)
+    sin = abi.BxEnvState()
+    sin.qp = qp_struct(state.qp, True)
+    done_in = torch.as_tensor(state.done, dtype=torch.float32, device=self.sys.device).contiguous()
+    sin.done = done_in.data_ptr()
+    steps_in = state.info.get('steps')
+    if steps_in is not None:
+      steps_in = torch.as_tensor(steps_in, dtype=torch.float32, device=self.sys.device).contiguous()
+      sin.steps = steps_in.data_ptr()
+    sout = abi.BxEnvState()
+    sout.qp = qp_struct(qp, True)
+    sout.obs = obs.data_ptr()
+    sout.reward = scal[0].data_ptr()
+    sout.done = scal[1].data_ptr()
+    sout.steps = scal[2].data_ptr()
+    sout.truncation = scal[3].data_ptr()
+    sout.metrics = met.data_ptr()
+    _native.check(_native.lib().bx_env_step(
+        self.sys._h, C.byref(p), B, C.byref(sin), C.c_void_p(act.data_ptr()), act.stride(0),
+        C.byref(sout), _stream()))
+    info = dict(state.info)
+    if p.episode_length > 0:
+      info['steps'] = scal[2]
+      info['truncation'] = scal[3]
+    metrics = dict(state.metrics)
+    metrics.update(self._metrics(met))
+    return State(qp=qp, obs=obs, reward=scal[0], done=scal[1], metrics=metrics, info=info)

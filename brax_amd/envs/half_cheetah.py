@@ -1,0 +1,26 @@
+"""HalfCheetah (`brax/envs/half_cheetah.py:147-218`) on MI355X.
+
+obs = [torso z, rot.w, rot.y, joint angles(6), vel.x, vel.z, ang.y,
+joint vels(6)] = 18; reward = forward_w * dx/dt - ctrl_w * |a|^2; never done.
+"""
+import numpy as np
+
+from brax_amd.envs import configs
+from brax_amd.envs.env import PhysicsEnv
+
+
+class Halfcheetah(PhysicsEnv):
+  """Trains a halfcheetah to run in the +x direction."""
+
+  kind = 3  # BX_ENV_HALFCHEETAH
+  metric_keys = ('reward_ctrl', 'reward_run', 'x_position', 'x_velocity')
+
+  def __init__(self, forward_reward_weight=1.0, ctrl_cost_weight=0.1, reset_noise_scale=0.1,
+               legacy_spring=False, exclude_current_positions_from_observation=True, **kwargs):
+    if legacy_spring or not exclude_current_positions_from_observation:
+      raise NotImplementedError('only the default HalfCheetah configuration is supported')
+    super().__init__(configs.HALFCHEETAH_CONFIG, **kwargs)
+    self.reset_noise_scale = reset_noise_scale
+    self.coef = np.array([forward_reward_weight, ctrl_cost_weight, 0, 0, 0, 0, 0, 0], np.float32)
+    D = self.sys.num_joint_dof
+    self.obs_size = 3 + D + 3 + D

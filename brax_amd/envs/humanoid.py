@@ -1,0 +1,35 @@
+"""Humanoid (upstream `brax/envs/humanoid.py:196-342`) on MI355X.
+
+obs (240) = qpos [torso z, rot, 17 angles] + qvel [vel, ang, 17 joint vels]
++ cinert (11x9) + cvel (11x3) + cang (11x3) + qfrc_actuator (30), where
+qfrc uses an UNMASKED take of the padded act_index (-1 reads action[0],
+`humanoid.py:318-320`) and cinert adds the INVERSE inertia diagonal.
+"""
+import numpy as np
+
+from brax_amd.envs import configs
+from brax_amd.envs.env import PhysicsEnv
+
+
+class Humanoid(PhysicsEnv):
+  """Trains a humanoid to run in the +x direction."""
+
+  kind = 2  # BX_ENV_HUMANOID
+  metric_keys = ('distance_from_origin', 'forward_reward', 'reward_alive', 'reward_linvel',
+                 'reward_quadctrl', 'x_position', 'x_velocity', 'y_position', 'y_velocity')
+
+  def __init__(self, forward_reward_weight=1.25, ctrl_cost_weight=0.1, healthy_reward=5.0,
+               terminate_when_unhealthy=True, healthy_z_range=(0.8, 2.1),
+               reset_noise_scale=1e-2, exclude_current_positions_from_observation=True,
+               legacy_spring=False, **kwargs):
+    if legacy_spring or not exclude_current_positions_from_observation:
+      raise NotImplementedError('only the default Humanoid configuration is supported')
+    super().__init__(configs.HUMANOID_CONFIG, **kwargs)
+    self.reset_noise_scale = reset_noise_scale
+    self.coef = np.array([forward_reward_weight, ctrl_cost_weight, 0, healthy_reward,
+                          healthy_z_range[0], healthy_z_range[1],
+                          1.0 if terminate_when_unhealthy else 0.0, 0], np.float32)
+    D = self.sys.num_joint_dof
+    M = self.sys.num_bodies - 1
+    qfrc = sum(int(d) for d in self.sys.desc['joint_dof'][self.sys.desc['act_joint']])
+    self.obs_size = 1 + 4 + D + 3 + 3 + D + 9 * M + 3 * M + 3 * M + qfrc

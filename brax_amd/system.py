@@ -1,0 +1,197 @@
+"""`brax.System` on MI355X (`brax/physics/system.py:46-340`).
+
+    sys = brax_amd.System(config)            # text proto or brax_amd.Config
+    qp = sys.default_qp()                    # QP (N,·) on the device
+    qp, info = sys.step(qp, act)             # batched if qp has a leading axis
+
+`step` runs the fused PBD kernel (`bx_system_step`); `default_qp` and `info`
+run their own kernels. Every call is stream-ordered on torch's current stream.
+There is no CPU fallback: without a GPU or the built library the constructor
+raises.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from brax_amd import _native
+from brax_amd import abi
+from brax_amd import compiler
+from brax_amd import config as cfgmod
+from brax_amd.base import Info, P, QP, packed_view
+
+
+def _stream():
+  return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _field(t, batched):
+  if t.dtype != torch.float32 or not t.is_cuda:
+    raise TypeError('QP fields must be float32 device tensors')
+  if t.stride(-1) != 1:
+    raise ValueError('QP fields need a unit innermost stride')
+  f = abi.BxField()
+  f.ptr = t.data_ptr()
+  f.env_stride = t.stride(0) if batched else 0
+  f.body_stride = t.stride(-2)
+  return f
+
+
+def qp_struct(qp, batched):
+  s = abi.BxQP()
+  s.pos = _field(qp.pos, batched)
+  s.rot = _field(qp.rot, batched)
+  s.vel = _field(qp.vel, batched)
+  s.ang = _field(qp.ang, batched)
+  return s
+
+
+class Body:
+  """Per-body constants (`bodies.py:25-59`): mass and INVERSE inertia."""
+
+  def __init__(self, desc, index):
+    self.mass = desc['body_mass'].copy()
+    self.inertia = desc['body_inv_inertia'].copy()
+    self.index = dict(index)
+    self.idx = np.arange(len(self.mass))
+
+
+class System:
+  """A brax system compiled for the MI355X kernels."""
+
+  def __init__(self, config, device=None):
+    if isinstance(config, str):
+      config = cfgmod.parse(config)
+    self.config, self.desc, meta = compiler.compile_system(config)
+    self.reset_desc = compiler.compile_reset(self.config, meta['body_index'])
+    self.num_bodies = int(self.desc['n_bodies'])
+    self.num_joints = len(self.config.joints)
+    self.num_joint_dof = meta['num_joint_dof']
+    self.num_forces_dof = meta['num_forces_dof']
+    self.num_actuators = len(self.config.actuators)
+    self.action_size = meta['action_size']
+    self.num_contacts = len(self.desc['row_group'])
+    self.body = Body(self.desc, meta['body_index'])
+    self.joint_groups = meta['joint_groups']
+    if device is None:
+      if not torch.cuda.is_available():
+        raise _native.NativeError('brax_amd.System needs a GPU (no CPU fallback)')
+      device = torch.device('cuda', torch.cuda.current_device())
+    self.device = torch.device(device)
+    if self.device.type != 'cuda':
+      raise _native.NativeError('brax_amd runs on MI355X devices only')
+    lib = _native.lib()
+    cd, keep = abi.make_desc(self.desc)
+    rd, keep_r = abi.make_reset_desc(self.reset_desc)
+    h = C.c_void_p()
+    _native.check(lib.bx_system_create(C.byref(cd), C.byref(rd),
+                                       self.device.index or 0, C.byref(h)))
+    del keep, keep_r
+    self._h = h
+    self.lanes = lib.bx_system_lanes(h)
+
+  def __del__(self):
+    h = getattr(self, '_h', None)
+    if h is not None and h.value:
+      try:
+        _native.lib().bx_system_destroy(h)
+      except Exception:  # pylint: disable=broad-except
+        pass
+
+  # ---------------------------------------------------------------- helpers
+  def _new_qp(self, lead):
+    return packed_view(torch.empty(lead + (self.num_bodies, 16), dtype=torch.float32,
+                                   device=self.device))
+
+  def _act(self, act, B):
+    if act is None:
+      act = torch.zeros((B, self.action_size), dtype=torch.float32, device=self.device)
+    act = torch.as_tensor(act, dtype=torch.float32, device=self.device)
+    if act.dim() == 1:
+      act = act.reshape(1, -1).expand(B, -1) if B > 1 else act.reshape(1, -1)
+    if act.shape[-1] != self.action_size:
+      raise ValueError(f'action has size {act.shape[-1]}, system expects {self.action_size}')
+    if act.stride(-1) != 1:
+      act = act.contiguous()
+    return act
+
+  # ---------------------------------------------------------------- API
+  def default_angle(self, default_index: int = 0):
+    """`System.default_angle` (system.py:86-110)."""
+    a = compiler.default_angle(self.config, default_index)
+    return torch.as_tensor(a, dtype=torch.float32, device=self.device)
+
+  def default_qp(self, default_index: int = 0, joint_angle=None, joint_velocity=None):
+    """`System.default_qp` (system.py:112-242) on the device.
+
+    joint_angle / joint_velocity may carry a leading batch axis; the result
+    then is batched too."""
+    if default_index != 0:
+      raise NotImplementedError('default_index != 0 is not supported on device yet')
+    if joint_angle is None:
+      joint_angle = self.default_angle(default_index)
+    ja = torch.as_tensor(joint_angle, dtype=torch.float32, device=self.device)
+    batched = ja.dim() == 2
+    ja = ja.reshape(-1, self.num_joint_dof).contiguous()
+    B = ja.shape[0]
+    if joint_velocity is None:
+      jv = torch.zeros_like(ja)
+    else:
+      jv = torch.as_tensor(joint_velocity, dtype=torch.float32,
+                           device=self.device).reshape(B, -1).contiguous()
+    out = self._new_qp((B,))
+    qs = qp_struct(out, True)
+    _native.check(_native.lib().bx_system_default_qp(
+        self._h, B, C.c_void_p(ja.data_ptr()), C.c_void_p(jv.data_ptr()), C.byref(qs),
+        _stream()))
+    return out if batched else out[0]
+
+  def step(self, qp: QP, act):
+    """`System.step` (system.py:244-325): (QP, act) -> (QP, Info)."""
+    batched = qp.pos.dim() == 3
+    B = qp.pos.shape[0] if batched else 1
+    act = self._act(act, B)
+    lead = (B,) if batched else ()
+    out = self._new_qp(lead)
+    N, R = self.num_bodies, self.num_contacts
+    cbuf = torch.empty(lead + (N, 12), dtype=torch.float32, device=self.device)
+    cvel, cang = cbuf[..., 0:3], cbuf[..., 3:6]
+    aang = cbuf[..., 9:12]
+    avel = cbuf[..., 6:9]
+    cpos = torch.empty(lead + (R, 3), dtype=torch.float32, device=self.device)
+    cnorm = torch.empty(lead + (R, 3), dtype=torch.float32, device=self.device)
+    cpen = torch.empty(lead + (R,), dtype=torch.float32, device=self.device)
+    info = abi.BxInfo()
+    info.contact_vel = _field(cvel, batched)
+    info.contact_ang = _field(cang, batched)
+    info.actuator_vel = _field(avel, batched)
+    info.actuator_ang = _field(aang, batched)
+    if R:
+      info.contact_pos = cpos.data_ptr()
+      info.contact_normal = cnorm.data_ptr()
+      info.contact_penetration = cpen.data_ptr()
+    qi = qp_struct(qp, batched)
+    qo = qp_struct(out, batched)
+    _native.check(_native.lib().bx_system_step(
+        self._h, B, C.byref(qi), C.c_void_p(act.data_ptr()),
+        act.stride(0) if act.dim() == 2 else 0, C.byref(qo), C.byref(info), _stream()))
+    zero = torch.zeros_like(cvel)
+    return out, Info(contact=P(cvel, cang), joint=P(zero, zero), actuator=P(avel, aang),
+                     contact_pos=cpos, contact_normal=cnorm, contact_penetration=cpen)
+
+  def info(self, qp: QP):
+    """`System.info` in pbd mode (system.py:327-340): the contact part."""
+    batched = qp.pos.dim() == 3
+    B = qp.pos.shape[0] if batched else 1
+    lead = (B,) if batched else ()
+    cbuf = torch.empty(lead + (self.num_bodies, 6), dtype=torch.float32, device=self.device)
+    info = abi.BxInfo()
+    info.contact_vel = _field(cbuf[..., 0:3], batched)
+    info.contact_ang = _field(cbuf[..., 3:6], batched)
+    qi = qp_struct(qp, batched)
+    _native.check(_native.lib().bx_system_info(self._h, B, C.byref(qi), C.byref(info),
+                                               _stream()))
+    zero = torch.zeros_like(cbuf[..., 0:3])
+    return Info(contact=P(cbuf[..., 0:3], cbuf[..., 3:6]), joint=P(zero, zero),
+                actuator=P(zero, zero), contact_pos=None, contact_normal=None,
+                contact_penetration=None)

@@ -166,6 +166,15 @@ typedef struct bx_env_params {
   int32_t episode_length;   /* <= 0: no EpisodeWrapper */
   int32_t action_repeat;    /* EpisodeWrapper action_repeat (>= 1) */
   int32_t auto_reset;       /* AutoResetWrapper present */
+  /* env constructor arguments (ant.py:173-183, humanoid.py:196-212,
+   * half_cheetah.py:147-158):
+   *   ANT:         forward_w(unused=1), ctrl_cost_weight, contact_cost_weight,
+   *                healthy_reward, healthy_z_min, healthy_z_max,
+   *                terminate_when_unhealthy, use_contact_forces
+   *   HUMANOID:    forward_reward_weight, ctrl_cost_weight, 0, healthy_reward,
+   *                healthy_z_min, healthy_z_max, terminate_when_unhealthy, 0
+   *   HALFCHEETAH: forward_reward_weight, ctrl_cost_weight, 0... */
+  float coef[8];
   /* AutoReset targets (first_qp / first_obs); required when auto_reset */
   bx_qp first_qp;
   const float* first_obs;
@@ -180,6 +189,9 @@ int bx_device_count(int* count);
 int bx_system_create(const bx_desc* desc, const bx_reset_desc* reset,
                      int device, bx_system** out);
 int bx_system_destroy(bx_system* sys);
+
+/* Lanes of a wavefront that own one env in this system's kernels (16/32/64). */
+int bx_system_lanes(bx_system* sys);
 
 /* Physics only: B independent System.step calls (system.py:244-325).
  * act: (B, action_size) with row stride act_stride. qp_in and qp_out may not

@@ -127,6 +127,14 @@ class Oracle:
       raise ValueError('obs size mismatch')
     return out, obs, rew, dn, met
 
+  def closest_segments(self, segs):
+    segs = self._a(segs).reshape(-1, 4, 3)
+    n = segs.shape[0]
+    a = np.empty((n, 3), self.dtype)
+    b = np.empty((n, 3), self.dtype)
+    self._fn('oracle_closest_segments')(C.c_int64(n), _p(segs), _p(a), _p(b))
+    return a, b
+
   def default_qp(self, angles, vels):
     assert self.creset is not None
     angles = self._a(angles)

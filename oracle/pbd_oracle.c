@@ -1406,6 +1406,47 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
   return rc;
 }
 
+/* geometry.closest_segment_to_segment_points (geometry.py:394-461), exported
+ * for the reference's known-answer cases (geometry_test.py:217-272) */
+void FN(oracle_closest_segments)(int64_t n, const R* seg, R* a_best, R* b_best) {
+  for (int64_t i = 0; i < n; i++) {
+    const R* s = seg + 12 * i;
+    R a0[3], a1[3], b0[3], b1[3];
+    for (int k = 0; k < 3; k++) { a0[k] = s[k]; a1[k] = s[3 + k]; b0[k] = s[6 + k]; b1[k] = s[9 + k]; }
+    R da[3], db[3];
+    for (int k = 0; k < 3; k++) { da[k] = a1[k] - a0[k]; db[k] = b1[k] - b0[k]; }
+    R la = safe_norm3(da);
+    la += (R)1e-6 * (R)(la == 0);
+    for (int k = 0; k < 3; k++) da[k] /= la;
+    R hla = la * (R)0.5;
+    R lb = safe_norm3(db);
+    lb += (R)1e-6 * (R)(lb == 0);
+    for (int k = 0; k < 3; k++) db[k] /= lb;
+    R hlb = lb * (R)0.5;
+    R am[3], bm[3], tr[3];
+    for (int k = 0; k < 3; k++) { am[k] = a0[k] + da[k] * hla; bm[k] = b0[k] + db[k] * hlb; tr[k] = am[k] - bm[k]; }
+    R dadb = dot3(da, db), datr = dot3(da, tr), dbtr = dot3(db, tr);
+    R den = 1 - dadb * dadb;
+    R ota = (-datr + dadb * dbtr) / (den + (R)1e-6);
+    R otb = dbtr + ota * dadb;
+    R ta = clip(ota, -hla, hla), tb = clip(otb, -hlb, hlb);
+    R ba[3], bb[3];
+    for (int k = 0; k < 3; k++) { ba[k] = am[k] + da[k] * ta; bb[k] = bm[k] + db[k] * tb; }
+    R na[3], nb[3], d1, d2, ab[3], t[3], v[3], tt;
+    for (int k = 0; k < 3; k++) { ab[k] = a1[k] - a0[k]; t[k] = bb[k] - a0[k]; }
+    tt = clip(dot3(t, ab) / (dot3(ab, ab) + (R)1e-6), 0, 1);
+    for (int k = 0; k < 3; k++) { na[k] = a0[k] + tt * ab[k]; v[k] = bb[k] - na[k]; }
+    d1 = dot3(v, v);
+    for (int k = 0; k < 3; k++) { ab[k] = b1[k] - b0[k]; t[k] = ba[k] - b0[k]; }
+    tt = clip(dot3(t, ab) / (dot3(ab, ab) + (R)1e-6), 0, 1);
+    for (int k = 0; k < 3; k++) { nb[k] = b0[k] + tt * ab[k]; v[k] = ba[k] - nb[k]; }
+    d2 = dot3(v, v);
+    if (d1 < d2) memcpy(ba, na, sizeof(na)); else memcpy(bb, nb, sizeof(nb));
+    memcpy(a_best + 3 * i, ba, sizeof(ba));
+    memcpy(b_best + 3 * i, bb, sizeof(bb));
+  }
+}
+
 /* -------------------------------------------------------------- reset ---- */
 
 /* System.default_qp (system.py:112-242) for B envs from explicit joint angles

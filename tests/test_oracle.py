@@ -1,0 +1,123 @@
+"""The C restatement (oracle/) pinned to the reference's golden vectors.
+
+Float64 restatement vs the reference's own float64 numpy execution: agreement
+to ~1e-10 shows the restatement is the reference's algorithm, so it can check
+the HIP path at sizes the goldens do not cover."""
+import numpy as np
+import pytest
+
+from tests.conftest import golden
+from tests.helpers import compiled
+
+ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah']
+SYS_TRAJ = ['mountain1', 'mountain2', 'mountain4']
+
+
+def _oracle(oracle_lib, name, guard=False, dtype=np.float64):
+  vc, d, rd, meta = compiled(name)
+  return oracle_lib.Oracle(d, rd, dtype, safe_guard=guard)
+
+
+@pytest.mark.parametrize('name', ENV_TRAJ + SYS_TRAJ)
+def test_system_step_matches_reference(oracle_lib, name):
+  o = _oracle(oracle_lib, name)
+  T = golden('traj_' + name)
+  for t in range(T['action'].shape[0]):
+    out, info = o.system_step(T['qp'][t], T['action'][t])
+    assert np.abs(out - T['qp'][t + 1]).max() < 1e-9
+    assert np.abs(info['contact'] - T['info_contact'][t]).max() < 1e-9
+    assert np.abs(info['actuator'] - T['info_actuator'][t]).max() < 1e-9
+    assert np.abs(info['contact_penetration'] - T['contact_penetration'][t]).max() < 1e-11
+
+
+@pytest.mark.parametrize('name', ENV_TRAJ)
+def test_env_step_matches_reference(oracle_lib, name):
+  o = _oracle(oracle_lib, name)
+  T = golden('traj_' + name)
+  O, M = T['obs'].shape[-1], T['metrics'].shape[-1]
+  for t in range(T['action'].shape[0]):
+    _, obs, rew, done, met = o.env_step(name, T['qp'][t], T['action'][t], O, M)
+    assert np.abs(obs - T['obs'][t + 1]).max() < 1e-9
+    assert np.abs(rew - T['reward'][t]).max() < 1e-12
+    assert np.array_equal(done, T['done'][t])
+    assert np.abs(met - T['metrics'][t]).max() < 1e-12
+
+
+@pytest.mark.parametrize('name', ENV_TRAJ)
+def test_reset_matches_reference(oracle_lib, name):
+  o = _oracle(oracle_lib, name)
+  T = golden('traj_' + name)
+  qp0 = o.default_qp(T['reset_qpos'], T['reset_qvel'])
+  assert np.abs(qp0 - T['qp'][0]).max() < 1e-12
+  ic = o.system_info(qp0)
+  B = qp0.shape[0]
+  obs = o.env_obs(name, qp0, ic, np.zeros((B, o.A)), T['obs'].shape[-1])
+  assert np.abs(obs - T['reset_obs']).max() < 1e-12
+
+
+def test_safe_norm_guard_is_negligible(oracle_lib):
+  # jit's allclose(x, 0) zero guard (jumpy.py:183-189) vs the numpy path
+  T = golden('traj_ant')
+  a = _oracle(oracle_lib, 'ant', guard=True).system_step(T['qp'][3], T['action'][3])[0]
+  b = _oracle(oracle_lib, 'ant', guard=False).system_step(T['qp'][3], T['action'][3])[0]
+  assert np.abs(a - b).max() < 1e-7
+
+
+def test_fp32_envelope(oracle_lib):
+  """Brax's algorithm in fp32 stays within SURVEY §8(c)'s envelope."""
+  T = golden('traj_ant')
+  o = _oracle(oracle_lib, 'ant', guard=True, dtype=np.float32)
+  out, _ = o.system_step(T['qp'][2], T['action'][2])
+  ref = T['qp'][3]
+  nw = lambda a, b: (np.abs(a - b).max(axis=(1, 2)) / np.maximum(1, np.abs(b).max(axis=(1, 2))))
+  assert nw(out[..., 0:3], ref[..., 0:3]).max() < 1e-5
+  assert nw(out[..., 7:10], ref[..., 7:10]).max() < 1e-3
+
+
+def test_closest_segment_kats(oracle_lib):
+  o = _oracle(oracle_lib, 'ant')
+  k = golden('kat')
+  a, b = o.closest_segments(k['seg_in'])
+  assert np.abs(a - k['seg_a']).max() < 1e-12 and np.abs(b - k['seg_b']).max() < 1e-12
+  # the reference's own literal cases (geometry_test.py:217-272)
+  cases = [
+      ([[0.73432405, 0.12372768, 0.20272314], [1.10600128, 0.88555209, 0.65209485],
+        [0.85599262, 0.61736299, 0.9843583], [1.84270939, 0.92891793, 1.36343326]],
+       [1.09063, 0.85404, 0.63351], [0.99596, 0.66156, 1.03813], 5),
+      ([[0, 0, -1], [0, 0, 1], [-1, 0, 0], [1, 0, 0]], [0, 0, 0], [0, 0, 0], 5),
+      ([[0.2, 0.2, 0], [1, 1, 0], [0.2, 0.4, 0], [1, 2, 0]], [0.3, 0.3, 0], [0.2, 0.4, 0], 2),
+      ([[0, 0, -1], [0, 0, 1], [1, 0, -1], [1, 0, 1]], [0, 0, 0], [1, 0, 0], 5),
+      ([[0, 0, -1], [0, 0, 1], [1, 0, 1], [1, 0, 3]], [0, 0, 1], [1, 0, 1], 5),
+      ([[0, 0, -1], [0, 0, -1], [1, 0, 0.1], [1, 0, 0.1]], [0, 0, -1], [1, 0, 0.1], 5),
+      ([[0, 0, -1], [0, 0, 1], [0, 0, -1], [0, 0, 1]], [0, 0, 0], [0, 0, 0], 5),
+  ]
+  for seg, ea, eb, places in cases:
+    a, b = o.closest_segments(np.array(seg, np.float64))
+    np.testing.assert_allclose(a[0], ea, atol=1.5 * 10**-places)
+    np.testing.assert_allclose(b[0], eb, atol=1.5 * 10**-places)
+
+
+def test_wrapper_semantics(oracle_lib):
+  """Episode + AutoReset semantics (wrappers.py:105-148) restated in numpy on
+  top of the oracle's unwrapped env step, vs the reference's wrapped rollout."""
+  T = golden('wrap_ant')
+  o = _oracle(oracle_lib, 'ant')
+  ep = int(T['episode_length'])
+  qp, obs = T['qp'][0], T['obs'][0]
+  done = T['done'][0]
+  steps = T['steps'][0]
+  for t in range(T['action'].shape[0]):
+    steps = np.where(done != 0, 0.0, steps)
+    qp1, obs1, rew, d_in, _ = o.env_step('ant', qp, T['action'][t], 87, 10)
+    steps = steps + 1
+    done = np.where(steps >= ep, 1.0, d_in)
+    trunc = np.where(steps >= ep, 1 - d_in, 0.0)
+    sel = done != 0
+    qp = np.where(sel[:, None, None], T['first_qp'], qp1)
+    obs = np.where(sel[:, None], T['first_obs'], obs1)
+    assert np.abs(qp - T['qp'][t + 1]).max() < 1e-9
+    assert np.abs(obs - T['obs'][t + 1]).max() < 1e-9
+    assert np.abs(rew - T['reward'][t + 1]).max() < 1e-12
+    assert np.array_equal(done, T['done'][t + 1])
+    assert np.array_equal(steps, T['steps'][t + 1])
+    assert np.array_equal(trunc, T['truncation'][t + 1])
