@@ -78,6 +78,7 @@ class BxEnvParams(C.Structure):
   _fields_ = [('kind', C.c_int32), ('obs_size', C.c_int32),
               ('n_metrics', C.c_int32), ('episode_length', C.c_int32),
               ('action_repeat', C.c_int32), ('auto_reset', C.c_int32),
+              ('coef', C.c_float * 8),
               ('first_qp', BxQP), ('first_obs', C.c_void_p)]
 
 
