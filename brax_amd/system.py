@@ -132,8 +132,12 @@ class System:
       joint_angle = self.default_angle(default_index)
     ja = torch.as_tensor(joint_angle, dtype=torch.float32, device=self.device)
     batched = ja.dim() == 2
-    ja = ja.reshape(-1, self.num_joint_dof).contiguous()
-    B = ja.shape[0]
+    if self.num_joint_dof == 0:
+      B = ja.shape[0] if batched else 1
+      ja = torch.zeros((B, 0), dtype=torch.float32, device=self.device)
+    else:
+      ja = ja.reshape(-1, self.num_joint_dof).contiguous()
+      B = ja.shape[0]
     if joint_velocity is None:
       jv = torch.zeros_like(ja)
     else:
