@@ -88,6 +88,8 @@ def main():
   ap.add_argument('--warmup', type=int, default=50)
   ap.add_argument('--batch', type=int, default=4096)
   ap.add_argument('--no-cpu-baseline', action='store_true')
+  ap.add_argument('--generic', action='store_true',
+                  help='force the generic item-loop kernel variant (A/B)')
   args = ap.parse_args()
 
   dist, rank, world, local = _dist()
@@ -98,6 +100,8 @@ def main():
 
   B = args.batch
   env = envs.create('ant', batch_size=B, episode_length=1000, auto_reset=True, device=dev)
+  if args.generic:
+    _native.check(_native.lib().bx_system_set_single(env.sys._h, 0))
   state = env.reset(np.array([rank, 0x5EED], np.uint32))
   acts = torch.empty((2, B, 8), dtype=torch.float32, device=dev)
   lib = _native.lib()

@@ -33,6 +33,7 @@ _SIGS = {
                           C.POINTER(C.c_void_p)], C.c_int),
     'bx_system_destroy': ([C.c_void_p], C.c_int),
     'bx_system_lanes': ([C.c_void_p], C.c_int),
+    'bx_system_set_single': ([C.c_void_p, C.c_int], C.c_int),
     'bx_system_step': ([C.c_void_p, C.c_int64, C.POINTER(abi.BxQP), C.c_void_p, C.c_int64,
                         C.POINTER(abi.BxQP), C.POINTER(abi.BxInfo), C.c_void_p], C.c_int),
     'bx_env_step': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64,

@@ -44,6 +44,7 @@ struct bx_system {
   std::vector<uint32_t> host;
   uint32_t* blob = nullptr;
   int L = 16;
+  bool single_ok = false;
   size_t lds_env = 0;    // bytes per block for the per-env kernels
   size_t lds_reset = 0;  // bytes per block for default_qp
 };
@@ -282,9 +283,18 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.l_ang = carve(2 * D);
   H.l_red = carve(64);
   H.env_words = off;
+  {
+    size_t mx = 0;
+    for (int b = 0; b < N; b++) mx = std::max({mx, jl[b].size(), al[b].size(), cl[b].size()});
+    H.single = (N <= L && J <= L && K <= L && R <= L && mx <= 8) ? 1 : 0;
+    H.act_same = 1;
+    for (int a = 0; a < K; a++)
+      if (d->act_joint[a] != a) H.act_same = 0;
+  }
   std::memcpy(B.w.data(), &H, sizeof(BlobHdr));
 
   S->hdr = H;
+  S->single_ok = H.single != 0;
   S->host = std::move(B.w);
   S->L = L;
   S->lds_env = (size_t)(64 / L) * H.env_words * 4;
@@ -347,6 +357,13 @@ int bx_system_destroy(bx_system* S) {
 
 int bx_system_lanes(bx_system* S) { return S ? S->L : 0; }
 
+int bx_system_set_single(bx_system* S, int on) {
+  if (!S) return fail("null system");
+  if (on && !S->single_ok) return fail("system does not fit the single-item-per-lane kernel");
+  S->hdr.single = on ? 1 : 0;
+  return 0;
+}
+
 int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* act,
                    int64_t act_stride, const bx_qp* qout, const bx_info* info, void* stream) {
   if (!S || !qin || !qout) return fail("null argument");
@@ -361,7 +378,7 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   a.act = act;
   a.act_stride = act_stride;
   if (info) a.info = *info;
-  HIP_OK(launch_system_step(S->L, n_envs, S->lds_env, as_stream(stream), a));
+  HIP_OK(launch_system_step(S->L, S->hdr.single != 0, n_envs, S->lds_env, as_stream(stream), a));
   return 0;
 }
 
@@ -384,7 +401,7 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   a.out = *out;
   a.act = act;
   a.act_stride = act_stride;
-  HIP_OK(launch_env_step(S->L, n_envs, S->lds_env, as_stream(stream), a));
+  HIP_OK(launch_env_step(S->L, S->hdr.single != 0, n_envs, S->lds_env, as_stream(stream), a));
   return 0;
 }
 

@@ -137,7 +137,7 @@ __device__ __forceinline__ void angle_update(const JointC& J, const q4& rp, cons
 }
 
 // Revolute/Spherical.apply_reduced (joints.py:270-309, 332-386)
-__device__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, q4& dpr,
+__device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, q4& dpr,
                             v3& dcp, q4& dcr) {
   // positional constraint: apply_position_update (joints.py:154-195)
   v3 pw = p.pos + rotate(J.off_p, p.rot);
@@ -204,7 +204,7 @@ __device__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, 
 }
 
 // Revolute/Spherical.axis_angle (joints.py:311-319, 388-415); returns dof
-__device__ int axis_angle(const JointC& J, const QP& p, const QP& c, v3* axes, float* ang) {
+__device__ __forceinline__ int axis_angle(const JointC& J, const QP& p, const QP& c, v3* axes, float* ang) {
   if (J.type == 1) {
     axes[0] = rotate(J.axp[0], p.rot);
     v3 ref_p = rotate(J.axp[2], p.rot);
@@ -283,7 +283,7 @@ __device__ __forceinline__ RowC load_row(const Cst& c, const BlobHdr& H, int r) 
 }
 
 // capsule_plane (colliders.py:744-759) / capsule_capsule (:805-819)
-__device__ void contact_gen(const RowC& R, const QP& a, const QP& b, v3& pos, v3& vel, v3& n,
+__device__ __forceinline__ void contact_gen(const RowC& R, const QP& a, const QP& b, v3& pos, v3& vel, v3& n,
                             float& pen) {
   if (R.fn == 0) {
     v3 e = a.pos + rotate(R.a_end, a.rot);
@@ -335,7 +335,7 @@ __device__ void contact_gen(const RowC& R, const QP& a, const QP& b, v3& pos, v3
 }
 
 // One/TwoWay._position_contact (colliders.py:306-377, 495-580)
-__device__ float position_contact(const RowC& R, const QP& a, const QP& b, const v3& ao_pos,
+__device__ __forceinline__ float position_contact(const RowC& R, const QP& a, const QP& b, const v3& ao_pos,
                                   const q4& ao_rot, const v3& bo_pos, const q4& bo_rot, v3 cpos,
                                   v3 n, float cpen, v3& oap, q4& oar, v3& obp, q4& obr) {
   float sc = R.scale;
@@ -408,7 +408,7 @@ __device__ float position_contact(const RowC& R, const QP& a, const QP& b, const
 
 // One/TwoWay._velocity_contact (colliders.py:379-442, 584-658);
 // (aov, aoa, aop) = qp_right_before of body a (vel, ang, pos), same for b.
-__device__ void velocity_contact(const RowC& R, float h, const QP& a, const QP& b, v3 aop,
+__device__ __forceinline__ void velocity_contact(const RowC& R, float h, const QP& a, const QP& b, v3 aop,
                                  v3 aov, v3 aoa, v3 bop, v3 bov, v3 boa, v3 cpos, v3 n, float cpen,
                                  float dlam, v3& oav, v3& oaa, v3& obv, v3& oba) {
   v3 ra = cpos - a.pos, rb = cpos - b.pos;
@@ -789,6 +789,312 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
   }
 }
 
+// ---------------------------------------------------------------------------
+// SINGLE mode: every lane owns at most one body, joint, actuator and contact
+// row of its env (N, J, K, R <= L) and every per-body gather list fits MAXG.
+// All constants and gather lists are hoisted into registers once per launch;
+// the lane's own body state stays in registers across the substep loop and
+// LDS carries only what other lanes read. No global loads inside the loop.
+// ---------------------------------------------------------------------------
+constexpr int MAXG = 8;
+
+struct GList {
+  int n;
+  int e[MAXG];
+};
+
+__device__ __forceinline__ GList load_glist(const Cst& c, int o_off, int o_l, int b) {
+  GList g;
+  int s = c.i(o_off + b);
+  g.n = c.i(o_off + b + 1) - s;
+#pragma unroll
+  for (int k = 0; k < MAXG; k++) g.e[k] = k < g.n ? c.i(o_l + s + k) : 0;
+  return g;
+}
+
+struct Hoist {
+  bool hasB, hasJ, hasA, hasR;
+  BodyC B;
+  JointC J;
+  ActC A;
+  RowC R;
+  GList jl, al, cl;
+};
+
+__device__ __forceinline__ void load_hoist(const Cst& c, const BlobHdr& H, int lane, Hoist& X) {
+  X.hasB = lane < H.N;
+  X.hasJ = lane < H.J;
+  X.hasA = lane < H.K;
+  X.hasR = lane < H.R;
+  int b = X.hasB ? lane : 0;
+  X.B = load_body(c, H, b);
+  X.jl = load_glist(c, H.o_jl_off, H.o_jl, b);
+  X.al = load_glist(c, H.o_al_off, H.o_al, b);
+  X.cl = load_glist(c, H.o_cl_off, H.o_cl, b);
+  if (!X.hasB) { X.jl.n = 0; X.al.n = 0; X.cl.n = 0; }
+  if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? lane : 0);
+  if (H.K > 0) X.A = load_act(c, H, X.hasA ? lane : 0);
+  if (H.R > 0) X.R = load_row(c, H, X.hasR ? lane : 0);
+}
+
+__device__ __forceinline__ v3 gsum3(const GList& g, const float* base, int stride) {
+  v3 s = mk(0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < MAXG; k++)
+    if (k < g.n) s = s + ld3(base + g.e[k] * stride);
+  return s;
+}
+
+// per-group normalised contact sums: sum_g (sum rows) / (eps + count)
+__device__ __forceinline__ void gsum_contact(const GList& g, const float* cslot, float eps, v3& a,
+                                             q4& r, bool rot4) {
+  a = mk(0.f, 0.f, 0.f);
+  r = q4{0.f, 0.f, 0.f, 0.f};
+  v3 ga = mk(0.f, 0.f, 0.f);
+  q4 gr{0.f, 0.f, 0.f, 0.f};
+  float cnt = 0.f;
+  int cur = -1;
+#pragma unroll
+  for (int k = 0; k < MAXG; k++) {
+    if (k < g.n) {
+      int grp = g.e[k] >> 24;
+      if (grp != cur && cur >= 0) {
+        float d = eps + cnt;
+        a = a + ga / d;
+        r = r + q4{gr.w / d, gr.x / d, gr.y / d, gr.z / d};
+        ga = mk(0.f, 0.f, 0.f);
+        gr = q4{0.f, 0.f, 0.f, 0.f};
+        cnt = 0.f;
+      }
+      cur = grp;
+      const float* s = cslot + (g.e[k] & 0xFFFFFF) * 8;
+      ga = ga + ld3(s);
+      if (rot4) gr = gr + ld4(s + 3);
+      else gr = gr + q4{0.f, s[3], s[4], s[5]};
+      cnt += s[7];
+    }
+  }
+  if (cur >= 0) {
+    float d = eps + cnt;
+    a = a + ga / d;
+    r = r + q4{gr.w / d, gr.x / d, gr.y / d, gr.z / d};
+  }
+}
+
+// Euler.velocity_projection (integrators.py:122-146) on one body
+__device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, float h) {
+  float rn = sqrtf(q.rot.w * q.rot.w + q.rot.x * q.rot.x + q.rot.y * q.rot.y + q.rot.z * q.rot.z);
+  q4 nr{q.rot.w / rn, q.rot.x / rn, q.rot.y / rn, q.rot.z / rn};
+  q.vel = mul((q.pos - ppos) / h, B.pm);
+  q4 dq = quat_mul(nr, quat_inv(prot));
+  v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
+  float scl = dq.w >= 0.f ? 1.f : -1.f;
+  q.ang = mul(mul(scl * B.rm, a), B.rm);
+  q.rot = nr;
+}
+
+// Torque/Angle.apply_reduced for actuator a (lane) -> aslot
+__device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, const Env& E,
+                                           const float* al, int a) {
+  QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
+  v3 axes[3];
+  float ang[3];
+  int dof = axis_angle(Jc, p, cq, axes, ang);
+  v3 tq = mk(0.f, 0.f, 0.f);
+#pragma unroll
+  for (int l = 0; l < 3; l++) {
+    if (l < dof) {
+      float t;
+      if (A.type == 0) {
+        t = al[l] * A.strength * -1.f;
+        if (ang[l] < Jc.lim[2 * l]) t = 0.f;
+        if (ang[l] > Jc.lim[2 * l + 1]) t = 0.f;
+      } else {
+        float tgt = clampf(al[l] * 3.14159265358979323846f / 180.f, Jc.lim[2 * l], Jc.lim[2 * l + 1]);
+        t = (tgt - ang[l]) * A.strength;
+      }
+      tq = tq + axes[l] * t;
+    }
+  }
+  float sgp = A.type == 0 ? 1.f : -1.f;
+  st3(E.aslot + (2 * a) * 4, sgp * mul(Jc.Ip, tq));
+  st3(E.aslot + (2 * a + 1) * 4, -sgp * mul(Jc.Ic, tq));
+}
+
+template <int L>
+__device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
+                                const float* act, const Hoist& X, v3& icv, v3& ica, v3& iaa) {
+  const float h = H.h;
+  const v3 g = mk(H.gx, H.gy, H.gz);
+  float* myqp = E.qp + lane * QP_STRIDE;
+  QP q;
+  if (X.hasB) q = ldqp(myqp);
+  icv = mk(0.f, 0.f, 0.f);
+  ica = mk(0.f, 0.f, 0.f);
+  iaa = mk(0.f, 0.f, 0.f);
+  // action values of the lane's actuator (constant over the step)
+  float al[3] = {0.f, 0.f, 0.f};
+  if (X.hasA && valid) {
+#pragma unroll
+    for (int l = 0; l < 3; l++) {
+      int ai = X.A.idx[l];
+      al[l] = act[ai < 0 ? 0 : ai] * (ai >= 0 ? 1.f : 0.f);
+    }
+  }
+  for (int it = 0; it < H.substeps / 2; it++) {
+    v3 ppos = q.pos;
+    q4 prot = q.rot;
+    v3 dpa_last = mk(0.f, 0.f, 0.f);
+#pragma unroll 1
+    for (int sub = 0; sub < 2; sub++) {
+      ppos = q.pos;
+      prot = q.rot;
+      if (sub == 1 && X.hasB) {
+        st3(E.prev + lane * PREV_STRIDE, ppos);
+        st4(E.prev + lane * PREV_STRIDE + 3, prot);
+      }
+      // actuators + damping (actuator a drives joint a when H.act_same)
+      if (X.hasA) {
+        const ActC& A = X.A;
+        if (H.act_same) {
+          act_torque(X.J, A, E, al, lane);
+        } else {
+          JointC Jc = load_joint(c, H, A.joint);
+          act_torque(Jc, A, E, al, lane);
+        }
+      }
+      if (X.hasJ) {
+        const JointC& Jc = X.J;
+        v3 tq = -1.f * Jc.damping * (ld3(E.qp + Jc.bp * QP_STRIDE + 10) - ld3(E.qp + Jc.bc * QP_STRIDE + 10));
+        st3(E.jslot + (2 * lane) * 8, mul(Jc.Ip, tq));
+        st3(E.jslot + (2 * lane + 1) * 8, -1.f * mul(Jc.Ic, tq));
+      }
+      sync();
+      if (X.hasB) {
+        v3 dpa = gsum3(X.al, E.aslot, 4);
+        v3 dpj = gsum3(X.jl, E.jslot, 8);
+        v3 vel = H.vexp * q.vel;
+        vel = vel + (mk(0.f, 0.f, 0.f) + g) * h;
+        q.vel = mul(vel, X.B.pm);
+        v3 an = H.aexp * q.ang;
+        an = an + ((dpa + mk(0.f, 0.f, 0.f)) + dpj) * h;
+        q.ang = mul(an, X.B.rm);
+        q.pos = q.pos + mul(q.vel * h, X.B.pm);
+        v3 am = mul(q.ang, X.B.rm);
+        q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
+        q4 r = q.rot + quat_mul(hq, q.rot);
+        float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
+        q.rot = q4{r.w / rn, r.x / rn, r.y / rn, r.z / rn};
+        stqp(myqp, q);
+        dpa_last = dpa;
+      }
+      sync();
+      if (X.hasJ) {
+        const JointC& Jc = X.J;
+        QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
+        v3 dpp, dcp;
+        q4 dpr, dcr;
+        joint_apply(Jc, p, cq, dpp, dpr, dcp, dcr);
+        float* sp = E.jslot + (2 * lane) * 8;
+        float* sc = E.jslot + (2 * lane + 1) * 8;
+        st3(sp, dpp); st4(sp + 3, dpr);
+        st3(sc, dcp); st4(sc + 3, dcr);
+      }
+      sync();
+      if (X.hasB) {
+        v3 dp = mk(0.f, 0.f, 0.f);
+        q4 dr{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < MAXG; k++)
+          if (k < X.jl.n) {
+            const float* s = E.jslot + X.jl.e[k] * 8;
+            dp = dp + ld3(s);
+            dr = dr + ld4(s + 3);
+          }
+        q.pos = q.pos + mul(dp, X.B.pm);
+        q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
+                   q.rot.z + dr.z * X.B.qm.z};
+        if (sub == 0) vproj(q, ppos, prot, X.B, h);
+        stqp(myqp, q);
+      }
+      sync();
+    }
+    // ---- collisions (system.py:288-313)
+    v3 cpos = mk(0.f, 0.f, 0.f), cn = mk(0.f, 0.f, 0.f);
+    float pen = 0.f, dl = 0.f;
+    if (X.hasR) {
+      const RowC& R = X.R;
+      QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+      v3 cvel;
+      contact_gen(R, a, b, cpos, cvel, cn, pen);
+      const float* pa = E.prev + R.a * PREV_STRIDE;
+      const float* pb = E.prev + R.b * PREV_STRIDE;
+      v3 oap, obp;
+      q4 oar, obr;
+      dl = position_contact(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, cn, pen, oap,
+                            oar, obp, obr);
+      float* rd = E.rowd + lane * 8;
+      st3(rd, cpos); st3(rd + 3, cn); rd[6] = pen; rd[7] = dl;
+      float* sa = E.cslot + (2 * lane) * 8;
+      float* sb = E.cslot + (2 * lane + 1) * 8;
+      st3(sa, oap); st4(sa + 3, oar);
+      sa[7] = (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f;
+      st3(sb, obp); st4(sb + 3, obr);
+      sb[7] = (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f;
+    }
+    sync();
+    if (X.hasB) {
+      v3 dp;
+      q4 dr;
+      gsum_contact(X.cl, E.cslot, 1e-6f, dp, dr, true);
+      q.pos = q.pos + mul(dp, X.B.pm);
+      q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
+                 q.rot.z + dr.z * X.B.qm.z};
+      float* rb = E.rb + lane * RB_STRIDE;
+      st3(rb, q.pos); st3(rb + 3, q.vel); st3(rb + 6, q.ang);
+      vproj(q, ppos, prot, X.B, h);
+      stqp(myqp, q);
+    }
+    sync();
+    if (X.hasR) {
+      const RowC& R = X.R;
+      QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+      const float* ra = E.rb + R.a * RB_STRIDE;
+      const float* rbb = E.rb + R.b * RB_STRIDE;
+      v3 oav, oaa, obv, oba;
+      velocity_contact(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
+                       ld3(rbb + 6), cpos, cn, pen, dl, oav, oaa, obv, oba);
+      float* sa = E.cslot + (2 * lane) * 8;
+      float* sb = E.cslot + (2 * lane + 1) * 8;
+      st3(sa, oav); st3(sa + 3, oaa);
+      sa[7] = (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f;
+      st3(sb, obv); st3(sb + 3, oba);
+      sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
+    }
+    sync();
+    if (X.hasB) {
+      v3 dv;
+      q4 da;
+      gsum_contact(X.cl, E.cslot, 1e-6f, dv, da, false);
+      v3 dav = mk(da.x, da.y, da.z);
+      q.vel = mul(q.vel + dv, X.B.pm);
+      q.ang = mul(q.ang + dav, X.B.rm);
+      stqp(myqp, q);
+      icv = icv + dv;
+      ica = ica + dav;
+      iaa = iaa + dpa_last;
+    }
+    sync();
+  }
+  if (X.hasB) {
+    float* acc = E.acc + lane * ACC_STRIDE;
+    st3(acc + ACC_ICV, icv);
+    st3(acc + ACC_ICA, ica);
+    st3(acc + ACC_IAA, iaa);
+  }
+  sync();
+}
+
 // System._pbd_info contact part (system.py:327-340 -> Collider.apply): info
 // contact (vel, ang) per body into acc[ACC_ICV], acc[ACC_ICA]
 template <int L>
@@ -984,7 +1290,7 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
 
 
 
-template <int L>
+template <int L, bool S>
 __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
   extern __shared__ float smem[];
   Cst c{A.blob};
@@ -1003,7 +1309,15 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
     }
   }
   sync();
-  pbd_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr);
+  if constexpr (S) {
+    Hoist X;
+    load_hoist(c, H, lane, X);
+    v3 icv, ica, iaa;
+    pbd_step_single<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, X, icv, ica,
+                       iaa);
+  } else {
+    pbd_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr);
+  }
   if (!valid) return;
   for (int b = lane; b < H.N; b += L) {
     store_qp_global(A.qout, e, b, E.qp + b * QP_STRIDE);
@@ -1037,7 +1351,7 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
 
 
 // Env.step fused with EpisodeWrapper/AutoResetWrapper (wrappers.py:105-148)
-template <int L>
+template <int L, bool S>
 __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   extern __shared__ float smem[];
   Cst c{A.blob};
@@ -1066,6 +1380,8 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   float done = P.auto_reset ? 0.f : done_in;
   float reward_sum = 0.f;
   const int reps = P.episode_length > 0 ? (P.action_repeat > 0 ? P.action_repeat : 1) : 1;
+  Hoist X;
+  if constexpr (S) load_hoist(c, H, lane, X);
   // action sum of squares (ctrl cost), shared by every repeat
   float sq = 0.f;
   if (valid && lane == 0)
@@ -1076,7 +1392,12 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
     float msum = 0.f;
     if (kind == BX_ENV_HUMANOID) humanoid_com(c, H, E.qp, com0, msum);
     sync();
-    pbd_step<L>(c, H, E, lane, valid, act);
+    if constexpr (S) {
+      v3 icv, ica, iaa;
+      pbd_step_single<L>(c, H, E, lane, valid, act, X, icv, ica, iaa);
+    } else {
+      pbd_step<L>(c, H, E, lane, valid, act);
+    }
     env_observe<L>(c, H, E, lane, kind, P.obs_size, act, valid, valid ? A.out.obs + e * P.obs_size : nullptr);
     // reward / done / metrics (lane 0 of the env)
     if (lane == 0 && valid) {
@@ -1297,20 +1618,20 @@ __global__ void uniform_kernel(float* out, int64_t n, uint64_t seed, uint64_t of
 // ---------------------------------------------------------------------------
 namespace bx {
 
-hipError_t launch_system_step(int L, int64_t n_envs, size_t lds, hipStream_t s, const StepArgs& a) {
+hipError_t launch_system_step(int L, bool single, int64_t n_envs, size_t lds, hipStream_t s, const StepArgs& a) {
   int epb = 64 / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
-  if (L == 16) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(system_step_kernel<16>, grid, dim3(64), lds, s, a); }
-  else if (L == 32) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(system_step_kernel<32>, grid, dim3(64), lds, s, a); }
-  else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(system_step_kernel<64>, grid, dim3(64), lds, s, a); }
+  if (L == 16) { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<16, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<16, false>), grid, dim3(64), lds, s, a); } }
+  else if (L == 32) { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<32, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<32, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<32, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<32, false>), grid, dim3(64), lds, s, a); } }
+  else { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<64, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<64, false>), grid, dim3(64), lds, s, a); } }
   return hipGetLastError();
 }
-hipError_t launch_env_step(int L, int64_t n_envs, size_t lds, hipStream_t s, const EnvArgs& a) {
+hipError_t launch_env_step(int L, bool single, int64_t n_envs, size_t lds, hipStream_t s, const EnvArgs& a) {
   int epb = 64 / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
-  if (L == 16) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(env_step_kernel<16>, grid, dim3(64), lds, s, a); }
-  else if (L == 32) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(env_step_kernel<32>, grid, dim3(64), lds, s, a); }
-  else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(env_step_kernel<64>, grid, dim3(64), lds, s, a); }
+  if (L == 16) { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<16, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<16, false>), grid, dim3(64), lds, s, a); } }
+  else if (L == 32) { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<32, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<32, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<32, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<32, false>), grid, dim3(64), lds, s, a); } }
+  else { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<64, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<64, false>), grid, dim3(64), lds, s, a); } }
   return hipGetLastError();
 }
 hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a) {

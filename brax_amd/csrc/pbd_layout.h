@@ -49,7 +49,9 @@ struct BlobHdr {
   // per-env LDS layout (float offsets) and size
   int32_t l_qp, l_prev, l_rb, l_jslot, l_aslot, l_rowd, l_cslot, l_acc, l_ang, l_red;
   int32_t env_words;
-  int32_t pad1[3];
+  int32_t single;  // every lane owns <= 1 item per kind, lists <= MAXG
+  int32_t act_same; // actuator a drives joint a for every a
+  int32_t pad1;
 };
 
 }  // namespace bx

@@ -193,6 +193,11 @@ int bx_system_destroy(bx_system* sys);
 /* Lanes of a wavefront that own one env in this system's kernels (16/32/64). */
 int bx_system_lanes(bx_system* sys);
 
+/* Select the register-hoisted kernel variant (default when the system fits:
+ * every lane owns <= 1 body/joint/actuator/contact row) or the generic
+ * item-loop variant (on = 0). For testing both paths on one system. */
+int bx_system_set_single(bx_system* sys, int on);
+
 /* Physics only: B independent System.step calls (system.py:244-325).
  * act: (B, action_size) with row stride act_stride. qp_in and qp_out may not
  * alias. info may be NULL. */
