@@ -102,11 +102,11 @@ def main():
   env = envs.create('ant', batch_size=B, episode_length=1000, auto_reset=True, device=dev)
   if args.generic:
     _native.check(_native.lib().bx_system_set_single(env.sys._h, 0))
-  state = env.reset(np.array([rank, 0x5EED], np.uint32))
+  from brax_amd import distributed as bd
+  state = env.reset(bd.rank_key(np.array([0, 0x5EED], np.uint32), rank))
   acts = torch.empty((2, B, 8), dtype=torch.float32, device=dev)
   lib = _native.lib()
-  gathered = (torch.empty((world, 2, B), dtype=torch.float32, device=dev)
-              if world > 1 else None)
+  exchange = bd.EpisodeExchange(B, dev) if world > 1 else None
 
   def one_step(st, k, ev=None):
     a = acts[k & 1]
@@ -118,9 +118,8 @@ def main():
     st = env.step(st, a)
     if ev is not None:
       ev[1].record()
-    if dist is not None:
-      rd = torch.stack([st.reward, st.done])
-      dist.all_gather_into_tensor(gathered, rd)
+    if exchange is not None:
+      exchange(st.reward, st.done)  # the one RCCL collective: (reward, done) all-gather
     return st
 
   for k in range(args.warmup):

@@ -1,0 +1,60 @@
+"""World-size-2 gloo rehearsal of the multi-GPU path (no GPU needed)."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from brax_amd import distributed as bd
+
+
+def _free_port():
+  s = socket.socket()
+  s.bind(('127.0.0.1', 0))
+  p = s.getsockname()[1]
+  s.close()
+  return p
+
+
+def _worker(rank, world, port, q):
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  B = 5
+  lo, hi = bd.env_range(rank, B)
+  reward = torch.arange(lo, hi, dtype=torch.float32)
+  done = (torch.arange(lo, hi) % 2).float()
+  ex = bd.EpisodeExchange(B, 'cpu')
+  out = ex(reward, done)
+  key = bd.rank_key(np.array([3, 7], np.uint32), rank)
+  q.put((rank, out.numpy().copy(), key.tolist()))
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+def test_episode_allgather_world2():
+  world = 2
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = _free_port()
+  procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+  for p in procs:
+    p.start()
+  res = [q.get(timeout=120) for _ in range(world)]
+  for p in procs:
+    p.join(timeout=60)
+    assert p.exitcode == 0
+  res.sort()
+  expect_r = np.arange(10, dtype=np.float32).reshape(2, 5)
+  for rank, out, key in res:
+    assert out.shape == (2, 2, 5)
+    np.testing.assert_array_equal(out[:, 0], expect_r)
+    np.testing.assert_array_equal(out[:, 1], expect_r % 2)
+  assert res[0][2] != res[1][2]  # disjoint per-rank RNG keys
+
+
+def test_env_range():
+  assert bd.env_range(0, 4096) == (0, 4096)
+  assert bd.env_range(3, 4096) == (12288, 16384)
