@@ -90,6 +90,8 @@ def main():
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--generic', action='store_true',
                   help='force the generic item-loop kernel variant (A/B)')
+  ap.add_argument('--variant', default='',
+                  help='lanes,mode kernel variant (mode 0 global, 1 single, 2 lds)')
   args = ap.parse_args()
 
   dist, rank, world, local = _dist()
@@ -102,6 +104,9 @@ def main():
   env = envs.create('ant', batch_size=B, episode_length=1000, auto_reset=True, device=dev)
   if args.generic:
     _native.check(_native.lib().bx_system_set_single(env.sys._h, 0))
+  if args.variant:
+    lanes, mode = (int(x) for x in args.variant.split(','))
+    _native.check(_native.lib().bx_system_set_variant(env.sys._h, lanes, mode))
   from brax_amd import distributed as bd
   state = env.reset(bd.rank_key(np.array([0, 0x5EED], np.uint32), rank))
   acts = torch.empty((2, B, 8), dtype=torch.float32, device=dev)

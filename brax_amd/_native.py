@@ -11,7 +11,7 @@ import subprocess
 from brax_amd import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, '_lib', 'libbrax_amd.so')
+LIB_PATH = os.environ.get('BRAX_AMD_LIB') or os.path.join(HERE, '_lib', 'libbrax_amd.so')
 CSRC = os.path.join(HERE, 'csrc')
 
 
@@ -34,6 +34,7 @@ _SIGS = {
     'bx_system_destroy': ([C.c_void_p], C.c_int),
     'bx_system_lanes': ([C.c_void_p], C.c_int),
     'bx_system_set_single': ([C.c_void_p, C.c_int], C.c_int),
+    'bx_system_set_variant': ([C.c_void_p, C.c_int, C.c_int], C.c_int),
     'bx_system_step': ([C.c_void_p, C.c_int64, C.POINTER(abi.BxQP), C.c_void_p, C.c_int64,
                         C.POINTER(abi.BxQP), C.POINTER(abi.BxInfo), C.c_void_p], C.c_int),
     'bx_env_step': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64,
@@ -46,6 +47,7 @@ _SIGS = {
     'bx_env_observe': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64,
                         C.POINTER(abi.BxQP), C.c_void_p, C.c_int64, C.c_void_p,
                         C.c_void_p], C.c_int),
+    'bx_debug_stamps': ([C.POINTER(C.c_ulonglong), C.c_int], C.c_int),
     'bx_uniform': ([C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_float, C.c_float,
                     C.c_void_p], C.c_int),
 }

@@ -43,7 +43,10 @@ struct bx_system {
   BlobHdr hdr{};
   std::vector<uint32_t> host;
   uint32_t* blob = nullptr;
-  int L = 16;
+  int L = 16;       // lanes per env
+  int min_L = 16;
+  int mode = 0;     // MODE_GLOBAL / MODE_SINGLE / MODE_LDS
+  int feat = 15;    // F_SPH | F_ANGLE | F_CC | F_TW used by this system
   bool single_ok = false;
   size_t lds_env = 0;    // bytes per block for the per-env kernels
   size_t lds_reset = 0;  // bytes per block for default_qp
@@ -265,6 +268,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     }
   }
   H.total_words = (int)B.w.size();
+  H.const_words = ((r ? H.o_base : H.total_words) + 3) & ~3;
 
   // per-env LDS layout
   int L = std::max({N, J, K, R, 1});
@@ -295,6 +299,18 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
 
   S->hdr = H;
   S->single_ok = H.single != 0;
+  S->min_L = L;
+  {
+    int f = 0;
+    for (int j = 0; j < J; j++) if (d->joint_type[j] != BX_JOINT_REVOLUTE) f |= 1;
+    for (int a = 0; a < K; a++) if (d->act_type[a] != BX_ACT_TORQUE) f |= 2;
+    for (int g = 0; g < G; g++) {
+      if (d->col_fn[g] != BX_COL_CAPSULE_PLANE) f |= 4;
+      if (!d->col_oneway[g]) f |= 8;
+    }
+    S->feat = f;
+  }
+  S->mode = S->single_ok ? 1 : 0;
   S->host = std::move(B.w);
   S->L = L;
   S->lds_env = (size_t)(64 / L) * H.env_words * 4;
@@ -305,6 +321,12 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
 }
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+size_t step_lds(const bx_system* S) {
+  size_t b = (size_t)(64 / S->L) * S->hdr.env_words * 4;
+  if (S->mode == 2) b += (size_t)S->hdr.const_words * 4;
+  return b;
+}
 
 bool field_ok(const bx_field& f) { return f.ptr != nullptr; }
 bool qp_ok(const bx_qp& q) {
@@ -359,8 +381,25 @@ int bx_system_lanes(bx_system* S) { return S ? S->L : 0; }
 
 int bx_system_set_single(bx_system* S, int on) {
   if (!S) return fail("null system");
-  if (on && !S->single_ok) return fail("system does not fit the single-item-per-lane kernel");
-  S->hdr.single = on ? 1 : 0;
+  if (on && (!S->single_ok || S->L != S->min_L)) return fail("system does not fit the single-item-per-lane kernel");
+  S->mode = on ? 1 : 0;
+  return 0;
+}
+
+int bx_system_set_variant(bx_system* S, int lanes, int mode) {
+  if (!S) return fail("null system");
+  if (lanes != 16 && lanes != 32 && lanes != 64) return fail("lanes must be 16, 32 or 64");
+  if (lanes < S->min_L) return fail("lanes below the system's minimum");
+  if (mode < 0 || mode > 2) return fail("mode must be 0 (global), 1 (single) or 2 (lds)");
+  if (mode == 1 && !S->single_ok) return fail("system does not fit the single-item-per-lane kernel");
+  int old_L = S->L, old_m = S->mode;
+  S->L = lanes;
+  S->mode = mode;
+  if (step_lds(S) > 160 * 1024) {
+    S->L = old_L;
+    S->mode = old_m;
+    return fail("variant exceeds the LDS budget");
+  }
   return 0;
 }
 
@@ -378,7 +417,7 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   a.act = act;
   a.act_stride = act_stride;
   if (info) a.info = *info;
-  HIP_OK(launch_system_step(S->L, S->hdr.single != 0, n_envs, S->lds_env, as_stream(stream), a));
+  HIP_OK(launch_system_step(S->L, S->mode, S->feat, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
 }
 
@@ -401,7 +440,7 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   a.out = *out;
   a.act = act;
   a.act_stride = act_stride;
-  HIP_OK(launch_env_step(S->L, S->hdr.single != 0, n_envs, S->lds_env, as_stream(stream), a));
+  HIP_OK(launch_env_step(S->L, S->mode, S->feat, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
 }
 
@@ -447,6 +486,11 @@ int bx_system_default_qp(bx_system* S, int64_t n_envs, const float* joint_angle,
   a.vel = joint_velocity;
   a.out = *qp_out;
   HIP_OK(launch_default_qp(n_envs, S->lds_reset, as_stream(stream), a));
+  return 0;
+}
+
+int bx_debug_stamps(unsigned long long* out, int reset) {
+  HIP_OK(debug_stamps(out, reset));
   return 0;
 }
 

@@ -121,6 +121,25 @@ __device__ __forceinline__ JointC load_joint(const Cst& c, const BlobHdr& H, int
   return r;
 }
 
+// ---------------------------------------------------------------------------
+// compile-time feature mask: kernels specialised for a system only carry the
+// joint / actuator / contact kinds it uses (Ant: revolute + torque + one-way
+// capsule-plane), which keeps dead paths out of the register allocation.
+// ---------------------------------------------------------------------------
+enum { F_SPH = 1, F_ANGLE = 2, F_CC = 4, F_TW = 8, F_ALL = 15 };
+template <int F> __device__ __forceinline__ bool is_rev(int type) {
+  if constexpr ((F & F_SPH) == 0) return true; else return type == 1;
+}
+template <int F> __device__ __forceinline__ bool is_torque(int type) {
+  if constexpr ((F & F_ANGLE) == 0) return true; else return type == 0;
+}
+template <int F> __device__ __forceinline__ bool is_plane(int fn) {
+  if constexpr ((F & F_CC) == 0) return true; else return fn == 0;
+}
+template <int F> __device__ __forceinline__ bool is_oneway(int ow) {
+  if constexpr ((F & F_TW) == 0) return true; else return ow != 0;
+}
+
 // Joint.apply_angle_update (joints.py:130-152): adds rot parts into dqp/dqc
 __device__ __forceinline__ void angle_update(const JointC& J, const q4& rp, const q4& rc, v3 dq,
                                              q4& dqp, q4& dqc) {
@@ -137,6 +156,7 @@ __device__ __forceinline__ void angle_update(const JointC& J, const q4& rp, cons
 }
 
 // Revolute/Spherical.apply_reduced (joints.py:270-309, 332-386)
+template <int F>
 __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, q4& dpr,
                             v3& dcp, q4& dcr) {
   // positional constraint: apply_position_update (joints.py:154-195)
@@ -156,7 +176,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
   dcp = J.sp * (-pv / J.mc);
   dcr = J.sp * (-0.5f * vec_quat_mul(mul(J.Ic, cross(rc, pv)), c.rot));
   q4 ap{0.f, 0.f, 0.f, 0.f}, ac{0.f, 0.f, 0.f, 0.f};
-  if (J.type == 1) {
+  if (is_rev<F>(J.type)) {
     v3 axis = rotate(J.axp[0], p.rot);
     v3 ref_p = rotate(J.axp[2], p.rot);
     v3 ref_c = rotate(J.axc[2], c.rot);
@@ -204,8 +224,9 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
 }
 
 // Revolute/Spherical.axis_angle (joints.py:311-319, 388-415); returns dof
+template <int F>
 __device__ __forceinline__ int axis_angle(const JointC& J, const QP& p, const QP& c, v3* axes, float* ang) {
-  if (J.type == 1) {
+  if (is_rev<F>(J.type)) {
     axes[0] = rotate(J.axp[0], p.rot);
     v3 ref_p = rotate(J.axp[2], p.rot);
     v3 ref_c = rotate(J.axc[2], c.rot);
@@ -283,9 +304,10 @@ __device__ __forceinline__ RowC load_row(const Cst& c, const BlobHdr& H, int r) 
 }
 
 // capsule_plane (colliders.py:744-759) / capsule_capsule (:805-819)
+template <int F>
 __device__ __forceinline__ void contact_gen(const RowC& R, const QP& a, const QP& b, v3& pos, v3& vel, v3& n,
                             float& pen) {
-  if (R.fn == 0) {
+  if (is_plane<F>(R.fn)) {
     v3 e = a.pos + rotate(R.a_end, a.rot);
     n = rotate(mk(0.f, 0.f, 1.f), b.rot);
     pos = e - n * R.a_rad;
@@ -335,11 +357,12 @@ __device__ __forceinline__ void contact_gen(const RowC& R, const QP& a, const QP
 }
 
 // One/TwoWay._position_contact (colliders.py:306-377, 495-580)
+template <int F>
 __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, const QP& b, const v3& ao_pos,
                                   const q4& ao_rot, const v3& bo_pos, const q4& bo_rot, v3 cpos,
                                   v3 n, float cpen, v3& oap, q4& oar, v3& obp, q4& obr) {
   float sc = R.scale;
-  if (R.oneway) {
+  if (is_oneway<F>(R.oneway)) {
     v3 pp = cpos, pc = cpos + n * cpen;
     v3 dx = pp - pc;
     pp = pp - a.pos;
@@ -408,11 +431,12 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
 
 // One/TwoWay._velocity_contact (colliders.py:379-442, 584-658);
 // (aov, aoa, aop) = qp_right_before of body a (vel, ang, pos), same for b.
+template <int F>
 __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const QP& a, const QP& b, v3 aop,
                                  v3 aov, v3 aoa, v3 bop, v3 bov, v3 boa, v3 cpos, v3 n, float cpen,
                                  float dlam, v3& oav, v3& oaa, v3& obv, v3& oba) {
   v3 ra = cpos - a.pos, rb = cpos - b.pos;
-  v3 rv = R.oneway ? a.vel + cross(a.ang, ra)
+  v3 rv = is_oneway<F>(R.oneway) ? a.vel + cross(a.ang, ra)
                    : (a.vel + cross(a.ang, ra)) - (b.vel + cross(b.ang, rb));
   float vn = dot(rv, n);
   v3 vt = rv - n * vn;
@@ -422,7 +446,7 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
   float mag = fminf(lim, vtn);
   v3 dvel = -vtd * mag;
   v3 pdyn;
-  if (R.oneway) {
+  if (is_oneway<F>(R.oneway)) {
     v3 aw = cross(ra, vtd);
     float w = 1.f / R.ma + dot(aw, aw);
     pdyn = dvel / (w + 1e-6f);
@@ -432,7 +456,7 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
     float w2 = 1.f / R.mb + dot(a2, mul(R.Ib, a2));
     pdyn = dvel / (w1 + w2 + 1e-6f);
   }
-  v3 rvo = R.oneway ? aov + cross(aoa, cpos - aop)
+  v3 rvo = is_oneway<F>(R.oneway) ? aov + cross(aoa, cpos - aop)
                     : (aov + cross(aoa, cpos - aop)) - (bov + cross(boa, cpos - bop));
   float vno = dot(rvo, n);
   float mn = fminf(R.elas * vno, 0.f);
@@ -444,7 +468,7 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
   v3 cr1 = cross(pp, n2);
   float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
   float dlr;
-  if (R.oneway) {
+  if (is_oneway<F>(R.oneway)) {
     dlr = c / (w1 + 1e-6f);
   } else {
     v3 cr2 = cross(pc, n2);
@@ -452,11 +476,11 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
     dlr = c / (w1 + w2 + 1e-6f);
   }
   float sm = cpen > 0.f ? 1.f : 0.f;
-  float sink = R.oneway ? (vno <= -R.thr ? 1.f : 0.f) : (vno <= 0.f ? 1.f : 0.f);
+  float sink = is_oneway<F>(R.oneway) ? (vno <= -R.thr ? 1.f : 0.f) : (vno <= 0.f ? 1.f : 0.f);
   v3 pv = (dlr * n2 * sink + pdyn) * sm;
   oav = pv / R.ma;
   oaa = cross(mul(R.Ia, ra), pv);
-  if (R.oneway) {
+  if (is_oneway<F>(R.oneway)) {
     obv = mk(0.f, 0.f, 0.f);
     oba = mk(0.f, 0.f, 0.f);
   } else {
@@ -467,6 +491,7 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
 
 // One/TwoWay._contact (colliders.py:267-304, 449-493): the impulse model used
 // by System.info at reset.
+template <int F>
 __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos, v3 cvel, v3 n,
                                 float cpen, v3& oav, v3& oaa, v3& obv, v3& oba) {
   v3 rpa = cpos - a.pos, rpb = cpos - b.pos;
@@ -474,7 +499,7 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
   float nv = dot(n, cvel);
   v3 x1 = cross(mul(R.Ia, cross(rpa, n)), rpa);
   float denom;
-  if (R.oneway) {
+  if (is_oneway<F>(R.oneway)) {
     denom = 1.f / R.ma + dot(n, x1);
   } else {
     v3 x2 = cross(mul(R.Ib, cross(rpb, n)), rpb);
@@ -490,7 +515,7 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
   v3 J = imp * n, Jd = -impd * dird;
   oav = (J / R.ma) * an + (Jd / R.ma) * ad;
   oaa = mul(R.Ia, cross(rpa, J)) * an + mul(R.Ia, cross(rpa, Jd)) * ad;
-  if (R.oneway) {
+  if (is_oneway<F>(R.oneway)) {
     obv = mk(0.f, 0.f, 0.f);
     oba = mk(0.f, 0.f, 0.f);
   } else {
@@ -498,6 +523,35 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
     obv = (Jb / R.mb) * an + (Jdb / R.mb) * ad;
     oba = mul(R.Ib, cross(rpb, Jb)) * an + mul(R.Ib, cross(rpb, Jdb)) * ad;
   }
+}
+
+// Torque/Angle.apply_reduced for actuator a (lane) -> aslot
+template <int F>
+__device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, const Env& E,
+                                           const float* al, int a) {
+  QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
+  v3 axes[3];
+  float ang[3];
+  int dof = axis_angle<F>(Jc, p, cq, axes, ang);
+  v3 tq = mk(0.f, 0.f, 0.f);
+#pragma unroll
+  for (int l = 0; l < 3; l++) {
+    if (l < dof) {
+      float t;
+      if (is_torque<F>(A.type)) {
+        t = al[l] * A.strength * -1.f;
+        if (ang[l] < Jc.lim[2 * l]) t = 0.f;
+        if (ang[l] > Jc.lim[2 * l + 1]) t = 0.f;
+      } else {
+        float tgt = clampf(al[l] * 3.14159265358979323846f / 180.f, Jc.lim[2 * l], Jc.lim[2 * l + 1]);
+        t = (tgt - ang[l]) * A.strength;
+      }
+      tq = tq + axes[l] * t;
+    }
+  }
+  float sgp = is_torque<F>(A.type) ? 1.f : -1.f;
+  st3(E.aslot + (2 * a) * 4, sgp * mul(Jc.Ip, tq));
+  st3(E.aslot + (2 * a + 1) * 4, -sgp * mul(Jc.Ic, tq));
 }
 
 // ---------------------------------------------------------------------------
@@ -566,28 +620,13 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       for (int a = lane; a < K; a += L) {
         ActC A = load_act(c, H, a);
         JointC Jc = load_joint(c, H, A.joint);
-        QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), q = ldqp(E.qp + Jc.bc * QP_STRIDE);
-        v3 axes[3];
-        float ang[3];
-        int dof = axis_angle(Jc, p, q, axes, ang);
-        v3 tq = mk(0.f, 0.f, 0.f);
-        for (int l = 0; l < dof; l++) {
+        float al[3];
+#pragma unroll
+        for (int l = 0; l < 3; l++) {
           int ai = A.idx[l];
-          float al = valid ? act[ai < 0 ? 0 : ai] * (ai >= 0 ? 1.f : 0.f) : 0.f;
-          float t;
-          if (A.type == 0) {
-            t = al * A.strength * -1.f;
-            if (ang[l] < Jc.lim[2 * l]) t = 0.f;
-            if (ang[l] > Jc.lim[2 * l + 1]) t = 0.f;
-          } else {
-            float tgt = clampf(al * 3.14159265358979323846f / 180.f, Jc.lim[2 * l], Jc.lim[2 * l + 1]);
-            t = (tgt - ang[l]) * A.strength;
-          }
-          tq = tq + axes[l] * t;
+          al[l] = valid ? act[ai < 0 ? 0 : ai] * (ai >= 0 ? 1.f : 0.f) : 0.f;
         }
-        float sgp = A.type == 0 ? 1.f : -1.f;
-        st3(E.aslot + (2 * a) * 4, sgp * mul(Jc.Ip, tq));
-        st3(E.aslot + (2 * a + 1) * 4, -sgp * mul(Jc.Ic, tq));
+        act_torque<F_ALL>(Jc, A, E, al, a);
       }
       for (int j = lane; j < J; j += L) {
         int o = H.o_joint + j * JOINT_STRIDE;
@@ -633,7 +672,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), q = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
         q4 dpr, dcr;
-        joint_apply(Jc, p, q, dpp, dpr, dcp, dcr);
+        joint_apply<F_ALL>(Jc, p, q, dpp, dpr, dcp, dcr);
         float* sp = E.jslot + (2 * j) * 8;
         float* sc = E.jslot + (2 * j + 1) * 8;
         st3(sp, dpp); st4(sp + 3, dpr);
@@ -680,12 +719,12 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cpos, cvel, n;
       float pen;
-      contact_gen(R, a, b, cpos, cvel, n, pen);
+      contact_gen<F_ALL>(R, a, b, cpos, cvel, n, pen);
       const float* pa = E.prev + R.a * PREV_STRIDE;
       const float* pb = E.prev + R.b * PREV_STRIDE;
       v3 oap, obp;
       q4 oar, obr;
-      float dl = position_contact(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, n, pen,
+      float dl = position_contact<F_ALL>(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, n, pen,
                                   oap, oar, obp, obr);
       float* rd = E.rowd + r * 8;
       st3(rd, cpos); st3(rd + 3, n); rd[6] = pen; rd[7] = dl;
@@ -747,7 +786,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       const float* rbb = E.rb + R.b * RB_STRIDE;
       const float* rd = E.rowd + r * 8;
       v3 oav, oaa, obv, oba;
-      velocity_contact(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
+      velocity_contact<F_ALL>(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
                        ld3(rbb + 6), ld3(rd), ld3(rd + 3), rd[6], rd[7], oav, oaa, obv, oba);
       float* sa = E.cslot + (2 * r) * 8;
       float* sb = E.cslot + (2 * r + 1) * 8;
@@ -893,37 +932,29 @@ __device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, f
   q.rot = nr;
 }
 
-// Torque/Angle.apply_reduced for actuator a (lane) -> aslot
-__device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, const Env& E,
-                                           const float* al, int a) {
-  QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
-  v3 axes[3];
-  float ang[3];
-  int dof = axis_angle(Jc, p, cq, axes, ang);
-  v3 tq = mk(0.f, 0.f, 0.f);
-#pragma unroll
-  for (int l = 0; l < 3; l++) {
-    if (l < dof) {
-      float t;
-      if (A.type == 0) {
-        t = al[l] * A.strength * -1.f;
-        if (ang[l] < Jc.lim[2 * l]) t = 0.f;
-        if (ang[l] > Jc.lim[2 * l + 1]) t = 0.f;
-      } else {
-        float tgt = clampf(al[l] * 3.14159265358979323846f / 180.f, Jc.lim[2 * l], Jc.lim[2 * l + 1]);
-        t = (tgt - ang[l]) * A.strength;
-      }
-      tq = tq + axes[l] * t;
-    }
-  }
-  float sgp = A.type == 0 ? 1.f : -1.f;
-  st3(E.aslot + (2 * a) * 4, sgp * mul(Jc.Ip, tq));
-  st3(E.aslot + (2 * a + 1) * 4, -sgp * mul(Jc.Ic, tq));
-}
+#ifdef BX_STAMPS
+__device__ unsigned long long bx_stamp_sum[16];
+#define BX_STAMP(k)                                                                \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long _t;                                                         \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    st_acc[k] += _t - st_last;                                                     \
+    st_last = _t;                                                                  \
+  } while (0)
+#else
+#define BX_STAMP(k) do {} while (0)
+#endif
 
-template <int L>
+template <int L, int F>
 __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
                                 const float* act, const Hoist& X, v3& icv, v3& ica, v3& iaa) {
+#ifdef BX_STAMPS
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
   const float h = H.h;
   const v3 g = mk(H.gx, H.gy, H.gz);
   float* myqp = E.qp + lane * QP_STRIDE;
@@ -957,10 +988,10 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       if (X.hasA) {
         const ActC& A = X.A;
         if (H.act_same) {
-          act_torque(X.J, A, E, al, lane);
+          act_torque<F>(X.J, A, E, al, lane);
         } else {
           JointC Jc = load_joint(c, H, A.joint);
-          act_torque(Jc, A, E, al, lane);
+          act_torque<F>(Jc, A, E, al, lane);
         }
       }
       if (X.hasJ) {
@@ -970,6 +1001,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         st3(E.jslot + (2 * lane + 1) * 8, -1.f * mul(Jc.Ic, tq));
       }
       sync();
+      BX_STAMP(0);
       if (X.hasB) {
         v3 dpa = gsum3(X.al, E.aslot, 4);
         v3 dpj = gsum3(X.jl, E.jslot, 8);
@@ -989,18 +1021,20 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         dpa_last = dpa;
       }
       sync();
+      BX_STAMP(1);
       if (X.hasJ) {
         const JointC& Jc = X.J;
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
         q4 dpr, dcr;
-        joint_apply(Jc, p, cq, dpp, dpr, dcp, dcr);
+        joint_apply<F>(Jc, p, cq, dpp, dpr, dcp, dcr);
         float* sp = E.jslot + (2 * lane) * 8;
         float* sc = E.jslot + (2 * lane + 1) * 8;
         st3(sp, dpp); st4(sp + 3, dpr);
         st3(sc, dcp); st4(sc + 3, dcr);
       }
       sync();
+      BX_STAMP(2);
       if (X.hasB) {
         v3 dp = mk(0.f, 0.f, 0.f);
         q4 dr{0.f, 0.f, 0.f, 0.f};
@@ -1018,6 +1052,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         stqp(myqp, q);
       }
       sync();
+      BX_STAMP(3);
     }
     // ---- collisions (system.py:288-313)
     v3 cpos = mk(0.f, 0.f, 0.f), cn = mk(0.f, 0.f, 0.f);
@@ -1026,12 +1061,12 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       const RowC& R = X.R;
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cvel;
-      contact_gen(R, a, b, cpos, cvel, cn, pen);
+      contact_gen<F>(R, a, b, cpos, cvel, cn, pen);
       const float* pa = E.prev + R.a * PREV_STRIDE;
       const float* pb = E.prev + R.b * PREV_STRIDE;
       v3 oap, obp;
       q4 oar, obr;
-      dl = position_contact(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, cn, pen, oap,
+      dl = position_contact<F>(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, cn, pen, oap,
                             oar, obp, obr);
       float* rd = E.rowd + lane * 8;
       st3(rd, cpos); st3(rd + 3, cn); rd[6] = pen; rd[7] = dl;
@@ -1043,6 +1078,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       sb[7] = (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f;
     }
     sync();
+    BX_STAMP(4);
     if (X.hasB) {
       v3 dp;
       q4 dr;
@@ -1056,13 +1092,14 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       stqp(myqp, q);
     }
     sync();
+    BX_STAMP(5);
     if (X.hasR) {
       const RowC& R = X.R;
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       const float* ra = E.rb + R.a * RB_STRIDE;
       const float* rbb = E.rb + R.b * RB_STRIDE;
       v3 oav, oaa, obv, oba;
-      velocity_contact(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
+      velocity_contact<F>(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
                        ld3(rbb + 6), cpos, cn, pen, dl, oav, oaa, obv, oba);
       float* sa = E.cslot + (2 * lane) * 8;
       float* sb = E.cslot + (2 * lane + 1) * 8;
@@ -1072,6 +1109,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
     }
     sync();
+    BX_STAMP(6);
     if (X.hasB) {
       v3 dv;
       q4 da;
@@ -1085,6 +1123,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       iaa = iaa + dpa_last;
     }
     sync();
+    BX_STAMP(7);
   }
   if (X.hasB) {
     float* acc = E.acc + lane * ACC_STRIDE;
@@ -1093,6 +1132,14 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     st3(acc + ACC_IAA, iaa);
   }
   sync();
+  BX_STAMP(9);
+#ifdef BX_STAMPS
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) atomicAdd(&bx_stamp_sum[k], st_acc[k]);
+    atomicAdd(&bx_stamp_sum[15], 1ull);
+  }
+#endif
 }
 
 // System._pbd_info contact part (system.py:327-340 -> Collider.apply): info
@@ -1105,9 +1152,9 @@ __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane)
     QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
     v3 cpos, cvel, n;
     float pen;
-    contact_gen(R, a, b, cpos, cvel, n, pen);
+    contact_gen<F_ALL>(R, a, b, cpos, cvel, n, pen);
     v3 oav, oaa, obv, oba;
-    impulse_contact(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
+    impulse_contact<F_ALL>(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
     float* sa = E.cslot + (2 * r) * 8;
     float* sb = E.cslot + (2 * r + 1) * 8;
     st3(sa, oav); st3(sa + 3, oaa);
@@ -1152,11 +1199,14 @@ __device__ void joint_angles(const Cst& c, const BlobHdr& H, const Env& E, int l
     QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), q = ldqp(E.qp + Jc.bc * QP_STRIDE);
     v3 axes[3];
     float ang[3];
-    axis_angle(Jc, p, q, axes, ang);
+    axis_angle<F_ALL>(Jc, p, q, axes, ang);
     v3 dv = p.ang - q.ang;
-    for (int l = 0; l < Jc.n_angles; l++) {
-      E.ang[Jc.angle_off + l] = ang[l];
-      E.ang[H.D + Jc.angle_off + l] = dot(dv, axes[l]);
+#pragma unroll
+    for (int l = 0; l < 3; l++) {
+      if (l < Jc.n_angles) {
+        E.ang[Jc.angle_off + l] = ang[l];
+        E.ang[H.D + Jc.angle_off + l] = dot(dv, axes[l]);
+      }
     }
   }
 }
@@ -1290,16 +1340,39 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
 
 
 
-template <int L, bool S>
+// kernel variants: MODE_GLOBAL (constants read from the HBM blob inside the
+// loops), MODE_SINGLE (constants hoisted to registers), MODE_LDS (the blob's
+// constant part copied to LDS once per workgroup, read there inside the loops)
+enum { MODE_GLOBAL = 0, MODE_SINGLE = 1, MODE_LDS = 2 };
+
+// copies the constant blob into LDS (MODE_LDS); returns the env-area base
+template <int MODE>
+__device__ __forceinline__ float* stage_constants(const uint32_t* blob, const BlobHdr& H,
+                                                  float* smem, Cst& c) {
+  if constexpr (MODE == MODE_LDS) {
+    uint32_t* cl = reinterpret_cast<uint32_t*>(smem);
+    for (int i = threadIdx.x; i < H.const_words; i += 64) cl[i] = blob[i];
+    __syncthreads();
+    c.w = cl;
+    return smem + H.const_words;
+  } else {
+    c.w = blob;
+    return smem;
+  }
+}
+
+template <int L, int MODE, int F>
 __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
   extern __shared__ float smem[];
-  Cst c{A.blob};
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
+  Cst c{A.blob};
+  float* ebase = stage_constants<MODE>(A.blob, H, smem, c);
+  constexpr bool S = MODE == MODE_SINGLE;
   const int lane = threadIdx.x % L;
   const int le = threadIdx.x / L;
   const int64_t e = (int64_t)blockIdx.x * (64 / L) + le;
   const bool valid = e < A.n_envs;
-  Env E = carve(smem + le * H.env_words, H);
+  Env E = carve(ebase + le * H.env_words, H);
   for (int b = lane; b < H.N; b += L) {
     if (valid) {
       load_qp_global(A.qin, e, b, E.qp + b * QP_STRIDE);
@@ -1313,7 +1386,7 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
     Hoist X;
     load_hoist(c, H, lane, X);
     v3 icv, ica, iaa;
-    pbd_step_single<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, X, icv, ica,
+    pbd_step_single<L, F>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, X, icv, ica,
                        iaa);
   } else {
     pbd_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr);
@@ -1351,16 +1424,18 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
 
 
 // Env.step fused with EpisodeWrapper/AutoResetWrapper (wrappers.py:105-148)
-template <int L, bool S>
+template <int L, int MODE, int F>
 __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   extern __shared__ float smem[];
-  Cst c{A.blob};
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
+  Cst c{A.blob};
+  float* ebase = stage_constants<MODE>(A.blob, H, smem, c);
+  constexpr bool S = MODE == MODE_SINGLE;
   const int lane = threadIdx.x % L;
   const int le = threadIdx.x / L;
   const int64_t e = (int64_t)blockIdx.x * (64 / L) + le;
   const bool valid = e < A.n_envs;
-  Env E = carve(smem + le * H.env_words, H);
+  Env E = carve(ebase + le * H.env_words, H);
   const bx_env_params& P = A.P;
   const int kind = P.kind;
   const float* act = valid ? A.act + e * A.act_stride : nullptr;
@@ -1394,7 +1469,7 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
     sync();
     if constexpr (S) {
       v3 icv, ica, iaa;
-      pbd_step_single<L>(c, H, E, lane, valid, act, X, icv, ica, iaa);
+      pbd_step_single<L, F>(c, H, E, lane, valid, act, X, icv, ica, iaa);
     } else {
       pbd_step<L>(c, H, E, lane, valid, act);
     }
@@ -1618,20 +1693,48 @@ __global__ void uniform_kernel(float* out, int64_t n, uint64_t seed, uint64_t of
 // ---------------------------------------------------------------------------
 namespace bx {
 
-hipError_t launch_system_step(int L, bool single, int64_t n_envs, size_t lds, hipStream_t s, const StepArgs& a) {
+template <typename Args>
+static void launch_one(void (*k)(Args), dim3 grid, size_t lds, hipStream_t s, const Args& a) {
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k, grid, dim3(64), lds, s, a);
+}
+
+// instantiated variants: (lanes, mode, features). Single mode at 16 lanes is
+// specialised per feature set; everything else carries all features.
+#define BX_DISPATCH(KERNEL, ARGS)                                                   \
+  if (mode == 1 && L == 16) {                                                       \
+    switch (feat) {                                                                 \
+      case 0: launch_one<ARGS>(KERNEL<16, 1, 0>, grid, lds, s, a); break;           \
+      case F_SPH: launch_one<ARGS>(KERNEL<16, 1, F_SPH>, grid, lds, s, a); break;   \
+      case F_CC | F_TW: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW>, grid, lds, s, a); break; \
+      default: launch_one<ARGS>(KERNEL<16, 1, F_ALL>, grid, lds, s, a); break;      \
+    }                                                                               \
+  } else {                                                                          \
+    switch (L * 4 + mode) {                                                         \
+      case 16 * 4 + 0: launch_one<ARGS>(KERNEL<16, 0, F_ALL>, grid, lds, s, a); break; \
+      case 16 * 4 + 2: launch_one<ARGS>(KERNEL<16, 2, F_ALL>, grid, lds, s, a); break; \
+      case 32 * 4 + 0: launch_one<ARGS>(KERNEL<32, 0, F_ALL>, grid, lds, s, a); break; \
+      case 32 * 4 + 1: launch_one<ARGS>(KERNEL<32, 1, F_ALL>, grid, lds, s, a); break; \
+      case 32 * 4 + 2: launch_one<ARGS>(KERNEL<32, 2, F_ALL>, grid, lds, s, a); break; \
+      case 64 * 4 + 0: launch_one<ARGS>(KERNEL<64, 0, F_ALL>, grid, lds, s, a); break; \
+      case 64 * 4 + 1: launch_one<ARGS>(KERNEL<64, 1, F_ALL>, grid, lds, s, a); break; \
+      case 64 * 4 + 2: launch_one<ARGS>(KERNEL<64, 2, F_ALL>, grid, lds, s, a); break; \
+      default: return hipErrorInvalidValue;                                         \
+    }                                                                               \
+  }
+
+hipError_t launch_system_step(int L, int mode, int feat, int64_t n_envs, size_t lds, hipStream_t s,
+                              const StepArgs& a) {
   int epb = 64 / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
-  if (L == 16) { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<16, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<16, false>), grid, dim3(64), lds, s, a); } }
-  else if (L == 32) { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<32, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<32, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<32, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<32, false>), grid, dim3(64), lds, s, a); } }
-  else { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<64, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)system_step_kernel<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(system_step_kernel<64, false>), grid, dim3(64), lds, s, a); } }
+  BX_DISPATCH(system_step_kernel, StepArgs)
   return hipGetLastError();
 }
-hipError_t launch_env_step(int L, bool single, int64_t n_envs, size_t lds, hipStream_t s, const EnvArgs& a) {
+hipError_t launch_env_step(int L, int mode, int feat, int64_t n_envs, size_t lds, hipStream_t s,
+                           const EnvArgs& a) {
   int epb = 64 / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
-  if (L == 16) { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<16, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<16, false>), grid, dim3(64), lds, s, a); } }
-  else if (L == 32) { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<32, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<32, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<32, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<32, false>), grid, dim3(64), lds, s, a); } }
-  else { if (single) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<64, true>), grid, dim3(64), lds, s, a); } else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)env_step_kernel<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(HIP_KERNEL_NAME(env_step_kernel<64, false>), grid, dim3(64), lds, s, a); } }
+  BX_DISPATCH(env_step_kernel, EnvArgs)
   return hipGetLastError();
 }
 hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a) {
@@ -1653,6 +1756,21 @@ hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
   dim3 grid((unsigned)((n + 255) / 256));
   hipLaunchKernelGGL(uniform_kernel, grid, dim3(256), 0, s, out, n, seed, offset, lo, hi);
   return hipGetLastError();
+}
+
+hipError_t debug_stamps(unsigned long long* out, int reset) {
+#ifdef BX_STAMPS
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(bx_stamp_sum), 16 * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    unsigned long long z[16] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(bx_stamp_sum), z, sizeof(z));
+  }
+  return e;
+#else
+  (void)out;
+  (void)reset;
+  return hipErrorNotSupported;
+#endif
 }
 
 }  // namespace bx

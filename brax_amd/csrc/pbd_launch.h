@@ -41,11 +41,13 @@ struct ResetArgs {
   bx_qp out;
 };
 
-hipError_t launch_system_step(int L, bool single, int64_t n_envs, size_t lds, hipStream_t s, const StepArgs& a);
-hipError_t launch_env_step(int L, bool single, int64_t n_envs, size_t lds, hipStream_t s, const EnvArgs& a);
+hipError_t launch_system_step(int L, int mode, int feat, int64_t n_envs, size_t lds, hipStream_t s, const StepArgs& a);
+hipError_t launch_env_step(int L, int mode, int feat, int64_t n_envs, size_t lds, hipStream_t s, const EnvArgs& a);
 hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a);
 hipError_t launch_default_qp(int64_t n_envs, size_t lds, hipStream_t s, const ResetArgs& a);
 hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset, float lo, float hi,
                           hipStream_t s);
+
+hipError_t debug_stamps(unsigned long long* out, int reset);
 
 }  // namespace bx

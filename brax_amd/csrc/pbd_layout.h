@@ -51,7 +51,8 @@ struct BlobHdr {
   int32_t env_words;
   int32_t single;  // every lane owns <= 1 item per kind, lists <= MAXG
   int32_t act_same; // actuator a drives joint a for every a
-  int32_t pad1;
+  int32_t const_words;  // words [0, const_words) = everything the step kernels read
+  int32_t pad2;
 };
 
 }  // namespace bx

@@ -198,6 +198,11 @@ int bx_system_lanes(bx_system* sys);
  * item-loop variant (on = 0). For testing both paths on one system. */
 int bx_system_set_single(bx_system* sys, int on);
 
+/* Kernel variant: lanes per env (16/32/64, >= the system's minimum) and
+ * constant placement (0: read from HBM in the loops, 1: hoisted to registers,
+ * needs <= 1 item per lane, 2: staged in LDS once per workgroup). */
+int bx_system_set_variant(bx_system* sys, int lanes, int mode);
+
 /* Physics only: B independent System.step calls (system.py:244-325).
  * act: (B, action_size) with row stride act_stride. qp_in and qp_out may not
  * alias. info may be NULL. */
@@ -232,6 +237,10 @@ int bx_env_observe(bx_system* sys, const bx_env_params* env, int64_t n_envs,
  * unpinned). */
 int bx_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
                float lo, float hi, void* stream);
+
+/* Diagnostic builds only (-DBX_STAMPS): per-phase s_memtime cycle sums of the
+ * single-mode step, [0..9] phases, [15] samples. Fails on product builds. */
+int bx_debug_stamps(unsigned long long* out16, int reset);
 
 /* Multi-rank episodic exchange is done over RCCL by the host (torch.distributed);
  * no collective lives in this library. */

@@ -3,13 +3,17 @@ restatement. Needs an MI355X.
 
 Parity gate, per env and field, normwise
     max|Δ| <= tol * max(1, max|x|)   against the reference's float64 states:
-  every field:             tol = max(1e-5, 3 * E32)
+  every field:             tol = max(1e-5, 2 * E32)
   Ant (the north-star config) pos/rot additionally <= 1e-5 flat
-where E32 is the largest normwise error of Brax's algorithm executed in fp32
-(the oracle's float32 build) over the same batch — i.e. the HIP kernel must
-be as accurate as Brax's own fp32 execution, within 3x. Velocities are
-(pos - pos_prev)/h, so fp32 rounding is amplified ~1/h per substep; a flat
-1e-5 is not reachable for them by Brax itself.
+E32 is the fp32 error envelope of Brax's OWN algorithm on the same sample:
+the largest normwise error, vs the float64 reference, of the oracle's float32
+build (the reference algorithm executed in true fp32) over the exact inputs
+and three copies perturbed by fp32-ulp relative noise (x * (1 + U[-6e-8,6e-8]),
+SURVEY §8(c)'s conditioning probe). The HIP kernel must be as close to the
+reference as fp32 rounding noise itself allows, within 2x. Velocities are
+(pos - pos_prev)/h, so fp32 rounding is amplified ~1/h per substep, and the
+contact masks (`penetration > 0`, `c < 0`, static-friction and sinking gates)
+flip on rounding; a flat 1e-5 is not reachable for those by Brax itself.
 """
 import numpy as np
 import pytest
@@ -48,51 +52,72 @@ def _to_qp(a, dev):
 
 def _gate(got, ref, e32, field):
   nw = normwise(got, ref)
-  tol = max(POS_TOL, 3.0 * float(np.max(e32)))
+  tol = max(POS_TOL, 2.0 * float(np.max(e32)))
   assert np.all(np.isfinite(got)), field
   assert nw.max() <= tol, f'{field}: normwise {nw.max():.3e} > tol {tol:.3e}'
   return nw.max(), tol
 
 
-def _e32(oracle_lib, name, qp, act):
-  vc, d, rd, meta = compiled(name)
-  o32 = oracle_lib.Oracle(d, rd, np.float32, safe_guard=True)
-  return o32
+class Envelope:
+  """Brax's algorithm in fp32 (oracle float32 build) on the exact inputs and
+  on 3 ulp-perturbed copies; `err(key, ref)` is the max normwise error."""
+
+  def __init__(self, oracle_lib, name, n_perturb=3):
+    vc, d, rd, meta = compiled(name)
+    self.o = oracle_lib.Oracle(d, rd, np.float32, safe_guard=True)
+    self.n = n_perturb
+
+  def _inputs(self, qp):
+    yield qp.astype(np.float32)
+    rng = np.random.default_rng(1234)
+    for _ in range(self.n):
+      noise = 1 + rng.uniform(-6e-8, 6e-8, qp.shape)
+      yield (qp * noise).astype(np.float32)
+
+  def system(self, qp, act):
+    outs = [self.o.system_step(q, act.astype(np.float32)) for q in self._inputs(qp)]
+    return outs
+
+  def env(self, name, qp, act, O, M):
+    return [self.o.env_step(name, q, act.astype(np.float32), O, M) for q in self._inputs(qp)]
+
+
+def _env_err(vals, ref):
+  return np.max([normwise(v, ref) for v in vals], axis=0)
 
 
 @pytest.mark.parametrize('name', ENV_TRAJ + SYS_TRAJ)
 def test_system_step_vs_golden(dev, oracle_lib, name):
   sys_ = _system(name, dev)
   T = golden('traj_' + name)
-  vc, d, rd, meta = compiled(name)
-  o32 = oracle_lib.Oracle(d, rd, np.float32, safe_guard=True)
+  env32 = Envelope(oracle_lib, name)
   for t in range(T['action'].shape[0]):
     qp_in = _to_qp(T['qp'][t], dev)
     act = torch.as_tensor(T['action'][t], dtype=torch.float32, device=dev)
     out, info = sys_.step(qp_in, act)
     got = _qp_np(out)
     ref = T['qp'][t + 1]
-    c32, i32 = o32.system_step(T['qp'][t].astype(np.float32), T['action'][t].astype(np.float32))
+    outs = env32.system(T['qp'][t], T['action'][t])
     for f, sl in QP_FIELDS.items():
-      e32 = normwise(c32[..., sl], ref[..., sl])
+      e32 = _env_err([o[0][..., sl] for o in outs], ref[..., sl])
       _gate(got[..., sl], ref[..., sl], e32, f)
       if name == 'ant' and f in ('pos', 'rot'):
         assert normwise(got[..., sl], ref[..., sl]).max() <= POS_TOL, f
     ic = torch.cat([info.contact.vel, info.contact.ang], -1).cpu().numpy()
-    e32 = normwise(i32['contact'], T['info_contact'][t])
-    _gate(ic, T['info_contact'][t], e32, 'info_contact')
+    _gate(ic, T['info_contact'][t], _env_err([o[1]['contact'] for o in outs],
+                                              T['info_contact'][t]), 'info_contact')
     pen = info.contact_penetration.cpu().numpy()
     _gate(pen, T['contact_penetration'][t],
-          normwise(i32['contact_penetration'], T['contact_penetration'][t]), 'pen')
+          _env_err([o[1]['contact_penetration'] for o in outs], T['contact_penetration'][t]),
+          'pen')
 
 
 @pytest.mark.parametrize('name', ENV_TRAJ)
 def test_env_step_vs_golden(dev, oracle_lib, name):
   from brax_amd import envs
-  env = envs.get_environment(name, device=dev) if name != 'ant' else envs.get_environment('ant', device=dev)
+  env = envs.get_environment(name, device=dev)
   T = golden('traj_' + name)
-  vc, d, rd, meta = compiled(name)
-  o32 = oracle_lib.Oracle(d, rd, np.float32, safe_guard=True)
+  env32 = Envelope(oracle_lib, name)
   O, M = T['obs'].shape[-1], T['metrics'].shape[-1]
   assert env.observation_size == O
   from brax_amd.envs.env import State
@@ -102,14 +127,14 @@ def test_env_step_vs_golden(dev, oracle_lib, name):
                reward=torch.zeros(B, device=dev), done=torch.zeros(B, device=dev))
     act = torch.as_tensor(T['action'][t], dtype=torch.float32, device=dev)
     nst = env.step(st, act)
-    _, obs32, rew32, done32, met32 = o32.env_step(name, T['qp'][t].astype(np.float32),
-                                                  T['action'][t].astype(np.float32), O, M)
-    _gate(nst.obs.cpu().numpy(), T['obs'][t + 1], normwise(obs32, T['obs'][t + 1]), 'obs')
+    outs = env32.env(name, T['qp'][t], T['action'][t], O, M)
+    _gate(nst.obs.cpu().numpy(), T['obs'][t + 1], _env_err([o[1] for o in outs], T['obs'][t + 1]),
+          'obs')
     _gate(nst.reward.cpu().numpy()[:, None], T['reward'][t][:, None],
-          normwise(rew32[:, None], T['reward'][t][:, None]), 'reward')
+          _env_err([o[2][:, None] for o in outs], T['reward'][t][:, None]), 'reward')
     assert np.array_equal(nst.done.cpu().numpy(), T['done'][t])
     met = np.stack([nst.metrics[k].cpu().numpy() for k in env.metric_keys], -1)
-    _gate(met, T['metrics'][t], normwise(met32, T['metrics'][t]), 'metrics')
+    _gate(met, T['metrics'][t], _env_err([o[4] for o in outs], T['metrics'][t]), 'metrics')
 
 
 @pytest.mark.parametrize('name', ENV_TRAJ)
@@ -195,15 +220,15 @@ def test_full_batch_properties(dev, oracle_lib):
   # parity vs the fp64 oracle on 256 sampled envs
   vc, d, rd, meta = compiled('ant')
   o64 = oracle_lib.Oracle(d, rd, np.float64, safe_guard=True)
-  o32 = oracle_lib.Oracle(d, rd, np.float32, safe_guard=True)
+  env32 = Envelope(oracle_lib, 'ant')
   idx = np.random.default_rng(0).choice(B, 256, replace=False)
   qp_in = st.qp.numpy()[idx]
   an = act.cpu().numpy()[idx].astype(np.float64)
   ref, _ = o64.system_step(qp_in, an)
-  c32, _ = o32.system_step(qp_in.astype(np.float32), an.astype(np.float32))
+  outs = env32.system(qp_in, an)
   got = a.qp.numpy()[idx]
   for f, sl in QP_FIELDS.items():
-    _gate(got[..., sl], ref[..., sl], normwise(c32[..., sl], ref[..., sl]), f)
+    _gate(got[..., sl], ref[..., sl], _env_err([o[0][..., sl] for o in outs], ref[..., sl]), f)
 
 
 def test_strided_views_match_packed(dev):
