@@ -72,6 +72,46 @@ def cpu_baseline(batch, min_seconds=10.0, max_steps=200):
                     f'{platform.processor() or platform.machine()}'}
 
 
+def phase_bench(sys_, dev, batch=1 << 20, reps=20):
+  """The integrator and collider phases as standalone SoA kernels
+  (brax_amd.phases) over `batch` envs: algorithmic GB/s vs the HBM peak,
+  timed with HIP events on the launch stream."""
+  from brax_amd import phases
+  from brax_amd.base import QP
+  N = sys_.num_bodies
+  g = torch.Generator(device=dev).manual_seed(0)
+  soa = torch.rand((13, N, batch), device=dev, generator=g) - 0.5
+  soa[3:7] += 1.0  # quaternion planes away from zero norm
+  aux = torch.rand((13, N, batch), device=dev, generator=g) - 0.5
+  aux[3:7] += 1.0
+  out = soa.clone()
+  contacts = torch.empty((10, sys_.num_contacts, batch), device=dev)
+  runs = {
+      'kinetic': (lambda: phases.kinetic(sys_, soa, out), phases.BYTES[0] * N),
+      'update_acc': (lambda: phases.update_acc(sys_, soa, aux[:6], out), phases.BYTES[1] * N),
+      'velocity_projection': (lambda: phases.velocity_projection(sys_, soa, aux, out),
+                              phases.BYTES[2] * N),
+      'capsule_plane': (lambda: phases.capsule_plane(sys_, soa, contacts),
+                        phases.BYTES['capsule_plane'] * sys_.num_contacts),
+  }
+  res = {}
+  for name, (fn, per_env) in runs.items():
+    for _ in range(3):
+      fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+      fn()
+    b.record()
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) * 1e3 / reps
+    gbs = per_env * batch / (us * 1e-6) / 1e9
+    res[name] = {'us': us, 'bytes_per_launch': per_env * batch, 'achieved': gbs,
+                 'frac': gbs / HBM_PEAK_GBS}
+  del soa, aux, out, contacts
+  return {'envs': batch, 'unit': 'GB/s', 'peak': HBM_PEAK_GBS, 'kernels': res}
+
+
 def _traffic():
   """HBM bytes per launch from the committed PMC profile, if present."""
   p = os.path.join(ROOT, 'profiles', 'traffic.json')
@@ -88,6 +128,9 @@ def main():
   ap.add_argument('--warmup', type=int, default=50)
   ap.add_argument('--batch', type=int, default=4096)
   ap.add_argument('--no-cpu-baseline', action='store_true')
+  ap.add_argument('--no-phases', action='store_true',
+                  help='skip the standalone SoA phase-kernel roofline leg')
+  ap.add_argument('--phase-envs', type=int, default=1 << 20)
   ap.add_argument('--generic', action='store_true',
                   help='force the generic item-loop kernel variant (A/B)')
   ap.add_argument('--variant', default='',
@@ -109,18 +152,19 @@ def main():
     _native.check(_native.lib().bx_system_set_variant(env.sys._h, lanes, mode))
   from brax_amd import distributed as bd
   state = env.reset(bd.rank_key(np.array([0, 0x5EED], np.uint32), rank))
-  acts = torch.empty((2, B, 8), dtype=torch.float32, device=dev)
+  # synthetic U[-1,1] actions, one (B, 8) slab per step, drawn on the device by
+  # the counter RNG before the timed region (inputs resident in HBM)
+  n_act = args.warmup + args.steps
+  acts = torch.empty((n_act, B, 8), dtype=torch.float32, device=dev)
   lib = _native.lib()
+  _native.check(lib.bx_uniform(C.c_void_p(acts.data_ptr()), acts.numel(), 1 + rank, 0, -1.0,
+                               1.0, C.c_void_p(torch.cuda.current_stream().cuda_stream)))
   exchange = bd.EpisodeExchange(B, dev) if world > 1 else None
 
   def one_step(st, k, ev=None):
-    a = acts[k & 1]
-    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    _native.check(lib.bx_uniform(C.c_void_p(a.data_ptr()), a.numel(), 1 + rank,
-                                 k * a.numel(), -1.0, 1.0, stream))
     if ev is not None:
       ev[0].record()
-    st = env.step(st, a)
+    st = env.step(st, acts[k])
     if ev is not None:
       ev[1].record()
     if exchange is not None:
@@ -172,8 +216,8 @@ def main():
       'scaling': 'weak',
       'vs_baseline': None,
       'dtype': 'f32',
-      'data': 'synthetic: U[-1,1] actions drawn on device each step; reset from the '
-              'Ant config with device-RNG joint noise',
+      'data': 'synthetic: U[-1,1] actions (device counter RNG, one slab per step, '
+              'resident in HBM); reset from the Ant config with device-RNG joint noise',
       'config': {'workload': 'Ant-v1 Env.step (10 PBD substeps + obs/reward + '
                              'Episode/AutoReset), envs.create(ant)',
                  'envs_per_gpu': B, 'episode_length': 1000, 'substeps': 10,
@@ -188,6 +232,8 @@ def main():
                    'valu_tflops': ANT_FLOPS_PER_ENV_STEP * B / (kern_ms * 1e-3) / 1e12,
                    'valu_peak_tflops': FP32_VALU_PEAK_TFLOPS},
   }
+  out['phase_roofline'] = (None if args.no_phases else
+                           phase_bench(env.unwrapped.sys, dev, args.phase_envs))
   if world == 1 and not args.no_cpu_baseline:
     out['cpu_baseline'] = cpu_baseline(B)
   else:

@@ -47,6 +47,10 @@ _SIGS = {
     'bx_env_observe': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64,
                         C.POINTER(abi.BxQP), C.c_void_p, C.c_int64, C.c_void_p,
                         C.c_void_p], C.c_int),
+    'bx_phase': ([C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                  C.c_void_p, C.c_int64, C.c_void_p], C.c_int),
+    'bx_phase_capsule_plane': ([C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                                C.c_int64, C.c_void_p], C.c_int),
     'bx_debug_stamps': ([C.POINTER(C.c_ulonglong), C.c_int], C.c_int),
     'bx_uniform': ([C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_float, C.c_float,
                     C.c_void_p], C.c_int),

@@ -47,6 +47,7 @@ struct bx_system {
   int min_L = 16;
   int mode = 0;     // MODE_GLOBAL / MODE_SINGLE / MODE_LDS
   int feat = 15;    // F_SPH | F_ANGLE | F_CC | F_TW used by this system
+  int gw = 8;       // gather width (max per-body list length, 4 or 8)
   bool single_ok = false;
   size_t lds_env = 0;    // bytes per block for the per-env kernels
   size_t lds_reset = 0;  // bytes per block for default_qp
@@ -279,18 +280,26 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.l_qp = carve(N * QP_STRIDE);
   H.l_prev = carve(N * PREV_STRIDE);
   H.l_rb = carve(N * RB_STRIDE);
-  H.l_jslot = carve(J * 16);
-  H.l_aslot = carve(K * 8);
+  // slot regions end with one zero slot (padding target of the gather lists)
+  H.l_jslot = carve((2 * J + 1) * 8);
+  H.l_aslot = carve((2 * K + 1) * 4);
   H.l_rowd = carve(R * 8);
-  H.l_cslot = carve(R * 16);
+  H.l_cslot = carve((2 * R + 1) * 8);
   H.l_acc = carve(N * ACC_STRIDE);
   H.l_ang = carve(2 * D);
   H.l_red = carve(64);
   H.env_words = off;
+  size_t mx = 0;
   {
-    size_t mx = 0;
-    for (int b = 0; b < N; b++) mx = std::max({mx, jl[b].size(), al[b].size(), cl[b].size()});
-    H.single = (N <= L && J <= L && K <= L && R <= L && mx <= 8) ? 1 : 0;
+    int max_groups = 0;
+    for (int b = 0; b < N; b++) {
+      mx = std::max({mx, jl[b].size(), al[b].size(), cl[b].size()});
+      std::vector<int> gs;
+      for (int v : cl[b])
+        if (std::find(gs.begin(), gs.end(), v >> 24) == gs.end()) gs.push_back(v >> 24);
+      max_groups = std::max(max_groups, (int)gs.size());
+    }
+    H.single = (N <= L && J <= L && K <= L && R <= L && mx <= 8 && max_groups <= 2) ? 1 : 0;
     H.act_same = 1;
     for (int a = 0; a < K; a++)
       if (d->act_joint[a] != a) H.act_same = 0;
@@ -300,6 +309,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   S->hdr = H;
   S->single_ok = H.single != 0;
   S->min_L = L;
+  S->gw = mx <= 4 ? 4 : 8;
   {
     int f = 0;
     for (int j = 0; j < J; j++) if (d->joint_type[j] != BX_JOINT_REVOLUTE) f |= 1;
@@ -417,7 +427,7 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   a.act = act;
   a.act_stride = act_stride;
   if (info) a.info = *info;
-  HIP_OK(launch_system_step(S->L, S->mode, S->feat, n_envs, step_lds(S), as_stream(stream), a));
+  HIP_OK(launch_system_step(S->L, S->mode, S->feat, S->gw, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
 }
 
@@ -440,7 +450,7 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   a.out = *out;
   a.act = act;
   a.act_stride = act_stride;
-  HIP_OK(launch_env_step(S->L, S->mode, S->feat, n_envs, step_lds(S), as_stream(stream), a));
+  HIP_OK(launch_env_step(S->L, S->mode, S->feat, S->gw, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
 }
 
@@ -486,6 +496,35 @@ int bx_system_default_qp(bx_system* S, int64_t n_envs, const float* joint_angle,
   a.vel = joint_velocity;
   a.out = *qp_out;
   HIP_OK(launch_default_qp(n_envs, S->lds_reset, as_stream(stream), a));
+  return 0;
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+int bx_phase(bx_system* S, int which, int64_t n_envs, int64_t plane, const float* in, float* out,
+             const float* aux, int64_t aux_plane, void* stream) {
+  if (!S || !in || !out) return fail("null argument");
+  if (which < 0 || which > 2) return fail("unknown phase");
+  if (n_envs <= 0 || n_envs % 4) return fail("n_envs must be a positive multiple of 4");
+  const int64_t N = S->hdr.N;
+  if (N * n_envs >= (int64_t)1 << 32) return fail("too many bodies for one phase launch");
+  if (plane < N * n_envs || plane % 4) return fail("plane stride must be >= N*n_envs and a multiple of 4");
+  if (which >= 1 && (!aux || aux_plane % 4 || aux_plane < N * n_envs)) return fail("bad aux planes");
+  if (!aligned16(in) || !aligned16(out) || (aux && !aligned16(aux))) return fail("SoA bases must be 16-byte aligned");
+  HIP_OK(launch_phase(which, S->blob, (int)N, n_envs, plane, in, out, aux, aux_plane, as_stream(stream)));
+  return 0;
+}
+
+int bx_phase_capsule_plane(bx_system* S, int64_t n_envs, int64_t plane, const float* in, float* out,
+                           int64_t out_plane, void* stream) {
+  if (!S || !in || !out) return fail("null argument");
+  if (n_envs <= 0 || n_envs % 4) return fail("n_envs must be a positive multiple of 4");
+  const int64_t N = S->hdr.N, R = S->hdr.R;
+  if (plane < N * n_envs || plane % 4) return fail("plane stride must be >= N*n_envs and a multiple of 4");
+  if (out_plane < R * n_envs || out_plane % 4) return fail("out plane stride must be >= R*n_envs");
+  if (!aligned16(in) || !aligned16(out)) return fail("SoA bases must be 16-byte aligned");
+  if (R == 0) return 0;
+  HIP_OK(launch_capsule_plane(S->blob, (int)R, n_envs, plane, in, out, out_plane, as_stream(stream)));
   return 0;
 }
 

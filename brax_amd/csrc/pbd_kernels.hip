@@ -574,6 +574,15 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
 
 __device__ __forceinline__ void sync() { __syncthreads(); }
 
+// the zero slots that padded gather-list entries point at
+__device__ __forceinline__ void zero_slots(const Env& E, const BlobHdr& H, int lane) {
+  if (lane < 8) {
+    E.jslot[2 * H.J * 8 + lane] = 0.f;
+    E.cslot[2 * H.R * 8 + lane] = 0.f;
+    if (lane < 4) E.aslot[2 * H.K * 4 + lane] = 0.f;
+  }
+}
+
 // global <-> LDS QP through strided field views
 __device__ __forceinline__ void load_qp_global(const bx_qp& q, int64_t e, int b, float* s) {
   const float* p = q.pos.ptr + e * q.pos.env_stride + b * q.pos.body_stride;
@@ -837,87 +846,95 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
 // ---------------------------------------------------------------------------
 constexpr int MAXG = 8;
 
+// A body's gather list, padded to M entries with the index of a zero slot so
+// every gather is M unconditional LDS reads issued back-to-back (one wait).
+template <int M>
 struct GList {
-  int n;
-  int e[MAXG];
+  int e[M];
 };
 
-__device__ __forceinline__ GList load_glist(const Cst& c, int o_off, int o_l, int b) {
-  GList g;
+template <int M>
+__device__ __forceinline__ GList<M> load_glist(const Cst& c, int o_off, int o_l, int b, bool has,
+                                               int zero_entry) {
+  GList<M> g;
   int s = c.i(o_off + b);
-  g.n = c.i(o_off + b + 1) - s;
+  int n = has ? c.i(o_off + b + 1) - s : 0;
 #pragma unroll
-  for (int k = 0; k < MAXG; k++) g.e[k] = k < g.n ? c.i(o_l + s + k) : 0;
+  for (int k = 0; k < M; k++) g.e[k] = k < n ? c.i(o_l + s + k) : zero_entry;
   return g;
 }
 
+template <int M>
 struct Hoist {
   bool hasB, hasJ, hasA, hasR;
   BodyC B;
   JointC J;
   ActC A;
   RowC R;
-  GList jl, al, cl;
+  GList<M> jl, al, cl;
 };
 
-__device__ __forceinline__ void load_hoist(const Cst& c, const BlobHdr& H, int lane, Hoist& X) {
+template <int M>
+__device__ __forceinline__ void load_hoist(const Cst& c, const BlobHdr& H, int lane, Hoist<M>& X) {
   X.hasB = lane < H.N;
   X.hasJ = lane < H.J;
   X.hasA = lane < H.K;
   X.hasR = lane < H.R;
   int b = X.hasB ? lane : 0;
   X.B = load_body(c, H, b);
-  X.jl = load_glist(c, H.o_jl_off, H.o_jl, b);
-  X.al = load_glist(c, H.o_al_off, H.o_al, b);
-  X.cl = load_glist(c, H.o_cl_off, H.o_cl, b);
-  if (!X.hasB) { X.jl.n = 0; X.al.n = 0; X.cl.n = 0; }
+  X.jl = load_glist<M>(c, H.o_jl_off, H.o_jl, b, X.hasB, 2 * H.J);
+  X.al = load_glist<M>(c, H.o_al_off, H.o_al, b, X.hasB, 2 * H.K);
+  // contact entries carry their collider group in bits 24..30; the padding
+  // entry takes the group of the body's first entry (it adds exact zeros)
+  int cz = 2 * H.R;
+  {
+    int s0 = c.i(H.o_cl_off + b);
+    int n0 = X.hasB ? c.i(H.o_cl_off + b + 1) - s0 : 0;
+    if (n0 > 0) cz |= c.i(H.o_cl + s0) & 0x7F000000;
+  }
+  X.cl = load_glist<M>(c, H.o_cl_off, H.o_cl, b, X.hasB, cz);
   if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? lane : 0);
   if (H.K > 0) X.A = load_act(c, H, X.hasA ? lane : 0);
   if (H.R > 0) X.R = load_row(c, H, X.hasR ? lane : 0);
 }
 
-__device__ __forceinline__ v3 gsum3(const GList& g, const float* base, int stride) {
+template <int M>
+__device__ __forceinline__ v3 gsum3(const GList<M>& g, const float* base, int stride) {
   v3 s = mk(0.f, 0.f, 0.f);
 #pragma unroll
-  for (int k = 0; k < MAXG; k++)
-    if (k < g.n) s = s + ld3(base + g.e[k] * stride);
+  for (int k = 0; k < M; k++) s = s + ld3(base + g.e[k] * stride);
   return s;
 }
 
-// per-group normalised contact sums: sum_g (sum rows) / (eps + count)
-__device__ __forceinline__ void gsum_contact(const GList& g, const float* cslot, float eps, v3& a,
-                                             q4& r, bool rot4) {
-  a = mk(0.f, 0.f, 0.f);
-  r = q4{0.f, 0.f, 0.f, 0.f};
-  v3 ga = mk(0.f, 0.f, 0.f);
-  q4 gr{0.f, 0.f, 0.f, 0.f};
-  float cnt = 0.f;
-  int cur = -1;
+// per-group normalised contact sums  sum_g (sum of rows) / (eps + count), for
+// bodies whose rows come from at most two collider groups (checked on the
+// host); groups keep the reference's order (first group, then second)
+template <int M>
+__device__ __forceinline__ void gsum_contact(const GList<M>& g, const float* cslot, float eps,
+                                             v3& a, q4& r, bool rot4) {
+  const int g0 = g.e[0] >> 24;
+  v3 a0 = mk(0.f, 0.f, 0.f), a1 = mk(0.f, 0.f, 0.f);
+  q4 r0{0.f, 0.f, 0.f, 0.f}, r1{0.f, 0.f, 0.f, 0.f};
+  float c0 = 0.f, c1 = 0.f;
 #pragma unroll
-  for (int k = 0; k < MAXG; k++) {
-    if (k < g.n) {
-      int grp = g.e[k] >> 24;
-      if (grp != cur && cur >= 0) {
-        float d = eps + cnt;
-        a = a + ga / d;
-        r = r + q4{gr.w / d, gr.x / d, gr.y / d, gr.z / d};
-        ga = mk(0.f, 0.f, 0.f);
-        gr = q4{0.f, 0.f, 0.f, 0.f};
-        cnt = 0.f;
-      }
-      cur = grp;
-      const float* s = cslot + (g.e[k] & 0xFFFFFF) * 8;
-      ga = ga + ld3(s);
-      if (rot4) gr = gr + ld4(s + 3);
-      else gr = gr + q4{0.f, s[3], s[4], s[5]};
-      cnt += s[7];
-    }
+  for (int k = 0; k < M; k++) {
+    const float* s = cslot + (g.e[k] & 0xFFFFFF) * 8;
+    float m0 = (g.e[k] >> 24) == g0 ? 1.f : 0.f;
+    float m1 = 1.f - m0;
+    v3 v = ld3(s);
+    q4 q = rot4 ? ld4(s + 3) : q4{0.f, s[3], s[4], s[5]};
+    float f = s[7];
+    a0 = a0 + v * m0;
+    a1 = a1 + v * m1;
+    r0 = r0 + q * m0;
+    r1 = r1 + q * m1;
+    c0 += f * m0;
+    c1 += f * m1;
   }
-  if (cur >= 0) {
-    float d = eps + cnt;
-    a = a + ga / d;
-    r = r + q4{gr.w / d, gr.x / d, gr.y / d, gr.z / d};
-  }
+  float d0 = eps + c0, d1 = eps + c1;
+  a = a0 / d0 + a1 / d1;
+  r = q4{r0.w / d0 + r1.w / d1, r0.x / d0 + r1.x / d1, r0.y / d0 + r1.y / d1,
+         r0.z / d0 + r1.z / d1};
 }
 
 // Euler.velocity_projection (integrators.py:122-146) on one body
@@ -947,9 +964,9 @@ __device__ unsigned long long bx_stamp_sum[16];
 #define BX_STAMP(k) do {} while (0)
 #endif
 
-template <int L, int F>
+template <int L, int F, int M>
 __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
-                                const float* act, const Hoist& X, v3& icv, v3& ica, v3& iaa) {
+                                const float* act, const Hoist<M>& X, v3& icv, v3& ica, v3& iaa) {
 #ifdef BX_STAMPS
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last;
@@ -1039,12 +1056,11 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         v3 dp = mk(0.f, 0.f, 0.f);
         q4 dr{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < MAXG; k++)
-          if (k < X.jl.n) {
-            const float* s = E.jslot + X.jl.e[k] * 8;
-            dp = dp + ld3(s);
-            dr = dr + ld4(s + 3);
-          }
+        for (int k = 0; k < M; k++) {
+          const float* s = E.jslot + X.jl.e[k] * 8;
+          dp = dp + ld3(s);
+          dr = dr + ld4(s + 3);
+        }
         q.pos = q.pos + mul(dp, X.B.pm);
         q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                    q.rot.z + dr.z * X.B.qm.z};
@@ -1361,7 +1377,7 @@ __device__ __forceinline__ float* stage_constants(const uint32_t* blob, const Bl
   }
 }
 
-template <int L, int MODE, int F>
+template <int L, int MODE, int F, int M>
 __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
   extern __shared__ float smem[];
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
@@ -1373,6 +1389,7 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
   const int64_t e = (int64_t)blockIdx.x * (64 / L) + le;
   const bool valid = e < A.n_envs;
   Env E = carve(ebase + le * H.env_words, H);
+  zero_slots(E, H, lane);
   for (int b = lane; b < H.N; b += L) {
     if (valid) {
       load_qp_global(A.qin, e, b, E.qp + b * QP_STRIDE);
@@ -1383,10 +1400,10 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
   }
   sync();
   if constexpr (S) {
-    Hoist X;
-    load_hoist(c, H, lane, X);
+    Hoist<M> X;
+    load_hoist<M>(c, H, lane, X);
     v3 icv, ica, iaa;
-    pbd_step_single<L, F>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, X, icv, ica,
+    pbd_step_single<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, X, icv, ica,
                        iaa);
   } else {
     pbd_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr);
@@ -1424,7 +1441,7 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
 
 
 // Env.step fused with EpisodeWrapper/AutoResetWrapper (wrappers.py:105-148)
-template <int L, int MODE, int F>
+template <int L, int MODE, int F, int M>
 __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   extern __shared__ float smem[];
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
@@ -1436,6 +1453,7 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   const int64_t e = (int64_t)blockIdx.x * (64 / L) + le;
   const bool valid = e < A.n_envs;
   Env E = carve(ebase + le * H.env_words, H);
+  zero_slots(E, H, lane);
   const bx_env_params& P = A.P;
   const int kind = P.kind;
   const float* act = valid ? A.act + e * A.act_stride : nullptr;
@@ -1455,8 +1473,8 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   float done = P.auto_reset ? 0.f : done_in;
   float reward_sum = 0.f;
   const int reps = P.episode_length > 0 ? (P.action_repeat > 0 ? P.action_repeat : 1) : 1;
-  Hoist X;
-  if constexpr (S) load_hoist(c, H, lane, X);
+  Hoist<M> X;
+  if constexpr (S) load_hoist<M>(c, H, lane, X);
   // action sum of squares (ctrl cost), shared by every repeat
   float sq = 0.f;
   if (valid && lane == 0)
@@ -1469,7 +1487,7 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
     sync();
     if constexpr (S) {
       v3 icv, ica, iaa;
-      pbd_step_single<L, F>(c, H, E, lane, valid, act, X, icv, ica, iaa);
+      pbd_step_single<L, F, M>(c, H, E, lane, valid, act, X, icv, ica, iaa);
     } else {
       pbd_step<L>(c, H, E, lane, valid, act);
     }
@@ -1699,38 +1717,41 @@ static void launch_one(void (*k)(Args), dim3 grid, size_t lds, hipStream_t s, co
   hipLaunchKernelGGL(k, grid, dim3(64), lds, s, a);
 }
 
-// instantiated variants: (lanes, mode, features). Single mode at 16 lanes is
-// specialised per feature set; everything else carries all features.
+// instantiated variants: (lanes, mode, features, gather width). Single mode
+// at 16 lanes is specialised per feature set and gather width; everything
+// else carries all features.
+#define BX_SINGLE16(KERNEL, ARGS, M)                                                \
+  switch (feat) {                                                                   \
+    case 0: launch_one<ARGS>(KERNEL<16, 1, 0, M>, grid, lds, s, a); break;          \
+    case F_SPH: launch_one<ARGS>(KERNEL<16, 1, F_SPH, M>, grid, lds, s, a); break;  \
+    case F_CC | F_TW: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW, M>, grid, lds, s, a); break; \
+    default: launch_one<ARGS>(KERNEL<16, 1, F_ALL, M>, grid, lds, s, a); break;     \
+  }
 #define BX_DISPATCH(KERNEL, ARGS)                                                   \
   if (mode == 1 && L == 16) {                                                       \
-    switch (feat) {                                                                 \
-      case 0: launch_one<ARGS>(KERNEL<16, 1, 0>, grid, lds, s, a); break;           \
-      case F_SPH: launch_one<ARGS>(KERNEL<16, 1, F_SPH>, grid, lds, s, a); break;   \
-      case F_CC | F_TW: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW>, grid, lds, s, a); break; \
-      default: launch_one<ARGS>(KERNEL<16, 1, F_ALL>, grid, lds, s, a); break;      \
-    }                                                                               \
+    if (gw <= 4) { BX_SINGLE16(KERNEL, ARGS, 4) } else { BX_SINGLE16(KERNEL, ARGS, 8) } \
   } else {                                                                          \
     switch (L * 4 + mode) {                                                         \
-      case 16 * 4 + 0: launch_one<ARGS>(KERNEL<16, 0, F_ALL>, grid, lds, s, a); break; \
-      case 16 * 4 + 2: launch_one<ARGS>(KERNEL<16, 2, F_ALL>, grid, lds, s, a); break; \
-      case 32 * 4 + 0: launch_one<ARGS>(KERNEL<32, 0, F_ALL>, grid, lds, s, a); break; \
-      case 32 * 4 + 1: launch_one<ARGS>(KERNEL<32, 1, F_ALL>, grid, lds, s, a); break; \
-      case 32 * 4 + 2: launch_one<ARGS>(KERNEL<32, 2, F_ALL>, grid, lds, s, a); break; \
-      case 64 * 4 + 0: launch_one<ARGS>(KERNEL<64, 0, F_ALL>, grid, lds, s, a); break; \
-      case 64 * 4 + 1: launch_one<ARGS>(KERNEL<64, 1, F_ALL>, grid, lds, s, a); break; \
-      case 64 * 4 + 2: launch_one<ARGS>(KERNEL<64, 2, F_ALL>, grid, lds, s, a); break; \
+      case 16 * 4 + 0: launch_one<ARGS>(KERNEL<16, 0, F_ALL, 8>, grid, lds, s, a); break; \
+      case 16 * 4 + 2: launch_one<ARGS>(KERNEL<16, 2, F_ALL, 8>, grid, lds, s, a); break; \
+      case 32 * 4 + 0: launch_one<ARGS>(KERNEL<32, 0, F_ALL, 8>, grid, lds, s, a); break; \
+      case 32 * 4 + 1: launch_one<ARGS>(KERNEL<32, 1, F_ALL, 8>, grid, lds, s, a); break; \
+      case 32 * 4 + 2: launch_one<ARGS>(KERNEL<32, 2, F_ALL, 8>, grid, lds, s, a); break; \
+      case 64 * 4 + 0: launch_one<ARGS>(KERNEL<64, 0, F_ALL, 8>, grid, lds, s, a); break; \
+      case 64 * 4 + 1: launch_one<ARGS>(KERNEL<64, 1, F_ALL, 8>, grid, lds, s, a); break; \
+      case 64 * 4 + 2: launch_one<ARGS>(KERNEL<64, 2, F_ALL, 8>, grid, lds, s, a); break; \
       default: return hipErrorInvalidValue;                                         \
     }                                                                               \
   }
 
-hipError_t launch_system_step(int L, int mode, int feat, int64_t n_envs, size_t lds, hipStream_t s,
+hipError_t launch_system_step(int L, int mode, int feat, int gw, int64_t n_envs, size_t lds, hipStream_t s,
                               const StepArgs& a) {
   int epb = 64 / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
   BX_DISPATCH(system_step_kernel, StepArgs)
   return hipGetLastError();
 }
-hipError_t launch_env_step(int L, int mode, int feat, int64_t n_envs, size_t lds, hipStream_t s,
+hipError_t launch_env_step(int L, int mode, int feat, int gw, int64_t n_envs, size_t lds, hipStream_t s,
                            const EnvArgs& a) {
   int epb = 64 / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));

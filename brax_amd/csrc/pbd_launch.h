@@ -41,13 +41,18 @@ struct ResetArgs {
   bx_qp out;
 };
 
-hipError_t launch_system_step(int L, int mode, int feat, int64_t n_envs, size_t lds, hipStream_t s, const StepArgs& a);
-hipError_t launch_env_step(int L, int mode, int feat, int64_t n_envs, size_t lds, hipStream_t s, const EnvArgs& a);
+hipError_t launch_system_step(int L, int mode, int feat, int gw, int64_t n_envs, size_t lds, hipStream_t s, const StepArgs& a);
+hipError_t launch_env_step(int L, int mode, int feat, int gw, int64_t n_envs, size_t lds, hipStream_t s, const EnvArgs& a);
 hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a);
 hipError_t launch_default_qp(int64_t n_envs, size_t lds, hipStream_t s, const ResetArgs& a);
 hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset, float lo, float hi,
                           hipStream_t s);
 
 hipError_t debug_stamps(unsigned long long* out, int reset);
+hipError_t launch_phase(int which, const uint32_t* blob, int N, int64_t B, int64_t plane,
+                        const float* in, float* out, const float* aux, int64_t aux_plane,
+                        hipStream_t s);
+hipError_t launch_capsule_plane(const uint32_t* blob, int R, int64_t B, int64_t plane,
+                                const float* in, float* out, int64_t out_plane, hipStream_t s);
 
 }  // namespace bx

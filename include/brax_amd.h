@@ -238,6 +238,24 @@ int bx_env_observe(bx_system* sys, const bx_env_params* env, int64_t n_envs,
 int bx_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
                float lo, float hi, void* stream);
 
+/*
+ * Standalone HBM-streaming phase kernels over a structure-of-arrays batch
+ * (the integrator and collider phases benchmarked in isolation).
+ * SoA: field plane k, body b, env e at base[k*plane + b*n_envs + e]; the 13
+ * state planes are pos xyz, rot wxyz, vel xyz, ang xyz. n_envs % 4 == 0,
+ * planes 16-byte aligned.
+ *   which 0: Euler.kinetic              (integrators.py:50-68)   in -> out pos, rot
+ *   which 1: Euler.update(acc_p=aux)    (integrators.py:85-93)   aux = dp vel 3 + ang 3 planes
+ *   which 2: Euler.velocity_projection  (integrators.py:122-146) aux = previous state planes
+ */
+int bx_phase(bx_system* sys, int which, int64_t n_envs, int64_t plane, const float* in,
+             float* out, const float* aux, int64_t aux_plane, void* stream);
+
+/* capsule_plane contacts (colliders.py:744-759) of every capsule-plane row:
+ * out planes pos xyz, vel xyz, normal xyz, penetration, each (R, n_envs). */
+int bx_phase_capsule_plane(bx_system* sys, int64_t n_envs, int64_t plane, const float* in,
+                           float* out, int64_t out_plane, void* stream);
+
 /* Diagnostic builds only (-DBX_STAMPS): per-phase s_memtime cycle sums of the
  * single-mode step, [0..9] phases, [15] samples. Fails on product builds. */
 int bx_debug_stamps(unsigned long long* out16, int reset);

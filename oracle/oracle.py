@@ -127,6 +127,24 @@ class Oracle:
       raise ValueError('obs size mismatch')
     return out, obs, rew, dn, met
 
+  def phase(self, which, qp, aux=None):
+    """0 kinetic, 1 update(acc) with aux (B,N,6) dp, 2 velocity_projection with
+    aux = previous state (B,N,13)."""
+    qp = self._a(qp)
+    B = qp.shape[0]
+    out = np.empty_like(qp)
+    aux = None if aux is None else self._a(aux)
+    self._fn('oracle_phase')(C.byref(self.cdesc), C.c_int(which), C.c_int64(B), _p(qp),
+                             _p(aux), _p(out))
+    return out
+
+  def capsule_plane(self, qp):
+    qp = self._a(qp)
+    B = qp.shape[0]
+    out = np.zeros((B, self.R, 10), self.dtype)
+    self._fn('oracle_phase_capsule_plane')(C.byref(self.cdesc), C.c_int64(B), _p(qp), _p(out))
+    return out
+
   def closest_segments(self, segs):
     segs = self._a(segs).reshape(-1, 4, 3)
     n = segs.shape[0]

@@ -1406,6 +1406,72 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
   return rc;
 }
 
+/* single phases over B envs (the standalone phase kernels' checker) */
+int FN(oracle_phase)(const bx_desc* d, int which, int64_t B, const R* qp, const R* aux, R* out) {
+  sysc s;
+  sys_init(&s, d);
+  int N = s.N, Rn = s.Rn;
+#pragma omp parallel
+  {
+    work_t w;
+    work_alloc(&w, N, Rn);
+    body_t* prev = calloc(N, sizeof(body_t));
+#pragma omp for schedule(static)
+    for (int64_t e = 0; e < B; e++) {
+      load_qp(w.qp, qp + e * 13 * N, N);
+      if (which == 0) {
+        kinetic(&s, &w);
+      } else if (which == 1) {
+        /* aux (B,N,6): dp vel, dp ang (integrators.py:85-93) */
+        for (int b = 0; b < N; b++) {
+          body_t* q = &w.qp[b];
+          const R* dp = aux + (e * N + b) * 6;
+          for (int k = 0; k < 3; k++) {
+            R v = s.vdamp_exp * q->vel[k];
+            v += (dp[k] + s.g[k]) * s.h;
+            q->vel[k] = v * s.pos_mask[3 * b + k];
+            R a = s.adamp_exp * q->ang[k];
+            a += dp[3 + k] * s.h;
+            q->ang[k] = a * s.rot_mask[3 * b + k];
+          }
+        }
+      } else if (which == 2) {
+        load_qp(prev, aux + e * 13 * N, N);
+        velocity_projection(&s, &w, prev);
+      }
+      store_qp(w.qp, out + e * 13 * N, N);
+    }
+    free(prev);
+    work_free(&w);
+  }
+  sys_free(&s);
+  return 0;
+}
+
+/* capsule_plane contacts of every capsule-plane row: out (B,R,10) =
+ * pos, vel, normal, penetration (rows of other kinds left untouched) */
+int FN(oracle_phase_capsule_plane)(const bx_desc* d, int64_t B, const R* qp, R* out) {
+  sysc s;
+  sys_init(&s, d);
+  int N = s.N, Rn = s.Rn;
+#pragma omp parallel
+  {
+    body_t* q = calloc(N, sizeof(body_t));
+#pragma omp for schedule(static)
+    for (int64_t e = 0; e < B; e++) {
+      load_qp(q, qp + e * 13 * N, N);
+      for (int r = 0; r < Rn; r++) {
+        if (d->col_fn[d->row_group[r]] != BX_COL_CAPSULE_PLANE) continue;
+        R* o = out + (e * Rn + r) * 10;
+        contact_row(&s, r, q, o, o + 3, o + 6, o + 9);
+      }
+    }
+    free(q);
+  }
+  sys_free(&s);
+  return 0;
+}
+
 /* geometry.closest_segment_to_segment_points (geometry.py:394-461), exported
  * for the reference's known-answer cases (geometry_test.py:217-272) */
 void FN(oracle_closest_segments)(int64_t n, const R* seg, R* a_best, R* b_best) {
