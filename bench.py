@@ -46,7 +46,7 @@ def _dist():
   return None, 0, 1, 0
 
 
-def cpu_baseline(batch, min_seconds=10.0, max_steps=200):
+def cpu_baseline(batch, min_seconds=10.0, max_steps=100000):
   """The oracle's float32 C restatement (OpenMP over envs) on this host's
   cores, on a bounded sample of the same workload."""
   from oracle.oracle import Oracle
@@ -70,6 +70,11 @@ def cpu_baseline(batch, min_seconds=10.0, max_steps=200):
           'sample': f'Ant, {B} envs x {steps} env-steps ({dt:.1f} s), float32 C '
                     f'restatement (oracle/pbd_oracle.c), {threads} OpenMP threads, '
                     f'{platform.processor() or platform.machine()}'}
+
+
+PHASE_KERNELS = {'kinetic': 'bx::kinetic_kernel', 'update_acc': 'bx::update_acc_kernel',
+                 'velocity_projection': 'bx::vproj_kernel',
+                 'capsule_plane': 'bx::capsule_plane_kernel'}
 
 
 def phase_bench(sys_, dev, batch=1 << 20, reps=20):
@@ -107,7 +112,10 @@ def phase_bench(sys_, dev, batch=1 << 20, reps=20):
     us = a.elapsed_time(b) * 1e3 / reps
     gbs = per_env * batch / (us * 1e-6) / 1e9
     res[name] = {'us': us, 'bytes_per_launch': per_env * batch, 'achieved': gbs,
-                 'frac': gbs / HBM_PEAK_GBS}
+                 'frac': gbs / HBM_PEAK_GBS, 'traffic': None}
+    k = ((_traffic() or {}).get('kernels') or {}).get(PHASE_KERNELS[name])
+    if k and k.get('envs') == batch:
+      res[name]['traffic'] = k['hbm_bytes_per_launch']
   del soa, aux, out, contacts
   return {'envs': batch, 'unit': 'GB/s', 'peak': HBM_PEAK_GBS, 'kernels': res}
 
@@ -202,8 +210,9 @@ def main():
   achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
   tr = _traffic()
   traffic = None
-  if tr and tr.get('batch') == B:
-    traffic = tr.get('hbm_bytes_per_launch')
+  for name, k in ((tr or {}).get('kernels') or {}).items():
+    if 'env_step_kernel' in name and k.get('batch') == B:
+      traffic = k['hbm_bytes_per_launch']
   out = {
       'metric': 'env-steps/sec (Ant, 4096 envs/GPU)',
       'value': value,

@@ -137,14 +137,29 @@ class PhysicsEnv(Env):
       p.first_obs = first_obs.data_ptr()
     return p
 
+  def _cached_params(self, opts, first_qp, first_obs):
+    """bx_env_params for this wrapper chain; rebuilt only when the options or
+    the auto-reset first state change (i.e. after a reset), not per step."""
+    key = (opts.get('episode_length'), opts.get('action_repeat'), bool(opts.get('auto_reset')),
+           id(first_qp), None if first_obs is None else first_obs.data_ptr())
+    cache = self.__dict__.setdefault('_pcache', {})
+    hit = cache.get(key)
+    if hit is not None and hit[1] is first_qp and hit[2] is first_obs:
+      return hit[0]
+    if len(cache) > 16:
+      cache.clear()
+    p = self._params(opts, first_qp, first_obs)
+    cache[key] = (p, first_qp, first_obs)  # keeps the first state alive with its pointers
+    return p
+
   def _alloc(self, B):
-    dev = self.sys.device
-    qp = packed_view(torch.empty((B, self.sys.num_bodies, 16), dtype=torch.float32, device=dev))
-    obs = torch.empty((B, self.obs_size), dtype=torch.float32, device=dev)
-    # one buffer for the per-env scalars: reward, done, steps, truncation
-    scal = torch.zeros((4, B), dtype=torch.float32, device=dev)
-    met = torch.empty((B, max(len(self.metric_keys), 1)), dtype=torch.float32, device=dev)
-    return qp, obs, scal, met
+    """Every output of one env step in ONE device allocation:
+    qp (B,N,16) | obs (B,O) | reward, done, steps, truncation (4,B) | metrics (B,M)."""
+    N, O, M = self.sys.num_bodies, self.obs_size, max(len(self.metric_keys), 1)
+    sizes = (B * N * 16, B * O, 4 * B, B * M)
+    buf = torch.empty((sum(sizes),), dtype=torch.float32, device=self.sys.device)
+    q, o, sc, m = buf.split(sizes)
+    return packed_view(q.view(B, N, 16)), o.view(B, O), sc.view(4, B), m.view(B, M)
 
   def _metrics(self, met):
     return {k: met[:, i] for i, k in enumerate(self.metric_keys)}
@@ -201,11 +216,14 @@ class PhysicsEnv(Env):
     return self._chain_step(state, action, {})
 
   def _chain_step(self, state, action, opts):
+    dev = self.sys.device
     B = state.qp.pos.shape[0]
-    act = torch.as_tensor(action, dtype=torch.float32, device=self.sys.device)
+    act = action
+    if type(act) is not torch.Tensor or act.dtype != torch.float32 or not act.is_cuda:
+      act = torch.as_tensor(act, dtype=torch.float32, device=dev)
     if act.dim() == 1:
       act = act.reshape(1, -1).expand(B, -1)
-    if act.shape != (B, self.action_size):
+    if act.shape[0] != B or act.shape[1] != self.action_size or act.dim() != 2:
       raise ValueError(f'action shape {tuple(act.shape)} != {(B, self.action_size)}')
     if act.stride(-1) != 1:
       act = act.contiguous()
@@ -214,31 +232,41 @@ class PhysicsEnv(Env):
     first_obs = state.info.get('first_obs') if auto else None
     if auto and (first_qp is None or first_obs is None):
       raise ValueError('AutoResetWrapper state lacks first_qp / first_obs')
-    p = self._params(opts, first_qp, first_obs)
+    p = self._cached_params(opts, first_qp, first_obs)
     qp, obs, scal, met = self._alloc(B)
     sin = abi.BxEnvState()
     sin.qp = qp_struct(state.qp, True)
-    done_in = torch.as_tensor(state.done, dtype=torch.float32, device=self.sys.device).contiguous()
+    done_in = _f32(state.done, dev)
     sin.done = done_in.data_ptr()
     steps_in = state.info.get('steps')
     if steps_in is not None:
-      steps_in = torch.as_tensor(steps_in, dtype=torch.float32, device=self.sys.device).contiguous()
+      steps_in = _f32(steps_in, dev)
       sin.steps = steps_in.data_ptr()
     sout = abi.BxEnvState()
     sout.qp = qp_struct(qp, True)
     sout.obs = obs.data_ptr()
-    sout.reward = scal[0].data_ptr()
-    sout.done = scal[1].data_ptr()
-    sout.steps = scal[2].data_ptr()
-    sout.truncation = scal[3].data_ptr()
+    base = scal.data_ptr()
+    sout.reward = base
+    sout.done = base + 4 * B
+    sout.steps = base + 8 * B
+    sout.truncation = base + 12 * B
     sout.metrics = met.data_ptr()
     _native.check(_native.lib().bx_env_step(
         self.sys._h, C.byref(p), B, C.byref(sin), C.c_void_p(act.data_ptr()), act.stride(0),
-        C.byref(sout), _stream()))
+        C.byref(sout), _stream(dev.index)))
+    reward, done, steps, trunc = scal.unbind(0)
     info = dict(state.info)
     if p.episode_length > 0:
-      info['steps'] = scal[2]
-      info['truncation'] = scal[3]
+      info['steps'] = steps
+      info['truncation'] = trunc
     metrics = dict(state.metrics)
-    metrics.update(self._metrics(met))
-    return State(qp=qp, obs=obs, reward=scal[0], done=scal[1], metrics=metrics, info=info)
+    if self.metric_keys:
+      metrics.update(zip(self.metric_keys, met.unbind(1)))
+    return State(qp=qp, obs=obs, reward=reward, done=done, metrics=metrics, info=info)
+
+
+def _f32(x, dev):
+  """A contiguous float32 device tensor (no copy when it already is one)."""
+  if type(x) is torch.Tensor and x.dtype == torch.float32 and x.is_cuda and x.is_contiguous():
+    return x
+  return torch.as_tensor(x, dtype=torch.float32, device=dev).contiguous()

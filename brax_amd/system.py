@@ -21,7 +21,17 @@ from brax_amd import config as cfgmod
 from brax_amd.base import Info, P, QP, packed_view
 
 
-def _stream():
+try:
+  _raw_stream = torch._C._cuda_getCurrentRawStream  # pylint: disable=protected-access
+except AttributeError:  # pragma: no cover
+  _raw_stream = None
+
+
+def _stream(device_index=None):
+  """The caller's current HIP stream (stream-ordered ABI)."""
+  if _raw_stream is not None:
+    return C.c_void_p(_raw_stream(torch.cuda.current_device() if device_index is None
+                                  else device_index))
   return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
@@ -38,11 +48,21 @@ def _field(t, batched):
 
 
 def qp_struct(qp, batched):
+  """bx_qp view of a QP. Batched structs are cached on the (frozen) QP: its
+  fields cannot be re-bound, so the pointers and strides stay valid."""
+  if batched:
+    s = qp.__dict__.get('_bxs')
+    # (a copied QP carries the attribute over: re-check the pointers)
+    if (s is not None and s.pos.ptr == qp.pos.data_ptr() and s.rot.ptr == qp.rot.data_ptr()
+        and s.vel.ptr == qp.vel.data_ptr() and s.ang.ptr == qp.ang.data_ptr()):
+      return s
   s = abi.BxQP()
   s.pos = _field(qp.pos, batched)
   s.rot = _field(qp.rot, batched)
   s.vel = _field(qp.vel, batched)
   s.ang = _field(qp.ang, batched)
+  if batched:
+    object.__setattr__(qp, '_bxs', s)
   return s
 
 

@@ -1,12 +1,15 @@
 #!/bin/bash
-# rocprofv3 passes: kernel-trace stats, then separate PMC passes.
+# rocprofv3 passes over bench.py: kernel-trace stats, then separate PMC passes
+# (FETCH_SIZE, WRITE_SIZE, SQ counters), each in its own run.
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 300 --warmup 30 --no-cpu-baseline > $OUT.trace.log 2>&1 || { echo trace failed; tail -20 $OUT.trace.log; exit 1; }
-tail -2 $OUT.trace.log
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > $OUT.fetch.log 2>&1 || { echo fetch failed; tail -20 $OUT.fetch.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > $OUT.write.log 2>&1 || { echo write failed; tail -20 $OUT.write.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d $OUT/sq -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > $OUT.sq.log 2>&1 || { echo sq failed; tail -20 $OUT.sq.log; }
-find $OUT -name "*.csv" | head -20
+ARGS="--steps 300 --warmup 30 --no-cpu-baseline --phase-envs 1048576"
+PARGS="--steps 50 --warmup 5 --no-cpu-baseline --phase-envs 1048576"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $ARGS > $OUT.trace.log 2>&1 || { echo trace failed; tail -20 $OUT.trace.log; exit 1; }
+tail -1 $OUT.trace.log
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 bench.py $PARGS > $OUT.fetch.log 2>&1 || { echo fetch failed; tail -20 $OUT.fetch.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 bench.py $PARGS > $OUT.write.log 2>&1 || { echo write failed; tail -20 $OUT.write.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d $OUT/sq -o run --output-format csv -- python3 bench.py $PARGS > $OUT.sq.log 2>&1 || { echo sq failed; tail -20 $OUT.sq.log; }
+find $OUT -name "*.csv"

@@ -1,0 +1,100 @@
+"""Summarise a run_prof.sh output directory into profiles/.
+
+    python tools/prof_summary.py gpurun_out/prof_<tag> <tag> [phase_envs]
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats), and
+profiles/<tag>_counters.json + profiles/traffic.json: per kernel, the mean
+PMC counters per dispatch and the HBM bytes per launch, corrected as
+MI355X_MICROARCH.md prescribes for gfx950 (FETCH_SIZE reports half of a wide
+coalesced read: doubled; WRITE_SIZE exact for 16-B-per-lane stores; both in KB).
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# algorithmic bytes per launch, for the kernels the bench runs
+ANT_ENV_STEP_B = 1428
+PHASE_B = {'kinetic_kernel': 80 * 10, 'update_acc_kernel': 72 * 10, 'vproj_kernel': 96 * 10,
+           'capsule_plane_kernel': 120 * 5}
+
+
+def short(name):
+  n = name.split('(')[0].replace('void ', '')
+  return n
+
+
+def counters(d):
+  out = defaultdict(lambda: defaultdict(list))
+  meta = {}
+  for sub in ('fetch', 'write', 'sq'):
+    p = os.path.join(d, sub, 'run_counter_collection.csv')
+    if not os.path.exists(p):
+      continue
+    with open(p) as f:
+      for r in csv.DictReader(f):
+        k = short(r['Kernel_Name'])
+        if not k.startswith('bx::') and 'bx::' not in k:
+          continue
+        out[k][r['Counter_Name']].append(float(r['Counter_Value']))
+        meta[k] = {'grid': int(r['Grid_Size']), 'workgroup': int(r['Workgroup_Size']),
+                   'vgpr': int(r['VGPR_Count']), 'sgpr': int(r['SGPR_Count']),
+                   'lds_bytes': int(r['LDS_Block_Size']), 'scratch': int(r['Scratch_Size'])}
+  return out, meta
+
+
+def main():
+  d, tag = sys.argv[1], sys.argv[2]
+  prof = os.path.join(ROOT, 'profiles')
+  shutil.copy(os.path.join(d, 'trace', 'run_kernel_stats.csv'),
+              os.path.join(prof, f'{tag}_kernel_stats.csv'))
+  stats = {}
+  with open(os.path.join(d, 'trace', 'run_kernel_stats.csv')) as f:
+    for r in csv.DictReader(f):
+      stats[short(r['Name'])] = {'calls': int(r['Calls']), 'avg_ns': float(r['AverageNs'])}
+  cnt, meta = counters(d)
+  res = {}
+  for k, cs in cnt.items():
+    e = {'counters': {c: {'dispatches': len(v), 'mean': sum(v) / len(v)} for c, v in cs.items()}}
+    e.update(meta.get(k, {}))
+    e['trace'] = stats.get(k)
+    f = e['counters'].get('FETCH_SIZE', {}).get('mean')
+    w = e['counters'].get('WRITE_SIZE', {}).get('mean')
+    if f is not None and w is not None:
+      e['hbm_read_bytes_per_launch'] = 2 * f * 1024
+      e['hbm_write_bytes_per_launch'] = w * 1024
+      e['hbm_bytes_per_launch'] = e['hbm_read_bytes_per_launch'] + e['hbm_write_bytes_per_launch']
+    res[k] = e
+  with open(os.path.join(prof, f'{tag}_counters.json'), 'w') as f:
+    json.dump(res, f, indent=1)
+  # traffic.json: what bench.py reports as roofline.traffic
+  traffic = {'round': tag, 'source': f'profiles/{tag}_counters.json',
+             'note': 'HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB -> B), '
+                     'gfx950 correction per MI355X_MICROARCH.md', 'kernels': {}}
+  for k, e in res.items():
+    if 'hbm_bytes_per_launch' not in e:
+      continue
+    ent = {'hbm_bytes_per_launch': e['hbm_bytes_per_launch'],
+           'hbm_read_bytes_per_launch': e['hbm_read_bytes_per_launch'],
+           'hbm_write_bytes_per_launch': e['hbm_write_bytes_per_launch'],
+           'grid': e.get('grid'), 'avg_ns': (e.get('trace') or {}).get('avg_ns')}
+    base = k.split('::')[-1].split('<')[0]
+    if base == 'env_step_kernel':
+      ent['batch'] = e['grid'] // 64 * 4  # 16 lanes per env, 4 envs per 64-wide workgroup
+      ent['algorithmic_bytes_per_launch'] = ANT_ENV_STEP_B * ent['batch']
+    elif base in PHASE_B:
+      envs = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20  # bench --phase-envs
+      ent['envs'] = envs
+      ent['algorithmic_bytes_per_launch'] = PHASE_B[base] * envs
+    traffic['kernels'][k] = ent
+  with open(os.path.join(prof, 'traffic.json'), 'w') as f:
+    json.dump(traffic, f, indent=1)
+  print(json.dumps(traffic, indent=1))
+
+
+if __name__ == '__main__':
+  main()
