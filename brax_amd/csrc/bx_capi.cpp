@@ -183,23 +183,23 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   for (int j0 = 0; j0 < J;) {
     int g = d->joint_group[j0], j1 = j0;
     while (j1 < J && d->joint_group[j1] == g) j1++;
-    for (int j = j0; j < j1; j++) jl[d->joint_body_p[j]].push_back(2 * j);
-    for (int j = j0; j < j1; j++) jl[d->joint_body_c[j]].push_back(2 * j + 1);
+    for (int j = j0; j < j1; j++) jl[d->joint_body_p[j]].push_back(j);
+    for (int j = j0; j < j1; j++) jl[d->joint_body_c[j]].push_back(J + j);
     j0 = j1;
   }
   for (int a0 = 0; a0 < K;) {
     int g = d->act_group[a0], a1 = a0;
     while (a1 < K && d->act_group[a1] == g) a1++;
-    for (int a = a0; a < a1; a++) al[d->joint_body_p[d->act_joint[a]]].push_back(2 * a);
-    for (int a = a0; a < a1; a++) al[d->joint_body_c[d->act_joint[a]]].push_back(2 * a + 1);
+    for (int a = a0; a < a1; a++) al[d->joint_body_p[d->act_joint[a]]].push_back(a);
+    for (int a = a0; a < a1; a++) al[d->joint_body_c[d->act_joint[a]]].push_back(K + a);
     a0 = a1;
   }
   for (int g = 0; g < G; g++) {
     for (int x = 0; x < R; x++)
-      if (d->row_group[x] == g) cl[d->row_body_a[x]].push_back((2 * x) | (g << 24));
+      if (d->row_group[x] == g) cl[d->row_body_a[x]].push_back(x | (g << 24));
     if (!d->col_oneway[g])
       for (int x = 0; x < R; x++)
-        if (d->row_group[x] == g) cl[d->row_body_b[x]].push_back((2 * x + 1) | (g << 24));
+        if (d->row_group[x] == g) cl[d->row_body_b[x]].push_back((R + x) | (g << 24));
   }
   auto put_lists = [&](std::vector<std::vector<int>>& L_, int& o_off, int& o_l) {
     o_off = B.alloc(N + 1);
@@ -281,14 +281,16 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.l_prev = carve(N * PREV_STRIDE);
   H.l_rb = carve(N * RB_STRIDE);
   // slot regions end with one zero slot (padding target of the gather lists)
-  H.l_jslot = carve((2 * J + 1) * 8);
-  H.l_aslot = carve((2 * K + 1) * 4);
-  H.l_rowd = carve(R * 8);
-  H.l_cslot = carve((2 * R + 1) * 8);
+  H.l_jslot = carve((2 * J + 1) * SLOT_STRIDE);
+  H.l_aslot = carve((2 * K + 1) * ASLOT_STRIDE);
+  H.l_rowd = carve(R * ROWD_STRIDE);
+  H.l_cslot = carve((2 * R + 1) * SLOT_STRIDE);
   H.l_acc = carve(N * ACC_STRIDE);
   H.l_ang = carve(2 * D);
   H.l_red = carve(64);
-  H.env_words = off;
+  // envs 64 words apart: with the odd-multiple record strides, the four
+  // envs' records of one ds_read_b128 lane group land on distinct bank slots
+  H.env_words = (off + 63) & ~63;
   size_t mx = 0;
   {
     int max_groups = 0;

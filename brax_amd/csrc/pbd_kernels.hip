@@ -53,13 +53,14 @@ __device__ __forceinline__ BodyC load_body(const Cst& c, const BlobHdr& H, int b
 // LDS views of one env
 // ---------------------------------------------------------------------------
 struct Env {
-  float* qp;     // N x 16: pos 0..2, rot 3..6, vel 7..9, ang 10..12
-  float* prev;   // N x 8 : pos, rot   (qprev)
-  float* rb;     // N x 12: pos, vel, ang (qp_right_before)
-  float* jslot;  // J x 2 x 8
-  float* aslot;  // K x 2 x 4
-  float* rowd;   // R x 8 : cpos 3, normal 3, pen, dlambda
-  float* cslot;  // R x 2 x 8
+  float* qp;     // N x QP_STRIDE: pos 0..2, rot 3..6, vel 7..9, ang 10..12
+  float* prev;   // N x PREV_STRIDE: pos, rot   (qprev)
+  float* rb;     // N x RB_STRIDE: pos, vel, ang (qp_right_before)
+  float* jslot;  // (2J + 1) x SLOT_STRIDE: parent slots, child slots, zero
+  float* aslot;  // (2K + 1) x ASLOT_STRIDE
+  float* rowd;   // R x ROWD_STRIDE: cpos 3, normal 3, pen, dlambda
+  float* cslot;  // (2R + 1) x SLOT_STRIDE: a-side, b-side, zero
+  int nJ, nK, nR;
   float* acc;    // N x 12: info contact vel 3, ang 3, info actuator ang 3, dp_a 3
   float* ang;    // 2 x D: joint angles, joint vels
   float* red;    // 64 scratch
@@ -70,16 +71,64 @@ __device__ __forceinline__ void st3(float* p, v3 v) { p[0] = v.x; p[1] = v.y; p[
 __device__ __forceinline__ q4 ld4(const float* p) { return q4{p[0], p[1], p[2], p[3]}; }
 __device__ __forceinline__ void st4(float* p, q4 q) { p[0] = q.w; p[1] = q.x; p[2] = q.y; p[3] = q.z; }
 
+// 16-byte LDS accesses (ds_read_b128 / ds_write_b128) on 16-byte aligned
+// records; the record strides in pbd_layout.h keep them bank-conflict-free
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 ld4a(const float* p) {
+  return *reinterpret_cast<const f32x4*>(__builtin_assume_aligned(p, 16));
+}
+__device__ __forceinline__ void st4a(float* p, f32x4 v) {
+  *reinterpret_cast<f32x4*>(__builtin_assume_aligned(p, 16)) = v;
+}
+
 struct QP {
   v3 pos;
   q4 rot;
   v3 vel, ang;
 };
+// QP records (QP_STRIDE, 16-byte aligned): 3 x b128 + b32
 __device__ __forceinline__ QP ldqp(const float* s) {
-  return QP{ld3(s), ld4(s + 3), ld3(s + 7), ld3(s + 10)};
+  f32x4 a = ld4a(s), b = ld4a(s + 4), c = ld4a(s + 8);
+  float d = s[12];
+  return QP{mk(a.x, a.y, a.z), q4{a.w, b.x, b.y, b.z}, mk(b.w, c.x, c.y), mk(c.z, c.w, d)};
 }
 __device__ __forceinline__ void stqp(float* s, const QP& q) {
-  st3(s, q.pos); st4(s + 3, q.rot); st3(s + 7, q.vel); st3(s + 10, q.ang);
+  st4a(s, f32x4{q.pos.x, q.pos.y, q.pos.z, q.rot.w});
+  st4a(s + 4, f32x4{q.rot.x, q.rot.y, q.rot.z, q.vel.x});
+  st4a(s + 8, f32x4{q.vel.y, q.vel.z, q.ang.x, q.ang.y});
+  s[12] = q.ang.z;
+}
+__device__ __forceinline__ v3 ld_ang(const float* s) {  // QP record's ang
+  f32x4 c = ld4a(s + 8);
+  return mk(c.z, c.w, s[12]);
+}
+// 8-word records (slots, prev, row data): v3 at 0..2, q4 at 3..6, scalar at 7
+__device__ __forceinline__ void st_slot(float* s, v3 v, q4 r, float f) {
+  st4a(s, f32x4{v.x, v.y, v.z, r.w});
+  st4a(s + 4, f32x4{r.x, r.y, r.z, f});
+}
+__device__ __forceinline__ void ld_slot(const float* s, v3& v, q4& r, float& f) {
+  f32x4 a = ld4a(s), b = ld4a(s + 4);
+  v = mk(a.x, a.y, a.z);
+  r = q4{a.w, b.x, b.y, b.z};
+  f = b.w;
+}
+__device__ __forceinline__ void st_v3a(float* s, v3 v) { st4a(s, f32x4{v.x, v.y, v.z, 0.f}); }
+__device__ __forceinline__ v3 ld_v3a(const float* s) {
+  f32x4 a = ld4a(s);
+  return mk(a.x, a.y, a.z);
+}
+// qp_right_before records (RB_STRIDE): pos, vel, ang in 3 x b128
+__device__ __forceinline__ void st_rb(float* s, v3 p, v3 v, v3 a) {
+  st4a(s, f32x4{p.x, p.y, p.z, v.x});
+  st4a(s + 4, f32x4{v.y, v.z, a.x, a.y});
+  st4a(s + 8, f32x4{a.z, 0.f, 0.f, 0.f});
+}
+__device__ __forceinline__ void ld_rb(const float* s, v3& p, v3& v, v3& a) {
+  f32x4 x = ld4a(s), y = ld4a(s + 4), z = ld4a(s + 8);
+  p = mk(x.x, x.y, x.z);
+  v = mk(x.w, y.x, y.y);
+  a = mk(y.z, y.w, z.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -550,25 +599,35 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
     }
   }
   float sgp = is_torque<F>(A.type) ? 1.f : -1.f;
-  st3(E.aslot + (2 * a) * 4, sgp * mul(Jc.Ip, tq));
-  st3(E.aslot + (2 * a + 1) * 4, -sgp * mul(Jc.Ic, tq));
+  st_v3a(E.aslot + a * ASLOT_STRIDE, sgp * mul(Jc.Ip, tq));
+  st_v3a(E.aslot + (E.nK + a) * ASLOT_STRIDE, -sgp * mul(Jc.Ic, tq));
 }
 
 // ---------------------------------------------------------------------------
 // per-env LDS carving
 // ---------------------------------------------------------------------------
+// every LDS region starts 16-byte aligned (offsets are multiples of 4 words,
+// env blocks of 64 words): telling the compiler lets it use ds_read_b128 /
+// ds_write_b128 (and b64/b96) instead of pairs of 4-byte accesses
+__device__ __forceinline__ float* al16(float* p) {
+  return reinterpret_cast<float*>(__builtin_assume_aligned(p, 16));
+}
+
 __device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
   Env E;
-  E.qp = base + H.l_qp;
-  E.prev = base + H.l_prev;
-  E.rb = base + H.l_rb;
-  E.jslot = base + H.l_jslot;
-  E.aslot = base + H.l_aslot;
-  E.rowd = base + H.l_rowd;
-  E.cslot = base + H.l_cslot;
-  E.acc = base + H.l_acc;
-  E.ang = base + H.l_ang;
-  E.red = base + H.l_red;
+  E.qp = al16(base + H.l_qp);
+  E.prev = al16(base + H.l_prev);
+  E.rb = al16(base + H.l_rb);
+  E.jslot = al16(base + H.l_jslot);
+  E.aslot = al16(base + H.l_aslot);
+  E.rowd = al16(base + H.l_rowd);
+  E.cslot = al16(base + H.l_cslot);
+  E.acc = al16(base + H.l_acc);
+  E.ang = al16(base + H.l_ang);
+  E.red = al16(base + H.l_red);
+  E.nJ = H.J;
+  E.nK = H.K;
+  E.nR = H.R;
   return E;
 }
 
@@ -576,10 +635,10 @@ __device__ __forceinline__ void sync() { __syncthreads(); }
 
 // the zero slots that padded gather-list entries point at
 __device__ __forceinline__ void zero_slots(const Env& E, const BlobHdr& H, int lane) {
-  if (lane < 8) {
-    E.jslot[2 * H.J * 8 + lane] = 0.f;
-    E.cslot[2 * H.R * 8 + lane] = 0.f;
-    if (lane < 4) E.aslot[2 * H.K * 4 + lane] = 0.f;
+  if (lane < SLOT_STRIDE) {
+    E.jslot[2 * H.J * SLOT_STRIDE + lane] = 0.f;
+    E.cslot[2 * H.R * SLOT_STRIDE + lane] = 0.f;
+    if (lane < ASLOT_STRIDE) E.aslot[2 * H.K * ASLOT_STRIDE + lane] = 0.f;
   }
 }
 
@@ -644,8 +703,8 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         v3 Ip = c.f3(H.o_body + bp * BODY_STRIDE + BODY_I);
         v3 Ic = c.f3(H.o_body + bc * BODY_STRIDE + BODY_I);
         v3 tq = -1.f * damp * (ld3(E.qp + bp * QP_STRIDE + 10) - ld3(E.qp + bc * QP_STRIDE + 10));
-        st3(E.jslot + (2 * j) * 8, mul(Ip, tq));
-        st3(E.jslot + (2 * j + 1) * 8, -1.f * mul(Ic, tq));
+        st3(E.jslot + j * SLOT_STRIDE, mul(Ip, tq));
+        st3(E.jslot + (E.nJ + j) * SLOT_STRIDE, -1.f * mul(Ic, tq));
       }
       sync();
       // Euler.update(acc) + Euler.kinetic (integrators.py:50-93)
@@ -653,9 +712,9 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         BodyC B = load_body(c, H, b);
         v3 dpa = mk(0.f, 0.f, 0.f), dpj = mk(0.f, 0.f, 0.f);
         for (int i = c.i(H.o_al_off + b), e = c.i(H.o_al_off + b + 1); i < e; i++)
-          dpa = dpa + ld3(E.aslot + c.i(H.o_al + i) * 4);
+          dpa = dpa + ld3(E.aslot + c.i(H.o_al + i) * ASLOT_STRIDE);
         for (int i = c.i(H.o_jl_off + b), e = c.i(H.o_jl_off + b + 1); i < e; i++)
-          dpj = dpj + ld3(E.jslot + c.i(H.o_jl + i) * 8);
+          dpj = dpj + ld3(E.jslot + c.i(H.o_jl + i) * SLOT_STRIDE);
         QP q = ldqp(E.qp + b * QP_STRIDE);
         v3 vel = H.vexp * q.vel;
         vel = vel + (mk(0.f, 0.f, 0.f) + mk(H.gx, H.gy, H.gz)) * h;
@@ -682,8 +741,8 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         v3 dpp, dcp;
         q4 dpr, dcr;
         joint_apply<F_ALL>(Jc, p, q, dpp, dpr, dcp, dcr);
-        float* sp = E.jslot + (2 * j) * 8;
-        float* sc = E.jslot + (2 * j + 1) * 8;
+        float* sp = E.jslot + j * SLOT_STRIDE;
+        float* sc = E.jslot + (E.nJ + j) * SLOT_STRIDE;
         st3(sp, dpp); st4(sp + 3, dpr);
         st3(sc, dcp); st4(sc + 3, dcr);
       }
@@ -694,7 +753,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         v3 dp = mk(0.f, 0.f, 0.f);
         q4 dr{0.f, 0.f, 0.f, 0.f};
         for (int i = c.i(H.o_jl_off + b), e = c.i(H.o_jl_off + b + 1); i < e; i++) {
-          const float* s = E.jslot + c.i(H.o_jl + i) * 8;
+          const float* s = E.jslot + c.i(H.o_jl + i) * SLOT_STRIDE;
           dp = dp + ld3(s);
           dr = dr + ld4(s + 3);
         }
@@ -735,10 +794,10 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       q4 oar, obr;
       float dl = position_contact<F_ALL>(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, n, pen,
                                   oap, oar, obp, obr);
-      float* rd = E.rowd + r * 8;
+      float* rd = E.rowd + r * ROWD_STRIDE;
       st3(rd, cpos); st3(rd + 3, n); rd[6] = pen; rd[7] = dl;
-      float* sa = E.cslot + (2 * r) * 8;
-      float* sb = E.cslot + (2 * r + 1) * 8;
+      float* sa = E.cslot + r * SLOT_STRIDE;
+      float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
       st3(sa, oap); st4(sa + 3, oar);
       sa[7] = (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f;
       st3(sb, obp); st4(sb + 3, obr);
@@ -756,7 +815,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         q4 gr{0.f, 0.f, 0.f, 0.f};
         float cnt = 0.f;
         for (; i < e && (c.i(H.o_cl + i) >> 24) == g; i++) {
-          const float* s = E.cslot + (c.i(H.o_cl + i) & 0xFFFFFF) * 8;
+          const float* s = E.cslot + (c.i(H.o_cl + i) & 0xFFFFFF) * SLOT_STRIDE;
           gp = gp + ld3(s);
           gr = gr + ld4(s + 3);
           cnt += s[7];
@@ -793,12 +852,12 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       const float* ra = E.rb + R.a * RB_STRIDE;
       const float* rbb = E.rb + R.b * RB_STRIDE;
-      const float* rd = E.rowd + r * 8;
+      const float* rd = E.rowd + r * ROWD_STRIDE;
       v3 oav, oaa, obv, oba;
       velocity_contact<F_ALL>(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
                        ld3(rbb + 6), ld3(rd), ld3(rd + 3), rd[6], rd[7], oav, oaa, obv, oba);
-      float* sa = E.cslot + (2 * r) * 8;
-      float* sb = E.cslot + (2 * r + 1) * 8;
+      float* sa = E.cslot + r * SLOT_STRIDE;
+      float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
       st3(sa, oav); st3(sa + 3, oaa);
       sa[7] = (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f;
       st3(sb, obv); st3(sb + 3, oba);
@@ -814,7 +873,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         v3 gv = mk(0.f, 0.f, 0.f), ga = mk(0.f, 0.f, 0.f);
         float cnt = 0.f;
         for (; i < e && (c.i(H.o_cl + i) >> 24) == g; i++) {
-          const float* s = E.cslot + (c.i(H.o_cl + i) & 0xFFFFFF) * 8;
+          const float* s = E.cslot + (c.i(H.o_cl + i) & 0xFFFFFF) * SLOT_STRIDE;
           gv = gv + ld3(s);
           ga = ga + ld3(s + 3);
           cnt += s[7];
@@ -902,7 +961,7 @@ template <int M>
 __device__ __forceinline__ v3 gsum3(const GList<M>& g, const float* base, int stride) {
   v3 s = mk(0.f, 0.f, 0.f);
 #pragma unroll
-  for (int k = 0; k < M; k++) s = s + ld3(base + g.e[k] * stride);
+  for (int k = 0; k < M; k++) s = s + ld_v3a(base + g.e[k] * stride);
   return s;
 }
 
@@ -918,12 +977,14 @@ __device__ __forceinline__ void gsum_contact(const GList<M>& g, const float* csl
   float c0 = 0.f, c1 = 0.f;
 #pragma unroll
   for (int k = 0; k < M; k++) {
-    const float* s = cslot + (g.e[k] & 0xFFFFFF) * 8;
+    const float* s = cslot + (g.e[k] & 0xFFFFFF) * SLOT_STRIDE;
     float m0 = (g.e[k] >> 24) == g0 ? 1.f : 0.f;
     float m1 = 1.f - m0;
-    v3 v = ld3(s);
-    q4 q = rot4 ? ld4(s + 3) : q4{0.f, s[3], s[4], s[5]};
-    float f = s[7];
+    v3 v;
+    q4 q;
+    float f;
+    ld_slot(s, v, q, f);
+    if (!rot4) q = q4{0.f, q.w, q.x, q.y};
     a0 = a0 + v * m0;
     a1 = a1 + v * m1;
     r0 = r0 + q * m0;
@@ -997,10 +1058,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     for (int sub = 0; sub < 2; sub++) {
       ppos = q.pos;
       prot = q.rot;
-      if (sub == 1 && X.hasB) {
-        st3(E.prev + lane * PREV_STRIDE, ppos);
-        st4(E.prev + lane * PREV_STRIDE + 3, prot);
-      }
+      if (sub == 1 && X.hasB) st_slot(E.prev + lane * PREV_STRIDE, ppos, prot, 0.f);
       // actuators + damping (actuator a drives joint a when H.act_same)
       if (X.hasA) {
         const ActC& A = X.A;
@@ -1013,15 +1071,15 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       }
       if (X.hasJ) {
         const JointC& Jc = X.J;
-        v3 tq = -1.f * Jc.damping * (ld3(E.qp + Jc.bp * QP_STRIDE + 10) - ld3(E.qp + Jc.bc * QP_STRIDE + 10));
-        st3(E.jslot + (2 * lane) * 8, mul(Jc.Ip, tq));
-        st3(E.jslot + (2 * lane + 1) * 8, -1.f * mul(Jc.Ic, tq));
+        v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
+        st_v3a(E.jslot + lane * SLOT_STRIDE, mul(Jc.Ip, tq));
+        st_v3a(E.jslot + (E.nJ + lane) * SLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
       }
       sync();
       BX_STAMP(0);
       if (X.hasB) {
-        v3 dpa = gsum3(X.al, E.aslot, 4);
-        v3 dpj = gsum3(X.jl, E.jslot, 8);
+        v3 dpa = gsum3(X.al, E.aslot, ASLOT_STRIDE);
+        v3 dpj = gsum3(X.jl, E.jslot, SLOT_STRIDE);
         v3 vel = H.vexp * q.vel;
         vel = vel + (mk(0.f, 0.f, 0.f) + g) * h;
         q.vel = mul(vel, X.B.pm);
@@ -1045,10 +1103,8 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         v3 dpp, dcp;
         q4 dpr, dcr;
         joint_apply<F>(Jc, p, cq, dpp, dpr, dcp, dcr);
-        float* sp = E.jslot + (2 * lane) * 8;
-        float* sc = E.jslot + (2 * lane + 1) * 8;
-        st3(sp, dpp); st4(sp + 3, dpr);
-        st3(sc, dcp); st4(sc + 3, dcr);
+        st_slot(E.jslot + lane * SLOT_STRIDE, dpp, dpr, 0.f);
+        st_slot(E.jslot + (E.nJ + lane) * SLOT_STRIDE, dcp, dcr, 0.f);
       }
       sync();
       BX_STAMP(2);
@@ -1057,9 +1113,12 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         q4 dr{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < M; k++) {
-          const float* s = E.jslot + X.jl.e[k] * 8;
-          dp = dp + ld3(s);
-          dr = dr + ld4(s + 3);
+          v3 v;
+          q4 r;
+          float f;
+          ld_slot(E.jslot + X.jl.e[k] * SLOT_STRIDE, v, r, f);
+          dp = dp + v;
+          dr = dr + r;
         }
         q.pos = q.pos + mul(dp, X.B.pm);
         q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
@@ -1078,20 +1137,21 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cvel;
       contact_gen<F>(R, a, b, cpos, cvel, cn, pen);
-      const float* pa = E.prev + R.a * PREV_STRIDE;
-      const float* pb = E.prev + R.b * PREV_STRIDE;
+      v3 pap, pbp;
+      q4 par, pbr;
+      float unused;
+      ld_slot(E.prev + R.a * PREV_STRIDE, pap, par, unused);
+      ld_slot(E.prev + R.b * PREV_STRIDE, pbp, pbr, unused);
       v3 oap, obp;
       q4 oar, obr;
-      dl = position_contact<F>(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, cn, pen, oap,
-                            oar, obp, obr);
-      float* rd = E.rowd + lane * 8;
-      st3(rd, cpos); st3(rd + 3, cn); rd[6] = pen; rd[7] = dl;
-      float* sa = E.cslot + (2 * lane) * 8;
-      float* sb = E.cslot + (2 * lane + 1) * 8;
-      st3(sa, oap); st4(sa + 3, oar);
-      sa[7] = (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f;
-      st3(sb, obp); st4(sb + 3, obr);
-      sb[7] = (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f;
+      dl = position_contact<F>(R, a, b, pap, par, pbp, pbr, cpos, cn, pen, oap, oar, obp, obr);
+      float* rd = E.rowd + lane * ROWD_STRIDE;
+      st4a(rd, f32x4{cpos.x, cpos.y, cpos.z, cn.x});
+      st4a(rd + 4, f32x4{cn.y, cn.z, pen, dl});
+      st_slot(E.cslot + lane * SLOT_STRIDE, oap, oar,
+              (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f);
+      st_slot(E.cslot + (E.nR + lane) * SLOT_STRIDE, obp, obr,
+              (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f);
     }
     sync();
     BX_STAMP(4);
@@ -1102,8 +1162,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       q.pos = q.pos + mul(dp, X.B.pm);
       q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                  q.rot.z + dr.z * X.B.qm.z};
-      float* rb = E.rb + lane * RB_STRIDE;
-      st3(rb, q.pos); st3(rb + 3, q.vel); st3(rb + 6, q.ang);
+      st_rb(E.rb + lane * RB_STRIDE, q.pos, q.vel, q.ang);
       vproj(q, ppos, prot, X.B, h);
       stqp(myqp, q);
     }
@@ -1112,17 +1171,16 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     if (X.hasR) {
       const RowC& R = X.R;
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
-      const float* ra = E.rb + R.a * RB_STRIDE;
-      const float* rbb = E.rb + R.b * RB_STRIDE;
+      v3 rap, rav, raa, rbp, rbv, rba;
+      ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
+      ld_rb(E.rb + R.b * RB_STRIDE, rbp, rbv, rba);
       v3 oav, oaa, obv, oba;
-      velocity_contact<F>(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
-                       ld3(rbb + 6), cpos, cn, pen, dl, oav, oaa, obv, oba);
-      float* sa = E.cslot + (2 * lane) * 8;
-      float* sb = E.cslot + (2 * lane + 1) * 8;
-      st3(sa, oav); st3(sa + 3, oaa);
-      sa[7] = (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f;
-      st3(sb, obv); st3(sb + 3, oba);
-      sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
+      velocity_contact<F>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos, cn, pen, dl, oav, oaa, obv,
+                          oba);
+      st_slot(E.cslot + lane * SLOT_STRIDE, oav, q4{oaa.x, oaa.y, oaa.z, 0.f},
+              (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f);
+      st_slot(E.cslot + (E.nR + lane) * SLOT_STRIDE, obv, q4{oba.x, oba.y, oba.z, 0.f},
+              (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f);
     }
     sync();
     BX_STAMP(6);
@@ -1171,8 +1229,8 @@ __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane)
     contact_gen<F_ALL>(R, a, b, cpos, cvel, n, pen);
     v3 oav, oaa, obv, oba;
     impulse_contact<F_ALL>(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
-    float* sa = E.cslot + (2 * r) * 8;
-    float* sb = E.cslot + (2 * r + 1) * 8;
+    float* sa = E.cslot + r * SLOT_STRIDE;
+    float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
     st3(sa, oav); st3(sa + 3, oaa);
     sa[7] = (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f;
     st3(sb, obv); st3(sb + 3, oba);
@@ -1187,7 +1245,7 @@ __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane)
       v3 gv = mk(0.f, 0.f, 0.f), ga = mk(0.f, 0.f, 0.f);
       float cnt = 0.f;
       for (; i < e && (c.i(H.o_cl + i) >> 24) == g; i++) {
-        const float* s = E.cslot + (c.i(H.o_cl + i) & 0xFFFFFF) * 8;
+        const float* s = E.cslot + (c.i(H.o_cl + i) & 0xFFFFFF) * SLOT_STRIDE;
         gv = gv + ld3(s);
         ga = ga + ld3(s + 3);
         cnt += s[7];
@@ -1379,7 +1437,7 @@ __device__ __forceinline__ float* stage_constants(const uint32_t* blob, const Bl
 
 template <int L, int MODE, int F, int M>
 __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
-  extern __shared__ float smem[];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
   Cst c{A.blob};
   float* ebase = stage_constants<MODE>(A.blob, H, smem, c);
@@ -1431,7 +1489,7 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
     }
   }
   for (int r = lane; r < H.R; r += L) {
-    const float* rd = E.rowd + r * 8;
+    const float* rd = E.rowd + r * ROWD_STRIDE;
     if (A.info.contact_pos) st3(A.info.contact_pos + (e * H.R + r) * 3, ld3(rd));
     if (A.info.contact_normal) st3(A.info.contact_normal + (e * H.R + r) * 3, ld3(rd + 3));
     if (A.info.contact_penetration) A.info.contact_penetration[e * H.R + r] = rd[6];
@@ -1443,7 +1501,7 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
 // Env.step fused with EpisodeWrapper/AutoResetWrapper (wrappers.py:105-148)
 template <int L, int MODE, int F, int M>
 __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
-  extern __shared__ float smem[];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
   Cst c{A.blob};
   float* ebase = stage_constants<MODE>(A.blob, H, smem, c);
@@ -1583,7 +1641,7 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
 // System.info contact part + optional Env._get_obs of the same state (reset)
 template <int L>
 __global__ void __launch_bounds__(64) info_obs_kernel(InfoArgs A) {
-  extern __shared__ float smem[];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   Cst c{A.blob};
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
   const int lane = threadIdx.x % L;
@@ -1626,7 +1684,7 @@ __global__ void __launch_bounds__(64) info_obs_kernel(InfoArgs A) {
 
 
 __global__ void __launch_bounds__(64) default_qp_kernel(ResetArgs A) {
-  extern __shared__ float smem[];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   Cst c{A.blob};
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
   const int64_t e = (int64_t)blockIdx.x * 64 + threadIdx.x;

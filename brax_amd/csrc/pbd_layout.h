@@ -33,7 +33,21 @@ enum {
   FK_BP = 0, FK_BC = 1, FK_IDX = 2, FK_ROT = 5, FK_REF = 9, FK_OFFP = 13, FK_OFFC = 16,
 };
 // per-env LDS record strides (floats)
-enum { QP_STRIDE = 16, PREV_STRIDE = 8, RB_STRIDE = 12, ACC_STRIDE = 12 };
+// LDS record strides (words). Every stride is 4 x an odd number of words, so
+// consecutive lanes' 16-byte records cover distinct bank slots: conflict-free
+// for ds_read_b128 (16-lane groups, 64 banks) and ds_write_b128 (8-lane
+// groups, 32 banks) when lane i touches record i (MI355X_MICROARCH.md §LDS).
+// Slot regions hold parent/a-side records first, then child/b-side records,
+// then one zero record: slot(j) = j, slot'(j) = n + j, zero = 2n.
+enum {
+  QP_STRIDE = 20,
+  PREV_STRIDE = 12,
+  RB_STRIDE = 12,
+  ACC_STRIDE = 12,
+  SLOT_STRIDE = 12,   // joint and contact slots: dp pos 3, dq rot 4, count 1
+  ASLOT_STRIDE = 4,   // actuator slots: dang 3
+  ROWD_STRIDE = 12    // contact row data: cpos 3, normal 3, pen, dlambda
+};
 enum { ACC_ICV = 0, ACC_ICA = 3, ACC_IAA = 6, ACC_DPA = 9 };
 
 struct BlobHdr {

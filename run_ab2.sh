@@ -12,7 +12,7 @@ done
 for rep in 1 2; do
 for lib in "$@"; do
   export BRAX_AMD_LIB=$PWD/$lib
-  timeout -k 10 120 python bench.py --steps 500 --warmup 50 --no-cpu-baseline > gpurun_out/bench_ab.log 2>&1 || exit $?
+  timeout -k 10 120 python bench.py --steps 500 --warmup 50 --no-cpu-baseline --no-phases > gpurun_out/bench_ab.log 2>&1 || exit $?
   python -c "import json;d=json.loads(open('gpurun_out/bench_ab.log').read().strip().splitlines()[-1]);print('$lib', round(d['value']/1e6,2),'M/s kernel_ms',round(d['roofline']['kernel_ms'],4),'ms/step',round(d['ms_per_step'],4))"
 done
 done
