@@ -631,7 +631,12 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
   return E;
 }
 
-__device__ __forceinline__ void sync() { __syncthreads(); }
+// Phase boundary inside one env block. Every kernel that calls this runs
+// 64-thread workgroups = ONE wavefront, and a wavefront's LDS instructions
+// execute in issue order, so a lane's ds_read issued after another lane's
+// ds_write sees it without draining lgkmcnt. Only the compiler must not move
+// or forward memory accesses across the boundary.
+__device__ __forceinline__ void sync() { asm volatile("" ::: "memory"); }
 
 // the zero slots that padded gather-list entries point at
 __device__ __forceinline__ void zero_slots(const Env& E, const BlobHdr& H, int lane) {
