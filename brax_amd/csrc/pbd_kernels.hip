@@ -16,6 +16,7 @@
 // the action and the env-layer outputs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "pbd_launch.h"
 #include "pbd_layout.h"
@@ -1016,7 +1017,9 @@ __device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, f
 }
 
 #ifdef BX_STAMPS
-__device__ unsigned long long bx_stamp_sum[16];
+// per-workgroup accumulators (no atomics: contended atomics inside the timed
+// windows distort them); summed on the host by debug_stamps
+__device__ unsigned long long bx_stamp_wave[4096][16];
 #define BX_STAMP(k)                                                                \
   do {                                                                             \
     __builtin_amdgcn_sched_barrier(0);                                             \
@@ -1026,8 +1029,25 @@ __device__ unsigned long long bx_stamp_sum[16];
     st_acc[k] += _t - st_last;                                                     \
     st_last = _t;                                                                  \
   } while (0)
+// kernel-level stamps (env_step_kernel): slots 10..14
+#define BX_KSTAMP_DECL                                                             \
+  unsigned long long kst_last, kst_acc[5] = {0, 0, 0, 0, 0};                       \
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(kst_last)::"memory");
+#define BX_KSTAMP(k)                                                               \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long _t;                                                         \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    kst_acc[(k) - 10] += _t - kst_last;                                            \
+    kst_last = _t;                                                                 \
+    if ((k) == 14 && threadIdx.x == 0)                                             \
+      for (int _i = 0; _i < 5; _i++) bx_stamp_wave[blockIdx.x & 4095][10 + _i] += kst_acc[_i]; \
+  } while (0)
 #else
 #define BX_STAMP(k) do {} while (0)
+#define BX_KSTAMP_DECL
+#define BX_KSTAMP(k) do {} while (0)
 #endif
 
 template <int L, int F, int M>
@@ -1215,8 +1235,8 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
 #ifdef BX_STAMPS
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int k = 0; k < 10; k++) atomicAdd(&bx_stamp_sum[k], st_acc[k]);
-    atomicAdd(&bx_stamp_sum[15], 1ull);
+    for (int k = 0; k < 10; k++) bx_stamp_wave[blockIdx.x & 4095][k] += st_acc[k];
+    bx_stamp_wave[blockIdx.x & 4095][15] += 1ull;
   }
 #endif
 }
@@ -1506,6 +1526,7 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
 // Env.step fused with EpisodeWrapper/AutoResetWrapper (wrappers.py:105-148)
 template <int L, int MODE, int F, int M>
 __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
+  BX_KSTAMP_DECL
   extern __shared__ __attribute__((aligned(16))) float smem[];
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
   Cst c{A.blob};
@@ -1542,6 +1563,7 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   float sq = 0.f;
   if (valid && lane == 0)
     for (int i = 0; i < H.A; i++) sq += act[i] * act[i];
+  BX_KSTAMP(10);
   for (int rep = 0; rep < reps; rep++) {
     v3 pos0 = ld3(E.qp);  // torso position before the step
     v3 com0 = mk(0.f, 0.f, 0.f);
@@ -1554,7 +1576,9 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
     } else {
       pbd_step<L>(c, H, E, lane, valid, act);
     }
+    BX_KSTAMP(11);
     env_observe<L>(c, H, E, lane, kind, P.obs_size, act, valid, valid ? A.out.obs + e * P.obs_size : nullptr);
+    BX_KSTAMP(12);
     // reward / done / metrics (lane 0 of the env)
     if (lane == 0 && valid) {
       const float dt = H.dt;
@@ -1611,6 +1635,7 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
     }
     sync();
   }
+  BX_KSTAMP(13);
   if (!valid) return;
   done = E.red[0];
   float trunc = 0.f;
@@ -1639,6 +1664,7 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   } else {
     for (int b = lane; b < H.N; b += L) store_qp_global(A.out.qp, e, b, E.qp + b * QP_STRIDE);
   }
+  BX_KSTAMP(14);
 }
 
 
@@ -1844,10 +1870,15 @@ hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
 
 hipError_t debug_stamps(unsigned long long* out, int reset) {
 #ifdef BX_STAMPS
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(bx_stamp_sum), 16 * sizeof(unsigned long long));
+  static unsigned long long host[4096][16];
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(bx_stamp_wave), sizeof(host));
+  for (int k = 0; k < 16; k++) {
+    out[k] = 0;
+    for (int w = 0; w < 4096; w++) out[k] += host[w][k];
+  }
   if (e == hipSuccess && reset) {
-    unsigned long long z[16] = {0};
-    e = hipMemcpyToSymbol(HIP_SYMBOL(bx_stamp_sum), z, sizeof(z));
+    memset(host, 0, sizeof(host));
+    e = hipMemcpyToSymbol(HIP_SYMBOL(bx_stamp_wave), host, sizeof(host));
   }
   return e;
 #else

@@ -31,3 +31,9 @@ print('samples', n, 'cycles/wave/step', tot / max(n, 1))
 for i, nm in enumerate(names):
   if v[i]:
     print(f'{nm:20s} {100 * v[i] / tot:5.1f}%  {v[i] / max(n, 1):9.0f} cyc')
+k = np.array(buf[10:15], dtype=np.float64)
+kn = ['prologue (consts, QP/act loads)', 'pbd step', 'observation', 'reward/metrics', 'epilogue (stores)']
+kt = k.sum()
+print('kernel cycles/wave/step', kt / max(n, 1))
+for i, nm in enumerate(kn):
+  print(f'{nm:32s} {100 * k[i] / kt:5.1f}%  {k[i] / max(n, 1):9.0f} cyc')
