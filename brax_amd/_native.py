@@ -36,16 +36,17 @@ _SIGS = {
     'bx_system_set_single': ([C.c_void_p, C.c_int], C.c_int),
     'bx_system_set_variant': ([C.c_void_p, C.c_int, C.c_int], C.c_int),
     'bx_system_step': ([C.c_void_p, C.c_int64, C.POINTER(abi.BxQP), C.c_void_p, C.c_int64,
-                        C.POINTER(abi.BxQP), C.POINTER(abi.BxInfo), C.c_void_p], C.c_int),
+                        C.c_int64, C.POINTER(abi.BxQP), C.POINTER(abi.BxInfo), C.c_void_p],
+                       C.c_int),
     'bx_env_step': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64,
-                     C.POINTER(abi.BxEnvState), C.c_void_p, C.c_int64,
+                     C.POINTER(abi.BxEnvState), C.c_void_p, C.c_int64, C.c_int64,
                      C.POINTER(abi.BxEnvState), C.c_void_p], C.c_int),
     'bx_system_default_qp': ([C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                               C.POINTER(abi.BxQP), C.c_void_p], C.c_int),
     'bx_system_info': ([C.c_void_p, C.c_int64, C.POINTER(abi.BxQP), C.POINTER(abi.BxInfo),
                         C.c_void_p], C.c_int),
     'bx_env_observe': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64,
-                        C.POINTER(abi.BxQP), C.c_void_p, C.c_int64, C.c_void_p,
+                        C.POINTER(abi.BxQP), C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
                         C.c_void_p], C.c_int),
     'bx_phase': ([C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
                   C.c_void_p, C.c_int64, C.c_void_p], C.c_int),
@@ -73,7 +74,7 @@ def lib():
       f = getattr(l, name)
       f.argtypes = args
       f.restype = res
-    if l.bx_abi_version() != 1:
+    if l.bx_abi_version() != abi.ABI_VERSION:
       raise NativeError('libbrax_amd ABI version mismatch')
     _lib = l
   return _lib

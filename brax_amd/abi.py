@@ -12,6 +12,8 @@ i32p = C.POINTER(C.c_int32)
 f64p = C.POINTER(C.c_double)
 f32p = C.POINTER(C.c_float)
 
+ABI_VERSION = 2  # include/brax_amd.h BX_ABI_VERSION
+
 _DESC_FIELDS = [
     ('n_bodies', C.c_int32), ('n_joints', C.c_int32), ('n_actuators', C.c_int32),
     ('n_rows', C.c_int32), ('n_groups', C.c_int32),
@@ -33,6 +35,8 @@ _DESC_FIELDS = [
     ('row_a_pos', f64p), ('row_a_end', f64p), ('row_a_radius', f64p),
     ('row_b_pos', f64p), ('row_b_end', f64p), ('row_b_radius', f64p),
     ('row_friction', f64p), ('row_elasticity', f64p),
+    ('n_forces', C.c_int32), ('force_type', i32p), ('force_body', i32p),
+    ('force_index', i32p), ('force_strength', f64p),
 ]
 
 
@@ -98,6 +102,7 @@ def make_desc(d):
   s.n_actuators = len(d['act_type'])
   s.n_rows = len(d['row_group'])
   s.n_groups = len(d['col_oneway'])
+  s.n_forces = len(d.get('force_type', ()))
   s.substeps = int(d['substeps'])
   s.action_size = int(d.get('action_size', 0))
   s.num_joint_dof = int(d.get('num_joint_dof', 0))
@@ -109,7 +114,8 @@ def make_desc(d):
   s.angular_damping = float(d['angular_damping'])
   for name, ctype in _DESC_FIELDS:
     if ctype is i32p or ctype is f64p:
-      a = _arr(d[name], np.int32 if ctype is i32p else np.float64)
+      v = d[name] if name in d or not name.startswith('force_') else np.zeros(0)
+      a = _arr(v, np.int32 if ctype is i32p else np.float64)
       keep.append(a)
       setattr(s, name, a.ctypes.data_as(ctype))
   return s, keep

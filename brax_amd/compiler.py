@@ -395,25 +395,40 @@ def _actuators(config, jmeta):
   return d, current
 
 
-def _forces(config, index, act_offset):
-  """Thruster/Twister groups (`forces.py:110-138`): act tail after joints."""
-  F = {'type': [], 'body': [], 'strength': [], 'index': []}
-  groups = {}
+def _forces(config, index):
+  """Thruster/Twister groups (`forces.py:110-138`).
+
+  Action indices continue after the ACTUATORS' dofs, counted on the joints as
+  they stand after sphericalisation (`forces.py:114-116`; joints.get has
+  already mutated the config), and are assigned in config order; the groups
+  then apply Thrusters first, Twisters second (`forces.py:130-136`)."""
+  dofs = {j.name: len(j.angle_limit) for j in config.joints}
+  cur = sum(dofs[a.joint] for a in config.actuators)
+  start = cur
+  items = {'thruster': [], 'twister': []}
   for f in config.forces:
     kind = f.WhichOneof('type')
-    groups.setdefault(kind, []).append(f)
-  cur = act_offset
-  for kind in sorted(groups):
-    for f in groups[kind]:
-      F['type'].append(THRUSTER if kind == 'thruster' else TWISTER)
+    if kind not in items:
+      raise ValueError(f'unknown force type: {kind}')
+    if f.body not in index:
+      raise KeyError(f.body)
+    items[kind].append((f, [cur, cur + 1, cur + 2]))
+    cur += 3
+  F = {'type': [], 'body': [], 'strength': [], 'index': []}
+  for kind, code in (('thruster', THRUSTER), ('twister', TWISTER)):
+    for f, idx in items[kind]:
+      F['type'].append(code)
       F['body'].append(index[f.body])
       F['strength'].append(f.strength)
-      F['index'].append([cur, cur + 1, cur + 2])
-      cur += 3
+      F['index'].append(idx)
+  # num_forces_dof = sum(f.act_index.shape[-1] for f in forces) (system.py:72)
+  # counts 3 per force GROUP, not per force: with several Thrusters the
+  # action is shorter than their index range and the tail clips (jp.take)
+  n_dof = 3 * sum(1 for kind in items if items[kind])
   return {'force_type': np.asarray(F['type'], np.int32),
           'force_body': np.asarray(F['body'], np.int32),
           'force_strength': np.asarray(F['strength'], np.float64),
-          'force_index': np.asarray(F['index'], np.int32).reshape(-1, 3)}, cur - act_offset
+          'force_index': np.asarray(F['index'], np.int32).reshape(-1, 3)}, n_dof
 
 
 def compile_system(config):
@@ -437,11 +452,8 @@ def compile_system(config):
   d.update(jd)
   ad, _ = _actuators(config, jmeta)
   d.update(ad)
-  fd, n_force_dof = _forces(config, index, num_joint_dof)
+  fd, n_force_dof = _forces(config, index)
   d.update(fd)
-  if len(fd['force_type']):
-    raise NotImplementedError('Thruster/Twister forces are not on the kernel '
-                              'path yet (SURVEY §8 a26)')
   d['num_joint_dof'] = np.int32(num_joint_dof)
   d['action_size'] = np.int32(num_joint_dof + n_force_dof)
   meta = dict(num_joint_dof=num_joint_dof, num_forces_dof=n_force_dof,

@@ -46,7 +46,7 @@ struct bx_system {
   int L = 16;       // lanes per env
   int min_L = 16;
   int mode = 0;     // MODE_GLOBAL / MODE_SINGLE / MODE_LDS
-  int feat = 15;    // F_SPH | F_ANGLE | F_CC | F_TW used by this system
+  int feat = 31;    // F_SPH | F_ANGLE | F_CC | F_TW | F_FORCE used by this system
   int gw = 8;       // gather width (max per-body list length, 4 or 8)
   bool single_ok = false;
   size_t lds_env = 0;    // bytes per block for the per-env kernels
@@ -90,6 +90,13 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     int fn = d->col_fn[d->row_group[x]];
     if (fn != BX_COL_CAPSULE_PLANE && fn != BX_COL_CAPSULE_CAPSULE)
       return fail("unsupported contact function");
+  }
+  for (int f = 0; f < d->n_forces; f++) {
+    if (d->force_body[f] < 0 || d->force_body[f] >= N) return fail("force body out of range");
+    if (d->force_type[f] != BX_FORCE_THRUSTER && d->force_type[f] != BX_FORCE_TWISTER)
+      return fail("unknown force type");
+    if (f > 0 && d->force_type[f] < d->force_type[f - 1])
+      return fail("forces must be ordered Thrusters, then Twisters");
   }
   if (G >= 128) return fail("too many collider groups");
   if (2 * R >= (1 << 24)) return fail("too many contact rows");
@@ -176,6 +183,16 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     B.f(o + R_SCALE, d->col_scale[g]);
     B.f(o + R_THR, d->col_velocity_threshold[g]);
     B.f(o + R_ERP, d->col_baumgarte_erp[g]);
+  }
+  H.NF = d->n_forces;
+  H.o_force = B.alloc(d->n_forces * FORCE_STRIDE);
+  for (int f = 0; f < d->n_forces; f++) {
+    int o = H.o_force + f * FORCE_STRIDE;
+    B.i(o + F_TYPE, d->force_type[f]);
+    B.i(o + F_BODY, d->force_body[f]);
+    for (int k = 0; k < 3; k++) B.i(o + F_IDX + k, d->force_index[3 * f + k]);
+    B.f(o + F_STR, d->force_strength[f]);
+    B.f(o + F_MASS, d->body_mass[d->force_body[f]]);
   }
   // gather lists (the reference's segment_sum order: per group, parents then
   // children / a-rows then b-rows)
@@ -320,6 +337,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       if (d->col_fn[g] != BX_COL_CAPSULE_PLANE) f |= 4;
       if (!d->col_oneway[g]) f |= 8;
     }
+    if (d->n_forces > 0) f |= 16;
     S->feat = f;
   }
   S->mode = S->single_ok ? 1 : 0;
@@ -415,12 +433,22 @@ int bx_system_set_variant(bx_system* S, int lanes, int mode) {
   return 0;
 }
 
+// the step reads actions through jp.take-style clipped indices (jumpy.py:151):
+// any positive width is valid, 0 only when the system reads no action
+static int check_act(const bx_system* S, const float* act, int64_t act_stride, int64_t act_width) {
+  const bool reads = S->hdr.K > 0 || S->hdr.NF > 0;
+  if (act_width < 0 || act_stride < 0) return fail("negative action width or stride");
+  if (reads && (!act || act_width == 0)) return fail("null or empty action");
+  return 0;
+}
+
 int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* act,
-                   int64_t act_stride, const bx_qp* qout, const bx_info* info, void* stream) {
+                   int64_t act_stride, int64_t act_width, const bx_qp* qout, const bx_info* info,
+                   void* stream) {
   if (!S || !qin || !qout) return fail("null argument");
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
   if (!qp_ok(*qin) || !qp_ok(*qout)) return fail("null qp field");
-  if (S->hdr.A > 0 && !act) return fail("null action");
+  if (check_act(S, act, act_stride, act_width)) return 1;
   StepArgs a{};
   a.blob = S->blob;
   a.n_envs = n_envs;
@@ -428,14 +456,17 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   a.qout = *qout;
   a.act = act;
   a.act_stride = act_stride;
+  a.act_width = act_width;
   if (info) a.info = *info;
   HIP_OK(launch_system_step(S->L, S->mode, S->feat, S->gw, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
 }
 
 int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx_env_state* in,
-                const float* act, int64_t act_stride, const bx_env_state* out, void* stream) {
+                const float* act, int64_t act_stride, int64_t act_width, const bx_env_state* out,
+                void* stream) {
   if (!S || !env || !in || !out) return fail("null argument");
+  if (check_act(S, act, act_stride, act_width)) return 1;
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
   if (!qp_ok(in->qp) || !qp_ok(out->qp)) return fail("null qp field");
   if (!in->done || !out->done || !out->reward || !out->obs) return fail("null env buffer");
@@ -452,6 +483,7 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   a.out = *out;
   a.act = act;
   a.act_stride = act_stride;
+  a.act_width = act_width;
   HIP_OK(launch_env_step(S->L, S->mode, S->feat, S->gw, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
 }
@@ -469,7 +501,8 @@ int bx_system_info(bx_system* S, int64_t n_envs, const bx_qp* qp, const bx_info*
 }
 
 int bx_env_observe(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx_qp* qp,
-                   const float* act, int64_t act_stride, float* obs, void* stream) {
+                   const float* act, int64_t act_stride, int64_t act_width, float* obs,
+                   void* stream) {
   if (!S || !env || !qp || !obs) return fail("null argument");
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
   InfoArgs a{};
@@ -480,6 +513,7 @@ int bx_env_observe(bx_system* S, const bx_env_params* env, int64_t n_envs, const
   a.obs_size = env->obs_size;
   a.act = act;
   a.act_stride = act_stride;
+  a.act_width = act_width;
   a.obs = obs;
   HIP_OK(launch_info_obs(S->L, n_envs, S->lds_env, as_stream(stream), a));
   return 0;

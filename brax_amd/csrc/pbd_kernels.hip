@@ -176,7 +176,7 @@ __device__ __forceinline__ JointC load_joint(const Cst& c, const BlobHdr& H, int
 // joint / actuator / contact kinds it uses (Ant: revolute + torque + one-way
 // capsule-plane), which keeps dead paths out of the register allocation.
 // ---------------------------------------------------------------------------
-enum { F_SPH = 1, F_ANGLE = 2, F_CC = 4, F_TW = 8, F_ALL = 15 };
+enum { F_SPH = 1, F_ANGLE = 2, F_CC = 4, F_TW = 8, F_FORCE = 16, F_ALL = 31 };
 template <int F> __device__ __forceinline__ bool is_rev(int type) {
   if constexpr ((F & F_SPH) == 0) return true; else return type == 1;
 }
@@ -319,6 +319,30 @@ __device__ __forceinline__ ActC load_act(const Cst& c, const BlobHdr& H, int a) 
 // ---------------------------------------------------------------------------
 // contacts (brax/physics/colliders.py)
 // ---------------------------------------------------------------------------
+// jp.take(act, index) with mode='clip' (jumpy.py:146-151): -1 -> 0, >= width -> last
+__device__ __forceinline__ int take_idx(int i, int w) { return i < 0 ? 0 : (i >= w ? w - 1 : i); }
+
+// dp_f of body b (forces.py:41-107), constant over a step: Thruster
+// dvel = a * strength / mass, Twister dang = a * strength / mass (the body's
+// MASS, forces.py:85), each segment-summed over the body in application order
+__device__ __forceinline__ void body_forces(const Cst& c, const BlobHdr& H, int b, const float* act,
+                                            int aw, bool valid, v3& fv, v3& fa) {
+  fv = mk(0.f, 0.f, 0.f);
+  fa = mk(0.f, 0.f, 0.f);
+  for (int f = 0; f < H.NF; f++) {
+    const int o = H.o_force + f * FORCE_STRIDE;
+    if (c.i(o + F_BODY) != b) continue;
+    const float st = c.f(o + F_STR), m = c.f(o + F_MASS);
+    v3 a = mk(0.f, 0.f, 0.f);
+    if (valid)
+      a = mk(act[take_idx(c.i(o + F_IDX), aw)], act[take_idx(c.i(o + F_IDX + 1), aw)],
+             act[take_idx(c.i(o + F_IDX + 2), aw)]);
+    v3 d = mk(a.x * st / m, a.y * st / m, a.z * st / m);
+    if (c.i(o + F_TYPE) == BX_FORCE_THRUSTER) fv = fv + d;
+    else fa = fa + d;
+  }
+}
+
 struct RowC {
   int group, a, b, fn, oneway;
   v3 a_pos, a_end, b_pos, b_end;
@@ -675,7 +699,7 @@ __device__ __forceinline__ void store_qp_global(const bx_qp& q, int64_t e, int b
 // ---------------------------------------------------------------------------
 template <int L>
 __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
-                         const float* act) {
+                         const float* act, int aw) {
   const int N = H.N, J = H.J, K = H.K, Rn = H.R;
   const float h = H.h;
   for (int b = lane; b < N; b += L) {
@@ -698,7 +722,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
 #pragma unroll
         for (int l = 0; l < 3; l++) {
           int ai = A.idx[l];
-          al[l] = valid ? act[ai < 0 ? 0 : ai] * (ai >= 0 ? 1.f : 0.f) : 0.f;
+          al[l] = valid ? act[take_idx(ai, aw)] * (ai >= 0 ? 1.f : 0.f) : 0.f;
         }
         act_torque<F_ALL>(Jc, A, E, al, a);
       }
@@ -722,11 +746,13 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         for (int i = c.i(H.o_jl_off + b), e = c.i(H.o_jl_off + b + 1); i < e; i++)
           dpj = dpj + ld3(E.jslot + c.i(H.o_jl + i) * SLOT_STRIDE);
         QP q = ldqp(E.qp + b * QP_STRIDE);
+        v3 fv, fa;  // dp_f (forces.py), acc_p = (dp_a + dp_f) + dp_j (system.py:268-271)
+        body_forces(c, H, b, act, aw, valid, fv, fa);
         v3 vel = H.vexp * q.vel;
-        vel = vel + (mk(0.f, 0.f, 0.f) + mk(H.gx, H.gy, H.gz)) * h;
+        vel = vel + (fv + mk(H.gx, H.gy, H.gz)) * h;
         vel = mul(vel, B.pm);
         v3 ang = H.aexp * q.ang;
-        ang = ang + ((dpa + mk(0.f, 0.f, 0.f)) + dpj) * h;
+        ang = ang + ((dpa + fa) + dpj) * h;
         ang = mul(ang, B.rm);
         q.vel = vel;
         q.ang = ang;
@@ -1052,7 +1078,8 @@ __device__ unsigned long long bx_stamp_wave[4096][16];
 
 template <int L, int F, int M>
 __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
-                                const float* act, const Hoist<M>& X, v3& icv, v3& ica, v3& iaa) {
+                                const float* act, int aw, const Hoist<M>& X, v3& icv, v3& ica,
+                                v3& iaa) {
 #ifdef BX_STAMPS
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last;
@@ -1072,8 +1099,13 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
 #pragma unroll
     for (int l = 0; l < 3; l++) {
       int ai = X.A.idx[l];
-      al[l] = act[ai < 0 ? 0 : ai] * (ai >= 0 ? 1.f : 0.f);
+      al[l] = act[take_idx(ai, aw)] * (ai >= 0 ? 1.f : 0.f);
     }
+  }
+  // dp_f of the lane's body: constant over the step (depends on the action only)
+  v3 fv = mk(0.f, 0.f, 0.f), fa = mk(0.f, 0.f, 0.f);
+  if constexpr ((F & F_FORCE) != 0) {
+    if (X.hasB) body_forces(c, H, lane, act, aw, valid, fv, fa);
   }
   for (int it = 0; it < H.substeps / 2; it++) {
     v3 ppos = q.pos;
@@ -1106,10 +1138,10 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         v3 dpa = gsum3(X.al, E.aslot, ASLOT_STRIDE);
         v3 dpj = gsum3(X.jl, E.jslot, SLOT_STRIDE);
         v3 vel = H.vexp * q.vel;
-        vel = vel + (mk(0.f, 0.f, 0.f) + g) * h;
+        vel = vel + (fv + g) * h;
         q.vel = mul(vel, X.B.pm);
         v3 an = H.aexp * q.ang;
-        an = an + ((dpa + mk(0.f, 0.f, 0.f)) + dpj) * h;
+        an = an + ((dpa + fa) + dpj) * h;
         q.ang = mul(an, X.B.rm);
         q.pos = q.pos + mul(q.vel * h, X.B.pm);
         v3 am = mul(q.ang, X.B.rm);
@@ -1327,7 +1359,7 @@ __device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3
 
 // observation element i of the env kind
 __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind, int i,
-                          const float* act, bool valid) {
+                          const float* act, int aw, bool valid) {
   const int N = H.N, D = H.D;
   const float* q0 = E.qp;
   if (kind == BX_ENV_ANT) {
@@ -1409,8 +1441,7 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
     ActC A = load_act(c, H, a);
     int dof = c.i(H.o_joint + A.joint * JOINT_STRIDE + J_DOF);
     if (i < dof) {
-      int ai = A.idx[i] < 0 ? 0 : A.idx[i];
-      return (valid ? act[ai] : 0.f) * A.strength;
+      return (valid ? act[take_idx(A.idx[i], aw)] : 0.f) * A.strength;
     }
     i -= dof;
   }
@@ -1419,7 +1450,7 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
 
 template <int L>
 __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int lane, int kind,
-                            int obs_size, const float* act, bool valid, float* obs_out) {
+                            int obs_size, const float* act, int aw, bool valid, float* obs_out) {
   joint_angles<L>(c, H, E, lane);
   if (kind == BX_ENV_HUMANOID && lane == 0) {
     v3 com;
@@ -1430,7 +1461,7 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
   }
   sync();
   if (valid)
-    for (int i = lane; i < obs_size; i += L) obs_out[i] = obs_elem(c, H, E, kind, i, act, valid);
+    for (int i = lane; i < obs_size; i += L) obs_out[i] = obs_elem(c, H, E, kind, i, act, aw, valid);
 }
 
 // ---------------------------------------------------------------------------
@@ -1486,10 +1517,11 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
     Hoist<M> X;
     load_hoist<M>(c, H, lane, X);
     v3 icv, ica, iaa;
-    pbd_step_single<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, X, icv, ica,
+    pbd_step_single<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr,
+                             (int)A.act_width, X, icv, ica,
                        iaa);
   } else {
-    pbd_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr);
+    pbd_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, (int)A.act_width);
   }
   if (!valid) return;
   for (int b = lane; b < H.N; b += L) {
@@ -1541,6 +1573,7 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   const bx_env_params& P = A.P;
   const int kind = P.kind;
   const float* act = valid ? A.act + e * A.act_stride : nullptr;
+  const int aw = (int)A.act_width;
   for (int b = lane; b < H.N; b += L) {
     if (valid) {
       load_qp_global(A.in.qp, e, b, E.qp + b * QP_STRIDE);
@@ -1562,7 +1595,7 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   // action sum of squares (ctrl cost), shared by every repeat
   float sq = 0.f;
   if (valid && lane == 0)
-    for (int i = 0; i < H.A; i++) sq += act[i] * act[i];
+    for (int i = 0; i < aw; i++) sq += act[i] * act[i];
   BX_KSTAMP(10);
   for (int rep = 0; rep < reps; rep++) {
     v3 pos0 = ld3(E.qp);  // torso position before the step
@@ -1572,12 +1605,13 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
     sync();
     if constexpr (S) {
       v3 icv, ica, iaa;
-      pbd_step_single<L, F, M>(c, H, E, lane, valid, act, X, icv, ica, iaa);
+      pbd_step_single<L, F, M>(c, H, E, lane, valid, act, aw, X, icv, ica, iaa);
     } else {
-      pbd_step<L>(c, H, E, lane, valid, act);
+      pbd_step<L>(c, H, E, lane, valid, act, aw);
     }
     BX_KSTAMP(11);
-    env_observe<L>(c, H, E, lane, kind, P.obs_size, act, valid, valid ? A.out.obs + e * P.obs_size : nullptr);
+    env_observe<L>(c, H, E, lane, kind, P.obs_size, act, aw, valid,
+                   valid ? A.out.obs + e * P.obs_size : nullptr);
     BX_KSTAMP(12);
     // reward / done / metrics (lane 0 of the env)
     if (lane == 0 && valid) {
@@ -1706,7 +1740,7 @@ __global__ void __launch_bounds__(64) info_obs_kernel(InfoArgs A) {
   }
   if (A.obs) {
     const float* act = valid && A.act ? A.act + e * A.act_stride : nullptr;
-    env_observe<L>(c, H, E, lane, A.kind, A.obs_size, act, valid && act != nullptr,
+    env_observe<L>(c, H, E, lane, A.kind, A.obs_size, act, (int)A.act_width, valid && act != nullptr,
                    valid ? A.obs + e * A.obs_size : nullptr);
   }
 }

@@ -12,7 +12,7 @@ struct StepArgs {
   int64_t n_envs;
   bx_qp qin, qout;
   const float* act;
-  int64_t act_stride;
+  int64_t act_stride, act_width;
   bx_info info;
 };
 struct EnvArgs {
@@ -21,7 +21,7 @@ struct EnvArgs {
   bx_env_params P;
   bx_env_state in, out;
   const float* act;
-  int64_t act_stride;
+  int64_t act_stride, act_width;
 };
 struct InfoArgs {
   const uint32_t* blob;
@@ -30,7 +30,7 @@ struct InfoArgs {
   bx_info info;
   int kind, obs_size;
   const float* act;
-  int64_t act_stride;
+  int64_t act_stride, act_width;
   float* obs;
 };
 struct ResetArgs {

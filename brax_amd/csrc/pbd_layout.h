@@ -22,6 +22,8 @@ enum {
   J_DAMP = 7, J_SP = 8, J_SA = 9, J_OFFP = 10, J_OFFC = 13, J_AXP = 16, J_AXC = 25, J_LIM = 34,
 };
 enum { ACT_STRIDE = 8, A_TYPE = 0, A_JOINT = 1, A_IDX = 2, A_STR = 5 };
+// forces (forces.py): Thrusters first, then Twisters (application order)
+enum { FORCE_STRIDE = 8, F_TYPE = 0, F_BODY = 1, F_IDX = 2, F_STR = 5, F_MASS = 6 };
 enum {
   ROW_STRIDE = 32,
   R_GROUP = 0, R_A = 1, R_B = 2, R_FN = 3, R_ONEWAY = 4, R_APOS = 5, R_AEND = 8, R_ARAD = 11,
@@ -66,7 +68,7 @@ struct BlobHdr {
   int32_t single;  // every lane owns <= 1 item per kind, lists <= MAXG
   int32_t act_same; // actuator a drives joint a for every a
   int32_t const_words;  // words [0, const_words) = everything the step kernels read
-  int32_t pad2;
+  int32_t NF, o_force;  // forces
 };
 
 }  // namespace bx

@@ -205,7 +205,7 @@ class PhysicsEnv(Env):
     act = torch.as_tensor(action, dtype=torch.float32, device=self.sys.device).contiguous()
     _native.check(_native.lib().bx_env_observe(
         self.sys._h, C.byref(p), B, C.byref(qs), C.c_void_p(act.data_ptr()),
-        act.shape[-1], C.c_void_p(obs.data_ptr()), _stream()))
+        act.shape[-1], act.shape[-1], C.c_void_p(obs.data_ptr()), _stream()))
     return obs
 
   def reset(self, rng) -> State:
@@ -253,7 +253,7 @@ class PhysicsEnv(Env):
     sout.metrics = met.data_ptr()
     _native.check(_native.lib().bx_env_step(
         self.sys._h, C.byref(p), B, C.byref(sin), C.c_void_p(act.data_ptr()), act.stride(0),
-        C.byref(sout), _stream(dev.index)))
+        act.shape[1], C.byref(sout), _stream(dev.index)))
     reward, done, steps, trunc = scal.unbind(0)
     info = dict(state.info)
     if p.episode_length > 0:

@@ -129,8 +129,11 @@ class System:
     act = torch.as_tensor(act, dtype=torch.float32, device=self.device)
     if act.dim() == 1:
       act = act.reshape(1, -1).expand(B, -1) if B > 1 else act.reshape(1, -1)
-    if act.shape[-1] != self.action_size:
-      raise ValueError(f'action has size {act.shape[-1]}, system expects {self.action_size}')
+    if act.dim() != 2 or act.shape[0] != B:
+      raise ValueError(f'action shape {tuple(act.shape)} does not match {B} envs')
+    # any width: indices are clipped like the reference's jp.take (jumpy.py:151)
+    if act.shape[-1] == 0 and (self.num_actuators or self.num_forces_dof):
+      raise ValueError('empty action for a system with actuators or forces')
     if act.stride(-1) != 1:
       act = act.contiguous()
     return act
@@ -197,8 +200,8 @@ class System:
     qi = qp_struct(qp, batched)
     qo = qp_struct(out, batched)
     _native.check(_native.lib().bx_system_step(
-        self._h, B, C.byref(qi), C.c_void_p(act.data_ptr()),
-        act.stride(0) if act.dim() == 2 else 0, C.byref(qo), C.byref(info), _stream()))
+        self._h, B, C.byref(qi), C.c_void_p(act.data_ptr()), act.stride(0), act.shape[1],
+        C.byref(qo), C.byref(info), _stream()))
     zero = torch.zeros_like(cvel)
     return out, Info(contact=P(cvel, cang), joint=P(zero, zero), actuator=P(avel, aang),
                      contact_pos=cpos, contact_normal=cnorm, contact_penetration=cpen)

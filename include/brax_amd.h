@@ -34,12 +34,13 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 1
+#define BX_ABI_VERSION 2
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
 enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_SPHERICAL = 3 };
 enum { BX_ACT_TORQUE = 0, BX_ACT_ANGLE = 1 };
 enum { BX_COL_CAPSULE_PLANE = 0, BX_COL_CAPSULE_CAPSULE = 1 };
+enum { BX_FORCE_THRUSTER = 0, BX_FORCE_TWISTER = 1 };
 /* env layer kinds (obs / reward programs) */
 enum { BX_ENV_NONE = 0, BX_ENV_ANT = 1, BX_ENV_HUMANOID = 2, BX_ENV_HALFCHEETAH = 3 };
 
@@ -99,6 +100,14 @@ typedef struct bx_desc {
   const double* row_b_radius;      /* [R] */
   const double* row_friction;      /* [R] friction_a * friction_b */
   const double* row_elasticity;    /* [R] */
+  /* forces (forces.py:27-138), in application order: Thrusters, then
+   * Twisters, each in config order; action indices assigned in config order
+   * after the actuators' (post-sphericalisation) dofs */
+  int32_t n_forces;
+  const int32_t* force_type;       /* [NF] BX_FORCE_* */
+  const int32_t* force_body;       /* [NF] */
+  const int32_t* force_index;      /* [NF,3] action index (clipped like jp.take) */
+  const double* force_strength;    /* [NF] */
 } bx_desc;
 
 /*
@@ -204,18 +213,20 @@ int bx_system_set_single(bx_system* sys, int on);
 int bx_system_set_variant(bx_system* sys, int lanes, int mode);
 
 /* Physics only: B independent System.step calls (system.py:244-325).
- * act: (B, action_size) with row stride act_stride. qp_in and qp_out may not
- * alias. info may be NULL. */
+ * act: (B, act_width) with row stride act_stride (0 broadcasts one row).
+ * Action indices are clipped to [0, act_width) like the reference's
+ * `jp.take(act, index)` (jumpy.py:146-151); act_width >= 1 unless the system
+ * reads no action. qp_in and qp_out may not alias. info may be NULL. */
 int bx_system_step(bx_system* sys, int64_t n_envs, const bx_qp* qp_in,
-                   const float* act, int64_t act_stride, const bx_qp* qp_out,
-                   const bx_info* info, void* stream);
+                   const float* act, int64_t act_stride, int64_t act_width,
+                   const bx_qp* qp_out, const bx_info* info, void* stream);
 
 /* Env layer fused with physics: for each env, EpisodeWrapper-repeat
  * action_repeat times (System.step + obs/reward/done/metrics), then the
  * episode counters and the AutoReset select. in/out may not alias. */
 int bx_env_step(bx_system* sys, const bx_env_params* env, int64_t n_envs,
                 const bx_env_state* in, const float* act, int64_t act_stride,
-                const bx_env_state* out, void* stream);
+                int64_t act_width, const bx_env_state* out, void* stream);
 
 /* Batched System.default_qp from per-env joint angles/velocities
  * (B, num_joint_dof) contiguous (system.py:112-242). */
@@ -230,7 +241,7 @@ int bx_system_info(bx_system* sys, int64_t n_envs, const bx_qp* qp,
 /* Env observation of a state (Env._get_obs with the reset-time Info). */
 int bx_env_observe(bx_system* sys, const bx_env_params* env, int64_t n_envs,
                    const bx_qp* qp, const float* act, int64_t act_stride,
-                   float* obs, void* stream);
+                   int64_t act_width, float* obs, void* stream);
 
 /* Counter-based uniform [lo,hi) fill keyed by (seed, global index); used for
  * reset noise and synthetic actions (the JAX threefry stream is parity

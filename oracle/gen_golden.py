@@ -129,6 +129,22 @@ def dump_desc(sys_):
   d['act_index'] = np.asarray(aidx, np.int32).reshape(-1, 3)
   d['act_group'] = np.asarray(agrp, np.int32)
 
+  # forces (forces.py:27-138), application order
+  from brax.physics import forces as rf
+  ft, fb, fs, fi = [], [], [], []
+  for f in sys_.forces:
+    for k in range(len(f.strength)):
+      ft.append(0 if isinstance(f, rf.Thruster) else 1)
+      fb.append(int(f.body.idx[k]))
+      fs.append(float(f.strength[k]))
+      fi.append(np.asarray(f.act_index[k]))
+  d['force_type'] = np.asarray(ft, np.int32)
+  d['force_body'] = np.asarray(fb, np.int32)
+  d['force_strength'] = np.asarray(fs, np.float64)
+  d['force_index'] = np.asarray(fi, np.int32).reshape(-1, 3)
+  d['action_size'] = np.int32(sys_.num_joint_dof + sys_.num_forces_dof)
+  d['num_joint_dof'] = np.int32(sys_.num_joint_dof)
+
   goneway, gfn, gscale, gthr, gerp = [], [], [], [], []
   rows = {k: [] for k in ('group', 'body_a', 'body_b', 'a_pos', 'a_end', 'a_radius',
                           'b_pos', 'b_end', 'b_radius', 'friction', 'elasticity')}
@@ -361,6 +377,23 @@ def kats():
   return k
 
 
+# registered envs whose pbd systems get physics goldens: (envs, steps, action
+# width; 0 = num_joint_dof + num_forces_dof). inverted_pendulum uses width 1 as
+# its Env does (action_size = 1, inverted_pendulum.py:151-153): the thruster's
+# indices 1, 2 clip to 0 (jp.take mode='clip').
+ROBOTS = {
+    'inverted_pendulum': (8, 6, 1),
+    'inverted_double_pendulum': (8, 6, 1),
+    'swimmer': (8, 6, 0),
+    'hopper': (8, 6, 0),
+    'walker2d': (8, 6, 0),
+    'reacher': (8, 6, 0),
+    'reacherangle': (8, 6, 0),
+    'acrobot': (8, 6, 0),
+    'ur5e': (4, 4, 0),
+}
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--only', default='')
@@ -395,6 +428,18 @@ def main():
     save('traj_halfcheetah', env_traj(env, 'halfcheetah', 16, 4))
   if want('wrap'):
     save('wrap_ant', wrapped_ant())
+  # physics-only rollouts of the other registered envs' systems (their pbd
+  # configs): Thruster/Twister forces, frozen bodies, systems without contacts
+  for mod, (B, T, aw) in ROBOTS.items():
+    if want(mod):
+      m = importlib.import_module('brax.envs.' + mod)
+      from google.protobuf import text_format
+      import brax
+      s = brax.System(text_format.Parse(m._SYSTEM_CONFIG, brax.Config()))  # pylint: disable=protected-access
+      save(f'desc_{mod}', dump_desc(s))
+      A = aw or (s.num_joint_dof + s.num_forces_dof)
+      qp0 = s.default_qp()
+      save(f'traj_{mod}', sys_traj(s, mod, qp0, B, T, 1.0, A))
   for n in (1, 2, 4):
     if want(f'mountain{n}'):
       s = ant_mountain_sys(n)

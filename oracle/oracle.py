@@ -74,11 +74,15 @@ class Oracle:
   def max_threads(self):
     return int(self._fn('oracle_max_threads')())
 
+  def _width(self, act):
+    """Rows of any width >= 1: indices clip like jp.take (jumpy.py:151)."""
+    self._fn('oracle_set_act_width')(C.c_int(act.shape[1]))
+
   def system_step(self, qp, act):
     qp = self._a(qp)
     B = qp.shape[0]
     act = self._a(act).reshape(B, -1)
-    assert act.shape[1] == self.A, (act.shape, self.A)
+    self._width(act)
     out = np.empty_like(qp)
     ic = np.empty((B, self.N, 6), self.dtype)
     ia = np.empty((B, self.N, 6), self.dtype)
@@ -102,6 +106,7 @@ class Oracle:
     B = qp.shape[0]
     ic = self._a(info_contact)
     act = self._a(act).reshape(B, -1)
+    self._width(act)
     obs = np.empty((B, obs_size), self.dtype)
     rc = self._fn('oracle_env_obs')(C.byref(self.cdesc), C.c_int(ENV_KIND[kind]),
                                     C.c_int64(B), _p(qp), _p(ic), _p(act), _p(obs),
@@ -114,6 +119,7 @@ class Oracle:
     qp = self._a(qp)
     B = qp.shape[0]
     act = self._a(act).reshape(B, -1)
+    self._width(act)
     out = np.empty_like(qp)
     obs = np.empty((B, obs_size), self.dtype)
     rew = np.empty(B, self.dtype)

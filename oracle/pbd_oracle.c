@@ -42,6 +42,12 @@ typedef REAL R;
 static int g_safe_guard = 1;
 
 void FN(oracle_set_safe_norm_guard)(int on) { g_safe_guard = on; }
+
+/* width of the action rows the next calls receive (0: action_size); indices
+ * are clipped into it like jp.take(mode='clip') (jumpy.py:146-151) */
+static int g_act_width = 0;
+void FN(oracle_set_act_width)(int w) { g_act_width = w; }
+static inline int take_idx(int i, int w) { return i < 0 ? 0 : (i >= w ? w - 1 : i); }
 void FN(oracle_set_threads)(int n) {
 #ifdef _OPENMP
   if (n > 0) omp_set_num_threads(n);
@@ -126,8 +132,9 @@ static inline R sgn(R x) { return (R)((x > 0) - (x < 0)); }
  * Python-double constants to fp32 the same way) */
 typedef struct {
   const bx_desc* d;
-  int N, J, K, Rn, G, A;
+  int N, J, K, Rn, G, A, aw, NF;
   R h, g[3], vdamp_exp, adamp_exp;
+  R *fstr, *fmass;
   R *mass, *inv_mass, *I, *pos_mask, *rot_mask, *quat_mask;
   R *joff_p, *joff_c, *jax_p, *jax_c, *jlim, *jdamp, *jsp, *jsa;
   R *astr;
@@ -145,6 +152,11 @@ static void sys_init(sysc* s, const bx_desc* d) {
   s->d = d;
   s->N = d->n_bodies; s->J = d->n_joints; s->K = d->n_actuators;
   s->Rn = d->n_rows; s->G = d->n_groups; s->A = d->action_size;
+  s->aw = g_act_width > 0 ? g_act_width : d->action_size;
+  s->NF = d->n_forces;
+  s->fstr = cvt(d->force_strength, s->NF);
+  s->fmass = (R*)malloc(sizeof(R) * (s->NF > 0 ? s->NF : 1));
+  for (int f = 0; f < s->NF; f++) s->fmass[f] = (R)d->body_mass[d->force_body[f]];
   s->h = (R)d->h;
   for (int k = 0; k < 3; k++) s->g[k] = (R)d->gravity[k];
   /* integrators.py:87,91: exp(damping * dt) of Python floats -> a constant */
@@ -185,7 +197,7 @@ static void sys_free(sysc* s) {
              &s->joff_p, &s->joff_c, &s->jax_p, &s->jax_c, &s->jlim, &s->jdamp,
              &s->jsp, &s->jsa, &s->astr, &s->gscale, &s->gthr, &s->gerp,
              &s->ra_pos, &s->ra_end, &s->ra_rad, &s->rb_pos, &s->rb_end,
-             &s->rb_rad, &s->rfric, &s->relas};
+             &s->rb_rad, &s->rfric, &s->relas, &s->fstr, &s->fmass};
   for (size_t i = 0; i < sizeof(p) / sizeof(p[0]); i++) free(*p[i]);
 }
 
@@ -509,7 +521,7 @@ static void actuators_apply(const sysc* s, work_t* w, const R* act) {
       R tq[3] = {0, 0, 0};
       for (int l = 0; l < dof; l++) {
         /* jp.take(act, act_index) * act_mask; take clips -1 to 0 */
-        int ai = idx[l] < 0 ? 0 : idx[l];
+        int ai = take_idx(idx[l], s->aw);
         R a_l = act[ai] * (idx[l] >= 0 ? (R)1 : (R)0);
         R t;
         if (s->d->act_type[a] == BX_ACT_TORQUE) {
@@ -544,15 +556,34 @@ static void actuators_apply(const sysc* s, work_t* w, const R* act) {
 
 /* ---------------------------------------------------------- integrator --- */
 
-/* Euler.update acc (integrators.py:85-93); acc = dp_a + dp_f + dp_j (ang) */
-static void update_acc(const sysc* s, work_t* w) {
+/* dp_f of body b (forces.py:41-107): Thruster dvel = a * strength / mass,
+ * Twister dang = a * strength / mass, segment-summed in application order
+ * (Thrusters, then Twisters) */
+static void body_forces(const sysc* s, int b, const R* act, R fv[3], R fa[3]) {
+  for (int k = 0; k < 3; k++) fv[k] = fa[k] = 0;
+  for (int f = 0; f < s->NF; f++) {
+    if (s->d->force_body[f] != b) continue;
+    for (int k = 0; k < 3; k++) {
+      R a = act[take_idx(s->d->force_index[3 * f + k], s->aw)];
+      R dv = a * s->fstr[f] / s->fmass[f];
+      if (s->d->force_type[f] == BX_FORCE_THRUSTER) fv[k] += dv;
+      else fa[k] += dv;
+    }
+  }
+}
+
+/* Euler.update acc (integrators.py:85-93); acc = (dp_a + dp_f) + dp_j
+ * (system.py:268-271) */
+static void update_acc(const sysc* s, work_t* w, const R* act) {
   for (int b = 0; b < s->N; b++) {
     body_t* q = &w->qp[b];
+    R fv[3], fa[3];
+    body_forces(s, b, act, fv, fa);
     for (int k = 0; k < 3; k++) {
       R v = s->vdamp_exp * q->vel[k];
-      v += ((R)0 + s->g[k]) * s->h;
+      v += (fv[k] + s->g[k]) * s->h;
       v *= s->pos_mask[3 * b + k];
-      R acc = (w->dp_a[3 * b + k] + (R)0) + w->dp_j[3 * b + k];
+      R acc = (w->dp_a[3 * b + k] + fa[k]) + w->dp_j[3 * b + k];
       R a = s->adamp_exp * q->ang[k];
       a += acc * s->h;
       a *= s->rot_mask[3 * b + k];
@@ -1057,7 +1088,7 @@ static void group_reduce(const sysc* s, work_t* w, int g, int width, R eps,
 static void one_substep(const sysc* s, work_t* w, const R* act) {
   actuators_apply(s, w, act);
   joints_damp(s, w);
-  update_acc(s, w);
+  update_acc(s, w, act);
   kinetic(s, w);
   joints_apply(s, w);
   update_pos(s, w);
@@ -1108,7 +1139,7 @@ int FN(oracle_system_step)(const bx_desc* d, int64_t B, const R* qp_in, const R*
                            R* cnorm, R* cpen) {
   sysc s;
   sys_init(&s, d);
-  int N = s.N, Rn = s.Rn, A = s.A;
+  int N = s.N, Rn = s.Rn, A = s.aw;
 #pragma omp parallel
   {
     work_t w;
@@ -1288,8 +1319,7 @@ static int obs_humanoid(const sysc* s, const body_t* qp, const R* act, R* obs) {
     int j = s->d->act_joint[a];
     int dof = s->d->joint_dof[j];
     for (int l = 0; l < dof; l++) {
-      int ai = s->d->act_index[3 * a + l];
-      if (ai < 0) ai = 0;
+      int ai = take_idx(s->d->act_index[3 * a + l], s->aw);
       obs[n++] = act[ai] * s->astr[a];
     }
   }
@@ -1311,7 +1341,7 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
       int n = 0;
       if (kind == BX_ENV_ANT) n = obs_ant(&s, q, info_c + e * 6 * N, obs + e * obs_size);
       else if (kind == BX_ENV_HALFCHEETAH) n = obs_halfcheetah(&s, q, obs + e * obs_size);
-      else if (kind == BX_ENV_HUMANOID) n = obs_humanoid(&s, q, act + e * s.A, obs + e * obs_size);
+      else if (kind == BX_ENV_HUMANOID) n = obs_humanoid(&s, q, act + e * s.aw, obs + e * obs_size);
       if (n != obs_size) rc = -1;
     }
     free(q);
@@ -1327,7 +1357,7 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
                         R* metrics, int n_metrics) {
   sysc s;
   sys_init(&s, d);
-  int N = s.N, Rn = s.Rn, A = s.A;
+  int N = s.N, Rn = s.Rn, A = s.aw;
   int rc = 0;
 #pragma omp parallel
   {

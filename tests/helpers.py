@@ -4,6 +4,7 @@ import numpy as np
 from brax_amd import compiler
 from brax_amd import config as cfgmod
 from brax_amd.envs import configs
+from brax_amd.envs import robots
 from brax_amd.envs.mountain import ant_mountain_config
 
 ENV_CONFIG = {
@@ -13,7 +14,14 @@ ENV_CONFIG = {
 }
 
 
+# the other registered envs' pbd systems (physics goldens, oracle/gen_golden.py)
+ROBOTS = ['inverted_pendulum', 'inverted_double_pendulum', 'swimmer', 'hopper', 'walker2d',
+          'reacher', 'reacherangle', 'acrobot', 'ur5e']
+
+
 def config_for(name):
+  if name in ROBOTS:
+    return cfgmod.parse(getattr(robots, name.upper() + '_CONFIG'))
   if name.startswith('mountain'):
     return ant_mountain_config(int(name[len('mountain'):]))
   return cfgmod.parse(ENV_CONFIG[name])

@@ -5,6 +5,7 @@ import os
 import re
 
 from brax_amd import _native
+from brax_amd import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -32,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_error_path():
   lib = _native.lib()
-  assert lib.bx_abi_version() == 1
+  assert lib.bx_abi_version() == abi.ABI_VERSION
   # a null descriptor fails at create with a message, no GPU touched
   h = ctypes.c_void_p()
   rc = lib.bx_system_create(None, None, 0, ctypes.byref(h))

@@ -4,9 +4,9 @@ import pytest
 
 from brax_amd import compiler
 from tests.conftest import golden
-from tests.helpers import compiled, config_for
+from tests.helpers import ROBOTS, compiled, config_for
 
-NAMES = ['ant', 'humanoid', 'halfcheetah', 'mountain1', 'mountain2', 'mountain4']
+NAMES = ['ant', 'humanoid', 'halfcheetah', 'mountain1', 'mountain2', 'mountain4'] + ROBOTS
 
 
 @pytest.mark.parametrize('name', NAMES)
