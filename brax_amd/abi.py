@@ -37,6 +37,7 @@ _DESC_FIELDS = [
     ('row_friction', f64p), ('row_elasticity', f64p),
     ('n_forces', C.c_int32), ('force_type', i32p), ('force_body', i32p),
     ('force_index', i32p), ('force_strength', f64p),
+    ('col_cutoff', i32p), ('row_flat', i32p),
 ]
 
 
@@ -114,11 +115,28 @@ def make_desc(d):
   s.angular_damping = float(d['angular_damping'])
   for name, ctype in _DESC_FIELDS:
     if ctype is i32p or ctype is f64p:
-      v = d[name] if name in d or not name.startswith('force_') else np.zeros(0)
+      if name in d:
+        v = d[name]
+      elif name == 'col_cutoff':
+        v = np.zeros(len(d['col_oneway']))
+      elif name == 'row_flat':
+        v = -np.ones(len(d['row_group']))
+      elif name.startswith('force_'):
+        v = np.zeros(0)
+      else:
+        raise KeyError(name)
       a = _arr(v, np.int32 if ctype is i32p else np.float64)
       keep.append(a)
       setattr(s, name, a.ctypes.data_as(ctype))
   return s, keep
+
+
+def info_rows(d):
+  """Contact rows of `Info` (`_get_contact_info`, system.py:36-43): every row
+  of a Pairs group, `cutoff` rows of a NearNeighbors group."""
+  groups = np.asarray(d['row_group'])
+  cut = np.asarray(d.get('col_cutoff', np.zeros(len(d['col_oneway']))))
+  return int(sum(int(c) if c else int((groups == g).sum()) for g, c in enumerate(cut)))
 
 
 def make_reset_desc(r):

@@ -158,6 +158,39 @@ def _capsule_axis(col):
   return rotate(np.array([0., 0., 1.]), euler_to_quat(vec(col.rotation)))
 
 
+def _near_neighbors(pairs, index, cutoff):
+  """NearNeighbors candidates (`colliders.py:55-89`, built at :1005-1013).
+
+  The candidates are the group's unique collidables in first-appearance
+  order (a, then b, per pair). The allowed-pair mask is set with BODY indices
+  (`col_a.body.idx`, `col_b.body.idx`) into the candidates' U x U distance
+  matrix (`jp.index_update(dist_mask, mask, 0)`), so entry (i, j) pairs
+  candidate i with candidate j, whichever bodies those are; the rows are
+  those entries, in flat (i * U + j) order. Each step keeps the `cutoff`
+  entries with the smallest candidate-centre distance (top_k of -dist; ties
+  to the lower flat index, as jax.lax.top_k).
+
+  Mask cells outside U x U follow the jit path: `.at[].set` drops
+  out-of-bounds scatter indices (the numpy backend raises IndexError there,
+  e.g. for Ant Mountain(2+)). More cutoff than allowed cells would make top_k
+  return masked (-inf) cells as pairs; that is refused here."""
+  uniq, seen = [], {}
+  for ca, ca_idx, ba, cb, cb_idx, bb in pairs:
+    for c, c_idx, b in ((ca, ca_idx, ba), (cb, cb_idx, bb)):
+      if (b.name, c_idx) not in seen:
+        seen[(b.name, c_idx)] = len(uniq)
+        uniq.append((c, c_idx, b))
+  U = len(uniq)
+  cells = sorted({(index[ba.name], index[bb.name]) for _, _, ba, _, _, bb in pairs})
+  cells = [(i, j) for i, j in cells if i < U and j < U]
+  if cutoff > len(cells):
+    raise NotImplementedError(f'collider_cutoff {cutoff} exceeds the {len(cells)} allowed '
+                              'NearNeighbors cells (top_k would pick masked cells)')
+  rows = [(uniq[i][0], uniq[i][1], uniq[i][2], uniq[j][0], uniq[j][1], uniq[j][2])
+          for i, j in cells]
+  return dict(pairs=rows, flat=[i * U + j for i, j in cells], cutoff=int(cutoff))
+
+
 def _colliders(config, index):
   """Collider groups and flattened contact rows (`colliders.py:891-1023`)."""
   # only the capsule/sphere/plane subset of `collider_pairs` is on the path
@@ -218,12 +251,11 @@ def _colliders(config, index):
       if (type_a, type_b) not in supported:
         raise NotImplementedError(
             f'collider pair {type_a}/{type_b} is outside the MI355X path')
+      grp = dict(oneway=b_is_frozen, fn=supported[(type_a, type_b)], pairs=flt, cutoff=0)
       if (config.collider_cutoff and len(flt) > config.collider_cutoff and
           (type_a, type_b) == ('capsule', 'capsule')):
-        raise NotImplementedError('NearNeighbors culling (collider_cutoff) is '
-                                  'not implemented yet (SURVEY §8(f).2)')
-      groups.append(dict(oneway=b_is_frozen, fn=supported[(type_a, type_b)],
-                         pairs=flt))
+        grp.update(_near_neighbors(flt, index, config.collider_cutoff))
+      groups.append(grp)
 
   h = config.dt / config.substeps
   g_norm = np.linalg.norm(vec(config.gravity))
@@ -231,13 +263,15 @@ def _colliders(config, index):
              col_baumgarte_erp=[])
   rows = {k: [] for k in ('group', 'body_a', 'body_b', 'a_pos', 'a_end',
                           'a_radius', 'b_pos', 'b_end', 'b_radius', 'friction',
-                          'elasticity')}
+                          'elasticity', 'flat')}
+  out['col_cutoff'] = []
   for gi, g in enumerate(groups):
     out['col_oneway'].append(1 if g['oneway'] else 0)
     out['col_fn'].append(g['fn'])
     out['col_scale'].append(config.solver_scale_collide)
     out['col_velocity_threshold'].append(g_norm * h * 4.0)
     out['col_baumgarte_erp'].append(config.baumgarte_erp * config.substeps / config.dt)
+    out['col_cutoff'].append(g['cutoff'])
     if g['fn'] == CAPSULE_PLANE:
       # CapsuleEnd (`geometry.py:261-288`): 1 or 2 ends; mixed -> pad by dup
       ends_l = []
@@ -250,6 +284,7 @@ def _colliders(config, index):
         for e in ends_l:
           if len(e) == 1:
             e.append(e[0])
+    flats = g.get('flat', [-1] * len(g['pairs']))
     for pi, (ca, _, ba, cb, _, bb) in enumerate(g['pairs']):
       fa = ca.material.friction * cb.material.friction
       ea = ca.material.elasticity * cb.material.elasticity
@@ -261,6 +296,7 @@ def _colliders(config, index):
         b_end = _capsule_axis(cb) * (cb.capsule.length * 0.5 - cb.capsule.radius)
         b_rad = cb.capsule.radius
       for e in ends:
+        rows['flat'].append(flats[pi])
         rows['group'].append(gi)
         rows['body_a'].append(index[ba.name])
         rows['body_b'].append(index[bb.name])
@@ -275,10 +311,11 @@ def _colliders(config, index):
   d = {}
   d['col_oneway'] = np.asarray(out['col_oneway'], np.int32)
   d['col_fn'] = np.asarray(out['col_fn'], np.int32)
+  d['col_cutoff'] = np.asarray(out['col_cutoff'], np.int32)
   for k in ('col_scale', 'col_velocity_threshold', 'col_baumgarte_erp'):
     d[k] = np.asarray(out[k], np.float64)
   for k, v in rows.items():
-    if k in ('group', 'body_a', 'body_b'):
+    if k in ('group', 'body_a', 'body_b', 'flat'):
       d['row_' + k] = np.asarray(v, np.int32)
     elif k.endswith(('pos', 'end')):
       d['row_' + k] = np.asarray(v, np.float64).reshape(-1, 3)

@@ -99,6 +99,22 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       return fail("forces must be ordered Thrusters, then Twisters");
   }
   if (G >= 128) return fail("too many collider groups");
+  // rows of a group are contiguous; a culled group's rows are in flat order
+  for (int x = 1; x < R; x++)
+    if (d->row_group[x] < d->row_group[x - 1]) return fail("contact rows must be grouped");
+  for (int g = 0; g < G; g++) {
+    if (d->col_cutoff[g] < 0) return fail("negative collider cutoff");
+    if (d->col_cutoff[g] == 0) continue;
+    if (d->col_fn[g] != BX_COL_CAPSULE_CAPSULE) return fail("culling is capsule-capsule only");
+    int n = 0, last = -1;
+    for (int x = 0; x < R; x++) {
+      if (d->row_group[x] != g) continue;
+      if (d->row_flat[x] <= last) return fail("culled rows must be in increasing flat order");
+      last = d->row_flat[x];
+      n++;
+    }
+    if (d->col_cutoff[g] > n) return fail("collider cutoff exceeds the group's rows");
+  }
   if (2 * R >= (1 << 24)) return fail("too many contact rows");
 
   Builder B;
@@ -183,6 +199,25 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     B.f(o + R_SCALE, d->col_scale[g]);
     B.f(o + R_THR, d->col_velocity_threshold[g]);
     B.f(o + R_ERP, d->col_baumgarte_erp[g]);
+  }
+  // collider groups: cutoff, row range, Info base (system.py:36-43 order)
+  H.o_group = B.alloc(G * GROUP_STRIDE);
+  {
+    int info = 0;
+    for (int g = 0; g < G; g++) {
+      int r0 = R, r1 = 0;
+      for (int x = 0; x < R; x++)
+        if (d->row_group[x] == g) { r0 = std::min(r0, x); r1 = std::max(r1, x + 1); }
+      if (r0 > r1) r0 = r1 = 0;
+      int o = H.o_group + g * GROUP_STRIDE;
+      B.i(o + G_CUT, d->col_cutoff[g]);
+      B.i(o + G_R0, r0);
+      B.i(o + G_R1, r1);
+      B.i(o + G_INFO, info);
+      info += d->col_cutoff[g] ? d->col_cutoff[g] : r1 - r0;
+      if (d->col_cutoff[g]) H.n_nn++;
+    }
+    H.info_rows = info;
   }
   H.NF = d->n_forces;
   H.o_force = B.alloc(d->n_forces * FORCE_STRIDE);
@@ -303,6 +338,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.l_rowd = carve(R * ROWD_STRIDE);
   H.l_cslot = carve((2 * R + 1) * SLOT_STRIDE);
   H.l_acc = carve(N * ACC_STRIDE);
+  H.l_ract = carve(R);
   H.l_ang = carve(2 * D);
   H.l_red = carve(64);
   // envs 64 words apart: with the odd-multiple record strides, the four
@@ -318,7 +354,8 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         if (std::find(gs.begin(), gs.end(), v >> 24) == gs.end()) gs.push_back(v >> 24);
       max_groups = std::max(max_groups, (int)gs.size());
     }
-    H.single = (N <= L && J <= L && K <= L && R <= L && mx <= 8 && max_groups <= 2) ? 1 : 0;
+    H.single = (N <= L && J <= L && K <= L && R <= L && mx <= 8 && max_groups <= 2 &&
+                H.n_nn == 0) ? 1 : 0;
     H.act_same = 1;
     for (int a = 0; a < K; a++)
       if (d->act_joint[a] != a) H.act_same = 0;

@@ -65,6 +65,7 @@ struct Env {
   float* acc;    // N x 12: info contact vel 3, ang 3, info actuator ang 3, dp_a 3
   float* ang;    // 2 x D: joint angles, joint vels
   float* red;    // 64 scratch
+  int* ract;     // R: NearNeighbors rank of the row this step, -1 = culled
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -650,6 +651,7 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
   E.acc = al16(base + H.l_acc);
   E.ang = al16(base + H.l_ang);
   E.red = al16(base + H.l_red);
+  E.ract = reinterpret_cast<int*>(base + H.l_ract);
   E.nJ = H.J;
   E.nK = H.K;
   E.nR = H.R;
@@ -662,6 +664,73 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
 // ds_write sees it without draining lgkmcnt. Only the compiler must not move
 // or forward memory accesses across the boundary.
 __device__ __forceinline__ void sync() { asm volatile("" ::: "memory"); }
+
+// NearNeighbors.update (colliders.py:71-85) for every culled group, from the
+// env's current qp: candidate-centre distance of each allowed cell, then the
+// `cutoff` nearest cells get ranks 0.. (top_k of -dist; equal distances to the
+// lower flat index = row index, as jax.lax.top_k). Ranks go to E.ract.
+template <int L>
+__device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane) {
+  // Pairs rows are always active (rank 0); culled rows start unselected
+  for (int r = lane; r < H.R; r += L) {
+    const int og = H.o_group + c.i(H.o_row + r * ROW_STRIDE + R_GROUP) * GROUP_STRIDE;
+    E.ract[r] = c.i(og + G_CUT) ? -1 : 0;
+  }
+  sync();
+  for (int g = 0; g < H.G; g++) {
+    const int og = H.o_group + g * GROUP_STRIDE;
+    const int cut = c.i(og + G_CUT);
+    if (cut == 0) continue;
+    const int r0 = c.i(og + G_R0), r1 = c.i(og + G_R1);
+    for (int k = 0; k < cut; k++) {
+      // the lane's nearest unselected cell, as a (distance bits, row) key:
+      // distances are >= 0, so their bit patterns order like the floats
+      unsigned long long best = ~0ull;
+      for (int r = r0 + lane; r < r1; r += L) {
+        if (E.ract[r] >= 0) continue;
+        const int o = H.o_row + r * ROW_STRIDE;
+        const int ba = c.i(o + R_A), bb = c.i(o + R_B);
+        QP a = ldqp(E.qp + ba * QP_STRIDE), b = ldqp(E.qp + bb * QP_STRIDE);
+        v3 pa = a.pos + rotate(c.f3(o + R_APOS), a.rot);
+        v3 pb = b.pos + rotate(c.f3(o + R_BPOS), b.rot);
+        float d = norm(pb - pa);
+        unsigned long long key = ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)r;
+        best = key < best ? key : best;
+      }
+      // minimum over the env's L lanes (aligned L-lane segment of the wave)
+#pragma unroll
+      for (int off = L / 2; off > 0; off >>= 1) {
+        unsigned lo = __shfl_xor((unsigned)best, off, L);
+        unsigned hi = __shfl_xor((unsigned)(best >> 32), off, L);
+        unsigned long long o2 = ((unsigned long long)hi << 32) | lo;
+        best = o2 < best ? o2 : best;
+      }
+      const int r = (int)(best & 0xFFFFFFFFu);
+      if (((r - r0) % L) == lane) E.ract[r] = k;
+      sync();
+    }
+  }
+}
+
+// 1 if row r takes part this step (every Pairs row; culled rows by rank)
+__device__ __forceinline__ bool row_active(const BlobHdr& H, const Env& E, int r) {
+  return H.n_nn == 0 || E.ract[r] >= 0;
+}
+
+// Info contact index of row r (system.py:36-43), -1 when culled this step
+__device__ __forceinline__ int row_info(const Cst& c, const BlobHdr& H, const Env& E, int r) {
+  const int og = H.o_group + c.i(H.o_row + r * ROW_STRIDE + R_GROUP) * GROUP_STRIDE;
+  if (c.i(og + G_CUT) == 0) return c.i(og + G_INFO) + r - c.i(og + G_R0);
+  const int k = E.ract[r];
+  return k < 0 ? -1 : c.i(og + G_INFO) + k;
+}
+
+// a culled row's slots: no update, not counted
+__device__ __forceinline__ void zero_row_slots(const Env& E, int r) {
+  float* sa = E.cslot + r * SLOT_STRIDE;
+  float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
+  for (int k = 0; k < 8; k++) { sa[k] = 0.f; sb[k] = 0.f; }
+}
 
 // the zero slots that padded gather-list entries point at
 __device__ __forceinline__ void zero_slots(const Env& E, const BlobHdr& H, int lane) {
@@ -706,6 +775,8 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
     float* acc = E.acc + b * ACC_STRIDE;
     for (int k = 0; k < 9; k++) acc[k] = 0.f;
   }
+  // cull.update once per step, before the substeps (system.py:320-321)
+  if (H.n_nn) nn_select<L>(c, H, E, lane);
   for (int it = 0; it < H.substeps / 2; it++) {
     for (int sub = 0; sub < 2; sub++) {
       // qprev = qp
@@ -815,6 +886,10 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
     // ---- collisions on the second substep (system.py:288-313)
     // Collider.position_apply (colliders.py:198-240)
     for (int r = lane; r < Rn; r += L) {
+      if (!row_active(H, E, r)) {
+        zero_row_slots(E, r);
+        continue;
+      }
       RowC R = load_row(c, H, r);
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cpos, cvel, n;
@@ -880,6 +955,10 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
     sync();
     // Collider.velocity_apply (colliders.py:155-196)
     for (int r = lane; r < Rn; r += L) {
+      if (!row_active(H, E, r)) {
+        zero_row_slots(E, r);
+        continue;
+      }
       RowC R = load_row(c, H, r);
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       const float* ra = E.rb + R.a * RB_STRIDE;
@@ -1278,7 +1357,14 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
 template <int L>
 __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane) {
   const int N = H.N, Rn = H.R;
+  // culled groups: the cells nearest in this qp (the reference's Info uses
+  // whatever its stateful cull object last selected)
+  if (H.n_nn) nn_select<L>(c, H, E, lane);
   for (int r = lane; r < Rn; r += L) {
+    if (!row_active(H, E, r)) {
+      zero_row_slots(E, r);
+      continue;
+    }
     RowC R = load_row(c, H, r);
     QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
     v3 cpos, cvel, n;
@@ -1546,10 +1632,13 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
     }
   }
   for (int r = lane; r < H.R; r += L) {
+    const int x = row_info(c, H, E, r);
+    if (x < 0) continue;
+    const int64_t o = e * H.info_rows + x;
     const float* rd = E.rowd + r * ROWD_STRIDE;
-    if (A.info.contact_pos) st3(A.info.contact_pos + (e * H.R + r) * 3, ld3(rd));
-    if (A.info.contact_normal) st3(A.info.contact_normal + (e * H.R + r) * 3, ld3(rd + 3));
-    if (A.info.contact_penetration) A.info.contact_penetration[e * H.R + r] = rd[6];
+    if (A.info.contact_pos) st3(A.info.contact_pos + o * 3, ld3(rd));
+    if (A.info.contact_normal) st3(A.info.contact_normal + o * 3, ld3(rd + 3));
+    if (A.info.contact_penetration) A.info.contact_penetration[o] = rd[6];
   }
 }
 

@@ -22,6 +22,8 @@ enum {
   J_DAMP = 7, J_SP = 8, J_SA = 9, J_OFFP = 10, J_OFFC = 13, J_AXP = 16, J_AXC = 25, J_LIM = 34,
 };
 enum { ACT_STRIDE = 8, A_TYPE = 0, A_JOINT = 1, A_IDX = 2, A_STR = 5 };
+// collider groups: NearNeighbors cutoff (0 = Pairs), row range, Info base
+enum { GROUP_STRIDE = 4, G_CUT = 0, G_R0 = 1, G_R1 = 2, G_INFO = 3 };
 // forces (forces.py): Thrusters first, then Twisters (application order)
 enum { FORCE_STRIDE = 8, F_TYPE = 0, F_BODY = 1, F_IDX = 2, F_STR = 5, F_MASS = 6 };
 enum {
@@ -69,6 +71,8 @@ struct BlobHdr {
   int32_t act_same; // actuator a drives joint a for every a
   int32_t const_words;  // words [0, const_words) = everything the step kernels read
   int32_t NF, o_force;  // forces
+  int32_t o_group, n_nn, info_rows;  // collider groups, culled groups, Info rows
+  int32_t l_ract;                    // LDS: per-row NearNeighbors rank (-1 = culled)
 };
 
 }  // namespace bx

@@ -76,7 +76,7 @@ def velocity_projection(sys_, soa, prev, out=None):
 def capsule_plane(sys_, soa, out=None):
   """Contacts of every capsule-plane row: (10, R, B) = pos, vel, normal, pen."""
   B, plane = _check(sys_, soa)
-  R = sys_.num_contacts
+  R = sys_.num_rows
   if out is None:
     out = torch.zeros((10, R, B), dtype=torch.float32, device=soa.device)
   _native.check(_native.lib().bx_phase_capsule_plane(

@@ -90,7 +90,8 @@ class System:
     self.num_forces_dof = meta['num_forces_dof']
     self.num_actuators = len(self.config.actuators)
     self.action_size = meta['action_size']
-    self.num_contacts = len(self.desc['row_group'])
+    self.num_rows = len(self.desc["row_group"])  # contact rows (every candidate cell)
+    self.num_contacts = abi.info_rows(self.desc)  # Info contact rows (system.py:36-43)
     self.body = Body(self.desc, meta['body_index'])
     self.joint_groups = meta['joint_groups']
     if device is None:

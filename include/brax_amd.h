@@ -108,6 +108,13 @@ typedef struct bx_desc {
   const int32_t* force_body;       /* [NF] */
   const int32_t* force_index;      /* [NF,3] action index (clipped like jp.take) */
   const double* force_strength;    /* [NF] */
+  /* NearNeighbors culling (colliders.py:55-89): per group the number of rows
+   * kept each step (0 = Pairs, every row active); per row its cell i*U+j in
+   * the candidate matrix (-1 for Pairs rows). A culled group's rows are its
+   * allowed cells in flat order; Info carries `cutoff` rows for it, nearest
+   * first (top_k order). */
+  const int32_t* col_cutoff;       /* [G] */
+  const int32_t* row_flat;         /* [R] */
 } bx_desc;
 
 /*

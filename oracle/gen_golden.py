@@ -147,9 +147,25 @@ def dump_desc(sys_):
 
   goneway, gfn, gscale, gthr, gerp = [], [], [], [], []
   rows = {k: [] for k in ('group', 'body_a', 'body_b', 'a_pos', 'a_end', 'a_radius',
-                          'b_pos', 'b_end', 'b_radius', 'friction', 'elasticity')}
+                          'b_pos', 'b_end', 'b_radius', 'friction', 'elasticity', 'flat')}
+  gcut = []
   for g, c in enumerate(sys_.colliders):
-    ca, cb = c.cull.get()
+    if isinstance(c.cull, rc.NearNeighbors):
+      # the reference's own NN object: its allowed cells are the finite
+      # entries of dist_off (colliders.py:63-66), in flat order
+      cand_a, cand_b = c.cull.candidate_a, c.cull.candidate_b
+      off = np.asarray(c.cull.dist_off)
+      U = off.shape[1]
+      cells = np.flatnonzero(np.isfinite(off.ravel()))
+      ia, ib = cells // U, cells % U
+      from brax import jumpy as jp
+      ca, cb = jp.take(cand_a, ia), jp.take(cand_b, ib)
+      flats = list(cells)
+      gcut.append(int(c.cull.cutoff))
+    else:
+      ca, cb = c.cull.get()
+      flats = None
+      gcut.append(0)
     goneway.append(1 if isinstance(c, rc.OneWayCollider) else 0)
     fn = c.contact_fn.__name__
     gfn.append({'capsule_plane': 0, 'capsule_capsule': 1}[fn])
@@ -160,6 +176,7 @@ def dump_desc(sys_):
     for p in range(P):
       ends = [ca.end[p]] if fn == 'capsule_capsule' else list(ca.end[p])
       for e in ends:
+        rows['flat'].append(-1 if flats is None else int(flats[p]))
         rows['group'].append(g)
         rows['body_a'].append(ca.body.idx[p])
         rows['body_b'].append(cb.body.idx[p])
@@ -172,11 +189,12 @@ def dump_desc(sys_):
         rows['friction'].append(ca.friction[p] * cb.friction[p])
         rows['elasticity'].append(ca.elasticity[p] * cb.elasticity[p])
   d['col_oneway'] = np.asarray(goneway, np.int32)
+  d['col_cutoff'] = np.asarray(gcut, np.int32)
   d['col_fn'] = np.asarray(gfn, np.int32)
   d['col_scale'] = np.asarray(gscale, np.float64)
   d['col_velocity_threshold'] = np.asarray(gthr, np.float64)
   d['col_baumgarte_erp'] = np.asarray(gerp, np.float64)
-  ints = ('group', 'body_a', 'body_b')
+  ints = ('group', 'body_a', 'body_b', 'flat')
   for k, v in rows.items():
     if k in ints:
       d['row_' + k] = np.asarray(v, np.int32)
@@ -293,7 +311,7 @@ def sys_traj(sys_, name, qp0, n_envs, n_steps, act_scale, A, seed_base=20_000):
   return r
 
 
-def ant_mountain_sys(count):
+def ant_mountain_sys(count, cutoff=0):
   """Ant Mountain scene, as built in `notebooks/multiagent.ipynb` cell 3."""
   from brax import envs
   import brax
@@ -316,8 +334,36 @@ def ant_mountain_sys(count):
     qp.pos.y = np.cos(i * np.pi / 2)
     qp.pos.z = (i + 1) * 2
   del config.collide_include[:]
-  config.collider_cutoff = 0
+  config.collider_cutoff = cutoff
   return brax.System(config)
+
+
+# the CapsuleTest scene (`physics_test.py:292-328`), as test input data
+CAPSULE_TEST_CONFIG = """
+dt: 20.0 substeps: 10000 friction: 0.6 gravity { z: -9.8 }
+bodies { name: "Capsule1" mass: 1 colliders { capsule { radius: 0.25 length: 1.0 } } inertia { x: 1 y: 1 z: 1 } }
+bodies { name: "Capsule2" mass: 1 colliders { rotation { y: 90 } capsule { radius: 0.25 length: 1.0 } } inertia { x: 1 y: 1 z: 1 } }
+bodies { name: "Capsule3" mass: 1 colliders { rotation { y: 45 } capsule { radius: 0.25 length: 1.0 } } inertia { x: 1 y: 1 z: 1 } }
+bodies { name: "Capsule4" mass: 1 colliders { rotation { x: 45 } capsule { radius: 0.25 length: 1.0 } } inertia { x: 1 y: 1 z: 1 } }
+bodies { name: "Ground" frozen { all: true } colliders { plane {} } }
+defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { x: 1 z: 1 } } qps { name: "Capsule3" pos { x: 3 z: 1 } } qps { name: "Capsule4" pos { x: 5 z: 1 } } }
+defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { z: 2 } } qps { name: "Capsule3" pos { x: 3 z: 1 } } qps { name: "Capsule4" pos { x: 5 z: 1 } } }
+"""
+
+
+def capsule_sys(kind):
+  """`physics_test.py:290-361` CapsuleTest scenes (numpy backend, not jit):
+  'ground' (default 0, dt 20, 10000 substeps), 'capsule' (default 1, dt 2,
+  400 substeps) and 'cull' (as 'capsule' with collider_cutoff = 1)."""
+  import brax
+  from google.protobuf import text_format
+  config = text_format.Parse(CAPSULE_TEST_CONFIG, brax.Config())
+  if kind != 'ground':
+    config.dt = 2.0
+    config.substeps = 400
+  if kind == 'cull':
+    config.collider_cutoff = 1
+  return brax.System(config), (0 if kind == 'ground' else 1)
 
 
 def wrapped_ant(n_envs=8, n_steps=6, episode_length=3):
@@ -440,6 +486,15 @@ def main():
       A = aw or (s.num_joint_dof + s.num_forces_dof)
       qp0 = s.default_qp()
       save(f'traj_{mod}', sys_traj(s, mod, qp0, B, T, 1.0, A))
+  if want('mountain1nn'):
+    s = ant_mountain_sys(1, cutoff=9)
+    save('desc_mountain1nn', dump_desc(s))
+    save('traj_mountain1nn', sys_traj(s, 'mountain1nn', s.default_qp(), 4, 4, 1.0, 8))
+  for kind in ('ground', 'capsule', 'cull'):
+    if want('capsule_' + kind):
+      s, di = capsule_sys(kind)
+      save(f'desc_capsule_{kind}', dump_desc(s))
+      save(f'traj_capsule_{kind}', sys_traj(s, 'capsule_' + kind, s.default_qp(di), 1, 1, 1.0, 0))
   for n in (1, 2, 4):
     if want(f'mountain{n}'):
       s = ant_mountain_sys(n)

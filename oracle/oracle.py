@@ -55,6 +55,7 @@ class Oracle:
     self.cdesc, self._keep = abi.make_desc(self.desc)
     self.N = int(desc['n_bodies'])
     self.R = len(desc['row_group'])
+    self.IR = abi.info_rows(self.desc)  # Info contact rows
     self.A = int(desc.get('action_size', 0))
     if reset_desc is not None:
       self.creset, self._keep_r = abi.make_reset_desc(reset_desc)
@@ -86,9 +87,9 @@ class Oracle:
     out = np.empty_like(qp)
     ic = np.empty((B, self.N, 6), self.dtype)
     ia = np.empty((B, self.N, 6), self.dtype)
-    cp = np.empty((B, self.R, 3), self.dtype)
-    cn = np.empty((B, self.R, 3), self.dtype)
-    pen = np.empty((B, self.R), self.dtype)
+    cp = np.empty((B, self.IR, 3), self.dtype)
+    cn = np.empty((B, self.IR, 3), self.dtype)
+    pen = np.empty((B, self.IR), self.dtype)
     self._fn('oracle_system_step')(C.byref(self.cdesc), C.c_int64(B), _p(qp), _p(act),
                                    _p(out), _p(ic), _p(ia), _p(cp), _p(cn), _p(pen))
     return out, dict(contact=ic, actuator=ia, contact_pos=cp, contact_normal=cn,

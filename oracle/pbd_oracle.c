@@ -214,6 +214,7 @@ typedef struct {
   R *gpos, *grot, *gvel, *gang;  /* per-group scratch (N,3/4) */
   R *c_pos, *c_norm, *c_pen, *c_vel, *dlam; /* contact rows */
   R *info_c, *info_a;            /* (N,6) accumulators */
+  int* ract;                     /* (R) NearNeighbors rank, -1 = culled */
 } work_t;
 
 static void work_alloc(work_t* w, int N, int Rn) {
@@ -231,11 +232,13 @@ static void work_alloc(work_t* w, int N, int Rn) {
   w->c_pen = calloc(r, sizeof(R)); w->c_vel = calloc(3 * r, sizeof(R));
   w->dlam = calloc(r, sizeof(R));
   w->info_c = calloc(6 * n, sizeof(R)); w->info_a = calloc(6 * n, sizeof(R));
+  w->ract = calloc(r, sizeof(int));
 }
 static void work_free(work_t* w) {
   void* p[] = {w->qp, w->qprev, w->qrb, w->dp_a, w->dp_j, w->acc, w->dq_pos, w->dq_rot,
                w->dp_vel, w->dp_ang, w->cnt, w->gpos, w->grot, w->gvel, w->gang,
-               w->c_pos, w->c_norm, w->c_pen, w->c_vel, w->dlam, w->info_c, w->info_a};
+               w->c_pos, w->c_norm, w->c_pen, w->c_vel, w->dlam, w->info_c, w->info_a,
+               w->ract};
   for (size_t i = 0; i < sizeof(p) / sizeof(p[0]); i++) free(p[i]);
 }
 
@@ -1083,6 +1086,60 @@ static void group_reduce(const sysc* s, work_t* w, int g, int width, R eps,
   }
 }
 
+/* ------------------------------------------------------- culling -------- */
+
+/* NearNeighbors.update (colliders.py:71-85): for each culled group, the
+ * `cutoff` allowed cells whose candidate centres (body pos + rotate(offset))
+ * are nearest get ranks 0.. in top_k order; ties to the lower flat index
+ * (= row order), as jax.lax.top_k. Pairs rows are always active (rank 0). */
+static void nn_select(const sysc* s, work_t* w) {
+  const bx_desc* d = s->d;
+  for (int r = 0; r < s->Rn; r++) w->ract[r] = d->col_cutoff[d->row_group[r]] ? -1 : 0;
+  for (int g = 0; g < s->G; g++) {
+    int cut = d->col_cutoff[g];
+    if (!cut) continue;
+    for (int k = 0; k < cut; k++) {
+      int best = -1;
+      R bd = 0;
+      for (int r = 0; r < s->Rn; r++) {
+        if (d->row_group[r] != g || w->ract[r] >= 0) continue;
+        const body_t* a = &w->qp[d->row_body_a[r]];
+        const body_t* b = &w->qp[d->row_body_b[r]];
+        R pa[3], pb[3], da[3];
+        rotate(s->ra_pos + 3 * r, a->rot, pa);
+        rotate(s->rb_pos + 3 * r, b->rot, pb);
+        for (int i = 0; i < 3; i++) da[i] = (b->pos[i] + pb[i]) - (a->pos[i] + pa[i]);
+        R dist = (R)sqrt(da[0] * da[0] + da[1] * da[1] + da[2] * da[2]);
+        if (best < 0 || dist < bd) { best = r; bd = dist; }
+      }
+      w->ract[best] = k;
+    }
+  }
+}
+
+/* Info contact index of row r (system.py:36-43), -1 when culled */
+static int row_info(const sysc* s, const work_t* w, int r) {
+  const bx_desc* d = s->d;
+  int g = d->row_group[r], base = 0, r0 = -1;
+  for (int x = 0; x < s->Rn; x++)
+    if (d->row_group[x] == g) { r0 = x; break; }
+  for (int h = 0; h < g; h++) {
+    if (d->col_cutoff[h]) { base += d->col_cutoff[h]; continue; }
+    for (int x = 0; x < s->Rn; x++) base += d->row_group[x] == h;
+  }
+  if (!d->col_cutoff[g]) return base + r - r0;
+  return w->ract[r] < 0 ? -1 : base + w->ract[r];
+}
+
+static int info_rows(const sysc* s) {
+  int n = 0;
+  for (int g = 0; g < s->G; g++) {
+    if (s->d->col_cutoff[g]) { n += s->d->col_cutoff[g]; continue; }
+    for (int x = 0; x < s->Rn; x++) n += s->d->row_group[x] == g;
+  }
+  return n;
+}
+
 /* --------------------------------------------------------------- step ---- */
 
 static void one_substep(const sysc* s, work_t* w, const R* act) {
@@ -1099,6 +1156,7 @@ static void pbd_step_env(const sysc* s, work_t* w, const R* act, R* rows_a, R* r
   int N = s->N, Rn = s->Rn;
   memset(w->info_c, 0, sizeof(R) * 6 * N);
   memset(w->info_a, 0, sizeof(R) * 6 * N);
+  nn_select(s, w);  /* cull.update, once per step (system.py:320-321) */
   for (int it = 0; it < s->d->substeps / 2; it++) {
     memcpy(w->qprev, w->qp, sizeof(body_t) * N);
     one_substep(s, w, act);
@@ -1107,10 +1165,17 @@ static void pbd_step_env(const sysc* s, work_t* w, const R* act, R* rows_a, R* r
     one_substep(s, w, act);
     /* Collider.position_apply (colliders.py:198-240) */
     for (int r = 0; r < Rn; r++)
-      contact_row(s, r, w->qp, w->c_pos + 3 * r, w->c_vel + 3 * r, w->c_norm + 3 * r, &w->c_pen[r]);
-    for (int r = 0; r < Rn; r++)
+      if (w->ract[r] >= 0)
+        contact_row(s, r, w->qp, w->c_pos + 3 * r, w->c_vel + 3 * r, w->c_norm + 3 * r, &w->c_pen[r]);
+    for (int r = 0; r < Rn; r++) {
+      if (w->ract[r] < 0) {  /* culled this step: no update, not counted */
+        memset(rows_a + 7 * r, 0, 7 * sizeof(R));
+        memset(rows_b + 7 * r, 0, 7 * sizeof(R));
+        continue;
+      }
       w->dlam[r] = position_contact(s, r, w->qp, w->qprev, w->c_pos + 3 * r, w->c_norm + 3 * r,
                                     w->c_pen[r], rows_a + 7 * r, rows_b + 7 * r);
+    }
     memset(w->dq_pos, 0, sizeof(R) * 3 * N);
     memset(w->dq_rot, 0, sizeof(R) * 4 * N);
     for (int g = 0; g < s->G; g++) group_reduce(s, w, g, 7, (R)1e-6, rows_a, rows_b, w->dq_pos, w->dq_rot);
@@ -1118,9 +1183,15 @@ static void pbd_step_env(const sysc* s, work_t* w, const R* act, R* rows_a, R* r
     memcpy(w->qrb, w->qp, sizeof(body_t) * N);
     velocity_projection(s, w, w->qprev);
     /* Collider.velocity_apply (colliders.py:155-196); rows at stride 6 */
-    for (int r = 0; r < Rn; r++)
+    for (int r = 0; r < Rn; r++) {
+      if (w->ract[r] < 0) {
+        memset(rows_a + 6 * r, 0, 6 * sizeof(R));
+        memset(rows_b + 6 * r, 0, 6 * sizeof(R));
+        continue;
+      }
       velocity_contact(s, r, w->qp, w->qrb, w->c_pos + 3 * r, w->c_norm + 3 * r, w->c_pen[r],
                        w->dlam[r], rows_a + 6 * r, rows_b + 6 * r);
+    }
     memset(w->dp_vel, 0, sizeof(R) * 3 * N);
     memset(w->dp_ang, 0, sizeof(R) * 3 * N);
     for (int g = 0; g < s->G; g++) group_reduce(s, w, g, 6, (R)1e-6, rows_a, rows_b, w->dp_vel, w->dp_ang);
@@ -1139,7 +1210,7 @@ int FN(oracle_system_step)(const bx_desc* d, int64_t B, const R* qp_in, const R*
                            R* cnorm, R* cpen) {
   sysc s;
   sys_init(&s, d);
-  int N = s.N, Rn = s.Rn, A = s.aw;
+  int N = s.N, Rn = s.Rn, A = s.aw, IR = info_rows(&s);
 #pragma omp parallel
   {
     work_t w;
@@ -1153,9 +1224,13 @@ int FN(oracle_system_step)(const bx_desc* d, int64_t B, const R* qp_in, const R*
       store_qp(w.qp, qp_out + e * 13 * N, N);
       if (info_contact) memcpy(info_contact + e * 6 * N, w.info_c, sizeof(R) * 6 * N);
       if (info_actuator) memcpy(info_actuator + e * 6 * N, w.info_a, sizeof(R) * 6 * N);
-      if (cpos) memcpy(cpos + e * 3 * Rn, w.c_pos, sizeof(R) * 3 * Rn);
-      if (cnorm) memcpy(cnorm + e * 3 * Rn, w.c_norm, sizeof(R) * 3 * Rn);
-      if (cpen) memcpy(cpen + e * Rn, w.c_pen, sizeof(R) * Rn);
+      for (int r = 0; r < Rn; r++) {
+        int x = row_info(&s, &w, r);
+        if (x < 0) continue;
+        if (cpos) memcpy(cpos + (e * IR + x) * 3, w.c_pos + 3 * r, sizeof(R) * 3);
+        if (cnorm) memcpy(cnorm + (e * IR + x) * 3, w.c_norm + 3 * r, sizeof(R) * 3);
+        if (cpen) cpen[e * IR + x] = w.c_pen[r];
+      }
     }
     free(ra); free(rb);
     work_free(&w);
@@ -1168,11 +1243,17 @@ int FN(oracle_system_step)(const bx_desc* d, int64_t B, const R* qp_in, const R*
  * colliders.py:116-153) for one env: info_c (N,6) */
 static void pbd_info_env(const sysc* s, work_t* w, R* rows_a, R* rows_b) {
   int N = s->N, Rn = s->Rn;
-  for (int r = 0; r < Rn; r++)
+  nn_select(s, w);  /* culled groups: the cells nearest in this qp */
+  for (int r = 0; r < Rn; r++) {
+    if (w->ract[r] < 0) {
+      memset(rows_a + 6 * r, 0, 6 * sizeof(R));
+      memset(rows_b + 6 * r, 0, 6 * sizeof(R));
+      continue;
+    }
     contact_row(s, r, w->qp, w->c_pos + 3 * r, w->c_vel + 3 * r, w->c_norm + 3 * r, &w->c_pen[r]);
-  for (int r = 0; r < Rn; r++)
     impulse_contact(s, r, w->qp, w->c_pos + 3 * r, w->c_vel + 3 * r, w->c_norm + 3 * r,
                     w->c_pen[r], rows_a + 6 * r, rows_b + 6 * r);
+  }
   memset(w->dp_vel, 0, sizeof(R) * 3 * N);
   memset(w->dp_ang, 0, sizeof(R) * 3 * N);
   for (int g = 0; g < s->G; g++) group_reduce(s, w, g, 6, (R)1e-8, rows_a, rows_b, w->dp_vel, w->dp_ang);

@@ -19,7 +19,34 @@ ROBOTS = ['inverted_pendulum', 'inverted_double_pendulum', 'swimmer', 'hopper', 
           'reacher', 'reacherangle', 'acrobot', 'ur5e']
 
 
+# the CapsuleTest scene (reference `brax/tests/physics_test.py:292-328`) as
+# test input data; variants 'ground', 'capsule', 'cull' as in its three tests
+CAPSULE_TEST_CONFIG = """
+dt: 20.0 substeps: 10000 friction: 0.6 gravity { z: -9.8 }
+bodies { name: "Capsule1" mass: 1 colliders { capsule { radius: 0.25 length: 1.0 } } inertia { x: 1 y: 1 z: 1 } }
+bodies { name: "Capsule2" mass: 1 colliders { rotation { y: 90 } capsule { radius: 0.25 length: 1.0 } } inertia { x: 1 y: 1 z: 1 } }
+bodies { name: "Capsule3" mass: 1 colliders { rotation { y: 45 } capsule { radius: 0.25 length: 1.0 } } inertia { x: 1 y: 1 z: 1 } }
+bodies { name: "Capsule4" mass: 1 colliders { rotation { x: 45 } capsule { radius: 0.25 length: 1.0 } } inertia { x: 1 y: 1 z: 1 } }
+bodies { name: "Ground" frozen { all: true } colliders { plane {} } }
+defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { x: 1 z: 1 } } qps { name: "Capsule3" pos { x: 3 z: 1 } } qps { name: "Capsule4" pos { x: 5 z: 1 } } }
+defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { z: 2 } } qps { name: "Capsule3" pos { x: 3 z: 1 } } qps { name: "Capsule4" pos { x: 5 z: 1 } } }
+"""
+CAPSULES = ['capsule_ground', 'capsule_capsule', 'capsule_cull']
+
+
 def config_for(name):
+  if name in CAPSULES:
+    cfg = cfgmod.parse(CAPSULE_TEST_CONFIG)
+    if name != 'capsule_ground':
+      cfg.dt = 2.0
+      cfg.substeps = 400
+    if name == 'capsule_cull':
+      cfg.collider_cutoff = 1
+    return cfg
+  if name == 'mountain1nn':
+    cfg = ant_mountain_config(1)
+    cfg.collider_cutoff = 9
+    return cfg
   if name in ROBOTS:
     return cfgmod.parse(getattr(robots, name.upper() + '_CONFIG'))
   if name.startswith('mountain'):

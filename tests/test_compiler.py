@@ -4,9 +4,10 @@ import pytest
 
 from brax_amd import compiler
 from tests.conftest import golden
-from tests.helpers import ROBOTS, compiled, config_for
+from tests.helpers import CAPSULES, ROBOTS, compiled, config_for
 
-NAMES = ['ant', 'humanoid', 'halfcheetah', 'mountain1', 'mountain2', 'mountain4'] + ROBOTS
+NAMES = (['ant', 'humanoid', 'halfcheetah', 'mountain1', 'mountain2', 'mountain4', 'mountain1nn']
+         + ROBOTS + CAPSULES)
 
 
 @pytest.mark.parametrize('name', NAMES)
@@ -50,12 +51,6 @@ def test_parents_generator_quirk():
 
 
 def test_unsupported_raise():
-  cfg = config_for('ant')
-  cfg.collider_cutoff = 3
-  cfg2 = config_for('mountain2')
-  cfg2.collider_cutoff = 3
-  with pytest.raises(NotImplementedError):
-    compiler.compile_system(cfg2)
   cfg3 = config_for('ant')
   cfg3.dynamics_mode = 'legacy_spring'
   with pytest.raises(ValueError):
@@ -68,3 +63,28 @@ def test_default_angle_matches_reference_reset():
   da = compiler.default_angle(vc)
   # reset_qpos = default_angle + U[-0.1, 0.1] noise
   assert np.all(np.abs(T['reset_qpos'] - da[None]) <= 0.1 + 1e-12)
+
+
+def test_near_neighbors_cells():
+  """NearNeighbors (colliders.py:55-89, 1005-1013): candidate rows are the
+  allowed cells of the U x U candidate matrix, addressed by BODY index; cells
+  outside U x U are dropped as jit's scatter drops them."""
+  cfg = config_for('mountain2')
+  cfg.collider_cutoff = 18
+  _, d, _ = compiler.compile_system(cfg)
+  g = int(np.flatnonzero(d['col_cutoff'])[0])
+  rows = d['row_group'] == g
+  flat = d['row_flat'][rows]
+  assert (np.diff(flat) > 0).all() and d['col_cutoff'][g] == 18
+  U = 18  # unique capsule candidates of two ants
+  i, j = flat // U, flat % U
+  assert (i < U).all() and (j < U).all() and (i != j).all()
+  # Ant 1's bodies sit at 10..18 (after the ground): cells on body 18 drop
+  assert not ((d['row_body_a'][rows] == 18) | (d['row_body_b'][rows] == 18)).all()
+  # ant without cutoff: every group is Pairs
+  _, d0, _ = compiler.compile_system(config_for('ant'))
+  assert (d0['col_cutoff'] == 0).all() and (d0['row_flat'] == -1).all()
+  # more cutoff than allowed cells is refused (top_k would pick masked cells)
+  cfg.collider_cutoff = int(rows.sum()) + 1  # still < the 153 pairs: culled
+  with pytest.raises(NotImplementedError):
+    compiler.compile_system(cfg)
