@@ -90,14 +90,14 @@ def phase_bench(sys_, dev, batch=1 << 20, reps=20):
   aux = torch.rand((13, N, batch), device=dev, generator=g) - 0.5
   aux[3:7] += 1.0
   out = soa.clone()
-  contacts = torch.empty((10, sys_.num_contacts, batch), device=dev)
+  contacts = torch.empty((10, sys_.num_rows, batch), device=dev)
   runs = {
       'kinetic': (lambda: phases.kinetic(sys_, soa, out), phases.BYTES[0] * N),
       'update_acc': (lambda: phases.update_acc(sys_, soa, aux[:6], out), phases.BYTES[1] * N),
       'velocity_projection': (lambda: phases.velocity_projection(sys_, soa, aux, out),
                               phases.BYTES[2] * N),
       'capsule_plane': (lambda: phases.capsule_plane(sys_, soa, contacts),
-                        phases.BYTES['capsule_plane'] * sys_.num_contacts),
+                        phases.BYTES['capsule_plane'] * sys_.num_rows),
   }
   res = {}
   for name, (fn, per_env) in runs.items():
@@ -120,6 +120,61 @@ def phase_bench(sys_, dev, batch=1 << 20, reps=20):
   return {'envs': batch, 'unit': 'GB/s', 'peak': HBM_PEAK_GBS, 'kernels': res}
 
 
+def _time(fn, steps, warmup):
+  """Wall-clock and HIP-event time of `steps` calls of fn after `warmup`."""
+  for _ in range(warmup):
+    fn()
+  torch.cuda.synchronize()
+  a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+  t0 = time.perf_counter()
+  a.record()
+  for _ in range(steps):
+    fn()
+  b.record()
+  torch.cuda.synchronize()
+  return time.perf_counter() - t0, a.elapsed_time(b) * 1e-3
+
+
+def secondary_configs(dev, steps=50):
+  """BASELINE.json's other single-GPU configs, one short leg each:
+  Humanoid Env.step at 4096 envs (configs[2]) and Ant Mountain(4)
+  System.step at 2048 envs, all pairs and NearNeighbors cutoff 36 (configs[4];
+  the reference's V100 plot, multiagent.ipynb:222-267, is at 1024 envs)."""
+  from brax_amd import envs
+  from brax_amd.envs.mountain import ant_mountain_config
+  import brax_amd
+  out = {}
+  B = 4096
+  env = envs.create('humanoid', batch_size=B, episode_length=1000, auto_reset=True, device=dev)
+  st = [env.reset(np.array([0, 7], np.uint32))]
+  act = torch.rand((B, env.action_size), device=dev) * 2 - 1
+
+  def hstep():
+    st[0] = env.step(st[0], act)
+  wall, gpu = _time(hstep, steps, 5)
+  out['humanoid_4096'] = {'value': B * steps / wall, 'unit': 'env-steps/s',
+                          'ms_per_step': wall * 1e3 / steps, 'gpu_ms_per_step': gpu * 1e3 / steps}
+  for cutoff in (0, 36):
+    cfg = ant_mountain_config(4)
+    cfg.collider_cutoff = cutoff
+    sys_ = brax_amd.System(cfg, device=dev)
+    Bm = 2048
+    qp0 = sys_.default_qp()
+    qp = [brax_amd.QP(*(t.unsqueeze(0).expand((Bm,) + t.shape).contiguous()
+                        for t in (qp0.pos, qp0.rot, qp0.vel, qp0.ang)))]
+    a = torch.rand((Bm, sys_.action_size), device=dev) * 2 - 1
+
+    def mstep():
+      qp[0], _ = sys_.step(qp[0], a)
+    n = max(steps // 5, 5)
+    wall, gpu = _time(mstep, n, 2)
+    out[f'mountain4_2048_cutoff{cutoff}'] = {
+        'value': Bm * n / wall, 'unit': 'env-steps/s (System.step)',
+        'ms_per_step': wall * 1e3 / n, 'gpu_ms_per_step': gpu * 1e3 / n,
+        'contact_rows': sys_.num_rows, 'lanes_per_env': sys_.lanes}
+  return out
+
+
 def _traffic():
   """HBM bytes per launch from the committed PMC profile, if present."""
   p = os.path.join(ROOT, 'profiles', 'traffic.json')
@@ -139,6 +194,8 @@ def main():
   ap.add_argument('--no-phases', action='store_true',
                   help='skip the standalone SoA phase-kernel roofline leg')
   ap.add_argument('--phase-envs', type=int, default=1 << 20)
+  ap.add_argument('--no-secondary', action='store_true',
+                  help='skip the Humanoid / Ant Mountain legs')
   ap.add_argument('--generic', action='store_true',
                   help='force the generic item-loop kernel variant (A/B)')
   ap.add_argument('--variant', default='',
@@ -241,6 +298,7 @@ def main():
                    'valu_tflops': ANT_FLOPS_PER_ENV_STEP * B / (kern_ms * 1e-3) / 1e12,
                    'valu_peak_tflops': FP32_VALU_PEAK_TFLOPS},
   }
+  out['secondary_configs'] = None if args.no_secondary else secondary_configs(dev)
   out['phase_roofline'] = (None if args.no_phases else
                            phase_bench(env.unwrapped.sys, dev, args.phase_envs))
   if world == 1 and not args.no_cpu_baseline:

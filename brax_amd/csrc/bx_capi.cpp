@@ -339,6 +339,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.l_cslot = carve((2 * R + 1) * SLOT_STRIDE);
   H.l_acc = carve(N * ACC_STRIDE);
   H.l_ract = carve(R);
+  H.l_alist = carve(H.info_rows);
   H.l_ang = carve(2 * D);
   H.l_red = carve(64);
   // envs 64 words apart: with the odd-multiple record strides, the four

@@ -66,6 +66,7 @@ struct Env {
   float* ang;    // 2 x D: joint angles, joint vels
   float* red;    // 64 scratch
   int* ract;     // R: NearNeighbors rank of the row this step, -1 = culled
+  int* alist;    // info_rows: the step's active rows in Info order
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -652,6 +653,7 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
   E.ang = al16(base + H.l_ang);
   E.red = al16(base + H.l_red);
   E.ract = reinterpret_cast<int*>(base + H.l_ract);
+  E.alist = reinterpret_cast<int*>(base + H.l_alist);
   E.nJ = H.J;
   E.nK = H.K;
   E.nR = H.R;
@@ -665,16 +667,30 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
 // or forward memory accesses across the boundary.
 __device__ __forceinline__ void sync() { asm volatile("" ::: "memory"); }
 
+// a culled row's slots: no update, not counted
+__device__ __forceinline__ void zero_row_slots(const Env& E, int r) {
+  float* sa = E.cslot + r * SLOT_STRIDE;
+  float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
+  for (int k = 0; k < 8; k++) { sa[k] = 0.f; sb[k] = 0.f; }
+}
+
 // NearNeighbors.update (colliders.py:71-85) for every culled group, from the
 // env's current qp: candidate-centre distance of each allowed cell, then the
 // `cutoff` nearest cells get ranks 0.. (top_k of -dist; equal distances to the
 // lower flat index = row index, as jax.lax.top_k). Ranks go to E.ract.
 template <int L>
 __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane) {
-  // Pairs rows are always active (rank 0); culled rows start unselected
+  // Pairs rows are always active (rank 0) at their fixed Info index; culled
+  // rows start unselected with empty (zero, uncounted) slots
   for (int r = lane; r < H.R; r += L) {
     const int og = H.o_group + c.i(H.o_row + r * ROW_STRIDE + R_GROUP) * GROUP_STRIDE;
-    E.ract[r] = c.i(og + G_CUT) ? -1 : 0;
+    if (c.i(og + G_CUT)) {
+      E.ract[r] = -1;
+      zero_row_slots(E, r);
+    } else {
+      E.ract[r] = 0;
+      E.alist[c.i(og + G_INFO) + r - c.i(og + G_R0)] = r;
+    }
   }
   sync();
   for (int g = 0; g < H.G; g++) {
@@ -682,18 +698,24 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
     const int cut = c.i(og + G_CUT);
     if (cut == 0) continue;
     const int r0 = c.i(og + G_R0), r1 = c.i(og + G_R1);
+    // candidate-centre distance of every cell, once (rowd word 8 is free
+    // until the position pass of the first substep)
+    for (int r = r0 + lane; r < r1; r += L) {
+      const int o = H.o_row + r * ROW_STRIDE;
+      const int ba = c.i(o + R_A), bb = c.i(o + R_B);
+      QP a = ldqp(E.qp + ba * QP_STRIDE), b = ldqp(E.qp + bb * QP_STRIDE);
+      v3 pa = a.pos + rotate(c.f3(o + R_APOS), a.rot);
+      v3 pb = b.pos + rotate(c.f3(o + R_BPOS), b.rot);
+      E.rowd[r * ROWD_STRIDE + 8] = norm(pb - pa);
+    }
+    sync();
     for (int k = 0; k < cut; k++) {
       // the lane's nearest unselected cell, as a (distance bits, row) key:
       // distances are >= 0, so their bit patterns order like the floats
       unsigned long long best = ~0ull;
       for (int r = r0 + lane; r < r1; r += L) {
         if (E.ract[r] >= 0) continue;
-        const int o = H.o_row + r * ROW_STRIDE;
-        const int ba = c.i(o + R_A), bb = c.i(o + R_B);
-        QP a = ldqp(E.qp + ba * QP_STRIDE), b = ldqp(E.qp + bb * QP_STRIDE);
-        v3 pa = a.pos + rotate(c.f3(o + R_APOS), a.rot);
-        v3 pb = b.pos + rotate(c.f3(o + R_BPOS), b.rot);
-        float d = norm(pb - pa);
+        const float d = E.rowd[r * ROWD_STRIDE + 8];
         unsigned long long key = ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)r;
         best = key < best ? key : best;
       }
@@ -706,7 +728,10 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
         best = o2 < best ? o2 : best;
       }
       const int r = (int)(best & 0xFFFFFFFFu);
-      if (((r - r0) % L) == lane) E.ract[r] = k;
+      if (((r - r0) % L) == lane) {
+        E.ract[r] = k;
+        E.alist[c.i(og + G_INFO) + k] = r;
+      }
       sync();
     }
   }
@@ -723,13 +748,6 @@ __device__ __forceinline__ int row_info(const Cst& c, const BlobHdr& H, const En
   if (c.i(og + G_CUT) == 0) return c.i(og + G_INFO) + r - c.i(og + G_R0);
   const int k = E.ract[r];
   return k < 0 ? -1 : c.i(og + G_INFO) + k;
-}
-
-// a culled row's slots: no update, not counted
-__device__ __forceinline__ void zero_row_slots(const Env& E, int r) {
-  float* sa = E.cslot + r * SLOT_STRIDE;
-  float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
-  for (int k = 0; k < 8; k++) { sa[k] = 0.f; sb[k] = 0.f; }
 }
 
 // the zero slots that padded gather-list entries point at
@@ -885,11 +903,9 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
     }
     // ---- collisions on the second substep (system.py:288-313)
     // Collider.position_apply (colliders.py:198-240)
-    for (int r = lane; r < Rn; r += L) {
-      if (!row_active(H, E, r)) {
-        zero_row_slots(E, r);
-        continue;
-      }
+    // with culling: only the step's active rows (culled slots stay zero)
+    for (int i = lane; i < (H.n_nn ? H.info_rows : Rn); i += L) {
+      const int r = H.n_nn ? E.alist[i] : i;
       RowC R = load_row(c, H, r);
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cpos, cvel, n;
@@ -954,11 +970,8 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
     }
     sync();
     // Collider.velocity_apply (colliders.py:155-196)
-    for (int r = lane; r < Rn; r += L) {
-      if (!row_active(H, E, r)) {
-        zero_row_slots(E, r);
-        continue;
-      }
+    for (int i = lane; i < (H.n_nn ? H.info_rows : Rn); i += L) {
+      const int r = H.n_nn ? E.alist[i] : i;
       RowC R = load_row(c, H, r);
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       const float* ra = E.rb + R.a * RB_STRIDE;

@@ -73,6 +73,7 @@ struct BlobHdr {
   int32_t NF, o_force;  // forces
   int32_t o_group, n_nn, info_rows;  // collider groups, culled groups, Info rows
   int32_t l_ract;                    // LDS: per-row NearNeighbors rank (-1 = culled)
+  int32_t l_alist;                   // LDS: active rows in Info order (info_rows)
 };
 
 }  // namespace bx
