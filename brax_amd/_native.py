@@ -48,6 +48,8 @@ _SIGS = {
     'bx_env_observe': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64,
                         C.POINTER(abi.BxQP), C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
                         C.c_void_p], C.c_int),
+    'bx_system_joint_angles': ([C.c_void_p, C.c_int64, C.POINTER(abi.BxQP), C.c_void_p,
+                                C.c_void_p, C.c_void_p], C.c_int),
     'bx_phase': ([C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
                   C.c_void_p, C.c_int64, C.c_void_p], C.c_int),
     'bx_phase_capsule_plane': ([C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,

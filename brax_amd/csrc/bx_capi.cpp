@@ -557,6 +557,22 @@ int bx_env_observe(bx_system* S, const bx_env_params* env, int64_t n_envs, const
   return 0;
 }
 
+int bx_system_joint_angles(bx_system* S, int64_t n_envs, const bx_qp* qp, float* angle,
+                           float* vel, void* stream) {
+  if (!S || !qp) return fail("null argument");
+  if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
+  if (S->hdr.D == 0) return 0;
+  if (!angle || !vel) return fail("null angle or velocity buffer");
+  InfoArgs a{};
+  a.blob = S->blob;
+  a.n_envs = n_envs;
+  a.q = *qp;
+  a.angle = angle;
+  a.angvel = vel;
+  HIP_OK(launch_info_obs(S->L, n_envs, S->lds_env, as_stream(stream), a));
+  return 0;
+}
+
 int bx_system_default_qp(bx_system* S, int64_t n_envs, const float* joint_angle,
                          const float* joint_velocity, const bx_qp* qp_out, void* stream) {
   if (!S || !qp_out) return fail("null argument");

@@ -1825,6 +1825,16 @@ __global__ void __launch_bounds__(64) info_obs_kernel(InfoArgs A) {
     }
   }
   sync();
+  if (A.angle) {  // Joint.angle_vel only
+    joint_angles<L>(c, H, E, lane);
+    sync();
+    if (valid)
+      for (int i = lane; i < H.D; i += L) {
+        A.angle[e * H.D + i] = E.ang[i];
+        A.angvel[e * H.D + i] = E.ang[H.D + i];
+      }
+    return;
+  }
   pbd_info<L>(c, H, E, lane);
   if (valid) {
     for (int b = lane; b < H.N; b += L) {

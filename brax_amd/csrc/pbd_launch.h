@@ -32,6 +32,8 @@ struct InfoArgs {
   const float* act;
   int64_t act_stride, act_width;
   float* obs;
+  float* angle;  // joint angles (B, D) and velocities (B, D), or null
+  float* angvel;
 };
 struct ResetArgs {
   const uint32_t* blob;

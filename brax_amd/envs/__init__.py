@@ -12,11 +12,20 @@ from brax_amd.envs.ant import Ant
 from brax_amd.envs.env import Env, PhysicsEnv, State, Wrapper
 from brax_amd.envs.half_cheetah import Halfcheetah
 from brax_amd.envs.humanoid import Humanoid
+from brax_amd.envs import torch_envs
 
 _envs = {
+    'acrobot': torch_envs.Acrobot,
     'ant': functools.partial(Ant, use_contact_forces=True),
     'halfcheetah': Halfcheetah,
+    'hopper': torch_envs.Hopper,
     'humanoid': Humanoid,
+    'inverted_pendulum': torch_envs.InvertedPendulum,
+    'inverted_double_pendulum': torch_envs.InvertedDoublePendulum,
+    'reacher': torch_envs.Reacher,
+    'reacherangle': torch_envs.ReacherAngle,
+    'swimmer': torch_envs.Swimmer,
+    'walker2d': torch_envs.Walker2d,
 }
 
 

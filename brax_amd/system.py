@@ -66,6 +66,21 @@ def qp_struct(qp, batched):
   return s
 
 
+class JointGroup:
+  """One entry of `System.joints` (`joints.get` groups joints by dof,
+  joints.py:418-474); only `angle_vel` is needed on the host side."""
+
+  def __init__(self, sys_, lo, hi, dof, names, free):
+    self._sys, self._lo, self._hi = sys_, lo, hi
+    self.dof, self.names, self.free_dofs = dof, list(names), free
+
+  def angle_vel(self, qp):
+    """`Joint.angle_vel` (joints.py:197-226): angles and velocities of this
+    group's dofs, (..., n) each, free dofs only for sphericalised groups."""
+    a, v = self._sys.joint_angle_vel(qp)
+    return a[..., self._lo:self._hi], v[..., self._lo:self._hi]
+
+
 class Body:
   """Per-body constants (`bodies.py:25-59`): mass and INVERSE inertia."""
 
@@ -94,6 +109,12 @@ class System:
     self.num_contacts = abi.info_rows(self.desc)  # Info contact rows (system.py:36-43)
     self.body = Body(self.desc, meta['body_index'])
     self.joint_groups = meta['joint_groups']
+    self.joints = []
+    lo = 0
+    for dof, names, free in self.joint_groups:
+      n = sum(free) if free is not None else dof * len(names)
+      self.joints.append(JointGroup(self, lo, lo + n, dof, names, free))
+      lo += n
     if device is None:
       if not torch.cuda.is_available():
         raise _native.NativeError('brax_amd.System needs a GPU (no CPU fallback)')
@@ -206,6 +227,21 @@ class System:
     zero = torch.zeros_like(cvel)
     return out, Info(contact=P(cvel, cang), joint=P(zero, zero), actuator=P(avel, aang),
                      contact_pos=cpos, contact_normal=cnorm, contact_penetration=cpen)
+
+  def joint_angle_vel(self, qp: QP):
+    """Angles and angular velocities of every joint dof, in joint order
+    (`bx_system_joint_angles`): two (B, num_joint_dof) tensors (unbatched QP:
+    (num_joint_dof,))."""
+    batched = qp.pos.dim() == 3
+    B = qp.pos.shape[0] if batched else 1
+    D = sum(j._hi - j._lo for j in self.joints)  # pylint: disable=protected-access
+    buf = torch.empty((2, B, D), dtype=torch.float32, device=self.device)
+    if D:
+      qs = qp_struct(qp, batched)
+      _native.check(_native.lib().bx_system_joint_angles(
+          self._h, B, C.byref(qs), C.c_void_p(buf[0].data_ptr()), C.c_void_p(buf[1].data_ptr()),
+          _stream()))
+    return (buf[0], buf[1]) if batched else (buf[0, 0], buf[1, 0])
 
   def info(self, qp: QP):
     """`System.info` in pbd mode (system.py:327-340): the contact part."""

@@ -232,10 +232,11 @@ def env_traj(env, name, n_envs, n_steps, act_seed_base=10_000):
   from brax import jumpy as jp
   for s in range(n_envs):
     rng = np.array([s, 0], np.uint32)
-    # re-derive the reset noise exactly as Env.reset does (`ant.py:198-203`)
-    _, r1, r2 = jp.random_split(rng, 3)
-    qpos_l.append(env.sys.default_angle() + env._noise(r1))
-    qvel_l.append(env._noise(r2))
+    if hasattr(env, '_noise'):
+      # re-derive the reset noise exactly as Env.reset does (`ant.py:198-203`)
+      _, r1, r2 = jp.random_split(rng, 3)
+      qpos_l.append(env.sys.default_angle() + env._noise(r1))
+      qvel_l.append(env._noise(r2))
     states.append(env.reset(rng))
   acts = np.stack([np.random.default_rng(act_seed_base + t).uniform(-1, 1, (n_envs, A))
                    for t in range(n_steps)])
@@ -281,8 +282,9 @@ def env_traj(env, name, n_envs, n_steps, act_seed_base=10_000):
     print(f'  {name}: step {t + 1}/{n_steps}  ({time.time() - t0:.1f}s)', flush=True)
   res = {k: np.stack(v) for k, v in out.items() if v}
   res['action'] = acts
-  res['reset_qpos'] = np.stack(qpos_l)
-  res['reset_qvel'] = np.stack(qvel_l)
+  if qpos_l:
+    res['reset_qpos'] = np.stack(qpos_l)
+    res['reset_qvel'] = np.stack(qvel_l)
   res['reset_obs'] = reset_obs
   res['metric_keys'] = np.array(metric_keys)
   return res
@@ -440,6 +442,10 @@ ROBOTS = {
 }
 
 
+TORCH_ENVS = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum',
+              'swimmer', 'reacher', 'reacherangle', 'acrobot']
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--only', default='')
@@ -472,6 +478,11 @@ def main():
     env = envs.get_environment('halfcheetah')
     save('desc_halfcheetah', dump_desc(env.sys))
     save('traj_halfcheetah', env_traj(env, 'halfcheetah', 16, 4))
+  # torch env layer over the other registered envs' systems
+  for name in TORCH_ENVS:
+    if want('env_' + name):
+      env = envs.get_environment(name)
+      save(f'envtraj_{name}', env_traj(env, name, 8, 4))
   if want('wrap'):
     save('wrap_ant', wrapped_ant())
   # physics-only rollouts of the other registered envs' systems (their pbd

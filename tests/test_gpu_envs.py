@@ -1,0 +1,120 @@
+"""The torch env layer over the other registered envs vs the reference's own
+rollouts (tests/golden/envtraj_*: `env.reset` from seeds, random actions,
+`env.step`, numpy backend, float64).
+
+Two checks per env and step:
+  * the env layer alone: `_get_obs` / `_step` of the golden post-step state
+    (fp32 evaluation of the reference's formulas) against the golden obs,
+    reward, done and metrics, normwise <= 2e-5;
+  * the whole `Env.step` (fused physics kernel + env layer) from the golden
+    state: the new state within the fp32 envelope of Brax's algorithm (as in
+    test_gpu_parity), obs and reward finite and within 2e-3 normwise (they
+    carry the state's fp32 error, amplified by 1/dt for velocities).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import golden
+from tests.helpers import QP_FIELDS, normwise
+
+pytestmark = pytest.mark.gpu
+
+ENVS = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum', 'swimmer',
+        'reacher', 'reacherangle', 'acrobot']
+TOL = 2e-5
+
+
+@pytest.fixture(scope='module')
+def dev():
+  assert torch.cuda.is_available(), 'GPU tests need a GPU'
+  return torch.device('cuda', 0)
+
+
+def _state(env, T, t, dev):
+  from brax_amd.base import qp_from_numpy
+  from brax_amd.envs.env import State
+  qp = qp_from_numpy(T['qp'][t], dev)
+  B = T['qp'].shape[1]
+  keys = [str(k) for k in T['metric_keys']]
+  met = {k: torch.zeros((B,), device=dev) for k in keys}
+  if t > 0:
+    for i, k in enumerate(keys):
+      met[k] = torch.as_tensor(T['metrics'][t - 1][:, i], dtype=torch.float32, device=dev)
+  obs = torch.as_tensor(T['obs'][t], dtype=torch.float32, device=dev)
+  z = torch.zeros((B,), device=dev)
+  return State(qp=qp, obs=obs, reward=z, done=z.clone(), metrics=met, info={})
+
+
+def _close(got, ref, tol, what):
+  got = np.asarray(got, np.float64)
+  ref = np.asarray(ref, np.float64)
+  assert np.all(np.isfinite(got)), what
+  nw = normwise(got.reshape(got.shape[0], -1), ref.reshape(ref.shape[0], -1))
+  assert nw.max() <= tol, f'{what}: normwise {nw.max():.3e} > {tol:.1e}'
+
+
+@pytest.mark.parametrize('name', ENVS)
+def test_env_layer_vs_golden(dev, name):
+  from brax_amd import envs
+  from brax_amd.base import qp_from_numpy
+  env = envs.get_environment(name, device=dev)
+  T = golden('envtraj_' + name)
+  keys = [str(k) for k in T['metric_keys']]
+  # reset observation of the golden reset state
+  _close(env._get_obs(qp_from_numpy(T['qp'][0], dev), None).cpu(), T['reset_obs'], TOL,
+         'reset obs')
+  for t in range(T['action'].shape[0]):
+    st = _state(env, T, t, dev)
+    act = torch.as_tensor(T['action'][t], dtype=torch.float32, device=dev)
+    qp1 = qp_from_numpy(T['qp'][t + 1], dev)
+    new = env._step(st, act, qp1, None)
+    _close(new.obs.cpu(), T['obs'][t + 1], TOL, f'obs t={t}')
+    _close(new.reward.cpu()[:, None], T['reward'][t][:, None], TOL, f'reward t={t}')
+    assert np.array_equal(new.done.cpu().numpy(), T['done'][t]), f'done t={t}'
+    for i, k in enumerate(keys):
+      _close(new.metrics[k].cpu()[:, None], T['metrics'][t][:, i:i + 1], TOL, f'{k} t={t}')
+
+
+@pytest.mark.parametrize('name', ENVS)
+def test_env_step_vs_golden(dev, oracle_lib, name):
+  from brax_amd import envs
+  from tests.helpers import compiled
+  env = envs.get_environment(name, device=dev)
+  T = golden('envtraj_' + name)
+  _, d, rd, _ = compiled(name)
+  o32 = oracle_lib.Oracle(d, rd, np.float32, safe_guard=True)
+  o64 = oracle_lib.Oracle(d, rd, np.float64)
+  for t in range(T['action'].shape[0]):
+    st = _state(env, T, t, dev)
+    act = torch.as_tensor(T['action'][t], dtype=torch.float32, device=dev)
+    new = env.step(st, act)
+    # the system action the env fed to the kernel (swimmer adds drag forces)
+    sys_act = env._system_action(st, env._action(act, act.shape[0])).cpu().numpy()
+    ref, _ = o64.system_step(T['qp'][t], sys_act)
+    rng = np.random.default_rng(1234)
+    ins = [T['qp'][t]] + [T['qp'][t] * (1 + rng.uniform(-6e-8, 6e-8, T['qp'][t].shape))
+                          for _ in range(3)]
+    outs = [o32.system_step(q.astype(np.float32), sys_act.astype(np.float32))[0] for q in ins]
+    got = new.qp.numpy()
+    for f, sl in QP_FIELDS.items():
+      e32 = np.max([normwise(x[..., sl], ref[..., sl]) for x in outs])
+      nw = normwise(got[..., sl], ref[..., sl])
+      assert nw.max() <= max(1e-5, 2 * e32), f'{f} t={t}: {nw.max():.3e} vs e32 {e32:.3e}'
+    # the golden's next state came from float64 actions incl. float64 drag
+    _close(new.obs.cpu(), T['obs'][t + 1], 2e-3, f'obs t={t}')
+    _close(new.reward.cpu()[:, None], T['reward'][t][:, None], 2e-3, f'reward t={t}')
+
+
+@pytest.mark.parametrize('name', ['hopper', 'inverted_pendulum'])
+def test_wrapped_torch_env(dev, name):
+  """Episode + AutoReset over a torch env run as device tensor ops."""
+  from brax_amd import envs
+  env = envs.create(name, batch_size=16, episode_length=5, auto_reset=True, device=dev)
+  st = env.reset(np.array([3, 1], np.uint32))
+  A = env.action_size
+  for k in range(12):
+    st = env.step(st, torch.rand((16, A), device=dev) * 2 - 1)
+    assert torch.isfinite(st.obs).all() and torch.isfinite(st.qp.pos).all()
+    assert int(st.info['steps'].max()) <= 5
+  assert 'truncation' in st.info and 'first_qp' in st.info
