@@ -49,9 +49,21 @@ def create(env_name: str, episode_length: int = 1000, action_repeat: int = 1,
   if auto_reset:
     env = wrappers.AutoResetWrapper(env)
   if eval_metrics:
-    raise NotImplementedError('EvalWrapper is not implemented yet')
+    env = wrappers.EvalWrapper(env)
   return env
 
 
 def create_fn(env_name: str, **kwargs) -> Callable[..., Env]:
   return functools.partial(create, env_name, **kwargs)
+
+
+def create_gym_env(env_name: str, batch_size: Optional[int] = None, seed: int = 0,
+                   backend: Optional[str] = None, **kwargs):
+  """`envs/__init__.py:118-130`: a gym-API env (VectorGymWrapper when batched);
+  observations, rewards and dones are device tensors."""
+  environment = create(env_name=env_name, batch_size=batch_size, **kwargs)
+  if batch_size is None:
+    return wrappers.GymWrapper(environment, seed=seed, backend=backend)
+  if batch_size <= 0:
+    raise ValueError('`batch_size` should either be None or a positive integer.')
+  return wrappers.VectorGymWrapper(environment, seed=seed, backend=backend)

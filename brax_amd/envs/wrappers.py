@@ -5,9 +5,13 @@ when they wrap a PhysicsEnv (optionally through Vector/VmapWrapper) their
 logic runs INSIDE the fused env-step kernel (one launch per step). Above any
 other env they run as device tensor ops with the same semantics.
 """
+import dataclasses
+from typing import Dict, Optional
+
+import numpy as np
 import torch
 
-from brax_amd.envs.env import Env, State, Wrapper
+from brax_amd.envs.env import Env, State, Wrapper, key_to_seed
 
 
 def wrap_for_training(env: Env, episode_length: int = 1000, action_repeat: int = 1):
@@ -140,3 +144,150 @@ class AutoResetWrapper(Wrapper):
             vel=torch.where(d3, fq.vel, state.qp.vel), ang=torch.where(d3, fq.ang, state.qp.ang))
     obs = torch.where(done.reshape(-1, 1), fo, state.obs)
     return state.replace(qp=qp, obs=obs)
+
+
+@dataclasses.dataclass(frozen=True)
+class EvalMetrics:
+  """`wrappers.py:150-166`: per-episode aggregated metrics."""
+  episode_metrics: Dict[str, torch.Tensor]
+  active_episodes: torch.Tensor
+  episode_steps: torch.Tensor
+
+
+class EvalWrapper(Wrapper):
+  """`wrappers.py:169-203`: episode metrics summed while an episode is active."""
+
+  def reset(self, rng) -> State:
+    st = self.env.reset(rng)
+    metrics = dict(st.metrics)
+    metrics['reward'] = st.reward
+    em = EvalMetrics(episode_metrics={k: torch.zeros_like(v) for k, v in metrics.items()},
+                     active_episodes=torch.ones_like(st.reward),
+                     episode_steps=torch.zeros_like(st.reward))
+    info = dict(st.info)
+    info['eval_metrics'] = em
+    return st.replace(metrics=metrics, info=info)
+
+  def step(self, state: State, action) -> State:
+    em = state.info['eval_metrics']
+    if not isinstance(em, EvalMetrics):
+      raise ValueError(f'Incorrect type for state_metrics: {type(em)}')
+    info = dict(state.info)
+    del info['eval_metrics']
+    nstate = self.env.step(state.replace(info=info), action)
+    metrics = dict(nstate.metrics)
+    metrics['reward'] = nstate.reward
+    episode_steps = torch.where(em.active_episodes != 0, nstate.info['steps'], em.episode_steps)
+    episode_metrics = {k: em.episode_metrics[k] + metrics[k] * em.active_episodes
+                       for k in em.episode_metrics}
+    active = em.active_episodes * (1 - nstate.done)
+    ninfo = dict(nstate.info)
+    ninfo['eval_metrics'] = EvalMetrics(episode_metrics=episode_metrics, active_episodes=active,
+                                        episode_steps=episode_steps)
+    return nstate.replace(metrics=metrics, info=ninfo)
+
+
+# ---------------------------------------------------------------------------
+# gym-API adapters (`wrappers.py:206-337`) -- gym itself is not a dependency:
+# spaces are plain Box descriptions; outputs stay device tensors (the role of
+# the reference's JaxToTorchWrapper DLPack hop, `to_torch.py:28-64`).
+# ---------------------------------------------------------------------------
+
+@dataclasses.dataclass(frozen=True)
+class Box:
+  """A gym.spaces.Box-like description (low, high, shape, dtype)."""
+  low: np.ndarray
+  high: np.ndarray
+  shape: tuple
+  dtype: str = 'float32'
+
+
+def _box(n, bound, batch=None):
+  shape = (n,) if batch is None else (batch, n)
+  high = np.full(shape, bound, np.float32)
+  return Box(low=-high, high=high, shape=shape)
+
+
+def split_key(key):
+  """Two child keys of a (2,) uint32 key (the reference's
+  `jp.random_split(key)`; threefry parity is unpinned)."""
+  s = key_to_seed(key)
+  out = []
+  for i in (1, 2):
+    z = (s + 0x9E3779B97F4A7C15 * i) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    z ^= z >> 31
+    out.append(np.array([z >> 32, z & 0xFFFFFFFF], np.uint32))
+  return out
+
+
+class GymWrapper:
+  """`wrappers.py:206-262`: one Brax env behind the gym Env API."""
+
+  def __init__(self, env: Env, seed: int = 0, backend: Optional[str] = None):
+    self._env = env
+    self.metadata = {'render.modes': ['human', 'rgb_array'],
+                     'video.frames_per_second': 1 / float(env.sys.config.dt)}
+    self.seed(seed)
+    self.backend = backend
+    self._state = None
+    self.observation_space = _box(env.observation_size, np.inf)
+    self.action_space = _box(env.action_size, 1.0)
+
+  def reset(self):
+    self._key, key2 = split_key(self._key)
+    self._state = self._env.reset(key2)
+    return self._state.obs
+
+  def step(self, action):
+    self._state = self._env.step(self._state, action)
+    info = {**self._state.metrics, **self._state.info}
+    return self._state.obs, self._state.reward, self._state.done, info
+
+  def seed(self, seed: int = 0):
+    self._key = np.array([0, seed], np.uint32)  # jax.random.PRNGKey(seed) layout
+
+  def render(self, mode='human'):
+    raise NotImplementedError('rendering (brax.io) is outside the MI355X path')
+
+
+class VectorGymWrapper(GymWrapper):
+  """`wrappers.py:265-337`: a batched Brax env behind the gym VectorEnv API."""
+
+  def __init__(self, env: Env, seed: int = 0, backend: Optional[str] = None):
+    if not hasattr(env, 'batch_size') or not env.batch_size:
+      raise ValueError('underlying env must be batched')
+    super().__init__(env, seed, backend)
+    self.num_envs = env.batch_size
+    self.single_observation_space = self.observation_space
+    self.single_action_space = self.action_space
+    self.observation_space = _box(env.observation_size, np.inf, self.num_envs)
+    self.action_space = _box(env.action_size, 1.0, self.num_envs)
+
+
+class TorchWrapper:
+  """`to_torch.py:28-64` (JaxToTorchWrapper): outputs as torch tensors on
+  `device`; brax_amd outputs already are device tensors, so this only moves
+  them when another device is asked for."""
+
+  def __init__(self, env, device=None):
+    self.env = env
+    self.device = device
+
+  def __getattr__(self, name):
+    return getattr(self.env, name)
+
+  def _t(self, x):
+    if isinstance(x, dict):
+      return {k: self._t(v) for k, v in x.items()}
+    if isinstance(x, torch.Tensor) and self.device is not None:
+      return x.to(self.device)
+    return x
+
+  def reset(self):
+    return self._t(self.env.reset())
+
+  def step(self, action):
+    obs, reward, done, info = self.env.step(action)
+    return self._t(obs), self._t(reward), self._t(done), self._t(info)

@@ -118,3 +118,42 @@ def test_wrapped_torch_env(dev, name):
     assert torch.isfinite(st.obs).all() and torch.isfinite(st.qp.pos).all()
     assert int(st.info['steps'].max()) <= 5
   assert 'truncation' in st.info and 'first_qp' in st.info
+
+
+def test_eval_wrapper_accumulates(dev):
+  """EvalWrapper (`wrappers.py:169-203`): episode metrics are the sums of the
+  per-step metrics while the episode is active; steps freeze when done."""
+  from brax_amd import envs
+  env = envs.create('ant', batch_size=32, episode_length=4, eval_metrics=True, device=dev)
+  st = env.reset(np.array([0, 11], np.uint32))
+  em0 = st.info['eval_metrics']
+  assert float(em0.active_episodes.min()) == 1.0
+  sums = torch.zeros(32, device=dev)
+  active = torch.ones(32, device=dev)
+  for k in range(6):
+    st = env.step(st, torch.rand((32, 8), device=dev) * 2 - 1)
+    sums = sums + st.reward * active
+    active = active * (1 - st.done)
+  em = st.info['eval_metrics']
+  torch.testing.assert_close(em.episode_metrics['reward'], sums)
+  torch.testing.assert_close(em.active_episodes, active)
+  assert float(em.episode_steps.max()) <= 4
+
+
+def test_vector_gym_wrapper(dev):
+  """VectorGymWrapper / create_gym_env (`wrappers.py:265-337`,
+  `envs/__init__.py:118-130`): device tensors out, auto-reset inside."""
+  from brax_amd import envs
+  from brax_amd.envs.to_torch import JaxToTorchWrapper
+  g = JaxToTorchWrapper(envs.create_gym_env('ant', batch_size=64, seed=3, device=dev),
+                        device=dev)
+  obs = g.reset()
+  assert obs.shape == (64, 87) and obs.is_cuda
+  assert g.action_space.shape == (64, 8) and g.single_observation_space.shape == (87,)
+  for _ in range(3):
+    obs, reward, done, info = g.step(torch.rand((64, 8), device=dev) * 2 - 1)
+  assert reward.shape == (64,) and done.shape == (64,)
+  assert 'truncation' in info and 'x_velocity' in info
+  single = envs.create_gym_env('hopper', device=dev)
+  o = single.reset()
+  assert o.shape[-1] == single.observation_space.shape[0]
