@@ -512,7 +512,7 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
     return fail("auto_reset needs first_qp and first_obs");
   if (env->episode_length > 0 && (!out->steps || !out->truncation))
     return fail("episode wrapper needs steps and truncation buffers");
-  if (env->kind < BX_ENV_ANT || env->kind > BX_ENV_HALFCHEETAH) return fail("unknown env kind");
+  if (env->kind < BX_ENV_ANT || env->kind > BX_ENV_HUMANOID_STANDUP) return fail("unknown env kind");
   EnvArgs a{};
   a.blob = S->blob;
   a.n_envs = n_envs;

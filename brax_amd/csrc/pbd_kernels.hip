@@ -1551,7 +1551,7 @@ template <int L>
 __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int lane, int kind,
                             int obs_size, const float* act, int aw, bool valid, float* obs_out) {
   joint_angles<L>(c, H, E, lane);
-  if (kind == BX_ENV_HUMANOID && lane == 0) {
+  if ((kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP) && lane == 0) {
     v3 com;
     float msum;
     humanoid_com(c, H, E.qp, com, msum);
@@ -1765,6 +1765,13 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
           m[0] = norm(com1); m[1] = fwd; m[2] = hr; m[3] = fwd; m[4] = -ctrl;
           m[5] = com1.x; m[6] = v.x; m[7] = com1.y; m[8] = v.y;
         }
+      } else if (kind == BX_ENV_HUMANOID_STANDUP) {
+        // humanoid_standup.py:232-247: uph = z / dt, reward = uph + 1 - 0.01 sum(a^2);
+        // done is left as it came in
+        float uph = (p1.z - 0.f) / dt;
+        float ctrl = P.coef[1] * sq;
+        reward = uph + 1.f - ctrl;
+        if (m) { m[0] = uph; m[1] = -ctrl; }
       }
       reward_sum = rep == 0 ? reward : reward_sum + reward;
       E.red[0] = done;

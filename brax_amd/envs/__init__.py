@@ -12,6 +12,7 @@ from brax_amd.envs.ant import Ant
 from brax_amd.envs.env import Env, PhysicsEnv, State, Wrapper
 from brax_amd.envs.half_cheetah import Halfcheetah
 from brax_amd.envs.humanoid import Humanoid
+from brax_amd.envs.humanoid_standup import HumanoidStandup
 from brax_amd.envs import torch_envs
 
 _envs = {
@@ -20,6 +21,7 @@ _envs = {
     'halfcheetah': Halfcheetah,
     'hopper': torch_envs.Hopper,
     'humanoid': Humanoid,
+    'humanoidstandup': HumanoidStandup,
     'inverted_pendulum': torch_envs.InvertedPendulum,
     'inverted_double_pendulum': torch_envs.InvertedDoublePendulum,
     'reacher': torch_envs.Reacher,

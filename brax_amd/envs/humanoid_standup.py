@@ -1,0 +1,29 @@
+"""HumanoidStandup (`brax/envs/humanoid_standup.py:210-297`) on MI355X.
+
+The Humanoid observation program (240 dims, `humanoid_standup.py:249-290`)
+on its own system (lying start, 22 contact rows); reward = torso z / dt + 1
+- 0.01 sum(a^2); done is left as it came in. One fused kernel launch
+(env kind BX_ENV_HUMANOID_STANDUP).
+"""
+import numpy as np
+
+from brax_amd.envs import robots
+from brax_amd.envs.env import PhysicsEnv
+
+
+class HumanoidStandup(PhysicsEnv):
+  """Trains a humanoid to stand up."""
+
+  kind = 4  # BX_ENV_HUMANOID_STANDUP
+  metric_keys = ('reward_linup', 'reward_quadctrl')
+
+  def __init__(self, legacy_spring=False, **kwargs):
+    if legacy_spring:
+      raise NotImplementedError('legacy_spring dynamics are outside the MI355X path')
+    super().__init__(robots.HUMANOID_STANDUP_CONFIG, **kwargs)
+    self.reset_noise_scale = 0.01
+    self.coef = np.array([0, 0.01, 0, 0, 0, 0, 0, 0], np.float32)
+    D = self.sys.num_joint_dof
+    M = self.sys.num_bodies - 1
+    qfrc = sum(int(d) for d in self.sys.desc['joint_dof'][self.sys.desc['act_joint']])
+    self.obs_size = 1 + 4 + D + 3 + 3 + D + 9 * M + 3 * M + 3 * M + qfrc

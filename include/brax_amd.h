@@ -42,7 +42,8 @@ enum { BX_ACT_TORQUE = 0, BX_ACT_ANGLE = 1 };
 enum { BX_COL_CAPSULE_PLANE = 0, BX_COL_CAPSULE_CAPSULE = 1 };
 enum { BX_FORCE_THRUSTER = 0, BX_FORCE_TWISTER = 1 };
 /* env layer kinds (obs / reward programs) */
-enum { BX_ENV_NONE = 0, BX_ENV_ANT = 1, BX_ENV_HUMANOID = 2, BX_ENV_HALFCHEETAH = 3 };
+enum { BX_ENV_NONE = 0, BX_ENV_ANT = 1, BX_ENV_HUMANOID = 2, BX_ENV_HALFCHEETAH = 3,
+       BX_ENV_HUMANOID_STANDUP = 4 };
 
 /*
  * System descriptor: the compiled constant arrays of `brax.System`
@@ -249,6 +250,13 @@ int bx_system_info(bx_system* sys, int64_t n_envs, const bx_qp* qp,
 int bx_env_observe(bx_system* sys, const bx_env_params* env, int64_t n_envs,
                    const bx_qp* qp, const float* act, int64_t act_stride,
                    int64_t act_width, float* obs, void* stream);
+
+/* Joint angles and angular velocities of every joint dof (Joint.angle_vel,
+ * joints.py:197-226,311-319,388-415; Spherical: line-of-nodes x-y'-z''
+ * angles), in joint order: angle and vel are (B, num_joint_dof) contiguous
+ * (num_joint_dof counted after sphericalisation). */
+int bx_system_joint_angles(bx_system* sys, int64_t n_envs, const bx_qp* qp, float* angle,
+                           float* vel, void* stream);
 
 /* Counter-based uniform [lo,hi) fill keyed by (seed, global index); used for
  * reset noise and synthetic actions (the JAX threefry stream is parity

@@ -474,6 +474,10 @@ def main():
     env = importlib.import_module('brax.envs.humanoid').Humanoid()
     save('desc_humanoid', dump_desc(env.sys))
     save('traj_humanoid', env_traj(env, 'humanoid', 16, 4))
+  if want('humanoidstandup'):
+    env = envs.get_environment('humanoidstandup')
+    save('desc_humanoidstandup', dump_desc(env.sys))
+    save('traj_humanoidstandup', env_traj(env, 'humanoidstandup', 16, 4))
   if want('halfcheetah'):
     env = envs.get_environment('halfcheetah')
     save('desc_halfcheetah', dump_desc(env.sys))

@@ -1422,7 +1422,8 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
       int n = 0;
       if (kind == BX_ENV_ANT) n = obs_ant(&s, q, info_c + e * 6 * N, obs + e * obs_size);
       else if (kind == BX_ENV_HALFCHEETAH) n = obs_halfcheetah(&s, q, obs + e * obs_size);
-      else if (kind == BX_ENV_HUMANOID) n = obs_humanoid(&s, q, act + e * s.aw, obs + e * obs_size);
+      else if (kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP)
+        n = obs_humanoid(&s, q, act + e * s.aw, obs + e * obs_size);
       if (n != obs_size) rc = -1;
     }
     free(q);
@@ -1507,6 +1508,14 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
          * y_position, y_velocity */
         m[0] = norm3(ca); m[1] = fwd; m[2] = 5; m[3] = fwd; m[4] = -ctrl;
         m[5] = ca[0]; m[6] = v[0]; m[7] = ca[1]; m[8] = v[1];
+      } else if (kind == BX_ENV_HUMANOID_STANDUP) {
+        /* humanoid_standup.py:232-247; done unchanged; sorted metrics:
+         * reward_linup, reward_quadctrl */
+        n = obs_humanoid(&s, w.qp, a, o);
+        R uph = (w.qp[0].pos[2] - (R)0) / dt;
+        R ctrl = (R)0.01 * sq;
+        reward[e] = uph + (R)1 - ctrl;
+        m[0] = uph; m[1] = -ctrl;
       }
       if (n != obs_size) rc = -1;
     }

@@ -8,6 +8,7 @@ from brax_amd.envs import robots
 from brax_amd.envs.mountain import ant_mountain_config
 
 ENV_CONFIG = {
+    'humanoidstandup': robots.HUMANOID_STANDUP_CONFIG,
     'ant': configs.ANT_CONFIG,
     'humanoid': configs.HUMANOID_CONFIG,
     'halfcheetah': configs.HALFCHEETAH_CONFIG,

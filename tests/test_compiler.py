@@ -6,7 +6,7 @@ from brax_amd import compiler
 from tests.conftest import golden
 from tests.helpers import CAPSULES, ROBOTS, compiled, config_for
 
-NAMES = (['ant', 'humanoid', 'halfcheetah', 'mountain1', 'mountain2', 'mountain4', 'mountain1nn']
+NAMES = (['ant', 'humanoid', 'halfcheetah', 'humanoidstandup', 'mountain1', 'mountain2', 'mountain4', 'mountain1nn']
          + ROBOTS + CAPSULES)
 
 

@@ -24,7 +24,7 @@ from tests.helpers import CAPSULES, QP_FIELDS, ROBOTS, compiled, normwise
 
 pytestmark = pytest.mark.gpu
 
-ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah']
+ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup']
 SYS_TRAJ = ['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES
 POS_TOL = 1e-5
 

@@ -9,7 +9,7 @@ import pytest
 from tests.conftest import golden
 from tests.helpers import CAPSULES, ROBOTS, compiled
 
-ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah']
+ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup']
 SYS_TRAJ = ['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES
 
 
