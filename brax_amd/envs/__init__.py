@@ -17,6 +17,8 @@ from brax_amd.envs import torch_envs
 
 _envs = {
     'acrobot': torch_envs.Acrobot,
+    'fast': torch_envs.Fast,
+    'grasp': torch_envs.Grasp,
     'ant': functools.partial(Ant, use_contact_forces=True),
     'halfcheetah': Halfcheetah,
     'hopper': torch_envs.Hopper,
@@ -24,9 +26,11 @@ _envs = {
     'humanoidstandup': HumanoidStandup,
     'inverted_pendulum': torch_envs.InvertedPendulum,
     'inverted_double_pendulum': torch_envs.InvertedDoublePendulum,
+    'pusher': torch_envs.Pusher,
     'reacher': torch_envs.Reacher,
     'reacherangle': torch_envs.ReacherAngle,
     'swimmer': torch_envs.Swimmer,
+    'ur5e': torch_envs.Ur5e,
     'walker2d': torch_envs.Walker2d,
 }
 

@@ -439,11 +439,13 @@ ROBOTS = {
     'reacherangle': (8, 6, 0),
     'acrobot': (8, 6, 0),
     'ur5e': (4, 4, 0),
+    'pusher': (8, 4, 0),
+    'grasp': (4, 3, 0),
 }
 
 
 TORCH_ENVS = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum',
-              'swimmer', 'reacher', 'reacherangle', 'acrobot']
+              'swimmer', 'reacher', 'reacherangle', 'acrobot', 'pusher', 'ur5e', 'grasp']
 
 
 def main():

@@ -21,7 +21,7 @@ from tests.helpers import QP_FIELDS, normwise
 pytestmark = pytest.mark.gpu
 
 ENVS = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum', 'swimmer',
-        'reacher', 'reacherangle', 'acrobot']
+        'reacher', 'reacherangle', 'acrobot', 'pusher', 'ur5e', 'grasp']
 TOL = 2e-5
 
 
@@ -46,6 +46,14 @@ def _state(env, T, t, dev):
   return State(qp=qp, obs=obs, reward=z, done=z.clone(), metrics=met, info={})
 
 
+def _info(T, t, dev, which='info_contact'):
+  """brax Info of the golden step t (only contact.vel is read by env layers)."""
+  from brax_amd.base import Info, P
+  c = torch.as_tensor(T[which][t], dtype=torch.float32, device=dev)
+  return Info(contact=P(c[..., :3], c[..., 3:]), joint=None, actuator=None, contact_pos=None,
+              contact_normal=None, contact_penetration=None)
+
+
 def _close(got, ref, tol, what):
   got = np.asarray(got, np.float64)
   ref = np.asarray(ref, np.float64)
@@ -62,13 +70,18 @@ def test_env_layer_vs_golden(dev, name):
   T = golden('envtraj_' + name)
   keys = [str(k) for k in T['metric_keys']]
   # reset observation of the golden reset state
-  _close(env._get_obs(qp_from_numpy(T['qp'][0], dev), None).cpu(), T['reset_obs'], TOL,
-         'reset obs')
+  if name not in ('ur5e', 'grasp'):  # their reset obs read the reset-time Info
+    _close(env._get_obs(qp_from_numpy(T['qp'][0], dev), None).cpu(), T['reset_obs'], TOL,
+           'reset obs')
   for t in range(T['action'].shape[0]):
     st = _state(env, T, t, dev)
     act = torch.as_tensor(T['action'][t], dtype=torch.float32, device=dev)
-    qp1 = qp_from_numpy(T['qp'][t + 1], dev)
-    new = env._step(st, act, qp1, None)
+    q1 = T['qp'][t + 1].copy()
+    if hasattr(env, '_teleport'):
+      # obs and reward are taken before a hit target is teleported (grasp.py:
+      # 150-183, ur5e.py:60-88); the target body does not move in the physics
+      q1[:, env.target_idx] = T['qp'][t][:, env.target_idx]
+    new = env._step(st, act, qp_from_numpy(q1, dev), _info(T, t, dev))
     _close(new.obs.cpu(), T['obs'][t + 1], TOL, f'obs t={t}')
     _close(new.reward.cpu()[:, None], T['reward'][t][:, None], TOL, f'reward t={t}')
     assert np.array_equal(new.done.cpu().numpy(), T['done'][t]), f'done t={t}'
@@ -89,14 +102,17 @@ def test_env_step_vs_golden(dev, oracle_lib, name):
     st = _state(env, T, t, dev)
     act = torch.as_tensor(T['action'][t], dtype=torch.float32, device=dev)
     new = env.step(st, act)
-    # the system action the env fed to the kernel (swimmer adds drag forces)
-    sys_act = env._system_action(st, env._action(act, act.shape[0])).cpu().numpy()
-    ref, _ = o64.system_step(T['qp'][t], sys_act)
+    # the (qp, action) the env fed to the kernel (swimmer adds drag forces,
+    # grasp moves the palm first)
+    qp_in, sys_act = env._pre_step(st, env._action(act, act.shape[0]))
+    qp_in, sys_act = qp_in.numpy(), sys_act.cpu().numpy()
+    ref, _ = o64.system_step(qp_in, sys_act)
     rng = np.random.default_rng(1234)
-    ins = [T['qp'][t]] + [T['qp'][t] * (1 + rng.uniform(-6e-8, 6e-8, T['qp'][t].shape))
-                          for _ in range(3)]
+    ins = [qp_in] + [qp_in * (1 + rng.uniform(-6e-8, 6e-8, qp_in.shape)) for _ in range(3)]
     outs = [o32.system_step(q.astype(np.float32), sys_act.astype(np.float32))[0] for q in ins]
     got = new.qp.numpy()
+    if hasattr(env, '_teleport'):  # teleported targets draw from the device RNG
+      got[:, env.target_idx] = ref[:, env.target_idx]
     for f, sl in QP_FIELDS.items():
       e32 = np.max([normwise(x[..., sl], ref[..., sl]) for x in outs])
       nw = normwise(got[..., sl], ref[..., sl])

@@ -31,7 +31,8 @@ def test_system_step_matches_reference(oracle_lib, name):
     assert np.abs(out - T['qp'][t + 1]).max() < tol
     ic = T['info_contact'][t]
     assert np.abs(info['contact'] - ic).max() < 10 * tol * max(1., np.abs(ic).max())
-    assert np.abs(info['actuator'] - T['info_actuator'][t]).max() < 1e-9
+    ia = T['info_actuator'][t]
+    assert np.abs(info['actuator'] - ia).max() < tol * max(1., np.abs(ia).max())
     got, ref = info['contact_penetration'], T['contact_penetration'][t]
     if (np.asarray(o.desc['col_cutoff']) > 0).any():
       # culled Info rows are in top_k order, and exactly tied distances (the
