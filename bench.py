@@ -242,17 +242,25 @@ def main():
   if dist is not None:
     dist.barrier()
   torch.cuda.synchronize()
+  # per-launch HIP events on every EVENT_EVERY-th step (the stream the kernel
+  # runs on): the kernel's average launch duration for `roofline`, without
+  # putting event packets between every pair of launches
+  EVENT_EVERY = 8
   events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for _ in range(args.steps)]
+            if k % EVENT_EVERY == 0 else None for k in range(args.steps)]
+  span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+  span[0].record()
   t0 = time.perf_counter()
   for k in range(args.steps):
     state = one_step(state, args.warmup + k, events[k])
+  span[1].record()
   torch.cuda.synchronize()
   if dist is not None:
     dist.barrier()
   torch.cuda.synchronize()
   elapsed = time.perf_counter() - t0
-  kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+  kern_ms = float(np.mean([ev[0].elapsed_time(ev[1]) for ev in events if ev is not None]))
+  span_ms = span[0].elapsed_time(span[1]) / args.steps
   if dist is not None:
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -292,6 +300,7 @@ def main():
                    'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
                    'traffic': traffic,
                    'kernel': 'bx::env_step_kernel<16>', 'kernel_ms': kern_ms,
+                   'span_ms_per_step': span_ms,
                    'bytes_per_launch': bytes_per_launch,
                    'note': 'fused env-step is VALU/latency-bound (AI ~61 flop/B, '
                            'SURVEY 8(d)); compute view below',

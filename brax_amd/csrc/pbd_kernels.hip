@@ -1676,6 +1676,13 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   const int kind = P.kind;
   const float* act = valid ? A.act + e * A.act_stride : nullptr;
   const int aw = (int)A.act_width;
+  // every independent load first, so their latencies overlap: the hoisted
+  // constants, the per-env scalars, then the state
+  Hoist<M> X;
+  if constexpr (S) load_hoist<M>(c, H, lane, X);
+  // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
+  float done_in = valid ? A.in.done[e] : 0.f;
+  float steps_in = valid && A.in.steps ? A.in.steps[e] : 0.f;
   for (int b = lane; b < H.N; b += L) {
     if (valid) {
       load_qp_global(A.in.qp, e, b, E.qp + b * QP_STRIDE);
@@ -1685,15 +1692,11 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
     }
   }
   sync();
-  // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
-  float done_in = valid ? A.in.done[e] : 0.f;
   float steps = 0.f;
-  if (valid && A.in.steps) steps = (P.auto_reset && done_in != 0.f) ? 0.f : A.in.steps[e];
+  if (valid && A.in.steps) steps = (P.auto_reset && done_in != 0.f) ? 0.f : steps_in;
   float done = P.auto_reset ? 0.f : done_in;
   float reward_sum = 0.f;
   const int reps = P.episode_length > 0 ? (P.action_repeat > 0 ? P.action_repeat : 1) : 1;
-  Hoist<M> X;
-  if constexpr (S) load_hoist<M>(c, H, lane, X);
   // action sum of squares (ctrl cost), shared by every repeat
   float sq = 0.f;
   if (valid && lane == 0)
