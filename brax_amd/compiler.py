@@ -19,6 +19,8 @@ own compiled arrays pin this compiler (tests/test_compiler.py).
 import copy
 import warnings
 
+import itertools
+
 import numpy as np
 
 from brax_amd import config as cfgmod
@@ -191,6 +193,22 @@ def _near_neighbors(pairs, index, cutoff):
   return dict(pairs=rows, flat=[i * U + j for i, j in cells], cutoff=int(cutoff))
 
 
+_BOX_CORNERS = np.array(list(itertools.product((-1, 1), (-1, 1), (-1, 1))), np.float64)
+
+
+def _point_ends(col, mesh_geoms):
+  """Body-frame contact points of a box (8 corners, `geometry.py:123-137`) or
+  a point mesh (its scaled vertices, `geometry.py:312-357`)."""
+  rot = euler_to_quat(vec(col.rotation))
+  if col.WhichOneof('type') == 'box':
+    pts = _BOX_CORNERS * vec(col.box.halfsize)
+  else:
+    g = mesh_geoms[col.mesh.name]
+    scale = col.mesh.scale if col.mesh.scale else 1
+    pts = np.array([[v.x * scale, v.y * scale, v.z * scale] for v in g.vertices], np.float64)
+  return [rotate(p, rot) + vec(col.position) for p in pts]
+
+
 def _colliders(config, index):
   """Collider groups and flattened contact rows (`colliders.py:891-1023`)."""
   # only the capsule/sphere/plane subset of `collider_pairs` is on the path
@@ -199,8 +217,15 @@ def _colliders(config, index):
                 ('capsule', 'plane'), ('capsule', 'capsule'),
                 ('capsule', 'mesh'), ('capsule', 'clipped_plane'),
                 ('mesh', 'plane'), ('box', 'box')]
+  # box-plane and mesh-plane contacts are point-plane contacts of the box
+  # corners / mesh vertices (`colliders.py:667-696`): exactly capsule_plane
+  # with a zero radius, so they compile to CAPSULE_PLANE rows
   supported = {('capsule', 'plane'): CAPSULE_PLANE,
-               ('capsule', 'capsule'): CAPSULE_CAPSULE}
+               ('capsule', 'capsule'): CAPSULE_CAPSULE,
+               ('box', 'plane'): CAPSULE_PLANE,
+               ('mesh', 'plane'): CAPSULE_PLANE}
+  mesh_geoms = {mg.name: mg for mg in config.mesh_geometries}
+  unique_meshes = {}
   cols = []
   for b in config.bodies:
     for c_idx, c in enumerate(b.colliders):
@@ -213,15 +238,16 @@ def _colliders(config, index):
         nc.capsule.length = 2 * c.sphere.radius
         nc.capsule.end = 1
         c = nc
+      if c.WhichOneof('type') == 'mesh':
+        unique_meshes[c.mesh.name] = 1
       cols.append((c, b, c_idx))
 
   include = {(ci.first, ci.second) for ci in config.collide_include}
   # NB: a generator, consumed by the first membership test (App. A.1)
   parents = ((j.parent, j.child) for j in config.joints)
   groups = []
-  for (type_a, type_b) in pair_types:
-    cols_a = [x for x in cols if x[0].WhichOneof('type') == type_a]
-    cols_b = [x for x in cols if x[0].WhichOneof('type') == type_b]
+
+  def pairs_of(cols_a, cols_b):
     cols_a = [x for x in cols_a if not x[1].frozen.all]
     cols_ab = []
     pair_count = {}
@@ -244,18 +270,29 @@ def _colliders(config, index):
           cols_ab.append((ca, ca_idx, ba, cb, cb_idx, bb))
           pair_count[(ba.name, ca_idx, bb.name, cb_idx)] = 1
           pair_count[(bb.name, cb_idx, ba.name, ca_idx)] = 1
-    for b_is_frozen in (True, False):
-      flt = [x for x in cols_ab if x[-1].frozen.all == b_is_frozen]
-      if not flt:
-        continue
-      if (type_a, type_b) not in supported:
-        raise NotImplementedError(
-            f'collider pair {type_a}/{type_b} is outside the MI355X path')
-      grp = dict(oneway=b_is_frozen, fn=supported[(type_a, type_b)], pairs=flt, cutoff=0)
-      if (config.collider_cutoff and len(flt) > config.collider_cutoff and
-          (type_a, type_b) == ('capsule', 'capsule')):
-        grp.update(_near_neighbors(flt, index, config.collider_cutoff))
-      groups.append(grp)
+    return cols_ab
+
+  for (type_a, type_b) in pair_types:
+    # mesh pairs form one collider per unique mesh name (colliders.py:941-949)
+    replicas = list(unique_meshes) if 'mesh' in (type_a, type_b) else [None]
+    for mesh_name in replicas:
+      def of_type(t, mesh_name=mesh_name):
+        return [x for x in cols if x[0].WhichOneof('type') == t and
+                (t != 'mesh' or x[0].mesh.name == mesh_name)]
+      cols_ab = pairs_of(of_type(type_a), of_type(type_b))
+      for b_is_frozen in (True, False):
+        flt = [x for x in cols_ab if x[-1].frozen.all == b_is_frozen]
+        if not flt:
+          continue
+        if (type_a, type_b) not in supported:
+          raise NotImplementedError(
+              f'collider pair {type_a}/{type_b} is outside the MI355X path')
+        grp = dict(oneway=b_is_frozen, fn=supported[(type_a, type_b)], pairs=flt, cutoff=0,
+                   kind=type_a)
+        if (config.collider_cutoff and len(flt) > config.collider_cutoff and
+            (type_a, type_b) == ('capsule', 'capsule')):
+          grp.update(_near_neighbors(flt, index, config.collider_cutoff))
+        groups.append(grp)
 
   h = config.dt / config.substeps
   g_norm = np.linalg.norm(vec(config.gravity))
@@ -272,7 +309,11 @@ def _colliders(config, index):
     out['col_velocity_threshold'].append(g_norm * h * 4.0)
     out['col_baumgarte_erp'].append(config.baumgarte_erp * config.substeps / config.dt)
     out['col_cutoff'].append(g['cutoff'])
-    if g['fn'] == CAPSULE_PLANE:
+    if g['kind'] in ('box', 'mesh'):
+      # Box corners (`geometry.py:123-137`) / PointMesh vertices (:312-357)
+      # in the body frame, as zero-radius capsule ends
+      ends_l = [_point_ends(ca, mesh_geoms) for ca, _, _, _, _, _ in g['pairs']]
+    elif g['fn'] == CAPSULE_PLANE:
       # CapsuleEnd (`geometry.py:261-288`): 1 or 2 ends; mixed -> pad by dup
       ends_l = []
       for ca, _, _, _, _, _ in g['pairs']:
@@ -288,6 +329,7 @@ def _colliders(config, index):
     for pi, (ca, _, ba, cb, _, bb) in enumerate(g['pairs']):
       fa = ca.material.friction * cb.material.friction
       ea = ca.material.elasticity * cb.material.elasticity
+      a_rad = 0. if g['kind'] in ('box', 'mesh') else ca.capsule.radius
       if g['fn'] == CAPSULE_PLANE:
         ends = ends_l[pi]
         b_end, b_rad = np.zeros(3), 0.
@@ -302,7 +344,7 @@ def _colliders(config, index):
         rows['body_b'].append(index[bb.name])
         rows['a_pos'].append(vec(ca.position))
         rows['a_end'].append(e)
-        rows['a_radius'].append(ca.capsule.radius)
+        rows['a_radius'].append(a_rad)
         rows['b_pos'].append(vec(cb.position))
         rows['b_end'].append(b_end)
         rows['b_radius'].append(b_rad)
@@ -521,8 +563,6 @@ def default_angle(config, default_index=0):
   return np.concatenate([angles[j.name] for j in config.joints])
 
 
-_BOX_CORNERS = np.array([[x, y, z] for x in (-1, 1) for y in (-1, 1)
-                         for z in (-1, 1)], np.float64)
 
 
 def compile_reset(config, index, default_index=0):

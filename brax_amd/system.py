@@ -98,7 +98,8 @@ class System:
     if isinstance(config, str):
       config = cfgmod.parse(config)
     self.config, self.desc, meta = compiler.compile_system(config)
-    self.reset_desc = compiler.compile_reset(self.config, meta['body_index'])
+    self._body_index = meta['body_index']
+    self.reset_desc = compiler.compile_reset(self.config, self._body_index)
     self.num_bodies = int(self.desc['n_bodies'])
     self.num_joints = len(self.config.joints)
     self.num_joint_dof = meta['num_joint_dof']
@@ -122,23 +123,35 @@ class System:
     self.device = torch.device(device)
     if self.device.type != 'cuda':
       raise _native.NativeError('brax_amd runs on MI355X devices only')
-    lib = _native.lib()
+    self._h = self._create(self.reset_desc)
+    self._default_h = {0: self._h}  # one handle per config.defaults index used
+    self.lanes = _native.lib().bx_system_lanes(self._h)
+
+  def _create(self, reset_desc):
     cd, keep = abi.make_desc(self.desc)
-    rd, keep_r = abi.make_reset_desc(self.reset_desc)
+    rd, keep_r = abi.make_reset_desc(reset_desc)
     h = C.c_void_p()
-    _native.check(lib.bx_system_create(C.byref(cd), C.byref(rd),
-                                       self.device.index or 0, C.byref(h)))
+    _native.check(_native.lib().bx_system_create(C.byref(cd), C.byref(rd),
+                                                 self.device.index or 0, C.byref(h)))
     del keep, keep_r
-    self._h = h
-    self.lanes = lib.bx_system_lanes(h)
+    return h
+
+  def _default_handle(self, default_index):
+    """Handle whose reset descriptor is `config.defaults[default_index]`
+    (system.py:112-242 reads the default by index; an index past the list
+    means no default, as there)."""
+    if default_index not in self._default_h:
+      self._default_h[default_index] = self._create(
+          compiler.compile_reset(self.config, self._body_index, default_index))
+    return self._default_h[default_index]
 
   def __del__(self):
-    h = getattr(self, '_h', None)
-    if h is not None and h.value:
-      try:
-        _native.lib().bx_system_destroy(h)
-      except Exception:  # pylint: disable=broad-except
-        pass
+    for h in getattr(self, '_default_h', {}).values():
+      if h is not None and h.value:
+        try:
+          _native.lib().bx_system_destroy(h)
+        except Exception:  # pylint: disable=broad-except
+          pass
 
   # ---------------------------------------------------------------- helpers
   def _new_qp(self, lead):
@@ -171,8 +184,6 @@ class System:
 
     joint_angle / joint_velocity may carry a leading batch axis; the result
     then is batched too."""
-    if default_index != 0:
-      raise NotImplementedError('default_index != 0 is not supported on device yet')
     if joint_angle is None:
       joint_angle = self.default_angle(default_index)
     ja = torch.as_tensor(joint_angle, dtype=torch.float32, device=self.device)
@@ -191,7 +202,7 @@ class System:
     out = self._new_qp((B,))
     qs = qp_struct(out, True)
     _native.check(_native.lib().bx_system_default_qp(
-        self._h, B, C.c_void_p(ja.data_ptr()), C.c_void_p(jv.data_ptr()), C.byref(qs),
+        self._default_handle(default_index), B, C.c_void_p(ja.data_ptr()), C.c_void_p(jv.data_ptr()), C.byref(qs),
         _stream()))
     return out if batched else out[0]
 

@@ -168,13 +168,19 @@ def dump_desc(sys_):
       gcut.append(0)
     goneway.append(1 if isinstance(c, rc.OneWayCollider) else 0)
     fn = c.contact_fn.__name__
-    gfn.append({'capsule_plane': 0, 'capsule_capsule': 1}[fn])
+    gfn.append({'capsule_plane': 0, 'capsule_capsule': 1, 'box_plane': 0,
+                'mesh_plane': 0}[fn])
     gscale.append(c.collide_scale)
     gthr.append(c.velocity_threshold)
     gerp.append(c.baumgarte_erp)
     P = len(ca.body.idx)
     for p in range(P):
-      ends = [ca.end[p]] if fn == 'capsule_capsule' else list(ca.end[p])
+      if fn == 'box_plane':
+        ends = list(ca.corner[p])  # point-plane rows, zero radius
+      elif fn == 'mesh_plane':
+        ends = list(ca.vertices[p])
+      else:
+        ends = [ca.end[p]] if fn == 'capsule_capsule' else list(ca.end[p])
       for e in ends:
         rows['flat'].append(-1 if flats is None else int(flats[p]))
         rows['group'].append(g)
@@ -182,7 +188,7 @@ def dump_desc(sys_):
         rows['body_b'].append(cb.body.idx[p])
         rows['a_pos'].append(ca.pos[p])
         rows['a_end'].append(e)
-        rows['a_radius'].append(ca.radius[p])
+        rows['a_radius'].append(ca.radius[p] if fn not in ('box_plane', 'mesh_plane') else 0.)
         rows['b_pos'].append(cb.pos[p])
         rows['b_end'].append(cb.end[p] if fn == 'capsule_capsule' else np.zeros(3))
         rows['b_radius'].append(cb.radius[p] if fn == 'capsule_capsule' else 0.)
@@ -512,6 +518,21 @@ def main():
       s, di = capsule_sys(kind)
       save(f'desc_capsule_{kind}', dump_desc(s))
       save(f'traj_capsule_{kind}', sys_traj(s, 'capsule_' + kind, s.default_qp(di), 1, 1, 1.0, 0))
+  # point-plane scenes (box corners, mesh vertices): oracle/scenes.py
+  import scenes
+  from google.protobuf import text_format
+  import brax
+  point_scenes = {
+      'box_ground': (scenes.BOX_TEST_CONFIG, 0, 1),
+      'box_slide': (scenes.BOX_TEST_CONFIG, 1, 1),
+      'mesh_ground': (scenes.mesh_test_config(), 0, 30),
+      'mesh_tilt': (scenes.mesh_test_config(), 1, 12),
+  }
+  for name, (txt, di, T) in point_scenes.items():
+    if want(name):
+      s = brax.System(text_format.Parse(txt, brax.Config()))
+      save(f'desc_{name}', dump_desc(s))
+      save(f'traj_{name}', sys_traj(s, name, s.default_qp(di), 1, T, 1.0, 0))
   for n in (1, 2, 4):
     if want(f'mountain{n}'):
       s = ant_mountain_sys(n)

@@ -33,6 +33,9 @@ defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { x:
 defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { z: 2 } } qps { name: "Capsule3" pos { x: 3 z: 1 } } qps { name: "Capsule4" pos { x: 5 z: 1 } } }
 """
 CAPSULES = ['capsule_ground', 'capsule_capsule', 'capsule_cull']
+# point-plane scenes: BoxTest (box corners) and an inline-mesh MeshTest
+# (mesh vertices), oracle/scenes.py
+POINTS = ['box_ground', 'box_slide', 'mesh_ground', 'mesh_tilt']
 
 
 def config_for(name):
@@ -44,6 +47,10 @@ def config_for(name):
     if name == 'capsule_cull':
       cfg.collider_cutoff = 1
     return cfg
+  if name in POINTS:
+    from oracle import scenes
+    return cfgmod.parse(scenes.BOX_TEST_CONFIG if name.startswith('box')
+                        else scenes.mesh_test_config())
   if name == 'mountain1nn':
     cfg = ant_mountain_config(1)
     cfg.collider_cutoff = 9

@@ -4,10 +4,10 @@ import pytest
 
 from brax_amd import compiler
 from tests.conftest import golden
-from tests.helpers import CAPSULES, ROBOTS, compiled, config_for
+from tests.helpers import CAPSULES, POINTS, ROBOTS, compiled, config_for
 
 NAMES = (['ant', 'humanoid', 'halfcheetah', 'humanoidstandup', 'mountain1', 'mountain2', 'mountain4', 'mountain1nn']
-         + ROBOTS + CAPSULES)
+         + ROBOTS + CAPSULES + POINTS)
 
 
 @pytest.mark.parametrize('name', NAMES)

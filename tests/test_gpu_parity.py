@@ -20,12 +20,12 @@ import pytest
 import torch
 
 from tests.conftest import golden
-from tests.helpers import CAPSULES, QP_FIELDS, ROBOTS, compiled, normwise
+from tests.helpers import CAPSULES, POINTS, QP_FIELDS, ROBOTS, compiled, normwise
 
 pytestmark = pytest.mark.gpu
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup']
-SYS_TRAJ = ['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES
+SYS_TRAJ = ['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + POINTS
 POS_TOL = 1e-5
 
 
@@ -309,6 +309,31 @@ def test_capsule_scenes_kat(dev, kind):
     np.testing.assert_allclose(z[:4], [0.5, 0.25, 0.25, 0.25], atol=0.005)
   else:
     np.testing.assert_allclose(z[:2], [0.5, 1.25], atol=0.005)
+
+
+@pytest.mark.parametrize('name', ['box_ground', 'box_slide', 'mesh_ground'])
+def test_point_scenes_kat(dev, name):
+  """Box corners / mesh vertices against the plane: the reference's BoxTest
+  outcomes (`physics_test.py:67-83`, 2 decimals) and MeshTest's
+  `test_mesh_hits_ground` (:392-408) on the inline hexagonal prism of
+  oracle/scenes.py (half-height 0.1: it rests at z = 0.1). The starting
+  state is `default_qp(default_index)` built on the device."""
+  sys_ = _system(name, dev)
+  di = 1 if name == 'box_slide' else 0
+  qp = sys_.default_qp(di)
+  q0 = golden('traj_' + name)['qp'][0][0]
+  np.testing.assert_allclose(torch.cat([qp.pos, qp.rot, qp.vel, qp.ang], -1).cpu().numpy(),
+                             q0, atol=1e-6)
+  for _ in range(30 if name == 'mesh_ground' else 1):
+    qp, info = sys_.step(qp, torch.zeros(0, device=dev))
+  pos, vel = qp.pos[0].cpu().numpy(), qp.vel[0].cpu().numpy()
+  if name == 'mesh_ground':
+    assert abs(pos[2] - 0.1) < 0.005
+    return
+  assert abs(pos[2] - 0.5) < 0.005
+  assert sys_.num_contacts == 8 and float(info.contact_penetration.max()) < 0.01
+  if name == 'box_slide':
+    assert 1 < pos[0] < 1.5 and abs(vel[0]) < 0.005
 
 
 def test_culling_selects_nearest(dev, oracle_lib):

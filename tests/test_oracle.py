@@ -7,10 +7,10 @@ import numpy as np
 import pytest
 
 from tests.conftest import golden
-from tests.helpers import CAPSULES, ROBOTS, compiled
+from tests.helpers import CAPSULES, POINTS, ROBOTS, compiled
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup']
-SYS_TRAJ = ['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES
+SYS_TRAJ = ['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + POINTS
 
 
 def _oracle(oracle_lib, name, guard=False, dtype=np.float64):
@@ -137,3 +137,24 @@ def test_wrapper_semantics(oracle_lib):
     assert np.array_equal(done, T['done'][t + 1])
     assert np.array_equal(steps, T['steps'][t + 1])
     assert np.array_equal(trunc, T['truncation'][t + 1])
+
+
+def test_force_kats_float64(oracle_lib):
+  """The reference's ForceTest (`physics_test.py:813-831`) holds for the
+  float64 restatement, as for the reference's own (numpy, float64) run."""
+  from brax_amd import compiler
+  from brax_amd import config as cfgmod
+  text = """
+    dt: 0.1 substeps: 5000
+    bodies { name: "body" mass: 1 inertia { x: 1 y: 1 z: 1 } }
+    forces { name: "thruster" body: "body" strength: 2.5 thruster {} }
+    forces { name: "twister" body: "body" strength: 2.5 twister {} }"""
+  vc, d, meta = compiler.compile_system(cfgmod.parse(text))
+  o = oracle_lib.Oracle(d, compiler.compile_reset(vc, meta['body_index']), np.float64)
+  qp = np.zeros((1, 1, 13))
+  qp[..., 3] = 1
+  for f in (1, 5, 10):
+    out, _ = o.system_step(qp, f * np.array([[1., 0, 0, 0, 0, 0]]))
+    assert round(abs(out[0, 0, 0] - 0.5 * 2.5 * f * 0.1 ** 2), 3) == 0
+    out, _ = o.system_step(qp, f * np.array([[0, 0, 0, 1., 0, 0]]))
+    assert round(abs(out[0, 0, 10] - 2.5 * f * 0.1), 3) == 0
