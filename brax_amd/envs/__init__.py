@@ -18,6 +18,7 @@ from brax_amd.envs import torch_envs
 _envs = {
     'acrobot': torch_envs.Acrobot,
     'fast': torch_envs.Fast,
+    'fetch': torch_envs.Fetch,
     'grasp': torch_envs.Grasp,
     'ant': functools.partial(Ant, use_contact_forces=True),
     'halfcheetah': Halfcheetah,

@@ -447,11 +447,12 @@ ROBOTS = {
     'ur5e': (4, 4, 0),
     'pusher': (8, 4, 0),
     'grasp': (4, 3, 0),
+    'fetch': (4, 4, 0),
 }
 
 
 TORCH_ENVS = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum',
-              'swimmer', 'reacher', 'reacherangle', 'acrobot', 'pusher', 'ur5e', 'grasp']
+              'swimmer', 'reacher', 'reacherangle', 'acrobot', 'pusher', 'ur5e', 'grasp', 'fetch']
 
 
 def main():

@@ -17,7 +17,7 @@ ENV_CONFIG = {
 
 # the other registered envs' pbd systems (physics goldens, oracle/gen_golden.py)
 ROBOTS = ['inverted_pendulum', 'inverted_double_pendulum', 'swimmer', 'hopper', 'walker2d',
-          'reacher', 'reacherangle', 'acrobot', 'ur5e', 'pusher', 'grasp']
+          'reacher', 'reacherangle', 'acrobot', 'ur5e', 'pusher', 'grasp', 'fetch']
 
 
 # the CapsuleTest scene (reference `brax/tests/physics_test.py:292-328`) as

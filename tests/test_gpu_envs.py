@@ -21,7 +21,7 @@ from tests.helpers import QP_FIELDS, normwise
 pytestmark = pytest.mark.gpu
 
 ENVS = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum', 'swimmer',
-        'reacher', 'reacherangle', 'acrobot', 'pusher', 'ur5e', 'grasp']
+        'reacher', 'reacherangle', 'acrobot', 'pusher', 'ur5e', 'grasp', 'fetch']
 TOL = 2e-5
 
 
@@ -70,7 +70,7 @@ def test_env_layer_vs_golden(dev, name):
   T = golden('envtraj_' + name)
   keys = [str(k) for k in T['metric_keys']]
   # reset observation of the golden reset state
-  if name not in ('ur5e', 'grasp'):  # their reset obs read the reset-time Info
+  if name not in ('ur5e', 'grasp', 'fetch'):  # their reset obs read the reset-time Info
     _close(env._get_obs(qp_from_numpy(T['qp'][0], dev), None).cpu(), T['reset_obs'], TOL,
            'reset obs')
   for t in range(T['action'].shape[0]):
