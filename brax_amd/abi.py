@@ -12,7 +12,7 @@ i32p = C.POINTER(C.c_int32)
 f64p = C.POINTER(C.c_double)
 f32p = C.POINTER(C.c_float)
 
-ABI_VERSION = 2  # include/brax_amd.h BX_ABI_VERSION
+ABI_VERSION = 3  # include/brax_amd.h BX_ABI_VERSION
 
 _DESC_FIELDS = [
     ('n_bodies', C.c_int32), ('n_joints', C.c_int32), ('n_actuators', C.c_int32),
@@ -38,7 +38,12 @@ _DESC_FIELDS = [
     ('n_forces', C.c_int32), ('force_type', i32p), ('force_body', i32p),
     ('force_index', i32p), ('force_strength', f64p),
     ('col_cutoff', i32p), ('row_flat', i32p),
+    ('dynamics_mode', C.c_int32), ('joint_stiffness', f64p),
+    ('joint_spring_damping', f64p), ('joint_limit_strength', f64p),
 ]
+
+DYN_PBD, DYN_LEGACY_SPRING = 0, 1
+_SPRING_FIELDS = ('joint_stiffness', 'joint_spring_damping', 'joint_limit_strength')
 
 
 class BxDesc(C.Structure):
@@ -70,7 +75,8 @@ class BxInfo(C.Structure):
   _fields_ = [('contact_vel', BxField), ('contact_ang', BxField),
               ('actuator_vel', BxField), ('actuator_ang', BxField),
               ('contact_pos', C.c_void_p), ('contact_normal', C.c_void_p),
-              ('contact_penetration', C.c_void_p)]
+              ('contact_penetration', C.c_void_p),
+              ('joint_vel', BxField), ('joint_ang', BxField)]
 
 
 class BxEnvState(C.Structure):
@@ -113,6 +119,7 @@ def make_desc(d):
     s.gravity[k] = float(d['gravity'][k])
   s.velocity_damping = float(d['velocity_damping'])
   s.angular_damping = float(d['angular_damping'])
+  s.dynamics_mode = int(d.get('dynamics_mode', DYN_PBD))
   for name, ctype in _DESC_FIELDS:
     if ctype is i32p or ctype is f64p:
       if name in d:
@@ -123,6 +130,8 @@ def make_desc(d):
         v = -np.ones(len(d['row_group']))
       elif name.startswith('force_'):
         v = np.zeros(0)
+      elif name in _SPRING_FIELDS:
+        v = np.zeros(len(d['joint_type']))
       else:
         raise KeyError(name)
       a = _arr(v, np.int32 if ctype is i32p else np.float64)

@@ -9,6 +9,7 @@ ordering rules and quirks are the reference's, restated:
   colliders.get        `brax/physics/colliders.py:891-1023`
   Collidable/Capsule*  `brax/physics/geometry.py:78-99,242-288`
   joints.get / Joint   `brax/physics/joints.py:418-474,36-77`
+  spring_joints.get    `brax/physics/spring_joints.py:40-87,302-331` (legacy_spring)
   actuators.get        `brax/physics/actuators.py:115-164`
   Euler.__init__       `brax/physics/integrators.py:32-48`
   Collider.__init__    `brax/physics/colliders.py:95-114`
@@ -26,7 +27,9 @@ import numpy as np
 from brax_amd import config as cfgmod
 
 # joint kinds (descriptor `joint_type`)
-REVOLUTE, SPHERICAL = 1, 3
+REVOLUTE, UNIVERSAL, SPHERICAL = 1, 2, 3
+# dynamics modes (descriptor `dynamics_mode`)
+DYN_PBD, DYN_LEGACY_SPRING = 0, 1
 # actuator kinds (descriptor `act_type`)
 TORQUE, ANGLE = 0, 1
 # contact functions (descriptor `col_fn`)
@@ -366,11 +369,83 @@ def _colliders(config, index):
   return d
 
 
+def _joint_geometry(j):
+  """Offsets and axes shared by both joint families (`joints.py:58-77`,
+  `spring_joints.py:72-86`)."""
+  axis_c = np.array([rotate(e, euler_to_quat(vec(j.rotation))) for e in np.eye(3)])
+  ref = euler_to_quat(vec(j.reference_rotation))
+  axis_p = np.array([rotate(a, ref) for a in axis_c])
+  return vec(j.parent_offset), vec(j.child_offset), axis_p, axis_c
+
+
+def _spring_joints(config, index):
+  """Springy joint groups of `legacy_spring` (`spring_joints.py:302-331`):
+  every joint (stiffness > 0 is enforced by validate_config) goes to its dof's
+  group, groups in dof order, Revolute / Universal / Spherical; no
+  sphericalisation. Defaults (`spring_joints.py:59-67`): spring_damping =
+  coeff * sqrt(stiffness) with coeff 0.5 for Revolute (`:120`) and 2.0
+  otherwise; limit_strength = stiffness."""
+  groups = {}
+  for joint in config.joints:
+    if joint.stiffness > 0:
+      groups.setdefault(len(joint.angle_limit), []).append(joint)
+  groups = sorted(groups.items(), key=lambda kv: kv[0])
+  keys = ('type', 'dof', 'free_dofs', 'body_p', 'body_c', 'off_p', 'off_c', 'axis_p',
+          'axis_c', 'limit', 'damping', 'scale_pos', 'scale_ang', 'group', 'stiffness',
+          'spring_damping', 'limit_strength')
+  J = {k: [] for k in keys}
+  meta = []
+  for gi, (dof, v) in enumerate(groups):
+    if dof not in (1, 2, 3):
+      raise RuntimeError(f'invalid number of joint limits: {dof}')
+    jtype = {1: REVOLUTE, 2: UNIVERSAL, 3: SPHERICAL}[dof]
+    coeff = 0.5 if dof == 1 else 2.0
+    meta.append((dof, [j.name for j in v], None))
+    for j in v:
+      off_p, off_c, axis_p, axis_c = _joint_geometry(j)
+      J['type'].append(jtype)
+      J['dof'].append(dof)
+      J['free_dofs'].append(-1)
+      J['body_p'].append(index[j.parent])
+      J['body_c'].append(index[j.child])
+      J['off_p'].append(off_p)
+      J['off_c'].append(off_c)
+      J['axis_p'].append(axis_p)
+      J['axis_c'].append(axis_c)
+      lim = np.zeros((3, 2))
+      lim[:dof] = np.array([[i.min, i.max] for i in j.angle_limit]) / 180.0 * np.pi
+      J['limit'].append(lim)
+      J['damping'].append(j.angular_damping)
+      J['scale_pos'].append(0.)
+      J['scale_ang'].append(0.)
+      J['group'].append(gi)
+      J['stiffness'].append(j.stiffness)
+      J['spring_damping'].append(j.spring_damping if j.HasField('spring_damping')
+                                 else coeff * np.sqrt(np.float64(j.stiffness)))
+      J['limit_strength'].append(j.limit_strength if j.HasField('limit_strength')
+                                 else j.stiffness)
+  return _joint_arrays(J), meta
+
+
+def _joint_arrays(J):
+  d = {}
+  for k in ('type', 'dof', 'free_dofs', 'body_p', 'body_c', 'group'):
+    d['joint_' + k] = np.asarray(J[k], np.int32)
+  d['joint_off_p'] = np.asarray(J['off_p'], np.float64).reshape(-1, 3)
+  d['joint_off_c'] = np.asarray(J['off_c'], np.float64).reshape(-1, 3)
+  d['joint_axis_p'] = np.asarray(J['axis_p'], np.float64).reshape(-1, 3, 3)
+  d['joint_axis_c'] = np.asarray(J['axis_c'], np.float64).reshape(-1, 3, 3)
+  d['joint_limit'] = np.asarray(J['limit'], np.float64).reshape(-1, 3, 2)
+  for k in ('damping', 'scale_pos', 'scale_ang', 'stiffness', 'spring_damping',
+            'limit_strength'):
+    d['joint_' + k] = np.asarray(J.get(k, [0.] * len(J['type'])), np.float64)
+  return d
+
+
 def _joints(config, mass, inv_inertia, index):
   """Joint groups (`joints.py:418-474`). MUTATES config.joints (App. A.2)."""
-  if config.dynamics_mode != 'pbd':
-    raise NotImplementedError('legacy_spring dynamics are outside the MI355X '
-                              'path (SURVEY §2, spring_joints.py)')
+  if config.dynamics_mode == 'legacy_spring':
+    return _spring_joints(config, index)
   groups = {}
   dofs = {len(j.angle_limit) for j in config.joints}
   sphericalize = len(dofs) > 1
@@ -403,13 +478,11 @@ def _joints(config, mass, inv_inertia, index):
       J['free_dofs'].append(free[k] if free is not None else -1)
       J['body_p'].append(index[j.parent])
       J['body_c'].append(index[j.child])
-      J['off_p'].append(vec(j.parent_offset))
-      J['off_c'].append(vec(j.child_offset))
-      axis_c = np.array([rotate(e, euler_to_quat(vec(j.rotation)))
-                         for e in np.eye(3)])
-      ref = euler_to_quat(vec(j.reference_rotation))
+      off_p, off_c, axis_p, axis_c = _joint_geometry(j)
+      J['off_p'].append(off_p)
+      J['off_c'].append(off_c)
       J['axis_c'].append(axis_c)
-      J['axis_p'].append(np.array([rotate(a, ref) for a in axis_c]))
+      J['axis_p'].append(axis_p)
       lim = np.zeros((3, 2))
       lim[:dof] = np.array([[i.min, i.max] for i in j.angle_limit]) / 180.0 * np.pi
       J['limit'].append(lim)
@@ -417,17 +490,7 @@ def _joints(config, mass, inv_inertia, index):
       J['scale_pos'].append(scale_pos)
       J['scale_ang'].append(scale_ang)
       J['group'].append(gi)
-  d = {}
-  for k in ('type', 'dof', 'free_dofs', 'body_p', 'body_c', 'group'):
-    d['joint_' + k] = np.asarray(J[k], np.int32)
-  d['joint_off_p'] = np.asarray(J['off_p'], np.float64).reshape(-1, 3)
-  d['joint_off_c'] = np.asarray(J['off_c'], np.float64).reshape(-1, 3)
-  d['joint_axis_p'] = np.asarray(J['axis_p'], np.float64).reshape(-1, 3, 3)
-  d['joint_axis_c'] = np.asarray(J['axis_c'], np.float64).reshape(-1, 3, 3)
-  d['joint_limit'] = np.asarray(J['limit'], np.float64).reshape(-1, 3, 2)
-  for k in ('damping', 'scale_pos', 'scale_ang'):
-    d['joint_' + k] = np.asarray(J[k], np.float64)
-  return d, meta
+  return _joint_arrays(J), meta
 
 
 def _actuators(config, jmeta):
@@ -526,6 +589,8 @@ def compile_system(config):
   d['gravity'] = vec(config.gravity)
   d['velocity_damping'] = np.float64(config.velocity_damping)
   d['angular_damping'] = np.float64(config.angular_damping)
+  d['dynamics_mode'] = np.int32(DYN_LEGACY_SPRING if config.dynamics_mode == 'legacy_spring'
+                                else DYN_PBD)
   d.update(_colliders(config, index))
   jd, jmeta = _joints(config, mass, inv_inertia, index)
   d.update(jd)

@@ -69,13 +69,19 @@ struct Builder {
 int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   const int N = d->n_bodies, J = d->n_joints, K = d->n_actuators, R = d->n_rows, G = d->n_groups;
   if (N <= 0) return fail("descriptor has no bodies");
+  if (d->dynamics_mode != BX_DYN_PBD && d->dynamics_mode != BX_DYN_LEGACY_SPRING)
+    return fail("unknown dynamics mode");
   if (d->substeps <= 0) return fail("substeps must be positive");
   for (int j = 0; j < J; j++) {
     if (d->joint_body_p[j] < 0 || d->joint_body_p[j] >= N || d->joint_body_c[j] < 0 ||
         d->joint_body_c[j] >= N)
       return fail("joint body index out of range");
-    if (d->joint_type[j] != BX_JOINT_REVOLUTE && d->joint_type[j] != BX_JOINT_SPHERICAL)
+    if (d->joint_type[j] != BX_JOINT_REVOLUTE && d->joint_type[j] != BX_JOINT_SPHERICAL &&
+        !(d->joint_type[j] == BX_JOINT_UNIVERSAL && d->dynamics_mode == BX_DYN_LEGACY_SPRING))
       return fail("unsupported joint type");
+    if (d->dynamics_mode == BX_DYN_LEGACY_SPRING &&
+        (!d->joint_stiffness || !d->joint_spring_damping || !d->joint_limit_strength))
+      return fail("legacy_spring descriptor needs joint stiffness, spring damping and limit strength");
   }
   for (int a = 0; a < K; a++) {
     if (d->act_joint[a] < 0 || d->act_joint[a] >= J) return fail("actuator joint out of range");
@@ -128,6 +134,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // integrators.py:87,91 — exp(damping * dt) of Python doubles, one constant
   H.vexp = (float)std::exp(d->velocity_damping * d->h);
   H.aexp = (float)std::exp(d->angular_damping * d->h);
+  H.spring = d->dynamics_mode == BX_DYN_LEGACY_SPRING ? 1 : 0;
   H.gx = (float)d->gravity[0]; H.gy = (float)d->gravity[1]; H.gz = (float)d->gravity[2];
 
   H.o_body = B.alloc(N * BODY_STRIDE);
@@ -146,7 +153,9 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   for (int j = 0; j < J; j++) {
     int o = H.o_joint + j * JOINT_STRIDE;
     int type = d->joint_type[j];
-    int nang = d->joint_free_dofs[j] >= 0 ? d->joint_free_dofs[j] : (type == BX_JOINT_REVOLUTE ? 1 : 3);
+    // angle_vel dofs (joints.py:218-225): the free dofs of a sphericalised
+    // group, else every dof of the joint (1 / 2 / 3)
+    int nang = d->joint_free_dofs[j] >= 0 ? d->joint_free_dofs[j] : d->joint_dof[j];
     B.i(o + J_TYPE, type);
     B.i(o + J_BP, d->joint_body_p[j]);
     B.i(o + J_BC, d->joint_body_c[j]);
@@ -167,6 +176,11 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       B.f(o + J_AXC + k, d->joint_axis_c[9 * j + k]);
     }
     for (int k = 0; k < 6; k++) B.f(o + J_LIM + k, d->joint_limit[6 * j + k]);
+    if (d->dynamics_mode == BX_DYN_LEGACY_SPRING) {
+      B.f(o + J_STIFF, d->joint_stiffness[j]);
+      B.f(o + J_SDAMP, d->joint_spring_damping[j]);
+      B.f(o + J_LSTR, d->joint_limit_strength[j]);
+    }
   }
   H.D = D;
   H.o_act = B.alloc(K * ACT_STRIDE);
@@ -355,8 +369,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         if (std::find(gs.begin(), gs.end(), v >> 24) == gs.end()) gs.push_back(v >> 24);
       max_groups = std::max(max_groups, (int)gs.size());
     }
+    // the register-hoisted kernel is the pbd step only; legacy_spring systems
+    // run the item-loop kernel
     H.single = (N <= L && J <= L && K <= L && R <= L && mx <= 8 && max_groups <= 2 &&
-                H.n_nn == 0) ? 1 : 0;
+                H.n_nn == 0 && !H.spring) ? 1 : 0;
     H.act_same = 1;
     for (int a = 0; a < K; a++)
       if (d->act_joint[a] != a) H.act_same = 0;

@@ -297,7 +297,64 @@ __device__ __forceinline__ int axis_angle(const JointC& J, const QP& p, const QP
   float phi = signed_angle(-a3c, a2c, lon);
   axes[0] = a1p; axes[1] = a2c; axes[2] = a3c;
   ang[0] = psi; ang[1] = theta; ang[2] = phi;
-  return 3;
+  // spring Universal.axis_angle (spring_joints.py:188-216): (psi, theta)
+  return J.type == BX_JOINT_UNIVERSAL ? 2 : 3;
+}
+
+// ---------------------------------------------------------------------------
+// legacy_spring joints (brax/physics/spring_joints.py)
+// ---------------------------------------------------------------------------
+struct SpringC {
+  float stiff, sdamp, lstr;
+};
+__device__ __forceinline__ SpringC load_spring(const Cst& c, const BlobHdr& H, int j) {
+  int o = H.o_joint + j * JOINT_STRIDE;
+  return SpringC{c.f(o + J_STIFF), c.f(o + J_SDAMP), c.f(o + J_LSTR)};
+}
+
+// Revolute/Universal/Spherical.apply_reduced (spring_joints.py:122-155,
+// 170-204, 262-287): the offset spring-damper impulse through Body.impulse
+// (bodies.py:46-59), then the alignment / limit torques and the joint's
+// angular damping. Outputs dP of parent and child (vel, ang).
+__device__ __forceinline__ void spring_joint_apply(const JointC& J, const SpringC& S, const QP& p,
+                                                   const QP& c, v3& dvp, v3& dap, v3& dvc,
+                                                   v3& dac) {
+  // QP.to_world (base.py:110-124)
+  v3 op = rotate(J.off_p, p.rot), oc = rotate(J.off_c, c.rot);
+  v3 pos_p = p.pos + op, vel_p = p.vel + cross(p.ang, op);
+  v3 pos_c = c.pos + oc, vel_c = c.vel + cross(c.ang, oc);
+  v3 imp = (pos_p - pos_c) * S.stiff + S.sdamp * (vel_p - vel_c);
+  v3 nimp = -imp;
+  dvp = nimp / J.mp;
+  dap = mul(J.Ip, cross(pos_p - p.pos, nimp));
+  dvc = imp / J.mc;
+  dac = mul(J.Ic, cross(pos_c - c.pos, imp));
+  v3 axes[3];
+  float ang[3];
+  const int dof = axis_angle<F_ALL>(J, p, c, axes, ang);
+  float dang[3];
+#pragma unroll
+  for (int l = 0; l < 3; l++) {
+    const float lo = J.lim[2 * l], hi = J.lim[2 * l + 1];
+    float d = ang[l] < lo ? lo - ang[l] : 0.f;
+    dang[l] = ang[l] > hi ? hi - ang[l] : d;
+  }
+  v3 tq;
+  if (J.type == BX_JOINT_REVOLUTE) {
+    v3 axis_c = rotate(J.axc[0], c.rot);
+    tq = S.stiff * cross(axes[0], axis_c);
+    tq = tq - (S.lstr * axes[0]) * dang[0];
+  } else if (dof == 2) {
+    v3 proj = axes[1] - dot(axes[1], axes[0]) * axes[0];
+    proj = proj / safe_norm(proj);
+    tq = (S.lstr / 5.f) * cross(proj, axes[1]);
+    tq = tq - S.lstr * (axes[0] * dang[0] + axes[1] * dang[1]);
+  } else {
+    tq = -S.lstr * ((axes[0] * dang[0] + axes[1] * dang[1]) + axes[2] * dang[2]);
+  }
+  tq = tq - J.damping * (p.ang - c.ang);
+  dap = dap + mul(J.Ip, tq);
+  dac = dac + mul(-J.Ic, tq);
 }
 
 // ---------------------------------------------------------------------------
@@ -1020,6 +1077,157 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
   }
 }
 
+// Collider.apply over the step's active rows (colliders.py:116-153): impulse
+// contacts into the row slots (vel 0..2, ang 3..5, any() flag 7) and the row
+// data (contact pos, normal, penetration) for Info
+template <int L>
+__device__ void impulse_rows(const Cst& c, const BlobHdr& H, const Env& E, int lane) {
+  for (int i = lane; i < (H.n_nn ? H.info_rows : H.R); i += L) {
+    const int r = H.n_nn ? E.alist[i] : i;
+    RowC R = load_row(c, H, r);
+    QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+    v3 cpos, cvel, n;
+    float pen;
+    contact_gen<F_ALL>(R, a, b, cpos, cvel, n, pen);
+    v3 oav, oaa, obv, oba;
+    impulse_contact<F_ALL>(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
+    float* rd = E.rowd + r * ROWD_STRIDE;
+    st3(rd, cpos); st3(rd + 3, n); rd[6] = pen;
+    float* sa = E.cslot + r * SLOT_STRIDE;
+    float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
+    st3(sa, oav); st3(sa + 3, oaa);
+    sa[7] = (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f;
+    st3(sb, obv); st3(sb + 3, oba);
+    sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
+  }
+}
+
+// per-body (vel, ang) update of the rows' slots: each collider group summed
+// and divided by (eps + #non-zero rows), groups added in order
+__device__ __forceinline__ void contact_reduce(const Cst& c, const BlobHdr& H, const Env& E, int b,
+                                               float eps, v3& dv, v3& da) {
+  dv = mk(0.f, 0.f, 0.f);
+  da = mk(0.f, 0.f, 0.f);
+  int i = c.i(H.o_cl_off + b), e = c.i(H.o_cl_off + b + 1);
+  while (i < e) {
+    int g = c.i(H.o_cl + i) >> 24;
+    v3 gv = mk(0.f, 0.f, 0.f), ga = mk(0.f, 0.f, 0.f);
+    float cnt = 0.f;
+    for (; i < e && (c.i(H.o_cl + i) >> 24) == g; i++) {
+      const float* s = E.cslot + (c.i(H.o_cl + i) & 0xFFFFFF) * SLOT_STRIDE;
+      gv = gv + ld3(s);
+      ga = ga + ld3(s + 3);
+      cnt += s[7];
+    }
+    float d = eps + cnt;
+    dv = dv + gv / d;
+    da = da + ga / d;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// System._spring_step (system.py:342-375), all L lanes of the env: per
+// substep Euler.kinetic, spring joints + actuators + forces at the
+// acceleration level, then Collider.apply at the velocity level. Info:
+// contact += dp_c, joint += dp_j (in E.rb words 0..5), actuator += dp_a.
+// ---------------------------------------------------------------------------
+template <int L>
+__device__ void spring_step(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
+                            const float* act, int aw) {
+  const int N = H.N, J = H.J, K = H.K;
+  const float h = H.h;
+  for (int b = lane; b < N; b += L) {
+    float* acc = E.acc + b * ACC_STRIDE;
+    for (int k = 0; k < 9; k++) acc[k] = 0.f;
+    float* ij = E.rb + b * RB_STRIDE;
+    for (int k = 0; k < 6; k++) ij[k] = 0.f;
+  }
+  if (H.n_nn) nn_select<L>(c, H, E, lane);
+  for (int sub = 0; sub < H.substeps; sub++) {
+    // Euler.kinetic (integrators.py:50-68)
+    for (int b = lane; b < N; b += L) {
+      BodyC B = load_body(c, H, b);
+      QP q = ldqp(E.qp + b * QP_STRIDE);
+      q.pos = q.pos + mul(q.vel * h, B.pm);
+      v3 am = mul(q.ang, B.rm);
+      q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
+      q4 r = q.rot + quat_mul(hq, q.rot);
+      float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
+      q.rot = q4{r.w / rn, r.x / rn, r.y / rn, r.z / rn};
+      stqp(E.qp + b * QP_STRIDE, q);
+    }
+    sync();
+    // spring Joint.apply (spring_joints.py:89-113) -> joint slots (vel, ang)
+    for (int j = lane; j < J; j += L) {
+      JointC Jc = load_joint(c, H, j);
+      SpringC S = load_spring(c, H, j);
+      QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), q = ldqp(E.qp + Jc.bc * QP_STRIDE);
+      v3 dvp, dap, dvc, dac;
+      spring_joint_apply(Jc, S, p, q, dvp, dap, dvc, dac);
+      float* sp = E.jslot + j * SLOT_STRIDE;
+      float* sc = E.jslot + (E.nJ + j) * SLOT_STRIDE;
+      st3(sp, dvp); st3(sp + 3, dap);
+      st3(sc, dvc); st3(sc + 3, dac);
+    }
+    // actuators (actuators.py:52-112) -> actuator slots
+    for (int a = lane; a < K; a += L) {
+      ActC A = load_act(c, H, a);
+      JointC Jc = load_joint(c, H, A.joint);
+      float al[3];
+#pragma unroll
+      for (int l = 0; l < 3; l++) {
+        int ai = A.idx[l];
+        al[l] = valid ? act[take_idx(ai, aw)] * (ai >= 0 ? 1.f : 0.f) : 0.f;
+      }
+      act_torque<F_ALL>(Jc, A, E, al, a);
+    }
+    sync();
+    // Euler.update(acc_p = dp_j + dp_a + dp_f) (integrators.py:85-93, system.py:353-357)
+    for (int b = lane; b < N; b += L) {
+      BodyC B = load_body(c, H, b);
+      v3 jv = mk(0.f, 0.f, 0.f), ja = mk(0.f, 0.f, 0.f), dpa = mk(0.f, 0.f, 0.f);
+      for (int i = c.i(H.o_jl_off + b), e = c.i(H.o_jl_off + b + 1); i < e; i++) {
+        const float* s = E.jslot + c.i(H.o_jl + i) * SLOT_STRIDE;
+        jv = jv + ld3(s);
+        ja = ja + ld3(s + 3);
+      }
+      for (int i = c.i(H.o_al_off + b), e = c.i(H.o_al_off + b + 1); i < e; i++)
+        dpa = dpa + ld3(E.aslot + c.i(H.o_al + i) * ASLOT_STRIDE);
+      v3 fv, fa;
+      body_forces(c, H, b, act, aw, valid, fv, fa);
+      QP q = ldqp(E.qp + b * QP_STRIDE);
+      v3 vel = H.vexp * q.vel;
+      vel = vel + ((jv + fv) + mk(H.gx, H.gy, H.gz)) * h;
+      q.vel = mul(vel, B.pm);
+      v3 ang = H.aexp * q.ang;
+      ang = ang + ((ja + dpa) + fa) * h;
+      q.ang = mul(ang, B.rm);
+      stqp(E.qp + b * QP_STRIDE, q);
+      float* ij = E.rb + b * RB_STRIDE;
+      st3(ij, ld3(ij) + jv);
+      st3(ij + 3, ld3(ij + 3) + ja);
+      float* acc = E.acc + b * ACC_STRIDE;
+      st3(acc + ACC_IAA, ld3(acc + ACC_IAA) + dpa);
+    }
+    sync();
+    // Collider.apply (colliders.py:116-153), then Euler.update(vel_p = dp_c)
+    impulse_rows<L>(c, H, E, lane);
+    sync();
+    for (int b = lane; b < N; b += L) {
+      BodyC B = load_body(c, H, b);
+      v3 dv, da;
+      contact_reduce(c, H, E, b, 1e-8f, dv, da);
+      float* s = E.qp + b * QP_STRIDE;
+      st3(s + 7, mul(ld3(s + 7) + dv, B.pm));
+      st3(s + 10, mul(ld3(s + 10) + da, B.rm));
+      float* acc = E.acc + b * ACC_STRIDE;
+      st3(acc + ACC_ICV, ld3(acc + ACC_ICV) + dv);
+      st3(acc + ACC_ICA, ld3(acc + ACC_ICA) + da);
+    }
+    sync();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // SINGLE mode: every lane owns at most one body, joint, actuator and contact
 // row of its env (N, J, K, R <= L) and every per-body gather list fits MAXG.
@@ -1619,6 +1827,8 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
     pbd_step_single<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr,
                              (int)A.act_width, X, icv, ica,
                        iaa);
+  } else if (H.spring) {
+    spring_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, (int)A.act_width);
   } else {
     pbd_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, (int)A.act_width);
   }
@@ -1642,6 +1852,16 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
     if (I.actuator_ang.ptr) {
       float* p = I.actuator_ang.ptr + e * I.actuator_ang.env_stride + b * I.actuator_ang.body_stride;
       p[0] = acc[ACC_IAA]; p[1] = acc[ACC_IAA + 1]; p[2] = acc[ACC_IAA + 2];
+    }
+    // Info.joint: the spring step's accumulated dp_j; zero_info under pbd
+    const float* ij = E.rb + b * RB_STRIDE;
+    if (I.joint_vel.ptr) {
+      float* p = I.joint_vel.ptr + e * I.joint_vel.env_stride + b * I.joint_vel.body_stride;
+      for (int k = 0; k < 3; k++) p[k] = H.spring ? ij[k] : 0.f;
+    }
+    if (I.joint_ang.ptr) {
+      float* p = I.joint_ang.ptr + e * I.joint_ang.env_stride + b * I.joint_ang.body_stride;
+      for (int k = 0; k < 3; k++) p[k] = H.spring ? ij[3 + k] : 0.f;
     }
   }
   for (int r = lane; r < H.R; r += L) {
@@ -1711,6 +1931,8 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
     if constexpr (S) {
       v3 icv, ica, iaa;
       pbd_step_single<L, F, M>(c, H, E, lane, valid, act, aw, X, icv, ica, iaa);
+    } else if (H.spring) {
+      spring_step<L>(c, H, E, lane, valid, act, aw);
     } else {
       pbd_step<L>(c, H, E, lane, valid, act, aw);
     }
@@ -1913,10 +2135,10 @@ __global__ void __launch_bounds__(64) default_qp_kernel(ResetArgs A) {
   }
   // bodies.min_z per root group, then lift (system.py:213-240)
   for (int g = 0; g < H.n_root_groups; g++) {
-    float zmin = __builtin_inff();
+    float zmin = 3.4028235e38f;  // finite-math build: no inf literals
     for (int b = 0; b < N; b++) {
       if (c.i(H.o_rgroup + b) != g) continue;
-      float bz = __builtin_inff();
+      float bz = 3.4028235e38f;
       for (int p = c.i(H.o_zoff + b), pe = c.i(H.o_zoff + b + 1); p < pe; p++) {
         int o = H.o_zpt + p * 4;
         v3 w = rotate(c.f3(o), ld4(q + b * 13 + 3));

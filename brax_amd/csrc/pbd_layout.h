@@ -20,6 +20,8 @@ enum {
   JOINT_STRIDE = 48,
   J_TYPE = 0, J_BP = 1, J_BC = 2, J_FREE = 3, J_DOF = 4, J_ANGLE_OFF = 5, J_NANGLES = 6,
   J_DAMP = 7, J_SP = 8, J_SA = 9, J_OFFP = 10, J_OFFC = 13, J_AXP = 16, J_AXC = 25, J_LIM = 34,
+  // legacy_spring joints (spring_joints.py:57-67)
+  J_STIFF = 40, J_SDAMP = 41, J_LSTR = 42,
 };
 enum { ACT_STRIDE = 8, A_TYPE = 0, A_JOINT = 1, A_IDX = 2, A_STR = 5 };
 // collider groups: NearNeighbors cutoff (0 = Pairs), row range, Info base
@@ -74,6 +76,7 @@ struct BlobHdr {
   int32_t o_group, n_nn, info_rows;  // collider groups, culled groups, Info rows
   int32_t l_ract;                    // LDS: per-row NearNeighbors rank (-1 = culled)
   int32_t l_alist;                   // LDS: active rows in Info order (info_rows)
+  int32_t spring;                    // dynamics_mode == legacy_spring
 };
 
 }  // namespace bx

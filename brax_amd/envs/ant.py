@@ -7,6 +7,7 @@ use_contact_forces (the registered 'ant'), else 27 (`ant.py:257-282`).
 import numpy as np
 
 from brax_amd.envs import configs
+from brax_amd.envs import robots
 from brax_amd.envs.env import PhysicsEnv
 
 
@@ -23,11 +24,10 @@ class Ant(PhysicsEnv):
                healthy_reward=1.0, terminate_when_unhealthy=True, healthy_z_range=(0.2, 1.0),
                reset_noise_scale=0.1, exclude_current_positions_from_observation=True,
                legacy_spring=False, **kwargs):
-    if legacy_spring:
-      raise NotImplementedError('legacy_spring dynamics are outside the MI355X path')
     if not exclude_current_positions_from_observation:
       raise NotImplementedError('exclude_current_positions_from_observation=False')
-    super().__init__(configs.ANT_CONFIG, **kwargs)
+    # `ant.py:183-184`: legacy_spring selects _SYSTEM_CONFIG_SPRING
+    super().__init__(robots.ANT_SPRING_CONFIG if legacy_spring else configs.ANT_CONFIG, **kwargs)
     self.reset_noise_scale = reset_noise_scale
     self._use_contact_forces = use_contact_forces
     self.coef = np.array([1.0, ctrl_cost_weight, contact_cost_weight, healthy_reward,

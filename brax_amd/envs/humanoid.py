@@ -8,6 +8,7 @@ qfrc uses an UNMASKED take of the padded act_index (-1 reads action[0],
 import numpy as np
 
 from brax_amd.envs import configs
+from brax_amd.envs import robots
 from brax_amd.envs.env import PhysicsEnv
 
 
@@ -22,9 +23,12 @@ class Humanoid(PhysicsEnv):
                terminate_when_unhealthy=True, healthy_z_range=(0.8, 2.1),
                reset_noise_scale=1e-2, exclude_current_positions_from_observation=True,
                legacy_spring=False, **kwargs):
-    if legacy_spring or not exclude_current_positions_from_observation:
-      raise NotImplementedError('only the default Humanoid configuration is supported')
-    super().__init__(configs.HUMANOID_CONFIG, **kwargs)
+    if not exclude_current_positions_from_observation:
+      raise NotImplementedError('exclude_current_positions_from_observation=False')
+    # `humanoid.py:209`: legacy_spring selects _SYSTEM_CONFIG_SPRING (three
+    # joint groups, no sphericalisation: qfrc is 17 wide there)
+    super().__init__(robots.HUMANOID_SPRING_CONFIG if legacy_spring else configs.HUMANOID_CONFIG,
+                     **kwargs)
     self.reset_noise_scale = reset_noise_scale
     self.coef = np.array([forward_reward_weight, ctrl_cost_weight, 0, healthy_reward,
                           healthy_z_range[0], healthy_z_range[1],

@@ -18,9 +18,9 @@ class HumanoidStandup(PhysicsEnv):
   metric_keys = ('reward_linup', 'reward_quadctrl')
 
   def __init__(self, legacy_spring=False, **kwargs):
-    if legacy_spring:
-      raise NotImplementedError('legacy_spring dynamics are outside the MI355X path')
-    super().__init__(robots.HUMANOID_STANDUP_CONFIG, **kwargs)
+    # `humanoid_standup.py:213`: legacy_spring selects _SYSTEM_CONFIG_SPRING
+    super().__init__(robots.HUMANOID_STANDUP_SPRING_CONFIG if legacy_spring
+                     else robots.HUMANOID_STANDUP_CONFIG, **kwargs)
     self.reset_noise_scale = 0.01
     self.coef = np.array([0, 0.01, 0, 0, 0, 0, 0, 0], np.float32)
     D = self.sys.num_joint_dof

@@ -41,14 +41,15 @@ class TorchEnv(Env):
   (B,) axis."""
 
   config = None          # robot description text
+  spring_config = None   # its legacy_spring variant (`_SYSTEM_CONFIG_SPRING`)
   qpos_noise = (0., 0.)  # reset joint-angle noise range
   qvel_noise = (0., 0.)  # reset joint-velocity noise range
   metric_keys = ()
 
   def __init__(self, batch_size=None, device=None, legacy_spring=False, **kwargs):
-    if legacy_spring:
-      raise NotImplementedError('legacy_spring dynamics are outside the MI355X path')
-    super().__init__(self.config, device=device)
+    if legacy_spring and self.spring_config is None:
+      raise NotImplementedError(f'{type(self).__name__} has no legacy_spring configuration')
+    super().__init__(self.spring_config if legacy_spring else self.config, device=device)
     self.batch_size = batch_size
     self.dev = self.sys.device
 
@@ -172,11 +173,13 @@ class _Locomotion2D(TorchEnv):
 class Hopper(_Locomotion2D):
   """`brax/envs/hopper.py`."""
   config = robots.HOPPER_CONFIG
+  spring_config = robots.HOPPER_SPRING_CONFIG
 
 
 class Walker2d(_Locomotion2D):
   """`brax/envs/walker2d.py` (its own healthy ranges, walker2d.py:132-141)."""
   config = robots.WALKER2D_CONFIG
+  spring_config = robots.WALKER2D_SPRING_CONFIG
 
   def __init__(self, healthy_z_range=(0.7, 2.0), healthy_angle_range=(-1.0, 1.0), **kwargs):
     super().__init__(healthy_z_range=healthy_z_range, healthy_angle_range=healthy_angle_range,
@@ -187,6 +190,7 @@ class InvertedPendulum(TorchEnv):
   """`brax/envs/inverted_pendulum.py:124-166`; action_size 1 (the thruster's
   three indices clip to action[0])."""
   config = robots.INVERTED_PENDULUM_CONFIG
+  spring_config = robots.INVERTED_PENDULUM_SPRING_CONFIG
   qpos_noise = qvel_noise = (-0.01, 0.01)
   obs_size = 4
 
@@ -208,6 +212,7 @@ class InvertedPendulum(TorchEnv):
 class InvertedDoublePendulum(TorchEnv):
   """`brax/envs/inverted_double_pendulum.py:131-186`."""
   config = robots.INVERTED_DOUBLE_PENDULUM_CONFIG
+  spring_config = robots.INVERTED_DOUBLE_PENDULUM_SPRING_CONFIG
   qpos_noise = qvel_noise = (-0.01, 0.01)
   obs_size = 8
 
@@ -236,6 +241,7 @@ class Swimmer(TorchEnv):
   """`brax/envs/swimmer.py:153-290`: viscous drag fed to the three Thrusters
   through the action tail."""
   config = robots.SWIMMER_CONFIG
+  spring_config = robots.SWIMMER_SPRING_CONFIG
   metric_keys = ('reward_fwd', 'reward_ctrl', 'x_position', 'y_position',
                  'distance_from_origin', 'x_velocity', 'y_velocity', 'forward_reward')
 
@@ -308,6 +314,7 @@ class Swimmer(TorchEnv):
 class Reacher(TorchEnv):
   """`brax/envs/reacher.py:150-236`."""
   config = robots.REACHER_CONFIG
+  spring_config = robots.REACHER_SPRING_CONFIG
   qpos_noise = (-.1, .1)
   qvel_noise = (-.005, .005)
   metric_keys = ('reward_dist', 'reward_ctrl')
@@ -357,6 +364,7 @@ class ReacherAngle(Reacher):
   """`brax/envs/reacherangle.py:30-106`: [-1, 1] actions mapped onto the
   joints' angle limits for the Angle actuators."""
   config = robots.REACHERANGLE_CONFIG
+  spring_config = robots.REACHERANGLE_SPRING_CONFIG
   metric_keys = ('rewardDist', 'rewardCtrl')
   target_sqrt = True
 
@@ -380,6 +388,7 @@ class ReacherAngle(Reacher):
 class Acrobot(TorchEnv):
   """`brax/envs/acrobot.py:40-95`."""
   config = robots.ACROBOT_CONFIG
+  spring_config = robots.ACROBOT_SPRING_CONFIG
   qpos_noise = qvel_noise = (-.01, .01)
   metric_keys = ('dist_penalty', 'vel_penalty', 'alive_bonus', 'r_tot')
   obs_size = 4
@@ -506,6 +515,7 @@ class _TargetEnv(TorchEnv):
 class Ur5e(_TargetEnv):
   """`brax/envs/ur5e.py:30-130`."""
   config = robots.UR5E_CONFIG
+  spring_config = robots.UR5E_SPRING_CONFIG
   metric_keys = ('hits', 'weightedHits', 'movingToTarget')
 
   def __init__(self, **kwargs):
@@ -562,6 +572,7 @@ class Fetch(Ur5e):
   lower legs) runs to a target; Ur5e's egocentric observation around the
   Torso."""
   config = robots.FETCH_CONFIG
+  spring_config = robots.FETCH_SPRING_CONFIG
   metric_keys = ('hits', 'weightedHits', 'movingToTarget', 'torsoIsUp', 'torsoHeight')
 
   def __init__(self, **kwargs):  # pylint: disable=super-init-not-called
@@ -610,6 +621,7 @@ class Grasp(_TargetEnv):
   """`brax/envs/grasp.py:29-190`: Angle actuators driven through [-1, 1]
   actions, plus 3 actions that translate the palm before the physics step."""
   config = robots.GRASP_CONFIG
+  spring_config = robots.GRASP_SPRING_CONFIG
   metric_keys = ('hits', 'touchingObject', 'movingToObject', 'movingObjectToTarget',
                  'closeToObject')
 

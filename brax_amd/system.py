@@ -214,7 +214,8 @@ class System:
     lead = (B,) if batched else ()
     out = self._new_qp(lead)
     N, R = self.num_bodies, self.num_contacts
-    cbuf = torch.empty(lead + (N, 12), dtype=torch.float32, device=self.device)
+    spring = int(self.desc.get('dynamics_mode', 0)) == abi.DYN_LEGACY_SPRING
+    cbuf = torch.empty(lead + (N, 18 if spring else 12), dtype=torch.float32, device=self.device)
     cvel, cang = cbuf[..., 0:3], cbuf[..., 3:6]
     aang = cbuf[..., 9:12]
     avel = cbuf[..., 6:9]
@@ -226,6 +227,9 @@ class System:
     info.contact_ang = _field(cang, batched)
     info.actuator_vel = _field(avel, batched)
     info.actuator_ang = _field(aang, batched)
+    if spring:  # Info.joint: accumulated spring dp_j (zero_info under pbd)
+      info.joint_vel = _field(cbuf[..., 12:15], batched)
+      info.joint_ang = _field(cbuf[..., 15:18], batched)
     if R:
       info.contact_pos = cpos.data_ptr()
       info.contact_normal = cnorm.data_ptr()
@@ -236,7 +240,8 @@ class System:
         self._h, B, C.byref(qi), C.c_void_p(act.data_ptr()), act.stride(0), act.shape[1],
         C.byref(qo), C.byref(info), _stream()))
     zero = torch.zeros_like(cvel)
-    return out, Info(contact=P(cvel, cang), joint=P(zero, zero), actuator=P(avel, aang),
+    joint = P(cbuf[..., 12:15], cbuf[..., 15:18]) if spring else P(zero, zero)
+    return out, Info(contact=P(cvel, cang), joint=joint, actuator=P(avel, aang),
                      contact_pos=cpos, contact_normal=cnorm, contact_penetration=cpen)
 
   def joint_angle_vel(self, qp: QP):
@@ -255,7 +260,8 @@ class System:
     return (buf[0], buf[1]) if batched else (buf[0, 0], buf[1, 0])
 
   def info(self, qp: QP):
-    """`System.info` in pbd mode (system.py:327-340): the contact part."""
+    """`System.info` (system.py:249-252, 327-340, 377-390): the contact part
+    (Collider.apply, the same impulse model in both dynamics modes)."""
     batched = qp.pos.dim() == 3
     B = qp.pos.shape[0] if batched else 1
     lead = (B,) if batched else ()

@@ -34,10 +34,12 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 2
+#define BX_ABI_VERSION 3
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
-enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_SPHERICAL = 3 };
+enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
+/* dynamics modes (config.proto dynamics_mode; system.py:244-247) */
+enum { BX_DYN_PBD = 0, BX_DYN_LEGACY_SPRING = 1 };
 enum { BX_ACT_TORQUE = 0, BX_ACT_ANGLE = 1 };
 enum { BX_COL_CAPSULE_PLANE = 0, BX_COL_CAPSULE_CAPSULE = 1 };
 enum { BX_FORCE_THRUSTER = 0, BX_FORCE_TWISTER = 1 };
@@ -116,6 +118,15 @@ typedef struct bx_desc {
    * first (top_k order). */
   const int32_t* col_cutoff;       /* [G] */
   const int32_t* row_flat;         /* [R] */
+  /* legacy_spring dynamics (system.py:342-390, spring_joints.py): joints are
+   * springy Revolute / Universal / Spherical groups by dof (no
+   * sphericalisation), constrained at the acceleration level; contacts use
+   * the impulse model with Baumgarte stabilisation every substep. The three
+   * arrays may be NULL for pbd systems. */
+  int32_t dynamics_mode;           /* BX_DYN_* */
+  const double* joint_stiffness;       /* [J] */
+  const double* joint_spring_damping;  /* [J] (default: 0.5 or 2 x sqrt(stiffness)) */
+  const double* joint_limit_strength;  /* [J] (default: stiffness) */
 } bx_desc;
 
 /*
@@ -162,6 +173,8 @@ typedef struct bx_info {
   float* contact_pos;                   /* (B,R,3) contiguous */
   float* contact_normal;                /* (B,R,3) */
   float* contact_penetration;           /* (B,R)   */
+  bx_field joint_vel, joint_ang;        /* (B,N,3) accumulated joint P
+                                           (legacy_spring; zero under pbd) */
 } bx_info;
 
 /* Env-layer state of one batch (ant.py:198-255, wrappers.py:83-148).

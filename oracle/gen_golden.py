@@ -69,16 +69,29 @@ def dump_desc(sys_):
   d['velocity_damping'] = np.float64(integ.velocity_damping)
   d['angular_damping'] = np.float64(integ.angular_damping)
 
+  from brax.physics import spring_joints as sj
   jt, jd, jfree, jbp, jbc, joffp, joffc, jaxp, jaxc, jlim, jdamp = ([] for _ in range(11))
   jsp, jsa, jgrp = [], [], []
+  jstiff, jsdamp, jlstr = [], [], []
   joint_base = []
+  kinds = {rj.Revolute: 1, rj.Spherical: 3, sj.Revolute: 1, sj.Universal: 2, sj.Spherical: 3}
+  spring = cfg.dynamics_mode == 'legacy_spring'
+  d['dynamics_mode'] = np.int32(1 if spring else 0)
   for g, j in enumerate(sys_.joints):
-    if not isinstance(j, (rj.Revolute, rj.Spherical)):
+    if type(j) not in kinds:
       raise RuntimeError('unsupported joint type %r' % type(j))
     n = len(j.body_p.idx)
     joint_base.append(len(jt))
     for k in range(n):
-      jt.append(1 if isinstance(j, rj.Revolute) else 3)
+      jt.append(kinds[type(j)])
+      if spring:
+        jstiff.append(j.stiffness[k])
+        jsdamp.append(j.spring_damping[k])
+        jlstr.append(j.limit_strength[k])
+      else:
+        jstiff.append(0.)
+        jsdamp.append(0.)
+        jlstr.append(0.)
       jd.append(j.dof)
       jfree.append(j.free_dofs[k] if j.free_dofs is not None else -1)
       jbp.append(j.body_p.idx[k])
@@ -91,8 +104,8 @@ def dump_desc(sys_):
       lim[:j.dof] = j.limit[k]
       jlim.append(lim)
       jdamp.append(j.angular_damping[k])
-      jsp.append(j.scale_pos[k])
-      jsa.append(j.scale_ang[k])
+      jsp.append(j.scale_pos[k] if not spring else 0.)
+      jsa.append(j.scale_ang[k] if not spring else 0.)
       jgrp.append(g)
   d['joint_type'] = np.asarray(jt, np.int32)
   d['joint_dof'] = np.asarray(jd, np.int32)
@@ -108,6 +121,9 @@ def dump_desc(sys_):
   d['joint_scale_pos'] = np.asarray(jsp, np.float64)
   d['joint_scale_ang'] = np.asarray(jsa, np.float64)
   d['joint_group'] = np.asarray(jgrp, np.int32)
+  d['joint_stiffness'] = np.asarray(jstiff, np.float64)
+  d['joint_spring_damping'] = np.asarray(jsdamp, np.float64)
+  d['joint_limit_strength'] = np.asarray(jlstr, np.float64)
 
   at, aj, astr, aidx, agrp = [], [], [], [], []
   for g, a in enumerate(sys_.actuators):
@@ -451,6 +467,23 @@ ROBOTS = {
 }
 
 
+# legacy_spring variants (`_SYSTEM_CONFIG_SPRING`, system.py:342-390): physics
+# rollouts of the registered envs' spring systems, from default_qp
+SPRING_ROBOTS = {
+    'inverted_pendulum': (8, 4, 1),
+    'inverted_double_pendulum': (8, 4, 1),
+    'swimmer': (8, 4, 0),
+    'hopper': (8, 4, 0),
+    'walker2d': (8, 4, 0),
+    'reacher': (8, 4, 0),
+    'reacherangle': (8, 4, 0),
+    'acrobot': (8, 4, 0),
+    'ur5e': (4, 3, 0),
+    'grasp': (4, 3, 0),
+    'fetch': (4, 3, 0),
+}
+
+
 TORCH_ENVS = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum',
               'swimmer', 'reacher', 'reacherangle', 'acrobot', 'pusher', 'ur5e', 'grasp', 'fetch']
 
@@ -487,6 +520,32 @@ def main():
     env = envs.get_environment('humanoidstandup')
     save('desc_humanoidstandup', dump_desc(env.sys))
     save('traj_humanoidstandup', env_traj(env, 'humanoidstandup', 16, 4))
+  # legacy_spring envs with the kernel env layer (Env(legacy_spring=True))
+  if want('ant_spring'):
+    env = ant_mod.Ant(use_contact_forces=True, legacy_spring=True)
+    save('desc_ant_spring', dump_desc(env.sys))
+    save('traj_ant_spring', env_traj(env, 'ant_spring', 16, 4))
+  if want('humanoid_spring'):
+    env = importlib.import_module('brax.envs.humanoid').Humanoid(legacy_spring=True)
+    save('desc_humanoid_spring', dump_desc(env.sys))
+    save('traj_humanoid_spring', env_traj(env, 'humanoid_spring', 8, 3))
+  if want('halfcheetah_spring'):
+    env = envs.get_environment('halfcheetah', legacy_spring=True)
+    save('desc_halfcheetah_spring', dump_desc(env.sys))
+    save('traj_halfcheetah_spring', env_traj(env, 'halfcheetah_spring', 8, 3))
+  if want('humanoidstandup_spring'):
+    env = envs.get_environment('humanoidstandup', legacy_spring=True)
+    save('desc_humanoidstandup_spring', dump_desc(env.sys))
+    save('traj_humanoidstandup_spring', env_traj(env, 'humanoidstandup_spring', 8, 3))
+  for mod, (B, T, aw) in SPRING_ROBOTS.items():
+    if want(mod + '_spring'):
+      m = importlib.import_module('brax.envs.' + mod)
+      from google.protobuf import text_format
+      import brax
+      s = brax.System(text_format.Parse(m._SYSTEM_CONFIG_SPRING, brax.Config()))  # pylint: disable=protected-access
+      save(f'desc_{mod}_spring', dump_desc(s))
+      A = aw or (s.num_joint_dof + s.num_forces_dof)
+      save(f'traj_{mod}_spring', sys_traj(s, mod + '_spring', s.default_qp(), B, T, 1.0, A))
   if want('halfcheetah'):
     env = envs.get_environment('halfcheetah')
     save('desc_halfcheetah', dump_desc(env.sys))

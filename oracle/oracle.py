@@ -90,10 +90,11 @@ class Oracle:
     cp = np.empty((B, self.IR, 3), self.dtype)
     cn = np.empty((B, self.IR, 3), self.dtype)
     pen = np.empty((B, self.IR), self.dtype)
+    ij = np.empty((B, self.N, 6), self.dtype)
     self._fn('oracle_system_step')(C.byref(self.cdesc), C.c_int64(B), _p(qp), _p(act),
-                                   _p(out), _p(ic), _p(ia), _p(cp), _p(cn), _p(pen))
+                                   _p(out), _p(ic), _p(ia), _p(cp), _p(cn), _p(pen), _p(ij))
     return out, dict(contact=ic, actuator=ia, contact_pos=cp, contact_normal=cn,
-                     contact_penetration=pen)
+                     contact_penetration=pen, joint=ij)
 
   def system_info(self, qp):
     qp = self._a(qp)

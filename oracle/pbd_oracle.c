@@ -137,6 +137,8 @@ typedef struct {
   R *fstr, *fmass;
   R *mass, *inv_mass, *I, *pos_mask, *rot_mask, *quat_mask;
   R *joff_p, *joff_c, *jax_p, *jax_c, *jlim, *jdamp, *jsp, *jsa;
+  R *jstiff, *jsdamp, *jlstr;  /* legacy_spring (spring_joints.py:57-67) */
+  int spring;
   R *astr;
   R *gscale, *gthr, *gerp;
   R *ra_pos, *ra_end, *ra_rad, *rb_pos, *rb_end, *rb_rad, *rfric, *relas;
@@ -144,7 +146,7 @@ typedef struct {
 
 static R* cvt(const double* s, int n) {
   R* o = (R*)malloc(sizeof(R) * (n > 0 ? n : 1));
-  for (int i = 0; i < n; i++) o[i] = (R)s[i];
+  for (int i = 0; i < n; i++) o[i] = s ? (R)s[i] : (R)0;
   return o;
 }
 
@@ -178,6 +180,10 @@ static void sys_init(sysc* s, const bx_desc* d) {
   s->jdamp = cvt(d->joint_damping, J);
   s->jsp = cvt(d->joint_scale_pos, J);
   s->jsa = cvt(d->joint_scale_ang, J);
+  s->spring = d->dynamics_mode == BX_DYN_LEGACY_SPRING;
+  s->jstiff = cvt(d->joint_stiffness, J);
+  s->jsdamp = cvt(d->joint_spring_damping, J);
+  s->jlstr = cvt(d->joint_limit_strength, J);
   s->astr = cvt(d->act_strength, s->K);
   s->gscale = cvt(d->col_scale, s->G);
   s->gthr = cvt(d->col_velocity_threshold, s->G);
@@ -197,7 +203,8 @@ static void sys_free(sysc* s) {
              &s->joff_p, &s->joff_c, &s->jax_p, &s->jax_c, &s->jlim, &s->jdamp,
              &s->jsp, &s->jsa, &s->astr, &s->gscale, &s->gthr, &s->gerp,
              &s->ra_pos, &s->ra_end, &s->ra_rad, &s->rb_pos, &s->rb_end,
-             &s->rb_rad, &s->rfric, &s->relas, &s->fstr, &s->fmass};
+             &s->rb_rad, &s->rfric, &s->relas, &s->fstr, &s->fmass,
+             &s->jstiff, &s->jsdamp, &s->jlstr};
   for (size_t i = 0; i < sizeof(p) / sizeof(p[0]); i++) free(*p[i]);
 }
 
@@ -214,6 +221,7 @@ typedef struct {
   R *gpos, *grot, *gvel, *gang;  /* per-group scratch (N,3/4) */
   R *c_pos, *c_norm, *c_pen, *c_vel, *dlam; /* contact rows */
   R *info_c, *info_a;            /* (N,6) accumulators */
+  R *sj_v, *sj_a, *info_j;       /* legacy_spring: dp_j (N,3)x2, Info.joint (N,6) */
   int* ract;                     /* (R) NearNeighbors rank, -1 = culled */
 } work_t;
 
@@ -233,12 +241,14 @@ static void work_alloc(work_t* w, int N, int Rn) {
   w->dlam = calloc(r, sizeof(R));
   w->info_c = calloc(6 * n, sizeof(R)); w->info_a = calloc(6 * n, sizeof(R));
   w->ract = calloc(r, sizeof(int));
+  w->sj_v = calloc(3 * n, sizeof(R)); w->sj_a = calloc(3 * n, sizeof(R));
+  w->info_j = calloc(6 * n, sizeof(R));
 }
 static void work_free(work_t* w) {
   void* p[] = {w->qp, w->qprev, w->qrb, w->dp_a, w->dp_j, w->acc, w->dq_pos, w->dq_rot,
                w->dp_vel, w->dp_ang, w->cnt, w->gpos, w->grot, w->gvel, w->gang,
                w->c_pos, w->c_norm, w->c_pen, w->c_vel, w->dlam, w->info_c, w->info_a,
-               w->ract};
+               w->ract, w->sj_v, w->sj_a, w->info_j};
   for (size_t i = 0; i < sizeof(p) / sizeof(p[0]); i++) free(p[i]);
 }
 
@@ -296,7 +306,8 @@ static int axis_angle(const sysc* s, int j, const body_t* p, const body_t* c,
   memcpy(axes[1], a2c, sizeof(a2c));
   memcpy(axes[2], a3c, sizeof(a3c));
   ang[0] = psi; ang[1] = theta; ang[2] = phi;
-  return 3;
+  /* spring Universal.axis_angle (spring_joints.py:188-216): (psi, theta) */
+  return s->d->joint_type[j] == BX_JOINT_UNIVERSAL ? 2 : 3;
 }
 
 /* Joint.apply_angle_update (joints.py:130-152); accumulates into dq (7 per side) */
@@ -1205,9 +1216,171 @@ static void pbd_step_env(const sysc* s, work_t* w, const R* act, R* rows_a, R* r
   }
 }
 
+/* -------------------------------------------------- legacy_spring ------- */
+
+/* spring Revolute/Universal/Spherical.apply_reduced (spring_joints.py:122-155,
+ * 170-204, 262-287) for joint j: dP of parent and child, (vel3, ang3) each */
+static void spring_joint_one(const sysc* s, int j, const body_t* qp, R* op, R* oc) {
+  int bp = s->d->joint_body_p[j], bc = s->d->joint_body_c[j];
+  const body_t* p = &qp[bp];
+  const body_t* c = &qp[bc];
+  const R* Ip = s->I + 3 * bp;
+  const R* Ic = s->I + 3 * bc;
+  R stiff = s->jstiff[j], sdamp = s->jsdamp[j], lstr = s->jlstr[j];
+  /* QP.to_world (base.py:110-124) */
+  R offp[3], offc[3], wp[3], wc[3], pos_p[3], pos_c[3], vel_p[3], vel_c[3];
+  rotate(s->joff_p + 3 * j, p->rot, offp);
+  rotate(s->joff_c + 3 * j, c->rot, offc);
+  cross3(p->ang, offp, wp);
+  cross3(c->ang, offc, wc);
+  for (int k = 0; k < 3; k++) {
+    pos_p[k] = p->pos[k] + offp[k]; vel_p[k] = p->vel[k] + wp[k];
+    pos_c[k] = c->pos[k] + offc[k]; vel_c[k] = c->vel[k] + wc[k];
+  }
+  R imp[3], nimp[3], rp[3], rc[3], cp[3], cc[3];
+  for (int k = 0; k < 3; k++) {
+    imp[k] = (pos_p[k] - pos_c[k]) * stiff + sdamp * (vel_p[k] - vel_c[k]);
+    nimp[k] = -imp[k];
+    rp[k] = pos_p[k] - p->pos[k];
+    rc[k] = pos_c[k] - c->pos[k];
+  }
+  /* Body.impulse (bodies.py:46-59) */
+  cross3(rp, nimp, cp);
+  cross3(rc, imp, cc);
+  for (int k = 0; k < 3; k++) {
+    op[k] = nimp[k] / s->mass[bp];
+    op[3 + k] = Ip[k] * cp[k];
+    oc[k] = imp[k] / s->mass[bc];
+    oc[3 + k] = Ic[k] * cc[k];
+  }
+  R axes[3][3], ang[3], dang[3] = {0, 0, 0};
+  int dof = axis_angle(s, j, p, c, axes, ang);
+  const R* lim = s->jlim + 6 * j;
+  for (int l = 0; l < dof; l++) {
+    R dd = ang[l] < lim[2 * l] ? lim[2 * l] - ang[l] : (R)0;
+    dang[l] = ang[l] > lim[2 * l + 1] ? lim[2 * l + 1] - ang[l] : dd;
+  }
+  R tq[3];
+  int type = s->d->joint_type[j];
+  if (type == BX_JOINT_REVOLUTE) {
+    R axc[3];
+    rotate(s->jax_c + 9 * j, c->rot, axc);
+    cross3(axes[0], axc, tq);
+    for (int k = 0; k < 3; k++) tq[k] = stiff * tq[k] - (lstr * axes[0][k]) * dang[0];
+  } else if (type == BX_JOINT_UNIVERSAL) {
+    R d21 = dot3(axes[1], axes[0]), proj[3];
+    for (int k = 0; k < 3; k++) proj[k] = axes[1][k] - d21 * axes[0][k];
+    R pn = safe_norm3(proj);
+    for (int k = 0; k < 3; k++) proj[k] /= pn;
+    cross3(proj, axes[1], tq);
+    for (int k = 0; k < 3; k++)
+      tq[k] = (lstr / (R)5) * tq[k] - lstr * (axes[0][k] * dang[0] + axes[1][k] * dang[1]);
+  } else {
+    for (int k = 0; k < 3; k++)
+      tq[k] = -lstr * ((axes[0][k] * dang[0] + axes[1][k] * dang[1]) + axes[2][k] * dang[2]);
+  }
+  for (int k = 0; k < 3; k++) {
+    tq[k] -= s->jdamp[j] * (p->ang[k] - c->ang[k]);
+    op[3 + k] += Ip[k] * tq[k];
+    oc[3 + k] += -Ic[k] * tq[k];
+  }
+}
+
+/* spring Joint.apply (spring_joints.py:89-113), segment-summed per group over
+ * concat(parents, children), groups added in order: w->sj_v, w->sj_a */
+static void spring_joints_apply(const sysc* s, work_t* w) {
+  int N = s->N, J = s->J;
+  memset(w->sj_v, 0, sizeof(R) * 3 * N);
+  memset(w->sj_a, 0, sizeof(R) * 3 * N);
+  int j0 = 0;
+  while (j0 < J) {
+    int g = s->d->joint_group[j0], j1 = j0;
+    while (j1 < J && s->d->joint_group[j1] == g) j1++;
+    memset(w->gvel, 0, sizeof(R) * 3 * N);
+    memset(w->gang, 0, sizeof(R) * 3 * N);
+    R (*op)[6] = calloc(j1 - j0, sizeof(R[6]));
+    R (*oc)[6] = calloc(j1 - j0, sizeof(R[6]));
+    for (int j = j0; j < j1; j++) spring_joint_one(s, j, w->qp, op[j - j0], oc[j - j0]);
+    for (int side = 0; side < 2; side++)
+      for (int j = j0; j < j1; j++) {
+        int b = side == 0 ? s->d->joint_body_p[j] : s->d->joint_body_c[j];
+        const R* v = side == 0 ? op[j - j0] : oc[j - j0];
+        for (int k = 0; k < 3; k++) { w->gvel[3 * b + k] += v[k]; w->gang[3 * b + k] += v[3 + k]; }
+      }
+    for (int i = 0; i < 3 * N; i++) { w->sj_v[i] += w->gvel[i]; w->sj_a[i] += w->gang[i]; }
+    free(op); free(oc);
+    j0 = j1;
+  }
+}
+
+/* System._spring_step (system.py:342-375) for one env */
+static void spring_step_env(const sysc* s, work_t* w, const R* act, R* rows_a, R* rows_b) {
+  int N = s->N, Rn = s->Rn;
+  memset(w->info_c, 0, sizeof(R) * 6 * N);
+  memset(w->info_a, 0, sizeof(R) * 6 * N);
+  memset(w->info_j, 0, sizeof(R) * 6 * N);
+  nn_select(s, w);  /* cull.update, once per step (system.py:371-372) */
+  for (int sub = 0; sub < s->d->substeps; sub++) {
+    kinetic(s, w);
+    spring_joints_apply(s, w);
+    actuators_apply(s, w, act);
+    /* Euler.update(acc_p = dp_j + dp_a + dp_f) (integrators.py:85-93) */
+    for (int b = 0; b < N; b++) {
+      body_t* q = &w->qp[b];
+      R fv[3], fa[3];
+      body_forces(s, b, act, fv, fa);
+      for (int k = 0; k < 3; k++) {
+        R dv = (w->sj_v[3 * b + k] + (R)0) + fv[k];
+        R da = (w->sj_a[3 * b + k] + w->dp_a[3 * b + k]) + fa[k];
+        R v = s->vdamp_exp * q->vel[k];
+        v += (dv + s->g[k]) * s->h;
+        v *= s->pos_mask[3 * b + k];
+        R a = s->adamp_exp * q->ang[k];
+        a += da * s->h;
+        a *= s->rot_mask[3 * b + k];
+        q->vel[k] = v;
+        q->ang[k] = a;
+      }
+    }
+    /* Collider.apply (colliders.py:116-153), then Euler.update(vel_p = dp_c) */
+    for (int r = 0; r < Rn; r++) {
+      if (w->ract[r] < 0) {
+        memset(rows_a + 6 * r, 0, 6 * sizeof(R));
+        memset(rows_b + 6 * r, 0, 6 * sizeof(R));
+        continue;
+      }
+      contact_row(s, r, w->qp, w->c_pos + 3 * r, w->c_vel + 3 * r, w->c_norm + 3 * r, &w->c_pen[r]);
+      impulse_contact(s, r, w->qp, w->c_pos + 3 * r, w->c_vel + 3 * r, w->c_norm + 3 * r,
+                      w->c_pen[r], rows_a + 6 * r, rows_b + 6 * r);
+    }
+    memset(w->dp_vel, 0, sizeof(R) * 3 * N);
+    memset(w->dp_ang, 0, sizeof(R) * 3 * N);
+    for (int g = 0; g < s->G; g++) group_reduce(s, w, g, 6, (R)1e-8, rows_a, rows_b, w->dp_vel, w->dp_ang);
+    update_vel(s, w);
+    for (int b = 0; b < N; b++)
+      for (int k = 0; k < 3; k++) {
+        w->info_c[6 * b + k] += w->dp_vel[3 * b + k];
+        w->info_c[6 * b + 3 + k] += w->dp_ang[3 * b + k];
+        w->info_j[6 * b + k] += w->sj_v[3 * b + k];
+        w->info_j[6 * b + 3 + k] += w->sj_a[3 * b + k];
+        w->info_a[6 * b + 3 + k] += w->dp_a[3 * b + k];
+      }
+  }
+}
+
+/* System.step (system.py:244-247): the config's dynamics mode */
+static void step_env(const sysc* s, work_t* w, const R* act, R* rows_a, R* rows_b) {
+  if (s->spring) {
+    spring_step_env(s, w, act, rows_a, rows_b);
+  } else {
+    pbd_step_env(s, w, act, rows_a, rows_b);
+    memset(w->info_j, 0, sizeof(R) * 6 * s->N);
+  }
+}
+
 int FN(oracle_system_step)(const bx_desc* d, int64_t B, const R* qp_in, const R* act,
                            R* qp_out, R* info_contact, R* info_actuator, R* cpos,
-                           R* cnorm, R* cpen) {
+                           R* cnorm, R* cpen, R* info_joint) {
   sysc s;
   sys_init(&s, d);
   int N = s.N, Rn = s.Rn, A = s.aw, IR = info_rows(&s);
@@ -1220,9 +1393,10 @@ int FN(oracle_system_step)(const bx_desc* d, int64_t B, const R* qp_in, const R*
 #pragma omp for schedule(static)
     for (int64_t e = 0; e < B; e++) {
       load_qp(w.qp, qp_in + e * 13 * N, N);
-      pbd_step_env(&s, &w, act + e * A, ra, rb);
+      step_env(&s, &w, act + e * A, ra, rb);
       store_qp(w.qp, qp_out + e * 13 * N, N);
       if (info_contact) memcpy(info_contact + e * 6 * N, w.info_c, sizeof(R) * 6 * N);
+      if (info_joint) memcpy(info_joint + e * 6 * N, w.info_j, sizeof(R) * 6 * N);
       if (info_actuator) memcpy(info_actuator + e * 6 * N, w.info_a, sizeof(R) * 6 * N);
       for (int r = 0; r < Rn; r++) {
         int x = row_info(&s, &w, r);
@@ -1453,7 +1627,7 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
       const R* a = act + e * A;
       load_qp(w.qp, qp_in + e * 13 * N, N);
       memcpy(q0, w.qp, sizeof(body_t) * N);
-      pbd_step_env(&s, &w, a, ra, rb);
+      step_env(&s, &w, a, ra, rb);
       store_qp(w.qp, qp_out + e * 13 * N, N);
       R* o = obs + e * obs_size;
       R* m = metrics + e * n_metrics;

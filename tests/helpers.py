@@ -33,12 +33,29 @@ defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { x:
 defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { z: 2 } } qps { name: "Capsule3" pos { x: 3 z: 1 } } qps { name: "Capsule4" pos { x: 5 z: 1 } } }
 """
 CAPSULES = ['capsule_ground', 'capsule_capsule', 'capsule_cull']
+# legacy_spring systems (`_SYSTEM_CONFIG_SPRING`, system.py:342-390): envs with
+# the kernel env layer, and physics rollouts of the other registered envs
+SPRING_ENVS = ['ant_spring', 'humanoid_spring', 'halfcheetah_spring', 'humanoidstandup_spring']
+SPRING_ROBOTS = [m + '_spring' for m in (
+    'inverted_pendulum', 'inverted_double_pendulum', 'swimmer', 'hopper', 'walker2d', 'reacher',
+    'reacherangle', 'acrobot', 'ur5e', 'grasp', 'fetch')]
+_SPRING_MOD = {'halfcheetah': 'HALF_CHEETAH', 'humanoidstandup': 'HUMANOID_STANDUP'}
+
+
+def env_kind(name):
+  """Env-layer kind of a golden name ('ant_spring' -> 'ant')."""
+  return name[:-len('_spring')] if name.endswith('_spring') else name
+
+
 # point-plane scenes: BoxTest (box corners) and an inline-mesh MeshTest
 # (mesh vertices), oracle/scenes.py
 POINTS = ['box_ground', 'box_slide', 'mesh_ground', 'mesh_tilt']
 
 
 def config_for(name):
+  if name.endswith('_spring'):
+    base = name[:-len('_spring')]
+    return cfgmod.parse(getattr(robots, _SPRING_MOD.get(base, base.upper()) + '_SPRING_CONFIG'))
   if name in CAPSULES:
     cfg = cfgmod.parse(CAPSULE_TEST_CONFIG)
     if name != 'capsule_ground':

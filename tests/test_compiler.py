@@ -4,10 +4,11 @@ import pytest
 
 from brax_amd import compiler
 from tests.conftest import golden
-from tests.helpers import CAPSULES, POINTS, ROBOTS, compiled, config_for
+from tests.helpers import (CAPSULES, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, compiled,
+                           config_for)
 
 NAMES = (['ant', 'humanoid', 'halfcheetah', 'humanoidstandup', 'mountain1', 'mountain2', 'mountain4', 'mountain1nn']
-         + ROBOTS + CAPSULES + POINTS)
+         + ROBOTS + CAPSULES + POINTS + SPRING_ENVS + SPRING_ROBOTS)
 
 
 @pytest.mark.parametrize('name', NAMES)
@@ -48,6 +49,18 @@ def test_parents_generator_quirk():
   pairs = set(zip(d['row_body_a'][d['row_group'] == 1].tolist(),
                   d['row_body_b'][d['row_group'] == 1].tolist()))
   assert (0, 1) in pairs or (1, 0) in pairs
+
+
+def test_spring_groups():
+  """legacy_spring (spring_joints.py:302-331): joints grouped by dof without
+  sphericalisation -> Revolute, Universal, Spherical groups; actuators index
+  every dof (no -1 padding); spring defaults from stiffness."""
+  _, d, _, meta = compiled('humanoid_spring')
+  assert int(d['dynamics_mode']) == compiler.DYN_LEGACY_SPRING
+  assert sorted(set(d['joint_type'].tolist())) == [1, 2, 3]
+  assert (np.diff(d['joint_group']) >= 0).all() and (d['joint_free_dofs'] == -1).all()
+  assert meta['num_joint_dof'] == 17 and (d['act_index'] >= 0).sum() == 17
+  assert (d['joint_stiffness'] > 0).all() and (d['joint_limit_strength'] > 0).all()
 
 
 def test_unsupported_raise():

@@ -7,10 +7,11 @@ import numpy as np
 import pytest
 
 from tests.conftest import golden
-from tests.helpers import CAPSULES, POINTS, ROBOTS, compiled
+from tests.helpers import CAPSULES, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, compiled, env_kind
 
-ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup']
-SYS_TRAJ = ['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + POINTS
+ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
+SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + POINTS
+            + SPRING_ROBOTS)
 
 
 def _oracle(oracle_lib, name, guard=False, dtype=np.float64):
@@ -52,7 +53,7 @@ def test_env_step_matches_reference(oracle_lib, name):
   T = golden('traj_' + name)
   O, M = T['obs'].shape[-1], T['metrics'].shape[-1]
   for t in range(T['action'].shape[0]):
-    _, obs, rew, done, met = o.env_step(name, T['qp'][t], T['action'][t], O, M)
+    _, obs, rew, done, met = o.env_step(env_kind(name), T['qp'][t], T['action'][t], O, M)
     assert np.abs(obs - T['obs'][t + 1]).max() < 1e-9
     assert np.abs(rew - T['reward'][t]).max() < 1e-12
     assert np.array_equal(done, T['done'][t])
@@ -67,7 +68,7 @@ def test_reset_matches_reference(oracle_lib, name):
   assert np.abs(qp0 - T['qp'][0]).max() < 1e-12
   ic = o.system_info(qp0)
   B = qp0.shape[0]
-  obs = o.env_obs(name, qp0, ic, np.zeros((B, o.A)), T['obs'].shape[-1])
+  obs = o.env_obs(env_kind(name), qp0, ic, np.zeros((B, o.A)), T['obs'].shape[-1])
   assert np.abs(obs - T['reset_obs']).max() < 1e-12
 
 
