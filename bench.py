@@ -198,6 +198,8 @@ def main():
                   help='skip the Humanoid / Ant Mountain legs')
   ap.add_argument('--generic', action='store_true',
                   help='force the generic item-loop kernel variant (A/B)')
+  ap.add_argument('--block', type=int, default=0,
+                  help='threads per workgroup of the step kernel (A/B; default 64)')
   ap.add_argument('--variant', default='',
                   help='lanes,mode kernel variant (mode 0 global, 1 single, 2 lds)')
   args = ap.parse_args()
@@ -215,6 +217,8 @@ def main():
   if args.variant:
     lanes, mode = (int(x) for x in args.variant.split(','))
     _native.check(_native.lib().bx_system_set_variant(env.sys._h, lanes, mode))
+  if args.block:
+    _native.check(_native.lib().bx_system_set_block(env.sys._h, args.block))
   from brax_amd import distributed as bd
   state = env.reset(bd.rank_key(np.array([0, 0x5EED], np.uint32), rank))
   # synthetic U[-1,1] actions, one (B, 8) slab per step, drawn on the device by

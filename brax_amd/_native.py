@@ -35,6 +35,7 @@ _SIGS = {
     'bx_system_lanes': ([C.c_void_p], C.c_int),
     'bx_system_set_single': ([C.c_void_p, C.c_int], C.c_int),
     'bx_system_set_variant': ([C.c_void_p, C.c_int, C.c_int], C.c_int),
+    'bx_system_set_block': ([C.c_void_p, C.c_int], C.c_int),
     'bx_system_step': ([C.c_void_p, C.c_int64, C.POINTER(abi.BxQP), C.c_void_p, C.c_int64,
                         C.c_int64, C.POINTER(abi.BxQP), C.POINTER(abi.BxInfo), C.c_void_p],
                        C.c_int),

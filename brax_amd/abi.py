@@ -40,6 +40,7 @@ _DESC_FIELDS = [
     ('col_cutoff', i32p), ('row_flat', i32p),
     ('dynamics_mode', C.c_int32), ('joint_stiffness', f64p),
     ('joint_spring_damping', f64p), ('joint_limit_strength', f64p),
+    ('row_ext', f64p), ('row_hm', i32p), ('n_hm', C.c_int32), ('hm_data', f64p),
 ]
 
 DYN_PBD, DYN_LEGACY_SPRING = 0, 1
@@ -120,6 +121,7 @@ def make_desc(d):
   s.velocity_damping = float(d['velocity_damping'])
   s.angular_damping = float(d['angular_damping'])
   s.dynamics_mode = int(d.get('dynamics_mode', DYN_PBD))
+  s.n_hm = len(d.get('hm_data', ()))
   for name, ctype in _DESC_FIELDS:
     if ctype is i32p or ctype is f64p:
       if name in d:
@@ -132,6 +134,12 @@ def make_desc(d):
         v = np.zeros(0)
       elif name in _SPRING_FIELDS:
         v = np.zeros(len(d['joint_type']))
+      elif name == 'row_ext':
+        v = np.zeros((len(d['row_group']), 16))
+      elif name == 'row_hm':
+        v = np.tile([-1, 0], (len(d['row_group']), 1))
+      elif name == 'hm_data':
+        v = np.zeros(0)
       else:
         raise KeyError(name)
       a = _arr(v, np.int32 if ctype is i32p else np.float64)

@@ -33,7 +33,8 @@ DYN_PBD, DYN_LEGACY_SPRING = 0, 1
 # actuator kinds (descriptor `act_type`)
 TORQUE, ANGLE = 0, 1
 # contact functions (descriptor `col_fn`)
-CAPSULE_PLANE, CAPSULE_CAPSULE = 0, 1
+CAPSULE_PLANE, CAPSULE_CAPSULE, HEIGHTMAP, CLIPPED_PLANE, CAPSULE_MESH = 0, 1, 2, 3, 4
+ROW_EXT = 16  # per-row extra constants of the extended contact functions
 # force kinds
 THRUSTER, TWISTER = 0, 1
 
@@ -197,6 +198,37 @@ def _near_neighbors(pairs, index, cutoff):
 
 
 _BOX_CORNERS = np.array(list(itertools.product((-1, 1), (-1, 1), (-1, 1))), np.float64)
+# `geometry.py:34-56`: the 12 triangles of a box (indices into _BOX_CORNERS)
+# and their outward normals
+_TRI_BOX_FACES = [0, 4, 1, 4, 1, 5, 0, 4, 2, 2, 4, 6, 6, 4, 5, 6, 5, 7,
+                  2, 6, 3, 3, 6, 7, 1, 3, 5, 5, 3, 7, 0, 2, 1, 1, 2, 3]
+_TRI_BOX_NORMALS = [[0, -1., 0], [0, -1., 0], [0, 0, -1.], [0, 0, -1.], [1., 0, 0], [1., 0, 0],
+                    [0, 1., 0], [0, 1., 0], [0, 0, 1.], [0, 0, 1.], [-1., 0, 0], [-1., 0, 0]]
+
+
+def _mesh_faces(col, mesh_geoms):
+  """Triangles (F,3,3) and face normals (F,3) in the body frame of a
+  TriangulatedBox (`geometry.py:157-198`) or a Mesh (`geometry.py:291-331`),
+  with BaseMesh's winding fix (`geometry.py:138-154`): a face whose first two
+  edges wind against its normal has its vertex order reversed."""
+  rot = euler_to_quat(vec(col.rotation))
+  if col.WhichOneof('type') == 'box':
+    vert = np.array([rotate(c, rot) for c in _BOX_CORNERS * vec(col.box.halfsize)])
+    vert = vert + vec(col.position)
+    normals = np.array([rotate(np.array(n), rot) for n in _TRI_BOX_NORMALS])
+    faces = vert[np.array(_TRI_BOX_FACES)].reshape(-1, 3, 3)
+  else:
+    g = mesh_geoms[col.mesh.name]
+    scale = col.mesh.scale if col.mesh.scale else 1
+    vert = np.array([[v.x * scale, v.y * scale, v.z * scale] for v in g.vertices], np.float64)
+    vert = np.array([rotate(v, rot) for v in vert]) + vec(col.position)
+    faces = vert[np.array(list(g.faces), np.int64)].reshape(-1, 3, 3)
+    normals = np.array([rotate(vec(n), rot) for n in g.face_normals])
+  out = []
+  for f, n in zip(faces, normals):
+    wind = np.dot(np.cross(f[0] - f[-1], f[0] - f[1]), n) >= 0
+    out.append(f if wind else f[::-1])
+  return np.array(out), normals
 
 
 def _point_ends(col, mesh_geoms):
@@ -226,7 +258,11 @@ def _colliders(config, index):
   supported = {('capsule', 'plane'): CAPSULE_PLANE,
                ('capsule', 'capsule'): CAPSULE_CAPSULE,
                ('box', 'plane'): CAPSULE_PLANE,
-               ('mesh', 'plane'): CAPSULE_PLANE}
+               ('mesh', 'plane'): CAPSULE_PLANE,
+               ('box', 'heightMap'): HEIGHTMAP,
+               ('capsule', 'clipped_plane'): CLIPPED_PLANE,
+               ('capsule', 'box'): CAPSULE_MESH,
+               ('capsule', 'mesh'): CAPSULE_MESH}
   mesh_geoms = {mg.name: mg for mg in config.mesh_geometries}
   unique_meshes = {}
   cols = []
@@ -303,7 +339,8 @@ def _colliders(config, index):
              col_baumgarte_erp=[])
   rows = {k: [] for k in ('group', 'body_a', 'body_b', 'a_pos', 'a_end',
                           'a_radius', 'b_pos', 'b_end', 'b_radius', 'friction',
-                          'elasticity', 'flat')}
+                          'elasticity', 'flat', 'ext', 'hm')}
+  hm_data = []
   out['col_cutoff'] = []
   for gi, g in enumerate(groups):
     out['col_oneway'].append(1 if g['oneway'] else 0)
@@ -312,11 +349,21 @@ def _colliders(config, index):
     out['col_velocity_threshold'].append(g_norm * h * 4.0)
     out['col_baumgarte_erp'].append(config.baumgarte_erp * config.substeps / config.dt)
     out['col_cutoff'].append(g['cutoff'])
+    ext_l = None
     if g['kind'] in ('box', 'mesh'):
       # Box corners (`geometry.py:123-137`) / PointMesh vertices (:312-357)
       # in the body frame, as zero-radius capsule ends
       ends_l = [_point_ends(ca, mesh_geoms) for ca, _, _, _, _, _ in g['pairs']]
-    elif g['fn'] == CAPSULE_PLANE:
+    elif g['fn'] == CAPSULE_MESH:
+      # one row per triangle of the box / mesh (`colliders.py:822-848`)
+      ends_l, ext_l = [], []
+      for ca, _, _, cb, _, _ in g['pairs']:
+        faces, normals = _mesh_faces(cb, mesh_geoms)
+        ends_l.append([_capsule_axis(ca) * (ca.capsule.length * 0.5 - ca.capsule.radius)]
+                      * len(faces))
+        ext_l.append([np.concatenate([f.reshape(-1), n, np.zeros(ROW_EXT - 12)])
+                      for f, n in zip(faces, normals)])
+    elif g['fn'] in (CAPSULE_PLANE, CLIPPED_PLANE):
       # CapsuleEnd (`geometry.py:261-288`): 1 or 2 ends; mixed -> pad by dup
       ends_l = []
       for ca, _, _, _, _, _ in g['pairs']:
@@ -333,14 +380,39 @@ def _colliders(config, index):
       fa = ca.material.friction * cb.material.friction
       ea = ca.material.elasticity * cb.material.elasticity
       a_rad = 0. if g['kind'] in ('box', 'mesh') else ca.capsule.radius
-      if g['fn'] == CAPSULE_PLANE:
+      ext, hm = [np.zeros(ROW_EXT)] * len(ends_l[pi]) if g['fn'] != CAPSULE_CAPSULE else [
+          np.zeros(ROW_EXT)], (-1, 0)
+      if g['fn'] == HEIGHTMAP:
+        # HeightMap (`geometry.py:270-288`): a square grid, row-major, cell
+        # size = size / (mesh_size - 1)
+        data = np.asarray(list(cb.heightMap.data), np.float64)
+        m = int(np.sqrt(len(data)))
+        if m * m != len(data):
+          raise ValueError('height map data length should be a perfect square.')
+        hm = (len(hm_data), m)
+        hm_data.extend(data.tolist())
+        ext = [np.concatenate([[cb.heightMap.size / (m - 1)], np.zeros(ROW_EXT - 1)])] * 8
+      elif g['fn'] == CLIPPED_PLANE:
+        # ClippedPlane (`geometry.py:214-239`): normal, x, y of the collider
+        # rotation, position, half sizes (body frame)
+        rot = euler_to_quat(vec(cb.rotation))
+        e = np.concatenate([rotate(np.array([0., 0., 1.]), rot), rotate(np.array([1., 0., 0.]), rot),
+                            rotate(np.array([0., 1., 0.]), rot), vec(cb.position),
+                            [cb.clipped_plane.halfsize_x, cb.clipped_plane.halfsize_y],
+                            np.zeros(ROW_EXT - 14)])
+        ext = [e] * len(ends_l[pi])
+      elif ext_l is not None:
+        ext = ext_l[pi]
+      if g['fn'] in (CAPSULE_PLANE, HEIGHTMAP, CLIPPED_PLANE, CAPSULE_MESH):
         ends = ends_l[pi]
         b_end, b_rad = np.zeros(3), 0.
       else:
         ends = [_capsule_axis(ca) * (ca.capsule.length * 0.5 - ca.capsule.radius)]
         b_end = _capsule_axis(cb) * (cb.capsule.length * 0.5 - cb.capsule.radius)
         b_rad = cb.capsule.radius
-      for e in ends:
+      for ei, e in enumerate(ends):
+        rows['ext'].append(ext[ei])
+        rows['hm'].append(hm)
         rows['flat'].append(flats[pi])
         rows['group'].append(gi)
         rows['body_a'].append(index[ba.name])
@@ -359,6 +431,9 @@ def _colliders(config, index):
   d['col_cutoff'] = np.asarray(out['col_cutoff'], np.int32)
   for k in ('col_scale', 'col_velocity_threshold', 'col_baumgarte_erp'):
     d[k] = np.asarray(out[k], np.float64)
+  d['row_ext'] = np.asarray(rows.pop('ext'), np.float64).reshape(-1, ROW_EXT)
+  d['row_hm'] = np.asarray(rows.pop('hm'), np.int32).reshape(-1, 2)
+  d['hm_data'] = np.asarray(hm_data, np.float64)
   for k, v in rows.items():
     if k in ('group', 'body_a', 'body_b', 'flat'):
       d['row_' + k] = np.asarray(v, np.int32)

@@ -48,6 +48,7 @@ struct bx_system {
   int mode = 0;     // MODE_GLOBAL / MODE_SINGLE / MODE_LDS
   int feat = 31;    // F_SPH | F_ANGLE | F_CC | F_TW | F_FORCE used by this system
   int gw = 8;       // gather width (max per-body list length, 4 or 8)
+  int tpb = 64;     // threads per workgroup of the step kernels (multiple of L)
   bool single_ok = false;
   size_t lds_env = 0;    // bytes per block for the per-env kernels
   size_t lds_reset = 0;  // bytes per block for default_qp
@@ -94,8 +95,14 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       return fail("contact row body out of range");
     if (d->row_group[x] < 0 || d->row_group[x] >= G) return fail("contact row group out of range");
     int fn = d->col_fn[d->row_group[x]];
-    if (fn != BX_COL_CAPSULE_PLANE && fn != BX_COL_CAPSULE_CAPSULE)
-      return fail("unsupported contact function");
+    if (fn < BX_COL_CAPSULE_PLANE || fn > BX_COL_CAPSULE_MESH) return fail("unsupported contact function");
+    if (fn >= BX_COL_HEIGHTMAP && !d->row_ext) return fail("extended contact rows need row_ext");
+    if (fn == BX_COL_HEIGHTMAP) {
+      if (!d->row_hm || !d->hm_data) return fail("height map rows need row_hm and hm_data");
+      int off = d->row_hm[2 * x], m = d->row_hm[2 * x + 1];
+      if (m < 2 || off < 0 || (int64_t)off + (int64_t)m * m > d->n_hm)
+        return fail("height map row out of range");
+    }
   }
   for (int f = 0; f < d->n_forces; f++) {
     if (d->force_body[f] < 0 || d->force_body[f] >= N) return fail("force body out of range");
@@ -213,7 +220,15 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     B.f(o + R_SCALE, d->col_scale[g]);
     B.f(o + R_THR, d->col_velocity_threshold[g]);
     B.f(o + R_ERP, d->col_baumgarte_erp[g]);
+    if (d->row_ext)
+      for (int k = 0; k < 16; k++) B.f(o + R_X + k, d->row_ext[16 * x + k]);
+    if (d->col_fn[g] == BX_COL_HEIGHTMAP) {
+      B.i(o + R_HM_OFF, d->row_hm[2 * x]);
+      B.i(o + R_HM_M, d->row_hm[2 * x + 1]);
+    }
   }
+  H.o_hm = B.alloc(d->n_hm > 0 ? d->n_hm : 0);
+  for (int k = 0; k < d->n_hm; k++) B.f(H.o_hm + k, d->hm_data[k]);
   // collider groups: cutoff, row range, Info base (system.py:36-43 order)
   H.o_group = B.alloc(G * GROUP_STRIDE);
   {
@@ -371,8 +386,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     }
     // the register-hoisted kernel is the pbd step only; legacy_spring systems
     // run the item-loop kernel
+    bool xcol = false;  // extended contact functions run in the item-loop kernel
+    for (int g = 0; g < G; g++) xcol |= d->col_fn[g] >= BX_COL_HEIGHTMAP;
     H.single = (N <= L && J <= L && K <= L && R <= L && mx <= 8 && max_groups <= 2 &&
-                H.n_nn == 0 && !H.spring) ? 1 : 0;
+                H.n_nn == 0 && !H.spring && !xcol) ? 1 : 0;
     H.act_same = 1;
     for (int a = 0; a < K; a++)
       if (d->act_joint[a] != a) H.act_same = 0;
@@ -407,7 +424,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 size_t step_lds(const bx_system* S) {
-  size_t b = (size_t)(64 / S->L) * S->hdr.env_words * 4;
+  size_t b = (size_t)(S->tpb / S->L) * S->hdr.env_words * 4;
   if (S->mode == 2) b += (size_t)S->hdr.const_words * 4;
   return b;
 }
@@ -476,13 +493,28 @@ int bx_system_set_variant(bx_system* S, int lanes, int mode) {
   if (lanes < S->min_L) return fail("lanes below the system's minimum");
   if (mode < 0 || mode > 2) return fail("mode must be 0 (global), 1 (single) or 2 (lds)");
   if (mode == 1 && !S->single_ok) return fail("system does not fit the single-item-per-lane kernel");
-  int old_L = S->L, old_m = S->mode;
+  int old_L = S->L, old_m = S->mode, old_t = S->tpb;
   S->L = lanes;
   S->mode = mode;
+  if (S->tpb % lanes) S->tpb = 64;
   if (step_lds(S) > 160 * 1024) {
     S->L = old_L;
     S->mode = old_m;
+    S->tpb = old_t;
     return fail("variant exceeds the LDS budget");
+  }
+  return 0;
+}
+
+int bx_system_set_block(bx_system* S, int threads) {
+  if (!S) return fail("null system");
+  if (threads < S->L || threads > 64 || threads % S->L)
+    return fail("threads must be a multiple of the lanes per env, at most 64");
+  int old = S->tpb;
+  S->tpb = threads;
+  if (step_lds(S) > 160 * 1024) {
+    S->tpb = old;
+    return fail("block exceeds the LDS budget");
   }
   return 0;
 }
@@ -512,7 +544,10 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   a.act_stride = act_stride;
   a.act_width = act_width;
   if (info) a.info = *info;
-  HIP_OK(launch_system_step(S->L, S->mode, S->feat, S->gw, n_envs, step_lds(S), as_stream(stream), a));
+  if (S->mode == 1)
+    HIP_OK(launch_system_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
+  else
+    HIP_OK(launch_system_step_generic(S->L, S->mode, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
 }
 
@@ -538,7 +573,10 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   a.act = act;
   a.act_stride = act_stride;
   a.act_width = act_width;
-  HIP_OK(launch_env_step(S->L, S->mode, S->feat, S->gw, n_envs, step_lds(S), as_stream(stream), a));
+  if (S->mode == 1)
+    HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
+  else
+    HIP_OK(launch_env_step_generic(S->L, S->mode, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
 }
 

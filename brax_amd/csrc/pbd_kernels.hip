@@ -22,6 +22,11 @@
 #include "pbd_layout.h"
 #include "pbd_math.h"
 
+// in-kernel stamps exist in the fast (SINGLE-mode) translation unit only
+#if !defined(BX_TU_FAST)
+#undef BX_STAMPS
+#endif
+
 namespace bx {
 
 // ---------------------------------------------------------------------------
@@ -436,22 +441,17 @@ __device__ __forceinline__ RowC load_row(const Cst& c, const BlobHdr& H, int r) 
   return x;
 }
 
-// capsule_plane (colliders.py:744-759) / capsule_capsule (:805-819)
-template <int F>
-__device__ __forceinline__ void contact_gen(const RowC& R, const QP& a, const QP& b, v3& pos, v3& vel, v3& n,
-                            float& pen) {
-  if (is_plane<F>(R.fn)) {
-    v3 e = a.pos + rotate(R.a_end, a.rot);
-    n = rotate(mk(0.f, 0.f, 1.f), b.rot);
-    pos = e - n * R.a_rad;
-    vel = a.vel + cross(a.ang, pos - a.pos);
-    pen = dot(b.pos - pos, n);
-    return;
-  }
-  v3 pa = a.pos + rotate(R.a_pos, a.rot), ea = rotate(R.a_end, a.rot);
-  v3 pb = b.pos + rotate(R.b_pos, b.rot), eb = rotate(R.b_end, b.rot);
-  v3 a0 = pa + ea, a1 = pa - ea, b0 = pb + eb, b1 = pb - eb;
-  // _closest_segment_to_segment_points (geometry.py:394-451)
+// closest_segment_point_and_dist (geometry.py:360-374): returns dist^2
+__device__ __forceinline__ float seg_point(v3 a, v3 b, v3 pt, v3& out) {
+  v3 ab = b - a;
+  float t = clampf(dot(pt - a, ab) / (dot(ab, ab) + 1e-6f), 0.f, 1.f);
+  out = a + t * ab;
+  v3 v = pt - out;
+  return dot(v, v);
+}
+
+// _closest_segment_to_segment_points (geometry.py:394-451)
+__device__ __forceinline__ void seg_seg(v3 a0, v3 a1, v3 b0, v3 b1, v3& ba, v3& bb) {
   v3 da = a1 - a0;
   float la = safe_norm(da);
   la += 1e-6f * (float)(la == 0.f);
@@ -469,24 +469,185 @@ __device__ __forceinline__ void contact_gen(const RowC& R, const QP& a, const QP
   float ota = (-datr + dadb * dbtr) / (den + 1e-6f);
   float otb = dbtr + ota * dadb;
   float ta = clampf(ota, -hla, hla), tb = clampf(otb, -hlb, hlb);
-  v3 ba = am + da * ta, bb = bm + db * tb;
-  v3 ab = a1 - a0;
-  float t1 = clampf(dot(bb - a0, ab) / (dot(ab, ab) + 1e-6f), 0.f, 1.f);
-  v3 na = a0 + t1 * ab;
-  v3 va = bb - na;
-  float d1 = dot(va, va);
-  v3 bbv = b1 - b0;
-  float t2 = clampf(dot(ba - b0, bbv) / (dot(bbv, bbv) + 1e-6f), 0.f, 1.f);
-  v3 nb = b0 + t2 * bbv;
-  v3 vb = ba - nb;
-  float d2 = dot(vb, vb);
+  ba = am + da * ta;
+  bb = bm + db * tb;
+  v3 na, nb;
+  float d1 = seg_point(a0, a1, bb, na);
+  float d2 = seg_point(b0, b1, ba, nb);
   if (d1 < d2) ba = na; else bb = nb;
+}
+
+// capsule_plane (colliders.py:744-759) / capsule_capsule (:805-819)
+template <int F>
+__device__ __forceinline__ void contact_gen(const RowC& R, const QP& a, const QP& b, v3& pos, v3& vel, v3& n,
+                            float& pen) {
+  if (is_plane<F>(R.fn)) {
+    v3 e = a.pos + rotate(R.a_end, a.rot);
+    n = rotate(mk(0.f, 0.f, 1.f), b.rot);
+    pos = e - n * R.a_rad;
+    vel = a.vel + cross(a.ang, pos - a.pos);
+    pen = dot(b.pos - pos, n);
+    return;
+  }
+  v3 pa = a.pos + rotate(R.a_pos, a.rot), ea = rotate(R.a_end, a.rot);
+  v3 pb = b.pos + rotate(R.b_pos, b.rot), eb = rotate(R.b_end, b.rot);
+  v3 a0 = pa + ea, a1 = pa - ea, b0 = pb + eb, b1 = pb - eb;
+  v3 ba, bb;
+  seg_seg(a0, a1, b0, b1, ba, bb);
   v3 pv = ba - bb;
   float dist = safe_norm(pv);
   n = pv / (1e-6f + dist);
   pen = R.a_rad + R.b_rad - dist;
   pos = (ba + bb) / 2.f;
   vel = (a.vel + cross(a.ang, pos - a.pos)) - (b.vel + cross(b.ang, pos - b.pos));
+}
+
+// ---- extended contact functions (item-loop kernels only) -----------------
+
+__device__ __forceinline__ float pdiv(float a, float b) { return (float)((double)a / (double)b); }
+
+// box_heightmap, one box corner (colliders.py:699-739); height indices as
+// under jit: a negative index wraps once, then the gather clamps
+__device__ __noinline__ void heightmap_contact(const Cst& c, const BlobHdr& H, int o, const RowC& R,
+                                               const QP& a, const QP& b, v3& pos, v3& vel, v3& n,
+                                               float& pen) {
+  const float cell = c.f(o + R_X);
+  const int off = H.o_hm + c.i(o + R_HM_OFF), M = c.i(o + R_HM_M);
+  v3 r = rotate(R.a_end, a.rot);
+  pos = a.pos + r;
+  vel = a.vel + cross(a.ang, r);
+  v3 p = rotate(pos - b.pos, quat_inv(b.rot));
+  // the grid position and the tilted-triangle normal carry no later
+  // correction: divide correctly rounded here (the build's a * rcp(b) is ~1.5
+  // ulp; the double quotient rounds to the fp32 IEEE one)
+  float u = pdiv(p.x, cell), v = pdiv(p.y, cell);
+  float fu = floorf(u), fv = floorf(v);
+  int iu = (int)fu, iv = (int)fv;
+  bool lower = ((u - fu) + (v - fv)) < 1.f;
+  float mu = lower ? -1.f : 1.f;
+  int tu[3] = {iu + (lower ? 0 : 1), iu + (lower ? 1 : 0), iu + (lower ? 0 : 1)};
+  int tv[3] = {iv + (lower ? 0 : 1), iv + (lower ? 0 : 1), iv + (lower ? 1 : 0)};
+  float hh[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    int i = tu[k], j = -tv[k];
+    i += i < 0 ? M : 0;
+    j += j < 0 ? M : 0;
+    i = i < 0 ? 0 : (i >= M ? M - 1 : i);
+    j = j < 0 ? 0 : (j >= M ? M - 1 : j);
+    hh[k] = c.f(off + i * M + j);
+  }
+  v3 raw = mk(mu * (hh[1] - hh[0]), mu * (hh[2] - hh[0]), cell);
+  const float rn = safe_norm(raw);
+  v3 n0 = mk(pdiv(raw.x, rn), pdiv(raw.y, rn), pdiv(raw.z, rn));
+  v3 p0 = mk((float)tu[0] * cell, (float)tv[0] * cell, hh[0]);
+  pen = dot(p0 - p, n0);
+  n = rotate(n0, b.rot);
+}
+
+// capsule_clippedplane, one capsule end (colliders.py:762-802)
+__device__ __noinline__ void clipped_contact(const Cst& c, int o, const RowC& R, const QP& a,
+                                             const QP& b, v3& pos, v3& vel, v3& n, float& pen) {
+  v3 e = a.pos + rotate(R.a_end, a.rot);
+  v3 nb = rotate(c.f3(o + R_X), b.rot);
+  float ndir = dot(a.pos, nb) > 0.f ? 1.f : -1.f;
+  n = nb * ndir;
+  pos = e - n * R.a_rad;
+  vel = a.vel + cross(a.ang, pos - a.pos);
+  v3 pt = rotate(c.f3(o + R_X + 9), b.rot) + b.pos;
+  pen = dot(pt - pos, n);
+  v3 nx = rotate(c.f3(o + R_X + 3), b.rot), ny = rotate(c.f3(o + R_X + 6), b.rot);
+  const float hx = c.f(o + R_X + 12), hy = c.f(o + R_X + 13);
+  v3 nn = n * ndir;
+  v3 yn = cross(nn, nx), xn = -cross(nn, ny);
+  bool front = dot(pos - (pt + nx * hx), xn) > 1e-6f;
+  front |= dot(pos - (pt - nx * hx), -xn) > 1e-6f;
+  front |= dot(pos - (pt + ny * hy), yn) > 1e-6f;
+  front |= dot(pos - (pt - ny * hy), -yn) > 1e-6f;
+  if (front) pen = -1.f;
+}
+
+// closest_triangle_point (geometry.py:462-498)
+__device__ __forceinline__ v3 tri_point(v3 p0, v3 p1, v3 p2, v3 pt) {
+  v3 e0 = p1 - p0, e1 = p2 - p0, d = pt - p0;
+  float a = dot(e0, e0), bb = dot(e0, e1), cc = dot(e1, e1);
+  float det = a * cc - bb * bb;
+  float u = (cc * dot(e0, d) - bb * dot(e1, d)) / det;
+  float v = (-bb * dot(e0, d) + a * dot(e1, d)) / det;
+  bool inside = (0.f <= u) & (u <= 1.f) & (0.f <= v) & (v <= 1.f) & (u + v <= 1.f);
+  v3 cp = p0 + u * e0 + v * e1;
+  v3 w = cp - pt;
+  float d0 = dot(w, w);
+  v3 c1, c2, c3;
+  float d1 = seg_point(p0, p1, pt, c1);
+  bool use0 = (d0 < d1) & inside;
+  v3 best = use0 ? cp : c1;
+  float md = use0 ? d0 : d1;
+  float d2 = seg_point(p1, p2, pt, c2);
+  if (d2 < md) best = c2;
+  md = fminf(md, d2);
+  float d3 = seg_point(p2, p0, pt, c3);
+  if (d3 < md) best = c3;
+  return best;
+}
+
+// capsule_mesh, one triangle of a box / mesh (colliders.py:822-848) with
+// closest_segment_triangle_points (geometry.py:501-541)
+__device__ __noinline__ void capsule_mesh_contact(const Cst& c, int o, const RowC& R, const QP& a,
+                                                  const QP& b, v3& pos, v3& vel, v3& n,
+                                                  float& pen) {
+  v3 pa = a.pos + rotate(R.a_pos, a.rot), ea = rotate(R.a_end, a.rot);
+  v3 s0 = pa + ea, s1 = pa - ea;
+  v3 tn = rotate(c.f3(o + R_X + 9), b.rot);
+  v3 p0 = b.pos + rotate(c.f3(o + R_X), b.rot);
+  v3 p1 = b.pos + rotate(c.f3(o + R_X + 3), b.rot);
+  v3 p2 = b.pos + rotate(c.f3(o + R_X + 6), b.rot);
+  v3 sp[4], tp[4];
+  seg_seg(s0, s1, p0, p1, sp[0], tp[0]);
+  seg_seg(s0, s1, p1, p2, sp[1], tp[1]);
+  seg_seg(s0, s1, p0, p2, sp[2], tp[2]);
+  {  // closest_segment_point_plane (geometry.py:377-391)
+    v3 ab = s1 - s0;
+    float t = (dot(p0, tn) - dot(tn, s0)) / (dot(tn, ab) + 1e-6f);
+    sp[3] = s0 + clampf(t, 0.f, 1.f) * ab;
+  }
+  tp[3] = tri_point(p0, p1, p2, sp[3]);
+  float dd[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    v3 w = sp[i] - tp[i];
+    dd[i] = dot(w, w);
+  }
+  float md = fminf(fminf(dd[0], dd[1]), fminf(dd[2], dd[3]));
+  v3 ss = mk(0.f, 0.f, 0.f), ts = mk(0.f, 0.f, 0.f);
+  float cnt = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    float m = dd[i] == md ? 1.f : 0.f;
+    ss = ss + sp[i] * m;
+    ts = ts + tp[i] * m;
+    cnt += m;
+  }
+  ss = ss / cnt;
+  ts = ts / cnt;
+  v3 pv = ss - ts;
+  float dist = safe_norm(pv);
+  n = pv / (1e-6f + dist);
+  pen = R.a_rad - dist;
+  pos = ts;
+  vel = (a.vel + cross(a.ang, pos - a.pos)) - (b.vel + cross(b.ang, pos - b.pos));
+}
+
+// every contact function of row r (the item-loop kernels)
+template <int F>
+__device__ __forceinline__ void contact_gen_x(const Cst& c, const BlobHdr& H, int r, const RowC& R,
+                                              const QP& a, const QP& b, v3& pos, v3& vel, v3& n,
+                                              float& pen) {
+  const int o = H.o_row + r * ROW_STRIDE;
+  if (R.fn == BX_COL_HEIGHTMAP) heightmap_contact(c, H, o, R, a, b, pos, vel, n, pen);
+  else if (R.fn == BX_COL_CLIPPED_PLANE) clipped_contact(c, o, R, a, b, pos, vel, n, pen);
+  else if (R.fn == BX_COL_CAPSULE_MESH) capsule_mesh_contact(c, o, R, a, b, pos, vel, n, pen);
+  else contact_gen<F>(R, a, b, pos, vel, n, pen);
 }
 
 // One/TwoWay._position_contact (colliders.py:306-377, 495-580)
@@ -906,8 +1067,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         v3 am = mul(q.ang, B.rm);
         q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
         q4 r = q.rot + quat_mul(hq, q.rot);
-        float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
-        q.rot = q4{r.w / rn, r.x / rn, r.y / rn, r.z / rn};
+        q.rot = qnormalize(r);
         stqp(E.qp + b * QP_STRIDE, q);
         if (sub == 1) st3(E.acc + b * ACC_STRIDE + ACC_DPA, dpa);
       }
@@ -945,8 +1105,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
           const float* pv = E.prev + b * PREV_STRIDE;
           v3 ppos = ld3(pv);
           q4 prot = ld4(pv + 3);
-          float rn = sqrtf(q.rot.w * q.rot.w + q.rot.x * q.rot.x + q.rot.y * q.rot.y + q.rot.z * q.rot.z);
-          q4 nr{q.rot.w / rn, q.rot.x / rn, q.rot.y / rn, q.rot.z / rn};
+          q4 nr = qnormalize(q.rot);
           q.vel = mul((q.pos - ppos) / h, B.pm);
           q4 dq = quat_mul(nr, quat_inv(prot));
           v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
@@ -967,7 +1126,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cpos, cvel, n;
       float pen;
-      contact_gen<F_ALL>(R, a, b, cpos, cvel, n, pen);
+      contact_gen_x<F_ALL>(c, H, r, R, a, b, cpos, cvel, n, pen);
       const float* pa = E.prev + R.a * PREV_STRIDE;
       const float* pb = E.prev + R.b * PREV_STRIDE;
       v3 oap, obp;
@@ -1015,8 +1174,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       const float* pv = E.prev + b * PREV_STRIDE;
       v3 ppos = ld3(pv);
       q4 prot = ld4(pv + 3);
-      float rn = sqrtf(q.rot.w * q.rot.w + q.rot.x * q.rot.x + q.rot.y * q.rot.y + q.rot.z * q.rot.z);
-      q4 nr{q.rot.w / rn, q.rot.x / rn, q.rot.y / rn, q.rot.z / rn};
+      q4 nr = qnormalize(q.rot);
       q.vel = mul((q.pos - ppos) / h, B.pm);
       q4 dq = quat_mul(nr, quat_inv(prot));
       v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
@@ -1088,7 +1246,7 @@ __device__ void impulse_rows(const Cst& c, const BlobHdr& H, const Env& E, int l
     QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
     v3 cpos, cvel, n;
     float pen;
-    contact_gen<F_ALL>(R, a, b, cpos, cvel, n, pen);
+    contact_gen_x<F_ALL>(c, H, r, R, a, b, cpos, cvel, n, pen);
     v3 oav, oaa, obv, oba;
     impulse_contact<F_ALL>(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
     float* rd = E.rowd + r * ROWD_STRIDE;
@@ -1152,8 +1310,7 @@ __device__ void spring_step(const Cst& c, const BlobHdr& H, const Env& E, int la
       v3 am = mul(q.ang, B.rm);
       q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
       q4 r = q.rot + quat_mul(hq, q.rot);
-      float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
-      q.rot = q4{r.w / rn, r.x / rn, r.y / rn, r.z / rn};
+      q.rot = qnormalize(r);
       stqp(E.qp + b * QP_STRIDE, q);
     }
     sync();
@@ -1332,8 +1489,7 @@ __device__ __forceinline__ void gsum_contact(const GList<M>& g, const float* csl
 
 // Euler.velocity_projection (integrators.py:122-146) on one body
 __device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, float h) {
-  float rn = sqrtf(q.rot.w * q.rot.w + q.rot.x * q.rot.x + q.rot.y * q.rot.y + q.rot.z * q.rot.z);
-  q4 nr{q.rot.w / rn, q.rot.x / rn, q.rot.y / rn, q.rot.z / rn};
+  q4 nr = qnormalize(q.rot);
   q.vel = mul((q.pos - ppos) / h, B.pm);
   q4 dq = quat_mul(nr, quat_inv(prot));
   v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
@@ -1447,8 +1603,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         v3 am = mul(q.ang, X.B.rm);
         q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
         q4 r = q.rot + quat_mul(hq, q.rot);
-        float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
-        q.rot = q4{r.w / rn, r.x / rn, r.y / rn, r.z / rn};
+        q.rot = qnormalize(r);
         stqp(myqp, q);
         dpa_last = dpa;
       }
@@ -1590,7 +1745,7 @@ __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane)
     QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
     v3 cpos, cvel, n;
     float pen;
-    contact_gen<F_ALL>(R, a, b, cpos, cvel, n, pen);
+    contact_gen_x<F_ALL>(c, H, r, R, a, b, cpos, cvel, n, pen);
     v3 oav, oaa, obv, oba;
     impulse_contact<F_ALL>(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
     float* sa = E.cslot + r * SLOT_STRIDE;
@@ -1788,7 +1943,7 @@ __device__ __forceinline__ float* stage_constants(const uint32_t* blob, const Bl
                                                   float* smem, Cst& c) {
   if constexpr (MODE == MODE_LDS) {
     uint32_t* cl = reinterpret_cast<uint32_t*>(smem);
-    for (int i = threadIdx.x; i < H.const_words; i += 64) cl[i] = blob[i];
+    for (int i = threadIdx.x; i < H.const_words; i += blockDim.x) cl[i] = blob[i];
     __syncthreads();
     c.w = cl;
     return smem + H.const_words;
@@ -1807,7 +1962,7 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
   constexpr bool S = MODE == MODE_SINGLE;
   const int lane = threadIdx.x % L;
   const int le = threadIdx.x / L;
-  const int64_t e = (int64_t)blockIdx.x * (64 / L) + le;
+  const int64_t e = (int64_t)blockIdx.x * (blockDim.x / L) + le;
   const bool valid = e < A.n_envs;
   Env E = carve(ebase + le * H.env_words, H);
   zero_slots(E, H, lane);
@@ -1888,7 +2043,7 @@ __global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
   constexpr bool S = MODE == MODE_SINGLE;
   const int lane = threadIdx.x % L;
   const int le = threadIdx.x / L;
-  const int64_t e = (int64_t)blockIdx.x * (64 / L) + le;
+  const int64_t e = (int64_t)blockIdx.x * (blockDim.x / L) + le;
   const bool valid = e < A.n_envs;
   Env E = carve(ebase + le * H.env_words, H);
   zero_slots(E, H, lane);
@@ -2045,7 +2200,7 @@ __global__ void __launch_bounds__(64) info_obs_kernel(InfoArgs A) {
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
   const int lane = threadIdx.x % L;
   const int le = threadIdx.x / L;
-  const int64_t e = (int64_t)blockIdx.x * (64 / L) + le;
+  const int64_t e = (int64_t)blockIdx.x * (blockDim.x / L) + le;
   const bool valid = e < A.n_envs;
   Env E = carve(smem + le * H.env_words, H);
   if (valid) {
@@ -2092,6 +2247,7 @@ __global__ void __launch_bounds__(64) info_obs_kernel(InfoArgs A) {
 // System.default_qp (system.py:112-242): one thread per env (reset path)
 
 
+#if !defined(BX_TU_FAST)  // reset / RNG kernels: IEEE translation unit
 __global__ void __launch_bounds__(64) default_qp_kernel(ResetArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Cst c{A.blob};
@@ -2135,7 +2291,7 @@ __global__ void __launch_bounds__(64) default_qp_kernel(ResetArgs A) {
   }
   // bodies.min_z per root group, then lift (system.py:213-240)
   for (int g = 0; g < H.n_root_groups; g++) {
-    float zmin = 3.4028235e38f;  // finite-math build: no inf literals
+    float zmin = 3.4028235e38f;
     for (int b = 0; b < N; b++) {
       if (c.i(H.o_rgroup + b) != g) continue;
       float bz = 3.4028235e38f;
@@ -2171,6 +2327,8 @@ __global__ void uniform_kernel(float* out, int64_t n, uint64_t seed, uint64_t of
   out[i] = lo + (hi - lo) * u;
 }
 
+#endif
+
 }  // namespace bx
 
 // ---------------------------------------------------------------------------
@@ -2179,50 +2337,93 @@ __global__ void uniform_kernel(float* out, int64_t n, uint64_t seed, uint64_t of
 namespace bx {
 
 template <typename Args>
-static void launch_one(void (*k)(Args), dim3 grid, size_t lds, hipStream_t s, const Args& a) {
+static void launch_one(void (*k)(Args), dim3 grid, int tpb, size_t lds, hipStream_t s, const Args& a) {
+  // tpb threads per workgroup (a multiple of L, <= 64): 64 / L envs share a
+  // wavefront by default; 32 halves that (twice the waves for one batch)
   if (lds > 65536) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k, grid, dim3(64), lds, s, a);
+  hipLaunchKernelGGL(k, grid, dim3(tpb), lds, s, a);
 }
 
-// instantiated variants: (lanes, mode, features, gather width). Single mode
-// at 16 lanes is specialised per feature set and gather width; everything
-// else carries all features.
+// instantiated variants: (lanes, mode, features, gather width). This file is
+// compiled twice (Makefile): BX_TU_FAST holds the register-hoisted SINGLE-mode
+// kernels, built with fast reciprocal division; BX_TU_GENERIC holds the
+// item-loop kernels (large scenes, legacy_spring, the extended contact
+// functions) and the reset / info kernels, built with IEEE division. Single
+// mode at 16 lanes is specialised per feature set and gather width;
+// everything else carries all features.
 #define BX_SINGLE16(KERNEL, ARGS, M)                                                \
   switch (feat) {                                                                   \
-    case 0: launch_one<ARGS>(KERNEL<16, 1, 0, M>, grid, lds, s, a); break;          \
-    case F_SPH: launch_one<ARGS>(KERNEL<16, 1, F_SPH, M>, grid, lds, s, a); break;  \
-    case F_CC | F_TW: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW, M>, grid, lds, s, a); break; \
-    default: launch_one<ARGS>(KERNEL<16, 1, F_ALL, M>, grid, lds, s, a); break;     \
+    case 0: launch_one<ARGS>(KERNEL<16, 1, 0, M>, grid, tpb, lds, s, a); break;     \
+    case F_SPH: launch_one<ARGS>(KERNEL<16, 1, F_SPH, M>, grid, tpb, lds, s, a); break; \
+    case F_CC | F_TW: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW, M>, grid, tpb, lds, s, a); break; \
+    default: launch_one<ARGS>(KERNEL<16, 1, F_ALL, M>, grid, tpb, lds, s, a); break; \
   }
-#define BX_DISPATCH(KERNEL, ARGS)                                                   \
-  if (mode == 1 && L == 16) {                                                       \
+#define BX_DISPATCH_SINGLE(KERNEL, ARGS)                                            \
+  if (L == 16) {                                                                    \
     if (gw <= 4) { BX_SINGLE16(KERNEL, ARGS, 4) } else { BX_SINGLE16(KERNEL, ARGS, 8) } \
+  } else if (L == 32) {                                                             \
+    launch_one<ARGS>(KERNEL<32, 1, F_ALL, 8>, grid, tpb, lds, s, a);                \
   } else {                                                                          \
-    switch (L * 4 + mode) {                                                         \
-      case 16 * 4 + 0: launch_one<ARGS>(KERNEL<16, 0, F_ALL, 8>, grid, lds, s, a); break; \
-      case 16 * 4 + 2: launch_one<ARGS>(KERNEL<16, 2, F_ALL, 8>, grid, lds, s, a); break; \
-      case 32 * 4 + 0: launch_one<ARGS>(KERNEL<32, 0, F_ALL, 8>, grid, lds, s, a); break; \
-      case 32 * 4 + 1: launch_one<ARGS>(KERNEL<32, 1, F_ALL, 8>, grid, lds, s, a); break; \
-      case 32 * 4 + 2: launch_one<ARGS>(KERNEL<32, 2, F_ALL, 8>, grid, lds, s, a); break; \
-      case 64 * 4 + 0: launch_one<ARGS>(KERNEL<64, 0, F_ALL, 8>, grid, lds, s, a); break; \
-      case 64 * 4 + 1: launch_one<ARGS>(KERNEL<64, 1, F_ALL, 8>, grid, lds, s, a); break; \
-      case 64 * 4 + 2: launch_one<ARGS>(KERNEL<64, 2, F_ALL, 8>, grid, lds, s, a); break; \
-      default: return hipErrorInvalidValue;                                         \
-    }                                                                               \
+    launch_one<ARGS>(KERNEL<64, 1, F_ALL, 8>, grid, tpb, lds, s, a);                \
+  }
+#define BX_DISPATCH_GENERIC(KERNEL, ARGS)                                           \
+  switch (L * 4 + mode) {                                                           \
+    case 16 * 4 + 0: launch_one<ARGS>(KERNEL<16, 0, F_ALL, 8>, grid, tpb, lds, s, a); break; \
+    case 16 * 4 + 2: launch_one<ARGS>(KERNEL<16, 2, F_ALL, 8>, grid, tpb, lds, s, a); break; \
+    case 32 * 4 + 0: launch_one<ARGS>(KERNEL<32, 0, F_ALL, 8>, grid, tpb, lds, s, a); break; \
+    case 32 * 4 + 2: launch_one<ARGS>(KERNEL<32, 2, F_ALL, 8>, grid, tpb, lds, s, a); break; \
+    case 64 * 4 + 0: launch_one<ARGS>(KERNEL<64, 0, F_ALL, 8>, grid, tpb, lds, s, a); break; \
+    case 64 * 4 + 2: launch_one<ARGS>(KERNEL<64, 2, F_ALL, 8>, grid, tpb, lds, s, a); break; \
+    default: return hipErrorInvalidValue;                                           \
   }
 
-hipError_t launch_system_step(int L, int mode, int feat, int gw, int64_t n_envs, size_t lds, hipStream_t s,
-                              const StepArgs& a) {
-  int epb = 64 / L;
+#if defined(BX_TU_FAST)
+hipError_t launch_system_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
+                                     hipStream_t s, const StepArgs& a) {
+  const int epb = tpb / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
-  BX_DISPATCH(system_step_kernel, StepArgs)
+  BX_DISPATCH_SINGLE(system_step_kernel, StepArgs)
   return hipGetLastError();
 }
-hipError_t launch_env_step(int L, int mode, int feat, int gw, int64_t n_envs, size_t lds, hipStream_t s,
-                           const EnvArgs& a) {
-  int epb = 64 / L;
+hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
+                                  hipStream_t s, const EnvArgs& a) {
+  const int epb = tpb / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
-  BX_DISPATCH(env_step_kernel, EnvArgs)
+  BX_DISPATCH_SINGLE(env_step_kernel, EnvArgs)
+  return hipGetLastError();
+}
+hipError_t debug_stamps(unsigned long long* out, int reset) {
+#ifdef BX_STAMPS
+  static unsigned long long host[4096][16];
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(bx_stamp_wave), sizeof(host));
+  for (int k = 0; k < 16; k++) {
+    out[k] = 0;
+    for (int w = 0; w < 4096; w++) out[k] += host[w][k];
+  }
+  if (e == hipSuccess && reset) {
+    memset(host, 0, sizeof(host));
+    e = hipMemcpyToSymbol(HIP_SYMBOL(bx_stamp_wave), host, sizeof(host));
+  }
+  return e;
+#else
+  (void)out;
+  (void)reset;
+  return hipErrorNotSupported;
+#endif
+}
+#else
+hipError_t launch_system_step_generic(int L, int mode, int tpb, int64_t n_envs, size_t lds,
+                                      hipStream_t s, const StepArgs& a) {
+  const int epb = tpb / L;
+  dim3 grid((unsigned)((n_envs + epb - 1) / epb));
+  BX_DISPATCH_GENERIC(system_step_kernel, StepArgs)
+  return hipGetLastError();
+}
+hipError_t launch_env_step_generic(int L, int mode, int tpb, int64_t n_envs, size_t lds,
+                                   hipStream_t s, const EnvArgs& a) {
+  const int epb = tpb / L;
+  dim3 grid((unsigned)((n_envs + epb - 1) / epb));
+  BX_DISPATCH_GENERIC(env_step_kernel, EnvArgs)
   return hipGetLastError();
 }
 hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a) {
@@ -2246,24 +2447,6 @@ hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
   return hipGetLastError();
 }
 
-hipError_t debug_stamps(unsigned long long* out, int reset) {
-#ifdef BX_STAMPS
-  static unsigned long long host[4096][16];
-  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(bx_stamp_wave), sizeof(host));
-  for (int k = 0; k < 16; k++) {
-    out[k] = 0;
-    for (int w = 0; w < 4096; w++) out[k] += host[w][k];
-  }
-  if (e == hipSuccess && reset) {
-    memset(host, 0, sizeof(host));
-    e = hipMemcpyToSymbol(HIP_SYMBOL(bx_stamp_wave), host, sizeof(host));
-  }
-  return e;
-#else
-  (void)out;
-  (void)reset;
-  return hipErrorNotSupported;
-#endif
-}
+#endif  // BX_TU_FAST
 
 }  // namespace bx

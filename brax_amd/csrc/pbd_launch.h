@@ -43,8 +43,16 @@ struct ResetArgs {
   bx_qp out;
 };
 
-hipError_t launch_system_step(int L, int mode, int feat, int gw, int64_t n_envs, size_t lds, hipStream_t s, const StepArgs& a);
-hipError_t launch_env_step(int L, int mode, int feat, int gw, int64_t n_envs, size_t lds, hipStream_t s, const EnvArgs& a);
+// SINGLE-mode step kernels (fast-reciprocal translation unit)
+hipError_t launch_system_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
+                                     hipStream_t s, const StepArgs& a);
+hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
+                                  hipStream_t s, const EnvArgs& a);
+// item-loop step kernels (IEEE-division translation unit)
+hipError_t launch_system_step_generic(int L, int mode, int tpb, int64_t n_envs, size_t lds,
+                                      hipStream_t s, const StepArgs& a);
+hipError_t launch_env_step_generic(int L, int mode, int tpb, int64_t n_envs, size_t lds,
+                                   hipStream_t s, const EnvArgs& a);
 hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a);
 hipError_t launch_default_qp(int64_t n_envs, size_t lds, hipStream_t s, const ResetArgs& a);
 hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset, float lo, float hi,

@@ -29,10 +29,13 @@ enum { GROUP_STRIDE = 4, G_CUT = 0, G_R0 = 1, G_R1 = 2, G_INFO = 3 };
 // forces (forces.py): Thrusters first, then Twisters (application order)
 enum { FORCE_STRIDE = 8, F_TYPE = 0, F_BODY = 1, F_IDX = 2, F_STR = 5, F_MASS = 6 };
 enum {
-  ROW_STRIDE = 32,
+  ROW_STRIDE = 48,
   R_GROUP = 0, R_A = 1, R_B = 2, R_FN = 3, R_ONEWAY = 4, R_APOS = 5, R_AEND = 8, R_ARAD = 11,
   R_BPOS = 12, R_BEND = 15, R_BRAD = 18, R_FRIC = 19, R_ELAS = 20, R_SCALE = 21, R_THR = 22,
   R_ERP = 23,
+  // extended contact functions (bx_desc row_ext): 16 floats, then the height
+  // map's word offset (from o_hm) and mesh size
+  R_X = 24, R_HM_OFF = 40, R_HM_M = 41,
 };
 enum {
   FK_STRIDE = 24,
@@ -77,6 +80,7 @@ struct BlobHdr {
   int32_t l_ract;                    // LDS: per-row NearNeighbors rank (-1 = culled)
   int32_t l_alist;                   // LDS: active rows in Info order (info_rows)
   int32_t spring;                    // dynamics_mode == legacy_spring
+  int32_t o_hm;                      // height map grids
 };
 
 }  // namespace bx

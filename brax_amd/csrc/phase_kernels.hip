@@ -89,9 +89,9 @@ __global__ void __launch_bounds__(256) kinetic_kernel(PhaseArgs A) {
       v3 am = mul(ang, rm);
       q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
       q4 r = rot + quat_mul(hq, rot);
-      float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
+      q4 nr = qnormalize(r);
       o[0].v[l] = pos.x; o[1].v[l] = pos.y; o[2].v[l] = pos.z;
-      o[3].v[l] = r.w / rn; o[4].v[l] = r.x / rn; o[5].v[l] = r.y / rn; o[6].v[l] = r.z / rn;
+      o[3].v[l] = nr.w; o[4].v[l] = nr.x; o[5].v[l] = nr.y; o[6].v[l] = nr.z;
     }
 #pragma unroll
     for (int k = 0; k < 7; k++) st4nt(A.out + k * A.plane + i, o[k]);
@@ -156,8 +156,7 @@ __global__ void __launch_bounds__(256) vproj_kernel(PhaseArgs A) {
       q4 rot{s[3].v[l], s[4].v[l], s[5].v[l], s[6].v[l]};
       v3 ppos = mk(p[0].v[l], p[1].v[l], p[2].v[l]);
       q4 prot{p[3].v[l], p[4].v[l], p[5].v[l], p[6].v[l]};
-      float rn = sqrtf(rot.w * rot.w + rot.x * rot.x + rot.y * rot.y + rot.z * rot.z);
-      q4 nr{rot.w / rn, rot.x / rn, rot.y / rn, rot.z / rn};
+      q4 nr = qnormalize(rot);
       v3 vel = mul((pos - ppos) / h, pm);
       q4 dq = quat_mul(nr, quat_inv(prot));
       v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;

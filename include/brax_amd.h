@@ -41,7 +41,11 @@ enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
 /* dynamics modes (config.proto dynamics_mode; system.py:244-247) */
 enum { BX_DYN_PBD = 0, BX_DYN_LEGACY_SPRING = 1 };
 enum { BX_ACT_TORQUE = 0, BX_ACT_ANGLE = 1 };
-enum { BX_COL_CAPSULE_PLANE = 0, BX_COL_CAPSULE_CAPSULE = 1 };
+enum { BX_COL_CAPSULE_PLANE = 0, BX_COL_CAPSULE_CAPSULE = 1,
+       /* box corner vs height map (colliders.py:699-739), capsule end vs
+        * clipped plane (:762-802), capsule vs one triangle of a box / mesh
+        * (:822-848) */
+       BX_COL_HEIGHTMAP = 2, BX_COL_CLIPPED_PLANE = 3, BX_COL_CAPSULE_MESH = 4 };
 enum { BX_FORCE_THRUSTER = 0, BX_FORCE_TWISTER = 1 };
 /* env layer kinds (obs / reward programs) */
 enum { BX_ENV_NONE = 0, BX_ENV_ANT = 1, BX_ENV_HUMANOID = 2, BX_ENV_HALFCHEETAH = 3,
@@ -127,6 +131,17 @@ typedef struct bx_desc {
   const double* joint_stiffness;       /* [J] */
   const double* joint_spring_damping;  /* [J] (default: 0.5 or 2 x sqrt(stiffness)) */
   const double* joint_limit_strength;  /* [J] (default: stiffness) */
+  /* extended contact functions: per-row constants (may be NULL when no row
+   * uses them)
+   *   HEIGHTMAP:     ext[0] cell size; row_hm (offset into hm_data, mesh size)
+   *   CLIPPED_PLANE: ext normal 0..2, x 3..5, y 6..8, position 9..11,
+   *                  half sizes 12, 13 (b's body frame)
+   *   CAPSULE_MESH:  ext triangle p0 0..2, p1 3..5, p2 6..8, normal 9..11
+   *                  (b's body frame, winding fixed as geometry.py:138-154) */
+  const double* row_ext;           /* [R,16] */
+  const int32_t* row_hm;           /* [R,2] */
+  int32_t n_hm;
+  const double* hm_data;           /* [n_hm] row-major square grids */
 } bx_desc;
 
 /*
@@ -232,6 +247,12 @@ int bx_system_set_single(bx_system* sys, int on);
  * constant placement (0: read from HBM in the loops, 1: hoisted to registers,
  * needs <= 1 item per lane, 2: staged in LDS once per workgroup). */
 int bx_system_set_variant(bx_system* sys, int lanes, int mode);
+
+/* Threads per workgroup of the step kernels: a multiple of the lanes per env,
+ * at most 64 (default 64, i.e. 64 / lanes envs per wavefront). Fewer envs per
+ * wave means more waves for the same batch (32: two waves per SIMD at 4096
+ * Ant envs). Results are identical bit for bit. */
+int bx_system_set_block(bx_system* sys, int threads);
 
 /* Physics only: B independent System.step calls (system.py:244-325).
  * act: (B, act_width) with row stride act_stride (0 broadcasts one row).

@@ -163,7 +163,9 @@ def dump_desc(sys_):
 
   goneway, gfn, gscale, gthr, gerp = [], [], [], [], []
   rows = {k: [] for k in ('group', 'body_a', 'body_b', 'a_pos', 'a_end', 'a_radius',
-                          'b_pos', 'b_end', 'b_radius', 'friction', 'elasticity', 'flat')}
+                          'b_pos', 'b_end', 'b_radius', 'friction', 'elasticity', 'flat',
+                          'ext', 'hm')}
+  hm_data = []
   gcut = []
   for g, c in enumerate(sys_.colliders):
     if isinstance(c.cull, rc.NearNeighbors):
@@ -185,26 +187,47 @@ def dump_desc(sys_):
     goneway.append(1 if isinstance(c, rc.OneWayCollider) else 0)
     fn = c.contact_fn.__name__
     gfn.append({'capsule_plane': 0, 'capsule_capsule': 1, 'box_plane': 0,
-                'mesh_plane': 0}[fn])
+                'mesh_plane': 0, 'box_heightmap': 2, 'capsule_clippedplane': 3,
+                'capsule_mesh': 4}[fn])
     gscale.append(c.collide_scale)
     gthr.append(c.velocity_threshold)
     gerp.append(c.baumgarte_erp)
     P = len(ca.body.idx)
     for p in range(P):
-      if fn == 'box_plane':
-        ends = list(ca.corner[p])  # point-plane rows, zero radius
+      ext = None
+      hm = (-1, 0)
+      if fn in ('box_plane', 'box_heightmap'):
+        ends = list(ca.corner[p])  # corner rows, zero radius
+        if fn == 'box_heightmap':
+          hm = (len(hm_data), int(cb.height[p].shape[0]))
+          hm_data.extend(np.asarray(cb.height[p], np.float64).reshape(-1).tolist())
+          ext = [np.r_[cb.cell_size[p], np.zeros(15)]] * len(ends)
       elif fn == 'mesh_plane':
         ends = list(ca.vertices[p])
+      elif fn == 'capsule_mesh':
+        F = cb.faces[p].shape[0]
+        ends = [ca.end[p]] * F
+        ext = [np.r_[np.asarray(cb.faces[p][f]).reshape(-1), cb.face_normals[p][f], np.zeros(4)]
+               for f in range(F)]
+      elif fn == 'capsule_clippedplane':
+        ends = list(ca.end[p])
+        ext = [np.r_[cb.normal[p], cb.x[p], cb.y[p], cb.pos[p], cb.halfsize_x[p],
+                     cb.halfsize_y[p], np.zeros(2)]] * len(ends)
       else:
         ends = [ca.end[p]] if fn == 'capsule_capsule' else list(ca.end[p])
-      for e in ends:
+      if ext is None:
+        ext = [np.zeros(16)] * len(ends)
+      for ei, e in enumerate(ends):
+        rows['ext'].append(ext[ei])
+        rows['hm'].append(hm)
         rows['flat'].append(-1 if flats is None else int(flats[p]))
         rows['group'].append(g)
         rows['body_a'].append(ca.body.idx[p])
         rows['body_b'].append(cb.body.idx[p])
         rows['a_pos'].append(ca.pos[p])
         rows['a_end'].append(e)
-        rows['a_radius'].append(ca.radius[p] if fn not in ('box_plane', 'mesh_plane') else 0.)
+        rows['a_radius'].append(ca.radius[p] if fn not in ('box_plane', 'mesh_plane',
+                                                           'box_heightmap') else 0.)
         rows['b_pos'].append(cb.pos[p])
         rows['b_end'].append(cb.end[p] if fn == 'capsule_capsule' else np.zeros(3))
         rows['b_radius'].append(cb.radius[p] if fn == 'capsule_capsule' else 0.)
@@ -216,6 +239,9 @@ def dump_desc(sys_):
   d['col_scale'] = np.asarray(gscale, np.float64)
   d['col_velocity_threshold'] = np.asarray(gthr, np.float64)
   d['col_baumgarte_erp'] = np.asarray(gerp, np.float64)
+  d['row_ext'] = np.asarray(rows.pop('ext'), np.float64).reshape(-1, 16)
+  d['row_hm'] = np.asarray(rows.pop('hm'), np.int32).reshape(-1, 2)
+  d['hm_data'] = np.asarray(hm_data, np.float64)
   ints = ('group', 'body_a', 'body_b', 'flat')
   for k, v in rows.items():
     if k in ints:
@@ -587,6 +613,11 @@ def main():
       'box_slide': (scenes.BOX_TEST_CONFIG, 1, 1),
       'mesh_ground': (scenes.mesh_test_config(), 0, 30),
       'mesh_tilt': (scenes.mesh_test_config(), 1, 12),
+      # extended contact functions (colliders.py:699-739, 762-802, 822-848)
+      'heightmap': (scenes.heightmap_config(0.05, 10), 1, 8),
+      'clipped': (scenes.clipped_plane_config(0.05, 10), 1, 8),
+      'box_capsule': (scenes.BOX_CAPSULE_NO_HULL_CONFIG, 1, 4),
+      'mesh_capsule': (scenes.mesh_capsule_config(), 0, 8),
   }
   for name, (txt, di, T) in point_scenes.items():
     if want(name):

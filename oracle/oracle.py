@@ -48,9 +48,11 @@ def _p(a):
 class Oracle:
   """C restatement at float64 (checker) or float32 (CPU baseline)."""
 
-  def __init__(self, desc, reset_desc=None, dtype=np.float64, safe_guard=True):
+  def __init__(self, desc, reset_desc=None, dtype=np.float64, safe_guard=True, fma=False):
+    """fma=True (float32 only): the build with a*b+c contracted to fused
+    multiply-adds, as XLA's jit and hipcc contract them."""
     self.dtype = np.dtype(dtype)
-    self.suf = '_f64' if self.dtype == np.float64 else '_f32'
+    self.suf = '_f64' if self.dtype == np.float64 else ('_f32fma' if fma else '_f32')
     self.desc = dict(desc)
     self.cdesc, self._keep = abi.make_desc(self.desc)
     self.N = int(desc['n_bodies'])

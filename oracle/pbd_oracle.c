@@ -142,6 +142,7 @@ typedef struct {
   R *astr;
   R *gscale, *gthr, *gerp;
   R *ra_pos, *ra_end, *ra_rad, *rb_pos, *rb_end, *rb_rad, *rfric, *relas;
+  R *rext, *hm;  /* extended contact functions: row constants (R,16), heightmaps */
 } sysc;
 
 static R* cvt(const double* s, int n) {
@@ -196,6 +197,8 @@ static void sys_init(sysc* s, const bx_desc* d) {
   s->rb_rad = cvt(d->row_b_radius, Rn);
   s->rfric = cvt(d->row_friction, Rn);
   s->relas = cvt(d->row_elasticity, Rn);
+  s->rext = cvt(d->row_ext, 16 * Rn);
+  s->hm = cvt(d->hm_data, d->n_hm);
 }
 
 static void sys_free(sysc* s) {
@@ -204,7 +207,7 @@ static void sys_free(sysc* s) {
              &s->jsp, &s->jsa, &s->astr, &s->gscale, &s->gthr, &s->gerp,
              &s->ra_pos, &s->ra_end, &s->ra_rad, &s->rb_pos, &s->rb_end,
              &s->rb_rad, &s->rfric, &s->relas, &s->fstr, &s->fmass,
-             &s->jstiff, &s->jsdamp, &s->jlstr};
+             &s->jstiff, &s->jsdamp, &s->jlstr, &s->rext, &s->hm};
   for (size_t i = 0; i < sizeof(p) / sizeof(p[0]); i++) free(*p[i]);
 }
 
@@ -669,12 +672,231 @@ static void velocity_projection(const sysc* s, work_t* w, const body_t* prev) {
 
 /* ----------------------------------------------------------- colliders --- */
 
-/* capsule_plane (colliders.py:744-759) / capsule_capsule (:805-819) */
+/* closest_segment_point_and_dist (geometry.py:360-374) */
+static R seg_point(const R* a, const R* b, const R* pt, R* out) {
+  R ab[3], t[3], v[3];
+  for (int k = 0; k < 3; k++) { ab[k] = b[k] - a[k]; t[k] = pt[k] - a[k]; }
+  R tt = dot3(t, ab) / (dot3(ab, ab) + (R)1e-6);
+  tt = clip(tt, 0, 1);
+  for (int k = 0; k < 3; k++) { out[k] = a[k] + tt * ab[k]; v[k] = pt[k] - out[k]; }
+  return dot3(v, v);
+}
+
+/* _closest_segment_to_segment_points (geometry.py:394-451) */
+static void seg_seg(const R* a0, const R* a1, const R* b0, const R* b1, R* ba, R* bb) {
+  R da[3], db[3];
+  for (int k = 0; k < 3; k++) { da[k] = a1[k] - a0[k]; db[k] = b1[k] - b0[k]; }
+  R la = safe_norm3(da);
+  la += (R)1e-6 * (R)(la == 0);
+  for (int k = 0; k < 3; k++) da[k] /= la;
+  R hla = la * (R)0.5;
+  R lb = safe_norm3(db);
+  lb += (R)1e-6 * (R)(lb == 0);
+  for (int k = 0; k < 3; k++) db[k] /= lb;
+  R hlb = lb * (R)0.5;
+  R am[3], bm[3], tr[3];
+  for (int k = 0; k < 3; k++) {
+    am[k] = a0[k] + da[k] * hla;
+    bm[k] = b0[k] + db[k] * hlb;
+    tr[k] = am[k] - bm[k];
+  }
+  R dadb = dot3(da, db), datr = dot3(da, tr), dbtr = dot3(db, tr);
+  R den = 1 - dadb * dadb;
+  R ota = (-datr + dadb * dbtr) / (den + (R)1e-6);
+  R otb = dbtr + ota * dadb;
+  R ta = clip(ota, -hla, hla), tb = clip(otb, -hlb, hlb);
+  for (int k = 0; k < 3; k++) { ba[k] = am[k] + da[k] * ta; bb[k] = bm[k] + db[k] * tb; }
+  R na[3], nb[3];
+  R d1 = seg_point(a0, a1, bb, na);
+  R d2 = seg_point(b0, b1, ba, nb);
+  if (d1 < d2) { memcpy(ba, na, sizeof(na)); } else { memcpy(bb, nb, sizeof(nb)); }
+}
+
+/* closest_segment_point_plane (geometry.py:377-391) */
+static void seg_plane(const R* a, const R* b, const R* p0, const R* n, R* out) {
+  R ba[3];
+  for (int k = 0; k < 3; k++) ba[k] = b[k] - a[k];
+  R dd = dot3(p0, n);
+  R den = dot3(n, ba);
+  R t = (dd - dot3(n, a)) / (den + (R)1e-6);
+  t = clip(t, 0, 1);
+  for (int k = 0; k < 3; k++) out[k] = a[k] + t * ba[k];
+}
+
+/* closest_triangle_point (geometry.py:462-498) */
+static void tri_point(const R* p0, const R* p1, const R* p2, const R* pt, R* out) {
+  R e0[3], e1[3], dv[3];
+  for (int k = 0; k < 3; k++) { e0[k] = p1[k] - p0[k]; e1[k] = p2[k] - p0[k]; dv[k] = pt[k] - p0[k]; }
+  R a = dot3(e0, e0), b = dot3(e0, e1), c = dot3(e1, e1);
+  R det = a * c - b * b;
+  R u = (c * dot3(e0, dv) - b * dot3(e1, dv)) / det;
+  R v = (-b * dot3(e0, dv) + a * dot3(e1, dv)) / det;
+  int inside = (0 <= u) && (u <= 1) && (0 <= v) && (v <= 1) && (u + v <= 1);
+  R cp[3], w[3];
+  for (int k = 0; k < 3; k++) { cp[k] = p0[k] + u * e0[k] + v * e1[k]; w[k] = cp[k] - pt[k]; }
+  R d0 = dot3(w, w);
+  R c1[3], c2[3], c3[3];
+  R d1 = seg_point(p0, p1, pt, c1);
+  int use0 = (d0 < d1) && inside;
+  R best[3];
+  for (int k = 0; k < 3; k++) best[k] = use0 ? cp[k] : c1[k];
+  R md = use0 ? d0 : d1;
+  R d2 = seg_point(p1, p2, pt, c2);
+  if (d2 < md) memcpy(best, c2, sizeof(c2));
+  md = md < d2 ? md : d2;
+  R d3 = seg_point(p2, p0, pt, c3);
+  if (d3 < md) memcpy(best, c3, sizeof(c3));
+  memcpy(out, best, sizeof(best));
+}
+
+/* world velocity difference of a contact point (base.py:126-133) */
+static void rel_vel(const body_t* a, const body_t* b, const R* pos, R* vel) {
+  R ra[3], rb[3], ca[3], cb[3];
+  for (int k = 0; k < 3; k++) { ra[k] = pos[k] - a->pos[k]; rb[k] = pos[k] - b->pos[k]; }
+  cross3(a->ang, ra, ca);
+  cross3(b->ang, rb, cb);
+  for (int k = 0; k < 3; k++) vel[k] = (a->vel[k] + ca[k]) - (b->vel[k] + cb[k]);
+}
+
+/* box_heightmap, one corner (colliders.py:699-739). Height indices follow
+ * jit: negative indices wrap once, then clamp into the grid. */
+static void contact_heightmap(const sysc* s, int r, const body_t* a, const body_t* b, R* pos,
+                              R* vel, R* nrm, R* pen) {
+  const R* x = s->rext + 16 * r;
+  const int off = s->d->row_hm[2 * r], M = s->d->row_hm[2 * r + 1];
+  const R cell = x[0];
+  R o[3], w[3], rel[3], inv[4], p[3];
+  rotate(s->ra_end + 3 * r, a->rot, o);
+  cross3(a->ang, o, w);
+  for (int k = 0; k < 3; k++) { pos[k] = a->pos[k] + o[k]; vel[k] = a->vel[k] + w[k]; }
+  for (int k = 0; k < 3; k++) rel[k] = pos[k] - b->pos[k];
+  quat_inv(b->rot, inv);
+  rotate(rel, inv, p);
+  R u = p[0] / cell, v = p[1] / cell;
+  int iu = (int)floor(u), iv = (int)floor(v);
+  R du = u - (R)iu, dv = v - (R)iv;
+  int lower = (du + dv) < 1;
+  R mu = lower ? (R)-1 : (R)1;
+  int tu[3] = {iu + (lower ? 0 : 1), iu + (lower ? 1 : 0), iu + (lower ? 0 : 1)};
+  int tv[3] = {iv + (lower ? 0 : 1), iv + (lower ? 0 : 1), iv + (lower ? 1 : 0)};
+  R h[3];
+  for (int k = 0; k < 3; k++) {
+    int i = tu[k], j = -tv[k];
+    if (i < 0) i += M;
+    if (j < 0) j += M;
+    i = i < 0 ? 0 : (i >= M ? M - 1 : i);
+    j = j < 0 ? 0 : (j >= M ? M - 1 : j);
+    h[k] = s->hm[off + i * M + j];
+  }
+  R raw[3] = {mu * (h[1] - h[0]), mu * (h[2] - h[0]), cell};
+  R rn = safe_norm3(raw);
+  R n0[3] = {raw[0] / rn, raw[1] / rn, raw[2] / rn};
+  R p0[3] = {(R)tu[0] * cell, (R)tv[0] * cell, h[0]};
+  R dp[3];
+  for (int k = 0; k < 3; k++) dp[k] = p0[k] - p[k];
+  *pen = dot3(dp, n0);
+  rotate(n0, b->rot, nrm);
+}
+
+/* capsule_clippedplane, one capsule end (colliders.py:762-802) */
+static void contact_clipped(const sysc* s, int r, const body_t* a, const body_t* b, R* pos,
+                            R* vel, R* nrm, R* pen) {
+  const R* x = s->rext + 16 * r;
+  R e[3], n[3];
+  rotate(s->ra_end + 3 * r, a->rot, e);
+  for (int k = 0; k < 3; k++) e[k] += a->pos[k];
+  rotate(x, b->rot, n);
+  R ndir = dot3(a->pos, n) > 0 ? (R)1 : (R)-1;
+  for (int k = 0; k < 3; k++) nrm[k] = n[k] * ndir;
+  for (int k = 0; k < 3; k++) pos[k] = e[k] - nrm[k] * s->ra_rad[r];
+  R rel[3], c[3];
+  for (int k = 0; k < 3; k++) rel[k] = pos[k] - a->pos[k];
+  cross3(a->ang, rel, c);
+  for (int k = 0; k < 3; k++) vel[k] = a->vel[k] + c[k];
+  R pp[3], pt[3];
+  rotate(x + 9, b->rot, pp);
+  for (int k = 0; k < 3; k++) pt[k] = pp[k] + b->pos[k];
+  R dp[3];
+  for (int k = 0; k < 3; k++) dp[k] = pt[k] - pos[k];
+  *pen = dot3(dp, nrm);
+  R nx[3], ny[3], nn[3], yn[3], xn[3];
+  rotate(x + 3, b->rot, nx);
+  rotate(x + 6, b->rot, ny);
+  for (int k = 0; k < 3; k++) nn[k] = nrm[k] * ndir;
+  cross3(nn, nx, yn);
+  cross3(nn, ny, xn);
+  for (int k = 0; k < 3; k++) xn[k] = -xn[k];
+  R hx = x[12], hy = x[13];
+  int front = 0;
+  for (int q = 0; q < 4; q++) {
+    R sp[3], sn[3], dd[3];
+    for (int k = 0; k < 3; k++) {
+      sp[k] = q < 2 ? pt[k] + (q == 0 ? nx[k] * hx : -(nx[k] * hx))
+                    : pt[k] + (q == 2 ? ny[k] * hy : -(ny[k] * hy));
+      sn[k] = q == 0 ? xn[k] : (q == 1 ? -xn[k] : (q == 2 ? yn[k] : -yn[k]));
+      dd[k] = pos[k] - sp[k];
+    }
+    front |= dot3(dd, sn) > (R)1e-6;
+  }
+  if (front) *pen = -1;
+}
+
+/* capsule_mesh, one triangle (colliders.py:822-848; geometry.py:501-541) */
+static void contact_capsule_mesh(const sysc* s, int r, const body_t* a, const body_t* b, R* pos,
+                                 R* vel, R* nrm, R* pen) {
+  const R* x = s->rext + 16 * r;
+  R pa[3], ea[3], a0[3], a1[3];
+  rotate(s->ra_pos + 3 * r, a->rot, pa);
+  rotate(s->ra_end + 3 * r, a->rot, ea);
+  for (int k = 0; k < 3; k++) { pa[k] += a->pos[k]; a0[k] = pa[k] + ea[k]; a1[k] = pa[k] - ea[k]; }
+  R tn[3], p[3][3];
+  rotate(x + 9, b->rot, tn);
+  for (int i = 0; i < 3; i++) {
+    rotate(x + 3 * i, b->rot, p[i]);
+    for (int k = 0; k < 3; k++) p[i][k] += b->pos[k];
+  }
+  /* closest_segment_triangle_points (geometry.py:501-541) */
+  R sp[4][3], tp[4][3], dd[4];
+  seg_seg(a0, a1, p[0], p[1], sp[0], tp[0]);
+  seg_seg(a0, a1, p[1], p[2], sp[1], tp[1]);
+  seg_seg(a0, a1, p[0], p[2], sp[2], tp[2]);
+  seg_plane(a0, a1, p[0], tn, sp[3]);
+  tri_point(p[0], p[1], p[2], sp[3], tp[3]);
+  for (int i = 0; i < 4; i++) {
+    R w[3];
+    for (int k = 0; k < 3; k++) w[k] = sp[i][k] - tp[i][k];
+    dd[i] = dot3(w, w);
+  }
+  R md = dd[0];
+  for (int i = 1; i < 4; i++) md = dd[i] < md ? dd[i] : md;
+  R ss[3] = {0, 0, 0}, ts[3] = {0, 0, 0}, cnt = 0;
+  for (int i = 0; i < 4; i++) {
+    R m = dd[i] == md ? (R)1 : (R)0;
+    for (int k = 0; k < 3; k++) { ss[k] += sp[i][k] * m; ts[k] += tp[i][k] * m; }
+    cnt += m;
+  }
+  R pv[3];
+  for (int k = 0; k < 3; k++) { ss[k] /= cnt; ts[k] /= cnt; pv[k] = ss[k] - ts[k]; }
+  R dist = safe_norm3(pv);
+  for (int k = 0; k < 3; k++) nrm[k] = pv[k] / ((R)1e-6 + dist);
+  *pen = s->ra_rad[r] - dist;
+  memcpy(pos, ts, sizeof(ts));
+  rel_vel(a, b, pos, vel);
+}
+
+/* capsule_plane (colliders.py:744-759) / capsule_capsule (:805-819) and the
+ * extended functions above */
 static void contact_row(const sysc* s, int r, const body_t* qp, R* pos, R* vel, R* nrm, R* pen) {
   const bx_desc* d = s->d;
   int g = d->row_group[r];
   const body_t* a = &qp[d->row_body_a[r]];
   const body_t* b = &qp[d->row_body_b[r]];
+  switch (d->col_fn[g]) {
+    case BX_COL_HEIGHTMAP: contact_heightmap(s, r, a, b, pos, vel, nrm, pen); return;
+    case BX_COL_CLIPPED_PLANE: contact_clipped(s, r, a, b, pos, vel, nrm, pen); return;
+    case BX_COL_CAPSULE_MESH: contact_capsule_mesh(s, r, a, b, pos, vel, nrm, pen); return;
+    default: break;
+  }
   if (d->col_fn[g] == BX_COL_CAPSULE_PLANE) {
     R e[3], z[3] = {0, 0, 1};
     rotate(s->ra_end + 3 * r, a->rot, e);
@@ -702,53 +924,8 @@ static void contact_row(const sysc* s, int r, const body_t* qp, R* pos, R* vel, 
     a0[k] = pa[k] + ea[k]; a1[k] = pa[k] - ea[k];
     b0[k] = pb[k] + eb[k]; b1[k] = pb[k] - eb[k];
   }
-  /* _closest_segment_to_segment_points (geometry.py:394-451) */
-  R da[3], db[3];
-  for (int k = 0; k < 3; k++) { da[k] = a1[k] - a0[k]; db[k] = b1[k] - b0[k]; }
-  R la = safe_norm3(da);
-  la += (R)1e-6 * (R)(la == 0);
-  for (int k = 0; k < 3; k++) da[k] /= la;
-  R hla = la * (R)0.5;
-  R lb = safe_norm3(db);
-  lb += (R)1e-6 * (R)(lb == 0);
-  for (int k = 0; k < 3; k++) db[k] /= lb;
-  R hlb = lb * (R)0.5;
-  R am[3], bm[3], tr[3];
-  for (int k = 0; k < 3; k++) {
-    am[k] = a0[k] + da[k] * hla;
-    bm[k] = b0[k] + db[k] * hlb;
-    tr[k] = am[k] - bm[k];
-  }
-  R dadb = dot3(da, db), datr = dot3(da, tr), dbtr = dot3(db, tr);
-  R den = 1 - dadb * dadb;
-  R ota = (-datr + dadb * dbtr) / (den + (R)1e-6);
-  R otb = dbtr + ota * dadb;
-  R ta = clip(ota, -hla, hla), tb = clip(otb, -hlb, hlb);
   R ba[3], bb[3];
-  for (int k = 0; k < 3; k++) { ba[k] = am[k] + da[k] * ta; bb[k] = bm[k] + db[k] * tb; }
-  /* closest_segment_point_and_dist (geometry.py:360-374) */
-  R na[3], nb[3], d1, d2;
-  {
-    R ab[3], t[3];
-    for (int k = 0; k < 3; k++) { ab[k] = a1[k] - a0[k]; t[k] = bb[k] - a0[k]; }
-    R tt = dot3(t, ab) / (dot3(ab, ab) + (R)1e-6);
-    tt = clip(tt, 0, 1);
-    for (int k = 0; k < 3; k++) na[k] = a0[k] + tt * ab[k];
-    R v[3];
-    for (int k = 0; k < 3; k++) v[k] = bb[k] - na[k];
-    d1 = dot3(v, v);
-  }
-  {
-    R ab[3], t[3];
-    for (int k = 0; k < 3; k++) { ab[k] = b1[k] - b0[k]; t[k] = ba[k] - b0[k]; }
-    R tt = dot3(t, ab) / (dot3(ab, ab) + (R)1e-6);
-    tt = clip(tt, 0, 1);
-    for (int k = 0; k < 3; k++) nb[k] = b0[k] + tt * ab[k];
-    R v[3];
-    for (int k = 0; k < 3; k++) v[k] = ba[k] - nb[k];
-    d2 = dot3(v, v);
-  }
-  if (d1 < d2) { memcpy(ba, na, sizeof(na)); } else { memcpy(bb, nb, sizeof(nb)); }
+  seg_seg(a0, a1, b0, b1, ba, bb);
   R pv[3];
   for (int k = 0; k < 3; k++) pv[k] = ba[k] - bb[k];
   R dist = safe_norm3(pv);

@@ -50,6 +50,9 @@ def env_kind(name):
 # point-plane scenes: BoxTest (box corners) and an inline-mesh MeshTest
 # (mesh vertices), oracle/scenes.py
 POINTS = ['box_ground', 'box_slide', 'mesh_ground', 'mesh_tilt']
+# the extended contact functions' scenes (oracle/scenes.py): box corners on a
+# height map, spheres on a clipped plane, capsules against box / mesh triangles
+XCOL = ['heightmap', 'clipped', 'box_capsule', 'mesh_capsule']
 
 
 def config_for(name):
@@ -64,6 +67,12 @@ def config_for(name):
     if name == 'capsule_cull':
       cfg.collider_cutoff = 1
     return cfg
+  if name in XCOL:
+    from oracle import scenes
+    return cfgmod.parse({'heightmap': lambda: scenes.heightmap_config(0.05, 10),
+                         'clipped': lambda: scenes.clipped_plane_config(0.05, 10),
+                         'box_capsule': lambda: scenes.BOX_CAPSULE_NO_HULL_CONFIG,
+                         'mesh_capsule': scenes.mesh_capsule_config}[name]())
   if name in POINTS:
     from oracle import scenes
     return cfgmod.parse(scenes.BOX_TEST_CONFIG if name.startswith('box')

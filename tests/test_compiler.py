@@ -4,11 +4,11 @@ import pytest
 
 from brax_amd import compiler
 from tests.conftest import golden
-from tests.helpers import (CAPSULES, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, compiled,
+from tests.helpers import (CAPSULES, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL, compiled,
                            config_for)
 
 NAMES = (['ant', 'humanoid', 'halfcheetah', 'humanoidstandup', 'mountain1', 'mountain2', 'mountain4', 'mountain1nn']
-         + ROBOTS + CAPSULES + POINTS + SPRING_ENVS + SPRING_ROBOTS)
+         + ROBOTS + CAPSULES + POINTS + SPRING_ENVS + SPRING_ROBOTS + XCOL)
 
 
 @pytest.mark.parametrize('name', NAMES)

@@ -96,7 +96,7 @@ def test_env_step_vs_golden(dev, oracle_lib, name):
   env = envs.get_environment(name, device=dev)
   T = golden('envtraj_' + name)
   _, d, rd, _ = compiled(name)
-  o32 = oracle_lib.Oracle(d, rd, np.float32, safe_guard=True)
+  o32s = [oracle_lib.Oracle(d, rd, np.float32, safe_guard=True, fma=f) for f in (False, True)]
   o64 = oracle_lib.Oracle(d, rd, np.float64)
   for t in range(T['action'].shape[0]):
     st = _state(env, T, t, dev)
@@ -109,7 +109,8 @@ def test_env_step_vs_golden(dev, oracle_lib, name):
     ref, _ = o64.system_step(qp_in, sys_act)
     rng = np.random.default_rng(1234)
     ins = [qp_in] + [qp_in * (1 + rng.uniform(-6e-8, 6e-8, qp_in.shape)) for _ in range(3)]
-    outs = [o32.system_step(q.astype(np.float32), sys_act.astype(np.float32))[0] for q in ins]
+    outs = [o.system_step(q.astype(np.float32), sys_act.astype(np.float32))[0]
+            for o in o32s for q in ins]
     got = new.qp.numpy()
     if hasattr(env, '_teleport'):  # teleported targets draw from the device RNG
       got[:, env.target_idx] = ref[:, env.target_idx]

@@ -20,14 +20,14 @@ import pytest
 import torch
 
 from tests.conftest import golden
-from tests.helpers import (CAPSULES, POINTS, QP_FIELDS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS,
+from tests.helpers import (CAPSULES, POINTS, QP_FIELDS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL,
                            compiled, env_kind, normwise)
 
 pytestmark = pytest.mark.gpu
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
 SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + POINTS
-            + SPRING_ROBOTS)
+            + SPRING_ROBOTS + XCOL)
 POS_TOL = 1e-5
 
 
@@ -61,12 +61,14 @@ def _gate(got, ref, e32, field):
 
 
 class Envelope:
-  """Brax's algorithm in fp32 (oracle float32 build) on the exact inputs and
-  on 3 ulp-perturbed copies; `err(key, ref)` is the max normwise error."""
+  """Brax's algorithm in fp32 on the exact inputs and on ulp-perturbed
+  copies, in two oracle builds: plain float32 and float32 with a*b+c
+  contracted to fused multiply-adds (XLA's jit contracts them, as hipcc does);
+  the envelope is the max normwise error over every run."""
 
   def __init__(self, oracle_lib, name, n_perturb=3, desc=None):
     d, rd = desc if desc is not None else compiled(name)[1:3]
-    self.o = oracle_lib.Oracle(d, rd, np.float32, safe_guard=True)
+    self.os = [oracle_lib.Oracle(d, rd, np.float32, safe_guard=True, fma=f) for f in (False, True)]
     self.n = n_perturb
 
   def _inputs(self, qp):
@@ -77,11 +79,11 @@ class Envelope:
       yield (qp * noise).astype(np.float32)
 
   def system(self, qp, act):
-    outs = [self.o.system_step(q, act.astype(np.float32)) for q in self._inputs(qp)]
-    return outs
+    return [o.system_step(q, act.astype(np.float32)) for o in self.os for q in self._inputs(qp)]
 
   def env(self, name, qp, act, O, M):
-    return [self.o.env_step(name, q, act.astype(np.float32), O, M) for q in self._inputs(qp)]
+    return [o.env_step(name, q, act.astype(np.float32), O, M) for o in self.os
+            for q in self._inputs(qp)]
 
 
 def _make_env(name, dev, **kw):
@@ -103,12 +105,13 @@ def test_system_step_vs_golden(dev, oracle_lib, name):
     from brax_amd import _native
     _native.check(_native.lib().bx_system_set_single(sys_._h, 0))
   T = golden('traj_' + name)
-  # legacy_spring Info.contact sums an impulse pass per substep (16 for
-  # HalfCheetah) through the discontinuous `penetration > 0`, `v_n < 0` and
-  # `|v_t| > 0.01` gates (colliders.py:290-293): 3 perturbed copies understate
-  # its fp32 envelope (E32 of env 3 at t = 2 grows 5.6e-6 -> 1.08e-5 with 15),
-  # so spring systems sample 15
-  env32 = Envelope(oracle_lib, name, n_perturb=15 if name.endswith('_spring') else 3)
+  # 15 perturbed copies per build: the envelope is a max over samples, and 3 understate
+  # it for small batches and for sums over discontinuous gates (legacy_spring
+  # Info.contact sums an impulse pass per substep through `penetration > 0`,
+  # `v_n < 0` and `|v_t| > 0.01`, colliders.py:290-293: E32 of HalfCheetah's
+  # env 3 at t = 2 grows 5.6e-6 -> 1.08e-5 from 3 to 15 copies; one-env
+  # scenes such as the height map likewise)
+  env32 = Envelope(oracle_lib, name, n_perturb=15)
   for t in range(T['action'].shape[0]):
     qp_in = _to_qp(T['qp'][t], dev)
     act = torch.as_tensor(T['action'][t], dtype=torch.float32, device=dev)
@@ -381,3 +384,57 @@ def test_culling_selects_nearest(dev, oracle_lib):
       e32 = _env_err([x[0][..., sl] for x in outs], ref[..., sl])
       _gate(out.numpy()[..., sl], ref[..., sl], e32, f)
     qp_np = ref
+
+
+def _scene_system(text, dev):
+  import brax_amd
+  return brax_amd.System(text, device=dev)
+
+
+def test_heightmap_kat(dev):
+  """HeightMapTest (`physics_test.py:252-257`): the box falls onto the
+  bottom-left quadrant of the height map and stays above z = 2."""
+  from oracle import scenes
+  sys_ = _scene_system(scenes.heightmap_config(), dev)
+  qp = sys_.default_qp()
+  qp, _ = sys_.step(qp, torch.zeros(0, device=dev))
+  assert float(qp.pos[0, 2]) > 2.0
+
+
+def test_clipped_plane_kat(dev):
+  """CapsuleClippedPlaneTest (`physics_test.py:463-475`, 4 decimals): sphere 1
+  rests on the clipped plane at z = 2, spheres 2 and 3 beside it on the
+  ground."""
+  from oracle import scenes
+  sys_ = _scene_system(scenes.clipped_plane_config(), dev)
+  qp, _ = sys_.step(sys_.default_qp(), torch.zeros(0, device=dev))
+  np.testing.assert_allclose(qp.pos[:3, 2].cpu().numpy(), [2.5, 0.5, 0.5], atol=1.5e-4)
+
+
+def test_box_capsule_kat(dev):
+  """BoxCapsuleTest (`physics_test.py:207-225`, 2 decimals): boxes fall onto
+  capsules and stay on them (unit and 10x mass), a capsule falls onto a frozen
+  box. Its box-box (hull) pairs are far apart and never touch; the scene runs
+  with them left out (oracle/scenes.py)."""
+  from oracle import scenes
+  sys_ = _scene_system(scenes.BOX_CAPSULE_NO_HULL_CONFIG, dev)
+  qp = sys_.default_qp()
+  for _ in range(30):
+    qp, _ = sys_.step(qp, torch.zeros(0, device=dev))
+  z = qp.pos[:, 2].cpu().numpy()
+  assert abs(z[0] - 2.5) < 0.005 and abs(z[1] - 1.0) < 0.005
+  assert z[2] >= 2.5 - 0.005 and abs(z[3] - 1.0) < 0.005
+  assert abs(z[5] - 1.5) < 0.005
+
+
+def test_mesh_capsule_kat(dev):
+  """MeshTest's `test_mesh_hits_capsule` (`physics_test.py:409-423`) on the
+  inline prism (half-height 0.1 at scale 0.1): the mesh comes to rest on the
+  capsule (top at z = 0.4), not on the ground."""
+  from oracle import scenes
+  cfg = scenes.mesh_capsule_config().replace('z: 0.7 }', 'z: 1.5 }')
+  sys_ = _scene_system(cfg, dev)
+  qp = sys_.default_qp()
+  for _ in range(30):
+    qp, _ = sys_.step(qp, torch.zeros(0, device=dev))
+  assert abs(float(qp.pos[0, 2]) - 0.5) < 0.01

@@ -7,11 +7,12 @@ import numpy as np
 import pytest
 
 from tests.conftest import golden
-from tests.helpers import CAPSULES, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, compiled, env_kind
+from tests.helpers import (CAPSULES, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL, compiled,
+                           env_kind)
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
 SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + POINTS
-            + SPRING_ROBOTS)
+            + SPRING_ROBOTS + XCOL)
 
 
 def _oracle(oracle_lib, name, guard=False, dtype=np.float64):
