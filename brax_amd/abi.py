@@ -41,6 +41,7 @@ _DESC_FIELDS = [
     ('dynamics_mode', C.c_int32), ('joint_stiffness', f64p),
     ('joint_spring_damping', f64p), ('joint_limit_strength', f64p),
     ('row_ext', f64p), ('row_hm', i32p), ('n_hm', C.c_int32), ('hm_data', f64p),
+    ('n_hull', C.c_int32), ('hull_vert', f64p), ('hull_face', f64p), ('hull_norm', f64p),
 ]
 
 DYN_PBD, DYN_LEGACY_SPRING = 0, 1
@@ -122,6 +123,7 @@ def make_desc(d):
   s.angular_damping = float(d['angular_damping'])
   s.dynamics_mode = int(d.get('dynamics_mode', DYN_PBD))
   s.n_hm = len(d.get('hm_data', ()))
+  s.n_hull = len(d.get('hull_vert', ()))
   for name, ctype in _DESC_FIELDS:
     if ctype is i32p or ctype is f64p:
       if name in d:
@@ -138,7 +140,7 @@ def make_desc(d):
         v = np.zeros((len(d['row_group']), 16))
       elif name == 'row_hm':
         v = np.tile([-1, 0], (len(d['row_group']), 1))
-      elif name == 'hm_data':
+      elif name in ('hm_data', 'hull_vert', 'hull_face', 'hull_norm'):
         v = np.zeros(0)
       else:
         raise KeyError(name)

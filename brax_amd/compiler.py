@@ -33,7 +33,7 @@ DYN_PBD, DYN_LEGACY_SPRING = 0, 1
 # actuator kinds (descriptor `act_type`)
 TORQUE, ANGLE = 0, 1
 # contact functions (descriptor `col_fn`)
-CAPSULE_PLANE, CAPSULE_CAPSULE, HEIGHTMAP, CLIPPED_PLANE, CAPSULE_MESH = 0, 1, 2, 3, 4
+CAPSULE_PLANE, CAPSULE_CAPSULE, HEIGHTMAP, CLIPPED_PLANE, CAPSULE_MESH, HULL_HULL = 0, 1, 2, 3, 4, 5
 ROW_EXT = 16  # per-row extra constants of the extended contact functions
 # force kinds
 THRUSTER, TWISTER = 0, 1
@@ -206,6 +206,27 @@ _TRI_BOX_NORMALS = [[0, -1., 0], [0, -1., 0], [0, 0, -1.], [0, 0, -1.], [1., 0, 
                     [0, 1., 0], [0, 1., 0], [0, 0, 1.], [0, 0, 1.], [-1., 0, 0], [-1., 0, 0]]
 
 
+# `geometry.py:57-73`: the box's 6 quads (clockwise) and their normals
+_BOX_QUADS = [0, 1, 5, 4, 0, 4, 6, 2, 6, 4, 5, 7, 2, 6, 7, 3, 1, 3, 7, 5, 0, 2, 3, 1]
+_BOX_QUAD_NORMALS = [[0, -1., 0], [0, 0, -1.], [1., 0, 0], [0, 1., 0], [0, 0, 1.], [-1., 0, 0]]
+
+
+def _hull_box(col):
+  """HullBox (`geometry.py:201-206` via BoxMesh/BaseMesh :138-198): the 8
+  corners, the 6 quads (winding fixed as for every mesh) and their normals,
+  in the body frame."""
+  rot = euler_to_quat(vec(col.rotation))
+  vert = np.array([rotate(c, rot) for c in _BOX_CORNERS * vec(col.box.halfsize)])
+  vert = vert + vec(col.position)
+  normals = np.array([rotate(np.array(n), rot) for n in _BOX_QUAD_NORMALS])
+  faces = vert[np.array(_BOX_QUADS)].reshape(-1, 4, 3)
+  out = []
+  for f, n in zip(faces, normals):
+    wind = np.dot(np.cross(f[0] - f[-1], f[0] - f[1]), n) >= 0
+    out.append(f if wind else f[::-1])
+  return vert, np.array(out), normals
+
+
 def _mesh_faces(col, mesh_geoms):
   """Triangles (F,3,3) and face normals (F,3) in the body frame of a
   TriangulatedBox (`geometry.py:157-198`) or a Mesh (`geometry.py:291-331`),
@@ -262,7 +283,8 @@ def _colliders(config, index):
                ('box', 'heightMap'): HEIGHTMAP,
                ('capsule', 'clipped_plane'): CLIPPED_PLANE,
                ('capsule', 'box'): CAPSULE_MESH,
-               ('capsule', 'mesh'): CAPSULE_MESH}
+               ('capsule', 'mesh'): CAPSULE_MESH,
+               ('box', 'box'): HULL_HULL}
   mesh_geoms = {mg.name: mg for mg in config.mesh_geometries}
   unique_meshes = {}
   cols = []
@@ -341,6 +363,18 @@ def _colliders(config, index):
                           'a_radius', 'b_pos', 'b_end', 'b_radius', 'friction',
                           'elasticity', 'flat', 'ext', 'hm')}
   hm_data = []
+  hulls = {}  # (body name, collider index) -> hull index (HullBox data)
+  hull_vert, hull_face, hull_norm = [], [], []
+
+  def hull_of(c, c_idx, b):
+    key = (b.name, c_idx)
+    if key not in hulls:
+      v, f, n = _hull_box(c)
+      hulls[key] = len(hull_vert)
+      hull_vert.append(v)
+      hull_face.append(f)
+      hull_norm.append(n)
+    return hulls[key]
   out['col_cutoff'] = []
   for gi, g in enumerate(groups):
     out['col_oneway'].append(1 if g['oneway'] else 0)
@@ -350,7 +384,16 @@ def _colliders(config, index):
     out['col_baumgarte_erp'].append(config.baumgarte_erp * config.substeps / config.dt)
     out['col_cutoff'].append(g['cutoff'])
     ext_l = None
-    if g['kind'] in ('box', 'mesh'):
+    if g['fn'] == HULL_HULL:
+      # hull_hull (`colliders.py:851-888`): SAT gives 4 contacts per pair
+      # (edge contact padded, or the face manifold); row e of a pair is
+      # contact e, ext = (hull a, hull b, e)
+      ends_l, ext_l = [], []
+      for ca, ca_idx, ba, cb, cb_idx, bb in g['pairs']:
+        ha, hb = hull_of(ca, ca_idx, ba), hull_of(cb, cb_idx, bb)
+        ends_l.append([np.zeros(3)] * 4)
+        ext_l.append([np.concatenate([[ha, hb, e], np.zeros(ROW_EXT - 3)]) for e in range(4)])
+    elif g['kind'] in ('box', 'mesh'):
       # Box corners (`geometry.py:123-137`) / PointMesh vertices (:312-357)
       # in the body frame, as zero-radius capsule ends
       ends_l = [_point_ends(ca, mesh_geoms) for ca, _, _, _, _, _ in g['pairs']]
@@ -380,6 +423,8 @@ def _colliders(config, index):
       fa = ca.material.friction * cb.material.friction
       ea = ca.material.elasticity * cb.material.elasticity
       a_rad = 0. if g['kind'] in ('box', 'mesh') else ca.capsule.radius
+      if g['fn'] == HULL_HULL:
+        a_rad = 0.
       ext, hm = [np.zeros(ROW_EXT)] * len(ends_l[pi]) if g['fn'] != CAPSULE_CAPSULE else [
           np.zeros(ROW_EXT)], (-1, 0)
       if g['fn'] == HEIGHTMAP:
@@ -403,7 +448,7 @@ def _colliders(config, index):
         ext = [e] * len(ends_l[pi])
       elif ext_l is not None:
         ext = ext_l[pi]
-      if g['fn'] in (CAPSULE_PLANE, HEIGHTMAP, CLIPPED_PLANE, CAPSULE_MESH):
+      if g['fn'] in (CAPSULE_PLANE, HEIGHTMAP, CLIPPED_PLANE, CAPSULE_MESH, HULL_HULL):
         ends = ends_l[pi]
         b_end, b_rad = np.zeros(3), 0.
       else:
@@ -434,6 +479,9 @@ def _colliders(config, index):
   d['row_ext'] = np.asarray(rows.pop('ext'), np.float64).reshape(-1, ROW_EXT)
   d['row_hm'] = np.asarray(rows.pop('hm'), np.int32).reshape(-1, 2)
   d['hm_data'] = np.asarray(hm_data, np.float64)
+  d['hull_vert'] = np.asarray(hull_vert, np.float64).reshape(-1, 8, 3)
+  d['hull_face'] = np.asarray(hull_face, np.float64).reshape(-1, 6, 4, 3)
+  d['hull_norm'] = np.asarray(hull_norm, np.float64).reshape(-1, 6, 3)
   for k, v in rows.items():
     if k in ('group', 'body_a', 'body_b', 'flat'):
       d['row_' + k] = np.asarray(v, np.int32)

@@ -95,7 +95,16 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       return fail("contact row body out of range");
     if (d->row_group[x] < 0 || d->row_group[x] >= G) return fail("contact row group out of range");
     int fn = d->col_fn[d->row_group[x]];
-    if (fn < BX_COL_CAPSULE_PLANE || fn > BX_COL_CAPSULE_MESH) return fail("unsupported contact function");
+    if (fn < BX_COL_CAPSULE_PLANE || fn > BX_COL_HULL_HULL) return fail("unsupported contact function");
+    if (fn == BX_COL_HULL_HULL) {
+      if (!d->hull_vert || !d->hull_face || !d->hull_norm) return fail("hull rows need the hull arrays");
+      for (int k = 0; k < 2; k++) {
+        int hx = (int)d->row_ext[16 * x + k];
+        if (hx < 0 || hx >= d->n_hull) return fail("hull row index out of range");
+      }
+      int e = (int)d->row_ext[16 * x + 2];
+      if (e < 0 || e > 3) return fail("hull row contact index out of range");
+    }
     if (fn >= BX_COL_HEIGHTMAP && !d->row_ext) return fail("extended contact rows need row_ext");
     if (fn == BX_COL_HEIGHTMAP) {
       if (!d->row_hm || !d->hm_data) return fail("height map rows need row_hm and hm_data");
@@ -229,6 +238,13 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   }
   H.o_hm = B.alloc(d->n_hm > 0 ? d->n_hm : 0);
   for (int k = 0; k < d->n_hm; k++) B.f(H.o_hm + k, d->hm_data[k]);
+  H.o_hull = B.alloc(d->n_hull > 0 ? d->n_hull * HULL_STRIDE : 0);
+  for (int h = 0; h < d->n_hull; h++) {
+    int o = H.o_hull + h * HULL_STRIDE;
+    for (int k = 0; k < 24; k++) B.f(o + HULL_V + k, d->hull_vert[24 * h + k]);
+    for (int k = 0; k < 72; k++) B.f(o + HULL_F + k, d->hull_face[72 * h + k]);
+    for (int k = 0; k < 18; k++) B.f(o + HULL_N + k, d->hull_norm[18 * h + k]);
+  }
   // collider groups: cutoff, row range, Info base (system.py:36-43 order)
   H.o_group = B.alloc(G * GROUP_STRIDE);
   {

@@ -638,6 +638,224 @@ __device__ __noinline__ void capsule_mesh_contact(const Cst& c, int o, const Row
   vel = (a.vel + cross(a.ang, pos - a.pos)) - (b.vel + cross(b.ang, pos - b.pos));
 }
 
+// ---- hull_hull: separating axis test between two boxes ---------------------
+// (colliders.py:851-888; geometry.py:580-914). Every row of a pair computes
+// the whole test and keeps its own contact e (4 rows a pair).
+struct HullW {
+  v3 v[8];
+  v3 f[6][4];
+  v3 n[6];
+};
+
+__device__ void hull_world(const Cst& c, const BlobHdr& H, int h, const QP& q, HullW& w) {
+  const int o = H.o_hull + h * HULL_STRIDE;
+  for (int i = 0; i < 8; i++) w.v[i] = q.pos + rotate(c.f3(o + HULL_V + 3 * i), q.rot);
+  for (int f = 0; f < 6; f++) {
+    w.n[f] = rotate(c.f3(o + HULL_N + 3 * f), q.rot);
+    for (int i = 0; i < 4; i++) w.f[f][i] = q.pos + rotate(c.f3(o + HULL_F + 12 * f + 3 * i), q.rot);
+  }
+}
+
+// get_face_support (geometry.py:794-801)
+__device__ float hull_face_support(const v3* verts, const v3* normals, const v3 (*faces)[4], int& idx) {
+  float best = 0.f;
+  for (int f = 0; f < 6; f++) {
+    float mn = 0.f;
+    for (int v = 0; v < 8; v++) {
+      float x = dot(normals[f], verts[v] - faces[f][0]);
+      mn = (v == 0 || x < mn) ? x : mn;
+    }
+    if (f == 0 || mn > best) { best = mn; idx = f; }
+  }
+  return best;
+}
+
+// _clip_edge_to_planes (geometry.py:580-624) against 4 planes; returns the mask
+__device__ bool hull_clip_edge(v3 p0, v3 p1, const v3* pp, const v3* pn, v3& o0, v3& o1) {
+  bool f0[4], f1[4];
+  v3 cand[4];
+  for (int j = 0; j < 4; j++) {
+    f0[j] = dot(p0 - pp[j], pn[j]) > 1e-6f;
+    f1[j] = dot(p1 - pp[j], pn[j]) > 1e-6f;
+    v3 ab = p1 - p0;
+    float t = (dot(pp[j], pn[j]) - dot(pn[j], p0)) / (dot(pn[j], ab) + 1e-6f);
+    cand[j] = p0 + clampf(t, 0.f, 1.f) * ab;
+  }
+  for (int side = 0; side < 2; side++) {
+    const v3 a = side == 0 ? p0 : p1, b = side == 0 ? p1 : p0;
+    const bool* fr = side == 0 ? f0 : f1;
+    int best = 0;
+    float bd = 0.f;
+    for (int j = 0; j < 4; j++) {
+      float d = dot((fr[j] ? cand[j] : a) - a, b - a);
+      if (j == 0 || d > bd) { bd = d; best = j; }
+    }
+    v3 r = fr[best] ? cand[best] : a;
+    if (side == 0) o0 = r; else o1 = r;
+  }
+  bool both = false;
+  for (int j = 0; j < 4; j++) both |= f0[j] && f1[j];
+  bool mask = !both;
+  if (!mask) { o0 = p0; o1 = p1; }
+  if (dot(p0 - p1, o0 - o1) < 0.f) mask = false;
+  return mask;
+}
+
+// _create_sat_contact_manifold + clip (geometry.py:627-747): contact e
+__device__ void hull_manifold(const v3* cp, const v3* sp, v3 cn, v3 sn, float sign, int e, v3& pos,
+                              v3& nrm, float& pen) {
+  v3 c0[4], cpn[4], s0[4], spn[4];
+  for (int i = 0; i < 4; i++) {
+    const int im = (i + 3) & 3;  // jp.roll(poly, 1)
+    c0[i] = cp[im];
+    cpn[i] = cross(cn, cp[i] - c0[i]);
+    s0[i] = sp[im];
+    spn[i] = cross(sn, sp[i] - s0[i]);
+  }
+  v3 pts[16];
+  bool msk[16];
+  for (int i = 0; i < 4; i++) {
+    bool m = hull_clip_edge(s0[i], sp[i], c0, cpn, pts[2 * i], pts[2 * i + 1]);
+    msk[2 * i] = msk[2 * i + 1] = m;
+  }
+  const float dd = dot(sp[0], sn), den = dot(cn, sn);
+  const float dn = den + 1e-6f * (float)(den == 0.f);
+  for (int i = 0; i < 4; i++) {
+    v3 a = c0[i] + ((dd - dot(c0[i], sn)) / dn) * cn;
+    v3 b = cp[i] + ((dd - dot(cp[i], sn)) / dn) * cn;
+    bool m = hull_clip_edge(a, b, s0, spn, pts[8 + 2 * i], pts[8 + 2 * i + 1]);
+    msk[8 + 2 * i] = msk[8 + 2 * i + 1] = m;
+  }
+  const v3 nh = cn / (1e-6f + safe_norm(cn));
+  v3 ref[16];
+  for (int i = 0; i < 16; i++) {
+    v3 d = pts[i] - cp[0];
+    ref[i] = pts[i] - dot(d, nh) * nh;
+    msk[i] = msk[i] && (dot(d, -cn) > 1e-6f);
+  }
+  // get_orthogonals (geometry.py:568-577)
+  float ca[3] = {fabsf(cn.x), fabsf(cn.y), fabsf(cn.z)};
+  int ix = 0;
+  for (int k = 1; k < 3; k++) if (ca[k] > ca[ix]) ix = k;
+  const float cix = ix == 0 ? cn.x : (ix == 1 ? cn.y : cn.z);
+  const float denom = cix + 1e-6f * (float)(cix == 0.f);
+  const float bv = -(((cn.x + cn.y) + cn.z) - cix) / denom;
+  v3 o1 = mk(ix == 0 ? bv : 1.f, ix == 1 ? bv : 1.f, ix == 2 ? bv : 1.f);
+  v3 o2 = cross(cn, o1);
+  v3 dir = e == 0 ? o1 : (e == 1 ? -o1 : (e == 2 ? o2 : -o2));
+  int best = 0;
+  float bvv = 0.f;
+  for (int i = 0; i < 16; i++) {
+    float v = dot(ref[i], dir) + (msk[i] ? 0.f : -1e6f);
+    if (i == 0 || v > bvv) { bvv = v; best = i; }
+  }
+  pos = ref[best];
+  nrm = sign * cn;
+  pen = msk[best] ? dot(pts[best] - ref[best], -cn) : -1.f;
+}
+
+__device__ __noinline__ void hull_contact(const Cst& c, const BlobHdr& H, int o, const QP& a,
+                                          const QP& b, v3& pos, v3& vel, v3& n, float& pen) {
+  const int ha = (int)c.f(o + R_X), hb = (int)c.f(o + R_X + 1), e = (int)c.f(o + R_X + 2);
+  HullW A, B;
+  hull_world(c, H, ha, a, A);
+  hull_world(c, H, hb, b, B);
+  v3 origin = mk(0.f, 0.f, 0.f);
+  for (int v = 0; v < 8; v++) origin = origin + A.v[v];
+  origin = origin / 8.f;
+  int i1 = 0, i2 = 0;
+  const float d1 = hull_face_support(A.v, B.n, B.f, i1);
+  const float d2 = hull_face_support(B.v, A.n, A.f, i2);
+  const bool use_b = d1 > d2;
+  const float face_dist = use_b ? d1 : d2;
+  const int fi = use_b ? i1 : i2;
+  const v3* ref_face = use_b ? B.f[fi] : A.f[fi];
+  const v3 ref_n = use_b ? B.n[fi] : A.n[fi];
+  const v3 (*inc_faces)[4] = use_b ? A.f : B.f;
+  const v3* inc_ns = use_b ? A.n : B.n;
+  int ii = 0;
+  float bd = 0.f;
+  for (int f = 0; f < 6; f++) {
+    float d = dot(inc_ns[f], ref_n);
+    if (f == 0 || d < bd) { bd = d; ii = f; }
+  }
+  // edge axes over every face pair (faces of a tiled, of b repeated) and
+  // edge pair; get_edge_support picks the best
+  int best = -1;
+  float best_v = 0.f, best_sd = 0.f;
+  v3 best_ax = mk(0.f, 0.f, 0.f), ba1 = best_ax, ba2 = best_ax, bb1 = best_ax, bb2 = best_ax;
+  for (int kp = 0; kp < 36; kp++) {
+    const int fa = kp % 6, fb = kp / 6;
+    for (int m = 0; m < 16; m++) {
+      const int ea = m & 3, eb = m >> 2;
+      const v3 a1 = A.f[fa][ea], a2 = A.f[fa][(ea + 3) & 3];
+      const v3 b1 = B.f[fb][eb], b2 = B.f[fb][(eb + 3) & 3];
+      v3 ax = cross(a1 - a2, b1 - b2);
+      ax = ax * (dot(a1 - origin, ax) > 0.f ? 1.f : -1.f);
+      bool bad = ax.x == 0.f && ax.y == 0.f && ax.z == 0.f;
+      float mx = 0.f;
+      for (int v = 0; v < 8; v++) {
+        float t = dot(ax, A.v[v] - a1);
+        mx = (v == 0 || t > mx) ? t : mx;
+      }
+      bad |= mx > 0.f;
+      v3 dm = (a1 + (a2 - a1) * 0.5f) - (b1 + (b2 - b1) * 0.5f);
+      const float aux = -dot(dm, dm);
+      int sv = 0;
+      float sd = 0.f;
+      for (int v = 0; v < 8; v++) {
+        float t = dot(ax, B.v[v] - a1);
+        if (v == 0 || t < sd) { sd = t; sv = v; }
+      }
+      const v3 spt = B.v[sv];
+      const float s1 = ((b1.x - spt.x) + (b1.y - spt.y)) + (b1.z - spt.z);
+      const float s2 = ((b2.x - spt.x) + (b2.y - spt.y)) + (b2.z - spt.z);
+      if (!(s1 == 0.f || s2 == 0.f)) bad = true;
+      if (bad) sd = -1e6f;
+      const float val = sd + aux;
+      if (best < 0 || val > best_v) {
+        best_v = val; best = kp * 16 + m; best_sd = sd; best_ax = ax;
+        ba1 = a1; ba2 = a2; bb1 = b1; bb2 = b2;
+      }
+    }
+  }
+  const float edge_dist = best_sd;
+  const bool maybe_edge = edge_dist > face_dist;
+  const v3 en = best_ax / safe_norm(best_ax);
+  const bool has_int = fmaxf(edge_dist, face_dist) < 0.f;
+  // _create_sat_edge_contact: closest points with the barycentric t
+  v3 da = ba2 - ba1, db = bb2 - bb1;
+  float la = safe_norm(da);
+  la += 1e-6f * (float)(la == 0.f);
+  da = da / la;
+  float lb = safe_norm(db);
+  lb += 1e-6f * (float)(lb == 0.f);
+  db = db / lb;
+  const float hla = la * 0.5f, hlb = lb * 0.5f;
+  const v3 am = ba1 + da * hla, bm = bb1 + db * hlb, tr = am - bm;
+  const float dadb = dot(da, db), datr = dot(da, tr), dbtr = dot(db, tr);
+  const float ota = (-datr + dadb * dbtr) / ((1.f - dadb * dadb) + 1e-6f);
+  const float otb = dbtr + ota * dadb;
+  v3 pa = am + da * clampf(ota, -hla, hla), pb = bm + db * clampf(otb, -hlb, hlb);
+  {
+    v3 na, nb;
+    float dd1 = seg_point(ba1, ba2, pb, na);
+    float dd2 = seg_point(bb1, bb2, pa, nb);
+    if (dd1 < dd2) pa = na; else pb = nb;
+  }
+  const float ta = (ota + hla) / la, tb = (otb + hlb) / lb;
+  const bool valid = has_int && maybe_edge && ta >= 0.f && ta <= 1.f && tb >= 0.f && tb <= 1.f;
+  const float edge_pen0 = valid ? -edge_dist : -1.f;
+  if (edge_pen0 > 0.f) {  // jp.cond(edge_contact.penetration[0] > 0, edge, face)
+    pos = pb + (pa - pb) * 0.5f;
+    n = -en;
+    pen = e == 0 ? edge_pen0 : -1.f;
+  } else {
+    hull_manifold(ref_face, inc_faces[ii], ref_n, inc_ns[ii], use_b ? 1.f : -1.f, e, pos, n, pen);
+  }
+  vel = (a.vel + cross(a.ang, pos - a.pos)) - (b.vel + cross(b.ang, pos - b.pos));
+}
+
 // every contact function of row r (the item-loop kernels)
 template <int F>
 __device__ __forceinline__ void contact_gen_x(const Cst& c, const BlobHdr& H, int r, const RowC& R,
@@ -647,6 +865,7 @@ __device__ __forceinline__ void contact_gen_x(const Cst& c, const BlobHdr& H, in
   if (R.fn == BX_COL_HEIGHTMAP) heightmap_contact(c, H, o, R, a, b, pos, vel, n, pen);
   else if (R.fn == BX_COL_CLIPPED_PLANE) clipped_contact(c, o, R, a, b, pos, vel, n, pen);
   else if (R.fn == BX_COL_CAPSULE_MESH) capsule_mesh_contact(c, o, R, a, b, pos, vel, n, pen);
+  else if (R.fn == BX_COL_HULL_HULL) hull_contact(c, H, o, a, b, pos, vel, n, pen);
   else contact_gen<F>(R, a, b, pos, vel, n, pen);
 }
 

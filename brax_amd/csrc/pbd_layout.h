@@ -81,6 +81,8 @@ struct BlobHdr {
   int32_t l_alist;                   // LDS: active rows in Info order (info_rows)
   int32_t spring;                    // dynamics_mode == legacy_spring
   int32_t o_hm;                      // height map grids
+  int32_t o_hull;                    // box hulls: 8 corners, 6x4 quad points, 6 normals
 };
+enum { HULL_STRIDE = 114, HULL_V = 0, HULL_F = 24, HULL_N = 96 };
 
 }  // namespace bx

@@ -45,7 +45,9 @@ enum { BX_COL_CAPSULE_PLANE = 0, BX_COL_CAPSULE_CAPSULE = 1,
        /* box corner vs height map (colliders.py:699-739), capsule end vs
         * clipped plane (:762-802), capsule vs one triangle of a box / mesh
         * (:822-848) */
-       BX_COL_HEIGHTMAP = 2, BX_COL_CLIPPED_PLANE = 3, BX_COL_CAPSULE_MESH = 4 };
+       BX_COL_HEIGHTMAP = 2, BX_COL_CLIPPED_PLANE = 3, BX_COL_CAPSULE_MESH = 4,
+       /* box vs box by the separating axis test (:851-888), 4 rows a pair */
+       BX_COL_HULL_HULL = 5 };
 enum { BX_FORCE_THRUSTER = 0, BX_FORCE_TWISTER = 1 };
 /* env layer kinds (obs / reward programs) */
 enum { BX_ENV_NONE = 0, BX_ENV_ANT = 1, BX_ENV_HUMANOID = 2, BX_ENV_HALFCHEETAH = 3,
@@ -142,6 +144,12 @@ typedef struct bx_desc {
   const int32_t* row_hm;           /* [R,2] */
   int32_t n_hm;
   const double* hm_data;           /* [n_hm] row-major square grids */
+  /* HULL_HULL rows: ext (hull a, hull b, contact e) into these box hulls
+   * (geometry.py:201-206), body frame */
+  int32_t n_hull;
+  const double* hull_vert;         /* [H,8,3] corners */
+  const double* hull_face;         /* [H,6,4,3] quads, winding fixed */
+  const double* hull_norm;         /* [H,6,3] face normals */
 } bx_desc;
 
 /*

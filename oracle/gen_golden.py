@@ -166,6 +166,7 @@ def dump_desc(sys_):
                           'b_pos', 'b_end', 'b_radius', 'friction', 'elasticity', 'flat',
                           'ext', 'hm')}
   hm_data = []
+  hull_ix, hull_v, hull_f, hull_n = {}, [], [], []
   gcut = []
   for g, c in enumerate(sys_.colliders):
     if isinstance(c.cull, rc.NearNeighbors):
@@ -188,7 +189,7 @@ def dump_desc(sys_):
     fn = c.contact_fn.__name__
     gfn.append({'capsule_plane': 0, 'capsule_capsule': 1, 'box_plane': 0,
                 'mesh_plane': 0, 'box_heightmap': 2, 'capsule_clippedplane': 3,
-                'capsule_mesh': 4}[fn])
+                'capsule_mesh': 4, 'hull_hull': 5}[fn])
     gscale.append(c.collide_scale)
     gthr.append(c.velocity_threshold)
     gerp.append(c.baumgarte_erp)
@@ -209,6 +210,18 @@ def dump_desc(sys_):
         ends = [ca.end[p]] * F
         ext = [np.r_[np.asarray(cb.faces[p][f]).reshape(-1), cb.face_normals[p][f], np.zeros(4)]
                for f in range(F)]
+      elif fn == 'hull_hull':
+        ends = [np.zeros(3)] * 4
+        hx = []
+        for col, p_ in ((ca, p), (cb, p)):
+          key = (int(col.body.idx[p_]), tuple(np.round(np.asarray(col.vertices[p_]).ravel(), 12)))
+          if key not in hull_ix:
+            hull_ix[key] = len(hull_v)
+            hull_v.append(np.asarray(col.vertices[p_]))
+            hull_f.append(np.asarray(col.faces[p_]))
+            hull_n.append(np.asarray(col.face_normals[p_]))
+          hx.append(hull_ix[key])
+        ext = [np.r_[hx[0], hx[1], e, np.zeros(13)] for e in range(4)]
       elif fn == 'capsule_clippedplane':
         ends = list(ca.end[p])
         ext = [np.r_[cb.normal[p], cb.x[p], cb.y[p], cb.pos[p], cb.halfsize_x[p],
@@ -227,7 +240,7 @@ def dump_desc(sys_):
         rows['a_pos'].append(ca.pos[p])
         rows['a_end'].append(e)
         rows['a_radius'].append(ca.radius[p] if fn not in ('box_plane', 'mesh_plane',
-                                                           'box_heightmap') else 0.)
+                                                           'box_heightmap', 'hull_hull') else 0.)
         rows['b_pos'].append(cb.pos[p])
         rows['b_end'].append(cb.end[p] if fn == 'capsule_capsule' else np.zeros(3))
         rows['b_radius'].append(cb.radius[p] if fn == 'capsule_capsule' else 0.)
@@ -242,6 +255,9 @@ def dump_desc(sys_):
   d['row_ext'] = np.asarray(rows.pop('ext'), np.float64).reshape(-1, 16)
   d['row_hm'] = np.asarray(rows.pop('hm'), np.int32).reshape(-1, 2)
   d['hm_data'] = np.asarray(hm_data, np.float64)
+  d['hull_vert'] = np.asarray(hull_v, np.float64).reshape(-1, 8, 3)
+  d['hull_face'] = np.asarray(hull_f, np.float64).reshape(-1, 6, 4, 3)
+  d['hull_norm'] = np.asarray(hull_n, np.float64).reshape(-1, 6, 3)
   ints = ('group', 'body_a', 'body_b', 'flat')
   for k, v in rows.items():
     if k in ints:
@@ -618,6 +634,9 @@ def main():
       'clipped': (scenes.clipped_plane_config(0.05, 10), 1, 8),
       'box_capsule': (scenes.BOX_CAPSULE_NO_HULL_CONFIG, 1, 4),
       'mesh_capsule': (scenes.mesh_capsule_config(), 0, 8),
+      # hull-hull SAT (colliders.py:851-888): edge and face manifolds
+      'box_box': (scenes.box_box_config(0.05, 20), 0, 10),
+      'box_capsule_hull': (scenes.BOX_CAPSULE_TEST_CONFIG, 1, 3),
   }
   for name, (txt, di, T) in point_scenes.items():
     if want(name):

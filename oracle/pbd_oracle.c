@@ -143,6 +143,7 @@ typedef struct {
   R *gscale, *gthr, *gerp;
   R *ra_pos, *ra_end, *ra_rad, *rb_pos, *rb_end, *rb_rad, *rfric, *relas;
   R *rext, *hm;  /* extended contact functions: row constants (R,16), heightmaps */
+  R *hv, *hf, *hn; /* box hulls: corners (H,8,3), quads (H,6,4,3), normals (H,6,3) */
 } sysc;
 
 static R* cvt(const double* s, int n) {
@@ -199,6 +200,9 @@ static void sys_init(sysc* s, const bx_desc* d) {
   s->relas = cvt(d->row_elasticity, Rn);
   s->rext = cvt(d->row_ext, 16 * Rn);
   s->hm = cvt(d->hm_data, d->n_hm);
+  s->hv = cvt(d->hull_vert, 24 * d->n_hull);
+  s->hf = cvt(d->hull_face, 72 * d->n_hull);
+  s->hn = cvt(d->hull_norm, 18 * d->n_hull);
 }
 
 static void sys_free(sysc* s) {
@@ -207,7 +211,7 @@ static void sys_free(sysc* s) {
              &s->jsp, &s->jsa, &s->astr, &s->gscale, &s->gthr, &s->gerp,
              &s->ra_pos, &s->ra_end, &s->ra_rad, &s->rb_pos, &s->rb_end,
              &s->rb_rad, &s->rfric, &s->relas, &s->fstr, &s->fmass,
-             &s->jstiff, &s->jsdamp, &s->jlstr, &s->rext, &s->hm};
+             &s->jstiff, &s->jsdamp, &s->jlstr, &s->rext, &s->hm, &s->hv, &s->hf, &s->hn};
   for (size_t i = 0; i < sizeof(p) / sizeof(p[0]); i++) free(*p[i]);
 }
 
@@ -884,6 +888,285 @@ static void contact_capsule_mesh(const sysc* s, int r, const body_t* a, const bo
   rel_vel(a, b, pos, vel);
 }
 
+/* ------------------------------------------------ hull_hull (SAT) ------- */
+
+typedef struct { R v[8][3]; R f[6][4][3]; R n[6][3]; } hull_w;
+
+static void hull_world(const sysc* s, int h, const body_t* q, hull_w* w) {
+  for (int i = 0; i < 8; i++) {
+    rotate(s->hv + 24 * h + 3 * i, q->rot, w->v[i]);
+    for (int k = 0; k < 3; k++) w->v[i][k] += q->pos[k];
+  }
+  for (int f = 0; f < 6; f++) {
+    rotate(s->hn + 18 * h + 3 * f, q->rot, w->n[f]);
+    for (int i = 0; i < 4; i++) {
+      rotate(s->hf + 72 * h + 12 * f + 3 * i, q->rot, w->f[f][i]);
+      for (int k = 0; k < 3; k++) w->f[f][i][k] += q->pos[k];
+    }
+  }
+}
+
+/* get_face_support (geometry.py:794-801): max over faces of the min signed
+ * distance of the vertices to the face plane; first index on ties */
+static R face_support(R (*verts)[3], R (*normals)[3], R (*faces)[4][3], int* idx) {
+  R best = 0;
+  for (int f = 0; f < 6; f++) {
+    R mn = 0;
+    for (int v = 0; v < 8; v++) {
+      R d[3];
+      for (int k = 0; k < 3; k++) d[k] = verts[v][k] - faces[f][0][k];
+      R x = dot3(normals[f], d);
+      mn = (v == 0 || x < mn) ? x : mn;
+    }
+    if (f == 0 || mn > best) { best = mn; *idx = f; }
+  }
+  return best;
+}
+
+/* _closest_segment_to_segment_points with the barycentric t (geometry.py:394-451) */
+static void seg_seg_t(const R* a0, const R* a1, const R* b0, const R* b1, R* ba, R* bb, R* t_a, R* t_b) {
+  R da[3], db[3];
+  for (int k = 0; k < 3; k++) { da[k] = a1[k] - a0[k]; db[k] = b1[k] - b0[k]; }
+  R la = safe_norm3(da);
+  la += (R)1e-6 * (R)(la == 0);
+  for (int k = 0; k < 3; k++) da[k] /= la;
+  R hla = la * (R)0.5;
+  R lb = safe_norm3(db);
+  lb += (R)1e-6 * (R)(lb == 0);
+  for (int k = 0; k < 3; k++) db[k] /= lb;
+  R hlb = lb * (R)0.5;
+  R am[3], bm[3], tr[3];
+  for (int k = 0; k < 3; k++) { am[k] = a0[k] + da[k] * hla; bm[k] = b0[k] + db[k] * hlb; tr[k] = am[k] - bm[k]; }
+  R dadb = dot3(da, db), datr = dot3(da, tr), dbtr = dot3(db, tr);
+  R den = 1 - dadb * dadb;
+  R ota = (-datr + dadb * dbtr) / (den + (R)1e-6);
+  R otb = dbtr + ota * dadb;
+  R ta = clip(ota, -hla, hla), tb = clip(otb, -hlb, hlb);
+  for (int k = 0; k < 3; k++) { ba[k] = am[k] + da[k] * ta; bb[k] = bm[k] + db[k] * tb; }
+  R na[3], nb[3];
+  R d1 = seg_point(a0, a1, bb, na);
+  R d2 = seg_point(b0, b1, ba, nb);
+  if (d1 < d2) { memcpy(ba, na, sizeof(na)); } else { memcpy(bb, nb, sizeof(nb)); }
+  *t_a = (ota + hla) / la;
+  *t_b = (otb + hlb) / lb;
+}
+
+/* _clip_edge_to_planes (geometry.py:580-624) against 4 planes */
+static int clip_edge(const R* p0, const R* p1, R (*pp)[3], R (*pn)[3], R out[2][3]) {
+  int f0[4], f1[4];
+  R cand[4][3];
+  for (int j = 0; j < 4; j++) {
+    R d0[3], d1[3];
+    for (int k = 0; k < 3; k++) { d0[k] = p0[k] - pp[j][k]; d1[k] = p1[k] - pp[j][k]; }
+    f0[j] = dot3(d0, pn[j]) > (R)1e-6;
+    f1[j] = dot3(d1, pn[j]) > (R)1e-6;
+    seg_plane(p0, p1, pp[j], pn[j], cand[j]);
+  }
+  for (int side = 0; side < 2; side++) {
+    const R* a = side == 0 ? p0 : p1;
+    const R* b = side == 0 ? p1 : p0;
+    const int* fr = side == 0 ? f0 : f1;
+    R ab[3];
+    for (int k = 0; k < 3; k++) ab[k] = b[k] - a[k];
+    int best = 0;
+    R bd = 0;
+    for (int j = 0; j < 4; j++) {
+      R e[3];
+      for (int k = 0; k < 3; k++) e[k] = (fr[j] ? cand[j][k] : a[k]) - a[k];
+      R dd = dot3(e, ab);
+      if (j == 0 || dd > bd) { bd = dd; best = j; }
+    }
+    for (int k = 0; k < 3; k++) out[side][k] = fr[best] ? cand[best][k] : a[k];
+  }
+  int any_both = 0;
+  for (int j = 0; j < 4; j++) any_both |= f0[j] && f1[j];
+  int mask = !any_both;
+  if (!mask) { memcpy(out[0], p0, 3 * sizeof(R)); memcpy(out[1], p1, 3 * sizeof(R)); }
+  R e1[3], e2[3];
+  for (int k = 0; k < 3; k++) { e1[k] = p0[k] - p1[k]; e2[k] = out[0][k] - out[1][k]; }
+  if (dot3(e1, e2) < 0) mask = 0;
+  return mask;
+}
+
+/* _create_sat_contact_manifold + clip (geometry.py:627-747): 4 contacts */
+static void sat_manifold(R (*cp)[3], R (*sp)[3], const R* cn, const R* sn, R sign, R pos[4][3],
+                         R nrm[4][3], R pen[4]) {
+  R c0[4][3], c1[4][3], cpn[4][3], s0[4][3], s1[4][3], spn[4][3];
+  for (int i = 0; i < 4; i++) {
+    int im = (i + 3) % 4;  /* jp.roll(poly, 1): element i comes from i - 1 */
+    R e[3];
+    for (int k = 0; k < 3; k++) { c0[i][k] = cp[im][k]; c1[i][k] = cp[i][k]; e[k] = c1[i][k] - c0[i][k]; }
+    cross3(cn, e, cpn[i]);
+    for (int k = 0; k < 3; k++) { s0[i][k] = sp[im][k]; s1[i][k] = sp[i][k]; e[k] = s1[i][k] - s0[i][k]; }
+    cross3(sn, e, spn[i]);
+  }
+  R pts[16][3];
+  int msk[16];
+  for (int i = 0; i < 4; i++) {
+    R o[2][3];
+    int m = clip_edge(s0[i], s1[i], c0, cpn, o);
+    memcpy(pts[2 * i], o[0], sizeof(o[0]));
+    memcpy(pts[2 * i + 1], o[1], sizeof(o[1]));
+    msk[2 * i] = msk[2 * i + 1] = m;
+  }
+  /* _project_poly_onto_poly_plane of the clipping edge points onto the subject plane */
+  R dd = dot3(sp[0], sn), den = dot3(cn, sn);
+  R dn = den + (R)1e-6 * (R)(den == 0);
+  R c0s[4][3], c1s[4][3];
+  for (int i = 0; i < 4; i++) {
+    R t0 = (dd - dot3(c0[i], sn)) / dn, t1 = (dd - dot3(c1[i], sn)) / dn;
+    for (int k = 0; k < 3; k++) { c0s[i][k] = c0[i][k] + t0 * cn[k]; c1s[i][k] = c1[i][k] + t1 * cn[k]; }
+  }
+  for (int i = 0; i < 4; i++) {
+    R o[2][3];
+    int m = clip_edge(c0s[i], c1s[i], s0, spn, o);
+    memcpy(pts[8 + 2 * i], o[0], sizeof(o[0]));
+    memcpy(pts[8 + 2 * i + 1], o[1], sizeof(o[1]));
+    msk[8 + 2 * i] = msk[8 + 2 * i + 1] = m;
+  }
+  /* reference points: projected onto the clipping plane (math.normalize) */
+  R nn = (R)1e-6 + safe_norm3(cn), nh[3], ref[16][3];
+  for (int k = 0; k < 3; k++) nh[k] = cn[k] / nn;
+  for (int i = 0; i < 16; i++) {
+    R d[3];
+    for (int k = 0; k < 3; k++) d[k] = pts[i][k] - cp[0][k];
+    R dist = dot3(d, nh);
+    for (int k = 0; k < 3; k++) ref[i][k] = pts[i][k] - dist * nh[k];
+    R ncn[3] = {-cn[0], -cn[1], -cn[2]};
+    msk[i] = msk[i] && (dot3(d, ncn) > (R)1e-6);  /* point_in_front_of_plane(p0, -n, pt) */
+  }
+  /* get_orthogonals (geometry.py:568-577) */
+  int ix = 0;
+  R ab = cn[0] < 0 ? -cn[0] : cn[0];
+  for (int k = 1; k < 3; k++) { R v = cn[k] < 0 ? -cn[k] : cn[k]; if (v > ab) { ab = v; ix = k; } }
+  R o1[3] = {1, 1, 1}, o2[3];
+  R denom = cn[ix] + (R)1e-6 * (R)(cn[ix] == 0);
+  o1[ix] = -(((cn[0] + cn[1]) + cn[2]) - cn[ix]) / denom;
+  cross3(cn, o1, o2);
+  R dirs[4][3];
+  for (int k = 0; k < 3; k++) { dirs[0][k] = o1[k]; dirs[1][k] = -o1[k]; dirs[2][k] = o2[k]; dirs[3][k] = -o2[k]; }
+  for (int c = 0; c < 4; c++) {
+    int best = 0;
+    R bv = 0;
+    for (int i = 0; i < 16; i++) {
+      R v = dot3(ref[i], dirs[c]) + (msk[i] ? (R)0 : (R)-1e6);
+      if (i == 0 || v > bv) { bv = v; best = i; }
+    }
+    R pd[3];
+    for (int k = 0; k < 3; k++) { pos[c][k] = ref[best][k]; pd[k] = pts[best][k] - ref[best][k]; nrm[c][k] = sign * cn[k]; }
+    R ncn[3] = {-cn[0], -cn[1], -cn[2]};
+    pen[c] = msk[best] ? dot3(pd, ncn) : (R)-1;
+  }
+}
+
+/* hull_hull (colliders.py:851-888) with sat_hull_hull (geometry.py:750-914):
+ * contact e of the pair */
+static void contact_hull(const sysc* s, int r, const body_t* a, const body_t* b, R* pos, R* vel,
+                         R* nrm, R* pen) {
+  const R* x = s->rext + 16 * r;
+  const int ha = (int)x[0], hb = (int)x[1], e = (int)x[2];
+  hull_w A, B;
+  hull_world(s, ha, a, &A);
+  hull_world(s, hb, b, &B);
+  R origin[3] = {0, 0, 0};
+  for (int v = 0; v < 8; v++)
+    for (int k = 0; k < 3; k++) origin[k] += A.v[v][k];
+  for (int k = 0; k < 3; k++) origin[k] /= 8;
+  int i1 = 0, i2 = 0;
+  R d1 = face_support(A.v, B.n, B.f, &i1);
+  R d2 = face_support(B.v, A.n, A.f, &i2);
+  int use_b = d1 > d2;
+  R face_dist = use_b ? d1 : d2;
+  int fi = use_b ? i1 : i2;
+  R (*ref_face)[3] = use_b ? B.f[fi] : A.f[fi];
+  R* ref_n = use_b ? B.n[fi] : A.n[fi];
+  R sign = use_b ? (R)1 : (R)-1;
+  R (*inc_faces)[4][3] = use_b ? A.f : B.f;
+  R (*inc_ns)[3] = use_b ? A.n : B.n;
+  int ii = 0;
+  R bd = 0;
+  for (int f = 0; f < 6; f++) {
+    R d = dot3(inc_ns[f], ref_n);
+    if (f == 0 || d < bd) { bd = d; ii = f; }
+  }
+  R fpos[4][3], fnrm[4][3], fpen[4];
+  sat_manifold(ref_face, inc_faces[ii], ref_n, inc_ns[ii], sign, fpos, fnrm, fpen);
+  /* edge axes over every face pair (tile a, repeat b) and edge pair */
+  int best = -1;
+  R best_v = 0, best_sd = 0, best_ax[3] = {0, 0, 0};
+  R ba1[3] = {0}, ba2[3] = {0}, bb1[3] = {0}, bb2[3] = {0};
+  for (int kp = 0; kp < 36; kp++) {
+    const int fa = kp % 6, fb = kp / 6;
+    for (int m = 0; m < 16; m++) {
+      const int ea = m % 4, eb = m / 4;
+      const R* a1 = A.f[fa][ea];
+      const R* a2 = A.f[fa][(ea + 3) % 4];
+      const R* b1 = B.f[fb][eb];
+      const R* b2 = B.f[fb][(eb + 3) % 4];
+      R e1[3], e2[3], ax[3], dv[3];
+      for (int k = 0; k < 3; k++) { e1[k] = a1[k] - a2[k]; e2[k] = b1[k] - b2[k]; dv[k] = a1[k] - origin[k]; }
+      cross3(e1, e2, ax);
+      R sg = dot3(dv, ax) > 0 ? (R)1 : (R)-1;
+      for (int k = 0; k < 3; k++) ax[k] *= sg;
+      int bad = ax[0] == 0 && ax[1] == 0 && ax[2] == 0;
+      R mx = 0;
+      for (int v = 0; v < 8; v++) {
+        R d[3];
+        for (int k = 0; k < 3; k++) d[k] = A.v[v][k] - a1[k];
+        R t = dot3(ax, d);
+        mx = (v == 0 || t > mx) ? t : mx;
+      }
+      bad |= mx > 0;
+      R am[3], bm[3], dm[3];
+      for (int k = 0; k < 3; k++) {
+        am[k] = a1[k] + (a2[k] - a1[k]) * (R)0.5;
+        bm[k] = b1[k] + (b2[k] - b1[k]) * (R)0.5;
+        dm[k] = am[k] - bm[k];
+      }
+      R aux = -dot3(dm, dm);
+      /* get_edge_support: the support vertex of B along -ax */
+      int sv = 0;
+      R sd = 0;
+      for (int v = 0; v < 8; v++) {
+        R d[3];
+        for (int k = 0; k < 3; k++) d[k] = B.v[v][k] - a1[k];
+        R t = dot3(ax, d);
+        if (v == 0 || t < sd) { sd = t; sv = v; }
+      }
+      R s1 = ((b1[0] - B.v[sv][0]) + (b1[1] - B.v[sv][1])) + (b1[2] - B.v[sv][2]);
+      R s2 = ((b2[0] - B.v[sv][0]) + (b2[1] - B.v[sv][1])) + (b2[2] - B.v[sv][2]);
+      if (!(s1 == 0 || s2 == 0)) bad = 1;
+      if (bad) sd = (R)-1e6;
+      R val = sd + aux;
+      if (best < 0 || val > best_v) {
+        best_v = val; best = kp * 16 + m; best_sd = sd;
+        memcpy(best_ax, ax, sizeof(ax));
+        memcpy(ba1, a1, sizeof(ba1)); memcpy(ba2, a2, sizeof(ba2));
+        memcpy(bb1, b1, sizeof(bb1)); memcpy(bb2, b2, sizeof(bb2));
+      }
+    }
+  }
+  R edge_dist = best_sd;
+  int maybe_edge = edge_dist > face_dist;
+  R an = safe_norm3(best_ax), en[3];
+  for (int k = 0; k < 3; k++) en[k] = best_ax[k] / an;
+  R best_dist = edge_dist > face_dist ? edge_dist : face_dist;
+  int has_int = best_dist < 0;
+  /* _create_sat_edge_contact */
+  R pa[3], pb[3], ta, tb;
+  seg_seg_t(ba1, ba2, bb1, bb2, pa, pb, &ta, &tb);
+  int valid = has_int && maybe_edge && ta >= 0 && ta <= 1 && tb >= 0 && tb <= 1;
+  R edge_pen0 = valid ? -edge_dist : (R)-1;
+  if (edge_pen0 > 0) {  /* jp.cond(edge_contact.penetration[0] > 0, edge, face) */
+    for (int k = 0; k < 3; k++) { pos[k] = pb[k] + (pa[k] - pb[k]) * (R)0.5; nrm[k] = -en[k]; }
+    *pen = e == 0 ? edge_pen0 : (R)-1;
+  } else {
+    for (int k = 0; k < 3; k++) { pos[k] = fpos[e][k]; nrm[k] = fnrm[e][k]; }
+    *pen = fpen[e];
+  }
+  rel_vel(a, b, pos, vel);
+}
+
 /* capsule_plane (colliders.py:744-759) / capsule_capsule (:805-819) and the
  * extended functions above */
 static void contact_row(const sysc* s, int r, const body_t* qp, R* pos, R* vel, R* nrm, R* pen) {
@@ -895,6 +1178,7 @@ static void contact_row(const sysc* s, int r, const body_t* qp, R* pos, R* vel, 
     case BX_COL_HEIGHTMAP: contact_heightmap(s, r, a, b, pos, vel, nrm, pen); return;
     case BX_COL_CLIPPED_PLANE: contact_clipped(s, r, a, b, pos, vel, nrm, pen); return;
     case BX_COL_CAPSULE_MESH: contact_capsule_mesh(s, r, a, b, pos, vel, nrm, pen); return;
+    case BX_COL_HULL_HULL: contact_hull(s, r, a, b, pos, vel, nrm, pen); return;
     default: break;
   }
   if (d->col_fn[g] == BX_COL_CAPSULE_PLANE) {

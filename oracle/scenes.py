@@ -184,3 +184,23 @@ defaults {{
   qps {{ name: "ClippedPlane" pos {{ x: 0 }} }}
 }}
 """
+
+
+def box_box_config(dt=0.5, substeps=200):
+  """BoxBoxTest (`physics_test.py:85-117`): a small box (rotated 45 degrees)
+  falls onto a box resting on the ground (hull-hull SAT contacts)."""
+  return f"""
+dt: {dt} substeps: {substeps} friction: 0.8 elasticity: 0.5
+gravity {{ z: -9.8 }}
+bodies {{ name: "box1" mass: 1 colliders {{ box {{ halfsize {{ x: 0.2 y: 0.2 z: 0.2 }}}} }} inertia {{ x: 1 y: 1 z: 1 }} }}
+bodies {{ name: "box2" mass: 1 colliders {{ box {{ halfsize {{ x: 0.1 y: 0.1 z: 0.1 }}}} }} inertia {{ x: 1 y: 1 z: 1 }} }}
+bodies {{ name: "Ground" frozen: {{ all: true }} colliders {{ plane {{}}}} }}
+defaults {{
+  qps {{ name: "box1" pos {{ x: 0 y: 1 z: .2 }} rot {{z: 0}} }}
+  qps {{ name: "box2" pos {{ x: 0.1 y: 1 z: .6 }} rot {{z: 45}} }}
+}}
+defaults {{
+  qps {{ name: "box1" pos {{ x: 0 y: 1 z: .2 }} rot {{z: 0}} }}
+  qps {{ name: "box2" pos {{ x: 0.1 y: 1 z: .49 }} rot {{x: 7 y: 4 z: 45}} vel {{ z: -0.3 }} }}
+}}
+"""

@@ -52,7 +52,7 @@ def env_kind(name):
 POINTS = ['box_ground', 'box_slide', 'mesh_ground', 'mesh_tilt']
 # the extended contact functions' scenes (oracle/scenes.py): box corners on a
 # height map, spheres on a clipped plane, capsules against box / mesh triangles
-XCOL = ['heightmap', 'clipped', 'box_capsule', 'mesh_capsule']
+XCOL = ['heightmap', 'clipped', 'box_capsule', 'mesh_capsule', 'box_box', 'box_capsule_hull']
 
 
 def config_for(name):
@@ -72,7 +72,9 @@ def config_for(name):
     return cfgmod.parse({'heightmap': lambda: scenes.heightmap_config(0.05, 10),
                          'clipped': lambda: scenes.clipped_plane_config(0.05, 10),
                          'box_capsule': lambda: scenes.BOX_CAPSULE_NO_HULL_CONFIG,
-                         'mesh_capsule': scenes.mesh_capsule_config}[name]())
+                         'mesh_capsule': scenes.mesh_capsule_config,
+                         'box_box': lambda: scenes.box_box_config(0.05, 20),
+                         'box_capsule_hull': lambda: scenes.BOX_CAPSULE_TEST_CONFIG}[name]())
   if name in POINTS:
     from oracle import scenes
     return cfgmod.parse(scenes.BOX_TEST_CONFIG if name.startswith('box')

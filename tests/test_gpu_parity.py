@@ -438,3 +438,29 @@ def test_mesh_capsule_kat(dev):
   for _ in range(30):
     qp, _ = sys_.step(qp, torch.zeros(0, device=dev))
   assert abs(float(qp.pos[0, 2]) - 0.5) < 0.01
+
+
+def test_box_box_kat(dev):
+  """BoxBoxTest (`physics_test.py:106-117`, 2 decimals): a box falls onto a
+  box (hull-hull SAT contacts) and stays stacked, x-y unchanged."""
+  from oracle import scenes
+  sys_ = _scene_system(scenes.box_box_config(), dev)
+  qp, _ = sys_.step(sys_.default_qp(), torch.zeros(0, device=dev))
+  p = qp.pos.cpu().numpy()
+  assert abs(p[0, 2] - 0.2) < 0.005 and abs(p[1, 2] - 0.5) < 0.005
+  assert abs(p[1, 0] - 0.1) < 0.005 and abs(p[1, 1] - 1.0) < 0.005
+
+
+def test_box_capsule_full_kat(dev):
+  """BoxCapsuleTest as the reference runs it, its box-box hull pairs included
+  (`physics_test.py:207-225`)."""
+  from oracle import scenes
+  sys_ = _scene_system(scenes.BOX_CAPSULE_TEST_CONFIG, dev)
+  qp = sys_.default_qp()
+  assert abs(float(qp.pos[0, 2]) - 3.5) < 0.005 and abs(float(qp.pos[2, 2]) - 3.5) < 0.005
+  for _ in range(30):
+    qp, _ = sys_.step(qp, torch.zeros(0, device=dev))
+  z = qp.pos[:, 2].cpu().numpy()
+  assert abs(z[0] - 2.5) < 0.005 and abs(z[1] - 1.0) < 0.005
+  assert z[2] >= 2.5 - 0.005 and abs(z[3] - 1.0) < 0.005
+  assert abs(z[5] - 1.5) < 0.005
