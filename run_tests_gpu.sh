@@ -2,7 +2,7 @@
 # GPU test suite + smoke -> gpurun_out/pytest_gpu.log
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 tail -15 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
