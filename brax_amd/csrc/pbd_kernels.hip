@@ -641,6 +641,12 @@ __device__ __noinline__ void capsule_mesh_contact(const Cst& c, int o, const Row
 // ---- hull_hull: separating axis test between two boxes ---------------------
 // (colliders.py:851-888; geometry.py:580-914). Every row of a pair computes
 // the whole test and keeps its own contact e (4 rows a pair).
+// Divisions here are correctly rounded (pdiv), whatever the TU's flags: the
+// edge contact is valid only for barycentric t in [0, 1], and
+// t = (ota + la/2) / la lands exactly on 1 for a closest point at an edge
+// end; v_rcp_f32 + multiply overshoots to 1 + ulp there and drops the
+// contact (BoxBoxTest step 8, measured on the MI355X).
+__device__ __forceinline__ v3 pdiv3(v3 a, float b) { return mk(pdiv(a.x, b), pdiv(a.y, b), pdiv(a.z, b)); }
 struct HullW {
   v3 v[8];
   v3 f[6][4];
@@ -678,7 +684,7 @@ __device__ bool hull_clip_edge(v3 p0, v3 p1, const v3* pp, const v3* pn, v3& o0,
     f0[j] = dot(p0 - pp[j], pn[j]) > 1e-6f;
     f1[j] = dot(p1 - pp[j], pn[j]) > 1e-6f;
     v3 ab = p1 - p0;
-    float t = (dot(pp[j], pn[j]) - dot(pn[j], p0)) / (dot(pn[j], ab) + 1e-6f);
+    float t = pdiv(dot(pp[j], pn[j]) - dot(pn[j], p0), dot(pn[j], ab) + 1e-6f);
     cand[j] = p0 + clampf(t, 0.f, 1.f) * ab;
   }
   for (int side = 0; side < 2; side++) {
@@ -721,12 +727,12 @@ __device__ void hull_manifold(const v3* cp, const v3* sp, v3 cn, v3 sn, float si
   const float dd = dot(sp[0], sn), den = dot(cn, sn);
   const float dn = den + 1e-6f * (float)(den == 0.f);
   for (int i = 0; i < 4; i++) {
-    v3 a = c0[i] + ((dd - dot(c0[i], sn)) / dn) * cn;
-    v3 b = cp[i] + ((dd - dot(cp[i], sn)) / dn) * cn;
+    v3 a = c0[i] + pdiv(dd - dot(c0[i], sn), dn) * cn;
+    v3 b = cp[i] + pdiv(dd - dot(cp[i], sn), dn) * cn;
     bool m = hull_clip_edge(a, b, s0, spn, pts[8 + 2 * i], pts[8 + 2 * i + 1]);
     msk[8 + 2 * i] = msk[8 + 2 * i + 1] = m;
   }
-  const v3 nh = cn / (1e-6f + safe_norm(cn));
+  const v3 nh = pdiv3(cn, 1e-6f + safe_norm(cn));
   v3 ref[16];
   for (int i = 0; i < 16; i++) {
     v3 d = pts[i] - cp[0];
@@ -739,7 +745,7 @@ __device__ void hull_manifold(const v3* cp, const v3* sp, v3 cn, v3 sn, float si
   for (int k = 1; k < 3; k++) if (ca[k] > ca[ix]) ix = k;
   const float cix = ix == 0 ? cn.x : (ix == 1 ? cn.y : cn.z);
   const float denom = cix + 1e-6f * (float)(cix == 0.f);
-  const float bv = -(((cn.x + cn.y) + cn.z) - cix) / denom;
+  const float bv = pdiv(-(((cn.x + cn.y) + cn.z) - cix), denom);
   v3 o1 = mk(ix == 0 ? bv : 1.f, ix == 1 ? bv : 1.f, ix == 2 ? bv : 1.f);
   v3 o2 = cross(cn, o1);
   v3 dir = e == 0 ? o1 : (e == 1 ? -o1 : (e == 2 ? o2 : -o2));
@@ -821,20 +827,20 @@ __device__ __noinline__ void hull_contact(const Cst& c, const BlobHdr& H, int o,
   }
   const float edge_dist = best_sd;
   const bool maybe_edge = edge_dist > face_dist;
-  const v3 en = best_ax / safe_norm(best_ax);
+  const v3 en = pdiv3(best_ax, safe_norm(best_ax));
   const bool has_int = fmaxf(edge_dist, face_dist) < 0.f;
   // _create_sat_edge_contact: closest points with the barycentric t
   v3 da = ba2 - ba1, db = bb2 - bb1;
   float la = safe_norm(da);
   la += 1e-6f * (float)(la == 0.f);
-  da = da / la;
+  da = pdiv3(da, la);
   float lb = safe_norm(db);
   lb += 1e-6f * (float)(lb == 0.f);
-  db = db / lb;
+  db = pdiv3(db, lb);
   const float hla = la * 0.5f, hlb = lb * 0.5f;
   const v3 am = ba1 + da * hla, bm = bb1 + db * hlb, tr = am - bm;
   const float dadb = dot(da, db), datr = dot(da, tr), dbtr = dot(db, tr);
-  const float ota = (-datr + dadb * dbtr) / ((1.f - dadb * dadb) + 1e-6f);
+  const float ota = pdiv(-datr + dadb * dbtr, (1.f - dadb * dadb) + 1e-6f);
   const float otb = dbtr + ota * dadb;
   v3 pa = am + da * clampf(ota, -hla, hla), pb = bm + db * clampf(otb, -hlb, hlb);
   {
@@ -843,7 +849,7 @@ __device__ __noinline__ void hull_contact(const Cst& c, const BlobHdr& H, int o,
     float dd2 = seg_point(bb1, bb2, pa, nb);
     if (dd1 < dd2) pa = na; else pb = nb;
   }
-  const float ta = (ota + hla) / la, tb = (otb + hlb) / lb;
+  const float ta = pdiv(ota + hla, la), tb = pdiv(otb + hlb, lb);
   const bool valid = has_int && maybe_edge && ta >= 0.f && ta <= 1.f && tb >= 0.f && tb <= 1.f;
   const float edge_pen0 = valid ? -edge_dist : -1.f;
   if (edge_pen0 > 0.f) {  // jp.cond(edge_contact.penetration[0] > 0, edge, face)

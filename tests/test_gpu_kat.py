@@ -243,3 +243,59 @@ def test_sphericalize_free_dofs(dev):
   assert list(s.joints[0].free_dofs) == [1, 2, 3]
   a, v = s.joints[0].angle_vel(s.default_qp())
   assert a.shape == (6,) and v.shape == (6,)
+
+
+ELASTIC = """
+dt: 0.01 substeps: 10 friction: 0.0 elasticity: 1.0 gravity { z: -9.8 }
+bodies { name: "sphere" mass: 1 colliders { capsule { radius: .5 length: 1.0 } } inertia { x: 1 y: 1 z: 1 } }
+bodies { name: "sphere_stationary" mass: 1 colliders { capsule { radius: .5 length: 1.0 } }
+         inertia { x: 1 y: 1 z: 1 } }
+bodies { name: "boxwall" mass: 1 colliders { box { halfsize { x: 1 y: 1 z: 1 } } }
+         inertia { x: 1 y: 1 z: 1 } frozen { all: true } }
+bodies { name: "Ground" frozen { all: true } colliders { plane {} } }
+defaults { qps { name: "sphere" vel { x: 10 y: 0 z: 0 } pos { z: .5 } }
+           qps { name: "sphere_stationary" pos { x: -20 y: 0 z: .5 } }
+           qps { name: "boxwall" pos { x: 10 } } }
+defaults { qps { name: "sphere" pos { z: 1.5 } vel { z: 5.0 } }
+           qps { name: "sphere_stationary" pos { x: 0 y: 0 z: .5 } }
+           qps { name: "boxwall" pos { x: 10 } } }
+"""
+
+
+def _bounce(dev, elasticity, default, steps, dt=None, freeze_ball=False):
+  import brax_amd
+  from brax_amd import config as cfgmod
+  cfg = cfgmod.parse(ELASTIC)
+  cfg.elasticity = elasticity
+  if dt is not None:
+    cfg.dt = dt
+  if freeze_ball:
+    cfg.bodies[1].frozen.all = True
+  s = brax_amd.System(cfg, device=dev)
+  qp0 = s.default_qp(default)
+  qp = qp0
+  for _ in range(steps):
+    qp, _ = s.step(qp, torch.zeros(0, device=dev))
+  return qp0, qp
+
+
+@pytest.mark.parametrize('elasticity', [0., .5, 1.])
+def test_ball_bounce(dev, elasticity):
+  """ElasticityTest (`physics_test.py:863-876`): a capsule hits a frozen box
+  wall (capsule-box contacts) and comes back with e^2 of its speed."""
+  qp0, qp = _bounce(dev, elasticity, 0, 100)
+  places(float(qp0.vel[0][0]) * -1 * elasticity ** 2, qp.vel[0][0], 2)
+
+
+@pytest.mark.parametrize('elasticity', [0., 1.])
+def test_ball_bounce_vertical(dev, elasticity):
+  """ElasticityTest (`:878-894`): a ball bounces off another ball."""
+  qp0, qp = _bounce(dev, elasticity, 1, 400, dt=2 * 5 / 9.8 / 100.)
+  assert abs(float(qp0.vel[0][2]) * elasticity ** 2 - float(qp.vel[0][2])) <= .02
+
+
+@pytest.mark.parametrize('elasticity', [0., 1.])
+def test_ball_bounce_vertical_frozen(dev, elasticity):
+  """ElasticityTest (`:896-914`): a ball bounces off a frozen ball."""
+  qp0, qp = _bounce(dev, elasticity, 1, 100, dt=2 * 5 / 9.8 / 100., freeze_ball=True)
+  assert abs(float(qp0.vel[0][2]) * elasticity ** 2 - float(qp.vel[0][2])) <= .04
