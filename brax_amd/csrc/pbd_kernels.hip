@@ -656,9 +656,22 @@ struct HullW {
 __device__ void hull_world(const Cst& c, const BlobHdr& H, int h, const QP& q, HullW& w) {
   const int o = H.o_hull + h * HULL_STRIDE;
   for (int i = 0; i < 8; i++) w.v[i] = q.pos + rotate(c.f3(o + HULL_V + 3 * i), q.rot);
+  // a face corner that is a hull vertex takes that vertex's world point bit
+  // for bit: the edge support test compares face-edge endpoints with the
+  // support vertex for exact equality (geometry.py:812-814), which holds in
+  // the reference because both come out of the same rotate; two separately
+  // scheduled (FMA-contracted) rotates here may differ in the last ulp
   for (int f = 0; f < 6; f++) {
     w.n[f] = rotate(c.f3(o + HULL_N + 3 * f), q.rot);
-    for (int i = 0; i < 4; i++) w.f[f][i] = q.pos + rotate(c.f3(o + HULL_F + 12 * f + 3 * i), q.rot);
+    for (int i = 0; i < 4; i++) {
+      const v3 fc = c.f3(o + HULL_F + 12 * f + 3 * i);
+      int m = -1;
+      for (int v = 0; v < 8; v++) {
+        const v3 bv = c.f3(o + HULL_V + 3 * v);
+        if (bv.x == fc.x && bv.y == fc.y && bv.z == fc.z) m = v;
+      }
+      w.f[f][i] = m >= 0 ? w.v[m] : q.pos + rotate(fc, q.rot);
+    }
   }
 }
 

@@ -188,17 +188,27 @@ class System:
       joint_angle = self.default_angle(default_index)
     ja = torch.as_tensor(joint_angle, dtype=torch.float32, device=self.device)
     batched = ja.dim() == 2
-    if self.num_joint_dof == 0:
+    D = self.num_joint_dof
+    if D == 0:
       B = ja.shape[0] if batched else 1
       ja = torch.zeros((B, 0), dtype=torch.float32, device=self.device)
     else:
-      ja = ja.reshape(-1, self.num_joint_dof).contiguous()
+      ja = ja.reshape(-1, ja.shape[-1]) if batched else ja.reshape(1, -1)
       B = ja.shape[0]
+    # the angle vector lists only the dofs with a nonzero limit
+    # (system.py:86-110,138-141); the reset tables index that prefix, so
+    # rows are padded to the kernel's num_joint_dof stride
+    def pad(x):
+      if x.shape[1] > D:
+        raise ValueError(f'{x.shape[1]} joint dofs given, the system has {D}')
+      return torch.nn.functional.pad(x, (0, D - x.shape[1])).contiguous()
+
+    ja = pad(ja)
     if joint_velocity is None:
       jv = torch.zeros_like(ja)
     else:
-      jv = torch.as_tensor(joint_velocity, dtype=torch.float32,
-                           device=self.device).reshape(B, -1).contiguous()
+      jv = pad(torch.as_tensor(joint_velocity, dtype=torch.float32,
+                               device=self.device).reshape(B, -1))
     out = self._new_qp((B,))
     qs = qp_struct(out, True)
     _native.check(_native.lib().bx_system_default_qp(

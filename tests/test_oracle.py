@@ -3,6 +3,8 @@
 Float64 restatement vs the reference's own float64 numpy execution: agreement
 to ~1e-10 shows the restatement is the reference's algorithm, so it can check
 the HIP path at sizes the goldens do not cover."""
+import math
+
 import numpy as np
 import pytest
 
@@ -152,6 +154,24 @@ def test_wrapper_semantics(oracle_lib):
     assert np.array_equal(done, T['done'][t + 1])
     assert np.array_equal(steps, T['steps'][t + 1])
     assert np.array_equal(trunc, T['truncation'][t + 1])
+
+
+@pytest.mark.parametrize('target', [15., 30., 45., 90.])
+def test_spring_1d_actuator_float64(oracle_lib, target):
+  """Actuator1DTest (`physics_legacy_test.py:555-594`) as the reference runs
+  it (numpy float64): the diverging spring joint sends the bob to |pos| ~
+  1e84 while its unit rotation holds the target angle (2 places)."""
+  from brax_amd import compiler
+  from tests.test_gpu_spring_kat import ACT1, _cfg
+  vc, d, meta = compiler.compile_system(_cfg(ACT1))
+  o = oracle_lib.Oracle(d, compiler.compile_reset(vc, meta['body_index']), np.float64)
+  out, _ = o.system_step(o.default_qp(np.zeros((1, 1)), np.zeros((1, 1))), np.array([[target]]))
+  assert np.abs(out[0, 1, 0:3]).max() > 1e80
+  # Revolute.axis_angle (joints.py:311-319) about the joint's x axis: the
+  # rotation is about x alone, so the angle is 2 atan2(q_x, q_w) mod 2 pi
+  w, x = out[0, 1, 3], out[0, 1, 4]
+  ang = math.remainder(2 * math.atan2(x, w), 2 * math.pi)
+  assert round(abs(target * math.pi / 180 - ang), 2) == 0
 
 
 def test_force_kats_float64(oracle_lib):
