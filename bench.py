@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 # Algorithmic HBM bytes per Ant env-step: QP in 520 + QP out
 # 520 + action 32 + obs 348 + reward/done 8 = 1,428 B.
 ANT_BYTES_PER_ENV_STEP = 1428
+ANT_KERNEL = 'bx::env_step_kernel<16, 1, 0, 4>'  # rocprof name of the Ant env step
 # Counted flops per Ant Env.step (reference numpy path).
 ANT_FLOPS_PER_ENV_STEP = 87382
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8 TB/s HBM3E
@@ -277,11 +278,11 @@ def main():
     return
   bytes_per_launch = ANT_BYTES_PER_ENV_STEP * B
   achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+  # PMC traffic of THIS kernel instantiation (Ant: 16 lanes, SINGLE mode,
+  # feature mask 0, gather width 4), not the Humanoid one that shares its name
   tr = _traffic()
-  traffic = None
-  for name, k in ((tr or {}).get('kernels') or {}).items():
-    if 'env_step_kernel' in name and k.get('batch') == B:
-      traffic = k['hbm_bytes_per_launch']
+  k = ((tr or {}).get('kernels') or {}).get(ANT_KERNEL)
+  traffic = k['hbm_bytes_per_launch'] if k and k.get('batch') == B else None
   out = {
       'metric': 'env-steps/sec (Ant, 4096 envs/GPU)',
       'value': value,
@@ -303,7 +304,7 @@ def main():
       'roofline': {'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
                    'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
                    'traffic': traffic,
-                   'kernel': 'bx::env_step_kernel<16>', 'kernel_ms': kern_ms,
+                   'kernel': ANT_KERNEL, 'kernel_ms': kern_ms,
                    'span_ms_per_step': span_ms,
                    'bytes_per_launch': bytes_per_launch,
                    'note': 'fused env-step is VALU/latency-bound (AI ~61 flop/B, '
