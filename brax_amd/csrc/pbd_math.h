@@ -30,6 +30,10 @@ __device__ __forceinline__ v3 cross(v3 a, v3 b) {
 __device__ __forceinline__ float norm(v3 a) { return sqrtf(dot(a, a)); }
 
 // jnp safe_norm: 0 when every |x_i| <= 1e-8 (allclose(x, 0), jumpy.py:183-189)
+// sqrt stays correctly rounded here and in qnormalize: the bare v_sqrt_f32
+// (1 ulp) turns normalised vectors' unit dot products into 1 - ulp, and
+// acos near 1 magnifies that to 3.5e-4 rad (spherical joint angles at their
+// reference offset, physics_legacy_test.py:494-552; measured)
 __device__ __forceinline__ float safe_norm(v3 a) {
   bool z = fabsf(a.x) <= 1e-8f && fabsf(a.y) <= 1e-8f && fabsf(a.z) <= 1e-8f;
   return z ? 0.f : norm(a);
@@ -63,9 +67,34 @@ __device__ __forceinline__ q4 vec_quat_mul(v3 u, q4 v) {
           u.x * v.y - u.y * v.x + u.z * v.w};
 }
 // math.py:173-187
+// sin and cos of a half joint angle. Joint angles come from atan2 (clipped
+// to limits), so |x| <= pi/2: Cephes' single-precision minimax polynomials
+// on [-pi/4, pi/4], the upper band reflected through pi/2 - |x| (exact
+// Sterbenz subtraction + 3-part Cody-Waite pi/2), <= 1.5 ulp like the
+// library's; ~20 VALU instead of sincosf's 129 (its large-argument
+// reduction is evaluated branch-free). Larger |x| takes the library.
+__device__ __forceinline__ void sincos_half(float x, float* s, float* c) {
+  const float ax = fabsf(x);
+  if (ax > 1.57079637f) {
+    sincosf(x, s, c);
+    return;
+  }
+  const bool hi = ax > 0.785398163f;
+  const float y = ((1.5703125f - ax) + 4.837512969970703125e-4f) + 7.54978995489188216e-8f;
+  const float z = hi ? y : ax;
+  const float z2 = z * z;
+  const float sp =
+      fmaf(fmaf(fmaf(-1.9515295891e-4f, z2, 8.3321608736e-3f), z2, -1.6666654611e-1f), z2 * z, z);
+  const float cp = fmaf(
+      fmaf(fmaf(fmaf(2.443315711809948e-5f, z2, -1.388731625493765e-3f), z2, 4.166664568298827e-2f),
+           z2, -0.5f),
+      z2, 1.f);
+  *s = copysignf(hi ? cp : sp, x);
+  *c = hi ? sp : cp;
+}
 __device__ __forceinline__ q4 quat_rot_axis(v3 axis, float angle) {
   float s, c;
-  sincosf(angle * 0.5f, &s, &c);
+  sincos_half(angle * 0.5f, &s, &c);
   return {c, axis.x * s, axis.y * s, axis.z * s};
 }
 __device__ __forceinline__ q4 quat_inv(q4 q) { return {q.w, -q.x, -q.y, -q.z}; }
