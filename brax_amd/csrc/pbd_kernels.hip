@@ -1805,7 +1805,11 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     v3 ppos = q.pos;
     q4 prot = q.rot;
     v3 dpa_last = mk(0.f, 0.f, 0.f);
+#if defined(BX_SUB_UNROLL)
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
     for (int sub = 0; sub < 2; sub++) {
       ppos = q.pos;
       prot = q.rot;
@@ -2175,6 +2179,13 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
 // constant part copied to LDS once per workgroup, read there inside the loops)
 enum { MODE_GLOBAL = 0, MODE_SINGLE = 1, MODE_LDS = 2 };
 
+// step kernels: optional register-budget hint (A/B knob, BX_WAVES1)
+#if defined(BX_WAVES1)
+#define BX_STEP_ATTR __attribute__((amdgpu_waves_per_eu(1, 1)))
+#else
+#define BX_STEP_ATTR
+#endif
+
 // copies the constant blob into LDS (MODE_LDS); returns the env-area base
 template <int MODE>
 __device__ __forceinline__ float* stage_constants(const uint32_t* blob, const BlobHdr& H,
@@ -2192,7 +2203,7 @@ __device__ __forceinline__ float* stage_constants(const uint32_t* blob, const Bl
 }
 
 template <int L, int MODE, int F, int M>
-__global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
+__global__ void __launch_bounds__(64) BX_STEP_ATTR system_step_kernel(StepArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
   Cst c{A.blob};
@@ -2272,7 +2283,7 @@ __global__ void __launch_bounds__(64) system_step_kernel(StepArgs A) {
 
 // Env.step fused with EpisodeWrapper/AutoResetWrapper (wrappers.py:105-148)
 template <int L, int MODE, int F, int M>
-__global__ void __launch_bounds__(64) env_step_kernel(EnvArgs A) {
+__global__ void __launch_bounds__(64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
   BX_KSTAMP_DECL
   extern __shared__ __attribute__((aligned(16))) float smem[];
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
