@@ -6,14 +6,14 @@ to fp32-ulp relative input noise (6e-8). A step where the second is large is
 ill-conditioned in float64 itself: any fp32 execution, the reference's jit
 included, lands anywhere within that spread.
 
-  python tools/cond_probe.py box_box [n_samples]
+  python tests/diag/cond_probe.py box_box [n_samples]
 """
 import os
 import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from oracle import oracle as ol  # noqa: E402
 from tests.conftest import golden  # noqa: E402

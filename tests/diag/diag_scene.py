@@ -4,7 +4,7 @@ Prints, per step, the normwise pos/vel error of the HIP path and of the fp32
 oracle builds against the float64 golden, and the contact penetrations of
 the three where they differ.
 
-  python tools/diag_scene.py box_box
+  python tests/diag/diag_scene.py box_box
 """
 import os
 import sys
@@ -12,7 +12,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import brax_amd  # noqa: E402
 from brax_amd.base import qp_from_numpy  # noqa: E402
