@@ -391,8 +391,8 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // envs' records of one ds_read_b128 lane group land on distinct bank slots
   H.env_words = (off + 63) & ~63;
   size_t mx = 0;
+  int max_groups = 0;
   {
-    int max_groups = 0;
     for (int b = 0; b < N; b++) {
       mx = std::max({mx, jl[b].size(), al[b].size(), cl[b].size()});
       std::vector<int> gs;
@@ -425,6 +425,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       if (!d->col_oneway[g]) f |= 8;
     }
     if (d->n_forces > 0) f |= 16;
+    if (max_groups <= 1) f |= 32;  // F_G1: one collider group per body
     S->feat = f;
   }
   S->mode = S->single_ok ? 1 : 0;

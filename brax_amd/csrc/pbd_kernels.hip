@@ -184,6 +184,9 @@ __device__ __forceinline__ JointC load_joint(const Cst& c, const BlobHdr& H, int
 // capsule-plane), which keeps dead paths out of the register allocation.
 // ---------------------------------------------------------------------------
 enum { F_SPH = 1, F_ANGLE = 2, F_CC = 4, F_TW = 8, F_FORCE = 16, F_ALL = 31 };
+// F_G1 (outside F_ALL): every body's contact rows come from one collider
+// group, so the per-group normalisation needs one accumulator
+enum { F_G1 = 32 };
 template <int F> __device__ __forceinline__ bool is_rev(int type) {
   if constexpr ((F & F_SPH) == 0) return true; else return type == 1;
 }
@@ -1695,9 +1698,31 @@ __device__ __forceinline__ v3 gsum3(const GList<M>& g, const float* base, int st
 // per-group normalised contact sums  sum_g (sum of rows) / (eps + count), for
 // bodies whose rows come from at most two collider groups (checked on the
 // host); groups keep the reference's order (first group, then second)
-template <int M>
+template <bool G1, int M>
 __device__ __forceinline__ void gsum_contact(const GList<M>& g, const float* cslot, float eps,
                                              v3& a, q4& r, bool rot4) {
+  if constexpr (G1) {
+    // one group: the two-group form below with its second accumulator all
+    // exact zeros (0 / eps = 0, x + 0 = x), so the same bits at half the work
+    v3 a0 = mk(0.f, 0.f, 0.f);
+    q4 r0{0.f, 0.f, 0.f, 0.f};
+    float c0 = 0.f;
+#pragma unroll
+    for (int k = 0; k < M; k++) {
+      v3 v;
+      q4 q;
+      float f;
+      ld_slot(cslot + (g.e[k] & 0xFFFFFF) * SLOT_STRIDE, v, q, f);
+      if (!rot4) q = q4{0.f, q.w, q.x, q.y};
+      a0 = a0 + v;
+      r0 = r0 + q;
+      c0 += f;
+    }
+    const float d0 = eps + c0;
+    a = a0 / d0;
+    r = q4{r0.w / d0, r0.x / d0, r0.y / d0, r0.z / d0};
+    return;
+  }
   const int g0 = g.e[0] >> 24;
   v3 a0 = mk(0.f, 0.f, 0.f), a1 = mk(0.f, 0.f, 0.f);
   q4 r0{0.f, 0.f, 0.f, 0.f}, r1{0.f, 0.f, 0.f, 0.f};
@@ -1912,7 +1937,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     if (X.hasB) {
       v3 dp;
       q4 dr;
-      gsum_contact(X.cl, E.cslot, 1e-6f, dp, dr, true);
+      gsum_contact<(F & F_G1) != 0>(X.cl, E.cslot, 1e-6f, dp, dr, true);
       q.pos = q.pos + mul(dp, X.B.pm);
       q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                  q.rot.z + dr.z * X.B.qm.z};
@@ -1941,7 +1966,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     if (X.hasB) {
       v3 dv;
       q4 da;
-      gsum_contact(X.cl, E.cslot, 1e-6f, dv, da, false);
+      gsum_contact<(F & F_G1) != 0>(X.cl, E.cslot, 1e-6f, dv, da, false);
       v3 dav = mk(da.x, da.y, da.z);
       q.vel = mul(q.vel + dv, X.B.pm);
       q.ang = mul(q.ang + dav, X.B.rm);
@@ -2604,7 +2629,10 @@ static void launch_one(void (*k)(Args), dim3 grid, int tpb, size_t lds, hipStrea
   switch (feat) {                                                                   \
     case 0: launch_one<ARGS>(KERNEL<16, 1, 0, M>, grid, tpb, lds, s, a); break;     \
     case F_SPH: launch_one<ARGS>(KERNEL<16, 1, F_SPH, M>, grid, tpb, lds, s, a); break; \
+    case F_G1: launch_one<ARGS>(KERNEL<16, 1, F_G1, M>, grid, tpb, lds, s, a); break; \
+    case F_SPH | F_G1: launch_one<ARGS>(KERNEL<16, 1, F_SPH | F_G1, M>, grid, tpb, lds, s, a); break; \
     case F_CC | F_TW: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW, M>, grid, tpb, lds, s, a); break; \
+    case F_CC | F_TW | F_G1: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW, M>, grid, tpb, lds, s, a); break; \
     default: launch_one<ARGS>(KERNEL<16, 1, F_ALL, M>, grid, tpb, lds, s, a); break; \
   }
 #define BX_DISPATCH_SINGLE(KERNEL, ARGS)                                            \
