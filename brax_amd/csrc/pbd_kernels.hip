@@ -2052,10 +2052,13 @@ __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane)
 // ---------------------------------------------------------------------------
 
 // joint angles and velocities into E.ang (Joint.angle_vel, joints.py:197-226)
+// hj: the lane's register-hoisted joint (SINGLE mode, J <= L: joint j ==
+// lane), which spares the blob reloads on the observation path
 template <int L>
-__device__ void joint_angles(const Cst& c, const BlobHdr& H, const Env& E, int lane) {
+__device__ void joint_angles(const Cst& c, const BlobHdr& H, const Env& E, int lane,
+                             const JointC* hj = nullptr) {
   for (int j = lane; j < H.J; j += L) {
-    JointC Jc = load_joint(c, H, j);
+    JointC Jc = hj ? *hj : load_joint(c, H, j);
     QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), q = ldqp(E.qp + Jc.bc * QP_STRIDE);
     v3 axes[3];
     float ang[3];
@@ -2179,8 +2182,9 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
 
 template <int L>
 __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int lane, int kind,
-                            int obs_size, const float* act, int aw, bool valid, float* obs_out) {
-  joint_angles<L>(c, H, E, lane);
+                            int obs_size, const float* act, int aw, bool valid, float* obs_out,
+                            const JointC* hj = nullptr) {
+  joint_angles<L>(c, H, E, lane, hj);
   if ((kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP) && lane == 0) {
     v3 com;
     float msum;
@@ -2367,7 +2371,7 @@ __global__ void __launch_bounds__(64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
     }
     BX_KSTAMP(11);
     env_observe<L>(c, H, E, lane, kind, P.obs_size, act, aw, valid,
-                   valid ? A.out.obs + e * P.obs_size : nullptr);
+                   valid ? A.out.obs + e * P.obs_size : nullptr, S ? &X.J : nullptr);
     BX_KSTAMP(12);
     // reward / done / metrics (lane 0 of the env)
     if (lane == 0 && valid) {
