@@ -263,6 +263,40 @@ def test_full_batch_properties(dev, oracle_lib):
     _gate(got[..., sl], ref[..., sl], _env_err([o[0][..., sl] for o in outs], ref[..., sl]), f)
 
 
+@pytest.mark.parametrize('name', ['humanoid', 'ant_spring', 'halfcheetah_spring'])
+def test_full_batch_properties_other_envs(dev, oracle_lib, name):
+  """The same full-batch properties for the spherical-joint kernel variant
+  (Humanoid) and the legacy_spring item-loop kernel, at B = 4096."""
+  env = _make_env(name, dev)
+  B = 4096
+  st = env.reset_batch(np.array([0, 3], np.uint32), B)
+  g = torch.Generator(device='cpu').manual_seed(1)
+  A = env.action_size
+  for _ in range(2):
+    st = env.step(st, (torch.rand((B, A), generator=g) * 2 - 1).to(dev))
+  act = (torch.rand((B, A), generator=g) * 2 - 1).to(dev)
+  a = env.step(st, act)
+  b = env.step(st, act)
+  torch.cuda.synchronize()
+  assert torch.equal(a.qp.pos, b.qp.pos) and torch.equal(a.obs, b.obs)
+  from brax_amd.envs.env import State
+  small = State(qp=st.qp[:5], obs=st.obs[:5], reward=st.reward[:5], done=st.done[:5])
+  c = env.step(small, act[:5])
+  assert torch.equal(c.qp.pos, a.qp.pos[:5]) and torch.equal(c.obs, a.obs[:5])
+  assert torch.isfinite(a.obs).all()
+  vc, d, rd, meta = compiled(name)
+  o64 = oracle_lib.Oracle(d, rd, np.float64, safe_guard=True)
+  env32 = Envelope(oracle_lib, name, n_perturb=15)
+  idx = np.random.default_rng(1).choice(B, 64, replace=False)
+  qp_in = st.qp.numpy()[idx]
+  an = act.cpu().numpy()[idx].astype(np.float64)
+  ref, _ = o64.system_step(qp_in, an)
+  outs = env32.system(qp_in, an)
+  got = a.qp.numpy()[idx]
+  for f, sl in QP_FIELDS.items():
+    _gate(got[..., sl], ref[..., sl], _env_err([o[0][..., sl] for o in outs], ref[..., sl]), f)
+
+
 def test_strided_views_match_packed(dev):
   """A QP of separate contiguous (B,N,3)/(B,N,4) tensors (the reference's own
   layout) steps to the same bits as the packed (B,N,16) layout."""
