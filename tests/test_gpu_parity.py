@@ -6,10 +6,11 @@ Parity gate, per env and field, normwise
   every field:             tol = max(1e-5, 2 * E32)
   Ant (the north-star config) pos/rot additionally <= 1e-5 flat
 E32 is the fp32 error envelope of Brax's OWN algorithm on the same sample:
-the largest normwise error, vs the float64 reference, of the oracle's float32
-build (the reference algorithm executed in true fp32) over the exact inputs
-and three copies perturbed by fp32-ulp relative noise (x * (1 + U[-6e-8,6e-8]),
-SURVEY §8(c)'s conditioning probe). The HIP kernel must be as close to the
+the largest normwise error, vs the float64 reference, of the oracle's two
+float32 builds (the reference algorithm executed in true fp32, plain and with
+a*b+c contracted to FMA as XLA's jit does) over the exact inputs and copies
+perturbed by fp32-ulp relative noise (x * (1 + U[-6e-8,6e-8]), SURVEY §8(c)'s
+conditioning probe; 15 copies for the system steps, 3 for the env layer). The HIP kernel must be as close to the
 reference as fp32 rounding noise itself allows, within 2x. Velocities are
 (pos - pos_prev)/h, so fp32 rounding is amplified ~1/h per substep, and the
 contact masks (`penetration > 0`, `c < 0`, static-friction and sinking gates)
@@ -295,6 +296,23 @@ def test_full_batch_properties_other_envs(dev, oracle_lib, name):
   got = a.qp.numpy()[idx]
   for f, sl in QP_FIELDS.items():
     _gate(got[..., sl], ref[..., sl], _env_err([o[0][..., sl] for o in outs], ref[..., sl]), f)
+
+
+@pytest.mark.parametrize('name', XCOL + ['capsule_cull', 'mountain1nn'])
+def test_item_loop_batch_replicas(dev, name):
+  """The item-loop kernels at a full batch: 1024 replicas of one golden state
+  step to exactly the bits of that state stepped alone (no cross-env or
+  batch-size dependence in the extended contact functions, culling or SAT)."""
+  sys_ = _system(name, dev)
+  T = golden('traj_' + name)
+  q1 = T['qp'][0][:1]
+  a1 = T['action'][0][:1]
+  one, _ = sys_.step(_to_qp(q1, dev), torch.as_tensor(a1, dtype=torch.float32, device=dev))
+  B = 1024
+  many, _ = sys_.step(_to_qp(np.repeat(q1, B, axis=0), dev),
+                      torch.as_tensor(np.repeat(a1, B, axis=0), dtype=torch.float32, device=dev))
+  got, ref = _qp_np(many), _qp_np(one)
+  assert np.array_equal(got, np.repeat(ref, B, axis=0))
 
 
 def test_strided_views_match_packed(dev):
