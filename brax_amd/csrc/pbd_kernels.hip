@@ -644,11 +644,12 @@ __device__ __noinline__ void capsule_mesh_contact(const Cst& c, int o, const Row
 // ---- hull_hull: separating axis test between two boxes ---------------------
 // (colliders.py:851-888; geometry.py:580-914). Every row of a pair computes
 // the whole test and keeps its own contact e (4 rows a pair).
-// Divisions here are correctly rounded (pdiv), whatever the TU's flags: the
-// edge contact is valid only for barycentric t in [0, 1], and
-// t = (ota + la/2) / la lands exactly on 1 for a closest point at an edge
-// end; v_rcp_f32 + multiply overshoots to 1 + ulp there and drops the
-// contact (BoxBoxTest step 8, measured on the MI355X).
+// Divisions here are correctly rounded (pdiv), whatever the TU's flags, as
+// a guard: the edge contact is valid only for barycentric t in [0, 1], and
+// t = (ota + la/2) / la is exactly 1 for a closest point at an edge end,
+// where v_rcp_f32 + multiply could overshoot to 1 + ulp. (The BoxBoxTest
+// step-8 mismatch measured on the MI355X was the exact-equality test of the
+// support vertex against face-edge endpoints; hull_world fixes that below.)
 __device__ __forceinline__ v3 pdiv3(v3 a, float b) { return mk(pdiv(a.x, b), pdiv(a.y, b), pdiv(a.z, b)); }
 struct HullW {
   v3 v[8];
