@@ -1,16 +1,20 @@
 """Benchmark: env-steps/sec of Ant at 4096 envs per GPU (BASELINE.json).
 
-One step = one `Env.step` of `envs.create('ant', batch_size=B,
-episode_length=1000, auto_reset=True)`, i.e. ONE fused kernel launch doing
-10 PBD substeps + observation + reward + Episode/AutoReset, on synthetic
-U[-1,1] actions drawn on the device each step. Inputs are resident in HBM.
+One step = a fresh (B, 8) slab of synthetic U[-1,1] actions drawn on the
+device by the counter RNG (`bx_uniform`, the reference's published loop draws
+one per step, notebooks/environments.ipynb:386-423) + one `Env.step` of
+`envs.create('ant', batch_size=B, episode_length=1000, auto_reset=True)`,
+i.e. ONE fused kernel launch doing 10 PBD substeps + observation + reward +
+Episode/AutoReset. Inputs are resident in HBM.
 
     python bench.py [--gpus N --steps K --warmup W --batch B]
     torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU)
 
-Multi-GPU: every rank owns B envs (weak scaling, env ids offset by rank) and
-the only collective is an RCCL all-gather of the per-env (reward, done) pair
-each step. Prints ONE JSON line on rank 0.
+Multi-GPU: rank r owns the global envs [r*B, (r+1)*B) (weak scaling). Reset
+noise and actions are keyed by global env id with one shared seed, so the
+ranks together step exactly the envs of one N*B batch; the only collective is
+an RCCL all-gather of the per-env (reward, done) pair each step. Prints ONE
+JSON line on rank 0.
 """
 import argparse
 import json
@@ -185,6 +189,66 @@ def _traffic():
   return None
 
 
+def kernel_train(env, state, act, n=200):
+  """Duration of the fused env-step kernel alone: `n` back-to-back
+  `bx_env_step` launches (fixed input state and action, ping-pong free: in and
+  out never alias) bracketed by HIP events on the stream they run on. The span
+  covers the launches and their inter-kernel gaps, never host work, so it
+  cannot exceed a timed step."""
+  import ctypes as C
+  from brax_amd import _native, abi
+  from brax_amd.system import _stream, qp_struct
+  u = env.unwrapped
+  dev = u.sys.device
+  B = state.qp.pos.shape[0]
+  qp, obs, scal, met = u._alloc(B)  # pylint: disable=protected-access
+  p = u._params({'episode_length': 1000, 'action_repeat': 1, 'auto_reset': True},  # pylint: disable=protected-access
+                state.info['first_qp'], state.info['first_obs'])
+  sin = abi.BxEnvState()
+  sin.qp = qp_struct(state.qp, True)
+  sin.done = state.done.data_ptr()
+  sin.steps = state.info['steps'].data_ptr()
+  sout = abi.BxEnvState()
+  sout.qp = qp_struct(qp, True)
+  sout.obs = obs.data_ptr()
+  base = scal.data_ptr()
+  sout.reward, sout.done, sout.steps, sout.truncation = base, base + 4 * B, base + 8 * B, base + 12 * B
+  sout.metrics = met.data_ptr()
+  lib = _native.lib()
+  stream = _stream(dev.index)
+  args = (u.sys._h, C.byref(p), B, C.byref(sin), C.c_void_p(act.data_ptr()), act.stride(0),  # pylint: disable=protected-access
+          act.shape[1], C.byref(sout), stream)
+  for _ in range(10):
+    _native.check(lib.bx_env_step(*args))
+  torch.cuda.synchronize()
+  a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+  a.record()
+  for _ in range(n):
+    lib.bx_env_step(*args)
+  b.record()
+  torch.cuda.synchronize()
+  return a.elapsed_time(b) / n
+
+
+def _rocprof_avg(kernel):
+  """The committed rocprof average of `kernel` (profiles/rocprof_latest.json),
+  when it was profiled from this exact library build."""
+  import hashlib
+  p = os.path.join(ROOT, 'profiles', 'rocprof_latest.json')
+  if not os.path.exists(p):
+    return None
+  from brax_amd import _native
+  with open(_native.LIB_PATH, 'rb') as f:
+    sha = hashlib.sha1(f.read()).hexdigest()
+  with open(p) as f:
+    d = json.load(f)
+  k = d.get('kernels', {}).get(kernel)
+  if d.get('lib_sha1') != sha or not k:
+    return None
+  return {'avg_ms': k['avg_ns'] * 1e-6, 'calls': k.get('calls'), 'source': d.get('source'),
+          'lib_sha1': sha}
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
@@ -209,6 +273,7 @@ def main():
   dev = torch.device('cuda', local)
   torch.cuda.set_device(dev)
   from brax_amd import _native, envs
+  from brax_amd import distributed as bd
   import ctypes as C
 
   B = args.batch
@@ -220,23 +285,21 @@ def main():
     _native.check(_native.lib().bx_system_set_variant(env.sys._h, lanes, mode))
   if args.block:
     _native.check(_native.lib().bx_system_set_block(env.sys._h, args.block))
-  from brax_amd import distributed as bd
-  state = env.reset(bd.rank_key(np.array([0, 0x5EED], np.uint32), rank))
-  # synthetic U[-1,1] actions, one (B, 8) slab per step, drawn on the device by
-  # the counter RNG before the timed region (inputs resident in HBM)
-  n_act = args.warmup + args.steps
-  acts = torch.empty((n_act, B, 8), dtype=torch.float32, device=dev)
+  # rank r resets the global envs [r*B, (r+1)*B) of one shared seed
+  bd.shard_env(env, rank, B)
+  state = env.reset(np.array([0, 0x5EED], np.uint32))
+  A = env.action_size
   lib = _native.lib()
-  _native.check(lib.bx_uniform(C.c_void_p(acts.data_ptr()), acts.numel(), 1 + rank, 0, -1.0,
-                               1.0, C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+  stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+  act = torch.empty((B, A), dtype=torch.float32, device=dev)
   exchange = bd.EpisodeExchange(B, dev) if world > 1 else None
 
-  def one_step(st, k, ev=None):
-    if ev is not None:
-      ev[0].record()
-    st = env.step(st, acts[k])
-    if ev is not None:
-      ev[1].record()
+  def one_step(st, k):
+    # the step's action slab, keyed by (step, global env id): drawn on the
+    # device inside the timed region
+    lib.bx_uniform(C.c_void_p(act.data_ptr()), B * A, 1,
+                   bd.action_offset(rank, B, A, k, world), -1.0, 1.0, stream)
+    st = env.step(st, act)
     if exchange is not None:
       exchange(st.reward, st.done)  # the one RCCL collective: (reward, done) all-gather
     return st
@@ -247,25 +310,14 @@ def main():
   if dist is not None:
     dist.barrier()
   torch.cuda.synchronize()
-  # per-launch HIP events on every EVENT_EVERY-th step (the stream the kernel
-  # runs on): the kernel's average launch duration for `roofline`, without
-  # putting event packets between every pair of launches
-  EVENT_EVERY = 8
-  events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            if k % EVENT_EVERY == 0 else None for k in range(args.steps)]
-  span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-  span[0].record()
   t0 = time.perf_counter()
   for k in range(args.steps):
-    state = one_step(state, args.warmup + k, events[k])
-  span[1].record()
+    state = one_step(state, args.warmup + k)
   torch.cuda.synchronize()
   if dist is not None:
     dist.barrier()
   torch.cuda.synchronize()
   elapsed = time.perf_counter() - t0
-  kern_ms = float(np.mean([ev[0].elapsed_time(ev[1]) for ev in events if ev is not None]))
-  span_ms = span[0].elapsed_time(span[1]) / args.steps
   if dist is not None:
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -276,10 +328,13 @@ def main():
   if rank != 0:
     dist.destroy_process_group()
     return
+  kern_ms = kernel_train(env, state, act)
   bytes_per_launch = ANT_BYTES_PER_ENV_STEP * B
+  flops_per_launch = ANT_FLOPS_PER_ENV_STEP * B
+  tflops = flops_per_launch / (kern_ms * 1e-3) / 1e12
   achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
   # PMC traffic of THIS kernel instantiation (Ant: 16 lanes, SINGLE mode,
-  # feature mask 0, gather width 4), not the Humanoid one that shares its name
+  # feature mask F_G1, gather width 4)
   tr = _traffic()
   k = ((tr or {}).get('kernels') or {}).get(ANT_KERNEL)
   traffic = k['hbm_bytes_per_launch'] if k and k.get('batch') == B else None
@@ -295,22 +350,27 @@ def main():
       'scaling': 'weak',
       'vs_baseline': None,
       'dtype': 'f32',
-      'data': 'synthetic: U[-1,1] actions (device counter RNG, one slab per step, '
-              'resident in HBM); reset from the Ant config with device-RNG joint noise',
+      'data': 'synthetic: U[-1,1] actions drawn on the device each step inside the timed '
+              'region (counter RNG keyed by step and global env id); reset from the Ant '
+              'config with device-RNG joint noise keyed by global env id',
       'config': {'workload': 'Ant-v1 Env.step (10 PBD substeps + obs/reward + '
                              'Episode/AutoReset), envs.create(ant)',
                  'envs_per_gpu': B, 'episode_length': 1000, 'substeps': 10,
                  'parallelism': f'env-shard x{world}'},
-      'roofline': {'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
-                   'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
+      # the fused env step is VALU/latency-bound (AI ~61 flop/B):
+      # headline = counted flops / kernel time vs the FP32 VALU peak; the HBM
+      # view (algorithmic bytes / kernel time vs 8 TB/s) is kept beside it
+      'roofline': {'bound': 'valu', 'achieved': tflops, 'peak': FP32_VALU_PEAK_TFLOPS,
+                   'unit': 'TFLOP/s', 'frac': tflops / FP32_VALU_PEAK_TFLOPS,
                    'traffic': traffic,
                    'kernel': ANT_KERNEL, 'kernel_ms': kern_ms,
-                   'span_ms_per_step': span_ms,
+                   'kernel_ms_source': 'HIP events over 200 back-to-back bx_env_step launches '
+                                       'on the launch stream (kernel_train)',
+                   'rocprof': _rocprof_avg(ANT_KERNEL),
+                   'flops_per_launch': flops_per_launch,
                    'bytes_per_launch': bytes_per_launch,
-                   'note': 'fused env-step is VALU/latency-bound (AI ~61 flop/B, '
-                           'SURVEY 8(d)); compute view below',
-                   'valu_tflops': ANT_FLOPS_PER_ENV_STEP * B / (kern_ms * 1e-3) / 1e12,
-                   'valu_peak_tflops': FP32_VALU_PEAK_TFLOPS},
+                   'hbm': {'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                           'frac': achieved_gbs / HBM_PEAK_GBS, 'traffic': traffic}},
   }
   out['secondary_configs'] = None if args.no_secondary else secondary_configs(dev)
   out['phase_roofline'] = (None if args.no_phases else

@@ -42,6 +42,10 @@ _SIGS = {
     'bx_env_step': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64,
                      C.POINTER(abi.BxEnvState), C.c_void_p, C.c_int64, C.c_int64,
                      C.POINTER(abi.BxEnvState), C.c_void_p], C.c_int),
+    'bx_env_sizes': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.POINTER(C.c_int32),
+                      C.POINTER(C.c_int32)], C.c_int),
+    'bx_env_reset': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64, C.c_uint64, C.c_int64,
+                      C.c_void_p, C.c_float, C.POINTER(abi.BxEnvState), C.c_void_p], C.c_int),
     'bx_system_default_qp': ([C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                               C.POINTER(abi.BxQP), C.c_void_p], C.c_int),
     'bx_system_info': ([C.c_void_p, C.c_int64, C.POINTER(abi.BxQP), C.POINTER(abi.BxInfo),

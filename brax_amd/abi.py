@@ -12,7 +12,7 @@ i32p = C.POINTER(C.c_int32)
 f64p = C.POINTER(C.c_double)
 f32p = C.POINTER(C.c_float)
 
-ABI_VERSION = 3  # include/brax_amd.h BX_ABI_VERSION
+ABI_VERSION = 4  # include/brax_amd.h BX_ABI_VERSION
 
 _DESC_FIELDS = [
     ('n_bodies', C.c_int32), ('n_joints', C.c_int32), ('n_actuators', C.c_int32),
@@ -45,6 +45,7 @@ _DESC_FIELDS = [
 ]
 
 DYN_PBD, DYN_LEGACY_SPRING = 0, 1
+OBS_XY = 1  # BX_OBS_XY: exclude_current_positions_from_observation=False
 _SPRING_FIELDS = ('joint_stiffness', 'joint_spring_damping', 'joint_limit_strength')
 
 
@@ -59,7 +60,7 @@ class BxResetDesc(C.Structure):
       ('fk_off_p', f64p), ('fk_off_c', f64p), ('base_qp', f64p),
       ('n_zpts', C.c_int32), ('zpt_body', i32p), ('zpt_local', f64p),
       ('zpt_radius', f64p), ('body_zero_cand', i32p), ('body_root_group', i32p),
-      ('n_root_groups', C.c_int32),
+      ('n_root_groups', C.c_int32), ('default_angle', f64p),
   ]
 
 
@@ -91,7 +92,7 @@ class BxEnvParams(C.Structure):
   _fields_ = [('kind', C.c_int32), ('obs_size', C.c_int32),
               ('n_metrics', C.c_int32), ('episode_length', C.c_int32),
               ('action_repeat', C.c_int32), ('auto_reset', C.c_int32),
-              ('coef', C.c_float * 8),
+              ('obs_flags', C.c_int32), ('coef', C.c_float * 8),
               ('first_qp', BxQP), ('first_obs', C.c_void_p)]
 
 
@@ -158,8 +159,14 @@ def info_rows(d):
   return int(sum(int(c) if c else int((groups == g).sum()) for g, c in enumerate(cut)))
 
 
-def make_reset_desc(r):
+def make_reset_desc(r, num_joint_dof=None):
+  """Reset descriptor -> (BxResetDesc, keepalive). default_angle is padded
+  with zeros to num_joint_dof (the kernels' joint-angle stride)."""
   keep = []
+  r = dict(r)
+  da = np.asarray(r.get('default_angle', np.zeros(0)), np.float64)
+  n = len(da) if num_joint_dof is None else int(num_joint_dof)
+  r['default_angle'] = np.pad(da, (0, max(n - len(da), 0)))[:max(n, len(da))]
   s = BxResetDesc()
   s.n_fk = len(r['fk_body_p'])
   s.n_zpts = len(r['zpt_body'])

@@ -851,4 +851,5 @@ def compile_reset(config, index, default_index=0):
   out['zpt_local'] = np.asarray(zl, np.float64).reshape(-1, 3)
   out['zpt_radius'] = np.asarray(zr, np.float64)
   out['body_zero_cand'] = zero
+  out['default_angle'] = default_angle(config, default_index)
   return out

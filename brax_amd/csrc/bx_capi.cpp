@@ -358,6 +358,9 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       }
     }
     B.i(H.o_zoff + N, k);
+    H.o_dangle = B.alloc(d->num_joint_dof);
+    for (int k = 0; k < d->num_joint_dof; k++)
+      B.f(H.o_dangle + k, r->default_angle ? r->default_angle[k] : 0.0);
     H.o_zero = B.alloc(N);
     H.o_rgroup = B.alloc(N);
     for (int b = 0; b < N; b++) {
@@ -440,6 +443,71 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Every entry point that touches device memory runs with the system's device
+// current and restores the caller's afterwards (HIP launches go to the current
+// device; a process may hold systems on several GPUs).
+struct DeviceScope {
+  int prev = -1, want;
+  hipError_t err = hipSuccess;
+  explicit DeviceScope(int d) : want(d) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != want) err = hipSetDevice(want);
+  }
+  ~DeviceScope() {
+    if (prev >= 0 && prev != want) (void)hipSetDevice(prev);
+  }
+};
+#define DEVICE_SCOPE(S)                                                             \
+  DeviceScope _dev((S)->device);                                                    \
+  if (_dev.err != hipSuccess) return fail(std::string("device ") + std::to_string((S)->device) + \
+                                          ": " + hipGetErrorString(_dev.err))
+
+// obs / metric widths of each env kind's layer (the kernel's obs_elem and
+// reward code), from the system's shape: ant.py:257-282, humanoid.py:282-334,
+// half_cheetah.py:200-214, humanoid_standup.py:249-289
+int env_sizes(const bx_system* S, const bx_env_params* P, int* obs, int* met) {
+  const BlobHdr& H = S->hdr;
+  const int D = H.D, N = H.N;
+  const bool xy = (P->obs_flags & BX_OBS_XY) != 0;
+  if (P->obs_flags & ~BX_OBS_XY) return fail("unknown obs_flags bits");
+  switch (P->kind) {
+    case BX_ENV_ANT:
+      *obs = 1 + 4 + D + 3 + 3 + D + (P->coef[7] != 0.f ? 6 * N : 0) + (xy ? 2 : 0);
+      *met = 10;
+      return 0;
+    case BX_ENV_HUMANOID:
+    case BX_ENV_HUMANOID_STANDUP: {
+      if (xy && P->kind == BX_ENV_HUMANOID_STANDUP)
+        return fail("HumanoidStandup has no current-position observation option");
+      int qfrc = 0;
+      for (int a = 0; a < H.K; a++) {
+        int j = (int)S->host[H.o_act + a * ACT_STRIDE + A_JOINT];
+        qfrc += (int)S->host[H.o_joint + j * JOINT_STRIDE + J_DOF];
+      }
+      *obs = 1 + 4 + D + 3 + 3 + D + 15 * (N - 1) + qfrc + (xy ? 2 : 0);
+      *met = P->kind == BX_ENV_HUMANOID ? 9 : 2;
+      return 0;
+    }
+    case BX_ENV_HALFCHEETAH:
+      *obs = 3 + D + 3 + D + (xy ? 1 : 0);
+      *met = 4;
+      return 0;
+  }
+  return fail("unknown env kind");
+}
+
+int check_env(const bx_system* S, const bx_env_params* P) {
+  int obs = 0, met = 0;
+  if (env_sizes(S, P, &obs, &met)) return 1;
+  if (P->obs_size != obs)
+    return fail("obs_size " + std::to_string(P->obs_size) + " != " + std::to_string(obs) +
+                " for this env kind and system");
+  if (P->n_metrics != met)
+    return fail("n_metrics " + std::to_string(P->n_metrics) + " != " + std::to_string(met) +
+                " for this env kind");
+  return 0;
+}
+
 size_t step_lds(const bx_system* S) {
   size_t b = (size_t)(S->tpb / S->L) * S->hdr.env_words * 4;
   if (S->mode == 2) b += (size_t)S->hdr.const_words * 4;
@@ -472,7 +540,8 @@ int bx_system_create(const bx_desc* desc, const bx_reset_desc* reset, int device
     delete S;
     return rc;
   }
-  hipError_t e = hipSetDevice(device);
+  DeviceScope dev(device);
+  hipError_t e = dev.err;
   if (e == hipSuccess) e = hipMalloc(&S->blob, S->host.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(S->blob, S->host.data(), S->host.size() * 4, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -488,7 +557,7 @@ int bx_system_create(const bx_desc* desc, const bx_reset_desc* reset, int device
 int bx_system_destroy(bx_system* S) {
   if (!S) return 0;
   if (S->blob) {
-    (void)hipSetDevice(S->device);
+    DEVICE_SCOPE(S);
     HIP_OK(hipFree(S->blob));
   }
   delete S;
@@ -549,6 +618,7 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
                    int64_t act_stride, int64_t act_width, const bx_qp* qout, const bx_info* info,
                    void* stream) {
   if (!S || !qin || !qout) return fail("null argument");
+  DEVICE_SCOPE(S);
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
   if (!qp_ok(*qin) || !qp_ok(*qout)) return fail("null qp field");
   if (check_act(S, act, act_stride, act_width)) return 1;
@@ -572,7 +642,9 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
                 const float* act, int64_t act_stride, int64_t act_width, const bx_env_state* out,
                 void* stream) {
   if (!S || !env || !in || !out) return fail("null argument");
+  DEVICE_SCOPE(S);
   if (check_act(S, act, act_stride, act_width)) return 1;
+  if (check_env(S, env)) return 1;
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
   if (!qp_ok(in->qp) || !qp_ok(out->qp)) return fail("null qp field");
   if (!in->done || !out->done || !out->reward || !out->obs) return fail("null env buffer");
@@ -580,7 +652,6 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
     return fail("auto_reset needs first_qp and first_obs");
   if (env->episode_length > 0 && (!out->steps || !out->truncation))
     return fail("episode wrapper needs steps and truncation buffers");
-  if (env->kind < BX_ENV_ANT || env->kind > BX_ENV_HUMANOID_STANDUP) return fail("unknown env kind");
   EnvArgs a{};
   a.blob = S->blob;
   a.n_envs = n_envs;
@@ -599,6 +670,7 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
 
 int bx_system_info(bx_system* S, int64_t n_envs, const bx_qp* qp, const bx_info* info, void* stream) {
   if (!S || !qp || !info) return fail("null argument");
+  DEVICE_SCOPE(S);
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
   InfoArgs a{};
   a.blob = S->blob;
@@ -613,6 +685,12 @@ int bx_env_observe(bx_system* S, const bx_env_params* env, int64_t n_envs, const
                    const float* act, int64_t act_stride, int64_t act_width, float* obs,
                    void* stream) {
   if (!S || !env || !qp || !obs) return fail("null argument");
+  DEVICE_SCOPE(S);
+  if (check_env(S, env)) return 1;
+  if (act_width < 0 || act_stride < 0) return fail("negative action width or stride");
+  if ((env->kind == BX_ENV_HUMANOID || env->kind == BX_ENV_HUMANOID_STANDUP) && S->hdr.K > 0 &&
+      (!act || act_width == 0))
+    return fail("the humanoid observation reads the action (qfrc_actuator)");
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
   InfoArgs a{};
   a.blob = S->blob;
@@ -620,6 +698,7 @@ int bx_env_observe(bx_system* S, const bx_env_params* env, int64_t n_envs, const
   a.q = *qp;
   a.kind = env->kind;
   a.obs_size = env->obs_size;
+  a.obs_flags = env->obs_flags;
   a.act = act;
   a.act_stride = act_stride;
   a.act_width = act_width;
@@ -631,6 +710,7 @@ int bx_env_observe(bx_system* S, const bx_env_params* env, int64_t n_envs, const
 int bx_system_joint_angles(bx_system* S, int64_t n_envs, const bx_qp* qp, float* angle,
                            float* vel, void* stream) {
   if (!S || !qp) return fail("null argument");
+  DEVICE_SCOPE(S);
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
   if (S->hdr.D == 0) return 0;
   if (!angle || !vel) return fail("null angle or velocity buffer");
@@ -644,9 +724,62 @@ int bx_system_joint_angles(bx_system* S, int64_t n_envs, const bx_qp* qp, float*
   return 0;
 }
 
+int bx_env_sizes(bx_system* S, const bx_env_params* env, int32_t* obs_size, int32_t* n_metrics) {
+  if (!S || !env || !obs_size || !n_metrics) return fail("null argument");
+  int o = 0, m = 0;
+  if (env_sizes(S, env, &o, &m)) return 1;
+  *obs_size = o;
+  *n_metrics = m;
+  return 0;
+}
+
+int bx_env_reset(bx_system* S, const bx_env_params* env, int64_t n_envs, uint64_t seed,
+                 int64_t env_offset, const uint64_t* env_seeds, float noise_scale,
+                 const bx_env_state* out, void* stream) {
+  if (!S || !env || !out) return fail("null argument");
+  DEVICE_SCOPE(S);
+  if (S->hdr.o_base == 0) return fail("system was created without a reset descriptor");
+  if (check_env(S, env)) return 1;
+  if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
+  if (env_offset < 0) return fail("negative env_offset");
+  if (!(noise_scale >= 0.f)) return fail("noise_scale must be >= 0");
+  if (!qp_ok(out->qp) || !out->obs || !out->reward || !out->done) return fail("null env buffer");
+  if (env->n_metrics > 0 && !out->metrics) return fail("null metrics buffer");
+  ResetArgs r{};
+  r.blob = S->blob;
+  r.n_envs = n_envs;
+  r.out = out->qp;
+  r.gen = 1;
+  r.seed = seed;
+  r.env_offset = env_offset;
+  r.seeds = env_seeds;
+  r.scale = noise_scale;
+  HIP_OK(launch_default_qp(n_envs, S->lds_reset, as_stream(stream), r));
+  InfoArgs a{};
+  a.blob = S->blob;
+  a.n_envs = n_envs;
+  a.q = out->qp;
+  a.kind = env->kind;
+  a.obs_size = env->obs_size;
+  a.obs_flags = env->obs_flags;
+  a.obs = out->obs;
+  // _get_obs(qp, info, jp.zeros(action_size)): a null action reads as zeros
+  a.act = nullptr;
+  a.act_width = 0;
+  a.zero_reward = out->reward;
+  a.zero_done = out->done;
+  a.zero_steps = out->steps;
+  a.zero_trunc = out->truncation;
+  a.zero_metrics = out->metrics;
+  a.n_metrics = env->n_metrics;
+  HIP_OK(launch_info_obs(S->L, n_envs, S->lds_env, as_stream(stream), a));
+  return 0;
+}
+
 int bx_system_default_qp(bx_system* S, int64_t n_envs, const float* joint_angle,
                          const float* joint_velocity, const bx_qp* qp_out, void* stream) {
   if (!S || !qp_out) return fail("null argument");
+  DEVICE_SCOPE(S);
   if (S->hdr.o_base == 0) return fail("system was created without a reset descriptor");
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
   if (S->hdr.num_joint_dof > 0 && (!joint_angle || !joint_velocity)) return fail("null joint arrays");
@@ -665,6 +798,7 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 int bx_phase(bx_system* S, int which, int64_t n_envs, int64_t plane, const float* in, float* out,
              const float* aux, int64_t aux_plane, void* stream) {
   if (!S || !in || !out) return fail("null argument");
+  DEVICE_SCOPE(S);
   if (which < 0 || which > 2) return fail("unknown phase");
   if (n_envs <= 0 || n_envs % 4) return fail("n_envs must be a positive multiple of 4");
   const int64_t N = S->hdr.N;
@@ -679,6 +813,7 @@ int bx_phase(bx_system* S, int which, int64_t n_envs, int64_t plane, const float
 int bx_phase_capsule_plane(bx_system* S, int64_t n_envs, int64_t plane, const float* in, float* out,
                            int64_t out_plane, void* stream) {
   if (!S || !in || !out) return fail("null argument");
+  DEVICE_SCOPE(S);
   if (n_envs <= 0 || n_envs % 4) return fail("n_envs must be a positive multiple of 4");
   const int64_t N = S->hdr.N, R = S->hdr.R;
   if (plane < N * n_envs || plane % 4) return fail("plane stride must be >= N*n_envs and a multiple of 4");

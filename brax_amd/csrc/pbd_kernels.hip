@@ -2091,10 +2091,21 @@ __device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3
 }
 
 // observation element i of the env kind
-__device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind, int i,
+__device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind, int flags, int i,
                           const float* act, int aw, bool valid) {
   const int N = H.N, D = H.D;
   const float* q0 = E.qp;
+  // exclude_current_positions_from_observation=False: the torso's x (and y)
+  // precede z (ant.py:262-265, humanoid.py:289-292, half_cheetah.py:206-209)
+  if (flags & BX_OBS_XY) {
+    if (kind == BX_ENV_HALFCHEETAH) {
+      if (i == 0) return q0[0];
+      i -= 1;
+    } else {
+      if (i < 2) return q0[i];
+      i -= 2;
+    }
+  }
   if (kind == BX_ENV_ANT) {
     if (i == 0) return q0[2];
     i -= 1;
@@ -2181,9 +2192,11 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
   return 0.f;
 }
 
+// obs_out null: nothing written (an env past the batch); act null: the
+// action reads as zeros (reset's _get_obs(qp, info, jp.zeros(action_size)))
 template <int L>
 __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int lane, int kind,
-                            int obs_size, const float* act, int aw, bool valid, float* obs_out,
+                            int flags, int obs_size, const float* act, int aw, float* obs_out,
                             const JointC* hj = nullptr) {
   joint_angles<L>(c, H, E, lane, hj);
   if ((kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP) && lane == 0) {
@@ -2194,8 +2207,9 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
     E.red[35] = msum;
   }
   sync();
-  if (valid)
-    for (int i = lane; i < obs_size; i += L) obs_out[i] = obs_elem(c, H, E, kind, i, act, aw, valid);
+  if (obs_out)
+    for (int i = lane; i < obs_size; i += L)
+      obs_out[i] = obs_elem(c, H, E, kind, flags, i, act, aw, act != nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -2371,7 +2385,7 @@ __global__ void __launch_bounds__(64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
       pbd_step<L>(c, H, E, lane, valid, act, aw);
     }
     BX_KSTAMP(11);
-    env_observe<L>(c, H, E, lane, kind, P.obs_size, act, aw, valid,
+    env_observe<L>(c, H, E, lane, kind, P.obs_flags, P.obs_size, act, aw,
                    valid ? A.out.obs + e * P.obs_size : nullptr, S ? &X.J : nullptr);
     BX_KSTAMP(12);
     // reward / done / metrics (lane 0 of the env)
@@ -2518,15 +2532,37 @@ __global__ void __launch_bounds__(64) info_obs_kernel(InfoArgs A) {
   }
   if (A.obs) {
     const float* act = valid && A.act ? A.act + e * A.act_stride : nullptr;
-    env_observe<L>(c, H, E, lane, A.kind, A.obs_size, act, (int)A.act_width, valid && act != nullptr,
+    env_observe<L>(c, H, E, lane, A.kind, A.obs_flags, A.obs_size, act, (int)A.act_width,
                    valid ? A.obs + e * A.obs_size : nullptr);
   }
+  // reset: reward, done, steps, truncation and metrics start at zero
+  // (ant.py:205-219, wrappers.py:94-97)
+  if (valid) {
+    if (lane == 0) {
+      if (A.zero_reward) A.zero_reward[e] = 0.f;
+      if (A.zero_done) A.zero_done[e] = 0.f;
+      if (A.zero_steps) A.zero_steps[e] = 0.f;
+      if (A.zero_trunc) A.zero_trunc[e] = 0.f;
+    }
+    if (A.zero_metrics)
+      for (int i = lane; i < A.n_metrics; i += L) A.zero_metrics[e * A.n_metrics + i] = 0.f;
+  }
+}
+
+// counter-based uniform: splitmix64 of (seed, global index) -> [lo, hi)
+__device__ __forceinline__ float uniform_at(uint64_t seed, uint64_t i, float lo, float hi) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + i + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  float u = (float)(z >> 40) * (1.0f / 16777216.0f);
+  return lo + (hi - lo) * u;
 }
 
 // System.default_qp (system.py:112-242): one thread per env (reset path)
 
 
-#if !defined(BX_TU_FAST)  // reset / RNG kernels: IEEE translation unit
+#if !defined(BX_TU_FAST)  // reset / RNG kernels: the generic translation unit
 __global__ void __launch_bounds__(64) default_qp_kernel(ResetArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Cst c{A.blob};
@@ -2537,15 +2573,23 @@ __global__ void __launch_bounds__(64) default_qp_kernel(ResetArgs A) {
   const int N = H.N, D = H.num_joint_dof;
   for (int b = 0; b < N; b++)
     for (int k = 0; k < 13; k++) q[b * 13 + k] = c.f(H.o_base + b * 13 + k);
-  const float* ja = A.angle + e * D;
-  const float* jv = A.vel + e * D;
+  const float* ja = A.gen ? nullptr : A.angle + e * D;
+  const float* jv = A.gen ? nullptr : A.vel + e * D;
+  // Env.reset noise (ant.py:200-203): keyed by the global env id
+  const uint64_t seed = A.seeds ? A.seeds[e] : A.seed;
+  const uint64_t g0 = A.seeds ? 0ull : (uint64_t)(A.env_offset + e) * (uint64_t)(2 * D);
   for (int f = 0; f < H.n_fk; f++) {
     int o = H.o_fk + f * FK_STRIDE;
     float a3[3], v3_[3];
     for (int l = 0; l < 3; l++) {
       int ix = c.i(o + FK_IDX + l);
-      a3[l] = ix >= 0 ? ja[ix] : 0.f;
-      v3_[l] = ix >= 0 ? jv[ix] : 0.f;
+      if (A.gen) {
+        a3[l] = ix >= 0 ? c.f(H.o_dangle + ix) + uniform_at(seed, g0 + ix, -A.scale, A.scale) : 0.f;
+        v3_[l] = ix >= 0 ? uniform_at(seed, g0 + D + ix, -A.scale, A.scale) : 0.f;
+      } else {
+        a3[l] = ix >= 0 ? ja[ix] : 0.f;
+        v3_[l] = ix >= 0 ? jv[ix] : 0.f;
+      }
     }
     q4 jr{c.f(o + FK_ROT), c.f(o + FK_ROT + 1), c.f(o + FK_ROT + 2), c.f(o + FK_ROT + 3)};
     q4 rot{c.f(o + FK_REF), c.f(o + FK_REF + 1), c.f(o + FK_REF + 2), c.f(o + FK_REF + 3)};
@@ -2598,12 +2642,7 @@ __global__ void uniform_kernel(float* out, int64_t n, uint64_t seed, uint64_t of
                                float hi) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint64_t z = seed * 0x9E3779B97F4A7C15ull + (uint64_t)(i + offset) + 0x632BE59BD9B4E019ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z = z ^ (z >> 31);
-  float u = (float)(z >> 40) * (1.0f / 16777216.0f);
-  out[i] = lo + (hi - lo) * u;
+  out[i] = uniform_at(seed, (uint64_t)i + offset, lo, hi);
 }
 
 #endif
@@ -2625,11 +2664,11 @@ static void launch_one(void (*k)(Args), dim3 grid, int tpb, size_t lds, hipStrea
 
 // instantiated variants: (lanes, mode, features, gather width). This file is
 // compiled twice (Makefile): BX_TU_FAST holds the register-hoisted SINGLE-mode
-// kernels, built with fast reciprocal division; BX_TU_GENERIC holds the
-// item-loop kernels (large scenes, legacy_spring, the extended contact
-// functions) and the reset / info kernels, built with IEEE division. Single
-// mode at 16 lanes is specialised per feature set and gather width;
-// everything else carries all features.
+// kernels; BX_TU_GENERIC holds the item-loop kernels (large scenes,
+// legacy_spring, the extended contact functions) and the reset / info
+// kernels. Both are built with fast reciprocal division by default
+// (GENERIC_PRECISE=1: IEEE division in the second). Single mode at 16 lanes is
+// specialised per feature set and gather width.
 #define BX_SINGLE16(KERNEL, ARGS, M)                                                \
   switch (feat) {                                                                   \
     case 0: launch_one<ARGS>(KERNEL<16, 1, 0, M>, grid, tpb, lds, s, a); break;     \

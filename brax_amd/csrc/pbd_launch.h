@@ -28,12 +28,19 @@ struct InfoArgs {
   int64_t n_envs;
   bx_qp q;
   bx_info info;
-  int kind, obs_size;
+  int kind, obs_size, obs_flags;
   const float* act;
   int64_t act_stride, act_width;
   float* obs;
   float* angle;  // joint angles (B, D) and velocities (B, D), or null
   float* angvel;
+  // reset: env scalars written as zeros (null = skip)
+  float* zero_reward;
+  float* zero_done;
+  float* zero_steps;
+  float* zero_trunc;
+  float* zero_metrics;
+  int n_metrics;
 };
 struct ResetArgs {
   const uint32_t* blob;
@@ -41,6 +48,14 @@ struct ResetArgs {
   const float* angle;
   const float* vel;
   bx_qp out;
+  // gen = 1: angle = default_angle + U(seed, g*2D + k), vel = U(seed, g*2D + D + k)
+  // with g = env_offset + e and U uniform in [-scale, scale) (angle/vel unused);
+  // seeds non-null: env e uses (seeds[e], k) and (seeds[e], D + k)
+  int gen;
+  uint64_t seed;
+  int64_t env_offset;
+  const uint64_t* seeds;
+  float scale;
 };
 
 // SINGLE-mode step kernels (fast-reciprocal translation unit)
@@ -48,7 +63,7 @@ hipError_t launch_system_step_single(int L, int feat, int gw, int tpb, int64_t n
                                      hipStream_t s, const StepArgs& a);
 hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
                                   hipStream_t s, const EnvArgs& a);
-// item-loop step kernels (IEEE-division translation unit)
+// item-loop step kernels (generic translation unit)
 hipError_t launch_system_step_generic(int L, int mode, int tpb, int64_t n_envs, size_t lds,
                                       hipStream_t s, const StepArgs& a);
 hipError_t launch_env_step_generic(int L, int mode, int tpb, int64_t n_envs, size_t lds,

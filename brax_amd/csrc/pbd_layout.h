@@ -82,6 +82,7 @@ struct BlobHdr {
   int32_t spring;                    // dynamics_mode == legacy_spring
   int32_t o_hm;                      // height map grids
   int32_t o_hull;                    // box hulls: 8 corners, 6x4 quad points, 6 normals
+  int32_t o_dangle;                  // reset: System.default_angle (num_joint_dof)
 };
 enum { HULL_STRIDE = 114, HULL_V = 0, HULL_F = 24, HULL_N = 96 };
 

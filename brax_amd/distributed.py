@@ -1,10 +1,12 @@
 """Multi-GPU sharding of env batches.
 
 The physics never crosses GPUs: rank r owns the contiguous global env ids
-[r*B, (r+1)*B) and its reset/action RNG streams are keyed by rank. The only
-collective is the per-step (reward, done) all-gather over RCCL (backend
-"nccl" on ROCm) — or gloo for host tensors in tests. The reference's analogue
-is `jax.pmap` env sharding (`agents/ppo/train.py:112,276-283`).
+[r*B, (r+1)*B). Reset noise and synthetic actions are keyed by GLOBAL env id
+(one shared seed, `env_offset = r*B`), so N shards of B envs hold exactly the
+states of one batch of N*B envs, whatever the GPU count. The only collective
+is the per-step (reward, done) all-gather over RCCL (backend "nccl" on ROCm) —
+or gloo for host tensors in tests. The reference's analogue is `jax.pmap` env
+sharding by global index (`agents/ppo/train.py:276-283`).
 """
 import numpy as np
 import torch
@@ -16,12 +18,19 @@ def env_range(rank: int, envs_per_rank: int):
   return rank * envs_per_rank, (rank + 1) * envs_per_rank
 
 
-def rank_key(rng, rank: int):
-  """Per-rank reset key: (seed_hi ^ rank, seed_lo) keeps streams disjoint."""
-  k = np.asarray(rng, np.uint32).reshape(-1)
-  hi = int(k[0]) if k.size > 1 else 0
-  lo = int(k[-1])
-  return np.array([(hi ^ (0x9E37 * (rank + 1))) & 0xFFFFFFFF, lo], np.uint32)
+def shard_env(env, rank: int, envs_per_rank: int):
+  """Makes `env` (any wrapper chain over a kernel env) the shard of global
+  envs [rank*B, (rank+1)*B): its resets draw the noise of those env ids."""
+  env.unwrapped.env_offset = env_range(rank, envs_per_rank)[0]
+  return env
+
+
+def action_offset(rank: int, envs_per_rank: int, action_size: int, step: int = 0,
+                  world: int = 1):
+  """`bx_uniform` offset of rank r's (B, A) action slab at `step` in a
+  stream keyed by (step, global env id, action index): slab t of the whole
+  job starts at t * world * B * A, rank r's rows at r * B * A within it."""
+  return (step * world + rank) * envs_per_rank * action_size
 
 
 class EpisodeExchange:

@@ -2,10 +2,12 @@
 
 obs = [torso z, torso rot(4), joint angles(8), torso vel(3), torso ang(3),
 joint vels(8), clip(contact.vel)(10x3), clip(contact.ang)(10x3)] = 87 with
-use_contact_forces (the registered 'ant'), else 27 (`ant.py:257-282`).
+use_contact_forces (the registered 'ant'), else 27 (`ant.py:257-282`); torso
+x, y lead it when exclude_current_positions_from_observation is False.
 """
 import numpy as np
 
+from brax_amd import abi
 from brax_amd.envs import configs
 from brax_amd.envs import robots
 from brax_amd.envs.env import PhysicsEnv
@@ -24,8 +26,6 @@ class Ant(PhysicsEnv):
                healthy_reward=1.0, terminate_when_unhealthy=True, healthy_z_range=(0.2, 1.0),
                reset_noise_scale=0.1, exclude_current_positions_from_observation=True,
                legacy_spring=False, **kwargs):
-    if not exclude_current_positions_from_observation:
-      raise NotImplementedError('exclude_current_positions_from_observation=False')
     # `ant.py:183-184`: legacy_spring selects _SYSTEM_CONFIG_SPRING
     super().__init__(robots.ANT_SPRING_CONFIG if legacy_spring else configs.ANT_CONFIG, **kwargs)
     self.reset_noise_scale = reset_noise_scale
@@ -34,5 +34,7 @@ class Ant(PhysicsEnv):
                           healthy_z_range[0], healthy_z_range[1],
                           1.0 if terminate_when_unhealthy else 0.0,
                           1.0 if use_contact_forces else 0.0], np.float32)
-    D = self.sys.num_joint_dof
-    self.obs_size = 1 + 4 + D + 3 + 3 + D + (6 * self.sys.num_bodies if use_contact_forces else 0)
+    # exclude_current_positions_from_observation=False: torso x, y lead the
+    # obs (ant.py:262-265)
+    self.obs_flags = 0 if exclude_current_positions_from_observation else abi.OBS_XY
+    self._set_sizes()

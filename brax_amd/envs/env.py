@@ -114,22 +114,38 @@ class PhysicsEnv(Env):
 
   kind = 0
   metric_keys = ()
+  obs_flags = 0  # abi.OBS_XY: exclude_current_positions_from_observation=False
 
   def __init__(self, config, batch_size=None, device=None, **kwargs):
     super().__init__(config, device=device)
     self.batch_size = batch_size
     self.coef = np.zeros(8, np.float32)
+    # global id of this batch's first env: reset noise is keyed by global env
+    # id, so a shard (env_offset = rank * B) resets to exactly those envs of
+    # one big batch (brax_amd.distributed.shard_env)
+    self.env_offset = 0
 
   # -------------------------------------------------------------- helpers
+  def _set_sizes(self):
+    """obs_size from the C ABI's own count for this kind and system
+    (`bx_env_sizes`), checked against the Python metric keys."""
+    p = self._params()
+    o, m = C.c_int32(), C.c_int32()
+    _native.check(_native.lib().bx_env_sizes(self.sys._h, C.byref(p), C.byref(o), C.byref(m)))
+    if m.value != len(self.metric_keys):
+      raise RuntimeError(f'{type(self).__name__}: {m.value} metrics, {len(self.metric_keys)} keys')
+    self.obs_size = o.value
+
   def _params(self, opts=None, first_qp=None, first_obs=None):
     opts = opts or {}
     p = abi.BxEnvParams()
     p.kind = self.kind
-    p.obs_size = self.obs_size
+    p.obs_size = getattr(self, 'obs_size', 0)
     p.n_metrics = len(self.metric_keys)
     p.episode_length = int(opts.get('episode_length', 0) or 0)
     p.action_repeat = int(opts.get('action_repeat', 1))
     p.auto_reset = 1 if opts.get('auto_reset') else 0
+    p.obs_flags = self.obs_flags
     for i in range(8):
       p.coef[i] = float(self.coef[i])
     if first_qp is not None:
@@ -168,21 +184,62 @@ class PhysicsEnv(Env):
   def _noise_scale(self):
     return self.reset_noise_scale
 
-  def reset_batch(self, rng, batch_size):
-    """Batched `Env.reset` (e.g. `ant.py:198-220`).
+  def reset_batch(self, rng, batch_size, env_offset=None):
+    """Batched `Env.reset` (e.g. `ant.py:198-220`) in one C call,
+    `bx_env_reset`: noise, default_qp, the reset-time Info and the
+    observation on the device.
 
-    Reset noise U[-s, s] comes from the device counter RNG keyed by `rng`
-    (parity with JAX threefry is unpinned); parity of the
-    reset itself is pinned through `reset_from`."""
+    `rng` is one key (2,) / int: env e draws its noise U[-s, s) from the
+    counter RNG keyed by (rng, global env id env_offset + e). A (B, 2) key
+    batch gives every env its own key (`VmapWrapper.reset`). Parity with JAX
+    threefry is unpinned; the reset itself is pinned through
+    `reset_from` with the same noise (`reset_noise`)."""
+    B = int(batch_size)
+    off = self.env_offset if env_offset is None else int(env_offset)
+    dev = self.sys.device
+    seeds = None
+    if isinstance(rng, (int, np.integer)) or np.asarray(
+        rng.cpu() if isinstance(rng, torch.Tensor) else rng).ndim < 2:
+      seed = key_to_seed(rng)
+    else:
+      k = np.asarray(rng.cpu() if isinstance(rng, torch.Tensor) else rng).astype(np.uint64)
+      if k.shape[0] != B:
+        raise ValueError(f'{k.shape[0]} keys for {B} envs')
+      seeds = torch.as_tensor(((k[:, 0] << np.uint64(32)) | k[:, -1]).view(np.int64),
+                              device=dev)
+      seed = 0
+    qp, obs, scal, met = self._alloc(B)
+    out = abi.BxEnvState()
+    out.qp = qp_struct(qp, True)
+    out.obs = obs.data_ptr()
+    base = scal.data_ptr()
+    out.reward = base
+    out.done = base + 4 * B
+    out.steps = base + 8 * B
+    out.truncation = base + 12 * B
+    out.metrics = met.data_ptr() if self.metric_keys else None
+    p = self._params()
+    _native.check(_native.lib().bx_env_reset(
+        self.sys._h, C.byref(p), B, seed, off,
+        None if seeds is None else C.c_void_p(seeds.data_ptr()), float(self._noise_scale()),
+        C.byref(out), _stream(dev.index)))
+    reward, done, _, _ = scal.unbind(0)
+    return State(qp=qp, obs=obs, reward=reward, done=done, metrics=self._metrics(met), info={})
+
+  def reset_noise(self, rng, batch_size, env_offset=None):
+    """The (qpos, qvel) that `reset_batch(rng, batch_size)` adds up, drawn
+    with `bx_uniform` from the same counter stream: (B, D) each."""
+    B = int(batch_size)
+    off = self.env_offset if env_offset is None else int(env_offset)
     s = float(self._noise_scale())
     D = self.sys.num_joint_dof
     dev = self.sys.device
-    noise = torch.empty((2, batch_size, D), dtype=torch.float32, device=dev)
-    if D and batch_size:
+    noise = torch.empty((B, 2, D), dtype=torch.float32, device=dev)
+    if noise.numel():
       _native.check(_native.lib().bx_uniform(C.c_void_p(noise.data_ptr()), noise.numel(),
-                                             key_to_seed(rng), 0, -s, s, _stream()))
-    qpos = self.sys.default_angle().reshape(1, -1) + noise[0]
-    return self.reset_from(qpos, noise[1])
+                                             key_to_seed(rng), off * 2 * D, -s, s,
+                                             _stream(dev.index)))
+    return self.sys.default_angle().reshape(1, -1) + noise[:, 0], noise[:, 1]
 
   def reset_from(self, joint_angle, joint_velocity):
     """Reset state from explicit joint angles/velocities (B, num_joint_dof)."""
@@ -205,7 +262,7 @@ class PhysicsEnv(Env):
     act = torch.as_tensor(action, dtype=torch.float32, device=self.sys.device).contiguous()
     _native.check(_native.lib().bx_env_observe(
         self.sys._h, C.byref(p), B, C.byref(qs), C.c_void_p(act.data_ptr()),
-        act.shape[-1], act.shape[-1], C.c_void_p(obs.data_ptr()), _stream()))
+        act.shape[-1], act.shape[-1], C.c_void_p(obs.data_ptr()), _stream(self.sys.device.index)))
     return obs
 
   def reset(self, rng) -> State:

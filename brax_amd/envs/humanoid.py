@@ -7,6 +7,7 @@ qfrc uses an UNMASKED take of the padded act_index (-1 reads action[0],
 """
 import numpy as np
 
+from brax_amd import abi
 from brax_amd.envs import configs
 from brax_amd.envs import robots
 from brax_amd.envs.env import PhysicsEnv
@@ -23,8 +24,6 @@ class Humanoid(PhysicsEnv):
                terminate_when_unhealthy=True, healthy_z_range=(0.8, 2.1),
                reset_noise_scale=1e-2, exclude_current_positions_from_observation=True,
                legacy_spring=False, **kwargs):
-    if not exclude_current_positions_from_observation:
-      raise NotImplementedError('exclude_current_positions_from_observation=False')
     # `humanoid.py:209`: legacy_spring selects _SYSTEM_CONFIG_SPRING (three
     # joint groups, no sphericalisation: qfrc is 17 wide there)
     super().__init__(robots.HUMANOID_SPRING_CONFIG if legacy_spring else configs.HUMANOID_CONFIG,
@@ -33,7 +32,6 @@ class Humanoid(PhysicsEnv):
     self.coef = np.array([forward_reward_weight, ctrl_cost_weight, 0, healthy_reward,
                           healthy_z_range[0], healthy_z_range[1],
                           1.0 if terminate_when_unhealthy else 0.0, 0], np.float32)
-    D = self.sys.num_joint_dof
-    M = self.sys.num_bodies - 1
-    qfrc = sum(int(d) for d in self.sys.desc['joint_dof'][self.sys.desc['act_joint']])
-    self.obs_size = 1 + 4 + D + 3 + 3 + D + 9 * M + 3 * M + 3 * M + qfrc
+    # torso x, y lead the obs when positions are included (humanoid.py:289-292)
+    self.obs_flags = 0 if exclude_current_positions_from_observation else abi.OBS_XY
+    self._set_sizes()

@@ -23,7 +23,4 @@ class HumanoidStandup(PhysicsEnv):
                      else robots.HUMANOID_STANDUP_CONFIG, **kwargs)
     self.reset_noise_scale = 0.01
     self.coef = np.array([0, 0.01, 0, 0, 0, 0, 0, 0], np.float32)
-    D = self.sys.num_joint_dof
-    M = self.sys.num_bodies - 1
-    qfrc = sum(int(d) for d in self.sys.desc['joint_dof'][self.sys.desc['act_joint']])
-    self.obs_size = 1 + 4 + D + 3 + 3 + D + 9 * M + 3 * M + 3 * M + qfrc
+    self._set_sizes()

@@ -27,7 +27,7 @@ def _uniform(shape, seed, offset, lo, hi, device):
   out = torch.empty(shape, dtype=torch.float32, device=device)
   if out.numel():
     _native.check(_native.lib().bx_uniform(C.c_void_p(out.data_ptr()), out.numel(), seed,
-                                           offset, float(lo), float(hi), _stream()))
+                                           offset, float(lo), float(hi), _stream(out.device.index)))
   return out
 
 

@@ -42,12 +42,14 @@ class VectorWrapper(Wrapper):
 
 
 class VmapWrapper(Wrapper):
-  """`wrappers.py:73-80`: rng carries a leading batch axis (B, 2)."""
+  """`wrappers.py:73-80`: rng carries a leading batch axis (B, 2); env e
+  resets from its own key rng[e], as `jax.vmap(env.reset)(rng)` does."""
 
   def reset(self, rng) -> State:
-    rng = torch.as_tensor(rng)
-    B = rng.shape[0] if rng.dim() == 2 else 1
-    return _reset_batch(self.env, rng[0] if rng.dim() == 2 else rng, B)
+    rng = np.asarray(rng.cpu() if isinstance(rng, torch.Tensor) else rng)
+    if rng.ndim != 2:
+      return _reset_batch(self.env, rng, 1)
+    return _reset_batch(self.env, rng, rng.shape[0])
 
   def step(self, state, action):
     return self.env.step(state, action)

@@ -22,8 +22,8 @@ KINETIC, UPDATE_ACC, VPROJ = 0, 1, 2
 BYTES = {KINETIC: 80, UPDATE_ACC: 72, VPROJ: 96, 'capsule_plane': 120}
 
 
-def _stream():
-  return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+def _stream(device):
+  return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
 def to_soa(qp: QP):
@@ -56,7 +56,7 @@ def _phase(sys_, which, soa, aux, out):
     aux_ptr, aux_plane = C.c_void_p(aux.data_ptr()), aux.shape[1] * aux.shape[2]
   _native.check(_native.lib().bx_phase(sys_._h, which, B, plane, C.c_void_p(soa.data_ptr()),
                                        C.c_void_p(out.data_ptr()), aux_ptr, aux_plane,
-                                       _stream()))
+                                       _stream(sys_.device)))
   return out
 
 
@@ -81,5 +81,5 @@ def capsule_plane(sys_, soa, out=None):
     out = torch.zeros((10, R, B), dtype=torch.float32, device=soa.device)
   _native.check(_native.lib().bx_phase_capsule_plane(
       sys_._h, B, plane, C.c_void_p(soa.data_ptr()), C.c_void_p(out.data_ptr()), R * B,
-      _stream()))
+      _stream(sys_.device)))
   return out

@@ -28,11 +28,12 @@ except AttributeError:  # pragma: no cover
 
 
 def _stream(device_index=None):
-  """The caller's current HIP stream (stream-ordered ABI)."""
+  """The caller's current HIP stream on `device_index` (stream-ordered ABI,
+  SURVEY §8(b)); every System call passes its own device's index."""
   if _raw_stream is not None:
     return C.c_void_p(_raw_stream(torch.cuda.current_device() if device_index is None
                                   else device_index))
-  return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+  return C.c_void_p(torch.cuda.current_stream(device_index).cuda_stream)
 
 
 def _field(t, batched):
@@ -129,7 +130,7 @@ class System:
 
   def _create(self, reset_desc):
     cd, keep = abi.make_desc(self.desc)
-    rd, keep_r = abi.make_reset_desc(reset_desc)
+    rd, keep_r = abi.make_reset_desc(reset_desc, self.num_joint_dof)
     h = C.c_void_p()
     _native.check(_native.lib().bx_system_create(C.byref(cd), C.byref(rd),
                                                  self.device.index or 0, C.byref(h)))
@@ -213,7 +214,7 @@ class System:
     qs = qp_struct(out, True)
     _native.check(_native.lib().bx_system_default_qp(
         self._default_handle(default_index), B, C.c_void_p(ja.data_ptr()), C.c_void_p(jv.data_ptr()), C.byref(qs),
-        _stream()))
+        _stream(self.device.index)))
     return out if batched else out[0]
 
   def step(self, qp: QP, act):
@@ -248,7 +249,7 @@ class System:
     qo = qp_struct(out, batched)
     _native.check(_native.lib().bx_system_step(
         self._h, B, C.byref(qi), C.c_void_p(act.data_ptr()), act.stride(0), act.shape[1],
-        C.byref(qo), C.byref(info), _stream()))
+        C.byref(qo), C.byref(info), _stream(self.device.index)))
     zero = torch.zeros_like(cvel)
     joint = P(cbuf[..., 12:15], cbuf[..., 15:18]) if spring else P(zero, zero)
     return out, Info(contact=P(cvel, cang), joint=joint, actuator=P(avel, aang),
@@ -266,7 +267,7 @@ class System:
       qs = qp_struct(qp, batched)
       _native.check(_native.lib().bx_system_joint_angles(
           self._h, B, C.byref(qs), C.c_void_p(buf[0].data_ptr()), C.c_void_p(buf[1].data_ptr()),
-          _stream()))
+          _stream(self.device.index)))
     return (buf[0], buf[1]) if batched else (buf[0, 0], buf[1, 0])
 
   def info(self, qp: QP):
@@ -281,7 +282,7 @@ class System:
     info.contact_ang = _field(cbuf[..., 3:6], batched)
     qi = qp_struct(qp, batched)
     _native.check(_native.lib().bx_system_info(self._h, B, C.byref(qi), C.byref(info),
-                                               _stream()))
+                                               _stream(self.device.index)))
     zero = torch.zeros_like(cbuf[..., 0:3])
     return Info(contact=P(cbuf[..., 0:3], cbuf[..., 3:6]), joint=P(zero, zero),
                 actuator=P(zero, zero), contact_pos=None, contact_normal=None,

@@ -13,7 +13,10 @@
  *   System.info(qp)              system.py:249-252,327-340  bx_system_info
  *   Env.step + EpisodeWrapper + AutoResetWrapper
  *     ant.py:222-255, wrappers.py:105-148                bx_env_step
- *   Env.reset                    ant.py:198-220          bx_env_reset
+ *   Env.reset (+ EpisodeWrapper/AutoResetWrapper.reset counters)
+ *     ant.py:198-220, humanoid.py:223-244,
+ *     half_cheetah.py:164-180, wrappers.py:94-97,128-133 bx_env_reset
+ *   Joint.angle_vel              joints.py:197-226       bx_system_joint_angles
  *
  * Conventions
  *   - Every array argument is a raw device pointer (HBM) owned by the caller.
@@ -34,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 3
+#define BX_ABI_VERSION 4
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
 enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
@@ -52,6 +55,10 @@ enum { BX_FORCE_THRUSTER = 0, BX_FORCE_TWISTER = 1 };
 /* env layer kinds (obs / reward programs) */
 enum { BX_ENV_NONE = 0, BX_ENV_ANT = 1, BX_ENV_HUMANOID = 2, BX_ENV_HALFCHEETAH = 3,
        BX_ENV_HUMANOID_STANDUP = 4 };
+/* observation options. BX_OBS_XY: exclude_current_positions_from_observation
+ * = False, the torso's x (and y) precede its z (ant.py:262-265,
+ * humanoid.py:289-292: x, y; half_cheetah.py:206-209: x) */
+enum { BX_OBS_XY = 1 };
 
 /*
  * System descriptor: the compiled constant arrays of `brax.System`
@@ -174,6 +181,9 @@ typedef struct bx_reset_desc {
   const int32_t* body_zero_cand;   /* [N] 1: min_z also sees 0.0 (plane/none) */
   const int32_t* body_root_group;  /* [N] lift group, -1 = not lifted */
   int32_t n_root_groups;
+  /* System.default_angle (system.py:86-110) of this default: the joint-angle
+   * vector that bx_env_reset adds its noise to */
+  const double* default_angle;     /* [num_joint_dof] */
 } bx_reset_desc;
 
 /* A strided view of one fp32 QP field: element (env e, body b, k) lives at
@@ -219,6 +229,7 @@ typedef struct bx_env_params {
   int32_t episode_length;   /* <= 0: no EpisodeWrapper */
   int32_t action_repeat;    /* EpisodeWrapper action_repeat (>= 1) */
   int32_t auto_reset;       /* AutoResetWrapper present */
+  int32_t obs_flags;        /* BX_OBS_* */
   /* env constructor arguments (ant.py:173-183, humanoid.py:196-212,
    * half_cheetah.py:147-158):
    *   ANT:         forward_w(unused=1), ctrl_cost_weight, contact_cost_weight,
@@ -288,6 +299,30 @@ int bx_system_default_qp(bx_system* sys, int64_t n_envs,
 int bx_system_info(bx_system* sys, int64_t n_envs, const bx_qp* qp,
                    const bx_info* info, void* stream);
 
+/* Observation and metric widths the env layer writes for `env` on this
+ * system (obs_size / n_metrics in bx_env_params must equal them). */
+int bx_env_sizes(bx_system* sys, const bx_env_params* env, int32_t* obs_size,
+                 int32_t* n_metrics);
+
+/* Env.reset of the kernel env kinds, batched, in two launches (ant.py:198-220,
+ * humanoid.py:223-244, half_cheetah.py:164-180, humanoid_standup.py:216-230):
+ * for env e (global id g = env_offset + e)
+ *   qpos = default_angle + U[-s, s)  counter RNG (seed, g * 2D + k)
+ *   qvel =                 U[-s, s)  counter RNG (seed, g * 2D + D + k)
+ *   qp   = System.default_qp(qpos, qvel)       (system.py:112-242)
+ *   obs  = _get_obs(qp, System.info(qp), 0)    (system.py:327-340)
+ *   reward = done = metrics = 0; steps = truncation = 0 when given.
+ * D = num_joint_dof, s = noise_scale. Keying by global env id makes the
+ * states independent of how a batch is sharded over GPUs.
+ * env_seeds (device, n_envs uint64, may be NULL) gives every env its own key
+ * instead, as `VmapWrapper.reset` over a (B, 2) key batch (wrappers.py:79-80):
+ * env e then draws from (env_seeds[e], k) and (env_seeds[e], D + k). The JAX
+ * threefry stream itself is parity-unpinned. The params'
+ * first_qp / first_obs are not read. */
+int bx_env_reset(bx_system* sys, const bx_env_params* env, int64_t n_envs, uint64_t seed,
+                 int64_t env_offset, const uint64_t* env_seeds, float noise_scale,
+                 const bx_env_state* out, void* stream);
+
 /* Env observation of a state (Env._get_obs with the reset-time Info). */
 int bx_env_observe(bx_system* sys, const bx_env_params* env, int64_t n_envs,
                    const bx_qp* qp, const float* act, int64_t act_stride,
@@ -300,9 +335,11 @@ int bx_env_observe(bx_system* sys, const bx_env_params* env, int64_t n_envs,
 int bx_system_joint_angles(bx_system* sys, int64_t n_envs, const bx_qp* qp, float* angle,
                            float* vel, void* stream);
 
-/* Counter-based uniform [lo,hi) fill keyed by (seed, global index); used for
- * reset noise and synthetic actions (the JAX threefry stream is parity
- * unpinned). */
+/* Counter-based uniform [lo,hi) fill: out[i] = U(seed, offset + i), a
+ * splitmix64 hash of (seed, global index); the same stream bx_env_reset draws
+ * its noise from. Used for synthetic actions (offset = global env id x width,
+ * so shards reproduce one big batch) and reset noise (the JAX threefry stream
+ * is parity unpinned). */
 int bx_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
                float lo, float hi, void* stream);
 

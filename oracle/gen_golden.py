@@ -588,6 +588,18 @@ def main():
       save(f'desc_{mod}_spring', dump_desc(s))
       A = aw or (s.num_joint_dof + s.num_forces_dof)
       save(f'traj_{mod}_spring', sys_traj(s, mod + '_spring', s.default_qp(), B, T, 1.0, A))
+  # exclude_current_positions_from_observation=False (ant.py:262-265,
+  # humanoid.py:289-292, half_cheetah.py:206-209)
+  if want('ant_xy'):
+    env = ant_mod.Ant(use_contact_forces=True, exclude_current_positions_from_observation=False)
+    save('traj_ant_xy', env_traj(env, 'ant_xy', 4, 2))
+  if want('humanoid_xy'):
+    env = importlib.import_module('brax.envs.humanoid').Humanoid(
+        exclude_current_positions_from_observation=False)
+    save('traj_humanoid_xy', env_traj(env, 'humanoid_xy', 4, 2))
+  if want('halfcheetah_xy'):
+    env = envs.get_environment('halfcheetah', exclude_current_positions_from_observation=False)
+    save('traj_halfcheetah_xy', env_traj(env, 'halfcheetah_xy', 4, 2))
   if want('halfcheetah'):
     env = envs.get_environment('halfcheetah')
     save('desc_halfcheetah', dump_desc(env.sys))

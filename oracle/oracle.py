@@ -60,7 +60,8 @@ class Oracle:
     self.IR = abi.info_rows(self.desc)  # Info contact rows
     self.A = int(desc.get('action_size', 0))
     if reset_desc is not None:
-      self.creset, self._keep_r = abi.make_reset_desc(reset_desc)
+      self.creset, self._keep_r = abi.make_reset_desc(reset_desc,
+                                                      desc.get('num_joint_dof'))
     else:
       self.creset = None
     self._fn('oracle_set_safe_norm_guard')(C.c_int(1 if safe_guard else 0))
@@ -105,21 +106,22 @@ class Oracle:
     self._fn('oracle_system_info')(C.byref(self.cdesc), C.c_int64(B), _p(qp), _p(ic))
     return ic
 
-  def env_obs(self, kind, qp, info_contact, act, obs_size):
+  def env_obs(self, kind, qp, info_contact, act, obs_size, obs_flags=0):
     qp = self._a(qp)
     B = qp.shape[0]
     ic = self._a(info_contact)
     act = self._a(act).reshape(B, -1)
     self._width(act)
     obs = np.empty((B, obs_size), self.dtype)
-    rc = self._fn('oracle_env_obs')(C.byref(self.cdesc), C.c_int(ENV_KIND[kind]),
+    rc = self._fn('oracle_env_obs')(C.byref(self.cdesc), C.c_int(ENV_KIND[kind] | obs_flags << 8),
                                     C.c_int64(B), _p(qp), _p(ic), _p(act), _p(obs),
                                     C.c_int(obs_size))
     if rc:
       raise ValueError('obs size mismatch')
     return obs
 
-  def env_step(self, kind, qp, act, obs_size, n_metrics, done=None):
+  def env_step(self, kind, qp, act, obs_size, n_metrics, done=None, obs_flags=0):
+    """obs_flags: BX_OBS_XY for exclude_current_positions_from_observation=False."""
     qp = self._a(qp)
     B = qp.shape[0]
     act = self._a(act).reshape(B, -1)
@@ -129,7 +131,7 @@ class Oracle:
     rew = np.empty(B, self.dtype)
     dn = self._a(np.zeros(B) if done is None else done).copy()
     met = np.zeros((B, n_metrics), self.dtype)
-    rc = self._fn('oracle_env_step')(C.byref(self.cdesc), C.c_int(ENV_KIND[kind]),
+    rc = self._fn('oracle_env_step')(C.byref(self.cdesc), C.c_int(ENV_KIND[kind] | obs_flags << 8),
                                      C.c_int64(B), _p(qp), _p(act), _p(out), _p(obs),
                                      C.c_int(obs_size), _p(rew), _p(dn), _p(met),
                                      C.c_int(n_metrics))

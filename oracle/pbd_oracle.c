@@ -1948,10 +1948,12 @@ static int angle_vel(const sysc* s, const body_t* qp, R* angles, R* vels) {
 static R clip1(R x) { return clip(x, -1, 1); }
 
 /* Ant._get_obs (ant.py:257-282), use_contact_forces=True -> 87 */
-static int obs_ant(const sysc* s, const body_t* qp, const R* info_c, R* obs) {
+static int obs_ant(const sysc* s, const body_t* qp, const R* info_c, R* obs, int xy) {
   int n = 0, N = s->N;
   R ang[64], vel[64];
   int nd = angle_vel(s, qp, ang, vel);
+  /* exclude_current_positions_from_observation=False: qp.pos[0] whole (ant.py:262-265) */
+  if (xy) { obs[n++] = qp[0].pos[0]; obs[n++] = qp[0].pos[1]; }
   obs[n++] = qp[0].pos[2];
   for (int k = 0; k < 4; k++) obs[n++] = qp[0].rot[k];
   for (int i = 0; i < nd; i++) obs[n++] = ang[i];
@@ -1966,10 +1968,12 @@ static int obs_ant(const sysc* s, const body_t* qp, const R* info_c, R* obs) {
 }
 
 /* Halfcheetah._get_obs (half_cheetah.py:200-214) -> 18 */
-static int obs_halfcheetah(const sysc* s, const body_t* qp, R* obs) {
+static int obs_halfcheetah(const sysc* s, const body_t* qp, R* obs, int xy) {
   int n = 0;
   R ang[64], vel[64];
   int nd = angle_vel(s, qp, ang, vel);
+  /* qp.pos[0, (0, 2)] when positions are included (half_cheetah.py:206-209) */
+  if (xy) obs[n++] = qp[0].pos[0];
   obs[n++] = qp[0].pos[2];
   obs[n++] = qp[0].rot[0];
   obs[n++] = qp[0].rot[2];
@@ -1993,10 +1997,12 @@ static void humanoid_com(const sysc* s, const body_t* qp, R* com) {
 }
 
 /* Humanoid._get_obs (humanoid.py:282-334) -> 240 */
-static int obs_humanoid(const sysc* s, const body_t* qp, const R* act, R* obs) {
+static int obs_humanoid(const sysc* s, const body_t* qp, const R* act, R* obs, int xy) {
   int n = 0, N = s->N;
   R ang[64], vel[64];
   int nd = angle_vel(s, qp, ang, vel);
+  /* qp.pos[0] whole when positions are included (humanoid.py:289-292) */
+  if (xy) { obs[n++] = qp[0].pos[0]; obs[n++] = qp[0].pos[1]; }
   obs[n++] = qp[0].pos[2];
   for (int k = 0; k < 4; k++) obs[n++] = qp[0].rot[k];
   for (int i = 0; i < nd; i++) obs[n++] = ang[i];
@@ -2048,6 +2054,8 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
   sys_init(&s, d);
   int N = s.N;
   int rc = 0;
+  const int xy = (kind >> 8) & BX_OBS_XY; /* kind | obs_flags << 8 */
+  kind &= 0xFF;
 #pragma omp parallel
   {
     body_t* q = calloc(N, sizeof(body_t));
@@ -2055,10 +2063,10 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
     for (int64_t e = 0; e < B; e++) {
       load_qp(q, qp + e * 13 * N, N);
       int n = 0;
-      if (kind == BX_ENV_ANT) n = obs_ant(&s, q, info_c + e * 6 * N, obs + e * obs_size);
-      else if (kind == BX_ENV_HALFCHEETAH) n = obs_halfcheetah(&s, q, obs + e * obs_size);
+      if (kind == BX_ENV_ANT) n = obs_ant(&s, q, info_c + e * 6 * N, obs + e * obs_size, xy);
+      else if (kind == BX_ENV_HALFCHEETAH) n = obs_halfcheetah(&s, q, obs + e * obs_size, xy);
       else if (kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP)
-        n = obs_humanoid(&s, q, act + e * s.aw, obs + e * obs_size);
+        n = obs_humanoid(&s, q, act + e * s.aw, obs + e * obs_size, xy);
       if (n != obs_size) rc = -1;
     }
     free(q);
@@ -2076,6 +2084,8 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
   sys_init(&s, d);
   int N = s.N, Rn = s.Rn, A = s.aw;
   int rc = 0;
+  const int xy = (kind >> 8) & BX_OBS_XY; /* kind | obs_flags << 8 */
+  kind &= 0xFF;
 #pragma omp parallel
   {
     work_t w;
@@ -2097,7 +2107,7 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
       for (int i = 0; i < A; i++) sq += a[i] * a[i];
       int n = 0;
       if (kind == BX_ENV_ANT) {
-        n = obs_ant(&s, w.qp, w.info_c, o);
+        n = obs_ant(&s, w.qp, w.info_c, o, xy);
         R vel[3];
         for (int k = 0; k < 3; k++) vel[k] = (w.qp[0].pos[k] - q0[0].pos[k]) / dt;
         R fwd = vel[0];
@@ -2118,7 +2128,7 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
         m[4] = fwd; m[5] = 1; m[6] = w.qp[0].pos[0]; m[7] = vel[0];
         m[8] = w.qp[0].pos[1]; m[9] = vel[1];
       } else if (kind == BX_ENV_HALFCHEETAH) {
-        n = obs_halfcheetah(&s, w.qp, o);
+        n = obs_halfcheetah(&s, w.qp, o, xy);
         R v0 = (w.qp[0].pos[0] - q0[0].pos[0]) / dt;
         R fwd = (R)1.0 * v0;
         R ctrl = (R)0.1 * sq;
@@ -2126,7 +2136,7 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
         /* done unchanged; metrics sorted: reward_ctrl, reward_run, x_position, x_velocity */
         m[0] = -ctrl; m[1] = fwd; m[2] = w.qp[0].pos[0]; m[3] = v0;
       } else if (kind == BX_ENV_HUMANOID) {
-        n = obs_humanoid(&s, w.qp, a, o);
+        n = obs_humanoid(&s, w.qp, a, o, xy);
         R cb[3], ca[3], v[3];
         humanoid_com(&s, q0, cb);
         humanoid_com(&s, w.qp, ca);
@@ -2146,7 +2156,7 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
       } else if (kind == BX_ENV_HUMANOID_STANDUP) {
         /* humanoid_standup.py:232-247; done unchanged; sorted metrics:
          * reward_linup, reward_quadctrl */
-        n = obs_humanoid(&s, w.qp, a, o);
+        n = obs_humanoid(&s, w.qp, a, o, 0);
         R uph = (w.qp[0].pos[2] - (R)0) / dt;
         R ctrl = (R)0.01 * sq;
         reward[e] = uph + (R)1 - ctrl;

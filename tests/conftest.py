@@ -23,3 +23,9 @@ def oracle_lib():
   from oracle import oracle  # test infrastructure
   oracle.build()
   return oracle
+
+
+def pytest_sessionfinish(session, exitstatus):
+  # the parity margins recorded by the GPU gates (tests/margins.py)
+  from tests import margins
+  margins.write(os.path.join(ROOT, 'gpurun_out', 'parity_margins.json'))

@@ -42,9 +42,21 @@ SPRING_ROBOTS = [m + '_spring' for m in (
 _SPRING_MOD = {'halfcheetah': 'HALF_CHEETAH', 'humanoidstandup': 'HUMANOID_STANDUP'}
 
 
+# exclude_current_positions_from_observation=False rollouts (traj_<env>_xy)
+XY_ENVS = ['ant_xy', 'humanoid_xy', 'halfcheetah_xy']
+
+
 def env_kind(name):
-  """Env-layer kind of a golden name ('ant_spring' -> 'ant')."""
-  return name[:-len('_spring')] if name.endswith('_spring') else name
+  """Env-layer kind of a golden name ('ant_spring', 'ant_xy' -> 'ant')."""
+  for suf in ('_spring', '_xy'):
+    if name.endswith(suf):
+      return name[:-len(suf)]
+  return name
+
+
+def obs_flags(name):
+  """BX_OBS_* of a golden name (abi.OBS_XY for the *_xy rollouts)."""
+  return 1 if name.endswith('_xy') else 0
 
 
 # point-plane scenes: BoxTest (box corners) and an inline-mesh MeshTest
@@ -56,6 +68,8 @@ XCOL = ['heightmap', 'clipped', 'box_capsule', 'mesh_capsule', 'box_box', 'box_c
 
 
 def config_for(name):
+  if name.endswith('_xy'):
+    name = name[:-len('_xy')]
   if name.endswith('_spring'):
     base = name[:-len('_spring')]
     return cfgmod.parse(getattr(robots, _SPRING_MOD.get(base, base.upper()) + '_SPRING_CONFIG'))

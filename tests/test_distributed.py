@@ -28,8 +28,7 @@ def _worker(rank, world, port, q):
   done = (torch.arange(lo, hi) % 2).float()
   ex = bd.EpisodeExchange(B, 'cpu')
   out = ex(reward, done)
-  key = bd.rank_key(np.array([3, 7], np.uint32), rank)
-  q.put((rank, out.numpy().copy(), key.tolist()))
+  q.put((rank, out.numpy().copy(), bd.action_offset(rank, B, 8, step=3, world=world)))
   dist.barrier()
   dist.destroy_process_group()
 
@@ -52,9 +51,35 @@ def test_episode_allgather_world2():
     assert out.shape == (2, 2, 5)
     np.testing.assert_array_equal(out[:, 0], expect_r)
     np.testing.assert_array_equal(out[:, 1], expect_r % 2)
-  assert res[0][2] != res[1][2]  # disjoint per-rank RNG keys
+  # rank r's action rows of step 3 continue rank r-1's in the global stream
+  assert res[1][2] - res[0][2] == 5 * 8
 
 
 def test_env_range():
   assert bd.env_range(0, 4096) == (0, 4096)
   assert bd.env_range(3, 4096) == (12288, 16384)
+
+
+def test_action_offsets_tile_the_global_stream():
+  """Per-rank action slabs keyed by (step, global env id) cover exactly the
+  rows one big batch of world*B envs draws at that step."""
+  B, A = 4096, 8
+  for world in (1, 2, 4, 8):
+    for step in (0, 1, 17):
+      offs = [bd.action_offset(r, B, A, step, world) for r in range(world)]
+      big = bd.action_offset(0, world * B, A, step, 1)
+      assert offs == [big + r * B * A for r in range(world)]
+
+
+class _Env:
+  def __init__(self):
+    self.env_offset = 0
+
+  @property
+  def unwrapped(self):
+    return self
+
+
+def test_shard_env_sets_global_offset():
+  e = bd.shard_env(_Env(), 3, 4096)
+  assert e.env_offset == 3 * 4096

@@ -21,8 +21,9 @@ import pytest
 import torch
 
 from tests.conftest import golden
+from tests.margins import record_margin
 from tests.helpers import (CAPSULES, POINTS, QP_FIELDS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL,
-                           compiled, env_kind, normwise)
+                           XY_ENVS, compiled, env_kind, normwise, obs_flags)
 
 pytestmark = pytest.mark.gpu
 
@@ -56,6 +57,7 @@ def _to_qp(a, dev):
 def _gate(got, ref, e32, field):
   nw = normwise(got, ref)
   tol = max(POS_TOL, 2.0 * float(np.max(e32)))
+  record_margin(field, float(nw.max()), tol)
   assert np.all(np.isfinite(got)), field
   assert nw.max() <= tol, f'{field}: normwise {nw.max():.3e} > tol {tol:.3e}'
   return nw.max(), tol
@@ -82,8 +84,8 @@ class Envelope:
   def system(self, qp, act):
     return [o.system_step(q, act.astype(np.float32)) for o in self.os for q in self._inputs(qp)]
 
-  def env(self, name, qp, act, O, M):
-    return [o.env_step(name, q, act.astype(np.float32), O, M) for o in self.os
+  def env(self, name, qp, act, O, M, flags=0):
+    return [o.env_step(name, q, act.astype(np.float32), O, M, obs_flags=flags) for o in self.os
             for q in self._inputs(qp)]
 
 
@@ -91,6 +93,8 @@ def _make_env(name, dev, **kw):
   from brax_amd import envs
   if name.endswith('_spring'):
     kw['legacy_spring'] = True
+  if name.endswith('_xy'):
+    kw['exclude_current_positions_from_observation'] = False
   return envs.get_environment(env_kind(name), device=dev, **kw)
 
 
@@ -138,6 +142,11 @@ def test_system_step_vs_golden(dev, oracle_lib, name):
     pen = info.contact_penetration.cpu().numpy()
     if pen.size == 0:
       continue
+    if 'contact_pos' in T:
+      # Info.contact_pos / contact_normal (_get_contact_info, system.py:36-43)
+      for k in ('contact_pos', 'contact_normal'):
+        g = getattr(info, k).cpu().numpy()
+        _gate(g, T[k][t], _env_err([o[1][k] for o in outs], T[k][t]), k)
     ref_pen = T['contact_penetration'][t]
     o_pen = [o[1]['contact_penetration'] for o in outs]
     if (np.asarray(sys_.desc['col_cutoff']) > 0).any():
@@ -147,11 +156,12 @@ def test_system_step_vs_golden(dev, oracle_lib, name):
     _gate(pen, ref_pen, _env_err(o_pen, ref_pen), 'pen')
 
 
-@pytest.mark.parametrize('name', ENV_TRAJ)
+@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS)
 def test_env_step_vs_golden(dev, oracle_lib, name):
   env = _make_env(name, dev)
   T = golden('traj_' + name)
   env32 = Envelope(oracle_lib, name)
+  fl = obs_flags(name)
   O, M = T['obs'].shape[-1], T['metrics'].shape[-1]
   assert env.observation_size == O
   from brax_amd.envs.env import State
@@ -161,7 +171,7 @@ def test_env_step_vs_golden(dev, oracle_lib, name):
                reward=torch.zeros(B, device=dev), done=torch.zeros(B, device=dev))
     act = torch.as_tensor(T['action'][t], dtype=torch.float32, device=dev)
     nst = env.step(st, act)
-    outs = env32.env(env_kind(name), T['qp'][t], T['action'][t], O, M)
+    outs = env32.env(env_kind(name), T['qp'][t], T['action'][t], O, M, fl)
     _gate(nst.obs.cpu().numpy(), T['obs'][t + 1], _env_err([o[1] for o in outs], T['obs'][t + 1]),
           'obs')
     _gate(nst.reward.cpu().numpy()[:, None], T['reward'][t][:, None],
@@ -171,7 +181,7 @@ def test_env_step_vs_golden(dev, oracle_lib, name):
     _gate(met, T['metrics'][t], _env_err([o[4] for o in outs], T['metrics'][t]), 'metrics')
 
 
-@pytest.mark.parametrize('name', ENV_TRAJ)
+@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS)
 def test_reset_vs_golden(dev, oracle_lib, name):
   """Reset = default_qp FK + lift + System.info (impulse contacts) + obs.
 
@@ -192,10 +202,12 @@ def test_reset_vs_golden(dev, oracle_lib, name):
   o32 = oracle_lib.Oracle(d, rd, np.float32, safe_guard=True)
   q32 = o32.default_qp(T['reset_qpos'], T['reset_qvel'])
   B = q32.shape[0]
-  obs32 = o32.env_obs(env_kind(name), q32, o32.system_info(q32), np.zeros((B, o32.A)), T['obs'].shape[-1])
+  obs32 = o32.env_obs(env_kind(name), q32, o32.system_info(q32), np.zeros((B, o32.A)),
+                      T['obs'].shape[-1], obs_flags=obs_flags(name))
   obs = st.obs.cpu().numpy()
   _gate(obs, T['reset_obs'], normwise(obs32, T['reset_obs']), 'obs')
-  n_state = 1 + 4 + 2 * meta['num_joint_dof'] + 6 if env_kind(name) == 'ant' else obs.shape[-1]
+  n_state = (1 + 4 + 2 * meta['num_joint_dof'] + 6 + 2 * obs_flags(name)
+             if env_kind(name) == 'ant' else obs.shape[-1])
   assert normwise(obs[:, :n_state], T['reset_obs'][:, :n_state]).max() <= 1e-5
 
 

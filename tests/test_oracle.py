@@ -9,8 +9,8 @@ import numpy as np
 import pytest
 
 from tests.conftest import golden
-from tests.helpers import (CAPSULES, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL, compiled,
-                           env_kind)
+from tests.helpers import (CAPSULES, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL, XY_ENVS,
+                           compiled, env_kind, obs_flags)
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
 SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + POINTS
@@ -64,19 +64,33 @@ def test_system_step_matches_reference(oracle_lib, name):
 
 
 @pytest.mark.parametrize('name', ENV_TRAJ)
+def test_contact_info_matches_reference(oracle_lib, name):
+  """Info.contact_pos / contact_normal (`_get_contact_info`,
+  system.py:36-43) of every Env.step's System.step, row for row."""
+  o = _oracle(oracle_lib, name)
+  T = golden('traj_' + name)
+  for t in range(T['action'].shape[0]):
+    _, info = o.system_step(T['qp'][t], T['action'][t])
+    for k in ('contact_pos', 'contact_normal'):
+      assert info[k].shape == T[k][t].shape, k
+      assert np.abs(info[k] - T[k][t]).max() < 1e-9, k
+
+
+@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS)
 def test_env_step_matches_reference(oracle_lib, name):
   o = _oracle(oracle_lib, name)
   T = golden('traj_' + name)
   O, M = T['obs'].shape[-1], T['metrics'].shape[-1]
   for t in range(T['action'].shape[0]):
-    _, obs, rew, done, met = o.env_step(env_kind(name), T['qp'][t], T['action'][t], O, M)
+    _, obs, rew, done, met = o.env_step(env_kind(name), T['qp'][t], T['action'][t], O, M,
+                                        obs_flags=obs_flags(name))
     assert np.abs(obs - T['obs'][t + 1]).max() < 1e-9
     assert np.abs(rew - T['reward'][t]).max() < 1e-12
     assert np.array_equal(done, T['done'][t])
     assert np.abs(met - T['metrics'][t]).max() < 1e-12
 
 
-@pytest.mark.parametrize('name', ENV_TRAJ)
+@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS)
 def test_reset_matches_reference(oracle_lib, name):
   o = _oracle(oracle_lib, name)
   T = golden('traj_' + name)
@@ -84,7 +98,8 @@ def test_reset_matches_reference(oracle_lib, name):
   assert np.abs(qp0 - T['qp'][0]).max() < 1e-12
   ic = o.system_info(qp0)
   B = qp0.shape[0]
-  obs = o.env_obs(env_kind(name), qp0, ic, np.zeros((B, o.A)), T['obs'].shape[-1])
+  obs = o.env_obs(env_kind(name), qp0, ic, np.zeros((B, o.A)), T['obs'].shape[-1],
+                  obs_flags=obs_flags(name))
   assert np.abs(obs - T['reset_obs']).max() < 1e-12
 
 

@@ -3,7 +3,7 @@ launch queue absorbing the kernels, then the synchronised rate, plus a
 cProfile of the Python path. Diagnostic, not part of the product."""
 import cProfile, pstats, sys, time, os
 import torch
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from brax_amd import envs
 dev = torch.device('cuda', 0)
 B = 4096

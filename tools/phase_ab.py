@@ -1,6 +1,6 @@
 """Phase-kernel roofline A/B across library builds: python phase_ab.py lib..."""
 import json, os, subprocess, sys
-ROOT = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if len(sys.argv) > 1 and sys.argv[1] != '--child':
   for rep in range(2):
     for lib in sys.argv[1:]:
