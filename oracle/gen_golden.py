@@ -533,8 +533,13 @@ TORCH_ENVS = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendul
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--only', default='')
+  ap.add_argument('--desc-only', action='store_true',
+                  help='write only the desc_*.npz descriptor dumps (no rollouts)')
   args = ap.parse_args()
   _setup()
+  if args.desc_only:
+    global env_traj, sys_traj, wrapped_ant, kats  # pylint: disable=global-statement
+    env_traj = sys_traj = wrapped_ant = kats = lambda *a, **k: None  # noqa: E731
   os.makedirs(OUT, exist_ok=True)
   from brax import envs
   from brax.envs import ant as ant_mod
@@ -544,6 +549,8 @@ def main():
     return only is None or n in only
 
   def save(name, d):
+    if d is None:
+      return
     path = os.path.join(OUT, name + '.npz')
     np.savez_compressed(path, **d)
     print('wrote', path, os.path.getsize(path), 'bytes', flush=True)

@@ -15,6 +15,9 @@ NAMES = (['ant', 'humanoid', 'halfcheetah', 'humanoidstandup', 'mountain1', 'mou
 def test_descriptor_bit_exact(name):
   _, d, _, _ = compiled(name)
   g = golden('desc_' + name)
+  # every descriptor field is pinned: the reference dump holds exactly the
+  # compiler's keys
+  assert set(g.files) == set(d.keys()), sorted(set(g.files) ^ set(d.keys()))
   for k in g.files:
     a, b = np.asarray(d[k]), g[k]
     assert a.shape == b.shape, k
