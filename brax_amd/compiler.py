@@ -69,73 +69,80 @@ def rotate(vv, q):
 # validate_config
 # --------------------------------------------------------------------------
 
-def validate_config(config):
-  """Normalises a config like `base.py:156-254` (returns a deep copy)."""
-  config = copy.deepcopy(config)
-  if config.dt <= 0:
-    raise ValueError('config.dt must be positive')
-  if config.substeps == 0:
-    config.substeps = 1
-  config.solver_scale_collide = config.solver_scale_collide or 1.0
+_AXES = tuple((part, ax) for part in ('position', 'rotation') for ax in 'xyz')
+_NAMED = ('bodies', 'joints', 'actuators', 'mesh_geometries')
 
-  def find_dupes(objs):
-    names = set()
-    for obj in objs:
-      if obj.name in names:
-        raise RuntimeError(f'duplicate name in config: {obj.name}')
-      names.add(obj.name)
 
-  find_dupes(config.bodies)
-  find_dupes(config.joints)
-  find_dupes(config.actuators)
-  find_dupes(config.mesh_geometries)
+def _reify_frozen(frozen, inherited=None):
+  """Makes one Frozen message explicit: `all` <-> six set axes.
 
-  if config.dynamics_mode == 'legacy_spring':
-    if any(j.stiffness == 0 for j in config.joints):
-      raise ValueError(
-          'joint.stiffness must be >0 when dynamics_mode == legacy_spring')
-  elif config.dynamics_mode == 'pbd':
-    if any(j.stiffness != 0 for j in config.joints):
+  With `inherited` (the config-level Frozen) an unset axis takes the
+  inherited value first (`base.py:219-224`). Returns the final `all` flag.
+  """
+  if inherited is not None:
+    for part, ax in _AXES:
+      own = getattr(getattr(frozen, part), ax)
+      setattr(getattr(frozen, part), ax, own or getattr(getattr(inherited, part), ax))
+  if frozen.all:
+    for part, ax in _AXES:
+      setattr(getattr(frozen, part), ax, 1.0)
+  if all(getattr(getattr(frozen, part), ax) for part, ax in _AXES):
+    frozen.all = True
+  return bool(frozen.all)
+
+
+def _resolve_dynamics_mode(config):
+  """`base.py:181-204`: an explicit mode is checked against the joints'
+  stiffness; anything else is inferred from it, with the reference's warning."""
+  stiff = [j.stiffness != 0 for j in config.joints]
+  mode = config.dynamics_mode
+  if mode == 'legacy_spring' and not all(stiff):
+    raise ValueError('joint.stiffness must be >0 when dynamics_mode == legacy_spring')
+  if mode == 'pbd':
+    if any(stiff):
       raise ValueError('joint.stiffness is invalid when dynamics_mode == pbd')
     if config.baumgarte_erp:
       raise ValueError('baumgarte_erp is invalid when dynamics_mode == pbd')
-  elif any(j.stiffness != 0 for j in config.joints):
-    config.dynamics_mode = 'legacy_spring'
-    warnings.warn('dynamics_mode not specified, but joint.stiffness >0. '
-                  'Setting dynamics_mode="legacy_spring".')
-  else:
-    config.dynamics_mode = 'pbd'
-    warnings.warn('dynamics_mode not specified, defaulting to "pbd".')
+  if mode in ('legacy_spring', 'pbd'):
+    return
+  config.dynamics_mode = 'legacy_spring' if any(stiff) else 'pbd'
+  warnings.warn('dynamics_mode not specified, but joint.stiffness >0. '
+                'Setting dynamics_mode="legacy_spring".' if any(stiff) else
+                'dynamics_mode not specified, defaulting to "pbd".')
 
-  allvec = cfgmod.Message('Vector3', x=1.0, y=1.0, z=1.0)
-  frozen = config.frozen
-  if frozen.all:
-    frozen.position.CopyFrom(allvec)
-    frozen.rotation.CopyFrom(allvec)
-  if all([frozen.position.x, frozen.position.y, frozen.position.z,
-          frozen.rotation.x, frozen.rotation.y, frozen.rotation.z]):
-    config.frozen.all = True
+
+def validate_config(config):
+  """Returns a normalised deep copy of `config`, as `base.py:156-254` does.
+
+  Steps: positive dt, substeps >= 1, solver_scale_collide defaults to 1;
+  unique names per named collection; the dynamics mode; explicit frozen
+  axes (config level, then each body inheriting it); unit inertia for
+  bodies that give none; collider materials from the config defaults. Mesh
+  files are not loaded (inline `mesh_geometries` only).
+  """
+  config = copy.deepcopy(config)
+  if config.dt <= 0:
+    raise ValueError('config.dt must be positive')
+  config.substeps = config.substeps or 1
+  config.solver_scale_collide = config.solver_scale_collide or 1.0
+  for coll in _NAMED:
+    names = [o.name for o in getattr(config, coll)]
+    dup = next((n for i, n in enumerate(names) if n in names[:i]), None)
+    if dup is not None:
+      raise RuntimeError(f'duplicate name in config: {dup}')
+  _resolve_dynamics_mode(config)
+
+  _reify_frozen(config.frozen)
+  body_all = []
   for b in config.bodies:
-    inertia = b.inertia
-    if inertia.x == 0 and inertia.y == 0 and inertia.z == 0:
-      b.inertia.x, b.inertia.y, b.inertia.z = 1, 1, 1
-    b.frozen.position.x = b.frozen.position.x or frozen.position.x
-    b.frozen.position.y = b.frozen.position.y or frozen.position.y
-    b.frozen.position.z = b.frozen.position.z or frozen.position.z
-    b.frozen.rotation.x = b.frozen.rotation.x or frozen.rotation.x
-    b.frozen.rotation.y = b.frozen.rotation.y or frozen.rotation.y
-    b.frozen.rotation.z = b.frozen.rotation.z or frozen.rotation.z
-    if b.frozen.all:
-      b.frozen.position.CopyFrom(allvec)
-      b.frozen.rotation.CopyFrom(allvec)
-    if all([b.frozen.position.x, b.frozen.position.y, b.frozen.position.z,
-            b.frozen.rotation.x, b.frozen.rotation.y, b.frozen.rotation.z]):
-      b.frozen.all = True
+    if not (b.inertia.x or b.inertia.y or b.inertia.z):
+      b.inertia.x = b.inertia.y = b.inertia.z = 1
+    body_all.append(_reify_frozen(b.frozen, config.frozen))
     for c in b.colliders:
       if not c.HasField('material'):
         c.material.friction = config.friction
         c.material.elasticity = config.elasticity
-  frozen.all = all(b.frozen.all for b in config.bodies)
+  config.frozen.all = all(body_all)
   return config
 
 

@@ -9,6 +9,7 @@ MI355X_MICROARCH.md prescribes for gfx950 (FETCH_SIZE reports half of a wide
 coalesced read: doubled; WRITE_SIZE exact for 16-B-per-lane stores; both in KB).
 """
 import csv
+import hashlib
 import json
 import os
 import shutil
@@ -17,8 +18,13 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# algorithmic bytes per launch, for the kernels the bench runs
-ANT_ENV_STEP_B = 1428
+# algorithmic bytes per env-step of the fused env kernels the bench runs,
+# keyed by the exact rocprof instantiation: QP in+out 2*52*N,
+# action 4*A, obs 4*O, reward/done 8.
+ENV_STEP_B = {
+    'bx::env_step_kernel<16, 1, 32, 4>': 1428,  # Ant: N=10, A=8, O=87
+    'bx::env_step_kernel<16, 1, 33, 4>': 2284,  # Humanoid: N=12, A=17, O=240
+}
 PHASE_B = {'kinetic_kernel': 80 * 10, 'update_acc_kernel': 72 * 10, 'vproj_kernel': 96 * 10,
            'capsule_plane_kernel': 120 * 5}
 
@@ -83,9 +89,9 @@ def main():
            'hbm_write_bytes_per_launch': e['hbm_write_bytes_per_launch'],
            'grid': e.get('grid'), 'avg_ns': (e.get('trace') or {}).get('avg_ns')}
     base = k.split('::')[-1].split('<')[0]
-    if base == 'env_step_kernel':
+    if k in ENV_STEP_B:
       ent['batch'] = e['grid'] // 64 * 4  # 16 lanes per env, 4 envs per 64-wide workgroup
-      ent['algorithmic_bytes_per_launch'] = ANT_ENV_STEP_B * ent['batch']
+      ent['algorithmic_bytes_per_launch'] = ENV_STEP_B[k] * ent['batch']
     elif base in PHASE_B:
       envs = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20  # bench --phase-envs
       ent['envs'] = envs
@@ -93,6 +99,14 @@ def main():
     traffic['kernels'][k] = ent
   with open(os.path.join(prof, 'traffic.json'), 'w') as f:
     json.dump(traffic, f, indent=1)
+  # rocprof_latest.json: the kernel-trace averages, keyed to the library build
+  # they were measured on (bench.py reports them only for that exact build)
+  lib = os.path.join(ROOT, 'brax_amd', '_lib', 'libbrax_amd.so')
+  with open(lib, 'rb') as f:
+    sha = hashlib.sha1(f.read()).hexdigest()
+  with open(os.path.join(prof, 'rocprof_latest.json'), 'w') as f:
+    json.dump({'round': tag, 'source': f'profiles/{tag}_kernel_stats.csv', 'lib_sha1': sha,
+               'kernels': stats}, f, indent=1)
   print(json.dumps(traffic, indent=1))
 
 
