@@ -373,7 +373,9 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
 
   // per-env LDS layout
   int L = std::max({N, J, K, R, 1});
-  L = L <= 16 ? 16 : (L <= 32 ? 32 : 64);
+  // an env is one 16/32/64-lane segment of a wave; past 64 items (large
+  // scenes) it spreads over a whole 128- or 256-thread workgroup
+  L = L <= 16 ? 16 : L <= 32 ? 32 : L <= 64 ? 64 : L <= 128 ? 128 : 256;
   H.L = L;
   int off = 0;
   auto carve = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
@@ -395,6 +397,8 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.env_words = (off + 63) & ~63;
   size_t mx = 0;
   int max_groups = 0;
+  bool xcol = false;  // extended contact functions run in the item-loop kernel
+  for (int g = 0; g < G; g++) xcol |= d->col_fn[g] >= BX_COL_HEIGHTMAP;
   {
     for (int b = 0; b < N; b++) {
       mx = std::max({mx, jl[b].size(), al[b].size(), cl[b].size()});
@@ -405,8 +409,6 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     }
     // the register-hoisted kernel is the pbd step only; legacy_spring systems
     // run the item-loop kernel
-    bool xcol = false;  // extended contact functions run in the item-loop kernel
-    for (int g = 0; g < G; g++) xcol |= d->col_fn[g] >= BX_COL_HEIGHTMAP;
     H.single = (N <= L && J <= L && K <= L && R <= L && mx <= 8 && max_groups <= 2 &&
                 H.n_nn == 0 && !H.spring && !xcol) ? 1 : 0;
     H.act_same = 1;
@@ -429,12 +431,14 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     }
     if (d->n_forces > 0) f |= 16;
     if (max_groups <= 1) f |= 32;  // F_G1: one collider group per body
+    if (xcol) f |= 64;             // F_X: extended contact functions
     S->feat = f;
   }
   S->mode = S->single_ok ? 1 : 0;
   S->host = std::move(B.w);
   S->L = L;
-  S->lds_env = (size_t)(64 / L) * H.env_words * 4;
+  S->tpb = L > 64 ? L : 64;
+  S->lds_env = (size_t)(L > 64 ? 1 : 64 / L) * H.env_words * 4;
   S->lds_reset = (size_t)64 * N * 13 * 4;
   if (S->lds_env > 160 * 1024) return fail("system too large for one workgroup's LDS");
   if (r && S->lds_reset > 160 * 1024) return fail("system too large for the reset kernel's LDS");
@@ -575,14 +579,16 @@ int bx_system_set_single(bx_system* S, int on) {
 
 int bx_system_set_variant(bx_system* S, int lanes, int mode) {
   if (!S) return fail("null system");
-  if (lanes != 16 && lanes != 32 && lanes != 64) return fail("lanes must be 16, 32 or 64");
-  if (lanes < S->min_L) return fail("lanes below the system's minimum");
+  if (lanes != 16 && lanes != 32 && lanes != 64 && lanes != 128 && lanes != 256)
+    return fail("lanes must be 16, 32, 64, 128 or 256");
   if (mode < 0 || mode > 2) return fail("mode must be 0 (global), 1 (single) or 2 (lds)");
-  if (mode == 1 && !S->single_ok) return fail("system does not fit the single-item-per-lane kernel");
+  if (mode == 1 && (!S->single_ok || lanes < S->min_L || lanes > 64))
+    return fail("system does not fit the single-item-per-lane kernel");
   int old_L = S->L, old_m = S->mode, old_t = S->tpb;
   S->L = lanes;
   S->mode = mode;
-  if (S->tpb % lanes) S->tpb = 64;
+  if (lanes > 64) S->tpb = lanes;
+  else if (S->tpb > 64 || S->tpb % lanes) S->tpb = 64;
   if (step_lds(S) > 160 * 1024) {
     S->L = old_L;
     S->mode = old_m;
@@ -594,8 +600,9 @@ int bx_system_set_variant(bx_system* S, int lanes, int mode) {
 
 int bx_system_set_block(bx_system* S, int threads) {
   if (!S) return fail("null system");
-  if (threads < S->L || threads > 64 || threads % S->L)
-    return fail("threads must be a multiple of the lanes per env, at most 64");
+  if (threads < S->L || threads > (S->L > 64 ? S->L : 64) || threads % S->L)
+    return fail("threads must be a multiple of the lanes per env, at most 64 (or the lanes "
+                "per env past 64)");
   int old = S->tpb;
   S->tpb = threads;
   if (step_lds(S) > 160 * 1024) {
@@ -634,7 +641,7 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   if (S->mode == 1)
     HIP_OK(launch_system_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   else
-    HIP_OK(launch_system_step_generic(S->L, S->mode, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
+    HIP_OK(launch_system_step_generic(S->L, S->mode, S->feat, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
 }
 
@@ -664,7 +671,7 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   if (S->mode == 1)
     HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   else
-    HIP_OK(launch_env_step_generic(S->L, S->mode, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
+    HIP_OK(launch_env_step_generic(S->L, S->mode, S->feat, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
 }
 

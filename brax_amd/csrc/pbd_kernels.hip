@@ -187,6 +187,10 @@ enum { F_SPH = 1, F_ANGLE = 2, F_CC = 4, F_TW = 8, F_FORCE = 16, F_ALL = 31 };
 // F_G1 (outside F_ALL): every body's contact rows come from one collider
 // group, so the per-group normalisation needs one accumulator
 enum { F_G1 = 32 };
+// F_X (outside F_ALL): the extended contact functions (height map, clipped
+// plane, capsule-mesh, box-box SAT), item-loop kernels only. F_GEN: every
+// feature, the item-loop kernels' general instantiation.
+enum { F_X = 64, F_GEN = F_ALL | F_X };
 template <int F> __device__ __forceinline__ bool is_rev(int type) {
   if constexpr ((F & F_SPH) == 0) return true; else return type == 1;
 }
@@ -884,12 +888,14 @@ template <int F>
 __device__ __forceinline__ void contact_gen_x(const Cst& c, const BlobHdr& H, int r, const RowC& R,
                                               const QP& a, const QP& b, v3& pos, v3& vel, v3& n,
                                               float& pen) {
-  const int o = H.o_row + r * ROW_STRIDE;
-  if (R.fn == BX_COL_HEIGHTMAP) heightmap_contact(c, H, o, R, a, b, pos, vel, n, pen);
-  else if (R.fn == BX_COL_CLIPPED_PLANE) clipped_contact(c, o, R, a, b, pos, vel, n, pen);
-  else if (R.fn == BX_COL_CAPSULE_MESH) capsule_mesh_contact(c, o, R, a, b, pos, vel, n, pen);
-  else if (R.fn == BX_COL_HULL_HULL) hull_contact(c, H, o, a, b, pos, vel, n, pen);
-  else contact_gen<F>(R, a, b, pos, vel, n, pen);
+  if constexpr ((F & F_X) != 0) {
+    const int o = H.o_row + r * ROW_STRIDE;
+    if (R.fn == BX_COL_HEIGHTMAP) { heightmap_contact(c, H, o, R, a, b, pos, vel, n, pen); return; }
+    if (R.fn == BX_COL_CLIPPED_PLANE) { clipped_contact(c, o, R, a, b, pos, vel, n, pen); return; }
+    if (R.fn == BX_COL_CAPSULE_MESH) { capsule_mesh_contact(c, o, R, a, b, pos, vel, n, pen); return; }
+    if (R.fn == BX_COL_HULL_HULL) { hull_contact(c, H, o, a, b, pos, vel, n, pen); return; }
+  }
+  contact_gen<F>(R, a, b, pos, vel, n, pen);
 }
 
 // One/TwoWay._position_contact (colliders.py:306-377, 495-580)
@@ -1126,6 +1132,13 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
 // ds_write sees it without draining lgkmcnt. Only the compiler must not move
 // or forward memory accesses across the boundary.
 __device__ __forceinline__ void sync() { asm volatile("" ::: "memory"); }
+// An env spread over L > 64 threads (large scenes: 128 or 256 threads = 2-4
+// waves of one workgroup, one env per workgroup) needs a real workgroup
+// barrier at each phase boundary; within one wave the compiler fence above.
+template <int L>
+__device__ __forceinline__ void esync() {
+  if constexpr (L > 64) __syncthreads(); else sync();
+}
 
 // a culled row's slots: no update, not counted
 __device__ __forceinline__ void zero_row_slots(const Env& E, int r) {
@@ -1152,7 +1165,7 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
       E.alist[c.i(og + G_INFO) + r - c.i(og + G_R0)] = r;
     }
   }
-  sync();
+  esync<L>();
   for (int g = 0; g < H.G; g++) {
     const int og = H.o_group + g * GROUP_STRIDE;
     const int cut = c.i(og + G_CUT);
@@ -1168,7 +1181,7 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
       v3 pb = b.pos + rotate(c.f3(o + R_BPOS), b.rot);
       E.rowd[r * ROWD_STRIDE + 8] = norm(pb - pa);
     }
-    sync();
+    esync<L>();
     for (int k = 0; k < cut; k++) {
       // the lane's nearest unselected cell, as a (distance bits, row) key:
       // distances are >= 0, so their bit patterns order like the floats
@@ -1180,19 +1193,29 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
         best = key < best ? key : best;
       }
       // minimum over the env's L lanes (aligned L-lane segment of the wave)
+      constexpr int W = L < 64 ? L : 64;
 #pragma unroll
-      for (int off = L / 2; off > 0; off >>= 1) {
-        unsigned lo = __shfl_xor((unsigned)best, off, L);
-        unsigned hi = __shfl_xor((unsigned)(best >> 32), off, L);
+      for (int off = W / 2; off > 0; off >>= 1) {
+        unsigned lo = __shfl_xor((unsigned)best, off, W);
+        unsigned hi = __shfl_xor((unsigned)(best >> 32), off, W);
         unsigned long long o2 = ((unsigned long long)hi << 32) | lo;
         best = o2 < best ? o2 : best;
+      }
+      if constexpr (L > 64) {
+        // then over the env's waves: each wave's minimum through LDS
+        // (red words 40.. hold one 64-bit key per wave)
+        unsigned long long* wk = reinterpret_cast<unsigned long long*>(E.red + 40);
+        if ((lane & 63) == 0) wk[lane >> 6] = best;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < L / 64; w++) best = wk[w] < best ? wk[w] : best;
       }
       const int r = (int)(best & 0xFFFFFFFFu);
       if (((r - r0) % L) == lane) {
         E.ract[r] = k;
         E.alist[c.i(og + G_INFO) + k] = r;
       }
-      sync();
+      esync<L>();
     }
   }
 }
@@ -1244,7 +1267,7 @@ __device__ __forceinline__ void store_qp_global(const bx_qp& q, int64_t e, int b
 // ---------------------------------------------------------------------------
 // the PBD step of one env (system.py:254-325), all L lanes of the env
 // ---------------------------------------------------------------------------
-template <int L>
+template <int L, int F>
 __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
                          const float* act, int aw) {
   const int N = H.N, J = H.J, K = H.K, Rn = H.R;
@@ -1273,7 +1296,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
           int ai = A.idx[l];
           al[l] = valid ? act[take_idx(ai, aw)] * (ai >= 0 ? 1.f : 0.f) : 0.f;
         }
-        act_torque<F_ALL>(Jc, A, E, al, a);
+        act_torque<F>(Jc, A, E, al, a);
       }
       for (int j = lane; j < J; j += L) {
         int o = H.o_joint + j * JOINT_STRIDE;
@@ -1285,7 +1308,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         st3(E.jslot + j * SLOT_STRIDE, mul(Ip, tq));
         st3(E.jslot + (E.nJ + j) * SLOT_STRIDE, -1.f * mul(Ic, tq));
       }
-      sync();
+      esync<L>();
       // Euler.update(acc) + Euler.kinetic (integrators.py:50-93)
       for (int b = lane; b < N; b += L) {
         BodyC B = load_body(c, H, b);
@@ -1313,20 +1336,20 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         stqp(E.qp + b * QP_STRIDE, q);
         if (sub == 1) st3(E.acc + b * ACC_STRIDE + ACC_DPA, dpa);
       }
-      sync();
+      esync<L>();
       // Joint.apply (joints.py:79-100)
       for (int j = lane; j < J; j += L) {
         JointC Jc = load_joint(c, H, j);
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), q = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
         q4 dpr, dcr;
-        joint_apply<F_ALL>(Jc, p, q, dpp, dpr, dcp, dcr);
+        joint_apply<F>(Jc, p, q, dpp, dpr, dcp, dcr);
         float* sp = E.jslot + j * SLOT_STRIDE;
         float* sc = E.jslot + (E.nJ + j) * SLOT_STRIDE;
         st3(sp, dpp); st4(sp + 3, dpr);
         st3(sc, dcp); st4(sc + 3, dcr);
       }
-      sync();
+      esync<L>();
       // Euler.update(pos) (+ velocity_projection on the first substep)
       for (int b = lane; b < N; b += L) {
         BodyC B = load_body(c, H, b);
@@ -1357,7 +1380,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         }
         stqp(s, q);
       }
-      sync();
+      esync<L>();
     }
     // ---- collisions on the second substep (system.py:288-313)
     // Collider.position_apply (colliders.py:198-240)
@@ -1368,12 +1391,12 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cpos, cvel, n;
       float pen;
-      contact_gen_x<F_ALL>(c, H, r, R, a, b, cpos, cvel, n, pen);
+      contact_gen_x<F>(c, H, r, R, a, b, cpos, cvel, n, pen);
       const float* pa = E.prev + R.a * PREV_STRIDE;
       const float* pb = E.prev + R.b * PREV_STRIDE;
       v3 oap, obp;
       q4 oar, obr;
-      float dl = position_contact<F_ALL>(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, n, pen,
+      float dl = position_contact<F>(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, n, pen,
                                   oap, oar, obp, obr);
       float* rd = E.rowd + r * ROWD_STRIDE;
       st3(rd, cpos); st3(rd + 3, n); rd[6] = pen; rd[7] = dl;
@@ -1384,7 +1407,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       st3(sb, obp); st4(sb + 3, obr);
       sb[7] = (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f;
     }
-    sync();
+    esync<L>();
     for (int b = lane; b < N; b += L) {
       BodyC B = load_body(c, H, b);
       v3 dp = mk(0.f, 0.f, 0.f);
@@ -1425,7 +1448,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       q.rot = nr;
       stqp(s, q);
     }
-    sync();
+    esync<L>();
     // Collider.velocity_apply (colliders.py:155-196)
     for (int i = lane; i < (H.n_nn ? H.info_rows : Rn); i += L) {
       const int r = H.n_nn ? E.alist[i] : i;
@@ -1435,7 +1458,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       const float* rbb = E.rb + R.b * RB_STRIDE;
       const float* rd = E.rowd + r * ROWD_STRIDE;
       v3 oav, oaa, obv, oba;
-      velocity_contact<F_ALL>(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
+      velocity_contact<F>(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
                        ld3(rbb + 6), ld3(rd), ld3(rd + 3), rd[6], rd[7], oav, oaa, obv, oba);
       float* sa = E.cslot + r * SLOT_STRIDE;
       float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
@@ -1444,7 +1467,7 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       st3(sb, obv); st3(sb + 3, oba);
       sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
     }
-    sync();
+    esync<L>();
     for (int b = lane; b < N; b += L) {
       BodyC B = load_body(c, H, b);
       v3 dv = mk(0.f, 0.f, 0.f), da = mk(0.f, 0.f, 0.f);
@@ -1473,14 +1496,14 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       st3(acc + ACC_ICA, ld3(acc + ACC_ICA) + da);
       st3(acc + ACC_IAA, ld3(acc + ACC_IAA) + ld3(acc + ACC_DPA));
     }
-    sync();
+    esync<L>();
   }
 }
 
 // Collider.apply over the step's active rows (colliders.py:116-153): impulse
 // contacts into the row slots (vel 0..2, ang 3..5, any() flag 7) and the row
 // data (contact pos, normal, penetration) for Info
-template <int L>
+template <int L, int F>
 __device__ void impulse_rows(const Cst& c, const BlobHdr& H, const Env& E, int lane) {
   for (int i = lane; i < (H.n_nn ? H.info_rows : H.R); i += L) {
     const int r = H.n_nn ? E.alist[i] : i;
@@ -1488,9 +1511,9 @@ __device__ void impulse_rows(const Cst& c, const BlobHdr& H, const Env& E, int l
     QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
     v3 cpos, cvel, n;
     float pen;
-    contact_gen_x<F_ALL>(c, H, r, R, a, b, cpos, cvel, n, pen);
+    contact_gen_x<F>(c, H, r, R, a, b, cpos, cvel, n, pen);
     v3 oav, oaa, obv, oba;
-    impulse_contact<F_ALL>(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
+    impulse_contact<F>(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
     float* rd = E.rowd + r * ROWD_STRIDE;
     st3(rd, cpos); st3(rd + 3, n); rd[6] = pen;
     float* sa = E.cslot + r * SLOT_STRIDE;
@@ -1531,7 +1554,7 @@ __device__ __forceinline__ void contact_reduce(const Cst& c, const BlobHdr& H, c
 // acceleration level, then Collider.apply at the velocity level. Info:
 // contact += dp_c, joint += dp_j (in E.rb words 0..5), actuator += dp_a.
 // ---------------------------------------------------------------------------
-template <int L>
+template <int L, int F>
 __device__ void spring_step(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
                             const float* act, int aw) {
   const int N = H.N, J = H.J, K = H.K;
@@ -1555,7 +1578,7 @@ __device__ void spring_step(const Cst& c, const BlobHdr& H, const Env& E, int la
       q.rot = qnormalize(r);
       stqp(E.qp + b * QP_STRIDE, q);
     }
-    sync();
+    esync<L>();
     // spring Joint.apply (spring_joints.py:89-113) -> joint slots (vel, ang)
     for (int j = lane; j < J; j += L) {
       JointC Jc = load_joint(c, H, j);
@@ -1578,9 +1601,9 @@ __device__ void spring_step(const Cst& c, const BlobHdr& H, const Env& E, int la
         int ai = A.idx[l];
         al[l] = valid ? act[take_idx(ai, aw)] * (ai >= 0 ? 1.f : 0.f) : 0.f;
       }
-      act_torque<F_ALL>(Jc, A, E, al, a);
+      act_torque<F>(Jc, A, E, al, a);
     }
-    sync();
+    esync<L>();
     // Euler.update(acc_p = dp_j + dp_a + dp_f) (integrators.py:85-93, system.py:353-357)
     for (int b = lane; b < N; b += L) {
       BodyC B = load_body(c, H, b);
@@ -1608,10 +1631,10 @@ __device__ void spring_step(const Cst& c, const BlobHdr& H, const Env& E, int la
       float* acc = E.acc + b * ACC_STRIDE;
       st3(acc + ACC_IAA, ld3(acc + ACC_IAA) + dpa);
     }
-    sync();
+    esync<L>();
     // Collider.apply (colliders.py:116-153), then Euler.update(vel_p = dp_c)
-    impulse_rows<L>(c, H, E, lane);
-    sync();
+    impulse_rows<L, F>(c, H, E, lane);
+    esync<L>();
     for (int b = lane; b < N; b += L) {
       BodyC B = load_body(c, H, b);
       v3 dv, da;
@@ -1623,7 +1646,7 @@ __device__ void spring_step(const Cst& c, const BlobHdr& H, const Env& E, int la
       st3(acc + ACC_ICV, ld3(acc + ACC_ICV) + dv);
       st3(acc + ACC_ICA, ld3(acc + ACC_ICA) + da);
     }
-    sync();
+    esync<L>();
   }
 }
 
@@ -2013,9 +2036,9 @@ __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane)
     QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
     v3 cpos, cvel, n;
     float pen;
-    contact_gen_x<F_ALL>(c, H, r, R, a, b, cpos, cvel, n, pen);
+    contact_gen_x<F_GEN>(c, H, r, R, a, b, cpos, cvel, n, pen);
     v3 oav, oaa, obv, oba;
-    impulse_contact<F_ALL>(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
+    impulse_contact<F_GEN>(R, a, b, cpos, cvel, n, pen, oav, oaa, obv, oba);
     float* sa = E.cslot + r * SLOT_STRIDE;
     float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
     st3(sa, oav); st3(sa + 3, oaa);
@@ -2023,7 +2046,7 @@ __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane)
     st3(sb, obv); st3(sb + 3, oba);
     sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
   }
-  sync();
+  esync<L>();
   for (int b = lane; b < N; b += L) {
     v3 dv = mk(0.f, 0.f, 0.f), da = mk(0.f, 0.f, 0.f);
     int i = c.i(H.o_cl_off + b), e = c.i(H.o_cl_off + b + 1);
@@ -2045,7 +2068,7 @@ __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane)
     st3(acc + ACC_ICV, dv);
     st3(acc + ACC_ICA, da);
   }
-  sync();
+  esync<L>();
 }
 
 // ---------------------------------------------------------------------------
@@ -2206,7 +2229,7 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
     st3(E.red + 32, com);
     E.red[35] = msum;
   }
-  sync();
+  esync<L>();
   if (obs_out)
     for (int i = lane; i < obs_size; i += L)
       obs_out[i] = obs_elem(c, H, E, kind, flags, i, act, aw, act != nullptr);
@@ -2247,7 +2270,7 @@ __device__ __forceinline__ float* stage_constants(const uint32_t* blob, const Bl
 }
 
 template <int L, int MODE, int F, int M>
-__global__ void __launch_bounds__(64) BX_STEP_ATTR system_step_kernel(StepArgs A) {
+__global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kernel(StepArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
   Cst c{A.blob};
@@ -2267,7 +2290,7 @@ __global__ void __launch_bounds__(64) BX_STEP_ATTR system_step_kernel(StepArgs A
       for (int k = 0; k < 13; k++) s[k] = k == 3 ? 1.f : 0.f;
     }
   }
-  sync();
+  esync<L>();
   if constexpr (S) {
     Hoist<M> X;
     load_hoist<M>(c, H, lane, X);
@@ -2276,9 +2299,9 @@ __global__ void __launch_bounds__(64) BX_STEP_ATTR system_step_kernel(StepArgs A
                              (int)A.act_width, X, icv, ica,
                        iaa);
   } else if (H.spring) {
-    spring_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, (int)A.act_width);
+    spring_step<L, F>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, (int)A.act_width);
   } else {
-    pbd_step<L>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, (int)A.act_width);
+    pbd_step<L, F>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr, (int)A.act_width);
   }
   if (!valid) return;
   for (int b = lane; b < H.N; b += L) {
@@ -2327,7 +2350,7 @@ __global__ void __launch_bounds__(64) BX_STEP_ATTR system_step_kernel(StepArgs A
 
 // Env.step fused with EpisodeWrapper/AutoResetWrapper (wrappers.py:105-148)
 template <int L, int MODE, int F, int M>
-__global__ void __launch_bounds__(64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
+__global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
   BX_KSTAMP_DECL
   extern __shared__ __attribute__((aligned(16))) float smem[];
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
@@ -2359,7 +2382,7 @@ __global__ void __launch_bounds__(64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
       for (int k = 0; k < 13; k++) s[k] = k == 3 ? 1.f : 0.f;
     }
   }
-  sync();
+  esync<L>();
   float steps = 0.f;
   if (valid && A.in.steps) steps = (P.auto_reset && done_in != 0.f) ? 0.f : steps_in;
   float done = P.auto_reset ? 0.f : done_in;
@@ -2375,14 +2398,14 @@ __global__ void __launch_bounds__(64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
     v3 com0 = mk(0.f, 0.f, 0.f);
     float msum = 0.f;
     if (kind == BX_ENV_HUMANOID) humanoid_com(c, H, E.qp, com0, msum);
-    sync();
+    esync<L>();
     if constexpr (S) {
       v3 icv, ica, iaa;
       pbd_step_single<L, F, M>(c, H, E, lane, valid, act, aw, X, icv, ica, iaa);
     } else if (H.spring) {
-      spring_step<L>(c, H, E, lane, valid, act, aw);
+      spring_step<L, F>(c, H, E, lane, valid, act, aw);
     } else {
-      pbd_step<L>(c, H, E, lane, valid, act, aw);
+      pbd_step<L, F>(c, H, E, lane, valid, act, aw);
     }
     BX_KSTAMP(11);
     env_observe<L>(c, H, E, lane, kind, P.obs_flags, P.obs_size, act, aw,
@@ -2449,7 +2472,7 @@ __global__ void __launch_bounds__(64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
       reward_sum = rep == 0 ? reward : reward_sum + reward;
       E.red[0] = done;
     }
-    sync();
+    esync<L>();
   }
   BX_KSTAMP(13);
   if (!valid) return;
@@ -2487,7 +2510,7 @@ __global__ void __launch_bounds__(64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
 
 // System.info contact part + optional Env._get_obs of the same state (reset)
 template <int L>
-__global__ void __launch_bounds__(64) info_obs_kernel(InfoArgs A) {
+__global__ void __launch_bounds__(L > 64 ? L : 64) info_obs_kernel(InfoArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Cst c{A.blob};
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
@@ -2504,10 +2527,10 @@ __global__ void __launch_bounds__(64) info_obs_kernel(InfoArgs A) {
       for (int k = 0; k < 13; k++) s[k] = k == 3 ? 1.f : 0.f;
     }
   }
-  sync();
+  esync<L>();
   if (A.angle) {  // Joint.angle_vel only
     joint_angles<L>(c, H, E, lane);
-    sync();
+    esync<L>();
     if (valid)
       for (int i = lane; i < H.D; i += L) {
         A.angle[e * H.D + i] = E.ang[i];
@@ -2687,14 +2710,24 @@ static void launch_one(void (*k)(Args), dim3 grid, int tpb, size_t lds, hipStrea
   } else {                                                                          \
     launch_one<ARGS>(KERNEL<64, 1, F_ALL, 8>, grid, tpb, lds, s, a);                \
   }
+// item-loop kernels: a lean instantiation (revolute joints, torque
+// actuators, capsule-plane / capsule-capsule rows one- or two-way, no forces:
+// Ant Mountain, the culled scenes) where the system allows, else every feature
+#define F_LEAN (F_CC | F_TW)
 #define BX_DISPATCH_GENERIC(KERNEL, ARGS)                                           \
-  switch (L * 4 + mode) {                                                           \
-    case 16 * 4 + 0: launch_one<ARGS>(KERNEL<16, 0, F_ALL, 8>, grid, tpb, lds, s, a); break; \
-    case 16 * 4 + 2: launch_one<ARGS>(KERNEL<16, 2, F_ALL, 8>, grid, tpb, lds, s, a); break; \
-    case 32 * 4 + 0: launch_one<ARGS>(KERNEL<32, 0, F_ALL, 8>, grid, tpb, lds, s, a); break; \
-    case 32 * 4 + 2: launch_one<ARGS>(KERNEL<32, 2, F_ALL, 8>, grid, tpb, lds, s, a); break; \
-    case 64 * 4 + 0: launch_one<ARGS>(KERNEL<64, 0, F_ALL, 8>, grid, tpb, lds, s, a); break; \
-    case 64 * 4 + 2: launch_one<ARGS>(KERNEL<64, 2, F_ALL, 8>, grid, tpb, lds, s, a); break; \
+  const bool lean = (feat & (F_SPH | F_ANGLE | F_FORCE | F_X)) == 0;                \
+  switch (L * 8 + mode * 2 + (lean ? 1 : 0)) {                                      \
+    case 16 * 8 + 0: case 16 * 8 + 1: launch_one<ARGS>(KERNEL<16, 0, F_GEN, 8>, grid, tpb, lds, s, a); break; \
+    case 16 * 8 + 4: case 16 * 8 + 5: launch_one<ARGS>(KERNEL<16, 2, F_GEN, 8>, grid, tpb, lds, s, a); break; \
+    case 32 * 8 + 0: case 32 * 8 + 1: launch_one<ARGS>(KERNEL<32, 0, F_GEN, 8>, grid, tpb, lds, s, a); break; \
+    case 32 * 8 + 4: case 32 * 8 + 5: launch_one<ARGS>(KERNEL<32, 2, F_GEN, 8>, grid, tpb, lds, s, a); break; \
+    case 64 * 8 + 0: launch_one<ARGS>(KERNEL<64, 0, F_GEN, 8>, grid, tpb, lds, s, a); break; \
+    case 64 * 8 + 1: launch_one<ARGS>(KERNEL<64, 0, F_LEAN, 8>, grid, tpb, lds, s, a); break; \
+    case 64 * 8 + 4: case 64 * 8 + 5: launch_one<ARGS>(KERNEL<64, 2, F_GEN, 8>, grid, tpb, lds, s, a); break; \
+    case 128 * 8 + 0: launch_one<ARGS>(KERNEL<128, 0, F_GEN, 8>, grid, tpb, lds, s, a); break; \
+    case 128 * 8 + 1: launch_one<ARGS>(KERNEL<128, 0, F_LEAN, 8>, grid, tpb, lds, s, a); break; \
+    case 256 * 8 + 0: launch_one<ARGS>(KERNEL<256, 0, F_GEN, 8>, grid, tpb, lds, s, a); break; \
+    case 256 * 8 + 1: launch_one<ARGS>(KERNEL<256, 0, F_LEAN, 8>, grid, tpb, lds, s, a); break; \
     default: return hipErrorInvalidValue;                                           \
   }
 
@@ -2733,14 +2766,14 @@ hipError_t debug_stamps(unsigned long long* out, int reset) {
 #endif
 }
 #else
-hipError_t launch_system_step_generic(int L, int mode, int tpb, int64_t n_envs, size_t lds,
+hipError_t launch_system_step_generic(int L, int mode, int feat, int tpb, int64_t n_envs, size_t lds,
                                       hipStream_t s, const StepArgs& a) {
   const int epb = tpb / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
   BX_DISPATCH_GENERIC(system_step_kernel, StepArgs)
   return hipGetLastError();
 }
-hipError_t launch_env_step_generic(int L, int mode, int tpb, int64_t n_envs, size_t lds,
+hipError_t launch_env_step_generic(int L, int mode, int feat, int tpb, int64_t n_envs, size_t lds,
                                    hipStream_t s, const EnvArgs& a) {
   const int epb = tpb / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
@@ -2748,9 +2781,11 @@ hipError_t launch_env_step_generic(int L, int mode, int tpb, int64_t n_envs, siz
   return hipGetLastError();
 }
 hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a) {
-  int epb = 64 / L;
+  int epb = L > 64 ? 1 : 64 / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
-  if (L == 16) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<16>, grid, dim3(64), lds, s, a); }
+  if (L == 128) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<128>, grid, dim3(128), lds, s, a); }
+  else if (L == 256) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<256>, grid, dim3(256), lds, s, a); }
+  else if (L == 16) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<16>, grid, dim3(64), lds, s, a); }
   else if (L == 32) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<32>, grid, dim3(64), lds, s, a); }
   else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<64>, grid, dim3(64), lds, s, a); }
   return hipGetLastError();

@@ -64,9 +64,9 @@ hipError_t launch_system_step_single(int L, int feat, int gw, int tpb, int64_t n
 hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
                                   hipStream_t s, const EnvArgs& a);
 // item-loop step kernels (generic translation unit)
-hipError_t launch_system_step_generic(int L, int mode, int tpb, int64_t n_envs, size_t lds,
+hipError_t launch_system_step_generic(int L, int mode, int feat, int tpb, int64_t n_envs, size_t lds,
                                       hipStream_t s, const StepArgs& a);
-hipError_t launch_env_step_generic(int L, int mode, int tpb, int64_t n_envs, size_t lds,
+hipError_t launch_env_step_generic(int L, int mode, int feat, int tpb, int64_t n_envs, size_t lds,
                                    hipStream_t s, const EnvArgs& a);
 hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a);
 hipError_t launch_default_qp(int64_t n_envs, size_t lds, hipStream_t s, const ResetArgs& a);
