@@ -50,6 +50,7 @@ struct bx_system {
   int gw = 8;       // gather width (max per-body list length, 4 or 8)
   int tpb = 64;     // threads per workgroup of the step kernels (multiple of L)
   bool single_ok = false;
+  bool multi_ok = false;  // MODE_MULTI (3): large pbd scenes, 256 threads per env
   size_t lds_env = 0;    // bytes per block for the per-env kernels
   size_t lds_reset = 0;  // bytes per block for default_qp
 };
@@ -313,6 +314,36 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   put_lists(jl, H.o_jl_off, H.o_jl);
   put_lists(al, H.o_al_off, H.o_al);
   put_lists(cl, H.o_cl_off, H.o_cl);
+  // MULTI-mode gather tasks: each body's contact list cut, per collider group,
+  // into runs of <= TASK_W slots (same order); a body's tasks in list order
+  std::vector<std::vector<int>> task_e;  // slot indices
+  std::vector<std::vector<int>> btask(N);  // task | group << 24
+  int max_btask = 0;
+  for (int b = 0; b < N; b++) {
+    size_t i = 0;
+    while (i < cl[b].size()) {
+      const int g = cl[b][i] >> 24;
+      std::vector<int> t;
+      while (i < cl[b].size() && (cl[b][i] >> 24) == g && (int)t.size() < TASK_W)
+        t.push_back(cl[b][i++] & 0xFFFFFF);
+      btask[b].push_back((int)task_e.size() | (g << 24));
+      task_e.push_back(t);
+    }
+    max_btask = std::max(max_btask, (int)btask[b].size());
+  }
+  H.T = (int)task_e.size();
+  H.o_task = B.alloc(H.T * TASK_W);
+  for (int t = 0; t < H.T; t++)
+    for (int k = 0; k < TASK_W; k++)
+      B.i(H.o_task + t * TASK_W + k, k < (int)task_e[t].size() ? task_e[t][k] : 2 * R);
+  H.o_btask = B.alloc(N * BTASK_W);
+  for (int b = 0; b < N; b++) {
+    // padding: the zero task (index T, a zero partial) in the last group
+    const int gl = btask[b].empty() ? 0 : (btask[b].back() >> 24);
+    for (int k = 0; k < BTASK_W; k++)
+      B.i(H.o_btask + b * BTASK_W + k,
+          k < (int)btask[b].size() ? btask[b][k] : (H.T | (gl << 24)));
+  }
 
   // reset tables
   if (r) {
@@ -385,13 +416,21 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // slot regions end with one zero slot (padding target of the gather lists)
   H.l_jslot = carve((2 * J + 1) * SLOT_STRIDE);
   H.l_aslot = carve((2 * K + 1) * ASLOT_STRIDE);
-  H.l_rowd = carve(R * ROWD_STRIDE);
-  H.l_cslot = carve((2 * R + 1) * SLOT_STRIDE);
   H.l_acc = carve(N * ACC_STRIDE);
   H.l_ract = carve(R);
   H.l_alist = carve(H.info_rows);
   H.l_ang = carve(2 * D);
   H.l_red = carve(64);
+  // the contact regions form each mode's tail: the item-loop / SINGLE
+  // kernels keep per-row data and 12-word slots, MULTI mode keeps the row data
+  // in registers and needs 8-word slots plus the task partials
+  const int tail = off;
+  H.l_mslot = carve((2 * R + 1) * MSLOT_STRIDE);
+  H.l_tslot = carve((H.T + 1) * MSLOT_STRIDE);
+  H.env_words_m = (off + 63) & ~63;
+  off = tail;
+  H.l_rowd = carve(R * ROWD_STRIDE);
+  H.l_cslot = carve((2 * R + 1) * SLOT_STRIDE);
   // envs 64 words apart: with the odd-multiple record strides, the four
   // envs' records of one ds_read_b128 lane group land on distinct bank slots
   H.env_words = (off + 63) & ~63;
@@ -411,6 +450,12 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     // run the item-loop kernel
     H.single = (N <= L && J <= L && K <= L && R <= L && mx <= 8 && max_groups <= 2 &&
                 H.n_nn == 0 && !H.spring && !xcol) ? 1 : 0;
+    // MULTI mode: a pbd scene past one wave (256 threads per env), every
+    // lane owning <= 1 body / joint / actuator / task and <= MULTI_MR rows
+    size_t mxja = 0;
+    for (int b = 0; b < N; b++) mxja = std::max({mxja, jl[b].size(), al[b].size()});
+    H.multi = (!H.single && L > 64 && !H.spring && !xcol && N <= 256 && J <= 256 && K <= 256 &&
+               H.T <= 256 && R <= MULTI_MR * 256 && mxja <= 8 && max_btask <= BTASK_W) ? 1 : 0;
     H.act_same = 1;
     for (int a = 0; a < K; a++)
       if (d->act_joint[a] != a) H.act_same = 0;
@@ -434,10 +479,13 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     if (xcol) f |= 64;             // F_X: extended contact functions
     S->feat = f;
   }
-  S->mode = S->single_ok ? 1 : 0;
+  // the MULTI kernel is instantiated for the lean feature set (revolute,
+  // torque, capsule-plane / capsule-capsule, no forces)
+  S->multi_ok = H.multi != 0 && (S->feat & (1 | 2 | 16 | 64)) == 0;
+  S->mode = S->single_ok ? 1 : (S->multi_ok ? 3 : 0);
   S->host = std::move(B.w);
-  S->L = L;
-  S->tpb = L > 64 ? L : 64;
+  S->L = S->multi_ok ? 256 : L;
+  S->tpb = S->L > 64 ? S->L : 64;
   S->lds_env = (size_t)(L > 64 ? 1 : 64 / L) * H.env_words * 4;
   S->lds_reset = (size_t)64 * N * 13 * 4;
   if (S->lds_env > 160 * 1024) return fail("system too large for one workgroup's LDS");
@@ -513,6 +561,7 @@ int check_env(const bx_system* S, const bx_env_params* P) {
 }
 
 size_t step_lds(const bx_system* S) {
+  if (S->mode == 3) return (size_t)S->hdr.env_words_m * 4;
   size_t b = (size_t)(S->tpb / S->L) * S->hdr.env_words * 4;
   if (S->mode == 2) b += (size_t)S->hdr.const_words * 4;
   return b;
@@ -581,9 +630,11 @@ int bx_system_set_variant(bx_system* S, int lanes, int mode) {
   if (!S) return fail("null system");
   if (lanes != 16 && lanes != 32 && lanes != 64 && lanes != 128 && lanes != 256)
     return fail("lanes must be 16, 32, 64, 128 or 256");
-  if (mode < 0 || mode > 2) return fail("mode must be 0 (global), 1 (single) or 2 (lds)");
+  if (mode < 0 || mode > 3) return fail("mode must be 0 (global), 1 (single), 2 (lds) or 3 (multi)");
   if (mode == 1 && (!S->single_ok || lanes < S->min_L || lanes > 64))
     return fail("system does not fit the single-item-per-lane kernel");
+  if (mode == 3 && (!S->multi_ok || lanes != 256))
+    return fail("system does not fit the MULTI-mode kernel (256 lanes)");
   int old_L = S->L, old_m = S->mode, old_t = S->tpb;
   S->L = lanes;
   S->mode = mode;
@@ -640,6 +691,8 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   if (info) a.info = *info;
   if (S->mode == 1)
     HIP_OK(launch_system_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
+  else if (S->mode == 3)
+    HIP_OK(launch_system_step_multi(S->feat, (S->hdr.R + 255) / 256, n_envs, step_lds(S), as_stream(stream), a));
   else
     HIP_OK(launch_system_step_generic(S->L, S->mode, S->feat, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
@@ -670,6 +723,9 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   a.act_width = act_width;
   if (S->mode == 1)
     HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
+  else if (S->mode == 3)  // MULTI-mode systems step envs with the item-loop kernel
+    HIP_OK(launch_env_step_generic(S->L, 0, S->feat, S->tpb, n_envs,
+                                   (size_t)S->hdr.env_words * 4, as_stream(stream), a));
   else
     HIP_OK(launch_env_step_generic(S->L, S->mode, S->feat, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   return 0;

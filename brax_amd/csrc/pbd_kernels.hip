@@ -72,6 +72,10 @@ struct Env {
   float* red;    // 64 scratch
   int* ract;     // R: NearNeighbors rank of the row this step, -1 = culled
   int* alist;    // info_rows: the step's active rows in Info order
+  int sstride;   // contact slot stride: SLOT_STRIDE, or MSLOT_STRIDE in MULTI mode
+  float* tslot;  // MULTI mode: (T + 1) x MSLOT_STRIDE gather-task partials, zero last
+  float* nd;     // NearNeighbors candidate distances, stride nds (scratch, before the substeps)
+  int nds;
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -1106,7 +1110,7 @@ __device__ __forceinline__ float* al16(float* p) {
   return reinterpret_cast<float*>(__builtin_assume_aligned(p, 16));
 }
 
-__device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
+__device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi = false) {
   Env E;
   E.qp = al16(base + H.l_qp);
   E.prev = al16(base + H.l_prev);
@@ -1123,6 +1127,22 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H) {
   E.nJ = H.J;
   E.nK = H.K;
   E.nR = H.R;
+  if (multi) {
+    // MULTI: 8-word contact slots and task partials; no row-data region (the
+    // row's contact stays in its lane's registers); the task partials double
+    // as NearNeighbors scratch before the substeps
+    E.rowd = nullptr;
+    E.cslot = al16(base + H.l_mslot);
+    E.tslot = al16(base + H.l_tslot);
+    E.sstride = MSLOT_STRIDE;
+    E.nd = E.tslot;
+    E.nds = 1;
+  } else {
+    E.tslot = nullptr;
+    E.sstride = SLOT_STRIDE;
+    E.nd = E.rowd + 8;  // rowd word 8 is free until the first position pass
+    E.nds = ROWD_STRIDE;
+  }
   return E;
 }
 
@@ -1142,8 +1162,8 @@ __device__ __forceinline__ void esync() {
 
 // a culled row's slots: no update, not counted
 __device__ __forceinline__ void zero_row_slots(const Env& E, int r) {
-  float* sa = E.cslot + r * SLOT_STRIDE;
-  float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
+  float* sa = E.cslot + r * E.sstride;
+  float* sb = E.cslot + (E.nR + r) * E.sstride;
   for (int k = 0; k < 8; k++) { sa[k] = 0.f; sb[k] = 0.f; }
 }
 
@@ -1171,15 +1191,15 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
     const int cut = c.i(og + G_CUT);
     if (cut == 0) continue;
     const int r0 = c.i(og + G_R0), r1 = c.i(og + G_R1);
-    // candidate-centre distance of every cell, once (rowd word 8 is free
-    // until the position pass of the first substep)
+    // candidate-centre distance of every cell, once (E.nd: scratch until the
+    // position pass of the first substep)
     for (int r = r0 + lane; r < r1; r += L) {
       const int o = H.o_row + r * ROW_STRIDE;
       const int ba = c.i(o + R_A), bb = c.i(o + R_B);
       QP a = ldqp(E.qp + ba * QP_STRIDE), b = ldqp(E.qp + bb * QP_STRIDE);
       v3 pa = a.pos + rotate(c.f3(o + R_APOS), a.rot);
       v3 pb = b.pos + rotate(c.f3(o + R_BPOS), b.rot);
-      E.rowd[r * ROWD_STRIDE + 8] = norm(pb - pa);
+      E.nd[r * E.nds] = norm(pb - pa);
     }
     esync<L>();
     for (int k = 0; k < cut; k++) {
@@ -1188,7 +1208,7 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
       unsigned long long best = ~0ull;
       for (int r = r0 + lane; r < r1; r += L) {
         if (E.ract[r] >= 0) continue;
-        const float d = E.rowd[r * ROWD_STRIDE + 8];
+        const float d = E.nd[r * E.nds];
         unsigned long long key = ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)r;
         best = key < best ? key : best;
       }
@@ -1237,8 +1257,9 @@ __device__ __forceinline__ int row_info(const Cst& c, const BlobHdr& H, const En
 __device__ __forceinline__ void zero_slots(const Env& E, const BlobHdr& H, int lane) {
   if (lane < SLOT_STRIDE) {
     E.jslot[2 * H.J * SLOT_STRIDE + lane] = 0.f;
-    E.cslot[2 * H.R * SLOT_STRIDE + lane] = 0.f;
+    if (lane < E.sstride) E.cslot[2 * H.R * E.sstride + lane] = 0.f;
     if (lane < ASLOT_STRIDE) E.aslot[2 * H.K * ASLOT_STRIDE + lane] = 0.f;
+    if (E.tslot && lane < MSLOT_STRIDE) E.tslot[H.T * MSLOT_STRIDE + lane] = 0.f;
   }
 }
 
@@ -2019,6 +2040,336 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// MULTI mode: large pbd scenes (Ant Mountain: 37 bodies, 32 joints, 702
+// contact rows). One env per 256-thread workgroup (4 waves, workgroup
+// barriers between phases). Lane l owns body l, joint l and actuator l with
+// their constants hoisted into registers (as SINGLE mode), contact rows l,
+// l + L, ... (<= MR, constants hoisted, the row's contact kept in registers
+// between the position and velocity passes) and gather task l. The
+// reference's per-body segment_sums over up to ~40 contact rows become two
+// short fixed-order phases: each task sums <= TASK_W slots of one body and
+// collider group into a partial, then each body adds its <= BTASK_W partials
+// group by group, each group divided by (eps + count) (colliders.py:198-240).
+// ---------------------------------------------------------------------------
+template <int MR>
+struct HoistM {
+  bool hasB, hasJ, hasA;
+  BodyC B;
+  JointC J;
+  ActC A;
+  GList<MAXG> jl, al;
+  int te[TASK_W];   // the lane's task: contact slot indices (padding: the zero slot)
+  int bt[BTASK_W];  // the lane's body: task | group << 24 (padding: the zero task)
+#if defined(BX_MULTI_HOIST_ROWS)
+  RowC R[MR];
+#endif
+};
+// a lane's m-th row constants, read from the L2-resident blob at each pass:
+// at <= 256 VGPRs the kernel runs two waves per SIMD (two envs per CU), which
+// hides those loads. Measured (Ant Mountain(4), 2048 envs, rows per lane 3):
+// 0.44 ms per step, against 0.68 ms with the rows hoisted into registers
+// (BX_MULTI_HOIST_ROWS: 256 VGPRs + 78 AGPRs, one wave per SIMD).
+#if defined(BX_MULTI_HOIST_ROWS)
+#define BX_MULTI_ROW(R, m, r) const RowC& R = X.R[m]
+#else
+#define BX_MULTI_ROW(R, m, r) const RowC R = load_row(c, H, r)
+#endif
+
+template <int L, int MR>
+__device__ __forceinline__ void load_hoist_multi(const Cst& c, const BlobHdr& H, int lane,
+                                                 HoistM<MR>& X) {
+  X.hasB = lane < H.N;
+  X.hasJ = lane < H.J;
+  X.hasA = lane < H.K;
+  const int b = X.hasB ? lane : 0;
+  X.B = load_body(c, H, b);
+  X.jl = load_glist<MAXG>(c, H.o_jl_off, H.o_jl, b, X.hasB, 2 * H.J);
+  X.al = load_glist<MAXG>(c, H.o_al_off, H.o_al, b, X.hasB, 2 * H.K);
+  const bool hasT = lane < H.T;
+#pragma unroll
+  for (int k = 0; k < TASK_W; k++) X.te[k] = hasT ? c.i(H.o_task + lane * TASK_W + k) : 2 * H.R;
+#pragma unroll
+  for (int k = 0; k < BTASK_W; k++) X.bt[k] = X.hasB ? c.i(H.o_btask + b * BTASK_W + k) : H.T;
+  if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? lane : 0);
+  if (H.K > 0) X.A = load_act(c, H, X.hasA ? lane : 0);
+#if defined(BX_MULTI_HOIST_ROWS)
+#pragma unroll
+  for (int m = 0; m < MR; m++) {
+    const int r = lane + m * L;
+    X.R[m] = load_row(c, H, r < H.R ? r : 0);
+  }
+#endif
+}
+
+// phase 1: the lane's task partial, its slots summed in list order
+__device__ __forceinline__ void task_sum(const int* te, const float* ms, float* out) {
+  v3 a = mk(0.f, 0.f, 0.f);
+  q4 r{0.f, 0.f, 0.f, 0.f};
+  float n = 0.f;
+#pragma unroll
+  for (int k = 0; k < TASK_W; k++) {
+    v3 v;
+    q4 q;
+    float f;
+    ld_slot(ms + te[k] * MSLOT_STRIDE, v, q, f);
+    a = a + v;
+    r = r + q;
+    n += f;
+  }
+  st_slot(out, a, r, n);
+}
+
+// phase 2: sum over the body's groups of (group's partials) / (eps + count)
+__device__ __forceinline__ void body_combine(const int* bt, const float* ts, float eps, v3& a,
+                                             q4& r) {
+  a = mk(0.f, 0.f, 0.f);
+  r = q4{0.f, 0.f, 0.f, 0.f};
+  v3 ga = mk(0.f, 0.f, 0.f);
+  q4 gr{0.f, 0.f, 0.f, 0.f};
+  float gn = 0.f;
+  int g = bt[0] >> 24;
+#pragma unroll
+  for (int k = 0; k < BTASK_W; k++) {
+    v3 v;
+    q4 q;
+    float f;
+    ld_slot(ts + (bt[k] & 0xFFFFFF) * MSLOT_STRIDE, v, q, f);
+    const int gk = bt[k] >> 24;
+    if (gk != g) {
+      const float d = eps + gn;
+      a = a + ga / d;
+      r = q4{r.w + gr.w / d, r.x + gr.x / d, r.y + gr.y / d, r.z + gr.z / d};
+      ga = mk(0.f, 0.f, 0.f);
+      gr = q4{0.f, 0.f, 0.f, 0.f};
+      gn = 0.f;
+      g = gk;
+    }
+    ga = ga + v;
+    gr = gr + q;
+    gn += f;
+  }
+  const float d = eps + gn;
+  a = a + ga / d;
+  r = q4{r.w + gr.w / d, r.x + gr.x / d, r.y + gr.y / d, r.z + gr.z / d};
+}
+
+// info: the env's Info contact rows (contact_pos 3, normal 3, penetration),
+// already offset to this env; null pointers are skipped
+struct RowInfoOut {
+  float* pos;
+  float* normal;
+  float* pen;
+};
+
+template <int L, int F, int MR>
+__device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
+                               const float* act, int aw, const HoistM<MR>& X, RowInfoOut io) {
+  const float h = H.h;
+  const v3 g = mk(H.gx, H.gy, H.gz);
+  float* myqp = E.qp + lane * QP_STRIDE;
+  QP q;
+  if (X.hasB) q = ldqp(myqp);
+  v3 icv = mk(0.f, 0.f, 0.f), ica = mk(0.f, 0.f, 0.f), iaa = mk(0.f, 0.f, 0.f);
+  float al[3] = {0.f, 0.f, 0.f};
+  if (X.hasA && valid) {
+#pragma unroll
+    for (int l = 0; l < 3; l++) {
+      int ai = X.A.idx[l];
+      al[l] = act[take_idx(ai, aw)] * (ai >= 0 ? 1.f : 0.f);
+    }
+  }
+  v3 fv = mk(0.f, 0.f, 0.f), fa = mk(0.f, 0.f, 0.f);
+  if constexpr ((F & F_FORCE) != 0) {
+    if (X.hasB) body_forces(c, H, lane, act, aw, valid, fv, fa);
+  }
+  // NearNeighbors.update once per step (system.py:320-321): ranks in E.ract,
+  // culled rows' slots zeroed (their lanes skip them below)
+  if (H.n_nn) nn_select<L>(c, H, E, lane);
+  // the row's contact between the position and velocity passes
+  v3 cpos[MR], cn[MR];
+  float pen[MR], dl[MR];
+#pragma unroll
+  for (int m = 0; m < MR; m++) {
+    cpos[m] = mk(0.f, 0.f, 0.f);
+    cn[m] = mk(0.f, 0.f, 0.f);
+    pen[m] = 0.f;
+    dl[m] = 0.f;
+  }
+  for (int it = 0; it < H.substeps / 2; it++) {
+    v3 ppos = q.pos;
+    q4 prot = q.rot;
+    v3 dpa_last = mk(0.f, 0.f, 0.f);
+#pragma unroll 1
+    for (int sub = 0; sub < 2; sub++) {
+      ppos = q.pos;
+      prot = q.rot;
+      if (sub == 1 && X.hasB) st_slot(E.prev + lane * PREV_STRIDE, ppos, prot, 0.f);
+      // actuators (actuators.py:52-112) + joint damping (joints.py:103-128)
+      if (X.hasA) {
+        if (H.act_same) {
+          act_torque<F>(X.J, X.A, E, al, lane);
+        } else {
+          JointC Jc = load_joint(c, H, X.A.joint);
+          act_torque<F>(Jc, X.A, E, al, lane);
+        }
+      }
+      if (X.hasJ) {
+        const JointC& Jc = X.J;
+        v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
+        st_v3a(E.jslot + lane * SLOT_STRIDE, mul(Jc.Ip, tq));
+        st_v3a(E.jslot + (E.nJ + lane) * SLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
+      }
+      esync<L>();
+      // Euler.update(acc) + Euler.kinetic (integrators.py:50-93)
+      if (X.hasB) {
+        v3 dpa = gsum3(X.al, E.aslot, ASLOT_STRIDE);
+        v3 dpj = gsum3(X.jl, E.jslot, SLOT_STRIDE);
+        v3 vel = H.vexp * q.vel;
+        vel = vel + (fv + g) * h;
+        q.vel = mul(vel, X.B.pm);
+        v3 an = H.aexp * q.ang;
+        an = an + ((dpa + fa) + dpj) * h;
+        q.ang = mul(an, X.B.rm);
+        q.pos = q.pos + mul(q.vel * h, X.B.pm);
+        v3 am = mul(q.ang, X.B.rm);
+        q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
+        q4 r = q.rot + quat_mul(hq, q.rot);
+        q.rot = qnormalize(r);
+        stqp(myqp, q);
+        dpa_last = dpa;
+      }
+      esync<L>();
+      // Joint.apply (joints.py:79-100)
+      if (X.hasJ) {
+        const JointC& Jc = X.J;
+        QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
+        v3 dpp, dcp;
+        q4 dpr, dcr;
+        joint_apply<F>(Jc, p, cq, dpp, dpr, dcp, dcr);
+        st_slot(E.jslot + lane * SLOT_STRIDE, dpp, dpr, 0.f);
+        st_slot(E.jslot + (E.nJ + lane) * SLOT_STRIDE, dcp, dcr, 0.f);
+      }
+      esync<L>();
+      // Euler.update(pos) (+ velocity_projection on the first substep)
+      if (X.hasB) {
+        v3 dp = mk(0.f, 0.f, 0.f);
+        q4 dr{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < MAXG; k++) {
+          v3 v;
+          q4 r;
+          float f;
+          ld_slot(E.jslot + X.jl.e[k] * SLOT_STRIDE, v, r, f);
+          dp = dp + v;
+          dr = dr + r;
+        }
+        q.pos = q.pos + mul(dp, X.B.pm);
+        q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
+                   q.rot.z + dr.z * X.B.qm.z};
+        if (sub == 0) vproj(q, ppos, prot, X.B, h);
+        stqp(myqp, q);
+      }
+      esync<L>();
+    }
+    // ---- collisions (system.py:288-313)
+    // Collider.position_apply (colliders.py:198-240): the lane's rows
+#pragma unroll
+    for (int m = 0; m < MR; m++) {
+      const int r = lane + m * L;
+      if (r >= H.R || !row_active(H, E, r)) continue;
+      BX_MULTI_ROW(R, m, r);
+      QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+      v3 cvel;
+      contact_gen<F>(R, a, b, cpos[m], cvel, cn[m], pen[m]);
+      v3 pap, pbp;
+      q4 par, pbr;
+      float unused;
+      ld_slot(E.prev + R.a * PREV_STRIDE, pap, par, unused);
+      ld_slot(E.prev + R.b * PREV_STRIDE, pbp, pbr, unused);
+      v3 oap, obp;
+      q4 oar, obr;
+      dl[m] = position_contact<F>(R, a, b, pap, par, pbp, pbr, cpos[m], cn[m], pen[m], oap, oar, obp,
+                                  obr);
+      st_slot(E.cslot + r * MSLOT_STRIDE, oap, oar,
+              (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f);
+      if (!is_oneway<F>(R.oneway))
+        st_slot(E.cslot + (H.R + r) * MSLOT_STRIDE, obp, obr,
+                (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f);
+    }
+    esync<L>();
+    if (lane < H.T) task_sum(X.te, E.cslot, E.tslot + lane * MSLOT_STRIDE);
+    esync<L>();
+    if (X.hasB) {
+      v3 dp;
+      q4 dr;
+      body_combine(X.bt, E.tslot, 1e-6f, dp, dr);
+      q.pos = q.pos + mul(dp, X.B.pm);
+      q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
+                 q.rot.z + dr.z * X.B.qm.z};
+      st_rb(E.rb + lane * RB_STRIDE, q.pos, q.vel, q.ang);
+      vproj(q, ppos, prot, X.B, h);
+      stqp(myqp, q);
+    }
+    esync<L>();
+    // Collider.velocity_apply (colliders.py:155-196)
+#pragma unroll
+    for (int m = 0; m < MR; m++) {
+      const int r = lane + m * L;
+      if (r >= H.R || !row_active(H, E, r)) continue;
+      BX_MULTI_ROW(R, m, r);
+      QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+      v3 rap, rav, raa, rbp, rbv, rba;
+      ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
+      ld_rb(E.rb + R.b * RB_STRIDE, rbp, rbv, rba);
+      v3 oav, oaa, obv, oba;
+      velocity_contact<F>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos[m], cn[m], pen[m], dl[m],
+                          oav, oaa, obv, oba);
+      st_slot(E.cslot + r * MSLOT_STRIDE, oav, q4{oaa.x, oaa.y, oaa.z, 0.f},
+              (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f);
+      if (!is_oneway<F>(R.oneway))
+        st_slot(E.cslot + (H.R + r) * MSLOT_STRIDE, obv, q4{oba.x, oba.y, oba.z, 0.f},
+                (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f);
+    }
+    esync<L>();
+    if (lane < H.T) task_sum(X.te, E.cslot, E.tslot + lane * MSLOT_STRIDE);
+    esync<L>();
+    if (X.hasB) {
+      v3 dv;
+      q4 da;
+      body_combine(X.bt, E.tslot, 1e-6f, dv, da);
+      v3 dav = mk(da.w, da.x, da.y);
+      q.vel = mul(q.vel + dv, X.B.pm);
+      q.ang = mul(q.ang + dav, X.B.rm);
+      stqp(myqp, q);
+      icv = icv + dv;
+      ica = ica + dav;
+      iaa = iaa + dpa_last;
+    }
+    esync<L>();
+  }
+  // Info contact rows of the last position pass (system.py:36-43)
+  if (valid) {
+#pragma unroll
+    for (int m = 0; m < MR; m++) {
+      const int r = lane + m * L;
+      if (r >= H.R) continue;
+      const int x = row_info(c, H, E, r);
+      if (x < 0) continue;
+      if (io.pos) st3(io.pos + x * 3, cpos[m]);
+      if (io.normal) st3(io.normal + x * 3, cn[m]);
+      if (io.pen) io.pen[x] = pen[m];
+    }
+  }
+  if (X.hasB) {
+    float* acc = E.acc + lane * ACC_STRIDE;
+    st3(acc + ACC_ICV, icv);
+    st3(acc + ACC_ICA, ica);
+    st3(acc + ACC_IAA, iaa);
+  }
+  esync<L>();
+}
+
 // System._pbd_info contact part (system.py:327-340 -> Collider.apply): info
 // contact (vel, ang) per body into acc[ACC_ICV], acc[ACC_ICA]
 template <int L>
@@ -2244,7 +2595,7 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
 // kernel variants: MODE_GLOBAL (constants read from the HBM blob inside the
 // loops), MODE_SINGLE (constants hoisted to registers), MODE_LDS (the blob's
 // constant part copied to LDS once per workgroup, read there inside the loops)
-enum { MODE_GLOBAL = 0, MODE_SINGLE = 1, MODE_LDS = 2 };
+enum { MODE_GLOBAL = 0, MODE_SINGLE = 1, MODE_LDS = 2, MODE_MULTI = 3 };
 
 // step kernels: optional register-budget hint (A/B knob, BX_WAVES1)
 #if defined(BX_WAVES1)
@@ -2280,7 +2631,8 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
   const int le = threadIdx.x / L;
   const int64_t e = (int64_t)blockIdx.x * (blockDim.x / L) + le;
   const bool valid = e < A.n_envs;
-  Env E = carve(ebase + le * H.env_words, H);
+  constexpr bool MU = MODE == MODE_MULTI;
+  Env E = carve(ebase + le * H.env_words, H, MU);
   zero_slots(E, H, lane);
   for (int b = lane; b < H.N; b += L) {
     if (valid) {
@@ -2291,7 +2643,17 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
     }
   }
   esync<L>();
-  if constexpr (S) {
+  if constexpr (MU) {
+    // M = contact rows per lane
+    HoistM<M> X;
+    load_hoist_multi<L, M>(c, H, lane, X);
+    const int64_t ro = valid ? e * H.info_rows : 0;
+    RowInfoOut io{A.info.contact_pos ? A.info.contact_pos + ro * 3 : nullptr,
+                  A.info.contact_normal ? A.info.contact_normal + ro * 3 : nullptr,
+                  A.info.contact_penetration ? A.info.contact_penetration + ro : nullptr};
+    pbd_step_multi<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr,
+                            (int)A.act_width, X, io);
+  } else if constexpr (S) {
     Hoist<M> X;
     load_hoist<M>(c, H, lane, X);
     v3 icv, ica, iaa;
@@ -2335,6 +2697,7 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
       for (int k = 0; k < 3; k++) p[k] = H.spring ? ij[3 + k] : 0.f;
     }
   }
+  if constexpr (MU) return;  // MULTI wrote its Info rows from registers
   for (int r = lane; r < H.R; r += L) {
     const int x = row_info(c, H, E, r);
     if (x < 0) continue;
@@ -2778,6 +3141,19 @@ hipError_t launch_env_step_generic(int L, int mode, int feat, int tpb, int64_t n
   const int epb = tpb / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
   BX_DISPATCH_GENERIC(env_step_kernel, EnvArgs)
+  return hipGetLastError();
+}
+hipError_t launch_system_step_multi(int feat, int mr, int64_t n_envs, size_t lds, hipStream_t s,
+                                    const StepArgs& a) {
+  if ((feat & (F_SPH | F_ANGLE | F_FORCE | F_X)) != 0) return hipErrorInvalidValue;
+  dim3 grid((unsigned)n_envs);
+  switch (mr) {
+    case 1: launch_one<StepArgs>(system_step_kernel<256, MODE_MULTI, F_LEAN, 1>, grid, 256, lds, s, a); break;
+    case 2: launch_one<StepArgs>(system_step_kernel<256, MODE_MULTI, F_LEAN, 2>, grid, 256, lds, s, a); break;
+    case 3: launch_one<StepArgs>(system_step_kernel<256, MODE_MULTI, F_LEAN, 3>, grid, 256, lds, s, a); break;
+    case 4: launch_one<StepArgs>(system_step_kernel<256, MODE_MULTI, F_LEAN, 4>, grid, 256, lds, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, const InfoArgs& a) {

@@ -63,6 +63,9 @@ hipError_t launch_system_step_single(int L, int feat, int gw, int tpb, int64_t n
                                      hipStream_t s, const StepArgs& a);
 hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
                                   hipStream_t s, const EnvArgs& a);
+// MULTI-mode step kernel (large pbd scenes, 256 threads per env; mr = rows per lane)
+hipError_t launch_system_step_multi(int feat, int mr, int64_t n_envs, size_t lds, hipStream_t s,
+                                    const StepArgs& a);
 // item-loop step kernels (generic translation unit)
 hipError_t launch_system_step_generic(int L, int mode, int feat, int tpb, int64_t n_envs, size_t lds,
                                       hipStream_t s, const StepArgs& a);

@@ -83,7 +83,15 @@ struct BlobHdr {
   int32_t o_hm;                      // height map grids
   int32_t o_hull;                    // box hulls: 8 corners, 6x4 quad points, 6 normals
   int32_t o_dangle;                  // reset: System.default_angle (num_joint_dof)
+  // MULTI mode (large pbd scenes): gather tasks and the mode's LDS tail
+  int32_t multi;                     // the system fits the MULTI-mode kernel
+  int32_t T, o_task, o_btask;        // tasks: TASK_W slot indices each; per body BTASK_W task refs
+  int32_t l_mslot, l_tslot;          // LDS: 8-word contact slots (2R+1), task partials (T+1)
+  int32_t env_words_m;               // per-env LDS words in MULTI mode
 };
+// MULTI-mode gather tasks: a task sums <= TASK_W contact slots of one body and
+// collider group; a body adds <= BTASK_W task partials (ref = task | group << 24)
+enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 8, MULTI_MR = 4 };
 enum { HULL_STRIDE = 114, HULL_V = 0, HULL_F = 24, HULL_N = 96 };
 
 }  // namespace bx

@@ -254,7 +254,8 @@ int bx_system_create(const bx_desc* desc, const bx_reset_desc* reset,
                      int device, bx_system** out);
 int bx_system_destroy(bx_system* sys);
 
-/* Lanes of a wavefront that own one env in this system's kernels (16/32/64). */
+/* Threads that own one env in this system's step kernels: 16/32/64 lanes of
+ * one wavefront, or a whole 128/256-thread workgroup for large scenes. */
 int bx_system_lanes(bx_system* sys);
 
 /* Select the register-hoisted kernel variant (default when the system fits:
@@ -262,9 +263,11 @@ int bx_system_lanes(bx_system* sys);
  * item-loop variant (on = 0). For testing both paths on one system. */
 int bx_system_set_single(bx_system* sys, int on);
 
-/* Kernel variant: lanes per env (16/32/64, >= the system's minimum) and
- * constant placement (0: read from HBM in the loops, 1: hoisted to registers,
- * needs <= 1 item per lane, 2: staged in LDS once per workgroup). */
+/* Kernel variant: threads per env (16/32/64/128/256) and constant placement
+ * (0: read from HBM in the loops, 1: hoisted to registers, needs <= 1 item per
+ * lane, 2: staged in LDS once per workgroup, 3: MULTI, the large-scene pbd
+ * kernel at 256 threads: items and <= 4 contact rows per lane hoisted to
+ * registers, per-body contact sums through gather tasks). */
 int bx_system_set_variant(bx_system* sys, int lanes, int mode);
 
 /* Threads per workgroup of the step kernels: a multiple of the lanes per env,

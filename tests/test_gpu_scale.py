@@ -139,17 +139,23 @@ def test_ant_32768_shards_reproduce_one_batch(dev, oracle_lib):
           _env_err([o[0][keep][..., sl] for o in outs], ref[keep][..., sl]), f)
 
 
+@pytest.mark.parametrize('variant', ['multi', 'itemloop'])
 @pytest.mark.parametrize('cutoff', [0, 36])
-def test_mountain4_full_batch(dev, oracle_lib, cutoff):
+def test_mountain4_full_batch(dev, oracle_lib, cutoff, variant):
   """BASELINE configs[4]: Ant Mountain(4) System.step at 2,048 envs
   (37 bodies, 630 capsule-capsule + 72 capsule-plane rows; NearNeighbors
   cutoff 36 as published): determinism, batch independence, unit
-  quaternions and parity with the fp64 oracle on sampled envs."""
+  quaternions and parity with the fp64 oracle on sampled envs. Both large-
+  scene kernels: MULTI (the default: 256 threads per env, gather tasks) and
+  the item loops at 256 threads per env."""
   import brax_amd
+  from brax_amd import _native
   from tests.test_gpu_parity import Envelope, _env_err, _gate
   cfg = config_for('mountain4')
   cfg.collider_cutoff = cutoff
   sys_ = brax_amd.System(cfg, device=dev)
+  assert sys_.lanes == 256
+  _native.check(_native.lib().bx_system_set_variant(sys_._h, 256, 3 if variant == 'multi' else 0))
   B = 2048
   q0 = sys_.default_qp()
   qp = brax_amd.QP(*(t.unsqueeze(0).expand((B,) + t.shape).contiguous()
