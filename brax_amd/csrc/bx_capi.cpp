@@ -69,6 +69,8 @@ struct Builder {
 };
 
 int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
+  // A/B knob: BX_NO_JOINT_HALVES=1 keeps one lane per joint
+  const bool jh_off = getenv("BX_NO_JOINT_HALVES") && atoi(getenv("BX_NO_JOINT_HALVES"));
   const int N = d->n_bodies, J = d->n_joints, K = d->n_actuators, R = d->n_rows, G = d->n_groups;
   if (N <= 0) return fail("descriptor has no bodies");
   if (d->dynamics_mode != BX_DYN_PBD && d->dynamics_mode != BX_DYN_LEGACY_SPRING)
@@ -477,6 +479,9 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     if (d->n_forces > 0) f |= 16;
     if (max_groups <= 1) f |= 32;  // F_G1: one collider group per body
     if (xcol) f |= 64;             // F_X: extended contact functions
+    // F_JH (joint halves, SINGLE mode at 16 lanes): <= 8 revolute joints, each
+    // driven by the actuator of the same index
+    if (H.single && L == 16 && J <= 8 && K <= 8 && H.act_same && !(f & 1) && !jh_off) f |= 128;
     S->feat = f;
   }
   // the MULTI kernel is instantiated for the lean feature set (revolute,

@@ -110,6 +110,10 @@ __device__ __forceinline__ void stqp(float* s, const QP& q) {
   st4a(s + 8, f32x4{q.vel.y, q.vel.z, q.ang.x, q.ang.y});
   s[12] = q.ang.z;
 }
+__device__ __forceinline__ q4 ld_rot(const float* s) {  // QP record's rot
+  f32x4 a = ld4a(s), b = ld4a(s + 4);
+  return q4{a.w, b.x, b.y, b.z};
+}
 __device__ __forceinline__ v3 ld_ang(const float* s) {  // QP record's ang
   f32x4 c = ld4a(s + 8);
   return mk(c.z, c.w, s[12]);
@@ -1100,6 +1104,106 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
   st_v3a(E.aslot + (E.nK + a) * ASLOT_STRIDE, -sgp * mul(Jc.Ic, tq));
 }
 
+
+// ---------------------------------------------------------------------------
+// joint halves (F_JH, SINGLE mode at 16 lanes with <= 8 revolute joints, Ant):
+// lane j works the parent side of joint j and lane j + 8 its child side. The
+// two sides of a revolute constraint are the same arithmetic on each body's
+// own frame (world anchor, lever arm, effective mass, impulse, rotation
+// update), so one instruction stream serves both halves and exchanges the few
+// cross terms with the partner lane by a DPP row rotation; the shared scalar
+// work (constraint norm, limit angle, angle-update direction) is computed
+// redundantly. Each lane then writes its side's slot. Halves the per-lane
+// instruction count of the joint and actuator phases (Ant leaves lanes 8-15
+// idle there otherwise).
+// ---------------------------------------------------------------------------
+enum { F_JH = 128 };
+
+// the partner half's value: lane ^ 8 within the env's 16-lane row
+__device__ __forceinline__ float xh(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
+}
+__device__ __forceinline__ v3 xh3(v3 v) { return mk(xh(v.x), xh(v.y), xh(v.z)); }
+__device__ __forceinline__ v3 sel3(bool s, v3 a, v3 b) {
+  return mk(s ? a.x : b.x, s ? a.y : b.y, s ? a.z : b.z);
+}
+
+// Joint.apply_angle_update (joints.py:130-152), this side's rotation part
+__device__ __forceinline__ q4 angle_update_half(const JointC& J, bool child, const q4& ro, v3 dq) {
+  float th = safe_norm(dq);
+  v3 n = dq / (th + 1e-6f);
+  float w1 = dot(n, mul(J.Ip, n));
+  float w2 = dot(n, mul(J.Ic, n));
+  float dl = -th / (w1 + w2 + 1e-6f);
+  v3 p = -dl * n;
+  return J.sa * ((child ? -0.5f : 0.5f) * vec_quat_mul(mul(sel3(child, J.Ic, J.Ip), p), ro));
+}
+
+// Revolute.apply_reduced (joints.py:79-100, 154-195, 270-309), one side: o is
+// this side's body (parent on lanes 0-7, child on 8-15); returns its dp, dq
+__device__ __forceinline__ void joint_apply_half(const JointC& J, bool child, const QP& o, v3& dpo,
+                                                 q4& dro) {
+  const float sg = child ? -1.f : 1.f;
+  // value selects (a conditional lvalue into the constants would force them to scratch)
+  const v3 I = sel3(child, J.Ic, J.Ip);
+  const float mc = J.mc, mp = J.mp;
+  const float m = child ? mc : mp;
+  // positional constraint
+  v3 wo = o.pos + rotate(sel3(child, J.off_c, J.off_p), o.rot);
+  v3 ro = wo - o.pos;
+  v3 wt = xh3(wo);
+  v3 dx = child ? wt - wo : wo - wt;
+  float cc = safe_norm(dx);
+  v3 n = dx / (cc + 1e-6f);
+  v3 cr = cross(ro, n);
+  float wm = 1.f / m + dot(cr, mul(I, cr));
+  float wp = xh(wm);
+  float w1 = child ? wp : wm, w2 = child ? wm : wp;
+  float dl = -cc / (w1 + w2 + 1e-6f);
+  v3 pv = dl * n;
+  dpo = J.sp * ((sg * pv) / m);
+  dro = J.sp * ((sg * 0.5f) * vec_quat_mul(mul(I, cross(ro, pv)), o.rot));
+  // the two angular constraints (axis alignment, limited hinge angle)
+  v3 u0 = rotate(sel3(child, J.axc[0], J.axp[0]), o.rot);
+  v3 u2 = rotate(sel3(child, J.axc[2], J.axp[2]), o.rot);
+  v3 t0 = xh3(u0), t2 = xh3(u2);
+  v3 axis = sel3(child, t0, u0), axis_c = sel3(child, u0, t0);
+  v3 ref_p = sel3(child, t2, u2), ref_c = sel3(child, u2, t2);
+  float psi = signed_angle(axis, ref_p, ref_c);
+  v3 dq1 = cross(axis, axis_c);
+  float ph = clampf(psi, J.lim[0], J.lim[1]);
+  q4 fix = quat_rot_axis(axis, ph);
+  v3 n1 = rotate(ref_p, fix);
+  v3 dq2 = cross(n1, ref_c);
+  q4 a1 = angle_update_half(J, child, o.rot, dq1);
+  q4 a2 = angle_update_half(J, child, o.rot, dq2);
+  dro = dro + (a1 + a2);
+}
+
+// Actuator.apply_reduced (actuators.py:52-112) for a revolute joint, one side
+template <int F>
+__device__ __forceinline__ void act_torque_half(const JointC& Jc, const ActC& A, const Env& E,
+                                                const float* al, int a, bool child, const q4& ro) {
+  v3 u0 = rotate(sel3(child, Jc.axc[0], Jc.axp[0]), ro);
+  v3 u2 = rotate(sel3(child, Jc.axc[2], Jc.axp[2]), ro);
+  v3 t0 = xh3(u0), t2 = xh3(u2);
+  v3 axis = sel3(child, t0, u0);
+  float ang = signed_angle(axis, sel3(child, t2, u2), sel3(child, u2, t2));
+  float t;
+  if (is_torque<F>(A.type)) {
+    t = al[0] * A.strength * -1.f;
+    if (ang < Jc.lim[0]) t = 0.f;
+    if (ang > Jc.lim[1]) t = 0.f;
+  } else {
+    float tgt = clampf(al[0] * 3.14159265358979323846f / 180.f, Jc.lim[0], Jc.lim[1]);
+    t = (tgt - ang) * A.strength;
+  }
+  v3 tq = mk(0.f, 0.f, 0.f) + axis * t;
+  float sgp = is_torque<F>(A.type) ? 1.f : -1.f;
+  if (child) st_v3a(E.aslot + (E.nK + a) * ASLOT_STRIDE, -sgp * mul(Jc.Ic, tq));
+  else st_v3a(E.aslot + a * ASLOT_STRIDE, sgp * mul(Jc.Ip, tq));
+}
+
 // ---------------------------------------------------------------------------
 // per-env LDS carving
 // ---------------------------------------------------------------------------
@@ -1709,10 +1813,13 @@ struct Hoist {
 };
 
 template <int M>
-__device__ __forceinline__ void load_hoist(const Cst& c, const BlobHdr& H, int lane, Hoist<M>& X) {
+__device__ __forceinline__ void load_hoist(const Cst& c, const BlobHdr& H, int lane, Hoist<M>& X,
+                                           bool jh = false) {
+  // jh (joint halves): lanes j and j + 8 both hold joint j and actuator j
+  const int jx = jh ? (lane & 7) : lane;
   X.hasB = lane < H.N;
-  X.hasJ = lane < H.J;
-  X.hasA = lane < H.K;
+  X.hasJ = jx < H.J;
+  X.hasA = jx < H.K;
   X.hasR = lane < H.R;
   int b = X.hasB ? lane : 0;
   X.B = load_body(c, H, b);
@@ -1727,8 +1834,8 @@ __device__ __forceinline__ void load_hoist(const Cst& c, const BlobHdr& H, int l
     if (n0 > 0) cz |= c.i(H.o_cl + s0) & 0x7F000000;
   }
   X.cl = load_glist<M>(c, H.o_cl_off, H.o_cl, b, X.hasB, cz);
-  if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? lane : 0);
-  if (H.K > 0) X.A = load_act(c, H, X.hasA ? lane : 0);
+  if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? jx : 0);
+  if (H.K > 0) X.A = load_act(c, H, X.hasA ? jx : 0);
   if (H.R > 0) X.R = load_row(c, H, X.hasR ? lane : 0);
 }
 
@@ -1851,6 +1958,9 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
 #endif
   const float h = H.h;
   const v3 g = mk(H.gx, H.gy, H.gz);
+  constexpr bool JH = (F & F_JH) != 0;
+  const int jx = lane & 7;         // JH: this lane's joint / actuator
+  const bool child = lane >= 8;    // JH: this lane's side
   float* myqp = E.qp + lane * QP_STRIDE;
   QP q;
   if (X.hasB) q = ldqp(myqp);
@@ -1885,6 +1995,17 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       prot = q.rot;
       if (sub == 1 && X.hasB) st_slot(E.prev + lane * PREV_STRIDE, ppos, prot, 0.f);
       // actuators + damping (actuator a drives joint a when H.act_same)
+      if constexpr (JH) {
+        // one side of joint / actuator jx per lane (act_same, checked on the host)
+        const int jb = child ? X.J.bc : X.J.bp;
+        if (X.hasA) act_torque_half<F>(X.J, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE));
+        if (X.hasJ) {
+          const JointC& Jc = X.J;
+          v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
+          if (child) st_v3a(E.jslot + (E.nJ + jx) * SLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
+          else st_v3a(E.jslot + jx * SLOT_STRIDE, mul(Jc.Ip, tq));
+        }
+      } else {
       if (X.hasA) {
         const ActC& A = X.A;
         if (H.act_same) {
@@ -1899,6 +2020,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
         st_v3a(E.jslot + lane * SLOT_STRIDE, mul(Jc.Ip, tq));
         st_v3a(E.jslot + (E.nJ + lane) * SLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
+      }
       }
       sync();
       BX_STAMP(0);
@@ -1921,7 +2043,17 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       }
       sync();
       BX_STAMP(1);
-      if (X.hasJ) {
+      if constexpr (JH) {
+        if (X.hasJ) {
+          const JointC& Jc = X.J;
+          const int jb = child ? Jc.bc : Jc.bp;
+          QP o = ldqp(E.qp + jb * QP_STRIDE);
+          v3 dpo;
+          q4 dro;
+          joint_apply_half(Jc, child, o, dpo, dro);
+          st_slot(E.jslot + (child ? E.nJ + jx : jx) * SLOT_STRIDE, dpo, dro, 0.f);
+        }
+      } else if (X.hasJ) {
         const JointC& Jc = X.J;
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
@@ -2655,7 +2787,7 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
                             (int)A.act_width, X, io);
   } else if constexpr (S) {
     Hoist<M> X;
-    load_hoist<M>(c, H, lane, X);
+    load_hoist<M>(c, H, lane, X, (F & F_JH) != 0);
     v3 icv, ica, iaa;
     pbd_step_single<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr,
                              (int)A.act_width, X, icv, ica,
@@ -2733,7 +2865,7 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
   // every independent load first, so their latencies overlap: the hoisted
   // constants, the per-env scalars, then the state
   Hoist<M> X;
-  if constexpr (S) load_hoist<M>(c, H, lane, X);
+  if constexpr (S) load_hoist<M>(c, H, lane, X, (F & F_JH) != 0);
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
   float done_in = valid ? A.in.done[e] : 0.f;
   float steps_in = valid && A.in.steps ? A.in.steps[e] : 0.f;
@@ -3063,6 +3195,10 @@ static void launch_one(void (*k)(Args), dim3 grid, int tpb, size_t lds, hipStrea
     case F_SPH | F_G1: launch_one<ARGS>(KERNEL<16, 1, F_SPH | F_G1, M>, grid, tpb, lds, s, a); break; \
     case F_CC | F_TW: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW, M>, grid, tpb, lds, s, a); break; \
     case F_CC | F_TW | F_G1: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW, M>, grid, tpb, lds, s, a); break; \
+    case F_G1 | F_JH: launch_one<ARGS>(KERNEL<16, 1, F_G1 | F_JH, M>, grid, tpb, lds, s, a); break; \
+    case F_JH: launch_one<ARGS>(KERNEL<16, 1, F_JH, M>, grid, tpb, lds, s, a); break; \
+    case F_CC | F_TW | F_JH: \
+    case F_CC | F_TW | F_G1 | F_JH: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW | F_JH, M>, grid, tpb, lds, s, a); break; \
     default: launch_one<ARGS>(KERNEL<16, 1, F_ALL, M>, grid, tpb, lds, s, a); break; \
   }
 #define BX_DISPATCH_SINGLE(KERNEL, ARGS)                                            \
