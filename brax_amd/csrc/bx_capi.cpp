@@ -545,6 +545,12 @@ int env_sizes(const bx_system* S, const bx_env_params* P, int* obs, int* met) {
       *met = P->kind == BX_ENV_HUMANOID ? 9 : 2;
       return 0;
     }
+    case BX_ENV_HOPPER:
+    case BX_ENV_WALKER2D:
+      // (x,) z, ang_y, joint angles, vel x, vel z, ang y, joint vels (hopper.py:231-246)
+      *obs = (xy ? 2 : 1) + 1 + D + 3 + D;
+      *met = 5;
+      return 0;
     case BX_ENV_HALFCHEETAH:
       *obs = 3 + D + 3 + D + (xy ? 1 : 0);
       *met = 4;

@@ -2583,6 +2583,12 @@ __device__ void joint_angles(const Cst& c, const BlobHdr& H, const Env& E, int l
 
 __device__ __forceinline__ float clip1(float x) { return clampf(x, -1.f, 1.f); }
 
+// math.quat_to_euler(q)[1] (math.py:80-91): asin(clip(2 q1 q3 + 2 q0 q2))
+// of a QP record's rot (w, x, y, z)
+__device__ __forceinline__ float euler_y(const float* q) {
+  return asinf(clampf(2.f * q[1] * q[3] + 2.f * q[0] * q[2], -1.f, 1.f));
+}
+
 // Humanoid center of mass over bodies [:-1] (humanoid.py:336-338) -> red[32..35]
 __device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3& com, float& msum) {
   v3 acc = mk(0.f, 0.f, 0.f);
@@ -2603,8 +2609,9 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
   const float* q0 = E.qp;
   // exclude_current_positions_from_observation=False: the torso's x (and y)
   // precede z (ant.py:262-265, humanoid.py:289-292, half_cheetah.py:206-209)
+  const bool loco2d = kind == BX_ENV_HOPPER || kind == BX_ENV_WALKER2D;
   if (flags & BX_OBS_XY) {
-    if (kind == BX_ENV_HALFCHEETAH) {
+    if (kind == BX_ENV_HALFCHEETAH || loco2d) {
       if (i == 0) return q0[0];
       i -= 1;
     } else {
@@ -2628,6 +2635,19 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
     if (i < 3 * N) return clip1(E.acc[(i / 3) * ACC_STRIDE + ACC_ICV + i % 3]);
     i -= 3 * N;
     return clip1(E.acc[(i / 3) * ACC_STRIDE + ACC_ICA + i % 3]);
+  }
+  if (loco2d) {
+    // hopper.py:231-246: [z, ang_y, joint angles, vel x, vel z, ang y, joint vels]
+    if (i == 0) return q0[2];
+    if (i == 1) return euler_y(q0 + 3);
+    i -= 2;
+    if (i < D) return E.ang[i];
+    i -= D;
+    if (i == 0) return q0[7];
+    if (i == 1) return q0[9];
+    if (i == 2) return q0[11];
+    i -= 3;
+    return E.ang[D + i];
   }
   if (kind == BX_ENV_HALFCHEETAH) {
     if (i == 0) return q0[2];
@@ -2956,6 +2976,23 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
           m[0] = norm(com1); m[1] = fwd; m[2] = hr; m[3] = fwd; m[4] = -ctrl;
           m[5] = com1.x; m[6] = v.x; m[7] = com1.y; m[8] = v.y;
         }
+      } else if (kind == BX_ENV_HOPPER || kind == BX_ENV_WALKER2D) {
+        // hopper.py:204-229 / walker2d.py: healthy z and torso pitch ranges
+        float xv = (p1.x - pos0.x) / dt;
+        float fwd = P.coef[0] * xv;
+        float ay = euler_y(E.qp + 3);
+        float z = p1.z;
+        float healthy = z < P.coef[3] ? 0.f : 1.f;
+        healthy = z > P.coef[4] ? 0.f : healthy;
+        healthy = ay > P.coef[6] ? 0.f : healthy;
+        healthy = ay < P.coef[5] ? 0.f : healthy;
+        bool term = P.coef[7] != 0.f;
+        float hr = term ? P.coef[2] : P.coef[2] * healthy;
+        float ctrl = P.coef[1] * sq;
+        reward = fwd + hr - ctrl;
+        done = term ? 1.f - healthy : 0.f;
+        // sorted: reward_ctrl, reward_forward, reward_healthy, x_position, x_velocity
+        if (m) { m[0] = -ctrl; m[1] = fwd; m[2] = hr; m[3] = p1.x; m[4] = xv; }
       } else if (kind == BX_ENV_HUMANOID_STANDUP) {
         // humanoid_standup.py:232-247: uph = z / dt, reward = uph + 1 - 0.01 sum(a^2);
         // done is left as it came in

@@ -123,69 +123,6 @@ def _replace_metrics(state, **kw):
   return m
 
 
-class _Locomotion2D(TorchEnv):
-  """Hopper / Walker2d (`hopper.py:120-250`, `walker2d.py:130-253`)."""
-
-  metric_keys = ('reward_forward', 'reward_ctrl', 'reward_healthy', 'x_position', 'x_velocity')
-
-  def __init__(self, forward_reward_weight=1.0, ctrl_cost_weight=1e-3, healthy_reward=1.0,
-               terminate_when_unhealthy=True, healthy_z_range=(0.7, float('inf')),
-               healthy_angle_range=(-0.2, 0.2), reset_noise_scale=5e-3,
-               exclude_current_positions_from_observation=True, **kwargs):
-    super().__init__(**kwargs)
-    self._fw, self._cw, self._hr = forward_reward_weight, ctrl_cost_weight, healthy_reward
-    self._term = terminate_when_unhealthy
-    self._z, self._ang = healthy_z_range, healthy_angle_range
-    self.qpos_noise = self.qvel_noise = (-reset_noise_scale, reset_noise_scale)
-    self._exclude = exclude_current_positions_from_observation
-    D = self.sys.joints[0]._hi - self.sys.joints[0]._lo  # pylint: disable=protected-access
-    self.obs_size = (1 if self._exclude else 2) + 1 + D + 2 + 1 + D
-
-  def _get_obs(self, qp, info):
-    ja, jv = self.sys.joints[0].angle_vel(qp)
-    ang_y = bm.quat_to_euler(qp.rot[:, 0])[:, 1:2]
-    pos = qp.pos[:, 0, 2:] if self._exclude else qp.pos[:, 0][:, [0, 2]]
-    qvel = [qp.vel[:, 0][:, [0, 2]], qp.ang[:, 0, 1:2], jv]
-    return torch.cat([pos, ang_y, ja] + qvel, -1)
-
-  def _step(self, state, action, qp, info):
-    dt = float(self.sys.config.dt)
-    x_velocity = (qp.pos[:, 0, 0] - state.qp.pos[:, 0, 0]) / dt
-    forward_reward = self._fw * x_velocity
-    ang_y = bm.quat_to_euler(qp.rot[:, 0])[:, 1]
-    z = qp.pos[:, 0, 2]
-    one, zero = torch.ones_like(z), torch.zeros_like(z)
-    healthy = torch.where(z < self._z[0], zero, one)
-    healthy = torch.where(z > self._z[1], zero, healthy)
-    healthy = torch.where(ang_y > self._ang[1], zero, healthy)
-    healthy = torch.where(ang_y < self._ang[0], zero, healthy)
-    healthy_reward = self._hr * one if self._term else self._hr * healthy
-    ctrl_cost = self._cw * (action * action).sum(-1)
-    obs = self._get_obs(qp, info)
-    reward = forward_reward + healthy_reward - ctrl_cost
-    done = 1.0 - healthy if self._term else zero
-    metrics = _replace_metrics(state, reward_forward=forward_reward, reward_ctrl=-ctrl_cost,
-                               reward_healthy=healthy_reward, x_position=qp.pos[:, 0, 0],
-                               x_velocity=x_velocity)
-    return state.replace(qp=qp, obs=obs, reward=reward, done=done, metrics=metrics)
-
-
-class Hopper(_Locomotion2D):
-  """`brax/envs/hopper.py`."""
-  config = robots.HOPPER_CONFIG
-  spring_config = robots.HOPPER_SPRING_CONFIG
-
-
-class Walker2d(_Locomotion2D):
-  """`brax/envs/walker2d.py` (its own healthy ranges, walker2d.py:132-141)."""
-  config = robots.WALKER2D_CONFIG
-  spring_config = robots.WALKER2D_SPRING_CONFIG
-
-  def __init__(self, healthy_z_range=(0.7, 2.0), healthy_angle_range=(-1.0, 1.0), **kwargs):
-    super().__init__(healthy_z_range=healthy_z_range, healthy_angle_range=healthy_angle_range,
-                     **kwargs)
-
-
 class InvertedPendulum(TorchEnv):
   """`brax/envs/inverted_pendulum.py:124-166`; action_size 1 (the thruster's
   three indices clip to action[0])."""
@@ -247,8 +184,8 @@ class Swimmer(TorchEnv):
 
   def __init__(self, forward_reward_weight=1.0, ctrl_cost_weight=1e-4, reset_noise_scale=0.1,
                exclude_current_positions_from_observation=True, legacy_reward=False, **kwargs):
-    if legacy_reward:
-      raise NotImplementedError('legacy_reward')
+    # legacy_reward is accepted and unused, as in the reference (swimmer.py:158)
+    del legacy_reward
     super().__init__(**kwargs)
     self._fw, self._cw = forward_reward_weight, ctrl_cost_weight
     self.qpos_noise = self.qvel_noise = (-reset_noise_scale, reset_noise_scale)

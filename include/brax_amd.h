@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 4
+#define BX_ABI_VERSION 5
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
 enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
@@ -54,7 +54,10 @@ enum { BX_COL_CAPSULE_PLANE = 0, BX_COL_CAPSULE_CAPSULE = 1,
 enum { BX_FORCE_THRUSTER = 0, BX_FORCE_TWISTER = 1 };
 /* env layer kinds (obs / reward programs) */
 enum { BX_ENV_NONE = 0, BX_ENV_ANT = 1, BX_ENV_HUMANOID = 2, BX_ENV_HALFCHEETAH = 3,
-       BX_ENV_HUMANOID_STANDUP = 4 };
+       BX_ENV_HUMANOID_STANDUP = 4,
+       /* the planar walkers (hopper.py:183-246, walker2d.py:194-253): one
+        * program, their own constructor defaults */
+       BX_ENV_HOPPER = 5, BX_ENV_WALKER2D = 6 };
 /* observation options. BX_OBS_XY: exclude_current_positions_from_observation
  * = False, the torso's x (and y) precede its z (ant.py:262-265,
  * humanoid.py:289-292: x, y; half_cheetah.py:206-209: x) */
@@ -237,7 +240,11 @@ typedef struct bx_env_params {
    *                terminate_when_unhealthy, use_contact_forces
    *   HUMANOID:    forward_reward_weight, ctrl_cost_weight, 0, healthy_reward,
    *                healthy_z_min, healthy_z_max, terminate_when_unhealthy, 0
-   *   HALFCHEETAH: forward_reward_weight, ctrl_cost_weight, 0... */
+   *   HALFCHEETAH: forward_reward_weight, ctrl_cost_weight, 0...
+   *   HOPPER / WALKER2D: forward_reward_weight, ctrl_cost_weight,
+   *                healthy_reward, healthy_z_min, healthy_z_max (+inf: pass
+   *                FLT_MAX), healthy_angle_min, healthy_angle_max,
+   *                terminate_when_unhealthy */
   float coef[8];
   /* AutoReset targets (first_qp / first_obs); required when auto_reset */
   bx_qp first_qp;

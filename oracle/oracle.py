@@ -17,7 +17,8 @@ from brax_amd import abi
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, '_build', 'liboracle.so')
 
-ENV_KIND = {'none': 0, 'ant': 1, 'humanoid': 2, 'halfcheetah': 3, 'humanoidstandup': 4}
+ENV_KIND = {'none': 0, 'ant': 1, 'humanoid': 2, 'halfcheetah': 3, 'humanoidstandup': 4,
+            'hopper': 5, 'walker2d': 6}
 
 
 def build():

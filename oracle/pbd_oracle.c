@@ -1985,6 +1985,29 @@ static int obs_halfcheetah(const sysc* s, const body_t* qp, R* obs, int xy) {
   return n;
 }
 
+/* math.quat_to_euler(q)[1] (math.py:80-91) */
+static R euler_y(const R* q) {
+  R v = (R)2 * q[1] * q[3] + (R)2 * q[0] * q[2];
+  v = v < (R)-1 ? (R)-1 : (v > (R)1 ? (R)1 : v);
+  return (R)asin((double)v);
+}
+
+/* Hopper / Walker2d._get_obs (hopper.py:231-246, walker2d.py:240-253) */
+static int obs_loco2d(const sysc* s, const body_t* qp, R* obs, int xy) {
+  int n = 0;
+  R ang[64], vel[64];
+  int nd = angle_vel(s, qp, ang, vel);
+  if (xy) obs[n++] = qp[0].pos[0];
+  obs[n++] = qp[0].pos[2];
+  obs[n++] = euler_y(qp[0].rot);
+  for (int i = 0; i < nd; i++) obs[n++] = ang[i];
+  obs[n++] = qp[0].vel[0];
+  obs[n++] = qp[0].vel[2];
+  obs[n++] = qp[0].ang[1];
+  for (int i = 0; i < nd; i++) obs[n++] = vel[i];
+  return n;
+}
+
 /* Humanoid._center_of_mass (humanoid.py:336-338): bodies [:-1] */
 static void humanoid_com(const sysc* s, const body_t* qp, R* com) {
   R m = 0;
@@ -2065,6 +2088,8 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
       int n = 0;
       if (kind == BX_ENV_ANT) n = obs_ant(&s, q, info_c + e * 6 * N, obs + e * obs_size, xy);
       else if (kind == BX_ENV_HALFCHEETAH) n = obs_halfcheetah(&s, q, obs + e * obs_size, xy);
+      else if (kind == BX_ENV_HOPPER || kind == BX_ENV_WALKER2D)
+        n = obs_loco2d(&s, q, obs + e * obs_size, xy);
       else if (kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP)
         n = obs_humanoid(&s, q, act + e * s.aw, obs + e * obs_size, xy);
       if (n != obs_size) rc = -1;
@@ -2153,6 +2178,27 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
          * y_position, y_velocity */
         m[0] = norm3(ca); m[1] = fwd; m[2] = 5; m[3] = fwd; m[4] = -ctrl;
         m[5] = ca[0]; m[6] = v[0]; m[7] = ca[1]; m[8] = v[1];
+      } else if (kind == BX_ENV_HOPPER || kind == BX_ENV_WALKER2D) {
+        /* hopper.py:204-229 with the constructor defaults (hopper.py:146-158,
+         * walker2d.py:153-163); sorted metrics: reward_ctrl, reward_forward,
+         * reward_healthy, x_position, x_velocity */
+        n = obs_loco2d(&s, w.qp, o, xy);
+        const int hop = kind == BX_ENV_HOPPER;
+        const R zmin = (R)0.7, zmax = hop ? (R)INFINITY : (R)2.0;
+        const R amin = hop ? (R)-0.2 : (R)-1.0, amax = hop ? (R)0.2 : (R)1.0;
+        R xv = (w.qp[0].pos[0] - q0[0].pos[0]) / dt;
+        R fwd = (R)1.0 * xv;
+        R ay = euler_y(w.qp[0].rot);
+        R z = w.qp[0].pos[2];
+        R healthy = z < zmin ? (R)0 : (R)1;
+        healthy = z > zmax ? (R)0 : healthy;
+        healthy = ay > amax ? (R)0 : healthy;
+        healthy = ay < amin ? (R)0 : healthy;
+        R hr = (R)1.0;
+        R ctrl = (R)1e-3 * sq;
+        reward[e] = fwd + hr - ctrl;
+        done_io[e] = (R)1 - healthy;
+        m[0] = -ctrl; m[1] = fwd; m[2] = hr; m[3] = w.qp[0].pos[0]; m[4] = xv;
       } else if (kind == BX_ENV_HUMANOID_STANDUP) {
         /* humanoid_standup.py:232-247; done unchanged; sorted metrics:
          * reward_linup, reward_quadctrl */

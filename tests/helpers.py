@@ -46,6 +46,16 @@ _SPRING_MOD = {'halfcheetah': 'HALF_CHEETAH', 'humanoidstandup': 'HUMANOID_STAND
 XY_ENVS = ['ant_xy', 'humanoid_xy', 'halfcheetah_xy']
 
 
+# kernel env kinds whose reference rollouts are the envtraj_* goldens (the
+# env-layer rollouts of oracle/gen_golden.py) rather than traj_*
+ENVTRAJ_KERNEL = ['hopper', 'walker2d']
+
+
+def env_golden(name):
+  """Golden file of a kernel env's reference rollout."""
+  return ('envtraj_' if name in ENVTRAJ_KERNEL else 'traj_') + name
+
+
 def env_kind(name):
   """Env-layer kind of a golden name ('ant_spring', 'ant_xy' -> 'ant')."""
   for suf in ('_spring', '_xy'):

@@ -22,8 +22,9 @@ import torch
 
 from tests.conftest import golden
 from tests.margins import record_margin
-from tests.helpers import (CAPSULES, POINTS, QP_FIELDS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL,
-                           XY_ENVS, compiled, env_kind, normwise, obs_flags)
+from tests.helpers import (CAPSULES, ENVTRAJ_KERNEL, POINTS, QP_FIELDS, ROBOTS, SPRING_ENVS,
+                           SPRING_ROBOTS, XCOL, XY_ENVS, compiled, env_golden, env_kind, normwise,
+                           obs_flags)
 
 pytestmark = pytest.mark.gpu
 
@@ -156,10 +157,10 @@ def test_system_step_vs_golden(dev, oracle_lib, name):
     _gate(pen, ref_pen, _env_err(o_pen, ref_pen), 'pen')
 
 
-@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS)
+@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS + ENVTRAJ_KERNEL)
 def test_env_step_vs_golden(dev, oracle_lib, name):
   env = _make_env(name, dev)
-  T = golden('traj_' + name)
+  T = golden(env_golden(name))
   env32 = Envelope(oracle_lib, name)
   fl = obs_flags(name)
   O, M = T['obs'].shape[-1], T['metrics'].shape[-1]
@@ -181,7 +182,7 @@ def test_env_step_vs_golden(dev, oracle_lib, name):
     _gate(met, T['metrics'][t], _env_err([o[4] for o in outs], T['metrics'][t]), 'metrics')
 
 
-@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS)
+@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS + ENVTRAJ_KERNEL)
 def test_reset_vs_golden(dev, oracle_lib, name):
   """Reset = default_qp FK + lift + System.info (impulse contacts) + obs.
 
@@ -191,7 +192,7 @@ def test_reset_vs_golden(dev, oracle_lib, name):
   The gate is therefore relative to E32 for obs; the non-contact part of the
   observation and the state are held to 1e-5."""
   env = _make_env(name, dev)
-  T = golden('traj_' + name)
+  T = golden(env_golden(name))
   st = env.reset_from(torch.as_tensor(T['reset_qpos'], dtype=torch.float32, device=dev),
                       torch.as_tensor(T['reset_qvel'], dtype=torch.float32, device=dev))
   got = _qp_np(st.qp)

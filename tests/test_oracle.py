@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 
 from tests.conftest import golden
-from tests.helpers import (CAPSULES, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL, XY_ENVS,
+from tests.helpers import (CAPSULES, ENVTRAJ_KERNEL, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS,
+                           XCOL, XY_ENVS, env_golden,
                            compiled, env_kind, obs_flags)
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
@@ -76,10 +77,10 @@ def test_contact_info_matches_reference(oracle_lib, name):
       assert np.abs(info[k] - T[k][t]).max() < 1e-9, k
 
 
-@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS)
+@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS + ENVTRAJ_KERNEL)
 def test_env_step_matches_reference(oracle_lib, name):
   o = _oracle(oracle_lib, name)
-  T = golden('traj_' + name)
+  T = golden(env_golden(name))
   O, M = T['obs'].shape[-1], T['metrics'].shape[-1]
   for t in range(T['action'].shape[0]):
     _, obs, rew, done, met = o.env_step(env_kind(name), T['qp'][t], T['action'][t], O, M,
@@ -90,10 +91,10 @@ def test_env_step_matches_reference(oracle_lib, name):
     assert np.abs(met - T['metrics'][t]).max() < 1e-12
 
 
-@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS)
+@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS + ENVTRAJ_KERNEL)
 def test_reset_matches_reference(oracle_lib, name):
   o = _oracle(oracle_lib, name)
-  T = golden('traj_' + name)
+  T = golden(env_golden(name))
   qp0 = o.default_qp(T['reset_qpos'], T['reset_qvel'])
   assert np.abs(qp0 - T['qp'][0]).max() < 1e-12
   ic = o.system_info(qp0)
