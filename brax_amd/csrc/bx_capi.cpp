@@ -551,6 +551,21 @@ int env_sizes(const bx_system* S, const bx_env_params* P, int* obs, int* met) {
       *obs = (xy ? 2 : 1) + 1 + D + 3 + D;
       *met = 5;
       return 0;
+    case BX_ENV_INVERTED_PENDULUM:  // cart x, joint angles, cart vel x, joint vels
+      if (xy) return fail("this env has no current-position observation option");
+      *obs = 2 + 2 * D;
+      *met = 0;
+      return 0;
+    case BX_ENV_INVERTED_DOUBLE_PENDULUM:  // cart x, sin, cos, cart vel x, joint vels
+      if (xy) return fail("this env has no current-position observation option");
+      *obs = 2 + 3 * D;
+      *met = 0;
+      return 0;
+    case BX_ENV_ACROBOT:  // joint angles, joint vels
+      if (xy) return fail("this env has no current-position observation option");
+      *obs = 2 * D;
+      *met = 4;
+      return 0;
     case BX_ENV_HALFCHEETAH:
       *obs = 3 + D + 3 + D + (xy ? 1 : 0);
       *met = 4;

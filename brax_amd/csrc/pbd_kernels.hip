@@ -2649,6 +2649,27 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
     i -= 3;
     return E.ang[D + i];
   }
+  if (kind == BX_ENV_INVERTED_PENDULUM) {
+    // [cart pos x, joint angles, cart vel x, joint vels]
+    if (i == 0) return q0[0];
+    i -= 1;
+    if (i < D) return E.ang[i];
+    i -= D;
+    if (i == 0) return q0[7];
+    return E.ang[D + i - 1];
+  }
+  if (kind == BX_ENV_INVERTED_DOUBLE_PENDULUM) {
+    // [cart pos x, sin(angles), cos(angles), cart vel x, joint vels]
+    if (i == 0) return q0[0];
+    i -= 1;
+    if (i < D) return sinf(E.ang[i]);
+    i -= D;
+    if (i < D) return cosf(E.ang[i]);
+    i -= D;
+    if (i == 0) return q0[7];
+    return E.ang[D + i - 1];
+  }
+  if (kind == BX_ENV_ACROBOT) return E.ang[i];  // [joint angles, joint vels]
   if (kind == BX_ENV_HALFCHEETAH) {
     if (i == 0) return q0[2];
     if (i == 1) return q0[3];
@@ -2993,6 +3014,27 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
         done = term ? 1.f - healthy : 0.f;
         // sorted: reward_ctrl, reward_forward, reward_healthy, x_position, x_velocity
         if (m) { m[0] = -ctrl; m[1] = fwd; m[2] = hr; m[3] = p1.x; m[4] = xv; }
+      } else if (kind == BX_ENV_INVERTED_PENDULUM) {
+        reward = 1.f;
+        done = fabsf(E.ang[0]) > .2f ? 1.f : 0.f;  // |obs[1]| > .2
+      } else if (kind == BX_ENV_INVERTED_DOUBLE_PENDULUM) {
+        // the pole tip (body 2's (0, 0, .3)) in the world
+        const float* q2 = E.qp + 2 * QP_STRIDE;
+        v3 tip = ld3(q2) + rotate(mk(0.f, 0.f, .3f), q4{q2[3], q2[4], q2[5], q2[6]});
+        float x = tip.x, y = tip.z;
+        float dist = 0.01f * (x * x) + (y - 2.f) * (y - 2.f);
+        float v1 = E.ang[H.D], v2 = E.ang[H.D + 1];
+        float velp = 1e-3f * (v1 * v1) + 5e-3f * (v2 * v2);
+        reward = 10.f - dist - velp;
+        done = y <= 1.f ? 1.f : 0.f;
+      } else if (kind == BX_ENV_ACROBOT) {
+        float a0 = E.ang[0], a1 = E.ang[1], w0 = E.ang[H.D], w1 = E.ang[H.D + 1];
+        float dist = a0 * a0 + a1 * a1;
+        float velp = 1e-3f * (w0 * w0 + w1 * w1);
+        reward = 10.f - dist - velp;
+        done = 0.f;
+        // sorted: alive_bonus (never updated: stays at its reset 0), dist_penalty, r_tot, vel_penalty
+        if (m) { m[0] = 0.f; m[1] = dist; m[2] = reward; m[3] = velp; }
       } else if (kind == BX_ENV_HUMANOID_STANDUP) {
         // humanoid_standup.py:232-247: uph = z / dt, reward = uph + 1 - 0.01 sum(a^2);
         // done is left as it came in

@@ -12,12 +12,13 @@ from brax_amd.envs.ant import Ant
 from brax_amd.envs.env import Env, PhysicsEnv, State, Wrapper
 from brax_amd.envs.half_cheetah import Halfcheetah
 from brax_amd.envs.hopper import Hopper, Walker2d
+from brax_amd.envs.pendulums import Acrobot, InvertedDoublePendulum, InvertedPendulum
 from brax_amd.envs.humanoid import Humanoid
 from brax_amd.envs.humanoid_standup import HumanoidStandup
 from brax_amd.envs import torch_envs
 
 _envs = {
-    'acrobot': torch_envs.Acrobot,
+    'acrobot': Acrobot,
     'fast': torch_envs.Fast,
     'fetch': torch_envs.Fetch,
     'grasp': torch_envs.Grasp,
@@ -26,8 +27,8 @@ _envs = {
     'hopper': Hopper,
     'humanoid': Humanoid,
     'humanoidstandup': HumanoidStandup,
-    'inverted_pendulum': torch_envs.InvertedPendulum,
-    'inverted_double_pendulum': torch_envs.InvertedDoublePendulum,
+    'inverted_pendulum': InvertedPendulum,
+    'inverted_double_pendulum': InvertedDoublePendulum,
     'pusher': torch_envs.Pusher,
     'reacher': torch_envs.Reacher,
     'reacherangle': torch_envs.ReacherAngle,

@@ -123,57 +123,6 @@ def _replace_metrics(state, **kw):
   return m
 
 
-class InvertedPendulum(TorchEnv):
-  """`brax/envs/inverted_pendulum.py:124-166`; action_size 1 (the thruster's
-  three indices clip to action[0])."""
-  config = robots.INVERTED_PENDULUM_CONFIG
-  spring_config = robots.INVERTED_PENDULUM_SPRING_CONFIG
-  qpos_noise = qvel_noise = (-0.01, 0.01)
-  obs_size = 4
-
-  @property
-  def action_size(self):
-    return 1
-
-  def _get_obs(self, qp, info):
-    ja, jv = self.sys.joints[0].angle_vel(qp)
-    return torch.cat([qp.pos[:, 0, :1], ja, qp.vel[:, 0, :1], jv], -1)
-
-  def _step(self, state, action, qp, info):
-    obs = self._get_obs(qp, info)
-    reward = torch.ones_like(obs[:, 0])
-    done = torch.where(obs[:, 1].abs() > .2, 1.0, 0.0)
-    return state.replace(qp=qp, obs=obs, reward=reward, done=done)
-
-
-class InvertedDoublePendulum(TorchEnv):
-  """`brax/envs/inverted_double_pendulum.py:131-186`."""
-  config = robots.INVERTED_DOUBLE_PENDULUM_CONFIG
-  spring_config = robots.INVERTED_DOUBLE_PENDULUM_SPRING_CONFIG
-  qpos_noise = qvel_noise = (-0.01, 0.01)
-  obs_size = 8
-
-  @property
-  def action_size(self):
-    return 1
-
-  def _get_obs(self, qp, info):
-    ja, jv = self.sys.joints[0].angle_vel(qp)
-    return torch.cat([qp.pos[:, 0, :1], torch.sin(ja), torch.cos(ja), qp.vel[:, 0, :1], jv], -1)
-
-  def _step(self, state, action, qp, info):
-    _, jv = self.sys.joints[0].angle_vel(qp)
-    tip, _ = qp[:, 2].to_world(torch.tensor([0., 0., .3], device=self.dev))
-    x, y = tip[:, 0], tip[:, 2]
-    dist_penalty = 0.01 * x ** 2 + (y - 2) ** 2
-    v1, v2 = jv[:, 0], jv[:, 1]
-    vel_penalty = 1e-3 * v1 ** 2 + 5e-3 * v2 ** 2
-    obs = self._get_obs(qp, info)
-    reward = 10.0 - dist_penalty - vel_penalty
-    done = torch.where(y <= 1, 1.0, 0.0)
-    return state.replace(qp=qp, obs=obs, reward=reward, done=done)
-
-
 class Swimmer(TorchEnv):
   """`brax/envs/swimmer.py:153-290`: viscous drag fed to the three Thrusters
   through the action tail."""
@@ -320,33 +269,6 @@ class ReacherAngle(Reacher):
     reward_dist = -torch.linalg.norm(obs[:, -3:], dim=-1)
     metrics = {'rewardDist': reward_dist, 'rewardCtrl': torch.zeros_like(reward_dist)}
     return state.replace(qp=qp, obs=obs, reward=reward_dist, metrics=metrics)
-
-
-class Acrobot(TorchEnv):
-  """`brax/envs/acrobot.py:40-95`."""
-  config = robots.ACROBOT_CONFIG
-  spring_config = robots.ACROBOT_SPRING_CONFIG
-  qpos_noise = qvel_noise = (-.01, .01)
-  metric_keys = ('dist_penalty', 'vel_penalty', 'alive_bonus', 'r_tot')
-  obs_size = 4
-
-  @property
-  def action_size(self):
-    return 1
-
-  def _get_obs(self, qp, info):
-    ja, jv = self.sys.joints[0].angle_vel(qp)
-    return torch.cat([ja, jv], -1)
-
-  def _step(self, state, action, qp, info):
-    ja, jv = self.sys.joints[0].angle_vel(qp)
-    obs = torch.cat([ja, jv], -1)
-    dist_penalty = ja[:, 0] ** 2 + ja[:, 1] ** 2
-    vel_penalty = 1e-3 * (jv[:, 0] ** 2 + jv[:, 1] ** 2)
-    r = 10.0 - dist_penalty - vel_penalty
-    metrics = _replace_metrics(state, dist_penalty=dist_penalty, vel_penalty=vel_penalty,
-                               r_tot=r)
-    return state.replace(qp=qp, obs=obs, reward=r, done=torch.zeros_like(r), metrics=metrics)
 
 
 class Pusher(TorchEnv):

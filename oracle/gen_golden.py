@@ -301,6 +301,12 @@ def env_traj(env, name, n_envs, n_steps, act_seed_base=10_000):
       _, r1, r2 = jp.random_split(rng, 3)
       qpos_l.append(env.sys.default_angle() + env._noise(r1))
       qvel_l.append(env._noise(r2))
+    elif name == 'acrobot':
+      # acrobot.py:56-61 draws the same U[-.01, .01) noise inline
+      _, r1, r2 = jp.random_split(rng, 3)
+      D = env.sys.num_joint_dof
+      qpos_l.append(env.sys.default_angle() + jp.random_uniform(r1, (D,), -.01, .01))
+      qvel_l.append(jp.random_uniform(r2, (D,), -.01, .01))
     states.append(env.reset(rng))
   acts = np.stack([np.random.default_rng(act_seed_base + t).uniform(-1, 1, (n_envs, A))
                    for t in range(n_steps)])

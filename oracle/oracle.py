@@ -18,7 +18,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, '_build', 'liboracle.so')
 
 ENV_KIND = {'none': 0, 'ant': 1, 'humanoid': 2, 'halfcheetah': 3, 'humanoidstandup': 4,
-            'hopper': 5, 'walker2d': 6}
+            'hopper': 5, 'walker2d': 6, 'inverted_pendulum': 7, 'inverted_double_pendulum': 8,
+            'acrobot': 9}
 
 
 def build():

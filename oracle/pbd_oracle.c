@@ -2008,6 +2008,24 @@ static int obs_loco2d(const sysc* s, const body_t* qp, R* obs, int xy) {
   return n;
 }
 
+/* InvertedPendulum / InvertedDoublePendulum / Acrobot._get_obs
+ * (inverted_pendulum.py:152-160, inverted_double_pendulum.py:166-178,
+ * acrobot.py:90-95) */
+static int obs_pendulums(const sysc* s, int kind, const body_t* qp, R* obs, R* ang, R* vel) {
+  int n = 0;
+  int nd = angle_vel(s, qp, ang, vel);
+  if (kind != BX_ENV_ACROBOT) obs[n++] = qp[0].pos[0];
+  if (kind == BX_ENV_INVERTED_DOUBLE_PENDULUM) {
+    for (int i = 0; i < nd; i++) obs[n++] = (R)sin((double)ang[i]);
+    for (int i = 0; i < nd; i++) obs[n++] = (R)cos((double)ang[i]);
+  } else {
+    for (int i = 0; i < nd; i++) obs[n++] = ang[i];
+  }
+  if (kind != BX_ENV_ACROBOT) obs[n++] = qp[0].vel[0];
+  for (int i = 0; i < nd; i++) obs[n++] = vel[i];
+  return n;
+}
+
 /* Humanoid._center_of_mass (humanoid.py:336-338): bodies [:-1] */
 static void humanoid_com(const sysc* s, const body_t* qp, R* com) {
   R m = 0;
@@ -2090,6 +2108,10 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
       else if (kind == BX_ENV_HALFCHEETAH) n = obs_halfcheetah(&s, q, obs + e * obs_size, xy);
       else if (kind == BX_ENV_HOPPER || kind == BX_ENV_WALKER2D)
         n = obs_loco2d(&s, q, obs + e * obs_size, xy);
+      else if (kind >= BX_ENV_INVERTED_PENDULUM && kind <= BX_ENV_ACROBOT) {
+        R ang[64], vel[64];
+        n = obs_pendulums(&s, kind, q, obs + e * obs_size, ang, vel);
+      }
       else if (kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP)
         n = obs_humanoid(&s, q, act + e * s.aw, obs + e * obs_size, xy);
       if (n != obs_size) rc = -1;
@@ -2199,6 +2221,31 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
         reward[e] = fwd + hr - ctrl;
         done_io[e] = (R)1 - healthy;
         m[0] = -ctrl; m[1] = fwd; m[2] = hr; m[3] = w.qp[0].pos[0]; m[4] = xv;
+      } else if (kind >= BX_ENV_INVERTED_PENDULUM && kind <= BX_ENV_ACROBOT) {
+        R ang[64], vel[64];
+        n = obs_pendulums(&s, kind, w.qp, o, ang, vel);
+        if (kind == BX_ENV_INVERTED_PENDULUM) {
+          reward[e] = 1;
+          done_io[e] = fabs((double)o[1]) > 0.2 ? (R)1 : (R)0;
+        } else if (kind == BX_ENV_INVERTED_DOUBLE_PENDULUM) {
+          /* jp.take(qp, 2).to_world([0, 0, .3]) */
+          const R off[3] = {0, 0, (R)0.3};
+          R tip[3];
+          rotate(off, w.qp[2].rot, tip);
+          R x = w.qp[2].pos[0] + tip[0], y = w.qp[2].pos[2] + tip[2];
+          R dist = (R)0.01 * (x * x) + (y - 2) * (y - 2);
+          R velp = (R)1e-3 * (vel[0] * vel[0]) + (R)5e-3 * (vel[1] * vel[1]);
+          reward[e] = (R)10 - dist - velp;
+          done_io[e] = y <= 1 ? (R)1 : (R)0;
+        } else {
+          R dist = ang[0] * ang[0] + ang[1] * ang[1];
+          R velp = (R)1e-3 * (vel[0] * vel[0] + vel[1] * vel[1]);
+          R r = (R)10 - dist - velp;
+          reward[e] = r;
+          done_io[e] = 0;
+          /* sorted: alive_bonus, dist_penalty, r_tot, vel_penalty */
+          m[0] = 0; m[1] = dist; m[2] = r; m[3] = velp;
+        }
       } else if (kind == BX_ENV_HUMANOID_STANDUP) {
         /* humanoid_standup.py:232-247; done unchanged; sorted metrics:
          * reward_linup, reward_quadctrl */

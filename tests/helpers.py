@@ -48,7 +48,7 @@ XY_ENVS = ['ant_xy', 'humanoid_xy', 'halfcheetah_xy']
 
 # kernel env kinds whose reference rollouts are the envtraj_* goldens (the
 # env-layer rollouts of oracle/gen_golden.py) rather than traj_*
-ENVTRAJ_KERNEL = ['hopper', 'walker2d']
+ENVTRAJ_KERNEL = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum', 'acrobot']
 
 
 def env_golden(name):
