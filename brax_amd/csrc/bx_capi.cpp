@@ -566,6 +566,24 @@ int env_sizes(const bx_system* S, const bx_env_params* P, int* obs, int* met) {
       *obs = 2 * D;
       *met = 4;
       return 0;
+    case BX_ENV_REACHER:
+    case BX_ENV_REACHERANGLE:  // cos, sin, target xy, tip vel xy, tip - target
+      if (xy) return fail("this env has no current-position observation option");
+      if (P->kind == BX_ENV_REACHERANGLE && H.A > 2)
+        return fail("ReacherAngle's action map holds at most 2 actions");
+      *obs = 2 * D + 7;
+      *met = 2;
+      return 0;
+    case BX_ENV_SWIMMER:  // (x, y,) ang z, joint angles, vel x, vel y, ang z, joint vels
+      if (N != 4) return fail("Swimmer's drag program takes 3 segments and a floor");
+      *obs = (xy ? 3 : 1) + D + 3 + D;
+      *met = 8;
+      return 0;
+    case BX_ENV_PUSHER:  // joint angles, joint vels, tip, object, goal positions
+      if (xy) return fail("this env has no current-position observation option");
+      *obs = 2 * D + 9;
+      *met = 3;
+      return 0;
     case BX_ENV_HALFCHEETAH:
       *obs = 3 + D + 3 + D + (xy ? 1 : 0);
       *met = 4;
@@ -788,6 +806,7 @@ int bx_env_observe(bx_system* S, const bx_env_params* env, int64_t n_envs, const
   a.kind = env->kind;
   a.obs_size = env->obs_size;
   a.obs_flags = env->obs_flags;
+  for (int k = 0; k < 8; k++) a.coef[k] = env->coef[k];
   a.act = act;
   a.act_stride = act_stride;
   a.act_width = act_width;
@@ -851,6 +870,7 @@ int bx_env_reset(bx_system* S, const bx_env_params* env, int64_t n_envs, uint64_
   a.kind = env->kind;
   a.obs_size = env->obs_size;
   a.obs_flags = env->obs_flags;
+  for (int k = 0; k < 8; k++) a.coef[k] = env->coef[k];
   a.obs = out->obs;
   // _get_obs(qp, info, jp.zeros(action_size)): a null action reads as zeros
   a.act = nullptr;

@@ -2583,6 +2583,12 @@ __device__ void joint_angles(const Cst& c, const BlobHdr& H, const Env& E, int l
 
 __device__ __forceinline__ float clip1(float x) { return clampf(x, -1.f, 1.f); }
 
+// math.quat_to_euler(q)[2] (math.py:80-91) of a QP record's rot (w, x, y, z)
+__device__ __forceinline__ float euler_z(const float* q) {
+  return atan2f(-2.f * q[1] * q[2] + 2.f * q[0] * q[3],
+                q[1] * q[1] + q[0] * q[0] - q[3] * q[3] - q[2] * q[2]);
+}
+
 // math.quat_to_euler(q)[1] (math.py:80-91): asin(clip(2 q1 q3 + 2 q0 q2))
 // of a QP record's rot (w, x, y, z)
 __device__ __forceinline__ float euler_y(const float* q) {
@@ -2603,8 +2609,17 @@ __device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3
 }
 
 // observation element i of the env kind
+// the arm tip of the reachers: body coef[1]'s (.11, 0, 0) in the world and
+// its velocity (QP.to_world, base.py:112-126)
+__device__ __forceinline__ void arm_tip(const Env& E, const float* coef, v3& tp, v3& tv) {
+  const float* a = E.qp + (int)coef[1] * QP_STRIDE;
+  v3 off = rotate(mk(.11f, 0.f, 0.f), q4{a[3], a[4], a[5], a[6]});
+  tp = ld3(a) + off;
+  tv = ld3(a + 7) + cross(ld3(a + 10), off);
+}
+
 __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind, int flags, int i,
-                          const float* act, int aw, bool valid) {
+                          const float* act, int aw, bool valid, const float* coef) {
   const int N = H.N, D = H.D;
   const float* q0 = E.qp;
   // exclude_current_positions_from_observation=False: the torso's x (and y)
@@ -2670,6 +2685,41 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
     return E.ang[D + i - 1];
   }
   if (kind == BX_ENV_ACROBOT) return E.ang[i];  // [joint angles, joint vels]
+  if (kind == BX_ENV_REACHER || kind == BX_ENV_REACHERANGLE) {
+    // reacher.py:205-224: [cos(angles), sin(angles), target xy, tip vel xy,
+    // tip - target]; the tip is the arm body's (.11, 0, 0)
+    if (i < D) return cosf(E.ang[i]);
+    i -= D;
+    if (i < D) return sinf(E.ang[i]);
+    i -= D;
+    const float* tq = E.qp + (int)coef[0] * QP_STRIDE;
+    if (i < 2) return tq[i];
+    i -= 2;
+    v3 tp, tv;
+    arm_tip(E, coef, tp, tv);
+    if (i < 2) return i == 0 ? tv.x : tv.y;
+    i -= 2;
+    v3 d = tp - ld3(tq);
+    return i == 0 ? d.x : (i == 1 ? d.y : d.z);
+  }
+  if (kind == BX_ENV_SWIMMER) {
+    // swimmer.py:257-272: [ang z, joint angles, vel x, vel y, ang z, joint vels]
+    if (i == 0) return euler_z(q0 + 3);
+    i -= 1;
+    if (i < D) return E.ang[i];
+    i -= D;
+    if (i < 2) return q0[7 + i];
+    if (i == 2) return q0[12];
+    i -= 3;
+    return E.ang[D + i];
+  }
+  if (kind == BX_ENV_PUSHER) {
+    // pusher.py:232-242: [joint angles, joint vels, tip, object, goal positions]
+    if (i < 2 * D) return E.ang[i];
+    i -= 2 * D;
+    const int b = (int)coef[i / 3];
+    return E.qp[b * QP_STRIDE + i % 3];
+  }
   if (kind == BX_ENV_HALFCHEETAH) {
     if (i == 0) return q0[2];
     if (i == 1) return q0[3];
@@ -2744,7 +2794,7 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
 template <int L>
 __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int lane, int kind,
                             int flags, int obs_size, const float* act, int aw, float* obs_out,
-                            const JointC* hj = nullptr) {
+                            const float* coef, const JointC* hj = nullptr) {
   joint_angles<L>(c, H, E, lane, hj);
   if ((kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP) && lane == 0) {
     v3 com;
@@ -2756,7 +2806,7 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
   esync<L>();
   if (obs_out)
     for (int i = lane; i < obs_size; i += L)
-      obs_out[i] = obs_elem(c, H, E, kind, flags, i, act, aw, act != nullptr);
+      obs_out[i] = obs_elem(c, H, E, kind, flags, i, act, aw, act != nullptr, coef);
 }
 
 // ---------------------------------------------------------------------------
@@ -2933,19 +2983,64 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
     v3 pos0 = ld3(E.qp);  // torso position before the step
     v3 com0 = mk(0.f, 0.f, 0.f);
     float msum = 0.f;
-    if (kind == BX_ENV_HUMANOID) humanoid_com(c, H, E.qp, com0, msum);
+    if (kind == BX_ENV_HUMANOID || kind == BX_ENV_SWIMMER) humanoid_com(c, H, E.qp, com0, msum);
+    // Pusher's rewards come from the state before the step (pusher.py:212-217)
+    float near0 = 0.f, dist0 = 0.f;
+    if (kind == BX_ENV_PUSHER) {
+      v3 tip = ld3(E.qp + (int)P.coef[0] * QP_STRIDE), obj = ld3(E.qp + (int)P.coef[1] * QP_STRIDE);
+      v3 goal = ld3(E.qp + (int)P.coef[2] * QP_STRIDE);
+      near0 = -norm(obj - tip);
+      dist0 = -norm(obj - goal);
+    }
+    // the action System.step reads: the env's own, or its pre-step program's
+    // output in LDS (red words 48..63)
+    const float* sact = act;
+    int saw = aw;
+    float* xact = E.red + 48;
+    if (kind == BX_ENV_REACHERANGLE) {
+      // reacherangle.py:79: min + range * (a + 1) / 2 onto the angle limits
+      if (valid && lane < aw) xact[lane] = P.coef[2 + lane] + P.coef[4 + lane] * ((act[lane] + 1.f) / 2.f);
+      sact = valid ? xact : nullptr;
+    } else if (kind == BX_ENV_SWIMMER) {
+      // swimmer.py:246-255: viscous drag on the 3 segments, appended to the
+      // action for the Thrusters: force_b = rot_b(vel_b * sph - diag(D)),
+      // D[b][k] = fix_k |v_bk| v_bk in the segment frame, and jp.diag keeps
+      // D's diagonal (D00, D11, D22) for every segment (the reference's
+      // broadcast); clipped to [-5, 5]
+      const float* q = E.qp + lane * QP_STRIDE;
+      q4 rot{0.f, 0.f, 0.f, 0.f};
+      v3 vel = mk(0.f, 0.f, 0.f);
+      if (lane < 3) {
+        rot = q4{q[3], q[4], q[5], q[6]};
+        vel = ld3(q + 7);
+        v3 lv = rotate(vel, quat_inv(rot));
+        float l = lane == 0 ? lv.x : (lane == 1 ? lv.y : lv.z);
+        E.red[60 + lane] = P.coef[3 + lane] * fabsf(l) * l;
+      }
+      esync<L>();
+      if (lane < 3 && valid) {
+        v3 f = vel * P.coef[2] - mk(E.red[60], E.red[61], E.red[62]);
+        f = rotate(f, rot);
+        xact[aw + 3 * lane] = clampf(f.x, -5.f, 5.f);
+        xact[aw + 3 * lane + 1] = clampf(f.y, -5.f, 5.f);
+        xact[aw + 3 * lane + 2] = clampf(f.z, -5.f, 5.f);
+      }
+      if (valid && lane < aw) xact[lane] = act[lane];
+      sact = valid ? xact : nullptr;
+      saw = aw + 9;
+    }
     esync<L>();
     if constexpr (S) {
       v3 icv, ica, iaa;
-      pbd_step_single<L, F, M>(c, H, E, lane, valid, act, aw, X, icv, ica, iaa);
+      pbd_step_single<L, F, M>(c, H, E, lane, valid, sact, saw, X, icv, ica, iaa);
     } else if (H.spring) {
-      spring_step<L, F>(c, H, E, lane, valid, act, aw);
+      spring_step<L, F>(c, H, E, lane, valid, sact, saw);
     } else {
-      pbd_step<L, F>(c, H, E, lane, valid, act, aw);
+      pbd_step<L, F>(c, H, E, lane, valid, sact, saw);
     }
     BX_KSTAMP(11);
     env_observe<L>(c, H, E, lane, kind, P.obs_flags, P.obs_size, act, aw,
-                   valid ? A.out.obs + e * P.obs_size : nullptr, S ? &X.J : nullptr);
+                   valid ? A.out.obs + e * P.obs_size : nullptr, P.coef, S ? &X.J : nullptr);
     BX_KSTAMP(12);
     // reward / done / metrics (lane 0 of the env)
     if (lane == 0 && valid) {
@@ -3035,6 +3130,38 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
         done = 0.f;
         // sorted: alive_bonus (never updated: stays at its reset 0), dist_penalty, r_tot, vel_penalty
         if (m) { m[0] = 0.f; m[1] = dist; m[2] = reward; m[3] = velp; }
+      } else if (kind == BX_ENV_REACHER || kind == BX_ENV_REACHERANGLE) {
+        // reacher.py:188-197 / reacherangle.py:79-95: -|tip - target| (- |a|^2)
+        v3 tp, tv;
+        arm_tip(E, P.coef, tp, tv);
+        float rd = -norm(tp - ld3(E.qp + (int)P.coef[0] * QP_STRIDE));
+        if (kind == BX_ENV_REACHER) {
+          float rc = -sq;
+          reward = rd + rc;
+          if (m) { m[0] = rc; m[1] = rd; }  // sorted: reward_ctrl, reward_dist
+        } else {
+          reward = rd;
+          if (m) { m[0] = 0.f; m[1] = rd; }  // sorted: rewardCtrl, rewardDist
+        }
+      } else if (kind == BX_ENV_SWIMMER) {
+        // swimmer.py:222-241: the segments' centre of mass; done as it came in
+        v3 com1;
+        humanoid_com(c, H, E.qp, com1, msum);
+        v3 v = (com1 - com0) / dt;
+        float fwd = P.coef[0] * v.x;
+        float ctrl = P.coef[1] * sq;
+        reward = fwd - ctrl;
+        // sorted: distance_from_origin, forward_reward, reward_ctrl, reward_fwd,
+        // x_position, x_velocity, y_position, y_velocity
+        if (m) {
+          m[0] = norm(p1); m[1] = fwd; m[2] = -ctrl; m[3] = fwd;
+          m[4] = com1.x; m[5] = v.x; m[6] = com1.y; m[7] = v.y;
+        }
+      } else if (kind == BX_ENV_PUSHER) {
+        // pusher.py:212-231; done as it came in
+        float rc = -sq;
+        reward = dist0 + 0.1f * rc + 0.5f * near0;
+        if (m) { m[0] = rc; m[1] = dist0; m[2] = near0; }  // sorted: ctrl, dist, near
       } else if (kind == BX_ENV_HUMANOID_STANDUP) {
         // humanoid_standup.py:232-247: uph = z / dt, reward = uph + 1 - 0.01 sum(a^2);
         // done is left as it came in
@@ -3130,7 +3257,7 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) info_obs_kernel(InfoArgs A) {
   if (A.obs) {
     const float* act = valid && A.act ? A.act + e * A.act_stride : nullptr;
     env_observe<L>(c, H, E, lane, A.kind, A.obs_flags, A.obs_size, act, (int)A.act_width,
-                   valid ? A.obs + e * A.obs_size : nullptr);
+                   valid ? A.obs + e * A.obs_size : nullptr, A.coef);
   }
   // reset: reward, done, steps, truncation and metrics start at zero
   // (ant.py:205-219, wrappers.py:94-97)

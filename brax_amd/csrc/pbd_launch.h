@@ -29,6 +29,7 @@ struct InfoArgs {
   bx_qp q;
   bx_info info;
   int kind, obs_size, obs_flags;
+  float coef[8];  // the env's bx_env_params.coef (body indices of the obs programs)
   const float* act;
   int64_t act_stride, act_width;
   float* obs;

@@ -1,0 +1,219 @@
+"""Reacher, ReacherAngle, Swimmer and Pusher on MI355X: kernel env programs
+BX_ENV_REACHER / REACHERANGLE / SWIMMER / PUSHER (`include/brax_amd.h`).
+
+* Reacher (`reacher.py:172-236`): obs = [cos(angles), sin(angles), target
+  xy, arm-tip vel xy, tip - target]; reward = -|tip - target| - |a|^2.
+* ReacherAngle (`reacherangle.py:60-106`): the same observation; the [-1, 1]
+  action is mapped onto the joints' angle limits for its Angle actuators
+  before the physics (inside the step kernel); reward = -|tip - target|.
+* Swimmer (`swimmer.py:153-283`): the viscous drag of the three segments is
+  computed from the state inside the step kernel and appended to the action
+  for the Thrusters; reward from the segments' centre of mass.
+* Pusher (`pusher.py:170-242`): rewards from the state before the step.
+
+Resets: the reachers draw joint noise and a target in a disc, the pusher
+places its object in a disc and fixes goal and table; these run as a
+default_qp kernel plus a position write and the kernel observation. Noise
+and targets come from the device counter RNG keyed by the reset key (JAX
+threefry parity unpinned); the reset itself is pinned through
+`reset_from`.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from brax_amd import _native
+from brax_amd.envs import robots
+from brax_amd.envs.env import PhysicsEnv, State, key_to_seed
+from brax_amd.system import _stream
+
+
+def _uniform(shape, seed, offset, lo, hi, device):
+  out = torch.empty(shape, dtype=torch.float32, device=device)
+  if out.numel():
+    _native.check(_native.lib().bx_uniform(C.c_void_p(out.data_ptr()), out.numel(), seed,
+                                           offset, float(lo), float(hi), _stream(out.device.index)))
+  return out
+
+
+# ---------------------------------------------------------------- constants
+# bx_env_params.coef of each program, from the config and its body index (no
+# device needed: the oracle tests build them on the CPU)
+
+def reacher_coef(config, body_index, angle=False):
+  c = np.zeros(8, np.float64)
+  c[0], c[1] = body_index['target'], body_index['body1']
+  if angle:
+    # reacherangle.py:67-75: per action, the limit it maps [-1, 1] onto
+    lim = [(l.min, l.max) for j in config.joints for l in j.angle_limit]
+    if len(lim) > 2:
+      raise ValueError('ReacherAngle program maps at most 2 actions')
+    for i, (lo, hi) in enumerate(lim):
+      c[2 + i] = lo
+      c[4 + i] = hi - lo
+  return c
+
+
+def swimmer_coef(forward_reward_weight=1.0, ctrl_cost_weight=1e-4):
+  """swimmer.py:166-193: drag constants of the mujoco swimmer."""
+  viscosity, density = 0.1, 10.0
+  i0, i1, i2 = 0.17278759594743870, 3.5709436495803999, 3.5709436495803999
+  body_mass = 34.557519189487735
+  inertia = np.array([i1 + i2 - i0, i0 + i1 - i2, i0 + i2 - i1])
+  inertia = np.sqrt(inertia / (body_mass * 6))
+  spherical = -3 * math.pi * np.mean(inertia) * viscosity
+  fix = 0.5 * density * np.array([inertia[1] * inertia[2], inertia[0] * inertia[2],
+                                  inertia[0] * inertia[1]])
+  return np.array([forward_reward_weight, ctrl_cost_weight, spherical, fix[0], fix[1], fix[2],
+                   0, 0], np.float64)
+
+
+def pusher_coef(body_index):
+  c = np.zeros(8, np.float64)
+  c[0] = body_index['r_wrist_roll_link']
+  c[1] = body_index['object']
+  c[2] = body_index['goal']
+  return c
+
+
+# ---------------------------------------------------------------- envs
+class _KernelTask(PhysicsEnv):
+  config = spring_config = None
+
+  def __init__(self, legacy_spring=False, **kwargs):
+    if legacy_spring and self.spring_config is None:
+      raise NotImplementedError(f'{type(self).__name__} has no legacy_spring configuration')
+    super().__init__(self.spring_config if legacy_spring else self.config, **kwargs)
+
+  def _state(self, qp):
+    """A reset State of qp: kernel observation, zero reward / done / metrics."""
+    B = qp.pos.shape[0]
+    dev = self.sys.device
+    obs = self.observe(qp, torch.zeros((B, self.action_size), dtype=torch.float32, device=dev))
+    z = torch.zeros((B,), dtype=torch.float32, device=dev)
+    metrics = {k: torch.zeros_like(z) for k in self.metric_keys}
+    return State(qp=qp, obs=obs, reward=z, done=torch.zeros_like(z), metrics=metrics, info={})
+
+
+class Reacher(_KernelTask):
+  """Trains a two-link arm's tip to a random target (`brax/envs/reacher.py`)."""
+  kind = 10  # BX_ENV_REACHER
+  config = robots.REACHER_CONFIG
+  spring_config = robots.REACHER_SPRING_CONFIG
+  metric_keys = ('reward_ctrl', 'reward_dist')  # sorted (reacher.py:180-183)
+  target_sqrt = False  # ReacherAngle: dist = .2 * sqrt(u)
+
+  def __init__(self, **kwargs):
+    super().__init__(**kwargs)
+    self._target_idx = self.sys.body.index['target']
+    self.coef = reacher_coef(self.sys.config, self.sys.body.index,
+                             angle=self.kind == 11)
+    self._set_sizes()
+
+  def reset_batch(self, rng, batch_size, env_offset=None):
+    """reacher.py:172-186: default angles + U[-.1, .1), velocities
+    U[-.005, .005), a target at U[0, .2) (sqrt for ReacherAngle) x the unit
+    circle, z = .01; keyed by (rng, global env id)."""
+    B = int(batch_size)
+    off = self.env_offset if env_offset is None else int(env_offset)
+    seed = key_to_seed(rng)
+    D = self.sys.num_joint_dof
+    dev = self.sys.device
+    noise = _uniform((B, 2 * D + 2), seed, off * (2 * D + 2), 0., 1., dev)
+    qpos = self.sys.default_angle().reshape(1, -1) + (noise[:, :D] * .2 - .1)
+    qvel = noise[:, D:2 * D] * .01 - .005
+    u = noise[:, 2 * D:]
+    dist = .2 * (torch.sqrt(u[:, 0]) if self.target_sqrt else u[:, 0])
+    ang = math.pi * 2. * u[:, 1]
+    target = torch.stack([dist * torch.cos(ang), dist * torch.sin(ang),
+                          torch.full_like(dist, .01)], -1)
+    return self.reset_from(qpos, qvel, target)
+
+  def reset_from(self, joint_angle, joint_velocity, target=None):
+    qp = self.sys.default_qp(joint_angle=joint_angle, joint_velocity=joint_velocity)
+    if target is not None:
+      qp.pos[:, self._target_idx] = torch.as_tensor(target, dtype=torch.float32,
+                                                    device=self.sys.device)
+    return self._state(qp)
+
+
+class ReacherAngle(Reacher):
+  """`brax/envs/reacherangle.py`: Angle actuators driven by [-1, 1] actions
+  mapped onto the joint limits."""
+  kind = 11  # BX_ENV_REACHERANGLE
+  config = robots.REACHERANGLE_CONFIG
+  spring_config = robots.REACHERANGLE_SPRING_CONFIG
+  metric_keys = ('rewardCtrl', 'rewardDist')
+  target_sqrt = True
+
+
+class Swimmer(_KernelTask):
+  """A three-segment swimmer in a viscous fluid (`brax/envs/swimmer.py`)."""
+  kind = 12  # BX_ENV_SWIMMER
+  config = robots.SWIMMER_CONFIG
+  spring_config = robots.SWIMMER_SPRING_CONFIG
+  # sorted (swimmer.py:204-213)
+  metric_keys = ('distance_from_origin', 'forward_reward', 'reward_ctrl', 'reward_fwd',
+                 'x_position', 'x_velocity', 'y_position', 'y_velocity')
+
+  def __init__(self, forward_reward_weight=1.0, ctrl_cost_weight=1e-4, reset_noise_scale=0.1,
+               exclude_current_positions_from_observation=True, legacy_reward=False, **kwargs):
+    # legacy_reward is accepted and unused, as in the reference (swimmer.py:158)
+    del legacy_reward
+    super().__init__(**kwargs)
+    self.reset_noise_scale = reset_noise_scale
+    self.coef = swimmer_coef(forward_reward_weight, ctrl_cost_weight)
+    from brax_amd import abi
+    self.obs_flags = 0 if exclude_current_positions_from_observation else abi.OBS_XY
+    self._set_sizes()
+
+  @property
+  def action_size(self):
+    return 2
+
+
+class Pusher(_KernelTask):
+  """A 7-dof arm pushing an object to a goal (`brax/envs/pusher.py`)."""
+  kind = 13  # BX_ENV_PUSHER
+  config = robots.PUSHER_CONFIG
+  metric_keys = ('reward_ctrl', 'reward_dist', 'reward_near')  # sorted (pusher.py:206)
+
+  def __init__(self, **kwargs):
+    super().__init__(**kwargs)
+    idx = self.sys.body.index
+    self._object_idx, self._goal_idx, self._table_idx = idx['object'], idx['goal'], idx['table']
+    self.coef = pusher_coef(idx)
+    self._set_sizes()
+
+  def reset_batch(self, rng, batch_size, env_offset=None):
+    """pusher.py:178-209: default angles; velocity noise U[-.005, .005) on
+    all but the last 4 dofs; the object at U[-.3, 0) x U[-.2, .2) scaled into
+    a .17 disc, 5 cm up; goal (.45, .05, .05); table at the origin."""
+    B = int(batch_size)
+    off = self.env_offset if env_offset is None else int(env_offset)
+    seed = key_to_seed(rng)
+    D = self.sys.num_joint_dof
+    dev = self.sys.device
+    u = _uniform((B, D + 2), seed, off * (D + 2), 0., 1., dev)
+    qvel = torch.zeros((B, D), device=dev)
+    qvel[:, :D - 4] = u[:, :D - 4] * .01 - .005
+    cyl = torch.stack([-.3 + .3 * u[:, D - 4], -.2 + .4 * u[:, D - 3], torch.zeros_like(u[:, 0])],
+                      -1)
+    norm = torch.linalg.norm(cyl, dim=-1, keepdim=True)
+    scale = torch.where(norm > .17, .17 / norm, torch.ones_like(norm))
+    obj = scale * cyl + torch.tensor([0., 0., .05], device=dev)
+    qpos = self.sys.default_angle().reshape(1, -1).expand(B, -1)
+    return self.reset_from(qpos, qvel, object_pos=obj)
+
+  def reset_from(self, joint_angle, joint_velocity, object_pos=None):
+    """Reset state from explicit joint angles / velocities and the object's
+    position (pusher.py:196-201: goal and table placed as the reference)."""
+    qp = self.sys.default_qp(joint_angle=joint_angle, joint_velocity=joint_velocity)
+    dev = self.sys.device
+    qp.pos[:, self._goal_idx] = torch.tensor([0.45, 0.05, 0.05], device=dev)
+    if object_pos is not None:
+      qp.pos[:, self._object_idx] = torch.as_tensor(object_pos, dtype=torch.float32, device=dev)
+    qp.pos[:, self._table_idx] = 0.
+    return self._state(qp)

@@ -123,208 +123,6 @@ def _replace_metrics(state, **kw):
   return m
 
 
-class Swimmer(TorchEnv):
-  """`brax/envs/swimmer.py:153-290`: viscous drag fed to the three Thrusters
-  through the action tail."""
-  config = robots.SWIMMER_CONFIG
-  spring_config = robots.SWIMMER_SPRING_CONFIG
-  metric_keys = ('reward_fwd', 'reward_ctrl', 'x_position', 'y_position',
-                 'distance_from_origin', 'x_velocity', 'y_velocity', 'forward_reward')
-
-  def __init__(self, forward_reward_weight=1.0, ctrl_cost_weight=1e-4, reset_noise_scale=0.1,
-               exclude_current_positions_from_observation=True, legacy_reward=False, **kwargs):
-    # legacy_reward is accepted and unused, as in the reference (swimmer.py:158)
-    del legacy_reward
-    super().__init__(**kwargs)
-    self._fw, self._cw = forward_reward_weight, ctrl_cost_weight
-    self.qpos_noise = self.qvel_noise = (-reset_noise_scale, reset_noise_scale)
-    self._exclude = exclude_current_positions_from_observation
-    viscosity, density = 0.1, 10.0
-    i0, i1, i2 = 0.17278759594743870, 3.5709436495803999, 3.5709436495803999
-    body_mass = 34.557519189487735
-    inertia = torch.tensor([i1 + i2 - i0, i0 + i1 - i2, i0 + i2 - i1], dtype=torch.float64)
-    inertia = torch.sqrt(inertia / (body_mass * 6))
-    self._spherical_drag = float(-3 * bm.PI * inertia.mean() * viscosity)
-    self._fix_drag = (0.5 * density * torch.stack([inertia[1] * inertia[2], inertia[0] * inertia[2],
-                                                   inertia[0] * inertia[1]])).float().to(self.dev)
-    D = self.sys.joints[0]._hi - self.sys.joints[0]._lo  # pylint: disable=protected-access
-    self.obs_size = (1 if self._exclude else 3) + D + 2 + 1 + D
-    self._mass = torch.as_tensor(self.sys.body.mass[:-1], dtype=torch.float32, device=self.dev)
-
-  @property
-  def action_size(self):
-    return 2
-
-  def _viscous_force(self, qp):
-    """`swimmer.py:246-255`."""
-    vel, rot = qp.vel[:, :-1], qp.rot[:, :-1]
-    force = vel * self._spherical_drag
-    lv = bm.rotate(vel, bm.quat_inv(rot))
-    # `force -= jp.diag(fix_drag * |v| * v)`: jp.diag of the (3 bodies, 3)
-    # matrix is its diagonal [d00, d11, d22], broadcast over every body's row
-    d = self._fix_drag * lv.abs() * lv
-    force = force - d.diagonal(dim1=1, dim2=2)[:, None, :]
-    force = bm.rotate(force, rot)
-    return torch.clamp(force, -5., 5.)
-
-  def _system_action(self, state, action):
-    force = self._viscous_force(state.qp)
-    return torch.cat([action, force.reshape(force.shape[0], -1)], -1)
-
-  def _center_of_mass(self, qp):
-    return (self._mass[None, :, None] * qp.pos[:, :-1]).sum(1) / self._mass.sum()
-
-  def _get_obs(self, qp, info):
-    ja, jv = self.sys.joints[0].angle_vel(qp)
-    ang_z = bm.quat_to_euler(qp.rot[:, 0])[:, 2:3]
-    qpos = [ang_z, ja] if self._exclude else [qp.pos[:, 0, :2], ang_z, ja]
-    qvel = [qp.vel[:, 0, :2], qp.ang[:, 0, 2:], jv]
-    return torch.cat(qpos + qvel, -1)
-
-  def _step(self, state, action, qp, info):
-    dt = float(self.sys.config.dt)
-    com_before = self._center_of_mass(state.qp)
-    com_after = self._center_of_mass(qp)
-    velocity = (com_after - com_before) / dt
-    forward_reward = self._fw * velocity[:, 0]
-    ctrl_cost = self._cw * (action * action).sum(-1)
-    obs = self._get_obs(qp, info)
-    reward = forward_reward - ctrl_cost
-    metrics = _replace_metrics(
-        state, reward_fwd=forward_reward, reward_ctrl=-ctrl_cost, x_position=com_after[:, 0],
-        y_position=com_after[:, 1], distance_from_origin=torch.linalg.norm(qp.pos[:, 0], dim=-1),
-        x_velocity=velocity[:, 0], y_velocity=velocity[:, 1], forward_reward=forward_reward)
-    return state.replace(qp=qp, obs=obs, reward=reward, metrics=metrics)
-
-
-class Reacher(TorchEnv):
-  """`brax/envs/reacher.py:150-236`."""
-  config = robots.REACHER_CONFIG
-  spring_config = robots.REACHER_SPRING_CONFIG
-  qpos_noise = (-.1, .1)
-  qvel_noise = (-.005, .005)
-  metric_keys = ('reward_dist', 'reward_ctrl')
-  target_sqrt = False  # ReacherAngle draws dist = .2 * sqrt(u)
-
-  def __init__(self, **kwargs):
-    super().__init__(**kwargs)
-    self._target_idx = self.sys.body.index['target']
-    self._arm_idx = self.sys.body.index['body1']
-    D = self.sys.joints[0]._hi - self.sys.joints[0]._lo  # pylint: disable=protected-access
-    self.obs_size = 2 * D + 2 + 2 + 3
-
-  def _reset_extra(self, seed, batch_size):
-    u = _uniform((2, batch_size), seed ^ 0x7A46E7, 0, 0., 1., self.dev)
-    dist = .2 * (torch.sqrt(u[0]) if self.target_sqrt else u[0])
-    ang = bm.PI * 2. * u[1]
-    target = torch.stack([dist * torch.cos(ang), dist * torch.sin(ang),
-                          torch.full_like(dist, .01)], -1)
-    return {'target': target}
-
-  def reset_from(self, joint_angle, joint_velocity, target=None, **extra):
-    return super().reset_from(joint_angle, joint_velocity, target=target, **extra)
-
-  def _reset_qp(self, qp, target=None):
-    if target is None:
-      return qp
-    pos = qp.pos.clone()
-    pos[:, self._target_idx] = torch.as_tensor(target, dtype=torch.float32, device=self.dev)
-    return QP(pos=pos, rot=qp.rot, vel=qp.vel, ang=qp.ang)
-
-  def _get_obs(self, qp, info):
-    ja, _ = self.sys.joints[0].angle_vel(qp)
-    target = qp.pos[:, self._target_idx]
-    tip_pos, tip_vel = qp[:, self._arm_idx].to_world(torch.tensor([0.11, 0., 0.], device=self.dev))
-    return torch.cat([torch.cos(ja), torch.sin(ja), target[:, :2], tip_vel[:, :2],
-                      tip_pos - target], -1)
-
-  def _step(self, state, action, qp, info):
-    obs = self._get_obs(qp, info)
-    reward_dist = -torch.linalg.norm(obs[:, -3:], dim=-1)
-    reward_ctrl = -(action * action).sum(-1)
-    metrics = _replace_metrics(state, reward_dist=reward_dist, reward_ctrl=reward_ctrl)
-    return state.replace(qp=qp, obs=obs, reward=reward_dist + reward_ctrl, metrics=metrics)
-
-
-class ReacherAngle(Reacher):
-  """`brax/envs/reacherangle.py:30-106`: [-1, 1] actions mapped onto the
-  joints' angle limits for the Angle actuators."""
-  config = robots.REACHERANGLE_CONFIG
-  spring_config = robots.REACHERANGLE_SPRING_CONFIG
-  metric_keys = ('rewardDist', 'rewardCtrl')
-  target_sqrt = True
-
-  def __init__(self, **kwargs):
-    super().__init__(**kwargs)
-    lim = [(l.min, l.max) for j in self.sys.config.joints for l in j.angle_limit]
-    self._min_act = torch.tensor([l[0] for l in lim], dtype=torch.float32, device=self.dev)
-    self._range_act = torch.tensor([l[1] - l[0] for l in lim], dtype=torch.float32,
-                                   device=self.dev)
-
-  def _system_action(self, state, action):
-    return self._min_act + self._range_act * ((action + 1) / 2.)
-
-  def _step(self, state, action, qp, info):
-    obs = self._get_obs(qp, info)
-    reward_dist = -torch.linalg.norm(obs[:, -3:], dim=-1)
-    metrics = {'rewardDist': reward_dist, 'rewardCtrl': torch.zeros_like(reward_dist)}
-    return state.replace(qp=qp, obs=obs, reward=reward_dist, metrics=metrics)
-
-
-class Pusher(TorchEnv):
-  """`brax/envs/pusher.py:170-242`: rewards from the state BEFORE the step."""
-  config = robots.PUSHER_CONFIG
-  metric_keys = ('reward_dist', 'reward_ctrl', 'reward_near')
-
-  def __init__(self, **kwargs):
-    super().__init__(**kwargs)
-    idx = self.sys.body.index
-    self._object_idx, self._tips_arm_idx = idx['object'], idx['r_wrist_roll_link']
-    self._goal_idx, self._table_idx = idx['goal'], idx['table']
-    self._goal_pos = torch.tensor([0.45, 0.05, 0.05], device=self.dev)
-    D = self.sys.joints[0]._hi - self.sys.joints[0]._lo  # pylint: disable=protected-access
-    self.obs_size = 2 * D + 9
-
-  def reset_batch(self, rng, batch_size):
-    """`pusher.py:178-209`: the arm starts at its default angles with
-    velocity noise on all but the last 4 dofs; the object is placed in a disc."""
-    seed = key_to_seed(rng)
-    D = self.sys.num_joint_dof
-    u = _uniform((3, batch_size), seed ^ 0x51E0, 0, 0., 1., self.dev)
-    cyl = torch.stack([-0.3 + 0.3 * u[0], -0.2 + 0.4 * u[1], torch.zeros_like(u[0])], -1)
-    qpos = self.sys.default_angle().reshape(1, -1).expand(batch_size, -1)
-    qvel = torch.zeros((batch_size, D), device=self.dev)
-    qvel[:, :D - 4] = _uniform((batch_size, D - 4), seed, 0, -0.005, 0.005, self.dev)
-    return self.reset_from(qpos, qvel, cylinder=cyl)
-
-  def _reset_qp(self, qp, cylinder=None):
-    pos = qp.pos.clone()
-    pos[:, self._goal_idx] = self._goal_pos
-    if cylinder is not None:
-      cylinder = torch.as_tensor(cylinder, dtype=torch.float32, device=self.dev)
-      norm = torch.linalg.norm(cylinder, dim=-1, keepdim=True)
-      scale = torch.where(norm > .17, .17 / norm, torch.ones_like(norm))
-      pos[:, self._object_idx] = scale * cylinder + torch.tensor([0., 0., .05], device=self.dev)
-    pos[:, self._table_idx] = 0.
-    return QP(pos=pos, rot=qp.rot, vel=qp.vel, ang=qp.ang)
-
-  def _get_obs(self, qp, info):
-    ja, jv = self.sys.joints[0].angle_vel(qp)
-    return torch.cat([ja, jv, qp.pos[:, self._tips_arm_idx], qp.pos[:, self._object_idx],
-                      qp.pos[:, self._goal_idx]], -1)
-
-  def _step(self, state, action, qp, info):
-    p0 = state.qp.pos
-    reward_near = -torch.linalg.norm(p0[:, self._object_idx] - p0[:, self._tips_arm_idx], dim=-1)
-    reward_dist = -torch.linalg.norm(p0[:, self._object_idx] - p0[:, self._goal_idx], dim=-1)
-    reward_ctrl = -(action * action).sum(-1)
-    obs = self._get_obs(qp, info)
-    reward = reward_dist + 0.1 * reward_ctrl + 0.5 * reward_near
-    metrics = _replace_metrics(state, reward_near=reward_near, reward_dist=reward_dist,
-                               reward_ctrl=reward_ctrl)
-    return state.replace(qp=qp, obs=obs, reward=reward, metrics=metrics)
-
-
 def _contacts(info, n):
   """`jp.where(sum(contact.vel^2) > 1e-5, 1, 0)` per body (grasp.py:163-164)."""
   if info is None:

@@ -301,6 +301,18 @@ def env_traj(env, name, n_envs, n_steps, act_seed_base=10_000):
       _, r1, r2 = jp.random_split(rng, 3)
       qpos_l.append(env.sys.default_angle() + env._noise(r1))
       qvel_l.append(env._noise(r2))
+    elif name in ('reacher', 'reacherangle'):
+      # reacher.py:172-176 / reacherangle.py:60-64 draw their noise inline
+      _, r1, r2 = jp.random_split(rng, 3)
+      D = env.sys.num_joint_dof
+      qpos_l.append(env.sys.default_angle() + jp.random_uniform(r1, (D,), -.1, .1))
+      qvel_l.append(jp.random_uniform(r2, (D,), -.005, .005))
+    elif name == 'pusher':
+      # pusher.py:178-195: default angles, velocity noise on all but 4 dofs
+      _, _, r2 = jp.random_split(rng, 3)
+      D = env.sys.num_joint_dof
+      qpos_l.append(env.sys.default_angle())
+      qvel_l.append(np.concatenate([jp.random_uniform(r2, (D - 4,), -0.005, 0.005), np.zeros(4)]))
     elif name == 'acrobot':
       # acrobot.py:56-61 draws the same U[-.01, .01) noise inline
       _, r1, r2 = jp.random_split(rng, 3)

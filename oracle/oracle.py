@@ -19,7 +19,7 @@ LIB = os.path.join(HERE, '_build', 'liboracle.so')
 
 ENV_KIND = {'none': 0, 'ant': 1, 'humanoid': 2, 'halfcheetah': 3, 'humanoidstandup': 4,
             'hopper': 5, 'walker2d': 6, 'inverted_pendulum': 7, 'inverted_double_pendulum': 8,
-            'acrobot': 9}
+            'acrobot': 9, 'reacher': 10, 'reacherangle': 11, 'swimmer': 12, 'pusher': 13}
 
 
 def build():
@@ -108,21 +108,30 @@ class Oracle:
     self._fn('oracle_system_info')(C.byref(self.cdesc), C.c_int64(B), _p(qp), _p(ic))
     return ic
 
-  def env_obs(self, kind, qp, info_contact, act, obs_size, obs_flags=0):
+  @staticmethod
+  def _coef(coef):
+    if coef is None:
+      return None, None
+    c = np.ascontiguousarray(np.asarray(coef, np.float64).reshape(8))
+    return c, c.ctypes.data_as(C.POINTER(C.c_double))
+
+  def env_obs(self, kind, qp, info_contact, act, obs_size, obs_flags=0, coef=None):
     qp = self._a(qp)
     B = qp.shape[0]
     ic = self._a(info_contact)
     act = self._a(act).reshape(B, -1)
     self._width(act)
     obs = np.empty((B, obs_size), self.dtype)
+    keep, cp = self._coef(coef)
     rc = self._fn('oracle_env_obs')(C.byref(self.cdesc), C.c_int(ENV_KIND[kind] | obs_flags << 8),
                                     C.c_int64(B), _p(qp), _p(ic), _p(act), _p(obs),
-                                    C.c_int(obs_size))
+                                    C.c_int(obs_size), cp)
+    del keep
     if rc:
       raise ValueError('obs size mismatch')
     return obs
 
-  def env_step(self, kind, qp, act, obs_size, n_metrics, done=None, obs_flags=0):
+  def env_step(self, kind, qp, act, obs_size, n_metrics, done=None, obs_flags=0, coef=None):
     """obs_flags: BX_OBS_XY for exclude_current_positions_from_observation=False."""
     qp = self._a(qp)
     B = qp.shape[0]
@@ -133,10 +142,12 @@ class Oracle:
     rew = np.empty(B, self.dtype)
     dn = self._a(np.zeros(B) if done is None else done).copy()
     met = np.zeros((B, n_metrics), self.dtype)
+    keep, cp = self._coef(coef)
     rc = self._fn('oracle_env_step')(C.byref(self.cdesc), C.c_int(ENV_KIND[kind] | obs_flags << 8),
                                      C.c_int64(B), _p(qp), _p(act), _p(out), _p(obs),
                                      C.c_int(obs_size), _p(rew), _p(dn), _p(met),
-                                     C.c_int(n_metrics))
+                                     C.c_int(n_metrics), cp)
+    del keep
     if rc:
       raise ValueError('obs size mismatch')
     return out, obs, rew, dn, met

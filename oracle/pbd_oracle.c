@@ -2026,6 +2026,56 @@ static int obs_pendulums(const sysc* s, int kind, const body_t* qp, R* obs, R* a
   return n;
 }
 
+/* math.quat_to_euler(q)[2] (math.py:80-91) */
+static R euler_z(const R* q) {
+  R y = (R)-2 * q[1] * q[2] + (R)2 * q[0] * q[3];
+  R x = q[1] * q[1] + q[0] * q[0] - q[3] * q[3] - q[2] * q[2];
+  return (R)atan2((double)y, (double)x);
+}
+
+/* the reachers' arm tip: body arm's (.11, 0, 0) via QP.to_world (base.py:112-126) */
+static void arm_tip(const body_t* qp, int arm, R* tp, R* tv) {
+  const R off0[3] = {(R)0.11, 0, 0};
+  R off[3], w[3];
+  rotate(off0, qp[arm].rot, off);
+  cross3(qp[arm].ang, off, w);
+  for (int k = 0; k < 3; k++) { tp[k] = qp[arm].pos[k] + off[k]; tv[k] = qp[arm].vel[k] + w[k]; }
+}
+
+/* Reacher(Angle) / Swimmer / Pusher._get_obs (reacher.py:205-224,
+ * swimmer.py:257-272, pusher.py:232-242); coef = bx_env_params.coef */
+static int obs_task(const sysc* s, int kind, const body_t* qp, const double* coef, R* obs, int xy) {
+  int n = 0;
+  R ang[64], vel[64];
+  int nd = angle_vel(s, qp, ang, vel);
+  if (kind == BX_ENV_REACHER || kind == BX_ENV_REACHERANGLE) {
+    int tg = (int)coef[0], arm = (int)coef[1];
+    for (int i = 0; i < nd; i++) obs[n++] = (R)cos((double)ang[i]);
+    for (int i = 0; i < nd; i++) obs[n++] = (R)sin((double)ang[i]);
+    obs[n++] = qp[tg].pos[0];
+    obs[n++] = qp[tg].pos[1];
+    R tp[3], tv[3];
+    arm_tip(qp, arm, tp, tv);
+    obs[n++] = tv[0];
+    obs[n++] = tv[1];
+    for (int k = 0; k < 3; k++) obs[n++] = tp[k] - qp[tg].pos[k];
+  } else if (kind == BX_ENV_SWIMMER) {
+    if (xy) { obs[n++] = qp[0].pos[0]; obs[n++] = qp[0].pos[1]; }
+    obs[n++] = euler_z(qp[0].rot);
+    for (int i = 0; i < nd; i++) obs[n++] = ang[i];
+    obs[n++] = qp[0].vel[0];
+    obs[n++] = qp[0].vel[1];
+    obs[n++] = qp[0].ang[2];
+    for (int i = 0; i < nd; i++) obs[n++] = vel[i];
+  } else if (kind == BX_ENV_PUSHER) {
+    for (int i = 0; i < nd; i++) obs[n++] = ang[i];
+    for (int i = 0; i < nd; i++) obs[n++] = vel[i];
+    for (int j = 0; j < 3; j++)
+      for (int k = 0; k < 3; k++) obs[n++] = qp[(int)coef[j]].pos[k];
+  }
+  return n;
+}
+
 /* Humanoid._center_of_mass (humanoid.py:336-338): bodies [:-1] */
 static void humanoid_com(const sysc* s, const body_t* qp, R* com) {
   R m = 0;
@@ -2090,9 +2140,13 @@ static int obs_humanoid(const sysc* s, const body_t* qp, const R* act, R* obs, i
 }
 
 int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const R* info_c,
-                       const R* act, R* obs, int obs_size) {
+                       const R* act, R* obs, int obs_size, const double* coef) {
   sysc s;
   sys_init(&s, d);
+  if ((kind & 0xFF) >= BX_ENV_REACHER && (kind & 0xFF) <= BX_ENV_PUSHER && !coef) {
+    sys_free(&s);
+    return -2;
+  }
   int N = s.N;
   int rc = 0;
   const int xy = (kind >> 8) & BX_OBS_XY; /* kind | obs_flags << 8 */
@@ -2111,7 +2165,8 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
       else if (kind >= BX_ENV_INVERTED_PENDULUM && kind <= BX_ENV_ACROBOT) {
         R ang[64], vel[64];
         n = obs_pendulums(&s, kind, q, obs + e * obs_size, ang, vel);
-      }
+      } else if (kind >= BX_ENV_REACHER && kind <= BX_ENV_PUSHER)
+        n = obs_task(&s, kind, q, coef, obs + e * obs_size, xy);
       else if (kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP)
         n = obs_humanoid(&s, q, act + e * s.aw, obs + e * obs_size, xy);
       if (n != obs_size) rc = -1;
@@ -2126,13 +2181,20 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
  * half_cheetah.py:178-197). done_io is read (HalfCheetah keeps it) and written. */
 int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, const R* act,
                         R* qp_out, R* obs, int obs_size, R* reward, R* done_io,
-                        R* metrics, int n_metrics) {
+                        R* metrics, int n_metrics, const double* coef) {
   sysc s;
   sys_init(&s, d);
   int N = s.N, Rn = s.Rn, A = s.aw;
   int rc = 0;
   const int xy = (kind >> 8) & BX_OBS_XY; /* kind | obs_flags << 8 */
   kind &= 0xFF;
+  if (kind >= BX_ENV_REACHER && kind <= BX_ENV_PUSHER && !coef) {
+    sys_free(&s);
+    return -2;
+  }
+  /* Swimmer appends its drag forces to the action (swimmer.py:218-220): the
+   * System.step reads A + 9 values, clipped at that width */
+  if (kind == BX_ENV_SWIMMER) s.aw = A + 9;
 #pragma omp parallel
   {
     work_t w;
@@ -2145,7 +2207,33 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
       const R* a = act + e * A;
       load_qp(w.qp, qp_in + e * 13 * N, N);
       memcpy(q0, w.qp, sizeof(body_t) * N);
-      step_env(&s, &w, a, ra, rb);
+      /* the action System.step reads */
+      R xa[64];
+      const R* sa = a;
+      if (kind == BX_ENV_REACHERANGLE) {
+        /* reacherangle.py:79: min + range * (a + 1) / 2 */
+        for (int i = 0; i < A; i++) xa[i] = (R)coef[2 + i] + (R)coef[4 + i] * ((a[i] + 1) / 2);
+        sa = xa;
+      } else if (kind == BX_ENV_SWIMMER) {
+        /* swimmer.py:246-255, jp.diag keeping D00, D11, D22 for every segment */
+        R D[3];
+        for (int b = 0; b < 3; b++) {
+          const R qi[4] = {q0[b].rot[0], -q0[b].rot[1], -q0[b].rot[2], -q0[b].rot[3]};
+          R lv[3];
+          rotate(q0[b].vel, qi, lv);
+          D[b] = (R)coef[3 + b] * (R)fabs((double)lv[b]) * lv[b];
+        }
+        for (int i = 0; i < A; i++) xa[i] = a[i];
+        for (int b = 0; b < 3; b++) {
+          R f[3], fw[3];
+          for (int k = 0; k < 3; k++) f[k] = q0[b].vel[k] * (R)coef[2] - D[k];
+          rotate(f, q0[b].rot, fw);
+          for (int k = 0; k < 3; k++)
+            xa[A + 3 * b + k] = fw[k] < (R)-5 ? (R)-5 : (fw[k] > (R)5 ? (R)5 : fw[k]);
+        }
+        sa = xa;
+      }
+      step_env(&s, &w, sa, ra, rb);
       store_qp(w.qp, qp_out + e * 13 * N, N);
       R* o = obs + e * obs_size;
       R* m = metrics + e * n_metrics;
@@ -2246,6 +2334,41 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
           /* sorted: alive_bonus, dist_penalty, r_tot, vel_penalty */
           m[0] = 0; m[1] = dist; m[2] = r; m[3] = velp;
         }
+      } else if (kind == BX_ENV_REACHER || kind == BX_ENV_REACHERANGLE) {
+        n = obs_task(&s, kind, w.qp, coef, o, xy);
+        R rd = -norm3(o + n - 3);  /* obs[-3:] = tip - target */
+        if (kind == BX_ENV_REACHER) {
+          R rc2 = -sq;
+          reward[e] = rd + rc2;
+          m[0] = rc2; m[1] = rd;  /* sorted: reward_ctrl, reward_dist */
+        } else {
+          reward[e] = rd;
+          m[0] = 0; m[1] = rd;    /* sorted: rewardCtrl, rewardDist */
+        }
+      } else if (kind == BX_ENV_SWIMMER) {
+        n = obs_task(&s, kind, w.qp, coef, o, xy);
+        R cb[3], ca[3], v[3];
+        humanoid_com(&s, q0, cb);
+        humanoid_com(&s, w.qp, ca);
+        for (int k = 0; k < 3; k++) v[k] = (ca[k] - cb[k]) / dt;
+        R fwd = (R)coef[0] * v[0];
+        R ctrl = (R)coef[1] * sq;
+        reward[e] = fwd - ctrl;
+        /* done unchanged; sorted: distance_from_origin, forward_reward,
+         * reward_ctrl, reward_fwd, x_position, x_velocity, y_position, y_velocity */
+        m[0] = norm3(w.qp[0].pos); m[1] = fwd; m[2] = -ctrl; m[3] = fwd;
+        m[4] = ca[0]; m[5] = v[0]; m[6] = ca[1]; m[7] = v[1];
+      } else if (kind == BX_ENV_PUSHER) {
+        n = obs_task(&s, kind, w.qp, coef, o, xy);
+        R v1[3], v2[3];
+        int tip = (int)coef[0], obj = (int)coef[1], goal = (int)coef[2];
+        for (int k = 0; k < 3; k++) {
+          v1[k] = q0[obj].pos[k] - q0[tip].pos[k];
+          v2[k] = q0[obj].pos[k] - q0[goal].pos[k];
+        }
+        R near = -norm3(v1), dist = -norm3(v2), rc2 = -sq;
+        reward[e] = dist + (R)0.1 * rc2 + (R)0.5 * near;
+        m[0] = rc2; m[1] = dist; m[2] = near;  /* sorted: ctrl, dist, near */
       } else if (kind == BX_ENV_HUMANOID_STANDUP) {
         /* humanoid_standup.py:232-247; done unchanged; sorted metrics:
          * reward_linup, reward_quadctrl */

@@ -48,7 +48,39 @@ XY_ENVS = ['ant_xy', 'humanoid_xy', 'halfcheetah_xy']
 
 # kernel env kinds whose reference rollouts are the envtraj_* goldens (the
 # env-layer rollouts of oracle/gen_golden.py) rather than traj_*
-ENVTRAJ_KERNEL = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum', 'acrobot']
+ENVTRAJ_KERNEL = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum', 'acrobot',
+                  'reacher', 'reacherangle', 'swimmer', 'pusher']
+# bodies a kernel env's reset places after default_qp (reacher.py:177-179,
+# pusher.py:196-201): name -> body names
+
+
+def reset_bodies(name):
+  return {'reacher': ['target'], 'reacherangle': ['target'],
+          'pusher': ['goal', 'object', 'table']}.get(name, [])
+
+
+def env_coef(name):
+  """bx_env_params.coef of a kernel env with its constructor defaults, built
+  on the CPU (None: the oracle's built-in defaults apply)."""
+  from brax_amd.envs import tasks
+  if name in ('reacher', 'reacherangle'):
+    cfg = config_for(name)
+    return tasks.reacher_coef(cfg, compiled(name)[3]['body_index'], angle=name == 'reacherangle')
+  if name == 'swimmer':
+    return tasks.swimmer_coef()
+  if name == 'pusher':
+    return tasks.pusher_coef(compiled(name)[3]['body_index'])
+  return None
+
+
+def golden_reset_qp(name, o, T):
+  """The oracle's default_qp of the golden reset angles, with the bodies the
+  env's reset places copied from the golden's reset state."""
+  qp0 = o.default_qp(T['reset_qpos'], T['reset_qvel'])
+  idx = [compiled(name)[3]['body_index'][b] for b in reset_bodies(name)]
+  for b in idx:
+    qp0[:, b, 0:3] = T['qp'][0][:, b, 0:3]
+  return qp0
 
 
 def env_golden(name):

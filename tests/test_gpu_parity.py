@@ -23,8 +23,8 @@ import torch
 from tests.conftest import golden
 from tests.margins import record_margin
 from tests.helpers import (CAPSULES, ENVTRAJ_KERNEL, POINTS, QP_FIELDS, ROBOTS, SPRING_ENVS,
-                           SPRING_ROBOTS, XCOL, XY_ENVS, compiled, env_golden, env_kind, normwise,
-                           obs_flags)
+                           SPRING_ROBOTS, XCOL, XY_ENVS, compiled, env_golden, env_kind,
+                           golden_reset_qp, normwise, obs_flags, reset_bodies)
 
 pytestmark = pytest.mark.gpu
 
@@ -85,9 +85,9 @@ class Envelope:
   def system(self, qp, act):
     return [o.system_step(q, act.astype(np.float32)) for o in self.os for q in self._inputs(qp)]
 
-  def env(self, name, qp, act, O, M, flags=0):
-    return [o.env_step(name, q, act.astype(np.float32), O, M, obs_flags=flags) for o in self.os
-            for q in self._inputs(qp)]
+  def env(self, name, qp, act, O, M, flags=0, coef=None):
+    return [o.env_step(name, q, act.astype(np.float32), O, M, obs_flags=flags, coef=coef)
+            for o in self.os for q in self._inputs(qp)]
 
 
 def _make_env(name, dev, **kw):
@@ -172,7 +172,7 @@ def test_env_step_vs_golden(dev, oracle_lib, name):
                reward=torch.zeros(B, device=dev), done=torch.zeros(B, device=dev))
     act = torch.as_tensor(T['action'][t], dtype=torch.float32, device=dev)
     nst = env.step(st, act)
-    outs = env32.env(env_kind(name), T['qp'][t], T['action'][t], O, M, fl)
+    outs = env32.env(env_kind(name), T['qp'][t], T['action'][t], O, M, fl, env.coef)
     _gate(nst.obs.cpu().numpy(), T['obs'][t + 1], _env_err([o[1] for o in outs], T['obs'][t + 1]),
           'obs')
     _gate(nst.reward.cpu().numpy()[:, None], T['reward'][t][:, None],
@@ -194,18 +194,26 @@ def test_reset_vs_golden(dev, oracle_lib, name):
   observation and the state are held to 1e-5."""
   env = _make_env(name, dev)
   T = golden(env_golden(name))
+  # the bodies the env's reset places (reacher target, pusher object) at the
+  # golden's reset positions
+  extra = {}
+  placed = reset_bodies(name)
+  if placed:
+    bi = compiled(name)[3]['body_index']
+    key = 'target' if 'target' in placed else 'object'
+    extra = {key if key == 'target' else 'object_pos': T['qp'][0][:, bi[key], 0:3]}
   st = env.reset_from(torch.as_tensor(T['reset_qpos'], dtype=torch.float32, device=dev),
-                      torch.as_tensor(T['reset_qvel'], dtype=torch.float32, device=dev))
+                      torch.as_tensor(T['reset_qvel'], dtype=torch.float32, device=dev), **extra)
   got = _qp_np(st.qp)
   for f, sl in QP_FIELDS.items():
     nw = normwise(got[..., sl], T['qp'][0][..., sl])
     assert nw.max() <= 1e-5, (f, nw.max())
   vc, d, rd, meta = compiled(name)
   o32 = oracle_lib.Oracle(d, rd, np.float32, safe_guard=True)
-  q32 = o32.default_qp(T['reset_qpos'], T['reset_qvel'])
+  q32 = golden_reset_qp(name, o32, T)
   B = q32.shape[0]
   obs32 = o32.env_obs(env_kind(name), q32, o32.system_info(q32), np.zeros((B, o32.A)),
-                      T['obs'].shape[-1], obs_flags=obs_flags(name))
+                      T['obs'].shape[-1], obs_flags=obs_flags(name), coef=env.coef)
   obs = st.obs.cpu().numpy()
   _gate(obs, T['reset_obs'], normwise(obs32, T['reset_obs']), 'obs')
   n_state = (1 + 4 + 2 * meta['num_joint_dof'] + 6 + 2 * obs_flags(name)

@@ -10,7 +10,7 @@ import pytest
 
 from tests.conftest import golden
 from tests.helpers import (CAPSULES, ENVTRAJ_KERNEL, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS,
-                           XCOL, XY_ENVS, env_golden,
+                           XCOL, XY_ENVS, env_coef, env_golden, golden_reset_qp,
                            compiled, env_kind, obs_flags)
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
@@ -84,7 +84,7 @@ def test_env_step_matches_reference(oracle_lib, name):
   O, M = T['obs'].shape[-1], T['metrics'].shape[-1]
   for t in range(T['action'].shape[0]):
     _, obs, rew, done, met = o.env_step(env_kind(name), T['qp'][t], T['action'][t], O, M,
-                                        obs_flags=obs_flags(name))
+                                        obs_flags=obs_flags(name), coef=env_coef(name))
     assert np.abs(obs - T['obs'][t + 1]).max() < 1e-9
     assert np.abs(rew - T['reward'][t]).max() < 1e-12
     assert np.array_equal(done, T['done'][t])
@@ -96,12 +96,12 @@ def test_env_step_matches_reference(oracle_lib, name):
 def test_reset_matches_reference(oracle_lib, name):
   o = _oracle(oracle_lib, name)
   T = golden(env_golden(name))
-  qp0 = o.default_qp(T['reset_qpos'], T['reset_qvel'])
+  qp0 = golden_reset_qp(name, o, T)
   assert np.abs(qp0 - T['qp'][0]).max() < 1e-12
   ic = o.system_info(qp0)
   B = qp0.shape[0]
   obs = o.env_obs(env_kind(name), qp0, ic, np.zeros((B, o.A)), T['obs'].shape[-1],
-                  obs_flags=obs_flags(name))
+                  obs_flags=obs_flags(name), coef=env_coef(name))
   assert np.abs(obs - T['reset_obs']).max() < 1e-12
 
 
