@@ -85,7 +85,7 @@ class BxInfo(C.Structure):
 class BxEnvState(C.Structure):
   _fields_ = [('qp', BxQP), ('obs', C.c_void_p), ('reward', C.c_void_p),
               ('done', C.c_void_p), ('metrics', C.c_void_p),
-              ('steps', C.c_void_p), ('truncation', C.c_void_p)]
+              ('steps', C.c_void_p), ('truncation', C.c_void_p), ('rng', C.c_void_p)]
 
 
 class BxEnvParams(C.Structure):

@@ -584,6 +584,12 @@ int env_sizes(const bx_system* S, const bx_env_params* P, int* obs, int* met) {
       *obs = 2 * D + 9;
       *met = 3;
       return 0;
+    case BX_ENV_UR5E:
+    case BX_ENV_FETCH:  // fwd, up, |target|, target dir, local pos, local vel, contacts
+      if (xy) return fail("this env has no current-position observation option");
+      *obs = 10 + 7 * N;
+      *met = P->kind == BX_ENV_UR5E ? 3 : 5;
+      return 0;
     case BX_ENV_HALFCHEETAH:
       *obs = 3 + D + 3 + D + (xy ? 1 : 0);
       *met = 4;
@@ -754,6 +760,8 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   if (!in->done || !out->done || !out->reward || !out->obs) return fail("null env buffer");
   if (env->auto_reset && (!qp_ok(env->first_qp) || !env->first_obs))
     return fail("auto_reset needs first_qp and first_obs");
+  if ((env->kind == BX_ENV_UR5E || env->kind == BX_ENV_FETCH) && (!in->rng || !out->rng))
+    return fail("the target envs need the per-env rng stream (in and out)");
   if (env->episode_length > 0 && (!out->steps || !out->truncation))
     return fail("episode wrapper needs steps and truncation buffers");
   EnvArgs a{};

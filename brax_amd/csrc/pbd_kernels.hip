@@ -2609,6 +2609,16 @@ __device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3
 }
 
 // observation element i of the env kind
+// counter-based uniform: splitmix64 of (seed, global index) -> [lo, hi)
+__device__ __forceinline__ float uniform_at(uint64_t seed, uint64_t i, float lo, float hi) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + i + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  float u = (float)(z >> 40) * (1.0f / 16777216.0f);
+  return lo + (hi - lo) * u;
+}
+
 // the arm tip of the reachers: body coef[1]'s (.11, 0, 0) in the world and
 // its velocity (QP.to_world, base.py:112-126)
 __device__ __forceinline__ void arm_tip(const Env& E, const float* coef, v3& tp, v3& tv) {
@@ -2712,6 +2722,40 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
     if (i == 2) return q0[12];
     i -= 3;
     return E.ang[D + i];
+  }
+  if (kind == BX_ENV_UR5E || kind == BX_ENV_FETCH) {
+    // ur5e.py:115-135 / fetch.py:101-121, egocentric in the torso's frame:
+    // [torso fwd, torso up, |target|, target dir, local pos (N x 3), local
+    // vel (N x 3), contact flags (N: |Info contact vel|^2 > 1e-5)]
+    const float* t = E.qp + (int)coef[0] * QP_STRIDE;
+    const q4 tr{t[3], t[4], t[5], t[6]};
+    if (i < 3) { v3 f = rotate(mk(1.f, 0.f, 0.f), tr); return i == 0 ? f.x : (i == 1 ? f.y : f.z); }
+    i -= 3;
+    if (i < 3) { v3 u = rotate(mk(0.f, 0.f, 1.f), tr); return i == 0 ? u.x : (i == 1 ? u.y : u.z); }
+    i -= 3;
+    const q4 ti = quat_inv(tr);
+    if (i < 4) {
+      v3 tl = rotate(ld3(E.qp + (int)coef[1] * QP_STRIDE) - ld3(t), ti);
+      float mag = norm(tl);
+      if (i == 0) return mag;
+      v3 d = tl / (1e-6f + mag);
+      return i == 1 ? d.x : (i == 2 ? d.y : d.z);
+    }
+    i -= 4;
+    if (i < 3 * N) {
+      const int b = i / 3;
+      v3 l = rotate(ld3(E.qp + b * QP_STRIDE) - ld3(t), ti);
+      return i % 3 == 0 ? l.x : (i % 3 == 1 ? l.y : l.z);
+    }
+    i -= 3 * N;
+    if (i < 3 * N) {
+      const int b = i / 3;
+      v3 l = rotate(ld3(E.qp + b * QP_STRIDE + 7), ti);
+      return i % 3 == 0 ? l.x : (i % 3 == 1 ? l.y : l.z);
+    }
+    i -= 3 * N;
+    const float* cv = E.acc + i * ACC_STRIDE + ACC_ICV;
+    return cv[0] * cv[0] + cv[1] * cv[1] + cv[2] * cv[2] > 0.00001f ? 1.f : 0.f;
   }
   if (kind == BX_ENV_PUSHER) {
     // pusher.py:232-242: [joint angles, joint vels, tip, object, goal positions]
@@ -2984,6 +3028,9 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
     v3 com0 = mk(0.f, 0.f, 0.f);
     float msum = 0.f;
     if (kind == BX_ENV_HUMANOID || kind == BX_ENV_SWIMMER) humanoid_com(c, H, E.qp, com0, msum);
+    // the target envs' torso before the step (red words 36..38)
+    if ((kind == BX_ENV_UR5E || kind == BX_ENV_FETCH) && lane == 0)
+      st3(E.red + 36, ld3(E.qp + (int)P.coef[0] * QP_STRIDE));
     // Pusher's rewards come from the state before the step (pusher.py:212-217)
     float near0 = 0.f, dist0 = 0.f;
     if (kind == BX_ENV_PUSHER) {
@@ -3157,6 +3204,45 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
           m[0] = norm(p1); m[1] = fwd; m[2] = -ctrl; m[3] = fwd;
           m[4] = com1.x; m[5] = v.x; m[6] = com1.y; m[7] = v.y;
         }
+      } else if (kind == BX_ENV_UR5E || kind == BX_ENV_FETCH) {
+        // ur5e.py:82-101 / fetch.py:58-99 (done as it came in); a hit target
+        // moves to a fresh spot drawn from the env's stream (after the obs)
+        const int ti = (int)P.coef[0], gi = (int)P.coef[1];
+        v3 t1 = ld3(E.qp + ti * QP_STRIDE);
+        v3 delta = t1 - ld3(E.red + 36);  // torso before the step
+        v3 rel = ld3(E.qp + gi * QP_STRIDE) - t1;
+        float dist = norm(rel);
+        v3 dir = rel / (1e-6f + dist);
+        float moving = .1f * dot(delta, dir);
+        float hit = dist < P.coef[2] ? 1.f : 0.f;
+        const float* tq = E.qp + ti * QP_STRIDE;
+        const q4 tr{tq[3], tq[4], tq[5], tq[6]};
+        if (kind == BX_ENV_UR5E) {
+          reward = moving + hit;
+          if (m) { m[0] = hit; m[1] = moving; m[2] = hit; }  // sorted: hits, movingToTarget, weightedHits
+        } else {
+          v3 up = rotate(mk(0.f, 0.f, 1.f), tr);
+          float is_up = .1f * dt * dot(up, mk(0.f, 0.f, 1.f));
+          float height = .1f * dt * E.qp[2];
+          float facing = dot(dir, rotate(mk(1.f, 0.f, 0.f), tr));
+          float whit = hit * facing;
+          reward = height + moving + is_up + whit;
+          // sorted: hits, movingToTarget, torsoHeight, torsoIsUp, weightedHits
+          if (m) { m[0] = hit; m[1] = moving; m[2] = height; m[3] = is_up; m[4] = whit; }
+        }
+        // one draw per env step (action repeats included), as the reference
+        // splits its key once per step
+        const uint32_t key = A.in.rng[e] + (uint32_t)rep;
+        if (rep == reps - 1) A.out.rng[e] = key + 1u;
+        if (hit != 0.f) {
+          float u0 = uniform_at(key, 0, 0.f, 1.f), u1 = uniform_at(key, 1, 0.f, 1.f);
+          float rr = P.coef[2] + P.coef[3] * u0;
+          float an = 3.14159265358979323846f * 2.f * u1;
+          float* g = E.qp + gi * QP_STRIDE;
+          g[0] = rr * cosf(an);
+          g[1] = rr * sinf(an);
+          g[2] = P.coef[4];
+        }
       } else if (kind == BX_ENV_PUSHER) {
         // pusher.py:212-231; done as it came in
         float rc = -sq;
@@ -3273,15 +3359,6 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) info_obs_kernel(InfoArgs A) {
   }
 }
 
-// counter-based uniform: splitmix64 of (seed, global index) -> [lo, hi)
-__device__ __forceinline__ float uniform_at(uint64_t seed, uint64_t i, float lo, float hi) {
-  uint64_t z = seed * 0x9E3779B97F4A7C15ull + i + 0x632BE59BD9B4E019ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z = z ^ (z >> 31);
-  float u = (float)(z >> 40) * (1.0f / 16777216.0f);
-  return lo + (hi - lo) * u;
-}
 
 // System.default_qp (system.py:112-242): one thread per env (reset path)
 

@@ -13,7 +13,7 @@ from brax_amd.envs.env import Env, PhysicsEnv, State, Wrapper
 from brax_amd.envs.half_cheetah import Halfcheetah
 from brax_amd.envs.hopper import Hopper, Walker2d
 from brax_amd.envs.pendulums import Acrobot, InvertedDoublePendulum, InvertedPendulum
-from brax_amd.envs.tasks import Pusher, Reacher, ReacherAngle, Swimmer
+from brax_amd.envs.tasks import Fetch, Pusher, Reacher, ReacherAngle, Swimmer, Ur5e
 from brax_amd.envs.humanoid import Humanoid
 from brax_amd.envs.humanoid_standup import HumanoidStandup
 from brax_amd.envs import torch_envs
@@ -21,7 +21,7 @@ from brax_amd.envs import torch_envs
 _envs = {
     'acrobot': Acrobot,
     'fast': torch_envs.Fast,
-    'fetch': torch_envs.Fetch,
+    'fetch': Fetch,
     'grasp': torch_envs.Grasp,
     'ant': functools.partial(Ant, use_contact_forces=True),
     'halfcheetah': Halfcheetah,
@@ -34,7 +34,7 @@ _envs = {
     'reacher': Reacher,
     'reacherangle': ReacherAngle,
     'swimmer': Swimmer,
-    'ur5e': torch_envs.Ur5e,
+    'ur5e': Ur5e,
     'walker2d': Walker2d,
 }
 

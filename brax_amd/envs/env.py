@@ -308,6 +308,14 @@ class PhysicsEnv(Env):
     sout.steps = base + 8 * B
     sout.truncation = base + 12 * B
     sout.metrics = met.data_ptr()
+    rng_in = state.info.get('rng')
+    if rng_in is None and getattr(self, 'needs_rng', False):
+      rng_in = torch.zeros((B,), dtype=torch.int32, device=dev)  # a state built by hand
+    rng_out = None
+    if rng_in is not None:  # the target envs' per-env streams (int32 (B,))
+      sin.rng = rng_in.data_ptr()
+      rng_out = torch.empty_like(rng_in)
+      sout.rng = rng_out.data_ptr()
     _native.check(_native.lib().bx_env_step(
         self.sys._h, C.byref(p), B, C.byref(sin), C.c_void_p(act.data_ptr()), act.stride(0),
         act.shape[1], C.byref(sout), _stream(dev.index)))
@@ -316,6 +324,8 @@ class PhysicsEnv(Env):
     if p.episode_length > 0:
       info['steps'] = steps
       info['truncation'] = trunc
+    if rng_out is not None:
+      info['rng'] = rng_out
     metrics = dict(state.metrics)
     if self.metric_keys:
       metrics.update(zip(self.metric_keys, met.unbind(1)))

@@ -217,3 +217,77 @@ class Pusher(_KernelTask):
       qp.pos[:, self._object_idx] = torch.as_tensor(object_pos, dtype=torch.float32, device=dev)
     qp.pos[:, self._table_idx] = 0.
     return self._state(qp)
+
+
+def target_coef(body_index, torso, radius, distance, height):
+  """UR5E / FETCH constants: torso body, target body, the target ring."""
+  c = np.zeros(8, np.float64)
+  c[0], c[1] = body_index[torso], body_index['Target']
+  c[2], c[3], c[4] = radius, distance, height
+  return c
+
+
+def rng_streams(seed, offset, batch_size, device):
+  """Per-env random streams (uint32 as int32): a hash of (reset seed, global
+  env id), advanced by one each env step inside the step kernel."""
+  ids = torch.arange(offset, offset + batch_size, dtype=torch.int64, device=device)
+  z = ids * 0x9E3779B97F4A7C15 + (int(seed) & 0x7FFFFFFFFFFFFFFF)
+  z = (z ^ (z >> 31)) * 0x94D049BB133111EB
+  return (z ^ (z >> 29)).to(torch.int32)
+
+
+class Ur5e(_KernelTask):
+  """A UR5e arm reaching for targets (`brax/envs/ur5e.py`): egocentric
+  observation in the wrist's frame; a hit target is teleported to a fresh
+  spot (the env's device stream; JAX key parity unpinned)."""
+  kind = 14  # BX_ENV_UR5E
+  config = robots.UR5E_CONFIG
+  spring_config = robots.UR5E_SPRING_CONFIG
+  metric_keys = ('hits', 'movingToTarget', 'weightedHits')  # sorted (ur5e.py:64-68)
+  torso = 'wrist_3_link'
+  needs_rng = True  # the step reads and advances info['rng']
+  ring = (.02, .5, .5)  # target radius, distance, height (ur5e.py:51-54,126-135)
+
+  def __init__(self, **kwargs):
+    super().__init__(**kwargs)
+    self.target_idx = self.sys.body.index['Target']
+    self.coef = target_coef(self.sys.body.index, self.torso, *self.ring)
+    self._set_sizes()
+
+  def reset_batch(self, rng, batch_size, env_offset=None):
+    """ur5e.py:59-75: the default pose, a target on the ring."""
+    B = int(batch_size)
+    off = self.env_offset if env_offset is None else int(env_offset)
+    seed = key_to_seed(rng)
+    u = _uniform((B, 2), seed, off * 2, 0., 1., self.sys.device)
+    radius, distance, height = self.ring
+    dist = radius + distance * u[:, 0]
+    ang = math.pi * 2. * u[:, 1]
+    target = torch.stack([dist * torch.cos(ang), dist * torch.sin(ang),
+                          torch.full_like(dist, height)], -1)
+    st = self.reset_from(self.sys.default_angle().reshape(1, -1).expand(B, -1),
+                         torch.zeros((B, self.sys.num_joint_dof), device=self.sys.device), target)
+    st.info['rng'] = rng_streams(seed, off, B, self.sys.device)
+    return st
+
+  def reset_from(self, joint_angle, joint_velocity, target=None):
+    qp = self.sys.default_qp(joint_angle=joint_angle, joint_velocity=joint_velocity)
+    if target is not None:
+      qp.pos[:, self.target_idx] = torch.as_tensor(target, dtype=torch.float32,
+                                                   device=self.sys.device)
+    st = self._state(qp)
+    st.info['rng'] = rng_streams(0, self.env_offset, qp.pos.shape[0], self.sys.device)
+    return st
+
+
+class Fetch(Ur5e):
+  """A dog of boxes fetching targets (`brax/envs/fetch.py`): Ur5e's
+  egocentric observation around the Torso, plus upright / height / facing
+  rewards."""
+  kind = 15  # BX_ENV_FETCH
+  config = robots.FETCH_CONFIG
+  spring_config = robots.FETCH_SPRING_CONFIG
+  # sorted (fetch.py:47-53)
+  metric_keys = ('hits', 'movingToTarget', 'torsoHeight', 'torsoIsUp', 'weightedHits')
+  torso = 'Torso'
+  ring = (2., 15., 1.)  # fetch.py:36-39,124-134

@@ -169,111 +169,6 @@ class _TargetEnv(TorchEnv):
     return QP(pos=pos, rot=qp.rot, vel=qp.vel, ang=qp.ang), info
 
 
-class Ur5e(_TargetEnv):
-  """`brax/envs/ur5e.py:30-130`."""
-  config = robots.UR5E_CONFIG
-  spring_config = robots.UR5E_SPRING_CONFIG
-  metric_keys = ('hits', 'weightedHits', 'movingToTarget')
-
-  def __init__(self, **kwargs):
-    super().__init__(**kwargs)
-    self.target_idx = self.sys.body.index['Target']
-    self.torso_idx = self.sys.body.index['wrist_3_link']
-    self.target_radius, self.target_distance = .02, .5
-    N = self.sys.num_bodies
-    self.obs_size = 3 + 3 + 1 + 3 + 3 * N + 3 * N + N
-
-  def _random_target(self, seed, B):
-    u = _uniform((2, B), seed ^ 0xE5, 0, 0., 1., self.dev)
-    dist = self.target_radius + self.target_distance * u[0]
-    ang = bm.PI * 2. * u[1]
-    return torch.stack([dist * torch.cos(ang), dist * torch.sin(ang),
-                        torch.full_like(dist, .5)], -1)
-
-  def _reset_target(self, qp, seed, B):
-    pos = qp.pos.clone()
-    pos[:, self.target_idx] = self._random_target(seed, B)
-    return QP(pos=pos, rot=qp.rot, vel=qp.vel, ang=qp.ang)
-
-  def _get_obs(self, qp, info):
-    rot_t = qp.rot[:, self.torso_idx]
-    B = qp.pos.shape[0]
-    ex = torch.tensor([1., 0., 0.], device=self.dev).expand(B, 3)
-    ez = torch.tensor([0., 0., 1.], device=self.dev).expand(B, 3)
-    torso_fwd, torso_up = bm.rotate(ex, rot_t), bm.rotate(ez, rot_t)
-    inv = bm.quat_inv(rot_t)[:, None]
-    pos_local = bm.rotate(qp.pos - qp.pos[:, self.torso_idx:self.torso_idx + 1], inv)
-    vel_local = bm.rotate(qp.vel, inv)
-    tl = pos_local[:, self.target_idx]
-    mag = torch.linalg.norm(tl, dim=-1, keepdim=True)
-    contacts = _contacts(info, self.sys.num_bodies).expand(B, -1)
-    return torch.cat([torso_fwd, torso_up, mag, tl / (1e-6 + mag), pos_local.reshape(B, -1),
-                      vel_local.reshape(B, -1), contacts], -1)
-
-  def _step(self, state, action, qp, info):
-    obs = self._get_obs(qp, info)
-    torso_delta = qp.pos[:, self.torso_idx] - state.qp.pos[:, self.torso_idx]
-    target_rel = qp.pos[:, self.target_idx] - qp.pos[:, self.torso_idx]
-    target_dist = torch.linalg.norm(target_rel, dim=-1)
-    target_dir = target_rel / (1e-6 + target_dist[:, None])
-    moving = .1 * (torso_delta * target_dir).sum(-1)
-    hit = torch.where(target_dist < self.target_radius, 1.0, 0.0)
-    reward = moving + hit
-    metrics = _replace_metrics(state, hits=hit, weightedHits=hit, movingToTarget=moving)
-    qp, info_s = self._teleport(state, qp, hit)
-    return state.replace(qp=qp, obs=obs, reward=reward, metrics=metrics, info=info_s)
-
-
-class Fetch(Ur5e):
-  """`brax/envs/fetch.py:24-134`: a dog of boxes (box-plane contacts on the
-  lower legs) runs to a target; Ur5e's egocentric observation around the
-  Torso."""
-  config = robots.FETCH_CONFIG
-  spring_config = robots.FETCH_SPRING_CONFIG
-  metric_keys = ('hits', 'weightedHits', 'movingToTarget', 'torsoIsUp', 'torsoHeight')
-
-  def __init__(self, **kwargs):  # pylint: disable=super-init-not-called
-    TorchEnv.__init__(self, **kwargs)
-    self.target_idx = self.sys.body.index['Target']
-    self.torso_idx = self.sys.body.index['Torso']
-    self.target_radius, self.target_distance = 2., 15.
-    N = self.sys.num_bodies
-    self.obs_size = 3 + 3 + 1 + 3 + 3 * N + 3 * N + N
-
-  def _random_target(self, seed, B):
-    """`fetch.py:124-134`: a random spot on a ring, z = 1."""
-    u = _uniform((2, B), seed ^ 0xFE, 0, 0., 1., self.dev)
-    dist = self.target_radius + self.target_distance * u[0]
-    ang = bm.PI * 2. * u[1]
-    return torch.stack([dist * torch.cos(ang), dist * torch.sin(ang),
-                        torch.ones_like(dist)], -1)
-
-  def _step(self, state, action, qp, info):
-    """`fetch.py:58-99`."""
-    dt = float(self.sys.config.dt)
-    obs = self._get_obs(qp, info)
-    t = self.torso_idx
-    torso_delta = qp.pos[:, t] - state.qp.pos[:, t]
-    target_rel = qp.pos[:, self.target_idx] - qp.pos[:, t]
-    target_dist = torch.linalg.norm(target_rel, dim=-1)
-    target_dir = target_rel / (1e-6 + target_dist[:, None])
-    moving = .1 * (torso_delta * target_dir).sum(-1)
-    B = qp.pos.shape[0]
-    ex = torch.tensor([1., 0., 0.], device=self.dev).expand(B, 3)
-    ez = torch.tensor([0., 0., 1.], device=self.dev).expand(B, 3)
-    torso_up = bm.rotate(ez, qp.rot[:, t])
-    torso_is_up = .1 * dt * torso_up[:, 2]
-    torso_height = .1 * dt * qp.pos[:, 0, 2]
-    torso_facing = (target_dir * bm.rotate(ex, qp.rot[:, t])).sum(-1)
-    hit = torch.where(target_dist < self.target_radius, 1.0, 0.0)
-    weighted = hit * torso_facing
-    reward = torso_height + moving + torso_is_up + weighted
-    metrics = _replace_metrics(state, hits=hit, weightedHits=weighted, movingToTarget=moving,
-                               torsoIsUp=torso_is_up, torsoHeight=torso_height)
-    qp, info_s = self._teleport(state, qp, hit)
-    return state.replace(qp=qp, obs=obs, reward=reward, metrics=metrics, info=info_s)
-
-
 class Grasp(_TargetEnv):
   """`brax/envs/grasp.py:29-190`: Angle actuators driven through [-1, 1]
   actions, plus 3 actions that translate the palm before the physics step."""

