@@ -93,7 +93,7 @@ class BxEnvParams(C.Structure):
               ('n_metrics', C.c_int32), ('episode_length', C.c_int32),
               ('action_repeat', C.c_int32), ('auto_reset', C.c_int32),
               ('obs_flags', C.c_int32), ('coef', C.c_float * 8),
-              ('first_qp', BxQP), ('first_obs', C.c_void_p)]
+              ('first_qp', BxQP), ('first_obs', C.c_void_p), ('act_map', C.c_void_p)]
 
 
 def _arr(x, dtype):

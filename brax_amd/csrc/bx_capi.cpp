@@ -423,6 +423,9 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.l_alist = carve(H.info_rows);
   H.l_ang = carve(2 * D);
   H.l_red = carve(64);
+  // env programs' System.step action (swimmer: + drag, grasp: 3 palm actions)
+  H.xact_words = std::max(16, (d->action_size + 12 + 3) & ~3);
+  H.l_xact = carve(H.xact_words);
   // the contact regions form each mode's tail: the item-loop / SINGLE
   // kernels keep per-row data and 12-word slots, MULTI mode keeps the row data
   // in registers and needs 8-word slots plus the task partials
@@ -589,6 +592,12 @@ int env_sizes(const bx_system* S, const bx_env_params* P, int* obs, int* met) {
       if (xy) return fail("this env has no current-position observation option");
       *obs = 10 + 7 * N;
       *met = P->kind == BX_ENV_UR5E ? 3 : 5;
+      return 0;
+    case BX_ENV_GRASP:  // object, target, local pos / vel, hand and object terms, contacts
+      if (xy) return fail("this env has no current-position observation option");
+      if (N < 16) return fail("Grasp's reward reads the contacts of bodies 3, 9, 12 and 15");
+      *obs = 1 + 3 + 1 + 3 + 6 * N + 3 + 3 + 1 + 1 + 3 + 1 + N;
+      *met = 5;
       return 0;
     case BX_ENV_HALFCHEETAH:
       *obs = 3 + D + 3 + D + (xy ? 1 : 0);
@@ -760,7 +769,11 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   if (!in->done || !out->done || !out->reward || !out->obs) return fail("null env buffer");
   if (env->auto_reset && (!qp_ok(env->first_qp) || !env->first_obs))
     return fail("auto_reset needs first_qp and first_obs");
-  if ((env->kind == BX_ENV_UR5E || env->kind == BX_ENV_FETCH) && (!in->rng || !out->rng))
+  if (env->kind == BX_ENV_GRASP && !env->act_map) return fail("Grasp needs its action map");
+  if (env->kind == BX_ENV_GRASP && act_width + 0 > S->hdr.xact_words)
+    return fail("action wider than the env program's action buffer");
+  if ((env->kind == BX_ENV_UR5E || env->kind == BX_ENV_FETCH || env->kind == BX_ENV_GRASP) &&
+      (!in->rng || !out->rng))
     return fail("the target envs need the per-env rng stream (in and out)");
   if (env->episode_length > 0 && (!out->steps || !out->truncation))
     return fail("episode wrapper needs steps and truncation buffers");

@@ -76,6 +76,7 @@ struct Env {
   float* tslot;  // MULTI mode: (T + 1) x MSLOT_STRIDE gather-task partials, zero last
   float* nd;     // NearNeighbors candidate distances, stride nds (scratch, before the substeps)
   int nds;
+  float* xact;   // the action an env program hands System.step (xact_words)
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -1231,6 +1232,7 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi =
   E.nJ = H.J;
   E.nK = H.K;
   E.nR = H.R;
+  E.xact = al16(base + H.l_xact);
   if (multi) {
     // MULTI: 8-word contact slots and task partials; no row-data region (the
     // row's contact stays in its lane's registers); the task partials double
@@ -2757,6 +2759,54 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
     const float* cv = E.acc + i * ACC_STRIDE + ACC_ICV;
     return cv[0] * cv[0] + cv[1] * cv[1] + cv[2] * cv[2] > 0.00001f ? 1.f : 0.f;
   }
+  if (kind == BX_ENV_GRASP) {
+    // grasp.py:132-175, in the palm's frame: [|object|, object dir, |target|,
+    // target dir, local pos (N x 3), local vel (N x 3), hand to object, hand
+    // vel, heading to object, |object to target|, its dir, object heading,
+    // contact flags (N)]
+    const int pi = (int)coef[0], oi = (int)coef[1], gi = (int)coef[2], hi = (int)coef[3];
+    const float* pq = E.qp + pi * QP_STRIDE;
+    const q4 ri = quat_inv(q4{pq[3], pq[4], pq[5], pq[6]});
+    if (i < 8) {
+      const int b = i < 4 ? oi : gi;
+      v3 l = rotate(ld3(E.qp + b * QP_STRIDE) - ld3(pq), ri);
+      float mag = norm(l);
+      const int k = i % 4;
+      if (k == 0) return mag;
+      v3 dd = l / (1e-6f + mag);
+      return k == 1 ? dd.x : (k == 2 ? dd.y : dd.z);
+    }
+    i -= 8;
+    if (i < 3 * N) {
+      v3 l = rotate(ld3(E.qp + (i / 3) * QP_STRIDE) - ld3(pq), ri);
+      return i % 3 == 0 ? l.x : (i % 3 == 1 ? l.y : l.z);
+    }
+    i -= 3 * N;
+    if (i < 3 * N) {
+      v3 l = rotate(ld3(E.qp + (i / 3) * QP_STRIDE + 7), ri);
+      return i % 3 == 0 ? l.x : (i % 3 == 1 ? l.y : l.z);
+    }
+    i -= 3 * N;
+    v3 h2o = ld3(E.qp + oi * QP_STRIDE) - ld3(pq);
+    v3 hv = ld3(E.qp + hi * QP_STRIDE + 7);
+    if (i < 3) return i == 0 ? h2o.x : (i == 1 ? h2o.y : h2o.z);
+    i -= 3;
+    if (i < 3) return i == 0 ? hv.x : (i == 1 ? hv.y : hv.z);
+    i -= 3;
+    if (i == 0) return dot(h2o / (1e-6f + norm(h2o)), hv);
+    i -= 1;
+    v3 o2t = ld3(E.qp + gi * QP_STRIDE) - ld3(E.qp + oi * QP_STRIDE);
+    float om = norm(o2t);
+    v3 od = o2t / (1e-6f + om);
+    if (i == 0) return om;
+    i -= 1;
+    if (i < 3) return i == 0 ? od.x : (i == 1 ? od.y : od.z);
+    i -= 3;
+    if (i == 0) return dot(od, ld3(E.qp + oi * QP_STRIDE + 7));
+    i -= 1;
+    const float* cv = E.acc + i * ACC_STRIDE + ACC_ICV;
+    return cv[0] * cv[0] + cv[1] * cv[1] + cv[2] * cv[2] > 0.00001f ? 1.f : 0.f;
+  }
   if (kind == BX_ENV_PUSHER) {
     // pusher.py:232-242: [joint angles, joint vels, tip, object, goal positions]
     if (i < 2 * D) return E.ang[i];
@@ -3040,10 +3090,10 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
       dist0 = -norm(obj - goal);
     }
     // the action System.step reads: the env's own, or its pre-step program's
-    // output in LDS (red words 48..63)
+    // output in LDS (E.xact)
     const float* sact = act;
     int saw = aw;
-    float* xact = E.red + 48;
+    float* xact = E.xact;
     if (kind == BX_ENV_REACHERANGLE) {
       // reacherangle.py:79: min + range * (a + 1) / 2 onto the angle limits
       if (valid && lane < aw) xact[lane] = P.coef[2 + lane] + P.coef[4 + lane] * ((act[lane] + 1.f) / 2.f);
@@ -3075,6 +3125,22 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
       if (valid && lane < aw) xact[lane] = act[lane];
       sact = valid ? xact : nullptr;
       saw = aw + 9;
+    } else if (kind == BX_ENV_GRASP) {
+      // grasp.py:63-77: the [-1, 1] action mapped onto the angle limits and
+      // the palm's range; the palm moves 15 % of the way to the last three
+      // (at most 2 units) before the physics
+      for (int i = lane; i < aw; i += L)
+        if (valid) xact[i] = P.act_map[i] + P.act_map[aw + i] * ((act[i] + 1.f) / 2.f);
+      esync<L>();
+      if (lane == 0 && valid) {
+        float* pp = E.qp + (int)P.coef[0] * QP_STRIDE;
+        v3 palm = ld3(pp);
+        v3 d = mk(xact[aw - 3], xact[aw - 2], xact[aw - 1]) - palm;
+        float nrm = norm(d);
+        float scl = nrm > 2.f ? 2.f / nrm : 1.f;
+        st3(pp, palm + scl * d * .15f);
+      }
+      sact = valid ? xact : nullptr;
     }
     esync<L>();
     if constexpr (S) {
@@ -3242,6 +3308,45 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
           g[0] = rr * cosf(an);
           g[1] = rr * sinf(an);
           g[2] = P.coef[4];
+        }
+      } else if (kind == BX_ENV_GRASP) {
+        // grasp.py:80-126 (done as it came in); a hit target moves to a
+        // fresh spot from the env's stream (after the obs)
+        const int oi = (int)P.coef[1], gi = (int)P.coef[2], hi = (int)P.coef[3];
+        v3 op = ld3(E.qp + oi * QP_STRIDE), hp = ld3(E.qp + (int)P.coef[0] * QP_STRIDE);
+        v3 hv = ld3(E.qp + hi * QP_STRIDE + 7);
+        v3 rel = op - hp;
+        float od = norm(rel);
+        float planar = norm(mul(rel, mk(1.f, 1.f, 0.f)));
+        v3 odir = rel / (1e-6f + od);
+        float mto = .1f * dt * dot(hv, odir);
+        float close = .1f * dt * 1.f / (1.f + planar);
+        v3 trel = ld3(E.qp + gi * QP_STRIDE) - op;
+        float td = norm(trel);
+        v3 tdir = trel / (1e-6f + td);
+        float mtt = 1.5f * dt * dot(ld3(E.qp + oi * QP_STRIDE + 7), tdir);
+        float touch = 0.f;
+        const int tb[4] = {3, 9, 12, 15};
+        for (int k = 0; k < 4; k++) {
+          const float* cv = E.acc + tb[k] * ACC_STRIDE + ACC_ICV;
+          touch += cv[0] * cv[0] + cv[1] * cv[1] + cv[2] * cv[2] > 0.00001f ? 1.f : 0.f;
+        }
+        touch = 0.2f * dt * touch;
+        float hit = td < P.coef[4] ? 1.f : 0.f;
+        reward = mto + close + touch + 5.f * hit + mtt;
+        // sorted: closeToObject, hits, movingObjectToTarget, movingToObject, touchingObject
+        if (m) { m[0] = close; m[1] = hit; m[2] = mtt; m[3] = mto; m[4] = touch; }
+        const uint32_t key = A.in.rng[e] + (uint32_t)rep;
+        if (rep == reps - 1) A.out.rng[e] = key + 1u;
+        if (hit != 0.f) {
+          float u0 = uniform_at(key, 0, 0.f, 1.f), u1 = uniform_at(key, 1, 0.f, 1.f);
+          float u2 = uniform_at(key, 2, 0.f, 1.f);
+          float rr = P.coef[4] + P.coef[5] * u0;
+          float an = 3.14159265358979323846f * 2.f * u1;
+          float* g = E.qp + gi * QP_STRIDE;
+          g[0] = rr * cosf(an);
+          g[1] = rr * sinf(an);
+          g[2] = P.coef[6] * u2;
         }
       } else if (kind == BX_ENV_PUSHER) {
         // pusher.py:212-231; done as it came in

@@ -88,6 +88,8 @@ struct BlobHdr {
   int32_t T, o_task, o_btask;        // tasks: TASK_W slot indices each; per body BTASK_W task refs
   int32_t l_mslot, l_tslot;          // LDS: 8-word contact slots (2R+1), task partials (T+1)
   int32_t env_words_m;               // per-env LDS words in MULTI mode
+  int32_t l_xact;                    // LDS: the action an env program hands System.step
+  int32_t xact_words;
 };
 // MULTI-mode gather tasks: a task sums <= TASK_W contact slots of one body and
 // collider group; a body adds <= BTASK_W task partials (ref = task | group << 24)

@@ -291,3 +291,72 @@ class Fetch(Ur5e):
   metric_keys = ('hits', 'movingToTarget', 'torsoHeight', 'torsoIsUp', 'weightedHits')
   torso = 'Torso'
   ring = (2., 15., 1.)  # fetch.py:36-39,124-134
+
+
+def grasp_coef(body_index):
+  """GRASP constants: palm, object, target, hand bodies and the target ring
+  (grasp.py:35-41)."""
+  c = np.zeros(8, np.float64)
+  c[0], c[1] = body_index['HandPalm'], body_index['Object']
+  c[2], c[3] = body_index['Target'], body_index['HandThumbProximal']
+  c[4], c[5], c[6] = 1.1, 10., 8.
+  return c
+
+
+def grasp_act_map(config):
+  """grasp.py:42-52: per action (min, range), the joints' angle limits then
+  the palm's translation range; (2, A)."""
+  lim = [(l.min, l.max) for j in config.joints for l in j.angle_limit]
+  lo = [l[0] for l in lim] + [-10., -10., 3.5]
+  rg = [l[1] - l[0] for l in lim] + [20., 20., 10.]
+  return np.array([lo, rg], np.float64)
+
+
+class Grasp(_KernelTask):
+  """A hand grasping an object and carrying it to targets
+  (`brax/envs/grasp.py`): [-1, 1] actions mapped onto the joints' angle
+  limits plus 3 that move the palm before the physics (inside the step
+  kernel); observation in the palm's frame; a hit target is teleported (the
+  env's device stream; JAX key parity unpinned)."""
+  kind = 16  # BX_ENV_GRASP
+  config = robots.GRASP_CONFIG
+  spring_config = robots.GRASP_SPRING_CONFIG
+  # sorted (grasp.py:47-53)
+  metric_keys = ('closeToObject', 'hits', 'movingObjectToTarget', 'movingToObject',
+                 'touchingObject')
+  needs_rng = True
+
+  def __init__(self, **kwargs):
+    super().__init__(**kwargs)
+    self.target_idx = self.sys.body.index['Target']
+    self.coef = grasp_coef(self.sys.body.index)
+    self.act_map = torch.as_tensor(grasp_act_map(self.sys.config), dtype=torch.float32,
+                                   device=self.sys.device).contiguous()
+    self._set_sizes()
+
+  @property
+  def action_size(self):
+    return self.sys.num_joint_dof + self.sys.num_forces_dof + 3  # grasp.py:128-130
+
+  def _params(self, opts=None, first_qp=None, first_obs=None):
+    p = super()._params(opts, first_qp, first_obs)
+    p.act_map = self.act_map.data_ptr() if hasattr(self, 'act_map') else None
+    return p
+
+  def reset_batch(self, rng, batch_size, env_offset=None):
+    """grasp.py:54-70: the default pose at rest (the target stays at its
+    configured spot)."""
+    B = int(batch_size)
+    off = self.env_offset if env_offset is None else int(env_offset)
+    D = self.sys.num_joint_dof
+    dev = self.sys.device
+    st = self.reset_from(self.sys.default_angle().reshape(1, -1).expand(B, -1),
+                         torch.zeros((B, D), device=dev))
+    st.info['rng'] = rng_streams(key_to_seed(rng), off, B, dev)
+    return st
+
+  def reset_from(self, joint_angle, joint_velocity):
+    qp = self.sys.default_qp(joint_angle=joint_angle, joint_velocity=joint_velocity)
+    st = self._state(qp)
+    st.info['rng'] = rng_streams(0, self.env_offset, qp.pos.shape[0], self.sys.device)
+    return st

@@ -65,7 +65,9 @@ enum { BX_ENV_NONE = 0, BX_ENV_ANT = 1, BX_ENV_HUMANOID = 2, BX_ENV_HALFCHEETAH 
         * pusher.py:211-242 */
        BX_ENV_REACHER = 10, BX_ENV_REACHERANGLE = 11, BX_ENV_SWIMMER = 12, BX_ENV_PUSHER = 13,
        /* egocentric target envs (ur5e.py:59-135, fetch.py:58-134) */
-       BX_ENV_UR5E = 14, BX_ENV_FETCH = 15 };
+       BX_ENV_UR5E = 14, BX_ENV_FETCH = 15,
+       /* a hand grasping an object (grasp.py:29-190) */
+       BX_ENV_GRASP = 16 };
 /* observation options. BX_OBS_XY: exclude_current_positions_from_observation
  * = False, the torso's x (and y) precede its z (ant.py:262-265,
  * humanoid.py:289-292: x, y; half_cheetah.py:206-209: x) */
@@ -268,11 +270,16 @@ typedef struct bx_env_params {
    *   PUSHER:      tip body, object body, goal body
    *   UR5E / FETCH: torso body, target body, target radius, target
    *                distance, target height (a hit target moves to a fresh
-   *                random spot on the ring [radius, radius + distance)) */
+   *                random spot on the ring [radius, radius + distance))
+   *   GRASP:       palm body, object body, target body, hand body (thumb
+   *                proximal), target radius, distance, height */
   float coef[8];
   /* AutoReset targets (first_qp / first_obs); required when auto_reset */
   bx_qp first_qp;
   const float* first_obs;
+  /* GRASP: device array [2, A] of per-action (min, range); System.step reads
+   * min + range * (a + 1) / 2 (grasp.py:42-52,65); NULL for the other kinds */
+  const float* act_map;
 } bx_env_params;
 
 typedef struct bx_system bx_system;

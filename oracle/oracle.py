@@ -20,7 +20,7 @@ LIB = os.path.join(HERE, '_build', 'liboracle.so')
 ENV_KIND = {'none': 0, 'ant': 1, 'humanoid': 2, 'halfcheetah': 3, 'humanoidstandup': 4,
             'hopper': 5, 'walker2d': 6, 'inverted_pendulum': 7, 'inverted_double_pendulum': 8,
             'acrobot': 9, 'reacher': 10, 'reacherangle': 11, 'swimmer': 12, 'pusher': 13,
-            'ur5e': 14, 'fetch': 15}
+            'ur5e': 14, 'fetch': 15, 'grasp': 16}
 
 
 def build():
@@ -131,6 +131,11 @@ class Oracle:
     if rc:
       raise ValueError('obs size mismatch')
     return obs
+
+  def set_act_map(self, act_map):
+    """Grasp's per-action (min, range) map, (2, A)."""
+    m = np.ascontiguousarray(np.asarray(act_map, np.float64))
+    self._fn('oracle_set_act_map')(m.ctypes.data_as(C.POINTER(C.c_double)), C.c_int(m.shape[1]))
 
   def env_step(self, kind, qp, act, obs_size, n_metrics, done=None, obs_flags=0, coef=None):
     """obs_flags: BX_OBS_XY for exclude_current_positions_from_observation=False."""

@@ -47,6 +47,13 @@ void FN(oracle_set_safe_norm_guard)(int on) { g_safe_guard = on; }
  * are clipped into it like jp.take(mode='clip') (jumpy.py:146-151) */
 static int g_act_width = 0;
 void FN(oracle_set_act_width)(int w) { g_act_width = w; }
+/* GRASP's action map [2, n] (per action min, range; grasp.py:42-52) */
+static double g_act_map[2 * 64];
+static int g_act_map_n = 0;
+void FN(oracle_set_act_map)(const double* m, int n) {
+  g_act_map_n = n < 64 ? n : 64;
+  for (int i = 0; i < g_act_map_n; i++) { g_act_map[i] = m[i]; g_act_map[64 + i] = m[n + i]; }
+}
 static inline int take_idx(int i, int w) { return i < 0 ? 0 : (i >= w ? w - 1 : i); }
 void FN(oracle_set_threads)(int n) {
 #ifdef _OPENMP
@@ -2108,6 +2115,48 @@ static int obs_ego(const sysc* s, const body_t* qp, const R* info_c, const doubl
   return n;
 }
 
+/* Grasp._get_obs (grasp.py:132-175), in the palm's frame; coef = palm,
+ * object, target, hand bodies */
+static int obs_grasp(const sysc* s, const body_t* qp, const R* info_c, const double* coef, R* obs) {
+  int n = 0, N = s->N, p = (int)coef[0], ob = (int)coef[1], tg = (int)coef[2], hd = (int)coef[3];
+  const R ri[4] = {qp[p].rot[0], -qp[p].rot[1], -qp[p].rot[2], -qp[p].rot[3]};
+  R d[3], v[3];
+  for (int w = 0; w < 2; w++) {
+    int b = w == 0 ? ob : tg;
+    for (int k = 0; k < 3; k++) d[k] = qp[b].pos[k] - qp[p].pos[k];
+    rotate(d, ri, v);
+    R mag = norm3(v);
+    obs[n++] = mag;
+    for (int k = 0; k < 3; k++) obs[n++] = v[k] / ((R)1e-6 + mag);
+  }
+  for (int b = 0; b < N; b++) {
+    for (int k = 0; k < 3; k++) d[k] = qp[b].pos[k] - qp[p].pos[k];
+    rotate(d, ri, v);
+    for (int k = 0; k < 3; k++) obs[n++] = v[k];
+  }
+  for (int b = 0; b < N; b++) {
+    rotate(qp[b].vel, ri, v);
+    for (int k = 0; k < 3; k++) obs[n++] = v[k];
+  }
+  R h2o[3], hdir[3], o2t[3], odir[3];
+  for (int k = 0; k < 3; k++) h2o[k] = qp[ob].pos[k] - qp[p].pos[k];
+  for (int k = 0; k < 3; k++) obs[n++] = h2o[k];
+  for (int k = 0; k < 3; k++) obs[n++] = qp[hd].vel[k];
+  R hm = norm3(h2o);
+  for (int k = 0; k < 3; k++) hdir[k] = h2o[k] / ((R)1e-6 + hm);
+  obs[n++] = dot3(hdir, qp[hd].vel);
+  for (int k = 0; k < 3; k++) o2t[k] = qp[tg].pos[k] - qp[ob].pos[k];
+  R om = norm3(o2t);
+  obs[n++] = om;
+  for (int k = 0; k < 3; k++) { odir[k] = o2t[k] / ((R)1e-6 + om); obs[n++] = odir[k]; }
+  obs[n++] = dot3(odir, qp[ob].vel);
+  for (int b = 0; b < N; b++) {
+    const R* c = info_c + 6 * b;
+    obs[n++] = c[0] * c[0] + c[1] * c[1] + c[2] * c[2] > (R)0.00001 ? (R)1 : (R)0;
+  }
+  return n;
+}
+
 /* Humanoid._center_of_mass (humanoid.py:336-338): bodies [:-1] */
 static void humanoid_com(const sysc* s, const body_t* qp, R* com) {
   R m = 0;
@@ -2175,7 +2224,7 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
                        const R* act, R* obs, int obs_size, const double* coef) {
   sysc s;
   sys_init(&s, d);
-  if ((kind & 0xFF) >= BX_ENV_REACHER && (kind & 0xFF) <= BX_ENV_FETCH && !coef) {
+  if ((kind & 0xFF) >= BX_ENV_REACHER && (kind & 0xFF) <= BX_ENV_GRASP && !coef) {
     sys_free(&s);
     return -2;
   }
@@ -2201,6 +2250,8 @@ int FN(oracle_env_obs)(const bx_desc* d, int kind, int64_t B, const R* qp, const
         n = obs_task(&s, kind, q, coef, obs + e * obs_size, xy);
       else if (kind == BX_ENV_UR5E || kind == BX_ENV_FETCH)
         n = obs_ego(&s, q, info_c + e * 6 * N, coef, obs + e * obs_size);
+      else if (kind == BX_ENV_GRASP)
+        n = obs_grasp(&s, q, info_c + e * 6 * N, coef, obs + e * obs_size);
       else if (kind == BX_ENV_HUMANOID || kind == BX_ENV_HUMANOID_STANDUP)
         n = obs_humanoid(&s, q, act + e * s.aw, obs + e * obs_size, xy);
       if (n != obs_size) rc = -1;
@@ -2222,7 +2273,7 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
   int rc = 0;
   const int xy = (kind >> 8) & BX_OBS_XY; /* kind | obs_flags << 8 */
   kind &= 0xFF;
-  if (kind >= BX_ENV_REACHER && kind <= BX_ENV_FETCH && !coef) {
+  if (kind >= BX_ENV_REACHER && kind <= BX_ENV_GRASP && !coef) {
     sys_free(&s);
     return -2;
   }
@@ -2265,6 +2316,18 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
           for (int k = 0; k < 3; k++)
             xa[A + 3 * b + k] = fw[k] < (R)-5 ? (R)-5 : (fw[k] > (R)5 ? (R)5 : fw[k]);
         }
+        sa = xa;
+      } else if (kind == BX_ENV_GRASP) {
+        /* grasp.py:63-77: the mapped action; the palm moves 15 % toward the
+         * last three (at most 2 units) before the physics */
+        for (int i = 0; i < A; i++)
+          xa[i] = (R)g_act_map[i] + (R)g_act_map[64 + i] * ((a[i] + 1) / 2);
+        int p = (int)coef[0];
+        R d[3];
+        for (int k = 0; k < 3; k++) d[k] = xa[A - 3 + k] - w.qp[p].pos[k];
+        R nrm = norm3(d);
+        R scl = nrm > (R)2 ? (R)2 / nrm : (R)1;
+        for (int k = 0; k < 3; k++) w.qp[p].pos[k] = w.qp[p].pos[k] + scl * d[k] * (R)0.15;
         sa = xa;
       }
       step_env(&s, &w, sa, ra, rb);
@@ -2420,6 +2483,32 @@ int FN(oracle_env_step)(const bx_desc* d, int kind, int64_t B, const R* qp_in, c
           reward[e] = height + moving + is_up + whit;
           m[0] = hit; m[1] = moving; m[2] = height; m[3] = is_up; m[4] = whit;
         }
+      } else if (kind == BX_ENV_GRASP) {
+        /* grasp.py:80-126 (teleport not restated; done unchanged) */
+        n = obs_grasp(&s, w.qp, w.info_c, coef, o);
+        int p = (int)coef[0], ob = (int)coef[1], tg = (int)coef[2], hd = (int)coef[3];
+        R rel[3], odir[3], trel[3], tdir[3];
+        for (int k = 0; k < 3; k++) rel[k] = w.qp[ob].pos[k] - w.qp[p].pos[k];
+        R od = norm3(rel);
+        const R pl[3] = {rel[0], rel[1], 0};
+        R planar = norm3(pl);
+        for (int k = 0; k < 3; k++) odir[k] = rel[k] / ((R)1e-6 + od);
+        R mto = (R)0.1 * dt * dot3(w.qp[hd].vel, odir);
+        R close = (R)0.1 * dt * (R)1 / ((R)1 + planar);
+        for (int k = 0; k < 3; k++) trel[k] = w.qp[tg].pos[k] - w.qp[ob].pos[k];
+        R td = norm3(trel);
+        for (int k = 0; k < 3; k++) tdir[k] = trel[k] / ((R)1e-6 + td);
+        R mtt = (R)1.5 * dt * dot3(w.qp[ob].vel, tdir);
+        const int tb[4] = {3, 9, 12, 15};
+        R touch = 0;
+        for (int k = 0; k < 4; k++) {
+          const R* c = w.info_c + 6 * tb[k];
+          touch += c[0] * c[0] + c[1] * c[1] + c[2] * c[2] > (R)0.00001 ? (R)1 : (R)0;
+        }
+        touch = (R)0.2 * dt * touch;
+        R hit = td < (R)coef[4] ? (R)1 : (R)0;
+        reward[e] = mto + close + touch + (R)5 * hit + mtt;
+        m[0] = close; m[1] = hit; m[2] = mtt; m[3] = mto; m[4] = touch;
       } else if (kind == BX_ENV_PUSHER) {
         n = obs_task(&s, kind, w.qp, coef, o, xy);
         R v1[3], v2[3];

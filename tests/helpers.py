@@ -49,7 +49,7 @@ XY_ENVS = ['ant_xy', 'humanoid_xy', 'halfcheetah_xy']
 # kernel env kinds whose reference rollouts are the envtraj_* goldens (the
 # env-layer rollouts of oracle/gen_golden.py) rather than traj_*
 ENVTRAJ_KERNEL = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum', 'acrobot',
-                  'reacher', 'reacherangle', 'swimmer', 'pusher', 'ur5e', 'fetch']
+                  'reacher', 'reacherangle', 'swimmer', 'pusher', 'ur5e', 'fetch', 'grasp']
 # bodies a kernel env's reset places after default_qp (reacher.py:177-179,
 # pusher.py:196-201): name -> body names
 
@@ -70,10 +70,20 @@ def env_coef(name):
     return tasks.swimmer_coef()
   if name == 'pusher':
     return tasks.pusher_coef(compiled(name)[3]['body_index'])
+  if name == 'grasp':
+    return tasks.grasp_coef(compiled(name)[3]['body_index'])
   if name in ('ur5e', 'fetch'):
     cls = tasks.Ur5e if name == 'ur5e' else tasks.Fetch
     return tasks.target_coef(compiled(name)[3]['body_index'], cls.torso, *cls.ring)
   return None
+
+
+def prep_oracle(o, name):
+  """Per-env oracle state: Grasp's action map."""
+  if name == 'grasp':
+    from brax_amd.envs import tasks
+    o.set_act_map(tasks.grasp_act_map(config_for(name)))
+  return o
 
 
 def golden_reset_qp(name, o, T):

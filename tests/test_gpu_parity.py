@@ -24,7 +24,7 @@ from tests.conftest import golden
 from tests.margins import record_margin
 from tests.helpers import (CAPSULES, ENVTRAJ_KERNEL, POINTS, QP_FIELDS, ROBOTS, SPRING_ENVS,
                            SPRING_ROBOTS, XCOL, XY_ENVS, compiled, env_golden, env_kind,
-                           golden_reset_qp, normwise, obs_flags, reset_bodies)
+                           golden_reset_qp, normwise, obs_flags, prep_oracle, reset_bodies)
 
 pytestmark = pytest.mark.gpu
 
@@ -72,7 +72,8 @@ class Envelope:
 
   def __init__(self, oracle_lib, name, n_perturb=3, desc=None):
     d, rd = desc if desc is not None else compiled(name)[1:3]
-    self.os = [oracle_lib.Oracle(d, rd, np.float32, safe_guard=True, fma=f) for f in (False, True)]
+    self.os = [prep_oracle(oracle_lib.Oracle(d, rd, np.float32, safe_guard=True, fma=f), name)
+               for f in (False, True)]
     self.n = n_perturb
 
   def _inputs(self, qp):

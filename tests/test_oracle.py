@@ -10,7 +10,7 @@ import pytest
 
 from tests.conftest import golden
 from tests.helpers import (CAPSULES, ENVTRAJ_KERNEL, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS,
-                           XCOL, XY_ENVS, env_coef, env_golden, golden_reset_qp,
+                           XCOL, XY_ENVS, env_coef, env_golden, golden_reset_qp, prep_oracle,
                            compiled, env_kind, obs_flags)
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
@@ -79,7 +79,7 @@ def test_contact_info_matches_reference(oracle_lib, name):
 
 @pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS + ENVTRAJ_KERNEL)
 def test_env_step_matches_reference(oracle_lib, name):
-  o = _oracle(oracle_lib, name)
+  o = prep_oracle(_oracle(oracle_lib, name), name)
   T = golden(env_golden(name))
   O, M = T['obs'].shape[-1], T['metrics'].shape[-1]
   for t in range(T['action'].shape[0]):
