@@ -32,7 +32,10 @@ sys.path.insert(0, ROOT)
 # Algorithmic HBM bytes per Ant env-step: QP in 520 + QP out
 # 520 + action 32 + obs 348 + reward/done 8 = 1,428 B.
 ANT_BYTES_PER_ENV_STEP = 1428
-ANT_KERNEL = 'bx::env_step_kernel<16, 1, 32, 4>'  # rocprof name of the Ant env step (F_G1)
+# rocprof name of the Ant env step: 16 lanes, SINGLE mode, features F_G1 |
+# F_JH (one collider group per body, joint halves), gather width 4, the Ant
+# env program only (EK_ANT)
+ANT_KERNEL = 'bx::env_step_kernel<16, 1, 160, 4, 1>'
 # Counted flops per Ant Env.step (reference numpy path).
 ANT_FLOPS_PER_ENV_STEP = 87382
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8 TB/s HBM3E

@@ -22,8 +22,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # keyed by the exact rocprof instantiation: QP in+out 2*52*N,
 # action 4*A, obs 4*O, reward/done 8.
 ENV_STEP_B = {
-    'bx::env_step_kernel<16, 1, 32, 4>': 1428,  # Ant: N=10, A=8, O=87
-    'bx::env_step_kernel<16, 1, 33, 4>': 2284,  # Humanoid: N=12, A=17, O=240
+    'bx::env_step_kernel<16, 1, 160, 4, 1>': 1428,  # Ant: N=10, A=8, O=87
+    'bx::env_step_kernel<16, 1, 33, 4, 2>': 2284,   # Humanoid: N=12, A=17, O=240
 }
 PHASE_B = {'kinetic_kernel': 80 * 10, 'update_acc_kernel': 72 * 10, 'vproj_kernel': 96 * 10,
            'capsule_plane_kernel': 120 * 5}
