@@ -2910,9 +2910,107 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
     E.red[35] = msum;
   }
   esync<L>();
-  if (obs_out)
-    for (int i = lane; i < obs_size; i += L)
-      obs_out[i] = obs_elem<EK>(c, H, E, kind, flags, i, act, aw, act != nullptr, coef);
+  if (!obs_out) return;
+  if constexpr (EK == EK_ANT) {
+    // the Ant observation (ant.py:257-282) written lane by lane without the
+    // per-element branch chain: lane l holds torso scalar l, joint l's angle
+    // and velocity, and body l's clipped contact vel / ang
+    const int N = H.N, D = H.D;
+    const int x = (flags & BX_OBS_XY) ? 2 : 0;
+    const float* q0 = E.qp;
+    for (int l = lane; l < x + 11; l += L) {
+      // (x, y,) z, rot 4 | vel 3, ang 3
+      const int k = l - x;
+      float v = l < x ? q0[l] : (k < 5 ? q0[2 + k] : q0[7 + (k - 5)]);
+      obs_out[k < 5 ? l : x + 5 + D + (k - 5)] = v;
+    }
+    for (int j = lane; j < D; j += L) {
+      obs_out[x + 5 + j] = E.ang[j];
+      obs_out[x + 11 + D + j] = E.ang[D + j];
+    }
+    if (coef[7] != 0.f)  // use_contact_forces
+      for (int b = lane; b < N; b += L) {
+        const float* a = E.acc + b * ACC_STRIDE;
+        float* o = obs_out + x + 11 + 2 * D + 3 * b;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          o[k] = clip1(a[ACC_ICV + k]);
+          o[3 * N + k] = clip1(a[ACC_ICA + k]);
+        }
+      }
+    return;
+  }
+  if constexpr (EK == EK_HUM && L <= 64) {
+    // the Humanoid / HumanoidStandup observation (humanoid.py:282-334) lane
+    // by lane: torso scalars and joints as Ant's, then lane b writes body b's
+    // cinert (9), com velocity (3) and com angular term (3), and lane a its
+    // actuator's qfrc entries at the exclusive prefix sum of the dofs
+    const int N = H.N, D = H.D, M = N - 1;
+    const int x = (flags & BX_OBS_XY) ? 2 : 0;
+    const float* q0 = E.qp;
+    for (int l = lane; l < x + 11; l += L) {
+      const int k = l - x;
+      float v = l < x ? q0[l] : (k < 5 ? q0[2 + k] : q0[7 + (k - 5)]);
+      obs_out[k < 5 ? l : x + 5 + D + (k - 5)] = v;
+    }
+    for (int j = lane; j < D; j += L) {
+      obs_out[x + 5 + j] = E.ang[j];
+      obs_out[x + 11 + D + j] = E.ang[D + j];
+    }
+    const int base = x + 11 + 2 * D;
+    const v3 com = ld3(E.red + 32);
+    const float msum = E.red[35];
+    for (int b = lane; b < M; b += L) {
+      const int ob = H.o_body + b * BODY_STRIDE;
+      const float mb = c.f(ob + BODY_MASS);
+      const float Ia[3] = {c.f(ob + BODY_I), c.f(ob + BODY_I + 1), c.f(ob + BODY_I + 2)};
+      const v3 d = ld3(E.qp + b * QP_STRIDE) - com;
+      const v3 vb = ld3(E.qp + b * QP_STRIDE + 7);
+      const float nn = norm(d);
+      const float dd[3] = {d.x, d.y, d.z};
+      float* o = obs_out + base + 9 * b;
+#pragma unroll
+      for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int cc = 0; cc < 3; cc++) {
+          float v = mb * (float)(r == cc) * (nn * nn);
+          v += (r == cc ? Ia[r] : 0.f) - dd[r] * dd[cc];
+          o[3 * r + cc] = v;
+        }
+      float* ov = obs_out + base + 9 * M + 3 * b;
+      ov[0] = mb * vb.x / msum;
+      ov[1] = mb * vb.y / msum;
+      ov[2] = mb * vb.z / msum;
+      const v3 cr = cross(d, vb);
+      const float den = 1e-7f + nn * nn;
+      float* oa = obs_out + base + 12 * M + 3 * b;
+      oa[0] = cr.x / den;
+      oa[1] = cr.y / den;
+      oa[2] = cr.z / den;
+    }
+    // qfrc_actuator: unmasked take (index -1 clips to 0), times strength
+    const bool ha = lane < H.K;
+    ActC A{};
+    int dof = 0;
+    if (ha) {
+      A = load_act(c, H, lane);
+      dof = c.i(H.o_joint + A.joint * JOINT_STRIDE + J_DOF);
+    }
+    int off = dof;  // inclusive scan over the env's lanes
+    constexpr int W = L < 64 ? L : 64;
+#pragma unroll
+    for (int sh = 1; sh < W; sh <<= 1) {
+      int t = __shfl_up(off, sh, W);
+      if ((lane % W) >= sh) off += t;
+    }
+    off -= dof;
+    float* oq = obs_out + base + 15 * M + off;
+    for (int i = 0; i < dof; i++)
+      oq[i] = (act ? act[take_idx(A.idx[i], aw)] : 0.f) * A.strength;
+    return;
+  }
+  for (int i = lane; i < obs_size; i += L)
+    obs_out[i] = obs_elem<EK>(c, H, E, kind, flags, i, act, aw, act != nullptr, coef);
 }
 
 // ---------------------------------------------------------------------------
