@@ -401,8 +401,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       B.i(H.o_rgroup + b, r->body_root_group[b]);
     }
   }
-  H.total_words = (int)B.w.size();
-  H.const_words = ((r ? H.o_base : H.total_words) + 3) & ~3;
+  H.const_words = (((r ? H.o_base : (int)B.w.size())) + 3) & ~3;
 
   // per-env LDS layout
   int L = std::max({N, J, K, R, 1});
@@ -426,6 +425,12 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // env programs' System.step action (swimmer: + drag, grasp: 3 palm actions)
   H.xact_words = std::max(16, (d->action_size + 12 + 3) & ~3);
   H.l_xact = carve(H.xact_words);
+  // the action row staged by the env step: every index an actuator or force
+  // reads (jp.take clips into the row, so no read lands past these words)
+  H.act_read = std::max(d->action_size, 1);
+  for (int k = 0; k < 3 * K; k++) H.act_read = std::max(H.act_read, d->act_index[k] + 1);
+  for (int k = 0; k < 3 * d->n_forces; k++) H.act_read = std::max(H.act_read, d->force_index[k] + 1);
+  H.l_arow = carve(H.act_read);
   // the contact regions form each mode's tail: the item-loop / SINGLE
   // kernels keep per-row data and 12-word slots, MULTI mode keeps the row data
   // in registers and needs 8-word slots plus the task partials
@@ -465,6 +470,94 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     for (int a = 0; a < K; a++)
       if (d->act_joint[a] != a) H.act_same = 0;
   }
+  // the SINGLE-mode lane image (pbd_layout.h LI_*): copies of the records
+  // above, so its words are the same bits the item-loop kernels read; a lane
+  // without an item of a kind gets item 0's record (as the kernels' clamped
+  // index did), and zeros where the system has none of that kind
+  if (H.single) {
+    H.o_lane = B.alloc(LANE_W * LANE_IMG_LANES);
+    auto put = [&](int lane, int w, uint32_t v) {
+      B.w[H.o_lane + (w / 4) * 4 * LANE_IMG_LANES + 4 * lane + w % 4] = v;
+    };
+    auto put_joint = [&](int lane, int base, int j) {
+      if (J == 0) return;
+      const uint32_t* s = &B.w[H.o_joint + j * JOINT_STRIDE];
+      const int bp = (int)s[J_BP], bc = (int)s[J_BC];
+      const uint32_t* p = &B.w[H.o_body + bp * BODY_STRIDE];
+      const uint32_t* c = &B.w[H.o_body + bc * BODY_STRIDE];
+      const int ints[6] = {J_TYPE, J_BP, J_BC, J_FREE, J_ANGLE_OFF, J_NANGLES};
+      for (int k = 0; k < 6; k++) put(lane, base + k, s[ints[k]]);
+      put(lane, base + LJ_DAMP, s[J_DAMP]);
+      put(lane, base + LJ_SP, s[J_SP]);
+      put(lane, base + LJ_SA, s[J_SA]);
+      for (int k = 0; k < 3; k++) {
+        put(lane, base + LJ_OFFP + k, s[J_OFFP + k]);
+        put(lane, base + LJ_OFFC + k, s[J_OFFC + k]);
+        put(lane, base + LJ_IP + k, p[BODY_I + k]);
+        put(lane, base + LJ_IC + k, c[BODY_I + k]);
+      }
+      for (int k = 0; k < 9; k++) {
+        put(lane, base + LJ_AXP + k, s[J_AXP + k]);
+        put(lane, base + LJ_AXC + k, s[J_AXC + k]);
+      }
+      for (int k = 0; k < 6; k++) put(lane, base + LJ_LIM + k, s[J_LIM + k]);
+      put(lane, base + LJ_MP, p[BODY_MASS]);
+      put(lane, base + LJ_MC, c[BODY_MASS]);
+    };
+    auto put_act = [&](int lane, int base, int a) {
+      if (K == 0) return;
+      const uint32_t* s = &B.w[H.o_act + a * ACT_STRIDE];
+      put(lane, base + LA_TYPE, s[A_TYPE]);
+      put(lane, base + LA_JOINT, s[A_JOINT]);
+      for (int k = 0; k < 3; k++) put(lane, base + LA_IDX + k, s[A_IDX + k]);
+      put(lane, base + LA_STR, s[A_STR]);
+    };
+    auto put_list = [&](int lane, int base, const std::vector<int>& v, bool has, uint32_t zero) {
+      for (int k = 0; k < 8; k++) put(lane, base + k, has && k < (int)v.size() ? (uint32_t)v[k] : zero);
+    };
+    for (int l = 0; l < LANE_IMG_LANES; l++) {
+      const bool hasB = l < N;
+      const int b = hasB ? l : 0;
+      const uint32_t* s = &B.w[H.o_body + b * BODY_STRIDE];
+      put(l, LI_BODY, s[BODY_MASS]);
+      for (int k = 0; k < 3; k++) {
+        put(l, LI_BODY + 1 + k, s[BODY_I + k]);
+        put(l, LI_BODY + 4 + k, s[BODY_PM + k]);
+        put(l, LI_BODY + 7 + k, s[BODY_RM + k]);
+      }
+      for (int k = 0; k < 4; k++) put(l, LI_BODY + 10 + k, s[BODY_QM + k]);
+      put_joint(l, LI_JOINT, l < J ? l : 0);
+      put_act(l, LI_ACT, l < K ? l : 0);
+      put_joint(l, LI_JOINT_H, (l & 7) < J ? (l & 7) : 0);
+      put_act(l, LI_ACT_H, (l & 7) < K ? (l & 7) : 0);
+      if (R > 0) {
+        const int x = l < R ? l : 0;
+        const uint32_t* w = &B.w[H.o_row + x * ROW_STRIDE];
+        const int ra = (int)w[R_A], rb = (int)w[R_B];
+        const uint32_t* pa = &B.w[H.o_body + ra * BODY_STRIDE];
+        const uint32_t* pb = &B.w[H.o_body + rb * BODY_STRIDE];
+        const int src[24] = {R_GROUP, R_A, R_B, R_FN, R_ONEWAY, R_APOS, R_APOS + 1, R_APOS + 2,
+                             R_AEND, R_AEND + 1, R_AEND + 2, R_ARAD, R_BPOS, R_BPOS + 1, R_BPOS + 2,
+                             R_BEND, R_BEND + 1, R_BEND + 2, R_BRAD, R_FRIC, R_ELAS, R_SCALE, R_THR,
+                             R_ERP};
+        for (int k = 0; k < 24; k++) put(l, LI_ROW + k, w[src[k]]);
+        put(l, LI_ROW + LR_MA, pa[BODY_MASS]);
+        put(l, LI_ROW + LR_MB, pb[BODY_MASS]);
+        for (int k = 0; k < 3; k++) {
+          put(l, LI_ROW + LR_IA + k, pa[BODY_I + k]);
+          put(l, LI_ROW + LR_IB + k, pb[BODY_I + k]);
+        }
+      }
+      put_list(l, LI_JL, jl[b], hasB, (uint32_t)(2 * J));
+      put_list(l, LI_AL, al[b], hasB, (uint32_t)(2 * K));
+      // contact entries carry their collider group in bits 24..30; the padding
+      // entry takes the group of the body's first entry (it adds exact zeros)
+      uint32_t cz = (uint32_t)(2 * R);
+      if (hasB && !cl[b].empty()) cz |= (uint32_t)cl[b][0] & 0x7F000000u;
+      put_list(l, LI_CL, cl[b], hasB, cz);
+    }
+  }
+  H.total_words = (int)B.w.size();
   std::memcpy(B.w.data(), &H, sizeof(BlobHdr));
 
   S->hdr = H;

@@ -77,6 +77,7 @@ struct Env {
   float* nd;     // NearNeighbors candidate distances, stride nds (scratch, before the substeps)
   int nds;
   float* xact;   // the action an env program hands System.step (xact_words)
+  float* arow;   // the env's action row, its first act_read words (env step)
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -1233,6 +1234,7 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi =
   E.nK = H.K;
   E.nR = H.R;
   E.xact = al16(base + H.l_xact);
+  E.arow = al16(base + H.l_arow);
   if (multi) {
     // MULTI: 8-word contact slots and task partials; no row-data region (the
     // row's contact stays in its lane's registers); the task partials double
@@ -1370,6 +1372,16 @@ __device__ __forceinline__ void zero_slots(const Env& E, const BlobHdr& H, int l
 }
 
 // global <-> LDS QP through strided field views
+__device__ __forceinline__ void load_qp_regs(const bx_qp& q, int64_t e, int b, float* s) {
+  const float* p = q.pos.ptr + e * q.pos.env_stride + b * q.pos.body_stride;
+  const float* r = q.rot.ptr + e * q.rot.env_stride + b * q.rot.body_stride;
+  const float* v = q.vel.ptr + e * q.vel.env_stride + b * q.vel.body_stride;
+  const float* a = q.ang.ptr + e * q.ang.env_stride + b * q.ang.body_stride;
+  s[0] = p[0]; s[1] = p[1]; s[2] = p[2];
+  s[3] = r[0]; s[4] = r[1]; s[5] = r[2]; s[6] = r[3];
+  s[7] = v[0]; s[8] = v[1]; s[9] = v[2];
+  s[10] = a[0]; s[11] = a[1]; s[12] = a[2];
+}
 __device__ __forceinline__ void load_qp_global(const bx_qp& q, int64_t e, int b, float* s) {
   const float* p = q.pos.ptr + e * q.pos.env_stride + b * q.pos.body_stride;
   const float* r = q.rot.ptr + e * q.rot.env_stride + b * q.rot.body_stride;
@@ -1814,31 +1826,99 @@ struct Hoist {
   GList<M> jl, al, cl;
 };
 
-template <int M>
-__device__ __forceinline__ void load_hoist(const Cst& c, const BlobHdr& H, int lane, Hoist<M>& X,
-                                           bool jh = false) {
-  // jh (joint halves): lanes j and j + 8 both hold joint j and actuator j
-  const int jx = jh ? (lane & 7) : lane;
+// The lane's hoisted constants from the blob's lane image (pbd_layout.h
+// LI_*): every load independent and unconditional, so the whole set costs one
+// L2 round trip (the records' own layout needs three dependent ones: list
+// offsets -> entries, joint / row -> the bodies it references).
+// JH (joint halves): lanes j and j + 8 both hold joint j and actuator j.
+template <int M, bool JH>
+__device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& H, int lane,
+                                           Hoist<M>& X) {
+  const int jx = JH ? (lane & 7) : lane;
   X.hasB = lane < H.N;
   X.hasJ = jx < H.J;
   X.hasA = jx < H.K;
   X.hasR = lane < H.R;
-  int b = X.hasB ? lane : 0;
-  X.B = load_body(c, H, b);
-  X.jl = load_glist<M>(c, H.o_jl_off, H.o_jl, b, X.hasB, 2 * H.J);
-  X.al = load_glist<M>(c, H.o_al_off, H.o_al, b, X.hasB, 2 * H.K);
-  // contact entries carry their collider group in bits 24..30; the padding
-  // entry takes the group of the body's first entry (it adds exact zeros)
-  int cz = 2 * H.R;
-  {
-    int s0 = c.i(H.o_cl_off + b);
-    int n0 = X.hasB ? c.i(H.o_cl_off + b + 1) - s0 : 0;
-    if (n0 > 0) cz |= c.i(H.o_cl + s0) & 0x7F000000;
+  const uint4* im = reinterpret_cast<const uint4*>(blob + H.o_lane) + lane;
+  uint32_t w[LANE_W];
+  auto grab = [&](int o, int n) {
+#pragma unroll
+    for (int k = 0; k < n; k += 4) {
+      const uint4 v = im[((o + k) / 4) * LANE_IMG_LANES];
+      w[o + k] = v.x; w[o + k + 1] = v.y; w[o + k + 2] = v.z; w[o + k + 3] = v.w;
+    }
+  };
+  constexpr int OJ = JH ? LI_JOINT_H : LI_JOINT, OA = JH ? LI_ACT_H : LI_ACT;
+  grab(LI_BODY, 16);
+  grab(OJ, 48);
+  grab(OA, 8);
+  grab(LI_ROW, 32);
+  grab(LI_JL, M);
+  grab(LI_AL, M);
+  grab(LI_CL, M);
+  auto f = [&](int i) { return __uint_as_float(w[i]); };
+  auto f3 = [&](int i) { return mk(f(i), f(i + 1), f(i + 2)); };
+  auto n = [&](int i) { return (int)w[i]; };
+  X.B.mass = f(LI_BODY);
+  X.B.I = f3(LI_BODY + 1);
+  X.B.pm = f3(LI_BODY + 4);
+  X.B.rm = f3(LI_BODY + 7);
+  X.B.qm = q4{f(LI_BODY + 10), f(LI_BODY + 11), f(LI_BODY + 12), f(LI_BODY + 13)};
+  JointC& J = X.J;
+  J.type = n(OJ + LJ_TYPE);
+  J.bp = n(OJ + LJ_BP);
+  J.bc = n(OJ + LJ_BC);
+  J.free = n(OJ + LJ_FREE);
+  J.angle_off = n(OJ + LJ_AOFF);
+  J.n_angles = n(OJ + LJ_NANG);
+  J.damping = f(OJ + LJ_DAMP);
+  J.sp = f(OJ + LJ_SP);
+  J.sa = f(OJ + LJ_SA);
+  J.off_p = f3(OJ + LJ_OFFP);
+  J.off_c = f3(OJ + LJ_OFFC);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    J.axp[k] = f3(OJ + LJ_AXP + 3 * k);
+    J.axc[k] = f3(OJ + LJ_AXC + 3 * k);
   }
-  X.cl = load_glist<M>(c, H.o_cl_off, H.o_cl, b, X.hasB, cz);
-  if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? jx : 0);
-  if (H.K > 0) X.A = load_act(c, H, X.hasA ? jx : 0);
-  if (H.R > 0) X.R = load_row(c, H, X.hasR ? lane : 0);
+#pragma unroll
+  for (int k = 0; k < 6; k++) J.lim[k] = f(OJ + LJ_LIM + k);
+  J.mp = f(OJ + LJ_MP);
+  J.mc = f(OJ + LJ_MC);
+  J.Ip = f3(OJ + LJ_IP);
+  J.Ic = f3(OJ + LJ_IC);
+  X.A.type = n(OA + LA_TYPE);
+  X.A.joint = n(OA + LA_JOINT);
+#pragma unroll
+  for (int k = 0; k < 3; k++) X.A.idx[k] = n(OA + LA_IDX + k);
+  X.A.strength = f(OA + LA_STR);
+  RowC& R = X.R;
+  R.group = n(LI_ROW + LR_GROUP);
+  R.a = n(LI_ROW + LR_A);
+  R.b = n(LI_ROW + LR_B);
+  R.fn = n(LI_ROW + LR_FN);
+  R.oneway = n(LI_ROW + LR_OW);
+  R.a_pos = f3(LI_ROW + LR_APOS);
+  R.a_end = f3(LI_ROW + LR_AEND);
+  R.a_rad = f(LI_ROW + LR_ARAD);
+  R.b_pos = f3(LI_ROW + LR_BPOS);
+  R.b_end = f3(LI_ROW + LR_BEND);
+  R.b_rad = f(LI_ROW + LR_BRAD);
+  R.fric = f(LI_ROW + LR_FRIC);
+  R.elas = f(LI_ROW + LR_ELAS);
+  R.scale = f(LI_ROW + LR_SCALE);
+  R.thr = f(LI_ROW + LR_THR);
+  R.erp = f(LI_ROW + LR_ERP);
+  R.ma = f(LI_ROW + LR_MA);
+  R.mb = f(LI_ROW + LR_MB);
+  R.Ia = f3(LI_ROW + LR_IA);
+  R.Ib = f3(LI_ROW + LR_IB);
+#pragma unroll
+  for (int k = 0; k < M; k++) {
+    X.jl.e[k] = n(LI_JL + k);
+    X.al.e[k] = n(LI_AL + k);
+    X.cl.e[k] = n(LI_CL + k);
+  }
 }
 
 template <int M>
@@ -3061,6 +3141,9 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
   constexpr bool MU = MODE == MODE_MULTI;
   Env E = carve(ebase + le * H.env_words, H, MU);
   zero_slots(E, H, lane);
+  // SINGLE: the lane image's loads go out before the state's
+  Hoist<M> X;
+  if constexpr (S) load_hoist<M, (F & F_JH) != 0>(A.blob, H, lane, X);
   for (int b = lane; b < H.N; b += L) {
     if (valid) {
       load_qp_global(A.qin, e, b, E.qp + b * QP_STRIDE);
@@ -3081,8 +3164,6 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
     pbd_step_multi<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr,
                             (int)A.act_width, X, io);
   } else if constexpr (S) {
-    Hoist<M> X;
-    load_hoist<M>(c, H, lane, X, (F & F_JH) != 0);
     v3 icv, ica, iaa;
     pbd_step_single<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr,
                              (int)A.act_width, X, icv, ica,
@@ -3157,20 +3238,60 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
   const int kind = P.kind;
   const float* act = valid ? A.act + e * A.act_stride : nullptr;
   const int aw = (int)A.act_width;
-  // every independent load first, so their latencies overlap: the hoisted
-  // constants, the per-env scalars, then the state
+  // every load first, with clamped (unconditional) addresses so their
+  // latencies overlap: the lane image, the per-env scalars, the state and the
+  // first chunk of the action row; an invalid env's lanes read env 0's
+  // (never stored)
+  const int64_t el = valid ? e : 0;
   Hoist<M> X;
-  if constexpr (S) load_hoist<M>(c, H, lane, X, (F & F_JH) != 0);
+  if constexpr (S) load_hoist<M, (F & F_JH) != 0>(A.blob, H, lane, X);
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
-  float done_in = valid ? A.in.done[e] : 0.f;
-  float steps_in = valid && A.in.steps ? A.in.steps[e] : 0.f;
-  for (int b = lane; b < H.N; b += L) {
-    if (valid) {
-      load_qp_global(A.in.qp, e, b, E.qp + b * QP_STRIDE);
-    } else {
-      float* s = E.qp + b * QP_STRIDE;
-      for (int k = 0; k < 13; k++) s[k] = k == 3 ? 1.f : 0.f;
+  float done_in = A.in.done[el];
+  float steps_in = A.in.steps ? A.in.steps[el] : 0.f;
+  if (!valid) done_in = steps_in = 0.f;
+  constexpr int C = L < 64 ? L : 64;  // action-row chunk: one element per lane
+  const float* arow_g = A.act + el * A.act_stride;
+  float a0 = 0.f;
+  if (aw > 0 && lane < C) a0 = arow_g[lane < aw ? lane : aw - 1];
+  if constexpr (S) {
+    // N <= L: the lane's body
+    float qv[13];
+    load_qp_regs(A.in.qp, el, lane < H.N ? lane : 0, qv);
+    if (lane < H.N) {
+      float* s = E.qp + lane * QP_STRIDE;
+#pragma unroll
+      for (int k = 0; k < 13; k++) s[k] = valid ? qv[k] : (k == 3 ? 1.f : 0.f);
     }
+  } else {
+    for (int b = lane; b < H.N; b += L) {
+      if (valid) {
+        load_qp_global(A.in.qp, e, b, E.qp + b * QP_STRIDE);
+      } else {
+        float* s = E.qp + b * QP_STRIDE;
+        for (int k = 0; k < 13; k++) s[k] = k == 3 ? 1.f : 0.f;
+      }
+    }
+  }
+  // the action row through LDS: its first act_read words stay staged (arow:
+  // every index an actuator or force reads, jp.take clipping into the row),
+  // and lane 0 sums the ctrl cost's squares in the reference's order (the
+  // zero padding past the row adds exact zeros)
+  float sq = 0.f;
+  for (int i0 = 0; i0 < aw; i0 += C) {
+    const int i = i0 + lane;
+    float v = a0;
+    if (i0 > 0 && lane < C) v = arow_g[i < aw ? i : aw - 1];
+    if (i >= aw || !valid) v = 0.f;
+    if (lane < C) {
+      E.red[lane] = v;
+      if (i < H.act_read) E.arow[i] = v;
+    }
+    esync<L>();
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < C; k++) sq += E.red[k] * E.red[k];
+    }
+    esync<L>();
   }
   esync<L>();
   float steps = 0.f;
@@ -3178,10 +3299,6 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
   float done = P.auto_reset ? 0.f : done_in;
   float reward_sum = 0.f;
   const int reps = P.episode_length > 0 ? (P.action_repeat > 0 ? P.action_repeat : 1) : 1;
-  // action sum of squares (ctrl cost), shared by every repeat
-  float sq = 0.f;
-  if (valid && lane == 0)
-    for (int i = 0; i < aw; i++) sq += act[i] * act[i];
   BX_KSTAMP(10);
   for (int rep = 0; rep < reps; rep++) {
     v3 pos0 = ld3(E.qp);  // torso position before the step
@@ -3199,9 +3316,9 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
       near0 = -norm(obj - tip);
       dist0 = -norm(obj - goal);
     }
-    // the action System.step reads: the env's own, or its pre-step program's
-    // output in LDS (E.xact)
-    const float* sact = act;
+    // the action System.step reads: the env's own (staged in E.arow), or its
+    // pre-step program's output (E.xact)
+    const float* sact = valid ? E.arow : nullptr;
     int saw = aw;
     float* xact = E.xact;
     if (KIND_IS(BX_ENV_REACHERANGLE)) {

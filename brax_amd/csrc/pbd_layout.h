@@ -90,6 +90,40 @@ struct BlobHdr {
   int32_t env_words_m;               // per-env LDS words in MULTI mode
   int32_t l_xact;                    // LDS: the action an env program hands System.step
   int32_t xact_words;
+  int32_t o_lane;                    // SINGLE mode: the lane image (below); 0 = none
+  int32_t l_arow, act_read;          // LDS: the env's action row, the words any step reads
+};
+
+// SINGLE-mode lane image: for each of 64 lanes, every constant the
+// register-hoisted kernels keep (the lane's body, joint, actuator and contact
+// row records, with the masses / inertias they reference, and its three
+// padded gather lists), so that a lane fetches them with independent 16-byte
+// loads instead of chains of dependent L2 reads (record index -> record ->
+// referenced body). Word w of lane l sits at o_lane + (w / 4) * 256 + 4 * l +
+// w % 4: the 16 lanes of an env read 256 contiguous bytes per load.
+enum {
+  LANE_IMG_LANES = 64,
+  LI_BODY = 0,      // mass, inv inertia 3, pos mask 3, rot mask 3, quat mask 4
+  LI_JOINT = 16,    // the lane's joint (LJ_*): lane j -> joint j
+  LI_ACT = 64,      // the lane's actuator (LA_*)
+  LI_ROW = 72,      // the lane's contact row (LR_*)
+  LI_JL = 104,      // joint, actuator and contact gather lists, 8 entries each
+  LI_AL = 112,
+  LI_CL = 120,
+  LI_JOINT_H = 128, // joint halves: lane l -> joint / actuator l & 7
+  LI_ACT_H = 176,
+  LANE_W = 184
+};
+enum {
+  LJ_TYPE = 0, LJ_BP = 1, LJ_BC = 2, LJ_FREE = 3, LJ_AOFF = 4, LJ_NANG = 5, LJ_DAMP = 6,
+  LJ_SP = 7, LJ_SA = 8, LJ_OFFP = 9, LJ_OFFC = 12, LJ_AXP = 15, LJ_AXC = 24, LJ_LIM = 33,
+  LJ_MP = 39, LJ_MC = 40, LJ_IP = 41, LJ_IC = 44  // 47 words
+};
+enum { LA_TYPE = 0, LA_JOINT = 1, LA_IDX = 2, LA_STR = 5 };
+enum {
+  LR_GROUP = 0, LR_A = 1, LR_B = 2, LR_FN = 3, LR_OW = 4, LR_APOS = 5, LR_AEND = 8,
+  LR_ARAD = 11, LR_BPOS = 12, LR_BEND = 15, LR_BRAD = 18, LR_FRIC = 19, LR_ELAS = 20,
+  LR_SCALE = 21, LR_THR = 22, LR_ERP = 23, LR_MA = 24, LR_MB = 25, LR_IA = 26, LR_IB = 29  // 32
 };
 // MULTI-mode gather tasks: a task sums <= TASK_W contact slots of one body and
 // collider group; a body adds <= BTASK_W task partials (ref = task | group << 24)
