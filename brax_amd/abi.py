@@ -12,7 +12,7 @@ i32p = C.POINTER(C.c_int32)
 f64p = C.POINTER(C.c_double)
 f32p = C.POINTER(C.c_float)
 
-ABI_VERSION = 5  # include/brax_amd.h BX_ABI_VERSION
+ABI_VERSION = 6  # include/brax_amd.h BX_ABI_VERSION
 
 _DESC_FIELDS = [
     ('n_bodies', C.c_int32), ('n_joints', C.c_int32), ('n_actuators', C.c_int32),
@@ -42,6 +42,7 @@ _DESC_FIELDS = [
     ('joint_spring_damping', f64p), ('joint_limit_strength', f64p),
     ('row_ext', f64p), ('row_hm', i32p), ('n_hm', C.c_int32), ('hm_data', f64p),
     ('n_hull', C.c_int32), ('hull_vert', f64p), ('hull_face', f64p), ('hull_norm', f64p),
+    ('row_nn_masked', i32p),
 ]
 
 DYN_PBD, DYN_LEGACY_SPRING = 0, 1
@@ -133,6 +134,8 @@ def make_desc(d):
         v = np.zeros(len(d['col_oneway']))
       elif name == 'row_flat':
         v = -np.ones(len(d['row_group']))
+      elif name == 'row_nn_masked':
+        v = np.zeros(len(d['row_group']))
       elif name.startswith('force_'):
         v = np.zeros(0)
       elif name in _SPRING_FIELDS:

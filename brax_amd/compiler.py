@@ -185,8 +185,11 @@ def _near_neighbors(pairs, index, cutoff):
 
   Mask cells outside U x U follow the jit path: `.at[].set` drops
   out-of-bounds scatter indices (the numpy backend raises IndexError there,
-  e.g. for Ant Mountain(2+)). More cutoff than allowed cells would make top_k
-  return masked (-inf) cells as pairs; that is refused here."""
+  e.g. for Ant Mountain(2+)). With more cutoff than allowed cells, top_k
+  also returns masked (sim = -inf) cells: every allowed cell first, then the
+  masked cells of lowest flat index (jax.lax.top_k keeps equal values in
+  index order). Those cells are rows too, flagged `masked`; the kernels rank
+  them after every allowed cell."""
   uniq, seen = [], {}
   for ca, ca_idx, ba, cb, cb_idx, bb in pairs:
     for c, c_idx, b in ((ca, ca_idx, ba), (cb, cb_idx, bb)):
@@ -196,12 +199,15 @@ def _near_neighbors(pairs, index, cutoff):
   U = len(uniq)
   cells = sorted({(index[ba.name], index[bb.name]) for _, _, ba, _, _, bb in pairs})
   cells = [(i, j) for i, j in cells if i < U and j < U]
-  if cutoff > len(cells):
-    raise NotImplementedError(f'collider_cutoff {cutoff} exceeds the {len(cells)} allowed '
-                              'NearNeighbors cells (top_k would pick masked cells)')
-  rows = [(uniq[i][0], uniq[i][1], uniq[i][2], uniq[j][0], uniq[j][1], uniq[j][2])
-          for i, j in cells]
-  return dict(pairs=rows, flat=[i * U + j for i, j in cells], cutoff=int(cutoff))
+  allowed = {i * U + j for i, j in cells}
+  if cutoff > U * U:
+    raise ValueError(f'collider_cutoff {cutoff} exceeds the {U * U} NearNeighbors cells')
+  extra = [f for f in range(U * U) if f not in allowed][:max(cutoff - len(cells), 0)]
+  flat = sorted(allowed | set(extra))
+  rows = [(uniq[f // U][0], uniq[f // U][1], uniq[f // U][2],
+           uniq[f % U][0], uniq[f % U][1], uniq[f % U][2]) for f in flat]
+  return dict(pairs=rows, flat=flat, masked=[int(f not in allowed) for f in flat],
+              cutoff=int(cutoff))
 
 
 _BOX_CORNERS = np.array(list(itertools.product((-1, 1), (-1, 1), (-1, 1))), np.float64)
@@ -368,7 +374,7 @@ def _colliders(config, index):
              col_baumgarte_erp=[])
   rows = {k: [] for k in ('group', 'body_a', 'body_b', 'a_pos', 'a_end',
                           'a_radius', 'b_pos', 'b_end', 'b_radius', 'friction',
-                          'elasticity', 'flat', 'ext', 'hm')}
+                          'elasticity', 'flat', 'nn_masked', 'ext', 'hm')}
   hm_data = []
   hulls = {}  # (body name, collider index) -> hull index (HullBox data)
   hull_vert, hull_face, hull_norm = [], [], []
@@ -426,6 +432,7 @@ def _colliders(config, index):
           if len(e) == 1:
             e.append(e[0])
     flats = g.get('flat', [-1] * len(g['pairs']))
+    masked = g.get('masked', [0] * len(g['pairs']))
     for pi, (ca, _, ba, cb, _, bb) in enumerate(g['pairs']):
       fa = ca.material.friction * cb.material.friction
       ea = ca.material.elasticity * cb.material.elasticity
@@ -466,6 +473,7 @@ def _colliders(config, index):
         rows['ext'].append(ext[ei])
         rows['hm'].append(hm)
         rows['flat'].append(flats[pi])
+        rows['nn_masked'].append(masked[pi])
         rows['group'].append(gi)
         rows['body_a'].append(index[ba.name])
         rows['body_b'].append(index[bb.name])
@@ -489,8 +497,10 @@ def _colliders(config, index):
   d['hull_vert'] = np.asarray(hull_vert, np.float64).reshape(-1, 8, 3)
   d['hull_face'] = np.asarray(hull_face, np.float64).reshape(-1, 6, 4, 3)
   d['hull_norm'] = np.asarray(hull_norm, np.float64).reshape(-1, 6, 3)
+  if not any(rows['nn_masked']):
+    rows.pop('nn_masked')  # the key exists only where a masked cell is a row
   for k, v in rows.items():
-    if k in ('group', 'body_a', 'body_b', 'flat'):
+    if k in ('group', 'body_a', 'body_b', 'flat', 'nn_masked'):
       d['row_' + k] = np.asarray(v, np.int32)
     elif k.endswith(('pos', 'end')):
       d['row_' + k] = np.asarray(v, np.float64).reshape(-1, 3)

@@ -134,12 +134,17 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     int n = 0, last = -1;
     for (int x = 0; x < R; x++) {
       if (d->row_group[x] != g) continue;
+      // a masked cell ranks after every allowed one: only where cutoff needs it
       if (d->row_flat[x] <= last) return fail("culled rows must be in increasing flat order");
       last = d->row_flat[x];
       n++;
     }
     if (d->col_cutoff[g] > n) return fail("collider cutoff exceeds the group's rows");
   }
+  if (d->row_nn_masked)
+    for (int x = 0; x < R; x++)
+      if (d->row_nn_masked[x] && !d->col_cutoff[d->row_group[x]])
+        return fail("masked NearNeighbors rows belong to culled groups");
   if (2 * R >= (1 << 24)) return fail("too many contact rows");
 
   Builder B;
@@ -234,6 +239,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     B.f(o + R_ERP, d->col_baumgarte_erp[g]);
     if (d->row_ext)
       for (int k = 0; k < 16; k++) B.f(o + R_X + k, d->row_ext[16 * x + k]);
+    B.i(o + R_NNMASK, d->row_nn_masked && d->row_nn_masked[x] ? 1 : 0);
     if (d->col_fn[g] == BX_COL_HEIGHTMAP) {
       B.i(o + R_HM_OFF, d->row_hm[2 * x]);
       B.i(o + R_HM_M, d->row_hm[2 * x + 1]);

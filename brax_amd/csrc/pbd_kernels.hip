@@ -1307,7 +1307,9 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
       QP a = ldqp(E.qp + ba * QP_STRIDE), b = ldqp(E.qp + bb * QP_STRIDE);
       v3 pa = a.pos + rotate(c.f3(o + R_APOS), a.rot);
       v3 pb = b.pos + rotate(c.f3(o + R_BPOS), b.rot);
-      E.nd[r * E.nds] = norm(pb - pa);
+      // a masked cell's sim is -inf: its key (+inf's bits) sorts after every
+      // finite distance, ties in row = flat order as jax.lax.top_k keeps them
+      E.nd[r * E.nds] = c.i(o + R_NNMASK) ? __uint_as_float(0x7F800000u) : norm(pb - pa);
     }
     esync<L>();
     for (int k = 0; k < cut; k++) {

@@ -36,6 +36,8 @@ enum {
   // extended contact functions (bx_desc row_ext): 16 floats, then the height
   // map's word offset (from o_hm) and mesh size
   R_X = 24, R_HM_OFF = 40, R_HM_M = 41,
+  // a NearNeighbors cell outside the allowed mask (top_k's -inf tail)
+  R_NNMASK = 42,
 };
 enum {
   FK_STRIDE = 24,

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 5
+#define BX_ABI_VERSION 6
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
 enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
@@ -170,6 +170,12 @@ typedef struct bx_desc {
   const double* hull_vert;         /* [H,8,3] corners */
   const double* hull_face;         /* [H,6,4,3] quads, winding fixed */
   const double* hull_norm;         /* [H,6,3] face normals */
+  /* NearNeighbors with more `cutoff` than allowed cells: top_k of the
+   * masked (-inf) cells picks the lowest flat indices (jax.lax.top_k keeps
+   * ties in index order), so those cells are rows too, flagged 1 here; they
+   * rank after every allowed cell, in flat order (colliders.py:78-85).
+   * NULL = no masked rows. */
+  const int32_t* row_nn_masked;    /* [R] */
 } bx_desc;
 
 /*

@@ -164,7 +164,7 @@ def dump_desc(sys_):
   goneway, gfn, gscale, gthr, gerp = [], [], [], [], []
   rows = {k: [] for k in ('group', 'body_a', 'body_b', 'a_pos', 'a_end', 'a_radius',
                           'b_pos', 'b_end', 'b_radius', 'friction', 'elasticity', 'flat',
-                          'ext', 'hm')}
+                          'nn_masked', 'ext', 'hm')}
   hm_data = []
   hull_ix, hull_v, hull_f, hull_n = {}, [], [], []
   gcut = []
@@ -176,6 +176,11 @@ def dump_desc(sys_):
       off = np.asarray(c.cull.dist_off)
       U = off.shape[1]
       cells = np.flatnonzero(np.isfinite(off.ravel()))
+      # more cutoff than allowed cells: top_k's tail is the masked (-inf)
+      # cells of lowest flat index (jax.lax.top_k's order for equal values)
+      extra = np.flatnonzero(~np.isfinite(off.ravel()))[:max(int(c.cull.cutoff) - len(cells), 0)]
+      cells = np.sort(np.concatenate([cells, extra]))
+      nn_masked = list((~np.isfinite(off.ravel()[cells])).astype(int))
       ia, ib = cells // U, cells % U
       from brax import jumpy as jp
       ca, cb = jp.take(cand_a, ia), jp.take(cand_b, ib)
@@ -184,6 +189,7 @@ def dump_desc(sys_):
     else:
       ca, cb = c.cull.get()
       flats = None
+      nn_masked = None
       gcut.append(0)
     goneway.append(1 if isinstance(c, rc.OneWayCollider) else 0)
     fn = c.contact_fn.__name__
@@ -234,6 +240,7 @@ def dump_desc(sys_):
         rows['ext'].append(ext[ei])
         rows['hm'].append(hm)
         rows['flat'].append(-1 if flats is None else int(flats[p]))
+        rows['nn_masked'].append(0 if nn_masked is None else int(nn_masked[p]))
         rows['group'].append(g)
         rows['body_a'].append(ca.body.idx[p])
         rows['body_b'].append(cb.body.idx[p])
@@ -258,7 +265,9 @@ def dump_desc(sys_):
   d['hull_vert'] = np.asarray(hull_v, np.float64).reshape(-1, 8, 3)
   d['hull_face'] = np.asarray(hull_f, np.float64).reshape(-1, 6, 4, 3)
   d['hull_norm'] = np.asarray(hull_n, np.float64).reshape(-1, 6, 3)
-  ints = ('group', 'body_a', 'body_b', 'flat')
+  ints = ('group', 'body_a', 'body_b', 'flat', 'nn_masked')
+  if not any(rows['nn_masked']):
+    rows.pop('nn_masked')  # the key exists only where a masked cell is a row
   for k, v in rows.items():
     if k in ints:
       d['row_' + k] = np.asarray(v, np.int32)
@@ -452,6 +461,28 @@ def capsule_sys(kind):
   if kind == 'cull':
     config.collider_cutoff = 1
   return brax.System(config), (0 if kind == 'ground' else 1)
+
+
+class stable_top_k:
+  """jumpy.top_k's numpy path with jax.lax.top_k's order for equal values
+  (lower index first); the numpy path (argpartition + argsort) picks among
+  ties arbitrarily, which decides WHICH masked NearNeighbors cells a cutoff
+  past the allowed cells returns. Used for twin_cull only."""
+
+  def __enter__(self):
+    from brax import jumpy
+    self.jp, self.orig = jumpy, jumpy.top_k
+
+    def top_k(operand, k):
+      if jumpy._which_np(operand) is not np:  # pylint: disable=protected-access
+        return self.orig(operand, k)
+      idx = np.argsort(-np.asarray(operand), kind='stable')[:k]
+      return operand[idx], idx
+    jumpy.top_k = top_k
+    return self
+
+  def __exit__(self, *exc):
+    self.jp.top_k = self.orig
 
 
 def wrapped_ant(n_envs=8, n_steps=6, episode_length=3):
@@ -679,6 +710,13 @@ def main():
       'box_box': (scenes.box_box_config(0.05, 20), 0, 10),
       'box_capsule_hull': (scenes.BOX_CAPSULE_TEST_CONFIG, 1, 3),
   }
+  # NearNeighbors with more cutoff than allowed cells (colliders.py:78-85):
+  # run under jax.lax.top_k's tie order
+  if want('twin_cull'):
+    s = brax.System(text_format.Parse(scenes.TWIN_CULL_CONFIG, brax.Config()))
+    save('desc_twin_cull', dump_desc(s))
+    with stable_top_k():
+      save('traj_twin_cull', sys_traj(s, 'twin_cull', s.default_qp(), 1, 4, 1.0, 0))
   for name, (txt, di, T) in point_scenes.items():
     if want(name):
       s = brax.System(text_format.Parse(txt, brax.Config()))

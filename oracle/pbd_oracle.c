@@ -1589,6 +1589,9 @@ static void nn_select(const sysc* s, work_t* w) {
         rotate(s->rb_pos + 3 * r, b->rot, pb);
         for (int i = 0; i < 3; i++) da[i] = (b->pos[i] + pb[i]) - (a->pos[i] + pa[i]);
         R dist = (R)sqrt(da[0] * da[0] + da[1] * da[1] + da[2] * da[2]);
+        /* a masked cell (more cutoff than allowed cells): sim = -inf, after
+         * every finite cell, ties to the lower flat index (colliders.py:78-85) */
+        if (d->row_nn_masked && d->row_nn_masked[r]) dist = (R)INFINITY;
         if (best < 0 || dist < bd) { best = r; bd = dist; }
       }
       w->ract[best] = k;

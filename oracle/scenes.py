@@ -204,3 +204,23 @@ defaults {{
   qps {{ name: "box2" pos {{ x: 0.1 y: 1 z: .49 }} rot {{x: 7 y: 4 z: 45}} vel {{ z: -0.3 }} }}
 }}
 """
+
+
+# NearNeighbors past its allowed cells (colliders.py:55-89, 1005-1013): two
+# bodies with two capsules each give 4 capsule-capsule pairs (> cutoff 3, so
+# the group is culled) over U = 4 candidates, but the mask is set with BODY
+# indices, so it allows one cell only, (0, 1). top_k(3) then also returns
+# the two masked (-inf) cells of lowest flat index: (0, 0), a capsule against
+# itself, and (0, 2).
+TWIN_CULL_CONFIG = """
+dt: 0.5 substeps: 50 friction: 0.6 gravity { z: -9.8 }
+bodies { name: "A" mass: 1 inertia { x: 1 y: 1 z: 1 }
+  colliders { capsule { radius: 0.25 length: 1.0 } }
+  colliders { position { x: 0.5 } rotation { y: 90 } capsule { radius: 0.2 length: 0.8 } } }
+bodies { name: "B" mass: 1 inertia { x: 1 y: 1 z: 1 }
+  colliders { capsule { radius: 0.25 length: 1.0 } }
+  colliders { position { y: 0.5 } rotation { x: 90 } capsule { radius: 0.2 length: 0.8 } } }
+bodies { name: "Ground" frozen { all: true } colliders { plane {} } }
+collider_cutoff: 3
+defaults { qps { name: "A" pos { z: 1 } } qps { name: "B" pos { x: 0.3 y: 0.2 z: 1.5 } } }
+"""

@@ -33,6 +33,10 @@ defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { x:
 defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { z: 2 } } qps { name: "Capsule3" pos { x: 3 z: 1 } } qps { name: "Capsule4" pos { x: 5 z: 1 } } }
 """
 CAPSULES = ['capsule_ground', 'capsule_capsule', 'capsule_cull']
+# NearNeighbors with more cutoff than allowed cells: top_k also returns
+# masked cells (oracle/scenes.py TWIN_CULL_CONFIG; golden generated under
+# jax.lax.top_k's tie order)
+NN_MASKED = ['twin_cull']
 # legacy_spring systems (`_SYSTEM_CONFIG_SPRING`, system.py:342-390): envs with
 # the kernel env layer, and physics rollouts of the other registered envs
 SPRING_ENVS = ['ant_spring', 'humanoid_spring', 'halfcheetah_spring', 'humanoidstandup_spring']
@@ -148,6 +152,9 @@ def config_for(name):
     from oracle import scenes
     return cfgmod.parse(scenes.BOX_TEST_CONFIG if name.startswith('box')
                         else scenes.mesh_test_config())
+  if name == 'twin_cull':
+    from oracle import scenes
+    return cfgmod.parse(scenes.TWIN_CULL_CONFIG)
   if name == 'mountain1nn':
     cfg = ant_mountain_config(1)
     cfg.collider_cutoff = 9

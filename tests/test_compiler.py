@@ -4,11 +4,11 @@ import pytest
 
 from brax_amd import compiler
 from tests.conftest import golden
-from tests.helpers import (CAPSULES, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL, compiled,
+from tests.helpers import (CAPSULES, NN_MASKED, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL, compiled,
                            config_for)
 
 NAMES = (['ant', 'humanoid', 'halfcheetah', 'humanoidstandup', 'mountain1', 'mountain2', 'mountain4', 'mountain1nn']
-         + ROBOTS + CAPSULES + POINTS + SPRING_ENVS + SPRING_ROBOTS + XCOL)
+         + ROBOTS + CAPSULES + NN_MASKED + POINTS + SPRING_ENVS + SPRING_ROBOTS + XCOL)
 
 
 @pytest.mark.parametrize('name', NAMES)
@@ -100,7 +100,20 @@ def test_near_neighbors_cells():
   # ant without cutoff: every group is Pairs
   _, d0, _ = compiler.compile_system(config_for('ant'))
   assert (d0['col_cutoff'] == 0).all() and (d0['row_flat'] == -1).all()
-  # more cutoff than allowed cells is refused (top_k would pick masked cells)
-  cfg.collider_cutoff = int(rows.sum()) + 1  # still < the 153 pairs: culled
-  with pytest.raises(NotImplementedError):
-    compiler.compile_system(cfg)
+  # more cutoff than allowed cells (still < the 153 pairs: culled): top_k's
+  # tail is the masked cells of lowest flat index, flagged
+  n = int(rows.sum())
+  cfg.collider_cutoff = n + 3
+  _, d2, _ = compiler.compile_system(cfg)
+  rows2 = d2['row_group'] == g
+  m = d2['row_nn_masked'][rows2]
+  assert m.sum() == 3 and rows2.sum() == n + 3
+  flat2 = d2['row_flat'][rows2]
+  assert (np.diff(flat2) > 0).all()
+  allowed = set(flat.tolist())
+  masked = [f for f in range(U * U) if f not in allowed][:3]
+  assert sorted(flat2[m == 1].tolist()) == masked
+  # a cutoff at or past the pairs is no culling at all (colliders.py:1003-1005)
+  cfg.collider_cutoff = 153
+  _, d3, _ = compiler.compile_system(cfg)
+  assert (d3['col_cutoff'] == 0).all()

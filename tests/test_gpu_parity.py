@@ -22,14 +22,14 @@ import torch
 
 from tests.conftest import golden
 from tests.margins import record_margin
-from tests.helpers import (CAPSULES, ENVTRAJ_KERNEL, POINTS, QP_FIELDS, ROBOTS, SPRING_ENVS,
+from tests.helpers import (CAPSULES, NN_MASKED, ENVTRAJ_KERNEL, POINTS, QP_FIELDS, ROBOTS, SPRING_ENVS,
                            SPRING_ROBOTS, XCOL, XY_ENVS, compiled, env_golden, env_kind,
                            golden_reset_qp, normwise, obs_flags, prep_oracle, reset_bodies)
 
 pytestmark = pytest.mark.gpu
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
-SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + POINTS
+SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + NN_MASKED + POINTS
             + SPRING_ROBOTS + XCOL)
 POS_TOL = 1e-5
 

@@ -9,12 +9,12 @@ import numpy as np
 import pytest
 
 from tests.conftest import golden
-from tests.helpers import (CAPSULES, ENVTRAJ_KERNEL, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS,
+from tests.helpers import (CAPSULES, NN_MASKED, ENVTRAJ_KERNEL, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS,
                            XCOL, XY_ENVS, env_coef, env_golden, golden_reset_qp, prep_oracle,
                            compiled, env_kind, obs_flags)
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
-SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + POINTS
+SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + NN_MASKED + POINTS
             + SPRING_ROBOTS + XCOL)
 
 
