@@ -437,6 +437,14 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   for (int k = 0; k < 3 * K; k++) H.act_read = std::max(H.act_read, d->act_index[k] + 1);
   for (int k = 0; k < 3 * d->n_forces; k++) H.act_read = std::max(H.act_read, d->force_index[k] + 1);
   H.l_arow = carve(H.act_read);
+  // NearNeighbors: each wave's sorted picks (64-bit keys) when an env spans
+  // up to 4 waves
+  {
+    int max_cut = 0;
+    for (int g = 0; g < G; g++) max_cut = std::max(max_cut, d->col_cutoff[g]);
+    H.nnl_words = 2 * 4 * max_cut;
+    H.l_nnl = carve(H.nnl_words);
+  }
   // the contact regions form each mode's tail: the item-loop / SINGLE
   // kernels keep per-row data and 12-word slots, MULTI mode keeps the row data
   // in registers and needs 8-word slots plus the task partials
@@ -1054,7 +1062,9 @@ int bx_phase_capsule_plane(bx_system* S, int64_t n_envs, int64_t plane, const fl
 }
 
 int bx_debug_stamps(unsigned long long* out, int reset) {
-  HIP_OK(debug_stamps(out, reset));
+  // bit 1 of reset selects the MULTI-mode stamps (BX_MSTAMPS build)
+  if (reset & 2) HIP_OK(debug_mstamps(out, reset & 1));
+  else HIP_OK(debug_stamps(out, reset));
   return 0;
 }
 

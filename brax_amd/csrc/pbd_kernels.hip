@@ -26,6 +26,10 @@
 #if !defined(BX_TU_FAST)
 #undef BX_STAMPS
 #endif
+// ... and the MULTI-mode ones in the item-loop translation unit only
+#if !defined(BX_TU_GENERIC)
+#undef BX_MSTAMPS
+#endif
 
 namespace bx {
 
@@ -78,6 +82,7 @@ struct Env {
   int nds;
   float* xact;   // the action an env program hands System.step (xact_words)
   float* arow;   // the env's action row, its first act_read words (env step)
+  float* nnl;    // NearNeighbors per-wave pick lists (nnl_words)
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -1235,6 +1240,7 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi =
   E.nR = H.R;
   E.xact = al16(base + H.l_xact);
   E.arow = al16(base + H.l_arow);
+  E.nnl = al16(base + H.l_nnl);
   if (multi) {
     // MULTI: 8-word contact slots and task partials; no row-data region (the
     // row's contact stays in its lane's registers); the task partials double
@@ -1279,6 +1285,58 @@ __device__ __forceinline__ void zero_row_slots(const Env& E, int r) {
 // env's current qp: candidate-centre distance of each allowed cell, then the
 // `cutoff` nearest cells get ranks 0.. (top_k of -dist; equal distances to the
 // lower flat index = row index, as jax.lax.top_k). Ranks go to E.ract.
+// min of v over the env's lanes of one wave: W = 16 (a DPP row), 32 or 64
+// (the rows combined through readlane), in every lane of the segment. Every
+// lane of the wave must be active. (A one-pass 64-bit variant with row
+// broadcasts measured slower: 31.7k vs 28.7k cycles of picks per step.)
+template <int W>
+__device__ __forceinline__ unsigned seg_min_u32(unsigned v) {
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false));  // row_ror:2
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, false));  // row_ror:1
+  if constexpr (W == 16) {
+    return v;
+  } else {
+    const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 0);
+    const unsigned b = (unsigned)__builtin_amdgcn_readlane((int)v, 16);
+    const unsigned c2 = (unsigned)__builtin_amdgcn_readlane((int)v, 32);
+    const unsigned d = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+    if constexpr (W == 32) return (threadIdx.x & 32) ? min(c2, d) : min(a, b);
+    return min(min(a, b), min(c2, d));
+  }
+}
+
+// a candidate cell's selection key: (distance bits, row); distances are >= 0,
+// so their bit patterns order like the floats; a masked cell's sim is -inf,
+// its key (+inf's bits) sorts after every finite distance, ties in row =
+// flat order as jax.lax.top_k keeps them
+__device__ __forceinline__ unsigned long long nn_key(const Cst& c, const BlobHdr& H, const Env& E,
+                                                     int r) {
+  const int o = H.o_row + r * ROW_STRIDE;
+  unsigned d = 0x7F800000u;
+  if (!c.i(o + R_NNMASK)) {
+    const int ba = c.i(o + R_A), bb = c.i(o + R_B);
+    QP a = ldqp(E.qp + ba * QP_STRIDE), b = ldqp(E.qp + bb * QP_STRIDE);
+    v3 pa = a.pos + rotate(c.f3(o + R_APOS), a.rot);
+    v3 pb = b.pos + rotate(c.f3(o + R_BPOS), b.rot);
+    d = __float_as_uint(norm(pb - pa));
+  }
+  return ((unsigned long long)d << 32) | (unsigned)r;
+}
+
+// NearNeighbors.update (colliders.py:71-85) for every culled group, from the
+// env's current qp: candidate-centre distance of each allowed cell, then the
+// `cutoff` nearest cells get ranks 0.. (top_k of -dist; equal distances to the
+// lower flat index = row index, as jax.lax.top_k). Ranks go to E.ract, the
+// selected rows in Info order to E.alist.
+//
+// Each lane holds its (<= NK) candidates' keys sorted in registers; the
+// env's part in each wave picks its `cutoff` smallest keys by DPP minima
+// (no LDS, no barrier per pick); with one wave per env those are the ranks,
+// with several, each wave's sorted list goes to LDS and every listed key
+// counts the smaller keys of the other lists (its rank in the union).
+// Groups with more than NK candidates per lane take the serial pick.
 template <int L>
 __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane) {
   // Pairs rows are always active (rank 0) at their fixed Info index; culled
@@ -1294,27 +1352,90 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
     }
   }
   esync<L>();
+  constexpr int W = L < 64 ? L : 64;  // the env's lanes in one wave
+  constexpr int NW = L / W;           // the env's waves
+  constexpr int NK = 4;               // candidates per lane held in registers
+  const int wl = lane % W;            // lane within the env's part of its wave
+  const int wv = lane / W;            // the env's wave
   for (int g = 0; g < H.G; g++) {
     const int og = H.o_group + g * GROUP_STRIDE;
     const int cut = c.i(og + G_CUT);
     if (cut == 0) continue;
-    const int r0 = c.i(og + G_R0), r1 = c.i(og + G_R1);
-    // candidate-centre distance of every cell, once (E.nd: scratch until the
-    // position pass of the first substep)
+    const int r0 = c.i(og + G_R0), r1 = c.i(og + G_R1), info = c.i(og + G_INFO);
+    if (r1 - r0 <= NK * L && (NW == 1 || 2 * NW * cut <= H.nnl_words)) {
+      unsigned long long k[NK];
+#pragma unroll
+      for (int i = 0; i < NK; i++) {
+        const int r = r0 + lane + i * L;
+        k[i] = r < r1 ? nn_key(c, H, E, r) : ~0ull;
+      }
+      // sorting network on the lane's keys
+      auto cs = [](unsigned long long& a, unsigned long long& b) {
+        const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
+        a = lo;
+        b = hi;
+      };
+      cs(k[0], k[1]); cs(k[2], k[3]); cs(k[0], k[2]); cs(k[1], k[3]); cs(k[1], k[2]);
+      unsigned long long* lst = reinterpret_cast<unsigned long long*>(E.nnl);
+      for (int kk = 0; kk < cut; kk++) {
+        const unsigned long long cur = k[0];
+        const unsigned hi = (unsigned)(cur >> 32), lo = (unsigned)cur;
+        // the segment's smallest key: its distance, then its row among equals
+        const unsigned dmin = seg_min_u32<W>(hi);
+        const unsigned rmin = seg_min_u32<W>(hi == dmin ? lo : ~0u);
+        const bool own = cur != ~0ull && hi == dmin && lo == rmin;
+        if (own) {
+          // the picked key leaves the lane's sorted registers
+          k[0] = k[1]; k[1] = k[2]; k[2] = k[3]; k[3] = ~0ull;
+          if constexpr (NW == 1) {
+            E.ract[(int)lo] = kk;
+            E.alist[info + kk] = (int)lo;
+          }
+        }
+        if constexpr (NW > 1) {
+          if (wl == 0) lst[wv * cut + kk] = ((unsigned long long)dmin << 32) | rmin;
+        }
+      }
+      if constexpr (NW > 1) {
+        esync<L>();
+        for (int t = lane; t < NW * cut; t += L) {
+          const int w = t / cut, i = t % cut;
+          const unsigned long long key = lst[t];
+          if (key == ~0ull) continue;
+          // + the smaller keys of each other (sorted) list: branch-free lower
+          // bounds, the lists' probes issued together
+          int base[NW];
+#pragma unroll
+          for (int w2 = 0; w2 < NW; w2++) base[w2] = w2 * cut;
+          for (int len = cut; len > 1;) {
+            const int half = len >> 1;
+#pragma unroll
+            for (int w2 = 0; w2 < NW; w2++)
+              base[w2] = lst[base[w2] + half - 1] < key ? base[w2] + half : base[w2];
+            len -= half;
+          }
+          int rank = i;
+#pragma unroll
+          for (int w2 = 0; w2 < NW; w2++)
+            if (w2 != w) rank += base[w2] - w2 * cut + (lst[base[w2]] < key ? 1 : 0);
+          if (rank < cut) {
+            E.ract[(int)(unsigned)key] = rank;
+            E.alist[info + rank] = (int)(unsigned)key;
+          }
+        }
+      }
+      esync<L>();
+      continue;
+    }
+    // serial pick: candidate-centre distance of every cell, once (E.nd:
+    // scratch until the position pass of the first substep), then `cut`
+    // minima over the env's lanes
     for (int r = r0 + lane; r < r1; r += L) {
-      const int o = H.o_row + r * ROW_STRIDE;
-      const int ba = c.i(o + R_A), bb = c.i(o + R_B);
-      QP a = ldqp(E.qp + ba * QP_STRIDE), b = ldqp(E.qp + bb * QP_STRIDE);
-      v3 pa = a.pos + rotate(c.f3(o + R_APOS), a.rot);
-      v3 pb = b.pos + rotate(c.f3(o + R_BPOS), b.rot);
-      // a masked cell's sim is -inf: its key (+inf's bits) sorts after every
-      // finite distance, ties in row = flat order as jax.lax.top_k keeps them
-      E.nd[r * E.nds] = c.i(o + R_NNMASK) ? __uint_as_float(0x7F800000u) : norm(pb - pa);
+      const unsigned long long key = nn_key(c, H, E, r);
+      E.nd[r * E.nds] = __uint_as_float((unsigned)(key >> 32));
     }
     esync<L>();
     for (int k = 0; k < cut; k++) {
-      // the lane's nearest unselected cell, as a (distance bits, row) key:
-      // distances are >= 0, so their bit patterns order like the floats
       unsigned long long best = ~0ull;
       for (int r = r0 + lane; r < r1; r += L) {
         if (E.ract[r] >= 0) continue;
@@ -1323,7 +1444,6 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
         best = key < best ? key : best;
       }
       // minimum over the env's L lanes (aligned L-lane segment of the wave)
-      constexpr int W = L < 64 ? L : 64;
 #pragma unroll
       for (int off = W / 2; off > 0; off >>= 1) {
         unsigned lo = __shfl_xor((unsigned)best, off, W);
@@ -1343,14 +1463,13 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
       const int r = (int)(best & 0xFFFFFFFFu);
       if (((r - r0) % L) == lane) {
         E.ract[r] = k;
-        E.alist[c.i(og + G_INFO) + k] = r;
+        E.alist[info + k] = r;
       }
       esync<L>();
     }
   }
 }
 
-// 1 if row r takes part this step (every Pairs row; culled rows by rank)
 __device__ __forceinline__ bool row_active(const BlobHdr& H, const Env& E, int r) {
   return H.n_nn == 0 || E.ract[r] >= 0;
 }
@@ -2378,9 +2497,30 @@ struct RowInfoOut {
   float* pen;
 };
 
+#ifdef BX_MSTAMPS
+// MULTI-mode phase stamps of each workgroup's first wave (diagnostic build)
+__device__ unsigned long long bx_mstamp_wave[4096][16];
+#define BX_MSTAMP(k)                                                               \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long _t;                                                         \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    ms_acc[k] += _t - ms_last;                                                     \
+    ms_last = _t;                                                                  \
+  } while (0)
+#else
+#define BX_MSTAMP(k) do {} while (0)
+#endif
+
 template <int L, int F, int MR>
 __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
                                const float* act, int aw, const HoistM<MR>& X, RowInfoOut io) {
+#ifdef BX_MSTAMPS
+  unsigned long long ms_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ms_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ms_last)::"memory");
+#endif
   const float h = H.h;
   const v3 g = mk(H.gx, H.gy, H.gz);
   float* myqp = E.qp + lane * QP_STRIDE;
@@ -2402,6 +2542,19 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
   // NearNeighbors.update once per step (system.py:320-321): ranks in E.ract,
   // culled rows' slots zeroed (their lanes skip them below)
   if (H.n_nn) nn_select<L>(c, H, E, lane);
+  BX_MSTAMP(9);
+  // the lane's rows: the m-th is active row x = lane + m * L in Info order
+  // (the culled scenes' selected rows compacted: E.alist), so lanes past
+  // the active count, and whole waves, skip the contact passes
+#if defined(BX_MULTI_HOIST_ROWS)
+  const int nact = H.R;  // hoisted rows are fixed per lane: no compaction
+#define BX_MULTI_RX(x) (x)
+#define BX_MULTI_SKIP(x, r) ((x) >= H.R || !row_active(H, E, r))
+#else
+  const int nact = H.n_nn ? H.info_rows : H.R;
+#define BX_MULTI_RX(x) (H.n_nn ? E.alist[x] : (x))
+#define BX_MULTI_SKIP(x, r) ((x) >= nact)
+#endif
   // the row's contact between the position and velocity passes
   v3 cpos[MR], cn[MR];
   float pen[MR], dl[MR];
@@ -2437,6 +2590,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
         st_v3a(E.jslot + (E.nJ + lane) * SLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
       }
       esync<L>();
+      BX_MSTAMP(0);
       // Euler.update(acc) + Euler.kinetic (integrators.py:50-93)
       if (X.hasB) {
         v3 dpa = gsum3(X.al, E.aslot, ASLOT_STRIDE);
@@ -2456,6 +2610,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
         dpa_last = dpa;
       }
       esync<L>();
+      BX_MSTAMP(1);
       // Joint.apply (joints.py:79-100)
       if (X.hasJ) {
         const JointC& Jc = X.J;
@@ -2467,6 +2622,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
         st_slot(E.jslot + (E.nJ + lane) * SLOT_STRIDE, dcp, dcr, 0.f);
       }
       esync<L>();
+      BX_MSTAMP(2);
       // Euler.update(pos) (+ velocity_projection on the first substep)
       if (X.hasB) {
         v3 dp = mk(0.f, 0.f, 0.f);
@@ -2487,13 +2643,15 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
         stqp(myqp, q);
       }
       esync<L>();
+      BX_MSTAMP(3);
     }
     // ---- collisions (system.py:288-313)
     // Collider.position_apply (colliders.py:198-240): the lane's rows
 #pragma unroll
     for (int m = 0; m < MR; m++) {
-      const int r = lane + m * L;
-      if (r >= H.R || !row_active(H, E, r)) continue;
+      const int x = lane + m * L;
+      const int r = x < nact ? BX_MULTI_RX(x) : 0;
+      if (BX_MULTI_SKIP(x, r)) continue;
       BX_MULTI_ROW(R, m, r);
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cvel;
@@ -2514,8 +2672,10 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
                 (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f);
     }
     esync<L>();
+    BX_MSTAMP(4);
     if (lane < H.T) task_sum(X.te, E.cslot, E.tslot + lane * MSLOT_STRIDE);
     esync<L>();
+    BX_MSTAMP(5);
     if (X.hasB) {
       v3 dp;
       q4 dr;
@@ -2528,11 +2688,13 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       stqp(myqp, q);
     }
     esync<L>();
+    BX_MSTAMP(6);
     // Collider.velocity_apply (colliders.py:155-196)
 #pragma unroll
     for (int m = 0; m < MR; m++) {
-      const int r = lane + m * L;
-      if (r >= H.R || !row_active(H, E, r)) continue;
+      const int x = lane + m * L;
+      const int r = x < nact ? BX_MULTI_RX(x) : 0;
+      if (BX_MULTI_SKIP(x, r)) continue;
       BX_MULTI_ROW(R, m, r);
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 rap, rav, raa, rbp, rbv, rba;
@@ -2548,6 +2710,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
                 (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f);
     }
     esync<L>();
+    BX_MSTAMP(7);
     if (lane < H.T) task_sum(X.te, E.cslot, E.tslot + lane * MSLOT_STRIDE);
     esync<L>();
     if (X.hasB) {
@@ -2563,15 +2726,21 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       iaa = iaa + dpa_last;
     }
     esync<L>();
+    BX_MSTAMP(8);
   }
   // Info contact rows of the last position pass (system.py:36-43)
   if (valid) {
 #pragma unroll
     for (int m = 0; m < MR; m++) {
+#if defined(BX_MULTI_HOIST_ROWS)
       const int r = lane + m * L;
       if (r >= H.R) continue;
       const int x = row_info(c, H, E, r);
       if (x < 0) continue;
+#else
+      const int x = lane + m * L;
+      if (x >= nact) continue;
+#endif
       if (io.pos) st3(io.pos + x * 3, cpos[m]);
       if (io.normal) st3(io.normal + x * 3, cn[m]);
       if (io.pen) io.pen[x] = pen[m];
@@ -2584,6 +2753,16 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
     st3(acc + ACC_IAA, iaa);
   }
   esync<L>();
+  BX_MSTAMP(10);
+#undef BX_MULTI_RX
+#undef BX_MULTI_SKIP
+#ifdef BX_MSTAMPS
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 11; k++) bx_mstamp_wave[blockIdx.x & 4095][k] += ms_acc[k];
+    bx_mstamp_wave[blockIdx.x & 4095][15] += 1ull;
+  }
+#endif
 }
 
 // System._pbd_info contact part (system.py:327-340 -> Collider.apply): info
@@ -3929,6 +4108,25 @@ hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, con
   else if (L == 32) { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<32>, grid, dim3(64), lds, s, a); }
   else { if (lds > 65536) (void)hipFuncSetAttribute((const void*)info_obs_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); hipLaunchKernelGGL(info_obs_kernel<64>, grid, dim3(64), lds, s, a); }
   return hipGetLastError();
+}
+hipError_t debug_mstamps(unsigned long long* out, int reset) {
+#ifdef BX_MSTAMPS
+  static unsigned long long host[4096][16];
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(bx_mstamp_wave), sizeof(host));
+  for (int k = 0; k < 16; k++) {
+    out[k] = 0;
+    for (int w = 0; w < 4096; w++) out[k] += host[w][k];
+  }
+  if (e == hipSuccess && reset) {
+    memset(host, 0, sizeof(host));
+    e = hipMemcpyToSymbol(HIP_SYMBOL(bx_mstamp_wave), host, sizeof(host));
+  }
+  return e;
+#else
+  (void)out;
+  (void)reset;
+  return hipErrorNotSupported;
+#endif
 }
 hipError_t launch_default_qp(int64_t n_envs, size_t lds, hipStream_t s, const ResetArgs& a) {
   dim3 grid((unsigned)((n_envs + 63) / 64));

@@ -78,6 +78,7 @@ hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
                           hipStream_t s);
 
 hipError_t debug_stamps(unsigned long long* out, int reset);
+hipError_t debug_mstamps(unsigned long long* out, int reset);  // MULTI mode (item-loop TU)
 hipError_t launch_phase(int which, const uint32_t* blob, int N, int64_t B, int64_t plane,
                         const float* in, float* out, const float* aux, int64_t aux_plane,
                         hipStream_t s);
