@@ -518,6 +518,27 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       put(lane, base + LJ_MP, p[BODY_MASS]);
       put(lane, base + LJ_MC, c[BODY_MASS]);
     };
+    // the limit row's pseudo-angles (kernels' pseudo_angle) and cos / sin,
+    // from the radians the record holds, in double
+    auto put_lim = [&](int lane, int base, int j) {
+      if (J == 0) return;
+      const uint32_t* s = &B.w[H.o_joint + j * JOINT_STRIDE];
+      for (int side = 0; side < 2; side++) {
+        float lf;
+        std::memcpy(&lf, &s[J_LIM + side], 4);
+        const double l = lf, c = std::cos(l), sn = std::sin(l);
+        double p;
+        if (l <= -M_PI) p = -3.0;
+        else if (l >= M_PI) p = 3.0;
+        else {
+          const double r = std::fabs(c) + std::fabs(sn), t = r > 0 ? c / r : 1.0;
+          p = sn >= 0 ? 1.0 - t : t - 1.0;
+        }
+        put(lane, base + (side ? LL_PHI : LL_PLO), fbits(p));
+        put(lane, base + (side ? LL_CHI : LL_CLO), fbits(c));
+        put(lane, base + (side ? LL_SHI : LL_SLO), fbits(sn));
+      }
+    };
     auto put_act = [&](int lane, int base, int a) {
       if (K == 0) return;
       const uint32_t* s = &B.w[H.o_act + a * ACT_STRIDE];
@@ -543,6 +564,8 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       put_joint(l, LI_JOINT, l < J ? l : 0);
       put_act(l, LI_ACT, l < K ? l : 0);
       put_joint(l, LI_JOINT_H, (l & 7) < J ? (l & 7) : 0);
+      put_lim(l, LI_JLIM, l < J ? l : 0);
+      put_lim(l, LI_JLIM_H, (l & 7) < J ? (l & 7) : 0);
       put_act(l, LI_ACT_H, (l & 7) < K ? (l & 7) : 0);
       if (R > 0) {
         const int x = l < R ? l : 0;

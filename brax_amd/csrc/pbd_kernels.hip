@@ -166,6 +166,12 @@ struct JointC {
   float mp, mc;
   v3 Ip, Ic;
 };
+// a revolute joint's first limit row as the hoisted kernels test it
+// (pbd_layout.h LL_*): pseudo-angles and cos / sin of [lo, hi]
+struct JLim {
+  float plo, phi, clo, slo, chi, shi;
+};
+
 __device__ __forceinline__ JointC load_joint(const Cst& c, const BlobHdr& H, int j) {
   int o = H.o_joint + j * JOINT_STRIDE;
   JointC r;
@@ -1148,8 +1154,8 @@ __device__ __forceinline__ q4 angle_update_half(const JointC& J, bool child, con
 
 // Revolute.apply_reduced (joints.py:79-100, 154-195, 270-309), one side: o is
 // this side's body (parent on lanes 0-7, child on 8-15); returns its dp, dq
-__device__ __forceinline__ void joint_apply_half(const JointC& J, bool child, const QP& o, v3& dpo,
-                                                 q4& dro) {
+__device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL, bool child,
+                                                 const QP& o, v3& dpo, q4& dro) {
   const float sg = child ? -1.f : 1.f;
   // value selects (a conditional lvalue into the constants would force them to scratch)
   const v3 I = sel3(child, J.Ic, J.Ip);
@@ -1176,11 +1182,20 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, bool child, co
   v3 t0 = xh3(u0), t2 = xh3(u2);
   v3 axis = sel3(child, t0, u0), axis_c = sel3(child, u0, t0);
   v3 ref_p = sel3(child, t2, u2), ref_c = sel3(child, u2, t2);
-  float psi = signed_angle(axis, ref_p, ref_c);
   v3 dq1 = cross(axis, axis_c);
-  float ph = clampf(psi, J.lim[0], J.lim[1]);
-  q4 fix = quat_rot_axis(axis, ph);
-  v3 n1 = rotate(ref_p, fix);
+  // ref_p turned about the axis by the hinge angle psi = atan2(y, x)
+  // (math.signed_angle) clamped to the limits: rotate(ref_p,
+  // quat_rot_axis(axis, ph)) is Rodrigues' formula with (cos ph, sin ph),
+  // which is (x, y) / |(x, y)| inside the limits and the limit's own cos /
+  // sin outside, so neither atan2 nor the half-angle sincos is evaluated
+  const float y = dot(cross(ref_p, ref_c), axis), x = dot(ref_p, ref_c);
+  const float pa = pseudo_angle(x, y);
+  const float r2 = x * x + y * y;
+  const float ri = r2 > 0.f ? rsqrtf(r2) : 0.f;
+  float cph = r2 > 0.f ? x * ri : 1.f, sph = y * ri;
+  cph = pa < JL.plo ? JL.clo : (pa > JL.phi ? JL.chi : cph);
+  sph = pa < JL.plo ? JL.slo : (pa > JL.phi ? JL.shi : sph);
+  v3 n1 = ref_p * cph + cross(axis, ref_p) * sph + axis * (dot(axis, ref_p) * (1.f - cph));
   v3 dq2 = cross(n1, ref_c);
   q4 a1 = angle_update_half(J, child, o.rot, dq1);
   q4 a2 = angle_update_half(J, child, o.rot, dq2);
@@ -1189,19 +1204,24 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, bool child, co
 
 // Actuator.apply_reduced (actuators.py:52-112) for a revolute joint, one side
 template <int F>
-__device__ __forceinline__ void act_torque_half(const JointC& Jc, const ActC& A, const Env& E,
-                                                const float* al, int a, bool child, const q4& ro) {
+__device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL, const ActC& A,
+                                                const Env& E, const float* al, int a, bool child,
+                                                const q4& ro) {
   v3 u0 = rotate(sel3(child, Jc.axc[0], Jc.axp[0]), ro);
   v3 u2 = rotate(sel3(child, Jc.axc[2], Jc.axp[2]), ro);
   v3 t0 = xh3(u0), t2 = xh3(u2);
   v3 axis = sel3(child, t0, u0);
-  float ang = signed_angle(axis, sel3(child, t2, u2), sel3(child, u2, t2));
+  const v3 ref_p = sel3(child, t2, u2), ref_c = sel3(child, u2, t2);
   float t;
   if (is_torque<F>(A.type)) {
+    // the torque is cut outside the limits: the hinge angle's limit test on
+    // pseudo-angles (no atan2)
+    const float pa = pseudo_angle(dot(ref_p, ref_c), dot(cross(ref_p, ref_c), axis));
     t = al[0] * A.strength * -1.f;
-    if (ang < Jc.lim[0]) t = 0.f;
-    if (ang > Jc.lim[1]) t = 0.f;
+    if (pa < JL.plo) t = 0.f;
+    if (pa > JL.phi) t = 0.f;
   } else {
+    float ang = signed_angle(axis, ref_p, ref_c);
     float tgt = clampf(al[0] * 3.14159265358979323846f / 180.f, Jc.lim[0], Jc.lim[1]);
     t = (tgt - ang) * A.strength;
   }
@@ -1942,6 +1962,7 @@ struct Hoist {
   bool hasB, hasJ, hasA, hasR;
   BodyC B;
   JointC J;
+  JLim JL;
   ActC A;
   RowC R;
   GList<M> jl, al, cl;
@@ -1977,6 +1998,8 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   grab(LI_JL, M);
   grab(LI_AL, M);
   grab(LI_CL, M);
+  constexpr int OL = JH ? LI_JLIM_H : LI_JLIM;
+  grab(OL, 8);
   auto f = [&](int i) { return __uint_as_float(w[i]); };
   auto f3 = [&](int i) { return mk(f(i), f(i + 1), f(i + 2)); };
   auto n = [&](int i) { return (int)w[i]; };
@@ -2034,6 +2057,8 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   R.mb = f(LI_ROW + LR_MB);
   R.Ia = f3(LI_ROW + LR_IA);
   R.Ib = f3(LI_ROW + LR_IB);
+  X.JL = JLim{f(OL + LL_PLO), f(OL + LL_PHI), f(OL + LL_CLO), f(OL + LL_SLO), f(OL + LL_CHI),
+               f(OL + LL_SHI)};
 #pragma unroll
   for (int k = 0; k < M; k++) {
     X.jl.e[k] = n(LI_JL + k);
@@ -2201,7 +2226,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       if constexpr (JH) {
         // one side of joint / actuator jx per lane (act_same, checked on the host)
         const int jb = child ? X.J.bc : X.J.bp;
-        if (X.hasA) act_torque_half<F>(X.J, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE));
+        if (X.hasA) act_torque_half<F>(X.J, X.JL, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE));
         if (X.hasJ) {
           const JointC& Jc = X.J;
           v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
@@ -2253,7 +2278,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
           QP o = ldqp(E.qp + jb * QP_STRIDE);
           v3 dpo;
           q4 dro;
-          joint_apply_half(Jc, child, o, dpo, dro);
+          joint_apply_half(Jc, X.JL, child, o, dpo, dro);
           st_slot(E.jslot + (child ? E.nJ + jx : jx) * SLOT_STRIDE, dpo, dro, 0.f);
         }
       } else if (X.hasJ) {

@@ -115,8 +115,14 @@ enum {
   LI_CL = 120,
   LI_JOINT_H = 128, // joint halves: lane l -> joint / actuator l & 7
   LI_ACT_H = 176,
-  LANE_W = 184
+  LI_JLIM = 184,    // the lane's joint's first limit row (LL_*), both mappings
+  LI_JLIM_H = 192,
+  LANE_W = 200
 };
+// a revolute limit row [lo, hi] as the SINGLE-mode kernels test it: the
+// pseudo-angles of the limits (a monotone stand-in for atan2 over (-pi, pi],
+// +-3 past +-pi) and their cosines / sines
+enum { LL_PLO = 0, LL_PHI = 1, LL_CLO = 2, LL_SLO = 3, LL_CHI = 4, LL_SHI = 5 };
 enum {
   LJ_TYPE = 0, LJ_BP = 1, LJ_BC = 2, LJ_FREE = 3, LJ_AOFF = 4, LJ_NANG = 5, LJ_DAMP = 6,
   LJ_SP = 7, LJ_SA = 8, LJ_OFFP = 9, LJ_OFFC = 12, LJ_AXP = 15, LJ_AXC = 24, LJ_LIM = 33,

@@ -102,6 +102,16 @@ __device__ __forceinline__ q4 quat_inv(q4 q) { return {q.w, -q.x, -q.y, -q.z}; }
 __device__ __forceinline__ float signed_angle(v3 axis, v3 ref_p, v3 ref_c) {
   return atan2f(dot(cross(ref_p, ref_c), axis), dot(ref_p, ref_c));
 }
+// A monotone stand-in for atan2(y, x) over (-pi, pi]: 1 - x / (|x| + |y|)
+// for y >= 0, x / (|x| + |y|) - 1 below, (0, 0) -> 0 as atan2(0, 0). Comparing
+// it with a limit's pseudo-angle decides `atan2(y, x) < limit` without the
+// transcendental (the two differ only inside the rounding band of the
+// boundary, where fp32 atan2 and the float64 reference differ too).
+__device__ __forceinline__ float pseudo_angle(float x, float y) {
+  const float r = fabsf(x) + fabsf(y);
+  const float t = r > 0.f ? x / r : 1.f;
+  return y >= 0.f ? 1.f - t : t - 1.f;
+}
 __device__ __forceinline__ float clampf(float x, float lo, float hi) {
   return x < lo ? lo : (x > hi ? hi : x);
 }
