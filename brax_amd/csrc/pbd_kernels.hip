@@ -241,9 +241,31 @@ __device__ __forceinline__ void angle_update(const JointC& J, const q4& rp, cons
 }
 
 // Revolute/Spherical.apply_reduced (joints.py:270-309, 332-386)
+// Rodrigues' turn of v about the unit axis by the angle with (cos, sin) =
+// (c, s): rotate(v, quat_rot_axis(axis, angle)) (math.py:25-40, 173-187)
+__device__ __forceinline__ v3 turn(v3 v, v3 axis, float c, float s) {
+  return v * c + cross(axis, v) * s + axis * (dot(axis, v) * (1.f - c));
+}
+// ref_p turned about the axis by the hinge angle atan2(y, x) clamped to the
+// limits (math.signed_angle, joints.py:170-176): (cos, sin) is (x, y) /
+// |(x, y)| inside the limits, the limit's own outside; the test on
+// pseudo-angles. Neither atan2 nor the half-angle sincos is evaluated.
+__device__ __forceinline__ v3 hinge_turn(v3 axis, v3 ref_p, v3 ref_c, const JLim& JL) {
+  const float y = dot(cross(ref_p, ref_c), axis), x = dot(ref_p, ref_c);
+  const float pa = pseudo_angle(x, y);
+  const float r2 = x * x + y * y;
+  const float ri = r2 > 0.f ? rsqrtf(r2) : 0.f;
+  float cph = r2 > 0.f ? x * ri : 1.f, sph = y * ri;
+  cph = pa < JL.plo ? JL.clo : (pa > JL.phi ? JL.chi : cph);
+  sph = pa < JL.plo ? JL.slo : (pa > JL.phi ? JL.shi : sph);
+  return turn(ref_p, axis, cph, sph);
+}
+
+// JL: the hoisted kernels' limit row (pseudo-angles, cos / sin): the
+// revolute hinge turn without atan2 / sincos; null: the reference's formulas
 template <int F>
 __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, q4& dpr,
-                            v3& dcp, q4& dcr) {
+                            v3& dcp, q4& dcr, const JLim* JL = nullptr) {
   // positional constraint: apply_position_update (joints.py:154-195)
   v3 pw = p.pos + rotate(J.off_p, p.rot);
   v3 cw = c.pos + rotate(J.off_c, c.rot);
@@ -265,12 +287,17 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
     v3 axis = rotate(J.axp[0], p.rot);
     v3 ref_p = rotate(J.axp[2], p.rot);
     v3 ref_c = rotate(J.axc[2], c.rot);
-    float psi = signed_angle(axis, ref_p, ref_c);
     v3 axis_c = rotate(J.axc[0], c.rot);
     v3 dq1 = cross(axis, axis_c);
-    float ph = clampf(psi, J.lim[0], J.lim[1]);
-    q4 fix = quat_rot_axis(axis, ph);
-    v3 n1 = rotate(ref_p, fix);
+    v3 n1;
+    if (JL) {
+      n1 = hinge_turn(axis, ref_p, ref_c, *JL);
+    } else {
+      float psi = signed_angle(axis, ref_p, ref_c);
+      float ph = clampf(psi, J.lim[0], J.lim[1]);
+      q4 fix = quat_rot_axis(axis, ph);
+      n1 = rotate(ref_p, fix);
+    }
     v3 dq2 = cross(n1, ref_c);
     q4 a1p{0, 0, 0, 0}, a1c{0, 0, 0, 0}, a2p{0, 0, 0, 0}, a2c{0, 0, 0, 0};
     angle_update(J, p.rot, c.rot, dq1, a1p, a1c);
@@ -1091,8 +1118,22 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
 // Torque/Angle.apply_reduced for actuator a (lane) -> aslot
 template <int F>
 __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, const Env& E,
-                                           const float* al, int a) {
+                                           const float* al, int a, const JLim* JL = nullptr) {
   QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
+  if (JL && is_rev<F>(Jc.type) && is_torque<F>(A.type)) {
+    // a revolute torque actuator needs its hinge angle only for the limit
+    // cut: the test on pseudo-angles (no atan2)
+    const v3 axis = rotate(Jc.axp[0], p.rot);
+    const v3 ref_p = rotate(Jc.axp[2], p.rot), ref_c = rotate(Jc.axc[2], cq.rot);
+    const float pa = pseudo_angle(dot(ref_p, ref_c), dot(cross(ref_p, ref_c), axis));
+    float t = al[0] * A.strength * -1.f;
+    if (pa < JL->plo) t = 0.f;
+    if (pa > JL->phi) t = 0.f;
+    const v3 tq = mk(0.f, 0.f, 0.f) + axis * t;
+    st_v3a(E.aslot + a * ASLOT_STRIDE, mul(Jc.Ip, tq));
+    st_v3a(E.aslot + (E.nK + a) * ASLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
+    return;
+  }
   v3 axes[3];
   float ang[3];
   int dof = axis_angle<F>(Jc, p, cq, axes, ang);
@@ -1183,19 +1224,7 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   v3 axis = sel3(child, t0, u0), axis_c = sel3(child, u0, t0);
   v3 ref_p = sel3(child, t2, u2), ref_c = sel3(child, u2, t2);
   v3 dq1 = cross(axis, axis_c);
-  // ref_p turned about the axis by the hinge angle psi = atan2(y, x)
-  // (math.signed_angle) clamped to the limits: rotate(ref_p,
-  // quat_rot_axis(axis, ph)) is Rodrigues' formula with (cos ph, sin ph),
-  // which is (x, y) / |(x, y)| inside the limits and the limit's own cos /
-  // sin outside, so neither atan2 nor the half-angle sincos is evaluated
-  const float y = dot(cross(ref_p, ref_c), axis), x = dot(ref_p, ref_c);
-  const float pa = pseudo_angle(x, y);
-  const float r2 = x * x + y * y;
-  const float ri = r2 > 0.f ? rsqrtf(r2) : 0.f;
-  float cph = r2 > 0.f ? x * ri : 1.f, sph = y * ri;
-  cph = pa < JL.plo ? JL.clo : (pa > JL.phi ? JL.chi : cph);
-  sph = pa < JL.plo ? JL.slo : (pa > JL.phi ? JL.shi : sph);
-  v3 n1 = ref_p * cph + cross(axis, ref_p) * sph + axis * (dot(axis, ref_p) * (1.f - cph));
+  v3 n1 = hinge_turn(axis, ref_p, ref_c, JL);
   v3 dq2 = cross(n1, ref_c);
   q4 a1 = angle_update_half(J, child, o.rot, dq1);
   q4 a2 = angle_update_half(J, child, o.rot, dq2);
@@ -2187,6 +2216,10 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   const float h = H.h;
   const v3 g = mk(H.gx, H.gy, H.gz);
   constexpr bool JH = (F & F_JH) != 0;
+  // revolute-only kernels take the atan2-free hinge (hinge_turn); with
+  // spherical joints in the same wave the extra branch costs more than it
+  // saves (Humanoid 74.5 -> 67.5 M env-steps/s, profiles/r02u_bench.log)
+  const JLim* JLP = (F & F_SPH) == 0 ? &X.JL : nullptr;
   const int jx = lane & 7;         // JH: this lane's joint / actuator
   const bool child = lane >= 8;    // JH: this lane's side
   float* myqp = E.qp + lane * QP_STRIDE;
@@ -2237,7 +2270,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       if (X.hasA) {
         const ActC& A = X.A;
         if (H.act_same) {
-          act_torque<F>(X.J, A, E, al, lane);
+          act_torque<F>(X.J, A, E, al, lane, JLP);
         } else {
           JointC Jc = load_joint(c, H, A.joint);
           act_torque<F>(Jc, A, E, al, lane);
@@ -2286,7 +2319,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
         q4 dpr, dcr;
-        joint_apply<F>(Jc, p, cq, dpp, dpr, dcp, dcr);
+        joint_apply<F>(Jc, p, cq, dpp, dpr, dcp, dcr, JLP);
         st_slot(E.jslot + lane * SLOT_STRIDE, dpp, dpr, 0.f);
         st_slot(E.jslot + (E.nJ + lane) * SLOT_STRIDE, dcp, dcr, 0.f);
       }
