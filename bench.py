@@ -13,8 +13,9 @@ Episode/AutoReset. Inputs are resident in HBM.
 Multi-GPU: rank r owns the global envs [r*B, (r+1)*B) (weak scaling). Reset
 noise and actions are keyed by global env id with one shared seed, so the
 ranks together step exactly the envs of one N*B batch; the only collective is
-an RCCL all-gather of the per-env (reward, done) pair each step. Prints ONE
-JSON line on rank 0.
+the episodic exchange: each rank sums its envs' (reward, done) on the device
+every step, and the sums are all-gathered over RCCL once per episode length
+(1000 steps). Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
@@ -295,7 +296,9 @@ def main():
   lib = _native.lib()
   stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
   act = torch.empty((B, A), dtype=torch.float32, device=dev)
-  exchange = bd.EpisodeExchange(B, dev) if world > 1 else None
+  # the episodic (reward, done) exchange: summed on the device every step,
+  # all-gathered over RCCL once per episode length
+  exchange = bd.EpisodeExchange(B, dev, every=1000) if world > 1 else None
 
   def one_step(st, k):
     # the step's action slab, keyed by (step, global env id): drawn on the
@@ -304,7 +307,7 @@ def main():
                    bd.action_offset(rank, B, A, k, world), -1.0, 1.0, stream)
     st = env.step(st, act)
     if exchange is not None:
-      exchange(st.reward, st.done)  # the one RCCL collective: (reward, done) all-gather
+      exchange(st.reward, st.done)  # the one RCCL collective, once per 1000 steps
     return st
 
   for k in range(args.warmup):

@@ -26,9 +26,13 @@ def _worker(rank, world, port, q):
   lo, hi = bd.env_range(rank, B)
   reward = torch.arange(lo, hi, dtype=torch.float32)
   done = (torch.arange(lo, hi) % 2).float()
-  ex = bd.EpisodeExchange(B, 'cpu')
-  out = ex(reward, done)
-  q.put((rank, out.numpy().copy(), bd.action_offset(rank, B, 8, step=3, world=world)))
+  ex = bd.EpisodeExchange(B, 'cpu', every=3)
+  # the step's (reward, done) rows of one (4, B) buffer, as an env step returns them
+  scal = torch.stack([reward, done, torch.zeros(B), torch.zeros(B)])
+  assert ex(*scal.unbind(0)[:2]) is None and ex(reward, done) is None
+  out = ex(*scal.unbind(0)[:2])  # the third step: the episodic gather
+  q.put((rank, out.numpy().copy(), bd.action_offset(rank, B, 8, step=3, world=world),
+         float(ex.acc.abs().sum())))
   dist.barrier()
   dist.destroy_process_group()
 
@@ -47,10 +51,12 @@ def test_episode_allgather_world2():
     assert p.exitcode == 0
   res.sort()
   expect_r = np.arange(10, dtype=np.float32).reshape(2, 5)
-  for rank, out, key in res:
+  for rank, out, key, left in res:
+    # three steps summed per env, every rank's envs in global order
     assert out.shape == (2, 2, 5)
-    np.testing.assert_array_equal(out[:, 0], expect_r)
-    np.testing.assert_array_equal(out[:, 1], expect_r % 2)
+    np.testing.assert_array_equal(out[:, 0], 3 * expect_r)
+    np.testing.assert_array_equal(out[:, 1], 3 * (expect_r % 2))
+    assert left == 0.0  # the sums restart after the exchange
   # rank r's action rows of step 3 continue rank r-1's in the global stream
   assert res[1][2] - res[0][2] == 5 * 8
 
