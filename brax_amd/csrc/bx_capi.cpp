@@ -892,9 +892,10 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
                 void* stream) {
   if (!S || !env || !in || !out) return fail("null argument");
   DEVICE_SCOPE(S);
-  if (check_act(S, act, act_stride, act_width)) return 1;
   if (check_env(S, env)) return 1;
+  // an empty batch is a no-op (its buffers, the action included, may be null)
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
+  if (check_act(S, act, act_stride, act_width)) return 1;
   if (!qp_ok(in->qp) || !qp_ok(out->qp)) return fail("null qp field");
   if (!in->done || !out->done || !out->reward || !out->obs) return fail("null env buffer");
   if (env->auto_reset && (!qp_ok(env->first_qp) || !env->first_obs))
