@@ -484,11 +484,42 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     for (int a = 0; a < K; a++)
       if (d->act_joint[a] != a) H.act_same = 0;
   }
+  // a contact row's 32 resolved words (LR_*): its record's geometry and
+  // constants with the masses / inverse inertias of the bodies it names
+  auto row_words = [&](int x, uint32_t* out) {
+    const uint32_t* w = &B.w[H.o_row + x * ROW_STRIDE];
+    const uint32_t* pa = &B.w[H.o_body + (int)w[R_A] * BODY_STRIDE];
+    const uint32_t* pb = &B.w[H.o_body + (int)w[R_B] * BODY_STRIDE];
+    const int src[24] = {R_GROUP, R_A, R_B, R_FN, R_ONEWAY, R_APOS, R_APOS + 1, R_APOS + 2,
+                         R_AEND, R_AEND + 1, R_AEND + 2, R_ARAD, R_BPOS, R_BPOS + 1, R_BPOS + 2,
+                         R_BEND, R_BEND + 1, R_BEND + 2, R_BRAD, R_FRIC, R_ELAS, R_SCALE, R_THR,
+                         R_ERP};
+    for (int k = 0; k < 24; k++) out[k] = w[src[k]];
+    out[LR_MA] = pa[BODY_MASS];
+    out[LR_MB] = pb[BODY_MASS];
+    for (int k = 0; k < 3; k++) {
+      out[LR_IA + k] = pa[BODY_I + k];
+      out[LR_IB + k] = pb[BODY_I + k];
+    }
+  };
+  // the MULTI-mode row image: every row's resolved words, 16-byte group g of
+  // row r at o_rimg + (g * R + r) * 4 (one round of independent loads per row
+  // and pass instead of record -> referenced body)
+  if (H.multi && R > 0) {
+    B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
+    H.o_rimg = B.alloc(32 * R);
+    uint32_t rw[32];
+    for (int x = 0; x < R; x++) {
+      row_words(x, rw);
+      for (int k = 0; k < 32; k++) B.w[H.o_rimg + ((k / 4) * R + x) * 4 + k % 4] = rw[k];
+    }
+  }
   // the SINGLE-mode lane image (pbd_layout.h LI_*): copies of the records
   // above, so its words are the same bits the item-loop kernels read; a lane
   // without an item of a kind gets item 0's record (as the kernels' clamped
   // index did), and zeros where the system has none of that kind
   if (H.single) {
+    B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
     H.o_lane = B.alloc(LANE_W * LANE_IMG_LANES);
     auto put = [&](int lane, int w, uint32_t v) {
       B.w[H.o_lane + (w / 4) * 4 * LANE_IMG_LANES + 4 * lane + w % 4] = v;
@@ -568,22 +599,9 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       put_lim(l, LI_JLIM_H, (l & 7) < J ? (l & 7) : 0);
       put_act(l, LI_ACT_H, (l & 7) < K ? (l & 7) : 0);
       if (R > 0) {
-        const int x = l < R ? l : 0;
-        const uint32_t* w = &B.w[H.o_row + x * ROW_STRIDE];
-        const int ra = (int)w[R_A], rb = (int)w[R_B];
-        const uint32_t* pa = &B.w[H.o_body + ra * BODY_STRIDE];
-        const uint32_t* pb = &B.w[H.o_body + rb * BODY_STRIDE];
-        const int src[24] = {R_GROUP, R_A, R_B, R_FN, R_ONEWAY, R_APOS, R_APOS + 1, R_APOS + 2,
-                             R_AEND, R_AEND + 1, R_AEND + 2, R_ARAD, R_BPOS, R_BPOS + 1, R_BPOS + 2,
-                             R_BEND, R_BEND + 1, R_BEND + 2, R_BRAD, R_FRIC, R_ELAS, R_SCALE, R_THR,
-                             R_ERP};
-        for (int k = 0; k < 24; k++) put(l, LI_ROW + k, w[src[k]]);
-        put(l, LI_ROW + LR_MA, pa[BODY_MASS]);
-        put(l, LI_ROW + LR_MB, pb[BODY_MASS]);
-        for (int k = 0; k < 3; k++) {
-          put(l, LI_ROW + LR_IA + k, pa[BODY_I + k]);
-          put(l, LI_ROW + LR_IB + k, pb[BODY_I + k]);
-        }
+        uint32_t rw[32];
+        row_words(l < R ? l : 0, rw);
+        for (int k = 0; k < 32; k++) put(l, LI_ROW + k, rw[k]);
       }
       put_list(l, LI_JL, jl[b], hasB, (uint32_t)(2 * J));
       put_list(l, LI_AL, al[b], hasB, (uint32_t)(2 * K));

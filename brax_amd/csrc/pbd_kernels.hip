@@ -2463,10 +2463,45 @@ struct HoistM {
 // hides those loads. Measured (Ant Mountain(4), 2048 envs, rows per lane 3):
 // 0.44 ms per step, against 0.68 ms with the rows hoisted into registers
 // (BX_MULTI_HOIST_ROWS: 256 VGPRs + 78 AGPRs, one wave per SIMD).
+// row r's constants from the MULTI row image (bx_capi.cpp): eight
+// independent 16-byte loads, consecutive rows' groups adjacent
+__device__ __forceinline__ RowC load_row_img(const Cst& c, const BlobHdr& H, int r) {
+  const uint4* im = reinterpret_cast<const uint4*>(c.w + H.o_rimg) + r;
+  uint32_t w[32];
+#pragma unroll
+  for (int g = 0; g < 8; g++) {
+    const uint4 v = im[g * H.R];
+    w[4 * g] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+  }
+  auto f = [&](int i) { return __uint_as_float(w[i]); };
+  auto f3 = [&](int i) { return mk(f(i), f(i + 1), f(i + 2)); };
+  RowC x;
+  x.group = (int)w[LR_GROUP];
+  x.a = (int)w[LR_A];
+  x.b = (int)w[LR_B];
+  x.fn = (int)w[LR_FN];
+  x.oneway = (int)w[LR_OW];
+  x.a_pos = f3(LR_APOS);
+  x.a_end = f3(LR_AEND);
+  x.a_rad = f(LR_ARAD);
+  x.b_pos = f3(LR_BPOS);
+  x.b_end = f3(LR_BEND);
+  x.b_rad = f(LR_BRAD);
+  x.fric = f(LR_FRIC);
+  x.elas = f(LR_ELAS);
+  x.scale = f(LR_SCALE);
+  x.thr = f(LR_THR);
+  x.erp = f(LR_ERP);
+  x.ma = f(LR_MA);
+  x.mb = f(LR_MB);
+  x.Ia = f3(LR_IA);
+  x.Ib = f3(LR_IB);
+  return x;
+}
 #if defined(BX_MULTI_HOIST_ROWS)
 #define BX_MULTI_ROW(R, m, r) const RowC& R = X.R[m]
 #else
-#define BX_MULTI_ROW(R, m, r) const RowC R = load_row(c, H, r)
+#define BX_MULTI_ROW(R, m, r) const RowC R = load_row_img(c, H, r)
 #endif
 
 template <int L, int MR>

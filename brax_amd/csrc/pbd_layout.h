@@ -95,6 +95,7 @@ struct BlobHdr {
   int32_t o_lane;                    // SINGLE mode: the lane image (below); 0 = none
   int32_t l_arow, act_read;          // LDS: the env's action row, the words any step reads
   int32_t l_nnl, nnl_words;          // LDS: NearNeighbors per-wave pick lists (envs over several waves)
+  int32_t o_rimg;                    // MULTI mode: the row image (32 resolved words per row, LR_*)
 };
 
 // SINGLE-mode lane image: for each of 64 lanes, every constant the
