@@ -10,7 +10,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from brax_amd import _native, envs  # noqa: E402
 
 dev = torch.device('cuda', 0)
-env = envs.create('ant', batch_size=4096, episode_length=1000, device=dev)
+name = sys.argv[1] if len(sys.argv) > 1 else 'ant'
+env = envs.create(name, batch_size=4096, episode_length=1000, device=dev)
 st = env.reset(np.array([0, 1], np.uint32))
 lib = _native.lib()
 buf = (C.c_ulonglong * 16)()
@@ -18,7 +19,7 @@ for k in range(60):
   if k == 10:
     torch.cuda.synchronize()
     _native.check(lib.bx_debug_stamps(buf, 1))
-  a = torch.rand((4096, 8), device=dev) * 2 - 1
+  a = torch.rand((4096, env.action_size), device=dev) * 2 - 1
   st = env.step(st, a)
 torch.cuda.synchronize()
 _native.check(lib.bx_debug_stamps(buf, 0))
