@@ -451,6 +451,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   const int tail = off;
   H.l_mslot = carve((2 * R + 1) * MSLOT_STRIDE);
   H.l_tslot = carve((H.T + 1) * MSLOT_STRIDE);
+  H.l_near = carve(R + 16);
   H.env_words_m = (off + 63) & ~63;
   off = tail;
   H.l_rowd = carve(R * ROWD_STRIDE);
@@ -512,6 +513,30 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     for (int x = 0; x < R; x++) {
       row_words(x, rw);
       for (int k = 0; k < 32; k++) B.w[H.o_rimg + ((k / 4) * R + x) * 4 + k % 4] = rw[k];
+    }
+    // broad-phase bounds (BI_*): reach = |a_end| + |b_end| + radii in double,
+    // rounded up to float
+    H.o_bimg = B.alloc(BI_WORDS * R);
+    for (int x = 0; x < R; x++) {
+      const int g = d->row_group[x];
+      double reach = d->row_a_radius[x] + d->row_b_radius[x];
+      double ea = 0, eb = 0;
+      for (int k = 0; k < 3; k++) {
+        ea += d->row_a_end[3 * x + k] * d->row_a_end[3 * x + k];
+        eb += d->row_b_end[3 * x + k] * d->row_b_end[3 * x + k];
+      }
+      reach += std::sqrt(ea) + std::sqrt(eb);
+      const float rf = std::nextafter((float)reach, 3.0e38f);
+      uint32_t bw[BI_WORDS] = {0};
+      bw[BI_A] = (uint32_t)d->row_body_a[x];
+      bw[BI_B] = (uint32_t)d->row_body_b[x];
+      std::memcpy(&bw[BI_REACH], &rf, 4);
+      bw[BI_SKIP] = d->col_fn[g] == BX_COL_CAPSULE_CAPSULE ? 1u : 0u;
+      for (int k = 0; k < 3; k++) {
+        bw[BI_APOS + k] = fbits(d->row_a_pos[3 * x + k]);
+        bw[BI_BPOS + k] = fbits(d->row_b_pos[3 * x + k]);
+      }
+      for (int k = 0; k < BI_WORDS; k++) B.w[H.o_bimg + ((k / 4) * R + x) * 4 + k % 4] = bw[k];
     }
   }
   // the SINGLE-mode lane image (pbd_layout.h LI_*): copies of the records

@@ -83,6 +83,7 @@ struct Env {
   float* xact;   // the action an env program hands System.step (xact_words)
   float* arow;   // the env's action row, its first act_read words (env step)
   float* nnl;    // NearNeighbors per-wave pick lists (nnl_words)
+  int* nearl;    // MULTI: the pass's near rows, then per-wave counts
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -1297,6 +1298,7 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi =
     E.rowd = nullptr;
     E.cslot = al16(base + H.l_mslot);
     E.tslot = al16(base + H.l_tslot);
+    E.nearl = reinterpret_cast<int*>(base + H.l_near);
     E.sstride = MSLOT_STRIDE;
     E.nd = E.tslot;
     E.nds = 1;
@@ -2739,12 +2741,81 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       BX_MSTAMP(3);
     }
     // ---- collisions (system.py:288-313)
+    // Broad phase, on every pass but the step's last (whose contacts are the
+    // step's Info): a capsule pair whose centres lie farther apart than its
+    // reach cannot penetrate, so both its passes' updates are exact zeros;
+    // its slots are zeroed here and the pair left out of both passes. The
+    // near rows are listed in (m, wave, lane) order (E.nearl).
+#if defined(BX_MULTI_HOIST_ROWS)
+    const bool bph = false;
+#else
+    // (culled scenes skip it: NearNeighbors already keeps only near cells)
+    const bool bph = H.o_bimg != 0 && H.n_nn == 0 && it + 1 < H.substeps / 2;
+#endif
+    int nwork = nact;
+    if (bph) {
+      constexpr int NWV = L / 64;
+      const int wv = lane >> 6;
+      int* cnt = E.nearl + H.R;
+      bool nr[MR];
+      int rr[MR], rk[MR];
+#pragma unroll
+      for (int m = 0; m < MR; m++) {
+        const int x = lane + m * L;
+        const int r = x < nact ? BX_MULTI_RX(x) : -1;
+        bool near = false;
+        if (r >= 0) {
+          const uint4* bi = reinterpret_cast<const uint4*>(c.w + H.o_bimg) + r;
+          const uint4 g0 = bi[0], g1 = bi[H.R], g2 = bi[2 * H.R];
+          near = g0.w == 0u;
+          if (!near) {
+            const float* qa = E.qp + (int)g0.x * QP_STRIDE;
+            const float* qb = E.qp + (int)g0.y * QP_STRIDE;
+            const v3 ca = ld3(qa) + rotate(mk(__uint_as_float(g1.x), __uint_as_float(g1.y),
+                                              __uint_as_float(g1.z)), ld_rot(qa));
+            const v3 cb = ld3(qb) + rotate(mk(__uint_as_float(g2.x), __uint_as_float(g2.y),
+                                              __uint_as_float(g2.z)), ld_rot(qb));
+            // + 1e-4: far above the fp32 error of the centres
+            near = !(norm(cb - ca) > __uint_as_float(g0.z) + 1e-4f);
+          }
+          if (!near) {
+            const f32x4 z{0.f, 0.f, 0.f, 0.f};
+            st4a(E.cslot + r * MSLOT_STRIDE, z);
+            st4a(E.cslot + r * MSLOT_STRIDE + 4, z);
+            st4a(E.cslot + (H.R + r) * MSLOT_STRIDE, z);
+            st4a(E.cslot + (H.R + r) * MSLOT_STRIDE + 4, z);
+          }
+        }
+        nr[m] = near;
+        rr[m] = r;
+        const unsigned long long bal = __ballot(near);
+        rk[m] = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+        if ((lane & 63) == 0) cnt[wv * MR + m] = __popcll(bal);
+      }
+      esync<L>();
+      int total = 0;
+#pragma unroll
+      for (int m = 0; m < MR; m++) {
+        int before = 0, mt = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < NWV; w2++) {
+          const int k = cnt[w2 * MR + m];
+          before += w2 < wv ? k : 0;
+          mt += k;
+        }
+        if (nr[m]) E.nearl[total + before + rk[m]] = rr[m];
+        total += mt;
+      }
+      nwork = total;
+      esync<L>();
+    }
     // Collider.position_apply (colliders.py:198-240): the lane's rows
 #pragma unroll
     for (int m = 0; m < MR; m++) {
       const int x = lane + m * L;
-      const int r = x < nact ? BX_MULTI_RX(x) : 0;
-      if (BX_MULTI_SKIP(x, r)) continue;
+      const int r = x < nwork ? (bph ? E.nearl[x] : BX_MULTI_RX(x)) : 0;
+      if (bph ? x >= nwork : BX_MULTI_SKIP(x, r)) continue;
       BX_MULTI_ROW(R, m, r);
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cvel;
@@ -2782,12 +2853,12 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
     }
     esync<L>();
     BX_MSTAMP(6);
-    // Collider.velocity_apply (colliders.py:155-196)
+    // Collider.velocity_apply (colliders.py:155-196): the position pass's rows
 #pragma unroll
     for (int m = 0; m < MR; m++) {
       const int x = lane + m * L;
-      const int r = x < nact ? BX_MULTI_RX(x) : 0;
-      if (BX_MULTI_SKIP(x, r)) continue;
+      const int r = x < nwork ? (bph ? E.nearl[x] : BX_MULTI_RX(x)) : 0;
+      if (bph ? x >= nwork : BX_MULTI_SKIP(x, r)) continue;
       BX_MULTI_ROW(R, m, r);
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 rap, rav, raa, rbp, rbv, rba;

@@ -96,6 +96,8 @@ struct BlobHdr {
   int32_t l_arow, act_read;          // LDS: the env's action row, the words any step reads
   int32_t l_nnl, nnl_words;          // LDS: NearNeighbors per-wave pick lists (envs over several waves)
   int32_t o_rimg;                    // MULTI mode: the row image (32 resolved words per row, LR_*)
+  int32_t o_bimg;                    // MULTI mode: the rows' broad-phase bounds (BI_*), 0 = none
+  int32_t l_near;                    // LDS (MULTI): the pass's near rows (R) + per-wave counts (16)
 };
 
 // SINGLE-mode lane image: for each of 64 lanes, every constant the
@@ -138,6 +140,12 @@ enum {
 // MULTI-mode gather tasks: a task sums <= TASK_W contact slots of one body and
 // collider group; a body adds <= BTASK_W task partials (ref = task | group << 24)
 enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 8, MULTI_MR = 4 };
+// MULTI-mode broad phase: per row, 16-byte group g of row r at
+// o_bimg + (g * R + r) * 4: (body a, body b, reach, may_skip), (a's centre
+// offset, 0), (b's centre offset, 0). A capsule-capsule row whose capsule
+// centres lie farther apart than reach (half segments + radii, rounded up)
+// cannot penetrate, and its position / velocity updates are exact zeros.
+enum { BI_A = 0, BI_B = 1, BI_REACH = 2, BI_SKIP = 3, BI_APOS = 4, BI_BPOS = 8, BI_WORDS = 12 };
 enum { HULL_STRIDE = 114, HULL_V = 0, HULL_F = 24, HULL_N = 96 };
 
 }  // namespace bx
