@@ -133,14 +133,51 @@ def rotate(vec, quat):
   return r + 2 * s * torch.cross(u.expand_as(r), vec.expand_as(r), dim=-1)
 
 
+class PackedQP(QP):
+  """A QP over one packed (…, N, 16) fp32 buffer (pos 0:3, rot 3:7,
+  vel 7:10, ang 10:13). Its field views are built on first access: the
+  kernels take the buffer itself, so a state that is only stepped never
+  builds them (each torch view costs ~1 µs of host time per step). Behaves
+  as a QP otherwise; `replace` returns a plain QP."""
+
+  def __new__(cls, buf=None, **fields):
+    if fields:  # dataclasses.replace(packed_qp, ...) rebuilds by fields
+      return QP(**fields)
+    return object.__new__(cls)
+
+  def __init__(self, buf=None, **fields):  # pylint: disable=super-init-not-called
+    del fields
+    object.__setattr__(self, '_buf', buf)
+
+  def _fields(self):
+    f = self.__dict__.get('_f')
+    if f is None:
+      f = torch.split(self._buf, [3, 4, 3, 3, 3], -1)[:4]
+      object.__setattr__(self, '_f', f)
+    return f
+
+  pos = property(lambda self: self._fields()[0])
+  rot = property(lambda self: self._fields()[1])
+  vel = property(lambda self: self._fields()[2])
+  ang = property(lambda self: self._fields()[3])
+
+  def replace(self, **kw):
+    return QP(**{k: kw.get(k, getattr(self, k)) for k in ('pos', 'rot', 'vel', 'ang')})
+
+  @property
+  def shape(self):
+    return tuple(self._buf.shape[:-1])
+
+
 def packed_view(buf):
   """QP whose fields are views of a (…, N, 16) fp32 buffer."""
-  return QP(pos=buf[..., 0:3], rot=buf[..., 3:7], vel=buf[..., 7:10],
-            ang=buf[..., 10:13])
+  return PackedQP(buf)
 
 
 def packed_buffer(qp):
   """The (…, N, 16) buffer behind a packed QP, or None."""
+  if type(qp) is PackedQP:
+    return qp._buf  # pylint: disable=protected-access
   base = qp.pos
   if base._base is None:  # pylint: disable=protected-access
     return None

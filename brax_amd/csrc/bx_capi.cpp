@@ -622,6 +622,22 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       put_joint(l, LI_JOINT_H, (l & 7) < J ? (l & 7) : 0);
       put_lim(l, LI_JLIM, l < J ? l : 0);
       put_lim(l, LI_JLIM_H, (l & 7) < J ? (l & 7) : 0);
+      if (J > 0) {
+        // the joint-halves side: the parent's on lanes 0-7, the child's on 8-15
+        const bool child = (l & 8) != 0;
+        const uint32_t* s = &B.w[H.o_joint + ((l & 7) < J ? (l & 7) : 0) * JOINT_STRIDE];
+        const int body = (int)s[child ? J_BC : J_BP];
+        const uint32_t* bw = &B.w[H.o_body + body * BODY_STRIDE];
+        for (int k = 0; k < 3; k++) {
+          put(l, LI_SIDE_H + LS_OFF + k, s[(child ? J_OFFC : J_OFFP) + k]);
+          put(l, LI_SIDE_H + LS_AX0 + k, s[(child ? J_AXC : J_AXP) + k]);
+          put(l, LI_SIDE_H + LS_AX2 + k, s[(child ? J_AXC : J_AXP) + 6 + k]);
+          put(l, LI_SIDE_H + LS_I + k, bw[BODY_I + k]);
+        }
+        put(l, LI_SIDE_H + LS_M, bw[BODY_MASS]);
+        put(l, LI_SIDE_H + LS_SG, fbits(child ? -1.0 : 1.0));
+        put(l, LI_SIDE_H + LS_BODY, (uint32_t)body);
+      }
       put_act(l, LI_ACT_H, (l & 7) < K ? (l & 7) : 0);
       if (R > 0) {
         uint32_t rw[32];
@@ -968,6 +984,45 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   else
     HIP_OK(launch_env_step_generic(S->L, S->mode, S->feat, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   return 0;
+}
+
+int bx_env_step_packed(bx_system* S, const bx_env_params* env, int64_t n_envs,
+                       const float* qp_in, const float* done_in, const float* steps_in,
+                       const uint32_t* rng_in, const float* act, int64_t act_stride,
+                       int64_t act_width, float* out, uint32_t* rng_out, void* stream) {
+  if (!S || !env) return fail("null argument");
+  if (n_envs <= 0) {
+    if (check_env(S, env)) return 1;
+    return n_envs == 0 ? 0 : fail("negative n_envs");
+  }
+  if (!qp_in || !out) return fail("null argument");
+  const int64_t N = S->hdr.N, B = n_envs;
+  auto packed = [&](float* base) {
+    bx_qp q;
+    const int64_t es = N * 16;
+    q.pos = bx_field{base, es, 16};
+    q.rot = bx_field{base + 3, es, 16};
+    q.vel = bx_field{base + 7, es, 16};
+    q.ang = bx_field{base + 10, es, 16};
+    return q;
+  };
+  bx_env_state in{};
+  in.qp = packed(const_cast<float*>(qp_in));
+  in.done = const_cast<float*>(done_in);
+  in.steps = const_cast<float*>(steps_in);
+  in.rng = const_cast<uint32_t*>(rng_in);
+  bx_env_state o{};
+  o.qp = packed(out);
+  float* p = out + B * N * 16;
+  o.obs = p;
+  p += B * env->obs_size;
+  o.reward = p;
+  o.done = p + B;
+  o.steps = p + 2 * B;
+  o.truncation = p + 3 * B;
+  o.metrics = env->n_metrics > 0 ? p + 4 * B : nullptr;
+  o.rng = rng_out;
+  return bx_env_step(S, env, n_envs, &in, act, act_stride, act_width, &o, stream);
 }
 
 int bx_system_info(bx_system* S, int64_t n_envs, const bx_qp* qp, const bx_info* info, void* stream) {

@@ -167,6 +167,14 @@ struct JointC {
   float mp, mc;
   v3 Ip, Ic;
 };
+// joint halves: this lane's side of its joint (pbd_layout.h LS_*), so the
+// per-substep code selects no constants by side
+struct JSide {
+  v3 off, ax0, ax2, I;
+  float m, sg;
+  int body;
+};
+
 // a revolute joint's first limit row as the hoisted kernels test it
 // (pbd_layout.h LL_*): pseudo-angles and cos / sin of [lo, hi]
 struct JLim {
@@ -1184,27 +1192,25 @@ __device__ __forceinline__ v3 sel3(bool s, v3 a, v3 b) {
 }
 
 // Joint.apply_angle_update (joints.py:130-152), this side's rotation part
-__device__ __forceinline__ q4 angle_update_half(const JointC& J, bool child, const q4& ro, v3 dq) {
+__device__ __forceinline__ q4 angle_update_half(const JointC& J, const JSide& S, const q4& ro, v3 dq) {
   float th = safe_norm(dq);
   v3 n = dq / (th + 1e-6f);
   float w1 = dot(n, mul(J.Ip, n));
   float w2 = dot(n, mul(J.Ic, n));
   float dl = -th / (w1 + w2 + 1e-6f);
   v3 p = -dl * n;
-  return J.sa * ((child ? -0.5f : 0.5f) * vec_quat_mul(mul(sel3(child, J.Ic, J.Ip), p), ro));
+  return J.sa * ((S.sg * 0.5f) * vec_quat_mul(mul(S.I, p), ro));
 }
 
 // Revolute.apply_reduced (joints.py:79-100, 154-195, 270-309), one side: o is
 // this side's body (parent on lanes 0-7, child on 8-15); returns its dp, dq
-__device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL, bool child,
-                                                 const QP& o, v3& dpo, q4& dro) {
-  const float sg = child ? -1.f : 1.f;
-  // value selects (a conditional lvalue into the constants would force them to scratch)
-  const v3 I = sel3(child, J.Ic, J.Ip);
-  const float mc = J.mc, mp = J.mp;
-  const float m = child ? mc : mp;
+__device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL, const JSide& S,
+                                                 bool child, const QP& o, v3& dpo, q4& dro) {
+  const float sg = S.sg;
+  const v3 I = S.I;
+  const float m = S.m;
   // positional constraint
-  v3 wo = o.pos + rotate(sel3(child, J.off_c, J.off_p), o.rot);
+  v3 wo = o.pos + rotate(S.off, o.rot);
   v3 ro = wo - o.pos;
   v3 wt = xh3(wo);
   v3 dx = child ? wt - wo : wo - wt;
@@ -1219,26 +1225,26 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   dpo = J.sp * ((sg * pv) / m);
   dro = J.sp * ((sg * 0.5f) * vec_quat_mul(mul(I, cross(ro, pv)), o.rot));
   // the two angular constraints (axis alignment, limited hinge angle)
-  v3 u0 = rotate(sel3(child, J.axc[0], J.axp[0]), o.rot);
-  v3 u2 = rotate(sel3(child, J.axc[2], J.axp[2]), o.rot);
+  v3 u0 = rotate(S.ax0, o.rot);
+  v3 u2 = rotate(S.ax2, o.rot);
   v3 t0 = xh3(u0), t2 = xh3(u2);
   v3 axis = sel3(child, t0, u0), axis_c = sel3(child, u0, t0);
   v3 ref_p = sel3(child, t2, u2), ref_c = sel3(child, u2, t2);
   v3 dq1 = cross(axis, axis_c);
   v3 n1 = hinge_turn(axis, ref_p, ref_c, JL);
   v3 dq2 = cross(n1, ref_c);
-  q4 a1 = angle_update_half(J, child, o.rot, dq1);
-  q4 a2 = angle_update_half(J, child, o.rot, dq2);
+  q4 a1 = angle_update_half(J, S, o.rot, dq1);
+  q4 a2 = angle_update_half(J, S, o.rot, dq2);
   dro = dro + (a1 + a2);
 }
 
 // Actuator.apply_reduced (actuators.py:52-112) for a revolute joint, one side
 template <int F>
-__device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL, const ActC& A,
-                                                const Env& E, const float* al, int a, bool child,
-                                                const q4& ro) {
-  v3 u0 = rotate(sel3(child, Jc.axc[0], Jc.axp[0]), ro);
-  v3 u2 = rotate(sel3(child, Jc.axc[2], Jc.axp[2]), ro);
+__device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL, const JSide& S,
+                                                const ActC& A, const Env& E, const float* al, int a,
+                                                bool child, const q4& ro) {
+  v3 u0 = rotate(S.ax0, ro);
+  v3 u2 = rotate(S.ax2, ro);
   v3 t0 = xh3(u0), t2 = xh3(u2);
   v3 axis = sel3(child, t0, u0);
   const v3 ref_p = sel3(child, t2, u2), ref_c = sel3(child, u2, t2);
@@ -1257,8 +1263,8 @@ __device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL
   }
   v3 tq = mk(0.f, 0.f, 0.f) + axis * t;
   float sgp = is_torque<F>(A.type) ? 1.f : -1.f;
-  if (child) st_v3a(E.aslot + (E.nK + a) * ASLOT_STRIDE, -sgp * mul(Jc.Ic, tq));
-  else st_v3a(E.aslot + a * ASLOT_STRIDE, sgp * mul(Jc.Ip, tq));
+  // parent: sgp * Ip tq, child: -sgp * Ic tq (the side's sign times its inertia)
+  st_v3a(E.aslot + (child ? E.nK + a : a) * ASLOT_STRIDE, (sgp * S.sg) * mul(S.I, tq));
 }
 
 // ---------------------------------------------------------------------------
@@ -1994,6 +2000,7 @@ struct Hoist {
   BodyC B;
   JointC J;
   JLim JL;
+  JSide S;
   ActC A;
   RowC R;
   GList<M> jl, al, cl;
@@ -2031,6 +2038,7 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   grab(LI_CL, M);
   constexpr int OL = JH ? LI_JLIM_H : LI_JLIM;
   grab(OL, 8);
+  if constexpr (JH) grab(LI_SIDE_H, 16);
   auto f = [&](int i) { return __uint_as_float(w[i]); };
   auto f3 = [&](int i) { return mk(f(i), f(i + 1), f(i + 2)); };
   auto n = [&](int i) { return (int)w[i]; };
@@ -2090,6 +2098,15 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   R.Ib = f3(LI_ROW + LR_IB);
   X.JL = JLim{f(OL + LL_PLO), f(OL + LL_PHI), f(OL + LL_CLO), f(OL + LL_SLO), f(OL + LL_CHI),
                f(OL + LL_SHI)};
+  if constexpr (JH) {
+    X.S.off = f3(LI_SIDE_H + LS_OFF);
+    X.S.ax0 = f3(LI_SIDE_H + LS_AX0);
+    X.S.ax2 = f3(LI_SIDE_H + LS_AX2);
+    X.S.I = f3(LI_SIDE_H + LS_I);
+    X.S.m = f(LI_SIDE_H + LS_M);
+    X.S.sg = f(LI_SIDE_H + LS_SG);
+    X.S.body = n(LI_SIDE_H + LS_BODY);
+  }
 #pragma unroll
   for (int k = 0; k < M; k++) {
     X.jl.e[k] = n(LI_JL + k);
@@ -2260,13 +2277,13 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       // actuators + damping (actuator a drives joint a when H.act_same)
       if constexpr (JH) {
         // one side of joint / actuator jx per lane (act_same, checked on the host)
-        const int jb = child ? X.J.bc : X.J.bp;
-        if (X.hasA) act_torque_half<F>(X.J, X.JL, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE));
+        const int jb = X.S.body;
+        if (X.hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE));
         if (X.hasJ) {
           const JointC& Jc = X.J;
           v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
-          if (child) st_v3a(E.jslot + (E.nJ + jx) * SLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
-          else st_v3a(E.jslot + jx * SLOT_STRIDE, mul(Jc.Ip, tq));
+          // parent: Ip tq, child: -Ic tq
+          st_v3a(E.jslot + (child ? E.nJ + jx : jx) * SLOT_STRIDE, X.S.sg * mul(X.S.I, tq));
         }
       } else {
       if (X.hasA) {
@@ -2309,11 +2326,10 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       if constexpr (JH) {
         if (X.hasJ) {
           const JointC& Jc = X.J;
-          const int jb = child ? Jc.bc : Jc.bp;
-          QP o = ldqp(E.qp + jb * QP_STRIDE);
+          QP o = ldqp(E.qp + X.S.body * QP_STRIDE);
           v3 dpo;
           q4 dro;
-          joint_apply_half(Jc, X.JL, child, o, dpo, dro);
+          joint_apply_half(Jc, X.JL, X.S, child, o, dpo, dro);
           st_slot(E.jslot + (child ? E.nJ + jx : jx) * SLOT_STRIDE, dpo, dro, 0.f);
         }
       } else if (X.hasJ) {

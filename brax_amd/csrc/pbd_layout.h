@@ -120,8 +120,13 @@ enum {
   LI_ACT_H = 176,
   LI_JLIM = 184,    // the lane's joint's first limit row (LL_*), both mappings
   LI_JLIM_H = 192,
-  LANE_W = 200
+  LI_SIDE_H = 200,  // joint halves: this lane's side of its joint (LS_*)
+  LANE_W = 216
 };
+// a joint-halves lane's side (lanes 8-15: the child's): its anchor offset,
+// hinge axis and reference axis in its body's frame, that body's inverse
+// inertia and mass, the side's sign (+1 parent, -1 child) and the body
+enum { LS_OFF = 0, LS_AX0 = 3, LS_AX2 = 6, LS_I = 9, LS_M = 12, LS_SG = 13, LS_BODY = 14 };
 // a revolute limit row [lo, hi] as the SINGLE-mode kernels test it: the
 // pseudo-angles of the limits (a monotone stand-in for atan2 over (-pi, pi],
 // +-3 past +-pi) and their cosines / sines

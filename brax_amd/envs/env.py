@@ -7,6 +7,7 @@ wrappers sit directly above it (`wrappers.py` folds them into the launch).
 States are batched: every leaf has a leading env axis (B, ...).
 """
 import abc
+import collections.abc
 import ctypes as C
 import dataclasses
 from typing import Any, Dict
@@ -16,7 +17,7 @@ import torch
 
 from brax_amd import _native
 from brax_amd import abi
-from brax_amd.base import QP, packed_view
+from brax_amd.base import PackedQP, QP, packed_view
 from brax_amd.system import System, _stream, qp_struct
 
 
@@ -32,6 +33,51 @@ class State:
 
   def replace(self, **kw):
     return dataclasses.replace(self, **kw)
+
+
+class _Metrics(collections.abc.MutableMapping):
+  """State.metrics of a kernel env step: the env's metric keys over the
+  columns of the step's (B, M) metrics buffer, plus the entries carried from
+  the input state. The column views are built on first access (ten views
+  are ~10 µs of host time per step); a dict otherwise."""
+
+  __slots__ = ('_m', '_keys', '_extra', '_d')
+
+  def __init__(self, m, keys, extra):
+    self._m, self._keys, self._extra, self._d = m, keys, extra, None
+
+  def _dict(self):
+    if self._d is None:
+      d = dict(self._extra)
+      if self._keys:
+        d.update(zip(self._keys, self._m.unbind(1)))
+      self._d = d
+    return self._d
+
+  def carried(self, keys):
+    """The entries a next step carries over (those it does not rewrite)."""
+    if self._d is None:
+      return self._extra if keys == self._keys else {
+          k: v for k, v in self._dict().items() if k not in keys}
+    return {k: v for k, v in self._d.items() if k not in keys}
+
+  def __getitem__(self, k):
+    return self._dict()[k]
+
+  def __setitem__(self, k, v):
+    self._dict()[k] = v
+
+  def __delitem__(self, k):
+    del self._dict()[k]
+
+  def __iter__(self):
+    return iter(self._dict())
+
+  def __len__(self):
+    return len(self._dict())
+
+  def __repr__(self):
+    return repr(self._dict())
 
 
 def key_to_seed(rng):
@@ -272,9 +318,15 @@ class PhysicsEnv(Env):
   def step(self, state: State, action) -> State:
     return self._chain_step(state, action, {})
 
+  def _step_packed(self, state, action, opts):
+    return _step_packed_impl(self, state, action, opts)
+
   def _chain_step(self, state, action, opts):
     dev = self.sys.device
-    B = state.qp.pos.shape[0]
+    qin = state.qp
+    if type(qin) is PackedQP:
+      return self._step_packed(state, action, opts)
+    B = qin.pos.shape[0]
     act = action
     if type(act) is not torch.Tensor or act.dtype != torch.float32 or not act.is_cuda:
       act = torch.as_tensor(act, dtype=torch.float32, device=dev)
@@ -330,6 +382,63 @@ class PhysicsEnv(Env):
     if self.metric_keys:
       metrics.update(zip(self.metric_keys, met.unbind(1)))
     return State(qp=qp, obs=obs, reward=reward, done=done, metrics=metrics, info=info)
+
+
+def _step_packed_impl(self, state, action, opts):
+  """`_chain_step` for a packed input QP through `bx_env_step_packed`: one
+  output allocation, every pointer plain, and only the views the State
+  needs (the QP fields and metric columns are built on first access)."""
+  dev = self.sys.device
+  qbuf = state.qp._buf  # pylint: disable=protected-access
+  B = qbuf.shape[0]
+  act = action
+  if type(act) is not torch.Tensor or act.dtype != torch.float32 or not act.is_cuda:
+    act = torch.as_tensor(act, dtype=torch.float32, device=dev)
+  if act.dim() == 1:
+    act = act.reshape(1, -1).expand(B, -1)
+  if act.dim() != 2 or act.shape[0] != B or act.shape[1] != self.action_size:
+    raise ValueError(f'action shape {tuple(act.shape)} != {(B, self.action_size)}')
+  if act.stride(-1) != 1:
+    act = act.contiguous()
+  if qbuf.dtype != torch.float32 or not qbuf.is_cuda or not qbuf.is_contiguous():
+    qbuf = qbuf.contiguous().float()
+  info_in = state.info
+  auto = bool(opts.get('auto_reset'))
+  first_qp = info_in.get('first_qp') if auto else None
+  first_obs = info_in.get('first_obs') if auto else None
+  if auto and (first_qp is None or first_obs is None):
+    raise ValueError('AutoResetWrapper state lacks first_qp / first_obs')
+  p = self._cached_params(opts, first_qp, first_obs)
+  done_in = _f32(state.done, dev)
+  steps_in = info_in.get('steps')
+  if steps_in is not None:
+    steps_in = _f32(steps_in, dev)
+  rng_in = info_in.get('rng')
+  if rng_in is None and getattr(self, 'needs_rng', False):
+    rng_in = torch.zeros((B,), dtype=torch.int32, device=dev)  # a state built by hand
+  rng_out = torch.empty_like(rng_in) if rng_in is not None else None
+  N, O, M = self.sys.num_bodies, self.obs_size, len(self.metric_keys)
+  out = torch.empty((B * (N * 16 + O + 4 + M),), dtype=torch.float32, device=dev)
+  _native.check(_native.lib().bx_env_step_packed(
+      self.sys._h, C.byref(p), B, qbuf.data_ptr(), done_in.data_ptr(),  # pylint: disable=protected-access
+      None if steps_in is None else steps_in.data_ptr(),
+      None if rng_in is None else rng_in.data_ptr(), act.data_ptr(), act.stride(0),
+      act.shape[1], out.data_ptr(), None if rng_out is None else rng_out.data_ptr(),
+      _stream(dev.index)))
+  q, obs, reward, done, steps, trunc, met = torch.split(out, (B * N * 16, B * O, B, B, B, B, B * M))
+  info = dict(info_in)
+  if p.episode_length > 0:
+    info['steps'] = steps
+    info['truncation'] = trunc
+  if rng_out is not None:
+    info['rng'] = rng_out
+  keys = self.metric_keys
+  m_in = state.metrics
+  extra = m_in.carried(keys) if type(m_in) is _Metrics else {
+      k: v for k, v in m_in.items() if k not in keys}
+  metrics = _Metrics(met.view(B, M) if M else None, keys, extra)
+  return State(qp=PackedQP(q.view(B, N, 16)), obs=obs.view(B, O), reward=reward, done=done,
+               metrics=metrics, info=info)
 
 
 def _f32(x, dev):

@@ -18,7 +18,7 @@ from brax_amd import _native
 from brax_amd import abi
 from brax_amd import compiler
 from brax_amd import config as cfgmod
-from brax_amd.base import Info, P, QP, packed_view
+from brax_amd.base import Info, P, PackedQP, QP, packed_view
 
 
 try:
@@ -51,6 +51,23 @@ def _field(t, batched):
 def qp_struct(qp, batched):
   """bx_qp view of a QP. Batched structs are cached on the (frozen) QP: its
   fields cannot be re-bound, so the pointers and strides stay valid."""
+  if batched and type(qp) is PackedQP and qp._buf.dim() == 3:  # pylint: disable=protected-access
+    # the packed buffer itself: no field views
+    s = qp.__dict__.get('_bxs')
+    if s is not None:
+      return s
+    buf = qp._buf  # pylint: disable=protected-access
+    if buf.dtype != torch.float32 or not buf.is_cuda or not buf.is_contiguous():
+      raise TypeError('QP fields must be float32 device tensors')
+    base, es = buf.data_ptr(), buf.stride(0)
+    s = abi.BxQP()
+    for name, off in (('pos', 0), ('rot', 3), ('vel', 7), ('ang', 10)):
+      f = getattr(s, name)
+      f.ptr = base + 4 * off
+      f.env_stride = es
+      f.body_stride = 16
+    object.__setattr__(qp, '_bxs', s)
+    return s
   if batched:
     s = qp.__dict__.get('_bxs')
     # (a copied QP carries the attribute over: re-check the pointers)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 6
+#define BX_ABI_VERSION 7
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
 enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
@@ -335,6 +335,18 @@ int bx_system_step(bx_system* sys, int64_t n_envs, const bx_qp* qp_in,
 int bx_env_step(bx_system* sys, const bx_env_params* env, int64_t n_envs,
                 const bx_env_state* in, const float* act, int64_t act_stride,
                 int64_t act_width, const bx_env_state* out, void* stream);
+
+/* bx_env_step on the packed layout, every pointer plain: the input state is
+ * qp_in (B,N,16) (pos 0:3, rot 3:7, vel 7:10, ang 10:13), done_in (B,),
+ * steps_in (B,) or NULL, rng_in (B,) or NULL; the output is ONE buffer
+ * `out` holding qp (B,N,16) | obs (B,O) | reward | done | steps |
+ * truncation (B each) | metrics (B,M), and rng_out (B,) or NULL. Same
+ * semantics and errors as bx_env_step; the host-side fast path of
+ * Env.step. */
+int bx_env_step_packed(bx_system* sys, const bx_env_params* env, int64_t n_envs,
+                       const float* qp_in, const float* done_in, const float* steps_in,
+                       const uint32_t* rng_in, const float* act, int64_t act_stride,
+                       int64_t act_width, float* out, uint32_t* rng_out, void* stream);
 
 /* Batched System.default_qp from per-env joint angles/velocities
  * (B, num_joint_dof) contiguous (system.py:112-242). */
