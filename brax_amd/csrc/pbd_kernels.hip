@@ -1192,13 +1192,18 @@ __device__ __forceinline__ v3 sel3(bool s, v3 a, v3 b) {
 }
 
 // Joint.apply_angle_update (joints.py:130-152), this side's rotation part
-__device__ __forceinline__ q4 angle_update_half(const JointC& J, const JSide& S, const q4& ro, v3 dq) {
+// Joint.apply_angle_update (joints.py:130-152): the impulse p of an angular
+// correction dq (the same for both sides) ...
+__device__ __forceinline__ v3 angle_impulse(const JointC& J, v3 dq) {
   float th = safe_norm(dq);
   v3 n = dq / (th + 1e-6f);
   float w1 = dot(n, mul(J.Ip, n));
   float w2 = dot(n, mul(J.Ic, n));
   float dl = -th / (w1 + w2 + 1e-6f);
-  v3 p = -dl * n;
+  return -dl * n;
+}
+// ... and this side's rotation part of it
+__device__ __forceinline__ q4 angle_update_side(const JointC& J, const JSide& S, const q4& ro, v3 p) {
   return J.sa * ((S.sg * 0.5f) * vec_quat_mul(mul(S.I, p), ro));
 }
 
@@ -1233,8 +1238,12 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   v3 dq1 = cross(axis, axis_c);
   v3 n1 = hinge_turn(axis, ref_p, ref_c, JL);
   v3 dq2 = cross(n1, ref_c);
-  q4 a1 = angle_update_half(J, S, o.rot, dq1);
-  q4 a2 = angle_update_half(J, S, o.rot, dq2);
+  // both halves hold the same dq1 and dq2: the parent lane computes dq1's
+  // impulse, the child lane dq2's, and they trade them
+  const v3 pm = angle_impulse(J, sel3(child, dq2, dq1));
+  const v3 po = xh3(pm);
+  q4 a1 = angle_update_side(J, S, o.rot, sel3(child, po, pm));
+  q4 a2 = angle_update_side(J, S, o.rot, sel3(child, pm, po));
   dro = dro + (a1 + a2);
 }
 
