@@ -250,7 +250,7 @@ def _rocprof_avg(kernel):
   if d.get('lib_sha1') != sha or not k:
     return None
   return {'avg_ms': k['avg_ns'] * 1e-6, 'calls': k.get('calls'), 'source': d.get('source'),
-          'lib_sha1': sha}
+          'lib_sha1': sha, 'sq': k.get('sq')}
 
 
 def main():
@@ -344,6 +344,8 @@ def main():
   tr = _traffic()
   k = ((tr or {}).get('kernels') or {}).get(ANT_KERNEL)
   traffic = k['hbm_bytes_per_launch'] if k and k.get('batch') == B else None
+  rp = _rocprof_avg(ANT_KERNEL)
+  sq = (rp or {}).get('sq') or {}
   out = {
       'metric': 'env-steps/sec (Ant, 4096 envs/GPU)',
       'value': value,
@@ -372,7 +374,10 @@ def main():
                    'kernel': ANT_KERNEL, 'kernel_ms': kern_ms,
                    'kernel_ms_source': 'HIP events over 200 back-to-back bx_env_step launches '
                                        'on the launch stream (kernel_train)',
-                   'rocprof': _rocprof_avg(ANT_KERNEL),
+                   # the SQ issue view of the same kernel (committed counters of
+                   # this library build): VALU instructions x 4 cycles / wave cycles
+                   'valu_issue_frac': sq.get('valu_issue_frac'),
+                   'rocprof': rp,
                    'flops_per_launch': flops_per_launch,
                    'bytes_per_launch': bytes_per_launch,
                    'hbm': {'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',

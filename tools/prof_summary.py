@@ -104,6 +104,19 @@ def main():
   lib = os.path.join(ROOT, 'brax_amd', '_lib', 'libbrax_amd.so')
   with open(lib, 'rb') as f:
     sha = hashlib.sha1(f.read()).hexdigest()
+  # per-wave SQ issue figures of the kernels the SQ pass counted
+  # (SQ_WAVE_CYCLES counts quad-cycles; one wave issues at most one VALU
+  # instruction per 4 cycles, MI355X_MICROARCH.md)
+  for k, e in res.items():
+    c = e.get('counters', {})
+    waves = c.get('SQ_WAVES', {}).get('mean')
+    if k in stats and waves and 'SQ_INSTS_VALU' in c and 'SQ_WAVE_CYCLES' in c:
+      valu = c['SQ_INSTS_VALU']['mean'] / waves
+      cyc = 4 * c['SQ_WAVE_CYCLES']['mean'] / waves
+      stats[k]['sq'] = {'source': f'profiles/{tag}_counters.json', 'waves': waves,
+                        'valu_insts_per_wave': valu,
+                        'lds_insts_per_wave': c.get('SQ_INSTS_LDS', {}).get('mean', 0) / waves,
+                        'cycles_per_wave': cyc, 'valu_issue_frac': 4 * valu / cyc}
   with open(os.path.join(prof, 'rocprof_latest.json'), 'w') as f:
     json.dump({'round': tag, 'source': f'profiles/{tag}_kernel_stats.csv', 'lib_sha1': sha,
                'kernels': stats}, f, indent=1)
