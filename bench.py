@@ -49,8 +49,16 @@ def _dist():
     import torch.distributed as dist
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # BX_DIST_BACKEND=gloo: a rehearsal of the N-rank path with several ranks
+    # on one GPU (RCCL refuses duplicate devices); the product run is RCCL
+    backend = os.environ.get('BX_DIST_BACKEND', 'nccl')
+    if backend != 'nccl':
+      local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
-    dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    if backend == 'nccl':
+      dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+      dist.init_process_group(backend)
     return dist, dist.get_rank(), ws, local
   return None, 0, 1, 0
 
