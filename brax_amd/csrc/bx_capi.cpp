@@ -576,12 +576,12 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     };
     // the limit row's pseudo-angles (kernels' pseudo_angle) and cos / sin,
     // from the radians the record holds, in double
-    auto put_lim = [&](int lane, int base, int j) {
+    auto put_lim = [&](int lane, int base, int j, int row) {
       if (J == 0) return;
       const uint32_t* s = &B.w[H.o_joint + j * JOINT_STRIDE];
       for (int side = 0; side < 2; side++) {
         float lf;
-        std::memcpy(&lf, &s[J_LIM + side], 4);
+        std::memcpy(&lf, &s[J_LIM + 2 * row + side], 4);
         const double l = lf, c = std::cos(l), sn = std::sin(l);
         double p;
         if (l <= -M_PI) p = -3.0;
@@ -620,8 +620,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       put_joint(l, LI_JOINT, l < J ? l : 0);
       put_act(l, LI_ACT, l < K ? l : 0);
       put_joint(l, LI_JOINT_H, (l & 7) < J ? (l & 7) : 0);
-      put_lim(l, LI_JLIM, l < J ? l : 0);
-      put_lim(l, LI_JLIM_H, (l & 7) < J ? (l & 7) : 0);
+      put_lim(l, LI_JLIM, l < J ? l : 0, 0);
+      put_lim(l, LI_JLIM12, l < J ? l : 0, 1);
+      put_lim(l, LI_JLIM12 + 8, l < J ? l : 0, 2);
+      put_lim(l, LI_JLIM_H, (l & 7) < J ? (l & 7) : 0, 0);
       if (J > 0) {
         // the joint-halves side: the parent's on lanes 0-7, the child's on 8-15
         const bool child = (l & 8) != 0;

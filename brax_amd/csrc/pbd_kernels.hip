@@ -270,11 +270,35 @@ __device__ __forceinline__ v3 hinge_turn(v3 axis, v3 ref_p, v3 ref_c, const JLim
   return turn(ref_p, axis, cph, sph);
 }
 
+// A limit row (LL_*) from this lane's lane image, fetched where it is used:
+// the spherical kernels have no registers to hold three rows over the step.
+// li: the lane's first 16-byte group; g: the row's group (LIM_G*). The empty
+// asm makes every use a fresh L2 read rather than a hoisted register copy.
+enum { LIM_G0 = LI_JLIM / 4, LIM_G1 = LI_JLIM12 / 4, LIM_G2 = LI_JLIM12 / 4 + 2 };
+__device__ __forceinline__ JLim ld_lim(const uint4* li, int g) {
+  asm volatile("" : "+s"(g));
+  const uint4 a = li[g * LANE_IMG_LANES], b = li[(g + 1) * LANE_IMG_LANES];
+  return JLim{__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z),
+              __uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y)};
+}
+// the limit cut of a torque actuator needs only the pseudo-angles
+__device__ __forceinline__ float2 ld_lim_p(const uint4* li, int g) {
+  asm volatile("" : "+s"(g));
+  const uint4 a = li[g * LANE_IMG_LANES];
+  return make_float2(__uint_as_float(a.x), __uint_as_float(a.y));
+}
+__device__ __forceinline__ constexpr int lim_group(int l) {
+  return l == 0 ? LIM_G0 : (l == 1 ? LIM_G1 : LIM_G2);
+}
+
 // JL: the hoisted kernels' limit row (pseudo-angles, cos / sin): the
-// revolute hinge turn without atan2 / sincos; null: the reference's formulas
+// revolute hinge turn without atan2 / sincos; LI (no JL): the lane image
+// whose limit rows the revolute and spherical limits read the same way;
+// neither: the reference's formulas
 template <int F>
 __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, q4& dpr,
-                            v3& dcp, q4& dcr, const JLim* JL = nullptr) {
+                            v3& dcp, q4& dcr, const JLim* JL = nullptr,
+                            const uint4* LI = nullptr) {
   // positional constraint: apply_position_update (joints.py:154-195)
   v3 pw = p.pos + rotate(J.off_p, p.rot);
   v3 cw = c.pos + rotate(J.off_c, c.rot);
@@ -301,6 +325,8 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
     v3 n1;
     if (JL) {
       n1 = hinge_turn(axis, ref_p, ref_c, *JL);
+    } else if (LI) {
+      n1 = hinge_turn(axis, ref_p, ref_c, ld_lim(LI, LIM_G0));
     } else {
       float psi = signed_angle(axis, ref_p, ref_c);
       float ph = clampf(psi, J.lim[0], J.lim[1]);
@@ -328,6 +354,19 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
     v3 n2v[3] = {lon, xz, a2c};
 #pragma unroll
     for (int l = 0; l < 3; l++) {
+      if (LI) {
+        // limit_angle on pseudo-angles: inside the limits the row's impulse
+        // is zero whatever the angle, outside n1 is turned by the limit's
+        // own (cos, sin); neither atan2 nor sincos
+        const JLim L = ld_lim(LI, lim_group(l));
+        const float y = dot(cross(n1v[l], n2v[l]), nv[l]), x = dot(n1v[l], n2v[l]);
+        const float pa = pseudo_angle(x, y);
+        const bool below = pa < L.plo, above = pa > L.phi;
+        const v3 n1 = turn(n1v[l], nv[l], below ? L.clo : L.chi, below ? L.slo : L.shi);
+        const v3 dq = cross(n1, n2v[l]) * ((below || above) ? 1.f : 0.f);
+        angle_update(J, p.rot, c.rot, dq, ap, ac);
+        continue;
+      }
       // limit_angle (joints.py:343-355)
       float ph = signed_angle(nv[l], n1v[l], n2v[l]);
       float lo = J.lim[2 * l], hi = J.lim[2 * l + 1];
@@ -1127,8 +1166,49 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
 // Torque/Angle.apply_reduced for actuator a (lane) -> aslot
 template <int F>
 __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, const Env& E,
-                                           const float* al, int a, const JLim* JL = nullptr) {
+                                           const float* al, int a, const JLim* JL = nullptr,
+                                           const uint4* LI = nullptr) {
   QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
+  if (LI && is_torque<F>(A.type)) {
+    // torque actuators on the lane image's limit rows: the angles
+    // (axis_angle) enter only the limit cut, taken on pseudo-angles
+    v3 tq;
+    const float t0 = al[0] * A.strength * -1.f;
+    if (is_rev<F>(Jc.type)) {
+      const v3 axis = rotate(Jc.axp[0], p.rot);
+      const v3 ref_p = rotate(Jc.axp[2], p.rot), ref_c = rotate(Jc.axc[2], cq.rot);
+      const float pa = pseudo_angle(dot(ref_p, ref_c), dot(cross(ref_p, ref_c), axis));
+      const float2 L = ld_lim_p(LI, LIM_G0);
+      tq = mk(0.f, 0.f, 0.f) + axis * ((pa < L.x || pa > L.y) ? 0.f : t0);
+    } else {
+      // Spherical.axis_angle (joints.py:388-415): psi, theta = +-acos(cb)
+      // (the pseudo-angle of (cb, +-sqrt(1 - cb^2))), phi
+      const v3 a1p = rotate(Jc.axp[0], p.rot), a2p = rotate(Jc.axp[1], p.rot);
+      const v3 a1c = rotate(Jc.axc[0], cq.rot), a2c = rotate(Jc.axc[1], cq.rot);
+      const v3 a3c = rotate(Jc.axc[2], cq.rot);
+      v3 lon = cross(a3c, a1p);
+      lon = lon / (1e-10f + safe_norm(lon));
+      v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
+      xz = xz / (1e-10f + safe_norm(xz));
+      const float cb = clampf(dot(xz, a1p), -1.f, 1.f);
+      const float sg = signf(dot(a1p, a3c));
+      float pa[3];
+      pa[0] = pseudo_angle(dot(a2p, lon), dot(cross(a2p, lon), a1p));
+      pa[1] = pseudo_angle(sg == 0.f ? 1.f : cb, sg * sqrtf(fmaxf(1.f - cb * cb, 0.f)));
+      pa[2] = pseudo_angle(dot(a2c, lon), dot(cross(a2c, lon), -a3c));
+      const v3 axes[3] = {a1p, a2c, a3c};
+      tq = mk(0.f, 0.f, 0.f);
+#pragma unroll
+      for (int l = 0; l < 3; l++) {
+        const float2 L = ld_lim_p(LI, lim_group(l));
+        const float t = al[l] * A.strength * -1.f;
+        tq = tq + axes[l] * ((pa[l] < L.x || pa[l] > L.y) ? 0.f : t);
+      }
+    }
+    st_v3a(E.aslot + a * ASLOT_STRIDE, mul(Jc.Ip, tq));
+    st_v3a(E.aslot + (E.nK + a) * ASLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
+    return;
+  }
   if (JL && is_rev<F>(Jc.type) && is_torque<F>(A.type)) {
     // a revolute torque actuator needs its hinge angle only for the limit
     // cut: the test on pseudo-angles (no atan2)
@@ -2244,10 +2324,13 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   const float h = H.h;
   const v3 g = mk(H.gx, H.gy, H.gz);
   constexpr bool JH = (F & F_JH) != 0;
-  // revolute-only kernels take the atan2-free hinge (hinge_turn); with
-  // spherical joints in the same wave the extra branch costs more than it
-  // saves (Humanoid 74.5 -> 67.5 M env-steps/s, profiles/r02u_bench.log)
-  const JLim* JLP = (F & F_SPH) == 0 ? &X.JL : nullptr;
+  // revolute-only kernels take the atan2-free hinge (hinge_turn) on the
+  // hoisted limit row. Kernels with spherical joints have no registers for
+  // three rows (hoisting them: 256 VGPRs + 548 B of scratch, Humanoid 74.5 ->
+  // 70.5 M env-steps/s): they read the rows from the lane image where they
+  // test them (ld_lim), and take the pseudo-angle limit tests for the
+  // spherical rows and torque cuts too (Humanoid 75.0 -> 78.9 M)
+  const uint4* LIP = (F & F_SPH) != 0 ? reinterpret_cast<const uint4*>(c.w + H.o_lane) + lane : nullptr;
   const int jx = lane & 7;         // JH: this lane's joint / actuator
   const bool child = lane >= 8;    // JH: this lane's side
   float* myqp = E.qp + lane * QP_STRIDE;
@@ -2298,7 +2381,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       if (X.hasA) {
         const ActC& A = X.A;
         if (H.act_same) {
-          act_torque<F>(X.J, A, E, al, lane, JLP);
+          act_torque<F>(X.J, A, E, al, lane, JLP, LIP);
         } else {
           JointC Jc = load_joint(c, H, A.joint);
           act_torque<F>(Jc, A, E, al, lane);
@@ -2346,7 +2429,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
         q4 dpr, dcr;
-        joint_apply<F>(Jc, p, cq, dpp, dpr, dcp, dcr, JLP);
+        joint_apply<F>(Jc, p, cq, dpp, dpr, dcp, dcr, JLP, LIP);
         st_slot(E.jslot + lane * SLOT_STRIDE, dpp, dpr, 0.f);
         st_slot(E.jslot + (E.nJ + lane) * SLOT_STRIDE, dcp, dcr, 0.f);
       }

@@ -121,13 +121,14 @@ enum {
   LI_JLIM = 184,    // the lane's joint's first limit row (LL_*), both mappings
   LI_JLIM_H = 192,
   LI_SIDE_H = 200,  // joint halves: this lane's side of its joint (LS_*)
-  LANE_W = 216
+  LI_JLIM12 = 216,  // the lane's joint's limit rows 1 and 2 (LL_*, 8 words each; lane j -> joint j)
+  LANE_W = 232
 };
 // a joint-halves lane's side (lanes 8-15: the child's): its anchor offset,
 // hinge axis and reference axis in its body's frame, that body's inverse
 // inertia and mass, the side's sign (+1 parent, -1 child) and the body
 enum { LS_OFF = 0, LS_AX0 = 3, LS_AX2 = 6, LS_I = 9, LS_M = 12, LS_SG = 13, LS_BODY = 14 };
-// a revolute limit row [lo, hi] as the SINGLE-mode kernels test it: the
+// a limit row [lo, hi] as the SINGLE-mode kernels test it: the
 // pseudo-angles of the limits (a monotone stand-in for atan2 over (-pi, pi],
 // +-3 past +-pi) and their cosines / sines
 enum { LL_PLO = 0, LL_PHI = 1, LL_CLO = 2, LL_SLO = 3, LL_CHI = 4, LL_SHI = 5 };
