@@ -237,7 +237,7 @@ template <int F> __device__ __forceinline__ bool is_oneway(int ow) {
 // Joint.apply_angle_update (joints.py:130-152): adds rot parts into dqp/dqc
 __device__ __forceinline__ void angle_update(const JointC& J, const q4& rp, const q4& rc, v3 dq,
                                              q4& dqp, q4& dqc) {
-  float th = safe_norm(dq);
+  float th = cancel_norm(dq);
   v3 n = dq / (th + 1e-6f);
   float w1 = dot(n, mul(J.Ip, n));
   float w2 = dot(n, mul(J.Ic, n));
@@ -304,7 +304,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
   v3 cw = c.pos + rotate(J.off_c, c.rot);
   v3 dx = pw - cw;
   v3 rp = pw - p.pos, rc = cw - c.pos;
-  float cc = safe_norm(dx);
+  float cc = cancel_norm(dx);
   v3 n = dx / (cc + 1e-6f);
   v3 cr1 = cross(rp, n), cr2 = cross(rc, n);
   float w1 = 1.f / J.mp + dot(cr1, mul(J.Ip, cr1));
@@ -1275,7 +1275,7 @@ __device__ __forceinline__ v3 sel3(bool s, v3 a, v3 b) {
 // Joint.apply_angle_update (joints.py:130-152): the impulse p of an angular
 // correction dq (the same for both sides) ...
 __device__ __forceinline__ v3 angle_impulse(const JointC& J, v3 dq) {
-  float th = safe_norm(dq);
+  float th = cancel_norm(dq);
   v3 n = dq / (th + 1e-6f);
   float w1 = dot(n, mul(J.Ip, n));
   float w2 = dot(n, mul(J.Ic, n));
@@ -1299,7 +1299,7 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   v3 ro = wo - o.pos;
   v3 wt = xh3(wo);
   v3 dx = child ? wt - wo : wo - wt;
-  float cc = safe_norm(dx);
+  float cc = cancel_norm(dx);
   v3 n = dx / (cc + 1e-6f);
   v3 cr = cross(ro, n);
   float wm = 1.f / m + dot(cr, mul(I, cr));
@@ -2330,6 +2330,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   // 70.5 M env-steps/s): they read the rows from the lane image where they
   // test them (ld_lim), and take the pseudo-angle limit tests for the
   // spherical rows and torque cuts too (Humanoid 75.0 -> 78.9 M)
+  const JLim* JLP = (F & F_SPH) == 0 ? &X.JL : nullptr;
   const uint4* LIP = (F & F_SPH) != 0 ? reinterpret_cast<const uint4*>(c.w + H.o_lane) + lane : nullptr;
   const int jx = lane & 7;         // JH: this lane's joint / actuator
   const bool child = lane >= 8;    // JH: this lane's side

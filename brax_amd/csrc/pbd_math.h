@@ -39,6 +39,20 @@ __device__ __forceinline__ float safe_norm(v3 a) {
   return z ? 0.f : norm(a);
 }
 
+// safe_norm with the bare v_sqrt_f32 (<= 1 ulp) in the SINGLE-mode TU, for
+// a constraint's magnitude only: c and the direction n = dx / (c + 1e-6)
+// meet again in the impulse (c / w(n)) n, so the ulp cancels to first order
+// and reaches the impulse through w's |n|^2 only (<= 2 ulp relative; the
+// joint position and angle impulses)
+__device__ __forceinline__ float cancel_norm(v3 a) {
+#if defined(BX_TU_FAST) && !defined(BX_IEEE_CANCEL_NORM)
+  bool z = fabsf(a.x) <= 1e-8f && fabsf(a.y) <= 1e-8f && fabsf(a.z) <= 1e-8f;
+  return z ? 0.f : __builtin_amdgcn_sqrtf(dot(a, a));
+#else
+  return safe_norm(a);
+#endif
+}
+
 __device__ __forceinline__ q4 operator+(q4 a, q4 b) {
   return {a.w + b.w, a.x + b.x, a.y + b.y, a.z + b.z};
 }
