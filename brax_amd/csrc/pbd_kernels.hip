@@ -1017,7 +1017,7 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
     v3 p1bar = ao_pos + rotate(r1, ao_rot);
     v3 dp = cpos - p1bar;
     v3 dt = dp - dot(dp, n) * n;
-    float c2 = safe_norm(dt);
+    float c2 = cancel_norm(dt);
     v3 n2 = dt / (c2 + 1e-6f);
     cr1 = cross(pp, n2);
     w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
@@ -1051,7 +1051,7 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
   v3 dt = dp - dot(dp, n) * n;
   pp = cpos - a.pos;
   pc = cpos - b.pos;
-  float c2 = safe_norm(dt);
+  float c2 = cancel_norm(dt);
   v3 n2 = dt / (c2 + 1e-6f);
   cr1 = cross(pp, n2);
   cr2 = cross(pc, n2);
@@ -1078,7 +1078,7 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
                    : (a.vel + cross(a.ang, ra)) - (b.vel + cross(b.ang, rb));
   float vn = dot(rv, n);
   v3 vt = rv - n * vn;
-  float vtn = safe_norm(vt);
+  float vtn = cancel_norm(vt);
   v3 vtd = vt / (1e-6f + vtn);
   float lim = R.fric * fabsf(dlam) / (2.f * h);
   float mag = fminf(lim, vtn);
@@ -1101,7 +1101,7 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
   v3 dvr = n * (-vn - mn);
   v3 pp = cpos - a.pos;
   v3 pc = (cpos + n * cpen) - b.pos;
-  float c = safe_norm(dvr);
+  float c = cancel_norm(dvr);
   v3 n2 = dvr / (c + 1e-6f);
   v3 cr1 = cross(pp, n2);
   float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));

@@ -43,7 +43,8 @@ __device__ __forceinline__ float safe_norm(v3 a) {
 // a constraint's magnitude only: c and the direction n = dx / (c + 1e-6)
 // meet again in the impulse (c / w(n)) n, so the ulp cancels to first order
 // and reaches the impulse through w's |n|^2 only (<= 2 ulp relative; the
-// joint position and angle impulses)
+// joint position and angle impulses, the contacts' friction and restitution
+// impulses, whose clamps against the norm move by the same ulp)
 __device__ __forceinline__ float cancel_norm(v3 a) {
 #if defined(BX_TU_FAST) && !defined(BX_IEEE_CANCEL_NORM)
   bool z = fabsf(a.x) <= 1e-8f && fabsf(a.y) <= 1e-8f && fabsf(a.z) <= 1e-8f;
