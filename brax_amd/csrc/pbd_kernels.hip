@@ -234,19 +234,15 @@ template <int F> __device__ __forceinline__ bool is_oneway(int ow) {
   if constexpr ((F & F_TW) == 0) return true; else return ow != 0;
 }
 
-// Joint.apply_angle_update (joints.py:130-152): adds rot parts into dqp/dqc
-__device__ __forceinline__ void angle_update(const JointC& J, const q4& rp, const q4& rc, v3 dq,
-                                             q4& dqp, q4& dqc) {
+// Joint.apply_angle_update (joints.py:130-152): the impulse p of an angular
+// correction dq; each side's rotation update is linear in it
+__device__ __forceinline__ v3 angle_impulse(const JointC& J, v3 dq) {
   float th = cancel_norm(dq);
   v3 n = dq / (th + 1e-6f);
   float w1 = dot(n, mul(J.Ip, n));
   float w2 = dot(n, mul(J.Ic, n));
   float dl = -th / (w1 + w2 + 1e-6f);
-  v3 p = -dl * n;
-  q4 a = J.sa * (0.5f * vec_quat_mul(mul(J.Ip, p), rp));
-  q4 b = J.sa * (-0.5f * vec_quat_mul(mul(J.Ic, p), rc));
-  dqp = dqp + a;
-  dqc = dqc + b;
+  return -dl * n;
 }
 
 // Revolute/Spherical.apply_reduced (joints.py:270-309, 332-386)
@@ -312,10 +308,12 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
   float dl = -cc / (w1 + w2 + 1e-6f);
   v3 pv = dl * n;
   dpp = J.sp * (pv / J.mp);
-  dpr = J.sp * (0.5f * vec_quat_mul(mul(J.Ip, cross(rp, pv)), p.rot));
   dcp = J.sp * (-pv / J.mc);
-  dcr = J.sp * (-0.5f * vec_quat_mul(mul(J.Ic, cross(rc, pv)), c.rot));
-  q4 ap{0.f, 0.f, 0.f, 0.f}, ac{0.f, 0.f, 0.f, 0.f};
+  // the angle constraints' impulses (apply_angle_update, joints.py:130-152);
+  // each body's rotation update is linear in its angular impulse, so these
+  // and the position constraint's add up before one quaternion product per
+  // body (below)
+  v3 pimp = mk(0.f, 0.f, 0.f);
   if (is_rev<F>(J.type)) {
     v3 axis = rotate(J.axp[0], p.rot);
     v3 ref_p = rotate(J.axp[2], p.rot);
@@ -334,11 +332,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
       n1 = rotate(ref_p, fix);
     }
     v3 dq2 = cross(n1, ref_c);
-    q4 a1p{0, 0, 0, 0}, a1c{0, 0, 0, 0}, a2p{0, 0, 0, 0}, a2c{0, 0, 0, 0};
-    angle_update(J, p.rot, c.rot, dq1, a1p, a1c);
-    angle_update(J, p.rot, c.rot, dq2, a2p, a2c);
-    ap = a1p + a2p;
-    ac = a1c + a2c;
+    pimp = angle_impulse(J, dq1) + angle_impulse(J, dq2);
   } else {
     v3 a1p = rotate(J.axp[0], p.rot), a2p = rotate(J.axp[1], p.rot);
     v3 a1c = rotate(J.axc[0], c.rot), a2c = rotate(J.axc[1], c.rot), a3c = rotate(J.axc[2], c.rot);
@@ -364,7 +358,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
         const bool below = pa < L.plo, above = pa > L.phi;
         const v3 n1 = turn(n1v[l], nv[l], below ? L.clo : L.chi, below ? L.slo : L.shi);
         const v3 dq = cross(n1, n2v[l]) * ((below || above) ? 1.f : 0.f);
-        angle_update(J, p.rot, c.rot, dq, ap, ac);
+        pimp = pimp + angle_impulse(J, dq);
         continue;
       }
       // limit_angle (joints.py:343-355)
@@ -376,11 +370,13 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
       q4 fix = quat_rot_axis(nv[l], ph);
       v3 n1 = rotate(n1v[l], fix);
       v3 dq = cross(n1, n2v[l]) * mask;
-      angle_update(J, p.rot, c.rot, dq, ap, ac);
+      pimp = pimp + angle_impulse(J, dq);
     }
   }
-  dpr = dpr + ap;
-  dcr = dcr + ac;
+  const v3 Pp = J.sp * cross(rp, pv) + J.sa * pimp;
+  const v3 Pc = J.sp * cross(rc, pv) + J.sa * pimp;
+  dpr = 0.5f * vec_quat_mul(mul(J.Ip, Pp), p.rot);
+  dcr = -0.5f * vec_quat_mul(mul(J.Ic, Pc), c.rot);
 }
 
 // Revolute/Spherical.axis_angle (joints.py:311-319, 388-415); returns dof
@@ -1271,21 +1267,6 @@ __device__ __forceinline__ v3 sel3(bool s, v3 a, v3 b) {
   return mk(s ? a.x : b.x, s ? a.y : b.y, s ? a.z : b.z);
 }
 
-// Joint.apply_angle_update (joints.py:130-152), this side's rotation part
-// Joint.apply_angle_update (joints.py:130-152): the impulse p of an angular
-// correction dq (the same for both sides) ...
-__device__ __forceinline__ v3 angle_impulse(const JointC& J, v3 dq) {
-  float th = cancel_norm(dq);
-  v3 n = dq / (th + 1e-6f);
-  float w1 = dot(n, mul(J.Ip, n));
-  float w2 = dot(n, mul(J.Ic, n));
-  float dl = -th / (w1 + w2 + 1e-6f);
-  return -dl * n;
-}
-// ... and this side's rotation part of it
-__device__ __forceinline__ q4 angle_update_side(const JointC& J, const JSide& S, const q4& ro, v3 p) {
-  return J.sa * ((S.sg * 0.5f) * vec_quat_mul(mul(S.I, p), ro));
-}
 
 // Revolute.apply_reduced (joints.py:79-100, 154-195, 270-309), one side: o is
 // this side's body (parent on lanes 0-7, child on 8-15); returns its dp, dq
@@ -1308,7 +1289,6 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   float dl = -cc / (w1 + w2 + 1e-6f);
   v3 pv = dl * n;
   dpo = J.sp * ((sg * pv) / m);
-  dro = J.sp * ((sg * 0.5f) * vec_quat_mul(mul(I, cross(ro, pv)), o.rot));
   // the two angular constraints (axis alignment, limited hinge angle)
   v3 u0 = rotate(S.ax0, o.rot);
   v3 u2 = rotate(S.ax2, o.rot);
@@ -1322,9 +1302,11 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   // impulse, the child lane dq2's, and they trade them
   const v3 pm = angle_impulse(J, sel3(child, dq2, dq1));
   const v3 po = xh3(pm);
-  q4 a1 = angle_update_side(J, S, o.rot, sel3(child, po, pm));
-  q4 a2 = angle_update_side(J, S, o.rot, sel3(child, pm, po));
-  dro = dro + (a1 + a2);
+  // the side's rotation update is linear in the angular impulse: the
+  // position constraint's and both angle constraints' add up before the one
+  // quaternion product (joints.py:150-152, 190-195)
+  const v3 P = J.sp * cross(ro, pv) + J.sa * (pm + po);
+  dro = (sg * 0.5f) * vec_quat_mul(mul(I, P), o.rot);
 }
 
 // Actuator.apply_reduced (actuators.py:52-112) for a revolute joint, one side
