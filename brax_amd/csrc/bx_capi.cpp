@@ -51,6 +51,7 @@ struct bx_system {
   int tpb = 64;     // threads per workgroup of the step kernels (multiple of L)
   bool single_ok = false;
   bool multi_ok = false;  // MODE_MULTI (3): large pbd scenes, 256 threads per env
+  int fold = 0;     // every joint j has torque actuator j (the Ant / Humanoid env kernels)
   size_t lds_env = 0;    // bytes per block for the per-env kernels
   size_t lds_reset = 0;  // bytes per block for default_qp
 };
@@ -677,6 +678,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     // driven by the actuator of the same index
     if (H.single && L == 16 && J <= 8 && K <= 8 && H.act_same && !(f & 1) && !jh_off) f |= 128;
     S->feat = f;
+    S->fold = (H.act_same && K == J && J > 0 && !(f & 2)) ? 1 : 0;
   }
   // the MULTI kernel is instantiated for the lean feature set (revolute,
   // torque, capsule-plane / capsule-capsule, no forces)
@@ -979,7 +981,7 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   a.act_stride = act_stride;
   a.act_width = act_width;
   if (S->mode == 1)
-    HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
+    HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a, S->fold));
   else if (S->mode == 3)  // MULTI-mode systems step envs with the item-loop kernel
     HIP_OK(launch_env_step_generic(S->L, 0, S->feat, S->tpb, n_envs,
                                    (size_t)S->hdr.env_words * 4, as_stream(stream), a));

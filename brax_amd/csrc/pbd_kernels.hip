@@ -1006,8 +1006,6 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
     float dl = -c / (w1 + 1e-6f);
     float cm = c < 0.f ? 1.f : 0.f;
     v3 pv = dl * n * cm;
-    oap = sc * (pv / R.ma);
-    oar = sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
     // static friction
     v3 r1 = rotate(cpos - a.pos, quat_inv(a.rot));
     v3 p1bar = ao_pos + rotate(r1, ao_rot);
@@ -1019,9 +1017,11 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
     w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
     float dlt = -c2 / (w1 + 0.f);
     float sm = fabsf(dlt) < fabsf(R.fric * dl) ? 1.f : 0.f;
-    pv = dlt * n2 * sm * cm;
-    oap = oap + sc * (pv / R.ma);
-    oar = oar + sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
+    // the normal and friction impulses share the lever arm: one position and
+    // one quaternion update for their sum (both linear in the impulse)
+    pv = pv + dlt * n2 * sm * cm;
+    oap = sc * (pv / R.ma);
+    oar = sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
     obp = mk(0.f, 0.f, 0.f);
     obr = q4{0.f, 0.f, 0.f, 0.f};
     return dl * cm;
@@ -1035,10 +1035,9 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
   float dl = -c / (w1 + w2 + 1e-6f);
   float cm = c < 0.f ? 1.f : 0.f;
   v3 pv = dl * n * cm;
-  oap = sc * (pv / R.ma);
-  oar = sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
-  obp = sc * (-pv / R.mb);
-  obr = sc * (-0.5f * vec_quat_mul(mul(R.Ib, cross(pc, pv)), b.rot));
+  // angular impulses of the normal and friction parts (their lever arms
+  // differ) add up before one quaternion product per body
+  const v3 la = cross(pp, pv), lb = cross(pc, pv);
   v3 r1 = rotate(cpos - a.pos, quat_inv(a.rot));
   v3 r2 = rotate(cpos - b.pos, quat_inv(b.rot));
   v3 p1bar = ao_pos + rotate(r1, ao_rot);
@@ -1055,11 +1054,12 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
   w2 = 1.f / R.mb + dot(cr2, mul(R.Ib, cr2));
   float dlt = -c2 / (w1 + w2);
   float sm = fabsf(dlt) < fabsf(dl) ? 1.f : 0.f;
-  pv = dlt * n2 * sm * cm;
-  oap = oap + sc * (pv / R.ma);
-  oar = oar + sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
-  obp = obp + sc * (-pv / R.mb);
-  obr = obr + sc * (0.5f * vec_quat_mul(mul(R.Ib, cross(pc, -pv)), b.rot));
+  const v3 pt = dlt * n2 * sm * cm;
+  const v3 ps = pv + pt;
+  oap = sc * (ps / R.ma);
+  oar = sc * (0.5f * vec_quat_mul(mul(R.Ia, la + cross(pp, pt)), a.rot));
+  obp = sc * (-ps / R.mb);
+  obr = sc * (-0.5f * vec_quat_mul(mul(R.Ib, lb + cross(pc, pt)), b.rot));
   return dl;
 }
 
@@ -1163,7 +1163,7 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
 template <int F>
 __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, const Env& E,
                                            const float* al, int a, const JLim* JL = nullptr,
-                                           const uint4* LI = nullptr) {
+                                           const uint4* LI = nullptr, const v3* tqd = nullptr) {
   QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
   if (LI && is_torque<F>(A.type)) {
     // torque actuators on the lane image's limit rows: the angles
@@ -1182,15 +1182,16 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
       const v3 a1p = rotate(Jc.axp[0], p.rot), a2p = rotate(Jc.axp[1], p.rot);
       const v3 a1c = rotate(Jc.axc[0], cq.rot), a2c = rotate(Jc.axc[1], cq.rot);
       const v3 a3c = rotate(Jc.axc[2], cq.rot);
-      v3 lon = cross(a3c, a1p);
-      lon = lon / (1e-10f + safe_norm(lon));
-      v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
-      xz = xz / (1e-10f + safe_norm(xz));
-      const float cb = clampf(dot(xz, a1p), -1.f, 1.f);
+      // pseudo-angles are scale-free in (x, y): lon and xz enter unnormalised,
+      // (cb, sqrt(1 - cb^2)) as (x, sqrt(|xz|^2 - x^2)) with x = xz . a1p
+      const v3 lon = cross(a3c, a1p);
+      const v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
+      const float xb = dot(xz, a1p), r2 = dot(xz, xz);
       const float sg = signf(dot(a1p, a3c));
+      const float yb = r2 > 0.f ? sg * __builtin_amdgcn_sqrtf(fmaxf(r2 - xb * xb, 0.f)) : sg;
       float pa[3];
       pa[0] = pseudo_angle(dot(a2p, lon), dot(cross(a2p, lon), a1p));
-      pa[1] = pseudo_angle(sg == 0.f ? 1.f : cb, sg * sqrtf(fmaxf(1.f - cb * cb, 0.f)));
+      pa[1] = pseudo_angle(sg == 0.f ? 1.f : xb, yb);
       pa[2] = pseudo_angle(dot(a2c, lon), dot(cross(a2c, lon), -a3c));
       const v3 axes[3] = {a1p, a2c, a3c};
       tq = mk(0.f, 0.f, 0.f);
@@ -1201,6 +1202,7 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
         tq = tq + axes[l] * ((pa[l] < L.x || pa[l] > L.y) ? 0.f : t);
       }
     }
+    if (tqd) tq = tq + *tqd;  // + the joint's damping (FOLD)
     st_v3a(E.aslot + a * ASLOT_STRIDE, mul(Jc.Ip, tq));
     st_v3a(E.aslot + (E.nK + a) * ASLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
     return;
@@ -1313,7 +1315,7 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
 template <int F>
 __device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL, const JSide& S,
                                                 const ActC& A, const Env& E, const float* al, int a,
-                                                bool child, const q4& ro) {
+                                                bool child, const q4& ro, const v3* tqd = nullptr) {
   v3 u0 = rotate(S.ax0, ro);
   v3 u2 = rotate(S.ax2, ro);
   v3 t0 = xh3(u0), t2 = xh3(u2);
@@ -1335,7 +1337,9 @@ __device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL
   v3 tq = mk(0.f, 0.f, 0.f) + axis * t;
   float sgp = is_torque<F>(A.type) ? 1.f : -1.f;
   // parent: sgp * Ip tq, child: -sgp * Ic tq (the side's sign times its inertia)
-  st_v3a(E.aslot + (child ? E.nK + a : a) * ASLOT_STRIDE, (sgp * S.sg) * mul(S.I, tq));
+  float* slot = E.aslot + (child ? E.nK + a : a) * ASLOT_STRIDE;
+  if (tqd) st_v3a(slot, S.sg * mul(S.I, sgp * tq + *tqd));  // + the joint's damping (FOLD)
+  else st_v3a(slot, (sgp * S.sg) * mul(S.I, tq));
 }
 
 // ---------------------------------------------------------------------------
@@ -2294,7 +2298,12 @@ __device__ unsigned long long bx_stamp_wave[4096][16];
 #define BX_KSTAMP(k) do {} while (0)
 #endif
 
-template <int L, int F, int M>
+// FOLD (the Ant / Humanoid env kernels; the host checks that every joint j
+// has torque actuator j): each joint's damping torque is added into its
+// actuator's slot, so the body phase gathers one list instead of two. The
+// actuator slots then no longer hold the actuators alone, which only
+// System.step's Info reads.
+template <int L, int F, int M, bool FOLD = false>
 __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
                                 const float* act, int aw, const Hoist<M>& X, v3& icv, v3& ica,
                                 v3& iaa) {
@@ -2353,8 +2362,14 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       if constexpr (JH) {
         // one side of joint / actuator jx per lane (act_same, checked on the host)
         const int jb = X.S.body;
+        if constexpr (FOLD) {
+          const JointC& Jc = X.J;
+          const v3 tqd = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
+          if (X.hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE), &tqd);
+        } else {
         if (X.hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE));
-        if (X.hasJ) {
+        }
+        if (!FOLD && X.hasJ) {
           const JointC& Jc = X.J;
           v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
           // parent: Ip tq, child: -Ic tq
@@ -2363,14 +2378,18 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       } else {
       if (X.hasA) {
         const ActC& A = X.A;
-        if (H.act_same) {
+        if (FOLD) {
+          const JointC& Jc = X.J;
+          const v3 tqd = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
+          act_torque<F>(X.J, A, E, al, lane, JLP, LIP, &tqd);
+        } else if (H.act_same) {
           act_torque<F>(X.J, A, E, al, lane, JLP, LIP);
         } else {
           JointC Jc = load_joint(c, H, A.joint);
           act_torque<F>(Jc, A, E, al, lane);
         }
       }
-      if (X.hasJ) {
+      if (!FOLD && X.hasJ) {
         const JointC& Jc = X.J;
         v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
         st_v3a(E.jslot + lane * SLOT_STRIDE, mul(Jc.Ip, tq));
@@ -2381,7 +2400,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       BX_STAMP(0);
       if (X.hasB) {
         v3 dpa = gsum3(X.al, E.aslot, ASLOT_STRIDE);
-        v3 dpj = gsum3(X.jl, E.jslot, SLOT_STRIDE);
+        v3 dpj = FOLD ? mk(0.f, 0.f, 0.f) : gsum3(X.jl, E.jslot, SLOT_STRIDE);
         v3 vel = H.vexp * q.vel;
         vel = vel + (fv + g) * h;
         q.vel = mul(vel, X.B.pm);
@@ -3808,7 +3827,7 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
     esync<L>();
     if constexpr (S) {
       v3 icv, ica, iaa;
-      pbd_step_single<L, F, M>(c, H, E, lane, valid, sact, saw, X, icv, ica, iaa);
+      pbd_step_single<L, F, M, EK == EK_ANT || EK == EK_HUM>(c, H, E, lane, valid, sact, saw, X, icv, ica, iaa);
     } else if (H.spring) {
       spring_step<L, F>(c, H, E, lane, valid, sact, saw);
     } else {
@@ -4290,16 +4309,18 @@ hipError_t launch_system_step_single(int L, int feat, int gw, int tpb, int64_t n
   return hipGetLastError();
 }
 hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
-                                  hipStream_t s, const EnvArgs& a) {
+                                  hipStream_t s, const EnvArgs& a, int fold) {
   const int epb = tpb / L;
   dim3 grid((unsigned)((n_envs + epb - 1) / epb));
   // the benchmarked envs get kernels holding only their own env program
   const int k = a.P.kind;
-  if (L == 16 && gw <= 4 && k == BX_ENV_ANT && feat == (F_G1 | F_JH)) {
+  // (their kernels fold each joint's damping into its actuator's slot: fold
+  // = every joint j has torque actuator j)
+  if (fold && L == 16 && gw <= 4 && k == BX_ENV_ANT && feat == (F_G1 | F_JH)) {
     launch_one<EnvArgs>(env_step_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
     return hipGetLastError();
   }
-  if (L == 16 && gw <= 4 && (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP) &&
+  if (fold && L == 16 && gw <= 4 && (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP) &&
       feat == (F_SPH | F_G1)) {
     launch_one<EnvArgs>(env_step_kernel<16, 1, F_SPH | F_G1, 4, EK_HUM>, grid, tpb, lds, s, a);
     return hipGetLastError();

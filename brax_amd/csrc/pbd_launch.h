@@ -63,7 +63,7 @@ struct ResetArgs {
 hipError_t launch_system_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
                                      hipStream_t s, const StepArgs& a);
 hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
-                                  hipStream_t s, const EnvArgs& a);
+                                  hipStream_t s, const EnvArgs& a, int fold);
 // MULTI-mode step kernel (large pbd scenes, 256 threads per env; mr = rows per lane)
 hipError_t launch_system_step_multi(int feat, int mr, int64_t n_envs, size_t lds, hipStream_t s,
                                     const StepArgs& a);
