@@ -337,11 +337,11 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
     v3 a1p = rotate(J.axp[0], p.rot), a2p = rotate(J.axp[1], p.rot);
     v3 a1c = rotate(J.axc[0], c.rot), a2c = rotate(J.axc[1], c.rot), a3c = rotate(J.axc[2], c.rot);
     v3 lon = cross(a3c, a1p);
-    lon = lon / (1e-6f + safe_norm(lon));
+    lon = lon / (1e-6f + dir_norm(lon));
     v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
-    xz = xz / (1e-6f + safe_norm(xz));
+    xz = xz / (1e-6f + dir_norm(xz));
     v3 a2n = cross(xz, a1p);
-    a2n = a2n / (1e-6f + safe_norm(a2n));
+    a2n = a2n / (1e-6f + dir_norm(a2n));
     float sg = signf(dot(a1p, a3c));
     v3 nv[3] = {a1p, -a2n * sg, a3c};
     v3 n1v[3] = {a2p, a1p, lon};

@@ -54,6 +54,10 @@ __device__ __forceinline__ float cancel_norm(v3 a) {
 #endif
 }
 
+// the same bare sqrt for a direction normalised and used as a turn axis or
+// lever direction, never fed to acos: its length is off by <= 1 ulp
+__device__ __forceinline__ float dir_norm(v3 a) { return cancel_norm(a); }
+
 __device__ __forceinline__ q4 operator+(q4 a, q4 b) {
   return {a.w + b.w, a.x + b.x, a.y + b.y, a.z + b.z};
 }
