@@ -572,6 +572,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         put(lane, base + LJ_AXC + k, s[J_AXC + k]);
       }
       for (int k = 0; k < 6; k++) put(lane, base + LJ_LIM + k, s[J_LIM + k]);
+      put(lane, base + LJ_DOF, s[J_DOF]);
       put(lane, base + LJ_MP, p[BODY_MASS]);
       put(lane, base + LJ_MC, c[BODY_MASS]);
     };

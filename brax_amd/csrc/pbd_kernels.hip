@@ -159,7 +159,7 @@ __device__ __forceinline__ void ld_rb(const float* s, v3& p, v3& v, v3& a) {
 // joints (brax/physics/joints.py)
 // ---------------------------------------------------------------------------
 struct JointC {
-  int type, bp, bc, free, angle_off, n_angles;
+  int type, bp, bc, free, angle_off, n_angles, dof;
   float damping, sp, sa;
   v3 off_p, off_c;
   v3 axp[3], axc[3];
@@ -190,6 +190,7 @@ __device__ __forceinline__ JointC load_joint(const Cst& c, const BlobHdr& H, int
   r.free = c.i(o + J_FREE);
   r.angle_off = c.i(o + J_ANGLE_OFF);
   r.n_angles = c.i(o + J_NANGLES);
+  r.dof = c.i(o + J_DOF);
   r.damping = c.f(o + J_DAMP);
   r.sp = c.f(o + J_SP);
   r.sa = c.f(o + J_SA);
@@ -2129,6 +2130,7 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   J.free = n(OJ + LJ_FREE);
   J.angle_off = n(OJ + LJ_AOFF);
   J.n_angles = n(OJ + LJ_NANG);
+  J.dof = n(OJ + LJ_DOF);
   J.damping = f(OJ + LJ_DAMP);
   J.sp = f(OJ + LJ_SP);
   J.sa = f(OJ + LJ_SA);
@@ -3435,7 +3437,8 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
 template <int L, int EK = EK_ANY>
 __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int lane, int kind,
                             int flags, int obs_size, const float* act, int aw, float* obs_out,
-                            const float* coef, const JointC* hj = nullptr) {
+                            const float* coef, const JointC* hj = nullptr,
+                            const BodyC* hbody = nullptr, const ActC* hact = nullptr) {
   joint_angles<L>(c, H, E, lane, hj);
   if ((KIND_IS(BX_ENV_HUMANOID) || KIND_IS(BX_ENV_HUMANOID_STANDUP)) && lane == 0) {
     v3 com;
@@ -3496,9 +3499,12 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
     const v3 com = ld3(E.red + 32);
     const float msum = E.red[35];
     for (int b = lane; b < M; b += L) {
+      // SINGLE mode: body b is the lane's, its constants hoisted (hbody)
       const int ob = H.o_body + b * BODY_STRIDE;
-      const float mb = c.f(ob + BODY_MASS);
-      const float Ia[3] = {c.f(ob + BODY_I), c.f(ob + BODY_I + 1), c.f(ob + BODY_I + 2)};
+      const float mb = hbody ? hbody->mass : c.f(ob + BODY_MASS);
+      const float Ia[3] = {hbody ? hbody->I.x : c.f(ob + BODY_I),
+                           hbody ? hbody->I.y : c.f(ob + BODY_I + 1),
+                           hbody ? hbody->I.z : c.f(ob + BODY_I + 2)};
       const v3 d = ld3(E.qp + b * QP_STRIDE) - com;
       const v3 vb = ld3(E.qp + b * QP_STRIDE + 7);
       const float nn = norm(d);
@@ -3527,7 +3533,11 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
     const bool ha = lane < H.K;
     ActC A{};
     int dof = 0;
-    if (ha) {
+    if (ha && hact && hj) {
+      // the lane's hoisted actuator and joint (act_same: actuator a drives joint a)
+      A = *hact;
+      dof = hj->dof;
+    } else if (ha) {
       A = load_act(c, H, lane);
       dof = c.i(H.o_joint + A.joint * JOINT_STRIDE + J_DOF);
     }
@@ -3834,8 +3844,12 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
       pbd_step<L, F>(c, H, E, lane, valid, sact, saw);
     }
     BX_KSTAMP(11);
+    // the Humanoid kernel's actuators drive the joints of their own index
+    // (its launch requires fold), so its observation takes the lane's
+    // hoisted body, joint and actuator
     env_observe<L, EK>(c, H, E, lane, kind, P.obs_flags, P.obs_size, act, aw,
-                   valid ? A.out.obs + e * P.obs_size : nullptr, P.coef, S ? &X.J : nullptr);
+                   valid ? A.out.obs + e * P.obs_size : nullptr, P.coef, S ? &X.J : nullptr,
+                   S ? &X.B : nullptr, (S && EK == EK_HUM) ? &X.A : nullptr);
     BX_KSTAMP(12);
     // reward / done / metrics (lane 0 of the env)
     if (lane == 0 && valid) {

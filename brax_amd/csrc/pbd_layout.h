@@ -135,7 +135,7 @@ enum { LL_PLO = 0, LL_PHI = 1, LL_CLO = 2, LL_SLO = 3, LL_CHI = 4, LL_SHI = 5 };
 enum {
   LJ_TYPE = 0, LJ_BP = 1, LJ_BC = 2, LJ_FREE = 3, LJ_AOFF = 4, LJ_NANG = 5, LJ_DAMP = 6,
   LJ_SP = 7, LJ_SA = 8, LJ_OFFP = 9, LJ_OFFC = 12, LJ_AXP = 15, LJ_AXC = 24, LJ_LIM = 33,
-  LJ_MP = 39, LJ_MC = 40, LJ_IP = 41, LJ_IC = 44  // 47 words
+  LJ_MP = 39, LJ_MC = 40, LJ_IP = 41, LJ_IC = 44, LJ_DOF = 47  // 48 words
 };
 enum { LA_TYPE = 0, LA_JOINT = 1, LA_IDX = 2, LA_STR = 5 };
 enum {
