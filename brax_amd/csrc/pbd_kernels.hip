@@ -296,9 +296,20 @@ template <int F>
 __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, q4& dpr,
                             v3& dcp, q4& dcr, const JLim* JL = nullptr,
                             const uint4* LI = nullptr) {
+  // each body rotates three or four of the joint's vectors: one matrix each
+  // in the SINGLE-mode TU (the item-loop / MULTI kernels keep rotate():
+  // their culled Mountain scene sits closer to its gate)
+#if defined(BX_TU_FAST)
+  const RotM Mp = rot_matrix(p.rot), Mc = rot_matrix(c.rot);
+  auto rp_ = [&](v3 v) { return mrot(Mp, v); };
+  auto rc_ = [&](v3 v) { return mrot(Mc, v); };
+#else
+  auto rp_ = [&](v3 v) { return rotate(v, p.rot); };
+  auto rc_ = [&](v3 v) { return rotate(v, c.rot); };
+#endif
   // positional constraint: apply_position_update (joints.py:154-195)
-  v3 pw = p.pos + rotate(J.off_p, p.rot);
-  v3 cw = c.pos + rotate(J.off_c, c.rot);
+  v3 pw = p.pos + rp_(J.off_p);
+  v3 cw = c.pos + rc_(J.off_c);
   v3 dx = pw - cw;
   v3 rp = pw - p.pos, rc = cw - c.pos;
   float cc = cancel_norm(dx);
@@ -316,10 +327,10 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
   // body (below)
   v3 pimp = mk(0.f, 0.f, 0.f);
   if (is_rev<F>(J.type)) {
-    v3 axis = rotate(J.axp[0], p.rot);
-    v3 ref_p = rotate(J.axp[2], p.rot);
-    v3 ref_c = rotate(J.axc[2], c.rot);
-    v3 axis_c = rotate(J.axc[0], c.rot);
+    v3 axis = rp_(J.axp[0]);
+    v3 ref_p = rp_(J.axp[2]);
+    v3 ref_c = rc_(J.axc[2]);
+    v3 axis_c = rc_(J.axc[0]);
     v3 dq1 = cross(axis, axis_c);
     v3 n1;
     if (JL) {
@@ -335,8 +346,8 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
     v3 dq2 = cross(n1, ref_c);
     pimp = angle_impulse(J, dq1) + angle_impulse(J, dq2);
   } else {
-    v3 a1p = rotate(J.axp[0], p.rot), a2p = rotate(J.axp[1], p.rot);
-    v3 a1c = rotate(J.axc[0], c.rot), a2c = rotate(J.axc[1], c.rot), a3c = rotate(J.axc[2], c.rot);
+    v3 a1p = rp_(J.axp[0]), a2p = rp_(J.axp[1]);
+    v3 a1c = rc_(J.axc[0]), a2c = rc_(J.axc[1]), a3c = rc_(J.axc[2]);
     v3 lon = cross(a3c, a1p);
     lon = lon / (1e-6f + dir_norm(lon));
     v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
@@ -1181,8 +1192,8 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
       // Spherical.axis_angle (joints.py:388-415): psi, theta = +-acos(cb)
       // (the pseudo-angle of (cb, +-sqrt(1 - cb^2))), phi
       const v3 a1p = rotate(Jc.axp[0], p.rot), a2p = rotate(Jc.axp[1], p.rot);
-      const v3 a1c = rotate(Jc.axc[0], cq.rot), a2c = rotate(Jc.axc[1], cq.rot);
-      const v3 a3c = rotate(Jc.axc[2], cq.rot);
+      const RotM Mc = rot_matrix(cq.rot);
+      const v3 a1c = mrot(Mc, Jc.axc[0]), a2c = mrot(Mc, Jc.axc[1]), a3c = mrot(Mc, Jc.axc[2]);
       // pseudo-angles are scale-free in (x, y): lon and xz enter unnormalised,
       // (cb, sqrt(1 - cb^2)) as (x, sqrt(|xz|^2 - x^2)) with x = xz . a1p
       const v3 lon = cross(a3c, a1p);

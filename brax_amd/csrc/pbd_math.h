@@ -71,6 +71,22 @@ __device__ __forceinline__ v3 rotate(v3 v, q4 q) {
   v3 r = 2.f * (dot(u, v) * u) + (s * s - dot(u, u)) * v;
   return r + 2.f * s * cross(u, v);
 }
+// rotate() of several vectors by one quaternion: the same formula
+// ((s^2 - |u|^2) v + 2 (u.v) u + 2 s u x v) as a matrix, built once (rows)
+struct RotM {
+  v3 r0, r1, r2;
+};
+__device__ __forceinline__ RotM rot_matrix(q4 q) {
+  const float k = q.w * q.w - (q.x * q.x + q.y * q.y + q.z * q.z);
+  const float tx = 2.f * q.x, ty = 2.f * q.y, tz = 2.f * q.z, ts = 2.f * q.w;
+  const float xy = tx * q.y, xz = tx * q.z, yz = ty * q.z;
+  const float sx = ts * q.x, sy = ts * q.y, sz = ts * q.z;
+  return {{k + tx * q.x, xy - sz, xz + sy}, {xy + sz, k + ty * q.y, yz - sx},
+          {xz - sy, yz + sx, k + tz * q.z}};
+}
+__device__ __forceinline__ v3 mrot(const RotM& m, v3 v) {
+  return {dot(m.r0, v), dot(m.r1, v), dot(m.r2, v)};
+}
 // math.py:130-145
 __device__ __forceinline__ q4 quat_mul(q4 u, q4 v) {
   return {u.w * v.w - u.x * v.x - u.y * v.y - u.z * v.z,
