@@ -1289,8 +1289,10 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   const float sg = S.sg;
   const v3 I = S.I;
   const float m = S.m;
+  // this side's three vectors through one rotation matrix
+  const RotM Mo = rot_matrix(o.rot);
   // positional constraint
-  v3 wo = o.pos + rotate(S.off, o.rot);
+  v3 wo = o.pos + mrot(Mo, S.off);
   v3 ro = wo - o.pos;
   v3 wt = xh3(wo);
   v3 dx = child ? wt - wo : wo - wt;
@@ -1304,8 +1306,8 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   v3 pv = dl * n;
   dpo = J.sp * ((sg * pv) / m);
   // the two angular constraints (axis alignment, limited hinge angle)
-  v3 u0 = rotate(S.ax0, o.rot);
-  v3 u2 = rotate(S.ax2, o.rot);
+  v3 u0 = mrot(Mo, S.ax0);
+  v3 u2 = mrot(Mo, S.ax2);
   v3 t0 = xh3(u0), t2 = xh3(u2);
   v3 axis = sel3(child, t0, u0), axis_c = sel3(child, u0, t0);
   v3 ref_p = sel3(child, t2, u2), ref_c = sel3(child, u2, t2);
