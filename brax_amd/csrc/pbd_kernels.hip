@@ -2269,8 +2269,9 @@ __device__ __forceinline__ void gsum_contact(const GList<M>& g, const float* csl
 }
 
 // Euler.velocity_projection (integrators.py:122-146) on one body
-__device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, float h) {
-  q4 nr = qnormalize(q.rot);
+__device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, float h,
+                                      bool bare = false) {
+  q4 nr = bare ? qnormalize_bare(q.rot) : qnormalize(q.rot);
   q.vel = mul((q.pos - ppos) / h, B.pm);
   q4 dq = quat_mul(nr, quat_inv(prot));
   v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
@@ -2426,7 +2427,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         v3 am = mul(q.ang, X.B.rm);
         q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
         q4 r = q.rot + quat_mul(hq, q.rot);
-        q.rot = qnormalize(r);
+        q.rot = (FOLD && JH) ? qnormalize_bare(r) : qnormalize(r);  // Ant env kernel: bare sqrt
         stqp(myqp, q);
         dpa_last = dpa;
       }
@@ -2467,7 +2468,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         q.pos = q.pos + mul(dp, X.B.pm);
         q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                    q.rot.z + dr.z * X.B.qm.z};
-        if (sub == 0) vproj(q, ppos, prot, X.B, h);
+        if (sub == 0) vproj(q, ppos, prot, X.B, h, FOLD && JH);
         stqp(myqp, q);
       }
       sync();
@@ -2507,7 +2508,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                  q.rot.z + dr.z * X.B.qm.z};
       st_rb(E.rb + lane * RB_STRIDE, q.pos, q.vel, q.ang);
-      vproj(q, ppos, prot, X.B, h);
+      vproj(q, ppos, prot, X.B, h, FOLD && JH);
       stqp(myqp, q);
     }
     sync();

@@ -152,6 +152,11 @@ __device__ __forceinline__ float clampf(float x, float lo, float hi) {
 }
 __device__ __forceinline__ float signf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
 
+// q / |q| with the bare v_sqrt_f32 (the Ant env kernel's integrator only)
+__device__ __forceinline__ q4 qnormalize_bare(q4 r) {
+  float rn = __builtin_amdgcn_sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
+  return {r.w / rn, r.x / rn, r.y / rn, r.z / rn};
+}
 // q / |q| (integrators.py:67, 133)
 __device__ __forceinline__ q4 qnormalize(q4 r) {
   float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
