@@ -1295,27 +1295,27 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   v3 wo = o.pos + mrot(Mo, S.off);
   v3 ro = wo - o.pos;
   v3 wt = xh3(wo);
-  v3 dx = child ? wt - wo : wo - wt;
+  // the parent's anchor minus the child's on both halves, bit for bit (IEEE
+  // a - b is exactly -(b - a)); the effective masses add commutatively
+  v3 dx = sg * (wo - wt);
   float cc = cancel_norm(dx);
   v3 n = dx / (cc + 1e-6f);
   v3 cr = cross(ro, n);
   float wm = 1.f / m + dot(cr, mul(I, cr));
   float wp = xh(wm);
-  float w1 = child ? wp : wm, w2 = child ? wm : wp;
-  float dl = -cc / (w1 + w2 + 1e-6f);
+  float dl = -cc / (wm + wp + 1e-6f);
   v3 pv = dl * n;
   dpo = J.sp * ((sg * pv) / m);
   // the two angular constraints (axis alignment, limited hinge angle)
   v3 u0 = mrot(Mo, S.ax0);
   v3 u2 = mrot(Mo, S.ax2);
   v3 t0 = xh3(u0), t2 = xh3(u2);
-  v3 axis = sel3(child, t0, u0), axis_c = sel3(child, u0, t0);
-  v3 ref_p = sel3(child, t2, u2), ref_c = sel3(child, u2, t2);
-  v3 dq1 = cross(axis, axis_c);
-  v3 n1 = hinge_turn(axis, ref_p, ref_c, JL);
-  v3 dq2 = cross(n1, ref_c);
-  // both halves hold the same dq1 and dq2: the parent lane computes dq1's
-  // impulse, the child lane dq2's, and they trade them
+  // the parent lane computes dq1's impulse, the child lane dq2's, and they
+  // trade them: each lane forms only its own correction, from its own
+  // vectors in the parent / child order that lane sees them (parent: u =
+  // the parent's, t = the child's; child: the reverse)
+  v3 dq1 = cross(u0, t0);                               // valid on the parent lane
+  v3 dq2 = cross(hinge_turn(t0, t2, u2, JL), u2);       // valid on the child lane
   const v3 pm = angle_impulse(J, sel3(child, dq2, dq1));
   const v3 po = xh3(pm);
   // the side's rotation update is linear in the angular impulse: the
