@@ -240,9 +240,14 @@ template <int F> __device__ __forceinline__ bool is_oneway(int ow) {
 __device__ __forceinline__ v3 angle_impulse(const JointC& J, v3 dq) {
   float th = cancel_norm(dq);
   v3 n = dq / (th + 1e-6f);
+#if defined(BX_TU_FAST)
+  // w1 + w2 as one quadratic form in Ip + Ic (loop-invariant; SINGLE-mode TU)
+  float dl = -th / (dot(n, mul(J.Ip + J.Ic, n)) + 1e-6f);
+#else
   float w1 = dot(n, mul(J.Ip, n));
   float w2 = dot(n, mul(J.Ic, n));
   float dl = -th / (w1 + w2 + 1e-6f);
+#endif
   return -dl * n;
 }
 
