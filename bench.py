@@ -7,6 +7,13 @@ one per step, notebooks/environments.ipynb:386-423) + one `Env.step` of
 i.e. ONE fused kernel launch doing 10 PBD substeps + observation + reward +
 Episode/AutoReset. Inputs are resident in HBM.
 
+The timed loop runs twice: first as a plain Python loop (reported as
+`eager_loop`), then as replays of a hipGraph holding K = gcd(steps, 50) of
+those steps (`brax_amd.envs.graph.StepGraph`: the same draw + step kernels per
+step, the draw's offset advanced by a device epoch counter so every replay
+draws fresh slabs). `value` is the graph loop: on a slow host the Python loop's
+~20 us per step otherwise leaves the GPU idle between 29 us kernels.
+
     python bench.py [--gpus N --steps K --warmup W --batch B]
     torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU)
 
@@ -19,6 +26,7 @@ every step, and the sums are all-gathered over RCCL once per episode length
 """
 import argparse
 import json
+import math
 import os
 import platform
 import sys
@@ -41,6 +49,8 @@ ANT_KERNEL = 'bx::env_step_kernel<16, 1, 160, 4, 1>'
 ANT_FLOPS_PER_ENV_STEP = 87382
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8 TB/s HBM3E
 FP32_VALU_PEAK_TFLOPS = 157.3
+# steps per captured graph of the timed loop (K = gcd(--steps, this))
+GRAPH_STEPS = 50
 
 
 def _dist():
@@ -154,7 +164,8 @@ def _time(fn, steps, warmup):
 
 def secondary_configs(dev, steps=50):
   """BASELINE.json's other single-GPU configs, one short leg each:
-  Humanoid Env.step at 4096 envs (configs[2]) and Ant Mountain(4)
+  Humanoid Env.step at 4096 envs (configs[2]), Ant Env.step at configs[3]'s
+  32,768-env global batch on one GPU, and Ant Mountain(4)
   System.step at 2048 envs, all pairs and NearNeighbors cutoff 36 (configs[4];
   the reference's V100 plot, multiagent.ipynb:222-267, is at 1024 envs)."""
   from brax_amd import envs
@@ -171,6 +182,26 @@ def secondary_configs(dev, steps=50):
   wall, gpu = _time(hstep, steps, 5)
   out['humanoid_4096'] = {'value': B * steps / wall, 'unit': 'env-steps/s',
                           'ms_per_step': wall * 1e3 / steps, 'gpu_ms_per_step': gpu * 1e3 / steps}
+  # the same Humanoid steps replayed from a captured graph (StepGraph)
+  from brax_amd.envs.graph import StepGraph
+  g = StepGraph(env, st[0], 10, seed=3)
+  wall, gpu = _time(g.replay, steps // 10, 2)
+  out['humanoid_4096_graph'] = {'value': B * (steps // 10) * 10 / wall, 'unit': 'env-steps/s',
+                                'ms_per_step': wall * 1e3 / (steps // 10 * 10)}
+  del env, st, g
+  # configs[3]'s global batch (32,768 Ant envs) on ONE GPU: what one rank of
+  # the 8-GPU run would hold if the whole batch sat on a single card.
+  Bg = 32768
+  env = envs.create('ant', batch_size=Bg, episode_length=1000, auto_reset=True, device=dev)
+  st = [env.reset(np.array([0, 7], np.uint32))]
+  act = torch.rand((Bg, env.action_size), device=dev) * 2 - 1
+
+  def gstep():
+    st[0] = env.step(st[0], act)
+  wall, gpu = _time(gstep, steps, 5)
+  out['ant_32768_one_gpu'] = {'value': Bg * steps / wall, 'unit': 'env-steps/s',
+                              'ms_per_step': wall * 1e3 / steps, 'gpu_ms_per_step': gpu * 1e3 / steps}
+  del env, st
   for cutoff in (0, 36):
     cfg = ant_mountain_config(4)
     cfg.collider_cutoff = cutoff
@@ -332,10 +363,38 @@ def main():
     dist.barrier()
   torch.cuda.synchronize()
   elapsed = time.perf_counter() - t0
+  eager_elapsed = elapsed
+  # the same loop replayed from a hipGraph: K steps (draw + Env.step + the
+  # episodic sum) per graph launch, the actions continuing the eager loop's
+  # (step, global env id) stream; see brax_amd/envs/graph.py
+  from brax_amd.envs.graph import StepGraph
+  K = math.gcd(args.steps, GRAPH_STEPS)
+  k0 = args.warmup + args.steps
+  g = StepGraph(env, state, K, seed=1, offset=bd.action_offset(rank, B, A, k0, world),
+                step_stride=world * B * A,
+                hook=None if exchange is None else exchange.accumulate)
+  for _ in range(max(args.warmup // K, 1)):
+    state = g.replay()
+    if exchange is not None:
+      exchange.advance(K)
+  torch.cuda.synchronize()
   if dist is not None:
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(args.steps // K):
+    state = g.replay()
+    if exchange is not None:
+      exchange.advance(K)  # the RCCL gather once per 1000 steps, on the host
+  torch.cuda.synchronize()
+  if dist is not None:
+    dist.barrier()
+  torch.cuda.synchronize()
+  elapsed = time.perf_counter() - t0
+  if dist is not None:
+    t = torch.tensor([elapsed, eager_elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed, eager_elapsed = (float(x) for x in t.tolist())
 
   total = B * world * args.steps
   value = total / elapsed
@@ -371,6 +430,8 @@ def main():
               'config with device-RNG joint noise keyed by global env id',
       'config': {'workload': 'Ant-v1 Env.step (10 PBD substeps + obs/reward + '
                              'Episode/AutoReset), envs.create(ant)',
+                 'launch': f'hipGraph replays of {K} captured steps (each: on-device action '
+                           'draw + fused Env.step kernel + episodic sum when N>1)',
                  'envs_per_gpu': B, 'episode_length': 1000, 'substeps': 10,
                  'parallelism': f'env-shard x{world}'},
       # the fused env step is VALU/latency-bound (AI ~61 flop/B):
@@ -391,6 +452,10 @@ def main():
                    'hbm': {'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                            'frac': achieved_gbs / HBM_PEAK_GBS, 'traffic': traffic}},
   }
+  # the same steps from the plain Python loop (one Env.step call per step):
+  # host-bound on a slow host, hence the graph above
+  out['eager_loop'] = {'value': total / eager_elapsed, 'unit': 'env-steps/s',
+                       'ms_per_step': eager_elapsed * 1e3 / args.steps}
   out['secondary_configs'] = None if args.no_secondary else secondary_configs(dev)
   out['phase_roofline'] = (None if args.no_phases else
                            phase_bench(env.unwrapped.sys, dev, args.phase_envs))

@@ -65,6 +65,8 @@ _SIGS = {
     'bx_debug_stamps': ([C.POINTER(C.c_ulonglong), C.c_int], C.c_int),
     'bx_uniform': ([C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_float, C.c_float,
                     C.c_void_p], C.c_int),
+    'bx_uniform_epoch': ([C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_void_p,
+                          C.c_uint64, C.c_float, C.c_float, C.c_void_p], C.c_int),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -1202,4 +1202,13 @@ int bx_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset, float lo, 
   return 0;
 }
 
+int bx_uniform_epoch(float* out, int64_t n, uint64_t seed, uint64_t offset, const int64_t* epoch,
+                     uint64_t epoch_stride, float lo, float hi, void* stream) {
+  if (n <= 0) return n == 0 ? 0 : fail("negative n");
+  if (!out || !epoch) return fail("null output or epoch counter");
+  HIP_OK(launch_uniform_epoch(out, n, seed, offset, epoch, epoch_stride, lo, hi,
+                              as_stream(stream)));
+  return 0;
+}
+
 }  // extern "C"

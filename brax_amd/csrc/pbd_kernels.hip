@@ -4266,6 +4266,18 @@ __global__ void uniform_kernel(float* out, int64_t n, uint64_t seed, uint64_t of
   out[i] = uniform_at(seed, (uint64_t)i + offset, lo, hi);
 }
 
+// the same fill with the offset advanced by a device-resident epoch counter
+// (offset + epoch * stride): a graph-captured rollout replays one launch and
+// still draws a fresh slab per replay (the counter is bumped inside the graph)
+__global__ void uniform_epoch_kernel(float* out, int64_t n, uint64_t seed, uint64_t offset,
+                                     const int64_t* __restrict__ epoch, uint64_t stride,
+                                     float lo, float hi) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t off = offset + (uint64_t)epoch[0] * stride;
+  out[i] = uniform_at(seed, (uint64_t)i + off, lo, hi);
+}
+
 #endif
 
 }  // namespace bx
@@ -4447,6 +4459,14 @@ hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
                           hipStream_t s) {
   dim3 grid((unsigned)((n + 255) / 256));
   hipLaunchKernelGGL(uniform_kernel, grid, dim3(256), 0, s, out, n, seed, offset, lo, hi);
+  return hipGetLastError();
+}
+hipError_t launch_uniform_epoch(float* out, int64_t n, uint64_t seed, uint64_t offset,
+                                const int64_t* epoch, uint64_t stride, float lo, float hi,
+                                hipStream_t s) {
+  dim3 grid((unsigned)((n + 255) / 256));
+  hipLaunchKernelGGL(uniform_epoch_kernel, grid, dim3(256), 0, s, out, n, seed, offset, epoch,
+                     stride, lo, hi);
   return hipGetLastError();
 }
 

@@ -57,6 +57,15 @@ class EpisodeExchange:
     self._nccl = dist.get_backend(group) == 'nccl'
 
   def __call__(self, reward, done):
+    self.accumulate(reward, done)
+    self.k += 1
+    return self.flush() if self.k % self.every == 0 else None
+
+  def accumulate(self, reward, done):
+    """The device half of a call: adds the step's (reward, done) to the
+    sums. Stream-ordered device work only, so a graph-captured rollout
+    (`brax_amd.envs.graph.StepGraph`) records it as its per-step hook and
+    calls `advance` on the host after each replay."""
     B = self.B
     if (reward.dtype == done.dtype == torch.float32 and reward.is_contiguous() and
         reward.device == self.acc.device and done.data_ptr() == reward.data_ptr() + 4 * B):
@@ -64,8 +73,16 @@ class EpisodeExchange:
     else:
       self.acc[0].add_(reward.float())
       self.acc[1].add_(done.float())
-    self.k += 1
-    return self.flush() if self.k % self.every == 0 else None
+
+  def advance(self, n):
+    """Counts `n` steps accumulated by a replayed graph; flushes (and
+    returns the gathered sums) when they complete an exchange period."""
+    out = None
+    for _ in range(int(n)):
+      self.k += 1
+      if self.k % self.every == 0:
+        out = self.flush()
+    return out
 
   def flush(self):
     """All-gathers the sums since the last exchange and resets them."""

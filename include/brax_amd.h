@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 7
+#define BX_ABI_VERSION 8
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
 enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
@@ -405,6 +405,15 @@ int bx_system_joint_angles(bx_system* sys, int64_t n_envs, const bx_qp* qp, floa
  * is parity unpinned). */
 int bx_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
                float lo, float hi, void* stream);
+
+/* bx_uniform with the offset read on the device: out[i] = U(seed, offset +
+ * (*epoch) * epoch_stride + i), `epoch` a device int64 the caller advances
+ * in stream order. A hipGraph-captured rollout (brax_amd.envs.graph) replays
+ * the same launch and still draws a fresh slab per replay, exactly the slab
+ * bx_uniform would draw at offset + epoch * epoch_stride (ABI 8). */
+int bx_uniform_epoch(float* out, int64_t n, uint64_t seed, uint64_t offset,
+                     const int64_t* epoch, uint64_t epoch_stride,
+                     float lo, float hi, void* stream);
 
 /*
  * Standalone HBM-streaming phase kernels over a structure-of-arrays batch
