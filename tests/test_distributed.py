@@ -31,8 +31,16 @@ def _worker(rank, world, port, q):
   scal = torch.stack([reward, done, torch.zeros(B), torch.zeros(B)])
   assert ex(*scal.unbind(0)[:2]) is None and ex(reward, done) is None
   out = ex(*scal.unbind(0)[:2])  # the third step: the episodic gather
-  q.put((rank, out.numpy().copy(), bd.action_offset(rank, B, 8, step=3, world=world),
-         float(ex.acc.abs().sum())))
+  out = out.numpy().copy()
+  left = float(ex.acc.abs().sum())
+  # a graph-replayed rollout's split: device sums per step, host count after
+  for _ in range(3):
+    ex.accumulate(*scal.unbind(0)[:2])
+  assert ex.advance(2) is None  # k = 5: mid-period
+  ex.accumulate(reward, done)  # a step past the period stays in the sums
+  out2 = ex.advance(1)  # k = 6: the second episodic gather
+  np.testing.assert_array_equal(out2.numpy()[:, 0], 4 * out[:, 0] / 3)
+  q.put((rank, out, bd.action_offset(rank, B, 8, step=3, world=world), left))
   dist.barrier()
   dist.destroy_process_group()
 
