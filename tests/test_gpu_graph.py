@@ -44,8 +44,10 @@ def _same(a, b):
     assert torch.equal(a.metrics[k], b.metrics[k]), k
 
 
-@pytest.mark.parametrize('name,B,K', [('ant', 512, 5), ('humanoid', 256, 3), ('fetch', 128, 4)])
-def test_graph_replays_match_eager_loop(dev, name, B, K):
+@pytest.mark.parametrize('name,B,K,overlap', [('ant', 512, 5, True), ('ant', 512, 5, False),
+                                              ('humanoid', 256, 3, True), ('fetch', 128, 4, True),
+                                              ('ant', 64, 1, True)])
+def test_graph_replays_match_eager_loop(dev, name, B, K, overlap):
   from brax_amd import envs
   from brax_amd import distributed as bd
   from brax_amd.envs.graph import StepGraph
@@ -55,7 +57,8 @@ def test_graph_replays_match_eager_loop(dev, name, B, K):
   # 2 replays of K steps: covers an auto-reset (episode length 7) and the
   # epoch counter's second slab set
   ref = _eager(env, st0, 2 * K, 5, dev, B, A, k0=3)
-  g = StepGraph(env, st0, K, seed=5, offset=bd.action_offset(0, B, A, 3, 1), step_stride=B * A)
+  g = StepGraph(env, st0, K, seed=5, offset=bd.action_offset(0, B, A, 3, 1), step_stride=B * A,
+                overlap_draw=overlap)
   out = g.replay()
   mid = _eager(env, st0, K, 5, dev, B, A, k0=3)
   _same(out, mid)

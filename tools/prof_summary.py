@@ -34,7 +34,29 @@ def short(name):
   return n
 
 
-def counters(d):
+def bench_grids(d):
+  """Per kernel, the grid size of its most frequent launch in the trace
+  pass: the bench configuration. Other grids of the same instantiation (the
+  32,768-env leg runs the Ant kernel on 8x the grid) are summarised apart
+  so they do not mix into the bench kernel's averages."""
+  n = defaultdict(lambda: defaultdict(list))
+  p = os.path.join(d, 'trace', 'run_kernel_trace.csv')
+  with open(p) as f:
+    for r in csv.DictReader(f):
+      k = short(r['Kernel_Name'])
+      n[k][int(r['Grid_Size_X'])].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+  grids, stats = {}, {}
+  for k, by in n.items():
+    g = max(by, key=lambda x: len(by[x]))
+    grids[k] = g
+    stats[k] = {'calls': len(by[g]), 'avg_ns': sum(by[g]) / len(by[g]), 'grid': g}
+    other = {str(x): {'calls': len(v), 'avg_ns': sum(v) / len(v)} for x, v in by.items() if x != g}
+    if other:
+      stats[k]['other_grids'] = other
+  return grids, stats
+
+
+def counters(d, grids):
   out = defaultdict(lambda: defaultdict(list))
   meta = {}
   for sub in ('fetch', 'write', 'sq'):
@@ -45,6 +67,8 @@ def counters(d):
       for r in csv.DictReader(f):
         k = short(r['Kernel_Name'])
         if not k.startswith('bx::') and 'bx::' not in k:
+          continue
+        if k in grids and int(r['Grid_Size']) != grids[k]:
           continue
         out[k][r['Counter_Name']].append(float(r['Counter_Value']))
         meta[k] = {'grid': int(r['Grid_Size']), 'workgroup': int(r['Workgroup_Size']),
@@ -58,11 +82,10 @@ def main():
   prof = os.path.join(ROOT, 'profiles')
   shutil.copy(os.path.join(d, 'trace', 'run_kernel_stats.csv'),
               os.path.join(prof, f'{tag}_kernel_stats.csv'))
-  stats = {}
-  with open(os.path.join(d, 'trace', 'run_kernel_stats.csv')) as f:
-    for r in csv.DictReader(f):
-      stats[short(r['Name'])] = {'calls': int(r['Calls']), 'avg_ns': float(r['AverageNs'])}
-  cnt, meta = counters(d)
+  # per-kernel averages from the dispatch trace at the bench grid (the
+  # --stats CSV copied above averages every grid of an instantiation)
+  grids, stats = bench_grids(d)
+  cnt, meta = counters(d, grids)
   res = {}
   for k, cs in cnt.items():
     e = {'counters': {c: {'dispatches': len(v), 'mean': sum(v) / len(v)} for c, v in cs.items()}}
