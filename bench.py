@@ -372,7 +372,8 @@ def main():
   k0 = args.warmup + args.steps
   g = StepGraph(env, state, K, seed=1, offset=bd.action_offset(rank, B, A, k0, world),
                 step_stride=world * B * A,
-                hook=None if exchange is None else exchange.accumulate)
+                hook=None if exchange is None else (
+                    lambda st: exchange.accumulate(st.reward, st.done)))
   for _ in range(max(args.warmup // K, 1)):
     state = g.replay()
     if exchange is not None:
