@@ -370,28 +370,41 @@ def main():
   from brax_amd.envs.graph import StepGraph
   K = math.gcd(args.steps, GRAPH_STEPS)
   k0 = args.warmup + args.steps
-  g = StepGraph(env, state, K, seed=1, offset=bd.action_offset(rank, B, A, k0, world),
-                step_stride=world * B * A,
-                hook=None if exchange is None else (
-                    lambda st: exchange.accumulate(st.reward, st.done)))
-  for _ in range(max(args.warmup // K, 1)):
-    state = g.replay()
-    if exchange is not None:
-      exchange.advance(K)
-  torch.cuda.synchronize()
+  graph_err = None
+  try:
+    g = StepGraph(env, state, K, seed=1, offset=bd.action_offset(rank, B, A, k0, world),
+                  step_stride=world * B * A,
+                  hook=None if exchange is None else (
+                      lambda st: exchange.accumulate(st.reward, st.done)))
+  except Exception as e:  # pylint: disable=broad-except
+    # a failed capture must not sink the run: every rank falls back to the
+    # eager loop's measurement, and the line says so
+    g, graph_err = None, f'{type(e).__name__}: {e}'
+  use_graph = g is not None
   if dist is not None:
-    dist.barrier()
-  torch.cuda.synchronize()
-  t0 = time.perf_counter()
-  for _ in range(args.steps // K):
-    state = g.replay()
-    if exchange is not None:
-      exchange.advance(K)  # the RCCL gather once per 1000 steps, on the host
-  torch.cuda.synchronize()
-  if dist is not None:
-    dist.barrier()
-  torch.cuda.synchronize()
-  elapsed = time.perf_counter() - t0
+    f = torch.tensor([int(use_graph)], dtype=torch.int32, device=dev)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN)
+    use_graph = bool(f.item())
+  elapsed = eager_elapsed
+  if use_graph:
+    for _ in range(max(args.warmup // K, 1)):
+      state = g.replay()
+      if exchange is not None:
+        exchange.advance(K)
+    torch.cuda.synchronize()
+    if dist is not None:
+      dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps // K):
+      state = g.replay()
+      if exchange is not None:
+        exchange.advance(K)  # the RCCL gather once per 1000 steps, on the host
+    torch.cuda.synchronize()
+    if dist is not None:
+      dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
   if dist is not None:
     t = torch.tensor([elapsed, eager_elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -431,8 +444,9 @@ def main():
               'config with device-RNG joint noise keyed by global env id',
       'config': {'workload': 'Ant-v1 Env.step (10 PBD substeps + obs/reward + '
                              'Episode/AutoReset), envs.create(ant)',
-                 'launch': f'hipGraph replays of {K} captured steps (each: on-device action '
-                           'draw + fused Env.step kernel + episodic sum when N>1)',
+                 'launch': (f'hipGraph replays of {K} captured steps (each: on-device action '
+                            'draw + fused Env.step kernel + episodic sum when N>1)' if use_graph
+                            else f'eager Python loop (graph capture failed: {graph_err})'),
                  'envs_per_gpu': B, 'episode_length': 1000, 'substeps': 10,
                  'parallelism': f'env-shard x{world}'},
       # the fused env step is VALU/latency-bound (AI ~61 flop/B):

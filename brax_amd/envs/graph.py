@@ -152,7 +152,10 @@ class StepGraph:
       dst.copy_(src)
     self._epoch.zero_()
     self.graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(self.graph):
+    # thread_local: only this thread's calls are checked during capture, so
+    # a process group's watchdog thread polling its collectives' events (the
+    # bench's barrier just before) cannot invalidate the capture
+    with torch.cuda.graph(self.graph, capture_error_mode='thread_local'):
       self._out = body()
     torch.cuda.current_stream(dev).synchronize()
 
