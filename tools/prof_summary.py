@@ -141,7 +141,10 @@ def main():
                         'lds_insts_per_wave': c.get('SQ_INSTS_LDS', {}).get('mean', 0) / waves,
                         'cycles_per_wave': cyc, 'valu_issue_frac': 4 * valu / cyc}
   with open(os.path.join(prof, 'rocprof_latest.json'), 'w') as f:
+    sys.path.insert(0, ROOT)
+    from bench import src_sha1
     json.dump({'round': tag, 'source': f'profiles/{tag}_kernel_stats.csv', 'lib_sha1': sha,
+               'src_sha1': src_sha1(),
                'kernels': stats}, f, indent=1)
   print(json.dumps(traffic, indent=1))
 
