@@ -183,13 +183,16 @@ def secondary_configs(dev, steps=50):
     st[0] = env.step(st[0], act)
   wall, gpu = _time(hstep, steps, 5)
   out['humanoid_4096'] = {'value': B * steps / wall, 'unit': 'env-steps/s',
-                          'ms_per_step': wall * 1e3 / steps, 'gpu_ms_per_step': gpu * 1e3 / steps}
-  # the same Humanoid steps replayed from a captured graph (StepGraph)
+                          'ms_per_step': wall * 1e3 / steps, 'gpu_ms_per_step': gpu * 1e3 / steps,
+                          'actions': 'one fixed slab (no per-step draw)'}
+  # Humanoid replayed from a captured graph (StepGraph), with the headline's
+  # per-step on-device action draw (one more kernel per step than the leg above)
   from brax_amd.envs.graph import StepGraph
   g = StepGraph(env, st[0], 10, seed=3)
   wall, gpu = _time(g.replay, steps // 10, 2)
   out['humanoid_4096_graph'] = {'value': B * (steps // 10) * 10 / wall, 'unit': 'env-steps/s',
-                                'ms_per_step': wall * 1e3 / (steps // 10 * 10)}
+                                'ms_per_step': wall * 1e3 / (steps // 10 * 10),
+                                'actions': 'drawn on the device every step'}
   del env, st, g
   # configs[3]'s global batch (32,768 Ant envs) on ONE GPU: what one rank of
   # the 8-GPU run would hold if the whole batch sat on a single card.
