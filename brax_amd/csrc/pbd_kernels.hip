@@ -3569,8 +3569,10 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
     }
     off -= dof;
     float* oq = obs_out + base + 15 * M + off;
-    for (int i = 0; i < dof; i++)
-      oq[i] = (act ? act[take_idx(A.idx[i], aw)] : 0.f) * A.strength;
+    // constant indices into A.idx (a dynamic one would put A on the stack)
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+      if (i < dof) oq[i] = (act ? act[take_idx(A.idx[i], aw)] : 0.f) * A.strength;
     return;
   }
   for (int i = lane; i < obs_size; i += L)
