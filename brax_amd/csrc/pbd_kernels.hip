@@ -3444,7 +3444,9 @@ __device__ float obs_elem(const Cst& c, const BlobHdr& H, const Env& E, int kind
     ActC A = load_act(c, H, a);
     int dof = c.i(H.o_joint + A.joint * JOINT_STRIDE + J_DOF);
     if (i < dof) {
-      return (valid ? act[take_idx(A.idx[i], aw)] : 0.f) * A.strength;
+      // constant indices into A.idx (a dynamic one would put A on the stack)
+      const int ix = i == 0 ? A.idx[0] : (i == 1 ? A.idx[1] : A.idx[2]);
+      return (valid ? act[take_idx(ix, aw)] : 0.f) * A.strength;
     }
     i -= dof;
   }
