@@ -8,11 +8,14 @@ i.e. ONE fused kernel launch doing 10 PBD substeps + observation + reward +
 Episode/AutoReset. Inputs are resident in HBM.
 
 The timed loop runs twice: first as a plain Python loop (reported as
-`eager_loop`), then as replays of a hipGraph holding K = gcd(steps, 50) of
-those steps (`brax_amd.envs.graph.StepGraph`: the same draw + step kernels per
-step, the draw's offset advanced by a device epoch counter so every replay
-draws fresh slabs). `value` is the graph loop: on a slow host the Python loop's
-~20 us per step otherwise leaves the GPU idle between 29 us kernels.
+`eager_loop`), then as replays of a hipGraph holding K of those steps (K =
+steps up to 200, else gcd(steps, 50); `brax_amd.envs.graph.StepGraph`): per
+replay ONE launch draws the K action slabs (each bit-identical to the eager
+loop's draw of that step, offset advanced by a device epoch counter), then K
+fused Env.step kernels. `value` is the graph loop: on a slow host the Python
+loop's ~20 us per step otherwise leaves the GPU idle between 29 us kernels.
+Before the timed loops, a 200-launch train of the step kernel alone
+(`roofline.kernel_ms`) and warm graph replays bring the clocks up.
 
     python bench.py [--gpus N --steps K --warmup W --batch B]
     torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU)
@@ -22,7 +25,9 @@ noise and actions are keyed by global env id with one shared seed, so the
 ranks together step exactly the envs of one N*B batch; the only collective is
 the episodic exchange: each rank sums its envs' (reward, done) on the device
 every step, and the sums are all-gathered over RCCL once per episode length
-(1000 steps). Prints ONE JSON line on rank 0.
+(1000 steps), or once per timed run when that is shorter, so the timed region
+always holds at least one collective (`collectives_in_timed_region`). Prints
+ONE JSON line on rank 0.
 """
 import argparse
 import json
@@ -51,8 +56,14 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8 TB/s HBM3E
 FP32_VALU_PEAK_TFLOPS = 157.3
 # the reference's published Ant 4,096-env rollout rate
 REF_PUBLISHED = 895723.0
-# steps per captured graph of the timed loop (K = gcd(--steps, this))
+# steps per captured graph of the timed loop: the whole timed run up to
+# GRAPH_MAX steps (one replay, one action draw), else gcd(steps, GRAPH_STEPS)
 GRAPH_STEPS = 50
+GRAPH_MAX = 200
+
+
+def graph_steps(steps):
+  return steps if steps <= GRAPH_MAX else math.gcd(steps, GRAPH_STEPS)
 
 
 def _dist():
@@ -75,14 +86,36 @@ def _dist():
   return None, 0, 1, 0
 
 
+def host_cpu():
+  """This host's CPU: `nproc`, the CPUs this process may run on, and the
+  /proc/cpuinfo model name."""
+  model = platform.processor() or platform.machine()
+  try:
+    with open('/proc/cpuinfo') as f:
+      for line in f:
+        if line.startswith('model name'):
+          model = line.split(':', 1)[1].strip()
+          break
+  except OSError:
+    pass
+  try:
+    allowed = len(os.sched_getaffinity(0))
+  except AttributeError:
+    allowed = os.cpu_count()
+  return {'nproc': os.cpu_count(), 'allowed_cpus': allowed, 'model': model}
+
+
 def cpu_baseline(batch, min_seconds=10.0, max_steps=100000):
   """The oracle's float32 C restatement (OpenMP over envs) on this host's
-  cores, on a bounded sample of the same workload."""
+  cores, on a bounded sample of the same workload. The thread count is
+  OpenMP's default: every CPU this process may use, or OMP_NUM_THREADS
+  where the host sets it (the GPU box sets it to its CPU share per GPU)."""
   from oracle.oracle import Oracle
   from tests.helpers import compiled
   _, d, rd, _ = compiled('ant')
   o = Oracle(d, rd, np.float32)
   threads = o.max_threads()
+  cpu = host_cpu()
   rng = np.random.default_rng(0)
   B = batch
   T = np.load(os.path.join(ROOT, 'tests', 'golden', 'traj_ant.npz'))
@@ -96,9 +129,12 @@ def cpu_baseline(batch, min_seconds=10.0, max_steps=100000):
     steps += 1
   dt = time.perf_counter() - t0
   return {'value': B * steps / dt, 'unit': 'env-steps/s', 'cores': threads, 'kind': 'port',
+          'nproc': cpu['nproc'], 'allowed_cpus': cpu['allowed_cpus'], 'cpu_model': cpu['model'],
+          'omp_num_threads': os.environ.get('OMP_NUM_THREADS'),
           'sample': f'Ant, {B} envs x {steps} env-steps ({dt:.1f} s), float32 C '
-                    f'restatement (oracle/pbd_oracle.c), {threads} OpenMP threads, '
-                    f'{platform.processor() or platform.machine()}'}
+                    f'restatement (oracle/pbd_oracle.c), {threads} OpenMP threads '
+                    f'(nproc {cpu["nproc"]}, {cpu["allowed_cpus"]} CPUs allowed, '
+                    f'OMP_NUM_THREADS={os.environ.get("OMP_NUM_THREADS")}), {cpu["model"]}'}
 
 
 PHASE_KERNELS = {'kinetic': 'bx::kinetic_kernel', 'update_acc': 'bx::update_acc_kernel',
@@ -357,8 +393,11 @@ def main():
   stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
   act = torch.empty((B, A), dtype=torch.float32, device=dev)
   # the episodic (reward, done) exchange: summed on the device every step,
-  # all-gathered over RCCL once per episode length
-  exchange = bd.EpisodeExchange(B, dev, every=1000) if world > 1 else None
+  # all-gathered over RCCL once per period: the episode length (1000), or the
+  # timed step count when shorter, so every timed region holds >= 1 collective
+  K = graph_steps(args.steps)
+  period = bd.exchange_period(1000, args.steps, K)
+  exchange = bd.EpisodeExchange(B, dev, every=period) if world > 1 else None
 
   def one_step(st, k):
     # the step's action slab, keyed by (step, global env id): drawn on the
@@ -367,11 +406,16 @@ def main():
                    bd.action_offset(rank, B, A, k, world), -1.0, 1.0, stream)
     st = env.step(st, act)
     if exchange is not None:
-      exchange(st.reward, st.done)  # the one RCCL collective, once per 1000 steps
+      exchange(st.reward, st.done)  # the RCCL all-gather once per period
     return st
 
   for k in range(args.warmup):
     state = one_step(state, k)
+  # the step kernel alone (its launch train also brings the clocks up before
+  # the timed loops)
+  kern_ms = kernel_train(env, state, act)
+  if exchange is not None:
+    exchange.reset()
   torch.cuda.synchronize()
   if dist is not None:
     dist.barrier()
@@ -385,11 +429,12 @@ def main():
   torch.cuda.synchronize()
   elapsed = time.perf_counter() - t0
   eager_elapsed = elapsed
-  # the same loop replayed from a hipGraph: K steps (draw + Env.step + the
-  # episodic sum) per graph launch, the actions continuing the eager loop's
-  # (step, global env id) stream; see brax_amd/envs/graph.py
+  eager_collectives = exchange.flushes if exchange is not None else 0
+  # the same loop replayed from a hipGraph: K steps per graph launch (one
+  # draw of the K action slabs, then K x (Env.step + the episodic sum)), the
+  # actions continuing the eager loop's (step, global env id) stream; see
+  # brax_amd/envs/graph.py
   from brax_amd.envs.graph import StepGraph
-  K = math.gcd(args.steps, GRAPH_STEPS)
   k0 = args.warmup + args.steps
   graph_err = None
   try:
@@ -407,11 +452,13 @@ def main():
     dist.all_reduce(f, op=dist.ReduceOp.MIN)
     use_graph = bool(f.item())
   elapsed = eager_elapsed
+  collectives = eager_collectives
   if use_graph:
-    for _ in range(max(args.warmup // K, 1)):
+    # warm replays (the first replay of a fresh graph uploads it)
+    for _ in range(max(args.warmup // K, 2)):
       state = g.replay()
-      if exchange is not None:
-        exchange.advance(K)
+    if exchange is not None:
+      exchange.reset()
     torch.cuda.synchronize()
     if dist is not None:
       dist.barrier()
@@ -420,12 +467,13 @@ def main():
     for _ in range(args.steps // K):
       state = g.replay()
       if exchange is not None:
-        exchange.advance(K)  # the RCCL gather once per 1000 steps, on the host
+        exchange.advance(K)  # the RCCL all-gather once per period, on the host
     torch.cuda.synchronize()
     if dist is not None:
       dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    collectives = exchange.flushes if exchange is not None else 0
   if dist is not None:
     t = torch.tensor([elapsed, eager_elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -436,7 +484,6 @@ def main():
   if rank != 0:
     dist.destroy_process_group()
     return
-  kern_ms = kernel_train(env, state, act)
   bytes_per_launch = ANT_BYTES_PER_ENV_STEP * B
   flops_per_launch = ANT_FLOPS_PER_ENV_STEP * B
   tflops = flops_per_launch / (kern_ms * 1e-3) / 1e12
@@ -470,11 +517,16 @@ def main():
               'config with device-RNG joint noise keyed by global env id',
       'config': {'workload': 'Ant-v1 Env.step (10 PBD substeps + obs/reward + '
                              'Episode/AutoReset), envs.create(ant)',
-                 'launch': (f'hipGraph replays of {K} captured steps (each: on-device action '
-                            'draw + fused Env.step kernel + episodic sum when N>1)' if use_graph
+                 'launch': (f'hipGraph replays of {K} captured steps (one on-device draw of '
+                            f'the {K} action slabs, then per step the fused Env.step kernel + '
+                            'the episodic sum when N>1)' if use_graph
                             else f'eager Python loop (graph capture failed: {graph_err})'),
                  'envs_per_gpu': B, 'episode_length': 1000, 'substeps': 10,
-                 'parallelism': f'env-shard x{world}'},
+                 'parallelism': f'env-shard x{world}',
+                 'exchange_period': period if world > 1 else None},
+      # RCCL all-gathers of the episodic (reward, done) sums inside the timed
+      # region (0 at N = 1: there is no collective on one GPU)
+      'collectives_in_timed_region': collectives,
       # the fused env step is VALU/latency-bound (AI ~61 flop/B):
       # headline = counted flops / kernel time vs the FP32 VALU peak; the HBM
       # view (algorithmic bytes / kernel time vs 8 TB/s) is kept beside it
@@ -496,7 +548,8 @@ def main():
   # the same steps from the plain Python loop (one Env.step call per step):
   # host-bound on a slow host, hence the graph above
   out['eager_loop'] = {'value': total / eager_elapsed, 'unit': 'env-steps/s',
-                       'ms_per_step': eager_elapsed * 1e3 / args.steps}
+                       'ms_per_step': eager_elapsed * 1e3 / args.steps,
+                       'collectives_in_timed_region': eager_collectives}
   out['secondary_configs'] = None if args.no_secondary else secondary_configs(dev)
   out['phase_roofline'] = (None if args.no_phases else
                            phase_bench(env.unwrapped.sys, dev, args.phase_envs))

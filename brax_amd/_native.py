@@ -67,6 +67,8 @@ _SIGS = {
                     C.c_void_p], C.c_int),
     'bx_uniform_epoch': ([C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_void_p,
                           C.c_uint64, C.c_float, C.c_float, C.c_void_p], C.c_int),
+    'bx_uniform_slabs': ([C.c_void_p, C.c_int64, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64,
+                          C.c_void_p, C.c_uint64, C.c_float, C.c_float, C.c_void_p], C.c_int),
 }
 
 EXPORTS = tuple(_SIGS)

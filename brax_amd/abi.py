@@ -12,7 +12,7 @@ i32p = C.POINTER(C.c_int32)
 f64p = C.POINTER(C.c_double)
 f32p = C.POINTER(C.c_float)
 
-ABI_VERSION = 8  # include/brax_amd.h BX_ABI_VERSION
+ABI_VERSION = 9  # include/brax_amd.h BX_ABI_VERSION
 
 _DESC_FIELDS = [
     ('n_bodies', C.c_int32), ('n_joints', C.c_int32), ('n_actuators', C.c_int32),
@@ -80,7 +80,8 @@ class BxInfo(C.Structure):
               ('actuator_vel', BxField), ('actuator_ang', BxField),
               ('contact_pos', C.c_void_p), ('contact_normal', C.c_void_p),
               ('contact_penetration', C.c_void_p),
-              ('joint_vel', BxField), ('joint_ang', BxField)]
+              ('joint_vel', BxField), ('joint_ang', BxField),
+              ('contact_cell', C.c_void_p)]
 
 
 class BxEnvState(C.Structure):

@@ -121,6 +121,10 @@ class Info:
   contact_pos: Any
   contact_normal: Any
   contact_penetration: Any
+  # beyond the reference's fields: the NearNeighbors cell i * U + j behind
+  # each contact row (the `idx` of `top_k`, colliders.py:84), -1 for Pairs
+  # rows; None for systems without culled collider groups
+  contact_cell: Any = None
 
   def replace(self, **kw):
     return dataclasses.replace(self, **kw)

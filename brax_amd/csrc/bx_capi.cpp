@@ -241,6 +241,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     if (d->row_ext)
       for (int k = 0; k < 16; k++) B.f(o + R_X + k, d->row_ext[16 * x + k]);
     B.i(o + R_NNMASK, d->row_nn_masked && d->row_nn_masked[x] ? 1 : 0);
+    B.i(o + R_FLAT, d->col_cutoff[g] ? d->row_flat[x] : -1);
     if (d->col_fn[g] == BX_COL_HEIGHTMAP) {
       B.i(o + R_HM_OFF, d->row_hm[2 * x]);
       B.i(o + R_HM_M, d->row_hm[2 * x + 1]);
@@ -1196,18 +1197,33 @@ int bx_debug_stamps(unsigned long long* out, int reset) {
 }
 
 int bx_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset, float lo, float hi, void* stream) {
-  if (n <= 0) return n == 0 ? 0 : fail("negative n");
-  if (!out) return fail("null output");
-  HIP_OK(launch_uniform(out, n, seed, offset, lo, hi, as_stream(stream)));
-  return 0;
+  return bx_uniform_slabs(out, n, 1, seed, offset, 0, nullptr, 0, lo, hi, stream);
 }
 
 int bx_uniform_epoch(float* out, int64_t n, uint64_t seed, uint64_t offset, const int64_t* epoch,
                      uint64_t epoch_stride, float lo, float hi, void* stream) {
-  if (n <= 0) return n == 0 ? 0 : fail("negative n");
-  if (!out || !epoch) return fail("null output or epoch counter");
-  HIP_OK(launch_uniform_epoch(out, n, seed, offset, epoch, epoch_stride, lo, hi,
-                              as_stream(stream)));
+  if (!epoch && n > 0) return fail("null epoch counter");
+  return bx_uniform_slabs(out, n, 1, seed, offset, 0, epoch, epoch_stride, lo, hi, stream);
+}
+
+int bx_uniform_slabs(float* out, int64_t slab_n, int64_t n_slabs, uint64_t seed, uint64_t offset,
+                     uint64_t slab_stride, const int64_t* epoch, uint64_t epoch_stride, float lo,
+                     float hi, void* stream) {
+  if (slab_n < 0 || n_slabs < 0) return fail("negative size");
+  if (slab_n == 0 || n_slabs == 0) return 0;
+  if (slab_n > INT64_MAX / n_slabs || slab_n * n_slabs > ((int64_t)1 << 40))
+    return fail("too many elements for one draw");
+  if (!out) return fail("null output");
+  // no system handle here: launch on the device that owns the stream (the
+  // caller's current device for the null stream)
+  int dev = -1;
+  hipStream_t st = as_stream(stream);
+  if (st) HIP_OK(hipStreamGetDevice(st, &dev));
+  else HIP_OK(hipGetDevice(&dev));
+  DeviceScope scope(dev);
+  if (scope.err != hipSuccess) return fail(std::string("device: ") + hipGetErrorString(scope.err));
+  HIP_OK(launch_uniform_slabs(out, slab_n, n_slabs, seed, offset, slab_stride, epoch, epoch_stride,
+                              lo, hi, st));
   return 0;
 }
 

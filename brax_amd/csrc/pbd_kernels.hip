@@ -2721,6 +2721,7 @@ struct RowInfoOut {
   float* pos;
   float* normal;
   float* pen;
+  int32_t* cell;  // the row's NearNeighbors cell (R_FLAT)
 };
 
 #ifdef BX_MSTAMPS
@@ -3035,10 +3036,12 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
 #else
       const int x = lane + m * L;
       if (x >= nact) continue;
+      const int r = BX_MULTI_RX(x);
 #endif
       if (io.pos) st3(io.pos + x * 3, cpos[m]);
       if (io.normal) st3(io.normal + x * 3, cn[m]);
       if (io.pen) io.pen[x] = pen[m];
+      if (io.cell) io.cell[x] = c.i(H.o_row + r * ROW_STRIDE + R_FLAT);
     }
   }
   if (X.hasB) {
@@ -3648,7 +3651,8 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
     const int64_t ro = valid ? e * H.info_rows : 0;
     RowInfoOut io{A.info.contact_pos ? A.info.contact_pos + ro * 3 : nullptr,
                   A.info.contact_normal ? A.info.contact_normal + ro * 3 : nullptr,
-                  A.info.contact_penetration ? A.info.contact_penetration + ro : nullptr};
+                  A.info.contact_penetration ? A.info.contact_penetration + ro : nullptr,
+                  A.info.contact_cell ? A.info.contact_cell + ro : nullptr};
     pbd_step_multi<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr,
                             (int)A.act_width, X, io);
   } else if constexpr (S) {
@@ -3702,6 +3706,7 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
     if (A.info.contact_pos) st3(A.info.contact_pos + o * 3, ld3(rd));
     if (A.info.contact_normal) st3(A.info.contact_normal + o * 3, ld3(rd + 3));
     if (A.info.contact_penetration) A.info.contact_penetration[o] = rd[6];
+    if (A.info.contact_cell) A.info.contact_cell[o] = c.i(H.o_row + r * ROW_STRIDE + R_FLAT);
   }
 }
 
@@ -4270,16 +4275,22 @@ __global__ void uniform_kernel(float* out, int64_t n, uint64_t seed, uint64_t of
   out[i] = uniform_at(seed, (uint64_t)i + offset, lo, hi);
 }
 
-// the same fill with the offset advanced by a device-resident epoch counter
-// (offset + epoch * stride): a graph-captured rollout replays one launch and
-// still draws a fresh slab per replay (the counter is bumped inside the graph)
-__global__ void uniform_epoch_kernel(float* out, int64_t n, uint64_t seed, uint64_t offset,
-                                     const int64_t* __restrict__ epoch, uint64_t stride,
+// the same fill over n_slabs slabs of slab_n elements with their own offsets,
+// advanced by a device-resident epoch counter: out[s * slab_n + j] =
+// U(seed, offset + epoch * epoch_stride + s * slab_stride + j). A
+// graph-captured rollout draws the action slabs of all its K steps in one
+// launch and still draws fresh slabs per replay (the counter is bumped inside
+// the graph); epoch null reads as 0
+__global__ void uniform_slabs_kernel(float* out, int64_t slab_n, int64_t n, uint64_t seed,
+                                     uint64_t offset, uint64_t slab_stride,
+                                     const int64_t* __restrict__ epoch, uint64_t epoch_stride,
                                      float lo, float hi) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint64_t off = offset + (uint64_t)epoch[0] * stride;
-  out[i] = uniform_at(seed, (uint64_t)i + off, lo, hi);
+  const uint64_t e = epoch ? (uint64_t)epoch[0] : 0ull;
+  const int64_t sl = i / slab_n, j = i - sl * slab_n;
+  out[i] = uniform_at(seed, offset + e * epoch_stride + (uint64_t)sl * slab_stride + (uint64_t)j,
+                      lo, hi);
 }
 
 #endif
@@ -4465,12 +4476,13 @@ hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
   hipLaunchKernelGGL(uniform_kernel, grid, dim3(256), 0, s, out, n, seed, offset, lo, hi);
   return hipGetLastError();
 }
-hipError_t launch_uniform_epoch(float* out, int64_t n, uint64_t seed, uint64_t offset,
-                                const int64_t* epoch, uint64_t stride, float lo, float hi,
-                                hipStream_t s) {
+hipError_t launch_uniform_slabs(float* out, int64_t slab_n, int64_t n_slabs, uint64_t seed,
+                                uint64_t offset, uint64_t slab_stride, const int64_t* epoch,
+                                uint64_t epoch_stride, float lo, float hi, hipStream_t s) {
+  const int64_t n = slab_n * n_slabs;
   dim3 grid((unsigned)((n + 255) / 256));
-  hipLaunchKernelGGL(uniform_epoch_kernel, grid, dim3(256), 0, s, out, n, seed, offset, epoch,
-                     stride, lo, hi);
+  hipLaunchKernelGGL(uniform_slabs_kernel, grid, dim3(256), 0, s, out, slab_n, n, seed, offset,
+                     slab_stride, epoch, epoch_stride, lo, hi);
   return hipGetLastError();
 }
 

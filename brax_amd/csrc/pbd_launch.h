@@ -76,9 +76,9 @@ hipError_t launch_info_obs(int L, int64_t n_envs, size_t lds, hipStream_t s, con
 hipError_t launch_default_qp(int64_t n_envs, size_t lds, hipStream_t s, const ResetArgs& a);
 hipError_t launch_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset, float lo, float hi,
                           hipStream_t s);
-hipError_t launch_uniform_epoch(float* out, int64_t n, uint64_t seed, uint64_t offset,
-                                const int64_t* epoch, uint64_t stride, float lo, float hi,
-                                hipStream_t s);
+hipError_t launch_uniform_slabs(float* out, int64_t slab_n, int64_t n_slabs, uint64_t seed,
+                                uint64_t offset, uint64_t slab_stride, const int64_t* epoch,
+                                uint64_t epoch_stride, float lo, float hi, hipStream_t s);
 
 hipError_t debug_stamps(unsigned long long* out, int reset);
 hipError_t debug_mstamps(unsigned long long* out, int reset);  // MULTI mode (item-loop TU)

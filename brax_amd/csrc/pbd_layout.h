@@ -38,6 +38,8 @@ enum {
   R_X = 24, R_HM_OFF = 40, R_HM_M = 41,
   // a NearNeighbors cell outside the allowed mask (top_k's -inf tail)
   R_NNMASK = 42,
+  // the row's NearNeighbors cell i * U + j (colliders.py:84-85), -1 for Pairs rows
+  R_FLAT = 43,
 };
 enum {
   FK_STRIDE = 24,

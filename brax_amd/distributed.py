@@ -37,6 +37,16 @@ def action_offset(rank: int, envs_per_rank: int, action_size: int, step: int = 0
   return (step * world + rank) * envs_per_rank * action_size
 
 
+def exchange_period(episode_length: int, timed_steps: int, replay: int = 1) -> int:
+  """Steps between episodic all-gathers in a timed run: the episode length,
+  or the timed step count when that is shorter (so a short timed region
+  still holds at least one collective), rounded down to a multiple of the
+  graph replay length (`EpisodeExchange.advance` counts whole replays)."""
+  replay = max(int(replay), 1)
+  p = min(int(episode_length), int(timed_steps))
+  return max(p - p % replay, replay)
+
+
 class EpisodeExchange:
   """Episodic exchange of every rank's per-env (reward, done).
 
@@ -55,6 +65,7 @@ class EpisodeExchange:
     self.acc = torch.zeros((2, envs_per_rank), dtype=torch.float32, device=device)
     self.out = torch.empty((self.world, 2, envs_per_rank), dtype=torch.float32, device=device)
     self._nccl = dist.get_backend(group) == 'nccl'
+    self.flushes = 0  # all-gathers done (bench.py reports those in its timed region)
 
   def __call__(self, reward, done):
     self.accumulate(reward, done)
@@ -74,23 +85,38 @@ class EpisodeExchange:
       self.acc[0].add_(reward.float())
       self.acc[1].add_(done.float())
 
+  def reset(self):
+    """Zeroes the sums and the step count (e.g. at the start of a timed
+    region, so its exchange periods start there)."""
+    self.acc.zero_()
+    self.k = 0
+    self.flushes = 0
+
   def advance(self, n):
     """Counts `n` steps accumulated by a replayed graph; flushes (and
-    returns the gathered sums) when they complete an exchange period."""
-    out = None
-    for _ in range(int(n)):
-      self.k += 1
-      if self.k % self.every == 0:
-        out = self.flush()
-    return out
+    returns the gathered sums) when they complete an exchange period. The
+    device sums already hold all n steps, so a period boundary must fall at
+    the end of the n steps: `every` must be a multiple of n and the count so
+    far too, else ValueError (a flush inside the replay would gather steps
+    past the boundary)."""
+    n = int(n)
+    if n < 1 or self.every % n or self.k % n:
+      raise ValueError(f'exchange period {self.every} and step count {self.k} must be '
+                       f'multiples of the replay length {n}')
+    self.k += n
+    return self.flush() if self.k % self.every == 0 else None
 
   def flush(self):
-    """All-gathers the sums since the last exchange and resets them."""
+    """All-gathers the sums since the last exchange, resets them and returns
+    the gathered (world, 2, B) sums (a fresh tensor per flush)."""
     if self._nccl:
-      dist.all_gather_into_tensor(self.out, self.acc, group=self.group)
+      out = torch.empty_like(self.out)
+      dist.all_gather_into_tensor(out, self.acc, group=self.group)
     else:
-      parts = list(self.out.unbind(0))
+      parts = list(torch.empty_like(self.out).unbind(0))
       dist.all_gather(parts, self.acc.clone(), group=self.group)
-      self.out = torch.stack(parts)
+      out = torch.stack(parts)
+    self.out = out
     self.acc.zero_()
-    return self.out
+    self.flushes += 1
+    return out

@@ -126,6 +126,7 @@ class System:
     self.action_size = meta['action_size']
     self.num_rows = len(self.desc["row_group"])  # contact rows (every candidate cell)
     self.num_contacts = abi.info_rows(self.desc)  # Info contact rows (system.py:36-43)
+    self._culled = bool((np.asarray(self.desc.get('col_cutoff', [0])) > 0).any())
     self.body = Body(self.desc, meta['body_index'])
     self.joint_groups = meta['joint_groups']
     self.joints = []
@@ -258,10 +259,14 @@ class System:
     if spring:  # Info.joint: accumulated spring dp_j (zero_info under pbd)
       info.joint_vel = _field(cbuf[..., 12:15], batched)
       info.joint_ang = _field(cbuf[..., 15:18], batched)
+    cell = None
     if R:
       info.contact_pos = cpos.data_ptr()
       info.contact_normal = cnorm.data_ptr()
       info.contact_penetration = cpen.data_ptr()
+      if self._culled:
+        cell = torch.empty(lead + (R,), dtype=torch.int32, device=self.device)
+        info.contact_cell = cell.data_ptr()
     qi = qp_struct(qp, batched)
     qo = qp_struct(out, batched)
     _native.check(_native.lib().bx_system_step(
@@ -270,7 +275,8 @@ class System:
     zero = torch.zeros_like(cvel)
     joint = P(cbuf[..., 12:15], cbuf[..., 15:18]) if spring else P(zero, zero)
     return out, Info(contact=P(cvel, cang), joint=joint, actuator=P(avel, aang),
-                     contact_pos=cpos, contact_normal=cnorm, contact_penetration=cpen)
+                     contact_pos=cpos, contact_normal=cnorm, contact_penetration=cpen,
+                     contact_cell=cell)
 
   def joint_angle_vel(self, qp: QP):
     """Angles and angular velocities of every joint dof, in joint order

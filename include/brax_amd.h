@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 8
+#define BX_ABI_VERSION 9
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
 enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
@@ -227,6 +227,11 @@ typedef struct bx_info {
   float* contact_penetration;           /* (B,R)   */
   bx_field joint_vel, joint_ang;        /* (B,N,3) accumulated joint P
                                            (legacy_spring; zero under pbd) */
+  /* (B,R) contiguous, bx_system_step only (ABI 9): the NearNeighbors cell
+   * i * U + j behind each Info contact row, i.e. the `idx` of
+   * `jp.top_k(sim.ravel(), cutoff)` in colliders.py:84 for a culled group's
+   * rows (nearest first), -1 for Pairs rows */
+  int32_t* contact_cell;
 } bx_info;
 
 /* Env-layer state of one batch (ant.py:198-255, wrappers.py:83-148).
@@ -414,6 +419,17 @@ int bx_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
 int bx_uniform_epoch(float* out, int64_t n, uint64_t seed, uint64_t offset,
                      const int64_t* epoch, uint64_t epoch_stride,
                      float lo, float hi, void* stream);
+
+/* n_slabs slabs of slab_n elements in one launch, each slab at its own
+ * offset: out[s * slab_n + j] = U(seed, offset + (*epoch) * epoch_stride +
+ * s * slab_stride + j), epoch NULL reading as 0. A graph-captured rollout of K
+ * steps draws its K action slabs with one launch (slab_stride = the job's
+ * per-step stride world x B x A, so every slab is bit-identical to the
+ * bx_uniform draw of that step; ABI 9). The bx_uniform* calls launch on the
+ * device that owns `stream` (the current device for NULL). */
+int bx_uniform_slabs(float* out, int64_t slab_n, int64_t n_slabs, uint64_t seed,
+                     uint64_t offset, uint64_t slab_stride, const int64_t* epoch,
+                     uint64_t epoch_stride, float lo, float hi, void* stream);
 
 /*
  * Standalone HBM-streaming phase kernels over a structure-of-arrays batch

@@ -385,16 +385,62 @@ def env_traj(env, name, n_envs, n_steps, act_seed_base=10_000):
   return res
 
 
+class record_top_k:
+  """Records every NearNeighbors selection `NearNeighbors.update` makes
+  (colliders.py:71-85): each `jumpy.top_k` call's operand (sim = -(dist +
+  dist_off), all candidate cells, flat) and the indices it returns (the
+  selected cells, nearest first), in call (= collider) order. Wraps
+  whichever top_k is installed (numpy's, or stable_top_k's)."""
+
+  def __enter__(self):
+    from brax import jumpy
+    self.jp, self.orig = jumpy, jumpy.top_k
+    self.calls = []
+
+    def top_k(operand, k):
+      val, idx = self.orig(operand, k)
+      self.calls.append((np.asarray(operand, np.float64).copy(), np.asarray(idx).copy()))
+      return val, idx
+    jumpy.top_k = top_k
+    return self
+
+  def take(self):
+    c, self.calls = self.calls, []
+    return c
+
+  def __exit__(self, *exc):
+    self.jp.top_k = self.orig
+
+
 def sys_traj(sys_, name, qp0, n_envs, n_steps, act_scale, A, seed_base=20_000):
-  """Physics-only System.step rollout from a fixed state."""
+  """Physics-only System.step rollout from a fixed state. For systems with
+  NearNeighbors culling, also the reference's own selection per step and
+  env: `nn_cell` (T, B, sum of cutoffs) the top_k indices (flat cells i * U +
+  j, nearest first, culled groups in collider order) and `nn_sim` (T, B,
+  sum of U * U) the similarities top_k ranked."""
+  from brax.physics import colliders as rc
   out = {k: [] for k in ('qp', 'info_contact', 'info_actuator', 'contact_penetration')}
   acts = np.stack([np.random.default_rng(seed_base + t).uniform(-1, 1, (n_envs, A))
                    * act_scale for t in range(n_steps)])
-  qps = [qp0 for _ in range(n_envs)]
+  # one start state for every env, or a list of per-env start states
+  qps = list(qp0) if isinstance(qp0, list) else [qp0 for _ in range(n_envs)]
   out['qp'].append(np.stack([qp_pack(q) for q in qps]))
   t0 = time.time()
+  culled = any(isinstance(c.cull, rc.NearNeighbors) for c in sys_.colliders)
+  cells, sims = [], []
   for t in range(n_steps):
-    res = [sys_.step(q, acts[t, b]) for b, q in enumerate(qps)]
+    if culled:
+      res, cs, ss = [], [], []
+      with record_top_k() as rec:
+        for b, q in enumerate(qps):
+          res.append(sys_.step(q, acts[t, b]))
+          calls = rec.take()
+          cs.append(np.concatenate([i for _, i in calls]).astype(np.int32))
+          ss.append(np.concatenate([o for o, _ in calls]))
+      cells.append(np.stack(cs))
+      sims.append(np.stack(ss))
+    else:
+      res = [sys_.step(q, acts[t, b]) for b, q in enumerate(qps)]
     qps = [r[0] for r in res]
     out['qp'].append(np.stack([qp_pack(q) for q in qps]))
     out['info_contact'].append(np.stack([np.concatenate(
@@ -405,6 +451,9 @@ def sys_traj(sys_, name, qp0, n_envs, n_steps, act_scale, A, seed_base=20_000):
     print(f'  {name}: step {t + 1}/{n_steps}  ({time.time() - t0:.1f}s)', flush=True)
   r = {k: np.stack(v) for k, v in out.items()}
   r['action'] = acts
+  if culled:
+    r['nn_cell'] = np.stack(cells)
+    r['nn_sim'] = np.stack(sims)
   return r
 
 
@@ -579,6 +628,16 @@ SPRING_ROBOTS = {
 }
 
 
+def _short_scenes():
+  import scenes
+  picks = [0, 1, 7, 17, 19, 21, 23]
+  return {'capsule_ground_s': (CAPSULE_TEST_CONFIG, 0, 5, None),
+          'capsule_capsule_s': (CAPSULE_TEST_CONFIG, 1, 17, picks),
+          'capsule_cull_s': (CAPSULE_TEST_CONFIG, 1, 17, picks),
+          'box_ground_s': (scenes.BOX_TEST_CONFIG, 0, 5, None),
+          'box_slide_s': (scenes.BOX_TEST_CONFIG, 1, 10, None)}
+
+
 TORCH_ENVS = ['hopper', 'walker2d', 'inverted_pendulum', 'inverted_double_pendulum',
               'swimmer', 'reacher', 'reacherangle', 'acrobot', 'pusher', 'ur5e', 'grasp', 'fetch']
 
@@ -687,6 +746,36 @@ def main():
     s = ant_mountain_sys(1, cutoff=9)
     save('desc_mountain1nn', dump_desc(s))
     save('traj_mountain1nn', sys_traj(s, 'mountain1nn', s.default_qp(), 4, 4, 1.0, 8))
+  # short-horizon twins of the reference's long physics-test scenes: the same
+  # bodies at the Ant's dt 0.05 / 10 substeps, from `burn` zero-action steps
+  # past default_qp (falling into contact), 8 steps recorded, so the fp32
+  # envelope stays small enough for the state gate to mean something (the
+  # long scenes integrate 400-10,000 substeps per step; they stay KATs)
+  sys.path.insert(0, HERE)
+  for name, (txt, di, burn, picks) in _short_scenes().items():
+    if want(name):
+      from google.protobuf import text_format
+      import brax
+      cfg = text_format.Parse(txt, brax.Config())
+      cfg.dt, cfg.substeps = 0.05, 10
+      if name.startswith('capsule_cull'):
+        cfg.collider_cutoff = 1
+      s = brax.System(cfg)
+      qp = s.default_qp(di)
+      for _ in range(burn):
+        qp, _ = s.step(qp, np.zeros(0))
+      save(f'desc_{name}', dump_desc(s))
+      if picks is None:
+        save(f'traj_{name}', sys_traj(s, name, qp, 1, 8, 1.0, 0))
+        continue
+      # resting contacts chatter at their gates (penetration > 0, the sinking
+      # test) every other step, where even float64 loses digits: one step
+      # each from the states `picks` steps past the burn-in whose capsule-
+      # capsule contact is active and well conditioned, as a batch of envs
+      states = [qp]
+      for _ in range(max(picks)):
+        states.append(s.step(states[-1], np.zeros(0))[0])
+      save(f'traj_{name}', sys_traj(s, name, [states[k] for k in picks], len(picks), 1, 1.0, 0))
   for kind in ('ground', 'capsule', 'cull'):
     if want('capsule_' + kind):
       s, di = capsule_sys(kind)
@@ -716,7 +805,7 @@ def main():
     s = brax.System(text_format.Parse(scenes.TWIN_CULL_CONFIG, brax.Config()))
     save('desc_twin_cull', dump_desc(s))
     with stable_top_k():
-      save('traj_twin_cull', sys_traj(s, 'twin_cull', s.default_qp(), 1, 4, 1.0, 0))
+      save('traj_twin_cull', sys_traj(s, 'twin_cull', s.default_qp(), 1, 8, 1.0, 0))
   for name, (txt, di, T) in point_scenes.items():
     if want(name):
       s = brax.System(text_format.Parse(txt, brax.Config()))

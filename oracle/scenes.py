@@ -213,7 +213,7 @@ defaults {{
 # the two masked (-inf) cells of lowest flat index: (0, 0), a capsule against
 # itself, and (0, 2).
 TWIN_CULL_CONFIG = """
-dt: 0.5 substeps: 50 friction: 0.6 gravity { z: -9.8 }
+dt: 0.05 substeps: 10 friction: 0.6 gravity { z: -9.8 }
 bodies { name: "A" mass: 1 inertia { x: 1 y: 1 z: 1 }
   colliders { capsule { radius: 0.25 length: 1.0 } }
   colliders { position { x: 0.5 } rotation { y: 90 } capsule { radius: 0.2 length: 0.8 } } }

@@ -33,6 +33,11 @@ defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { x:
 defaults { qps { name: "Capsule1" pos { z: 1 } } qps { name: "Capsule2" pos { z: 2 } } qps { name: "Capsule3" pos { x: 3 z: 1 } } qps { name: "Capsule4" pos { x: 5 z: 1 } } }
 """
 CAPSULES = ['capsule_ground', 'capsule_capsule', 'capsule_cull']
+# short-horizon twins of the long physics-test scenes (dt 0.05, 10 substeps,
+# from a state falling into contact; oracle/gen_golden.py _short_scenes):
+# the golden trajectory gates run on these, the long scenes stay KATs
+SHORT_SCENES = ['capsule_ground_s', 'capsule_capsule_s', 'capsule_cull_s', 'box_ground_s',
+                'box_slide_s']
 # NearNeighbors with more cutoff than allowed cells: top_k also returns
 # masked cells (oracle/scenes.py TWIN_CULL_CONFIG; golden generated under
 # jax.lax.top_k's tie order)
@@ -127,6 +132,11 @@ XCOL = ['heightmap', 'clipped', 'box_capsule', 'mesh_capsule', 'box_box', 'box_c
 
 
 def config_for(name):
+  if name in SHORT_SCENES:
+    base = name[:-2]
+    cfg = config_for('box_ground' if base.startswith('box') else base)
+    cfg.dt, cfg.substeps = 0.05, 10
+    return cfg
   if name.endswith('_xy'):
     name = name[:-len('_xy')]
   if name.endswith('_spring'):
@@ -155,9 +165,10 @@ def config_for(name):
   if name == 'twin_cull':
     from oracle import scenes
     return cfgmod.parse(scenes.TWIN_CULL_CONFIG)
-  if name == 'mountain1nn':
-    cfg = ant_mountain_config(1)
-    cfg.collider_cutoff = 9
+  if name in ('mountain1nn', 'mountain2nn'):
+    n = int(name[len('mountain')])
+    cfg = ant_mountain_config(n)
+    cfg.collider_cutoff = 9 * n
     return cfg
   if name in ROBOTS:
     return cfgmod.parse(getattr(robots, name.upper() + '_CONFIG'))

@@ -34,12 +34,24 @@ def _worker(rank, world, port, q):
   out = out.numpy().copy()
   left = float(ex.acc.abs().sum())
   # a graph-replayed rollout's split: device sums per step, host count after
-  for _ in range(3):
+  # each replay of 2 steps, period 4 (the bench's exchange_period logic)
+  ex = bd.EpisodeExchange(B, 'cpu', every=bd.exchange_period(1000, 4, replay=2))
+  assert ex.every == 4
+  for _ in range(2):
     ex.accumulate(*scal.unbind(0)[:2])
-  assert ex.advance(2) is None  # k = 5: mid-period
-  ex.accumulate(reward, done)  # a step past the period stays in the sums
-  out2 = ex.advance(1)  # k = 6: the second episodic gather
+  assert ex.advance(2) is None  # k = 2: mid-period
+  for _ in range(2):
+    ex.accumulate(reward, done)
+  out2 = ex.advance(2)  # k = 4: the episodic gather
   np.testing.assert_array_equal(out2.numpy()[:, 0], 4 * out[:, 0] / 3)
+  assert ex.flushes == 1
+  try:
+    ex.advance(3)  # a period boundary inside the replay: refused
+    raise AssertionError('advance(3) with every=4 must raise')
+  except ValueError:
+    pass
+  ex.reset()
+  assert ex.k == 0 and ex.flushes == 0 and float(ex.acc.abs().sum()) == 0
   q.put((rank, out, bd.action_offset(rank, B, 8, step=3, world=world), left))
   dist.barrier()
   dist.destroy_process_group()
@@ -67,6 +79,14 @@ def test_episode_allgather_world2():
     assert left == 0.0  # the sums restart after the exchange
   # rank r's action rows of step 3 continue rank r-1's in the global stream
   assert res[1][2] - res[0][2] == 5 * 8
+
+
+def test_exchange_period():
+  assert bd.exchange_period(1000, 20, 20) == 20  # the driver's 20-step run: one gather
+  assert bd.exchange_period(1000, 1000, 50) == 1000
+  assert bd.exchange_period(1000, 5000, 50) == 1000
+  assert bd.exchange_period(1000, 30, 20) == 20
+  assert bd.exchange_period(7, 3, 5) == 5
 
 
 def test_env_range():

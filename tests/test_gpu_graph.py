@@ -44,10 +44,23 @@ def _same(a, b):
     assert torch.equal(a.metrics[k], b.metrics[k]), k
 
 
-@pytest.mark.parametrize('name,B,K,overlap', [('ant', 512, 5, True), ('ant', 512, 5, False),
-                                              ('humanoid', 256, 3, True), ('fetch', 128, 4, True),
-                                              ('ant', 64, 1, True)])
-def test_graph_replays_match_eager_loop(dev, name, B, K, overlap):
+def _eager_ranked(env, state, steps, seed, dev, B, A, k0, rank, world):
+  from brax_amd import _native
+  from brax_amd import distributed as bd
+  act = torch.empty((B, A), dtype=torch.float32, device=dev)
+  for k in range(steps):
+    _native.check(_native.lib().bx_uniform(
+        C.c_void_p(act.data_ptr()), B * A, seed, bd.action_offset(rank, B, A, k0 + k, world),
+        -1.0, 1.0, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    state = env.step(state, act)
+  return state
+
+
+@pytest.mark.parametrize('name,B,K,draw', [('ant', 512, 5, 'batched'), ('ant', 512, 5, 'per_step'),
+                                           ('humanoid', 256, 3, 'batched'),
+                                           ('fetch', 128, 4, 'batched'),
+                                           ('ant', 64, 1, 'batched')])
+def test_graph_replays_match_eager_loop(dev, name, B, K, draw):
   from brax_amd import envs
   from brax_amd import distributed as bd
   from brax_amd.envs.graph import StepGraph
@@ -58,7 +71,7 @@ def test_graph_replays_match_eager_loop(dev, name, B, K, overlap):
   # epoch counter's second slab set
   ref = _eager(env, st0, 2 * K, 5, dev, B, A, k0=3)
   g = StepGraph(env, st0, K, seed=5, offset=bd.action_offset(0, B, A, 3, 1), step_stride=B * A,
-                overlap_draw=overlap)
+                draw=draw)
   out = g.replay()
   mid = _eager(env, st0, K, 5, dev, B, A, k0=3)
   _same(out, mid)
@@ -68,6 +81,49 @@ def test_graph_replays_match_eager_loop(dev, name, B, K, overlap):
   assert g.epoch == 2
   if 'rng' in st0.info:
     assert torch.equal(out.info['rng'], ref.info['rng'])
+
+
+@pytest.mark.parametrize('draw', ['batched', 'per_step'])
+def test_graph_rank_slabs_match_eager_loop(dev, draw):
+  """Rank 1 of a world of 2: the job's per-step stride (world x B x A) and
+  the rank's row offset; the one-launch slab draw gives every step the bits
+  of the eager loop's bx_uniform at action_offset(1, B, A, step, 2)."""
+  from brax_amd import envs
+  from brax_amd import distributed as bd
+  from brax_amd.envs.graph import StepGraph
+  B, K, world, rank, k0 = 128, 4, 2, 1, 6
+  env = envs.create('ant', batch_size=B, episode_length=1000, auto_reset=True, device=dev)
+  A = env.action_size
+  bd.shard_env(env, rank, B)
+  st0 = env.reset(np.array([0, 4], np.uint32))
+  ref = _eager_ranked(env, st0, 3 * K, 2, dev, B, A, k0, rank, world)
+  g = StepGraph(env, st0, K, seed=2, offset=bd.action_offset(rank, B, A, k0, world),
+                step_stride=world * B * A, draw=draw)
+  for _ in range(3):
+    out = g.replay()
+  torch.cuda.synchronize()
+  _same(out, ref)
+
+
+def test_graph_target_env_without_rng_advances_stream(dev):
+  """A hand-built Fetch state without info['rng']: the graph makes the
+  stream a static input, so replays continue it like the eager loop (which
+  starts a zero stream once and carries it)."""
+  from brax_amd import envs
+  from brax_amd.envs.graph import StepGraph
+  B, K = 64, 3
+  env = envs.create('fetch', batch_size=B, episode_length=1000, auto_reset=True, device=dev)
+  st0 = env.reset(np.array([0, 2], np.uint32))
+  info = {k: v for k, v in st0.info.items() if k != 'rng'}
+  st0 = st0.replace(info=info)
+  g = StepGraph(env, st0, K, seed=7)
+  g.replay()
+  out = g.replay()
+  st = st0.replace(info=dict(info, rng=torch.zeros((B,), dtype=torch.int32, device=dev)))
+  ref = _eager(env, st, 2 * K, 7, dev, B, env.action_size)
+  torch.cuda.synchronize()
+  _same(out, ref)
+  assert torch.equal(out.info['rng'], ref.info['rng'])
 
 
 def test_graph_hook_and_exchange_accumulate(dev):

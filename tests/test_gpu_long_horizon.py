@@ -1,0 +1,232 @@
+"""Long-horizon parity: 1,000-step auto-reset rollouts of 4,096 envs, the HIP
+path against Brax's algorithm in fp32 (the oracle's float32 C restatement),
+compared statistically ("Long rollouts are compared
+statistically (mean episode return, x_velocity distributions)"; the
+reference's own long rollouts: `brax/tests/env_test.py:33-75`, 1,000-step
+scans of `env.step`).
+
+Both sides start from the same reset states (the GPU's `bx_env_reset` output,
+copied to the host) and step on the same action stream (each step's
+`bx_uniform` slab, copied to the host), with the reference's Episode +
+AutoReset semantics (`wrappers.py:105-148`; restated in numpy for the oracle
+below). Single steps are gated at the fp32 envelope elsewhere
+(test_gpu_parity.py); over 1,000 steps the two fp32 executions decorrelate
+chaotically, so the gate is on distributions, per env:
+
+* return over the rollout (sum of rewards), per-env mean episode length,
+  per-env mean `x_velocity` metric: means within 3 standard errors
+  (two-sample), and the two-sample Kolmogorov-Smirnov statistic below its
+  alpha = 0.001 critical value 1.95 * sqrt(2 / B);
+* terminations (done without truncation) per env-step: two proportions
+  within 3 standard errors;
+* divergence, over each env's first episode: the steps until the median
+  per-env position error between the two paths passes 1e-4 must be at least
+  half of what separates Brax's own two fp32 roundings (the oracle's plain
+  and FMA-contracted float32 builds) on the same inputs, and the median
+  ratio of the two error curves at most 4: the HIP path may not drift from
+  Brax-fp32 faster than fp32 rounding itself makes Brax drift.
+
+The statistics are written to gpurun_out/long_horizon_<env>.json (committed
+under profiles/).
+"""
+import ctypes as C
+import json
+import os
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import compiled
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+B, T, L = 4096, 1000, 1000
+CASES = {  # env: (obs size, metric count, x_velocity column, action seed)
+    'ant': (87, 10, 7, 21),
+    'humanoid': (240, 9, 6, 22),
+}
+
+
+@pytest.fixture(scope='module')
+def dev():
+  assert torch.cuda.is_available(), 'GPU tests need a GPU'
+  return torch.device('cuda', 0)
+
+
+def ks_stat(a, b):
+  """Two-sample Kolmogorov-Smirnov statistic sup |F_a - F_b|."""
+  a, b = np.sort(a), np.sort(b)
+  grid = np.concatenate([a, b])
+  fa = np.searchsorted(a, grid, side='right') / a.size
+  fb = np.searchsorted(b, grid, side='right') / b.size
+  return float(np.abs(fa - fb).max())
+
+
+def compare(a, b):
+  """Means within 3 SE and the KS statistic vs its alpha = 0.001 critical value."""
+  a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+  se = float(np.sqrt(a.var(ddof=1) / a.size + b.var(ddof=1) / b.size))
+  d = ks_stat(a, b)
+  crit = 1.949 * np.sqrt((a.size + b.size) / (a.size * b.size))
+  return {'mean_hip': float(a.mean()), 'mean_oracle': float(b.mean()), 'se': se,
+          'z': float(abs(a.mean() - b.mean()) / se) if se > 0 else 0.0,
+          'ks': d, 'ks_crit': float(crit)}
+
+
+def episode_stats(reward, done, trunc, xvel):
+  """Per-env statistics of (T, B) rollouts: return, mean episode length,
+  mean x_velocity, and the terminations (done and not truncated)."""
+  reward, done, trunc, xvel = (np.asarray(x, np.float64) for x in (reward, done, trunc, xvel))
+  ret = reward.sum(0)
+  n_done = done.sum(0)
+  # completed episodes per env (the last one ends at step T by truncation
+  # unless it terminated): mean length = T / episodes
+  mean_len = T / np.maximum(n_done, 1)
+  term = (done * (1 - trunc)).sum()
+  return ret, mean_len, xvel.mean(0), float(term)
+
+
+def oracle_rollout(o, name, qp0, acts, O, M, xcol, track=None):
+  """Episode + AutoReset rollout through the oracle (wrappers.py:105-148):
+  steps reset where the previous step was done, the env steps from done = 0,
+  done at steps >= L (truncation = 1 - the env's own done there), done envs
+  back to first_qp. Returns (T, B) reward, done, truncation, x_velocity, and
+  the (T, B, N, 3) positions of the `track` env slice when given."""
+  qp = qp0.copy()
+  first = qp0.copy()
+  steps = np.zeros(qp0.shape[0])
+  done_prev = np.zeros(qp0.shape[0])
+  R, D, TR, X, P = [], [], [], [], []
+  for t in range(acts.shape[0]):
+    steps = np.where(done_prev > 0, 0, steps)
+    nq, _, rew, dn, met = o.env_step(name, qp, acts[t], O, M)
+    steps = steps + 1
+    done = np.where(steps >= L, 1.0, dn)
+    trunc = np.where(steps >= L, 1.0 - dn, 0.0)
+    qp = np.where(done[:, None, None] > 0, first, nq).astype(qp.dtype)
+    R.append(rew)
+    D.append(done)
+    TR.append(trunc)
+    X.append(met[:, xcol])
+    if track is not None:
+      P.append(nq[track, :, 0:3].copy())
+    done_prev = done
+  out = [np.stack(v) for v in (R, D, TR, X)]
+  return out + [np.stack(P) if track is not None else None]
+
+
+def divergence_curve(pa, pb, keep, min_alive=0.25):
+  """Median over the envs still in their first episode (keep (T, envs)) of
+  the per-env max position error, per step; NaN once fewer than min_alive
+  of the envs remain."""
+  err = np.abs(pa - pb).max(axis=(2, 3))  # (T, envs)
+  err = np.where(keep, err, np.nan)
+  alive = keep.mean(1)
+  med = np.full(err.shape[0], np.nan)
+  ok = alive >= min_alive
+  med[ok] = np.nanmedian(err[ok], axis=1)
+  return med
+
+
+def divergence_step(med, thresh=1e-4):
+  """First step whose median error passes thresh (len + 1 if none)."""
+  hit = np.nonzero(np.nan_to_num(med) > thresh)[0]
+  return int(hit[0]) + 1 if hit.size else med.size + 1
+
+
+@pytest.mark.parametrize('name', list(CASES))
+def test_long_horizon_statistics(dev, oracle_lib, name):
+  from brax_amd import _native, envs
+  O, M, xcol, seed = CASES[name]
+  env = envs.create(name, batch_size=B, episode_length=L, auto_reset=True, device=dev)
+  A = env.action_size
+  st = env.reset(np.array([0, 77], np.uint32))
+  qp0 = st.qp.numpy().astype(np.float32)
+  stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+  acts = torch.empty((T, B, A), dtype=torch.float32, device=dev)
+  _native.check(_native.lib().bx_uniform(C.c_void_p(acts.data_ptr()), acts.numel(), seed, 0,
+                                         -1.0, 1.0, stream))
+  rew_g, done_g, tr_g, xv_g = (torch.empty((T, B), device=dev) for _ in range(4))
+  NT = 256  # envs whose positions are tracked for the divergence curve
+  pos_g = torch.empty((T, NT, qp0.shape[1], 3), device=dev)
+  t0 = time.perf_counter()
+  for t in range(T):
+    st = env.step(st, acts[t])
+    rew_g[t] = st.reward
+    done_g[t] = st.done
+    tr_g[t] = st.info['truncation']
+    xv_g[t] = st.metrics['x_velocity']
+    # the pre-reset state is not kept by AutoReset: track envs until their
+    # first done (both sides reset to the same first_qp after it)
+    pos_g[t] = st.qp.pos[:NT]
+  torch.cuda.synchronize()
+  t_gpu = time.perf_counter() - t0
+  hip = [x.cpu().numpy().astype(np.float64) for x in (rew_g, done_g, tr_g, xv_g)]
+  pos_h = pos_g.cpu().numpy().astype(np.float64)
+  acts_h = acts.cpu().numpy()
+  del acts
+
+  _, d, rd, _ = compiled(name)
+  o32 = oracle_lib.Oracle(d, rd, np.float32)
+  t0 = time.perf_counter()
+  track = slice(0, NT)
+  rew_o, done_o, tr_o, xv_o, pos_o = oracle_rollout(o32, name, qp0, acts_h, O, M, xcol, track)
+  t_cpu = time.perf_counter() - t0
+  # Brax's own two fp32 roundings on the tracked envs over the first 300
+  # steps: the divergence yardstick
+  Td = 300
+  ofma = oracle_lib.Oracle(d, rd, np.float32, fma=True)
+  fma = oracle_rollout(ofma, name, qp0[:NT], acts_h[:Td, :NT], O, M, xcol, slice(None))
+  pos_fma = fma[4]
+  # positions after auto-reset are first_qp for both sides; compare the
+  # post-step (pre-reset) positions, which both rollouts record
+  pos_o32 = pos_o[:Td]
+  # the GPU records post-reset positions: mask steps where the GPU or the
+  # oracle reset the env (their pre-reset positions differ by construction)
+  done_any = (hip[1][:Td, :NT] + done_o[:Td, :NT] + fma[1]) > 0
+  first_done = np.where(done_any.any(0), done_any.argmax(0), Td)
+  keep = np.arange(Td)[:, None] < first_done[None, :]
+  med_hip = divergence_curve(pos_h[:Td], pos_o32, keep)
+  med_fma = divergence_curve(pos_fma, pos_o32, keep)
+  div_hip, div_fma = divergence_step(med_hip), divergence_step(med_fma)
+  # the drift ratio where both curves are defined and above the first
+  # step's rounding floor
+  both = np.isfinite(med_hip) & np.isfinite(med_fma) & (med_fma > 0)
+  ratio = float(np.median(med_hip[both] / med_fma[both])) if both.any() else 1.0
+
+  rh, lh, xh, th = episode_stats(*hip)
+  ro, lo, xo, to = episode_stats(rew_o, done_o, tr_o, xv_o)
+  stats = {'env': name, 'envs': B, 'steps': T, 'episode_length': L,
+           'seconds_gpu': t_gpu, 'seconds_oracle_f32': t_cpu,
+           'return': compare(rh, ro), 'episode_length_mean': compare(lh, lo),
+           'x_velocity_mean': compare(xh, xo),
+           'terminations': {'hip': th, 'oracle': to},
+           'divergence_steps_to_1e-4': {'hip_vs_f32': div_hip, 'f32fma_vs_f32': div_fma},
+           'drift_ratio_hip_over_f32fma': ratio,
+           'median_pos_err_hip_vs_f32': [None if np.isnan(x) else float(x) for x in med_hip[:100]],
+           'median_pos_err_f32fma_vs_f32': [None if np.isnan(x) else float(x) for x in med_fma[:100]]}
+  n = float(B * T)
+  p1, p2 = th / n, to / n
+  pp = (th + to) / (2 * n)
+  se = np.sqrt(max(pp * (1 - pp), 1e-30) * 2 / n)
+  stats['terminations']['z'] = float(abs(p1 - p2) / se) if pp > 0 else 0.0
+  for side, dn in (('hip', hip[1]), ('oracle', done_o)):
+    v, c = np.unique(dn.sum(0).astype(np.int64), return_counts=True)
+    stats.setdefault('episodes_per_env_histogram', {})[side] = dict(zip(map(int, v), map(int, c)))
+  os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
+  np.savez_compressed(os.path.join(ROOT, 'gpurun_out', f'long_horizon_{name}.npz'),
+                      done_hip=hip[1].astype(np.uint8), done_oracle=done_o.astype(np.uint8),
+                      ret_hip=rh, ret_oracle=ro)
+  with open(os.path.join(ROOT, 'gpurun_out', f'long_horizon_{name}.json'), 'w') as f:
+    json.dump(stats, f, indent=1)
+  print(json.dumps({k: v for k, v in stats.items() if not k.startswith('median')}))
+  for k in ('return', 'episode_length_mean', 'x_velocity_mean'):
+    s = stats[k]
+    assert s['z'] < 3.0, (k, s)
+    assert s['ks'] < s['ks_crit'], (k, s)
+  assert stats['terminations']['z'] < 3.0, stats['terminations']
+  assert div_hip >= 0.5 * div_fma, stats['divergence_steps_to_1e-4']
+  assert ratio <= 4.0, ratio

@@ -9,13 +9,13 @@ import numpy as np
 import pytest
 
 from tests.conftest import golden
-from tests.helpers import (CAPSULES, NN_MASKED, ENVTRAJ_KERNEL, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS,
+from tests.helpers import (CAPSULES, NN_MASKED, SHORT_SCENES, ENVTRAJ_KERNEL, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS,
                            XCOL, XY_ENVS, env_coef, env_golden, golden_reset_qp, prep_oracle,
                            compiled, env_kind, obs_flags)
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
 SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + NN_MASKED + POINTS
-            + SPRING_ROBOTS + XCOL)
+            + SPRING_ROBOTS + XCOL + SHORT_SCENES)
 
 
 def _oracle(oracle_lib, name, guard=False, dtype=np.float64):
@@ -35,6 +35,10 @@ def test_system_step_matches_reference(oracle_lib, name):
   for t in range(T['action'].shape[0]):
     out, info = o.system_step(T['qp'][t], T['action'][t])
     tol = tol0
+    if name in ('capsule_capsule_s', 'capsule_cull_s'):
+      # states 7-23 steps into a resting stack (contacts chattering at their
+      # gates): float64 rounding order differs by up to 6e-9 there
+      tol = 1e-8
     if name in XCOL:
       # the extended contact functions select among near-ties (SAT argmax
       # over 576 edge pairs, the closest of 4 segment-triangle candidates):
