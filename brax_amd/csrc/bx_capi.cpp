@@ -1118,6 +1118,23 @@ int bx_env_reset(bx_system* S, const bx_env_params* env, int64_t n_envs, uint64_
   r.env_offset = env_offset;
   r.seeds = env_seeds;
   r.scale = noise_scale;
+  r.kind = env->kind;
+  for (int k = 0; k < 8; k++) r.coef[k] = env->coef[k];
+  r.rng_out = out->rng;
+  // the bodies a reset program places must exist (coef holds their indices)
+  auto body_ok = [&](float x) { return x >= 0.f && x < (float)S->hdr.N && x == (float)(int)x; };
+  if ((env->kind == BX_ENV_REACHER || env->kind == BX_ENV_REACHERANGLE) && !body_ok(env->coef[0]))
+    return fail("reacher reset: coef[0] must be the target body");
+  if (env->kind == BX_ENV_PUSHER &&
+      !(body_ok(env->coef[1]) && body_ok(env->coef[2]) && body_ok(env->coef[3])))
+    return fail("pusher reset: coef[1..3] must be the object, goal and table bodies");
+  if (env->kind == BX_ENV_PUSHER && S->hdr.num_joint_dof < 4)
+    return fail("pusher reset: the last 4 dofs get no velocity noise; the system has fewer");
+  if ((env->kind == BX_ENV_UR5E || env->kind == BX_ENV_FETCH) && !body_ok(env->coef[1]))
+    return fail("target env reset: coef[1] must be the target body");
+  if ((env->kind == BX_ENV_UR5E || env->kind == BX_ENV_FETCH || env->kind == BX_ENV_GRASP) &&
+      !out->rng)
+    return fail("the target envs' reset writes their per-env rng stream: out->rng is null");
   HIP_OK(launch_default_qp(n_envs, S->lds_reset, as_stream(stream), r));
   InfoArgs a{};
   a.blob = S->blob;

@@ -4205,17 +4205,41 @@ __global__ void __launch_bounds__(64) default_qp_kernel(ResetArgs A) {
     for (int k = 0; k < 13; k++) q[b * 13 + k] = c.f(H.o_base + b * 13 + k);
   const float* ja = A.gen ? nullptr : A.angle + e * D;
   const float* jv = A.gen ? nullptr : A.vel + e * D;
-  // Env.reset noise (ant.py:200-203): keyed by the global env id
+  // Env.reset draws (gen = 1), keyed by the global env id g (W draws per
+  // env: (seed, g * W + k)) or by the env's own key (seeds[e], k):
+  //   default (ant.py:200-203 ...): qpos = default + U[-s, s) at k = dof,
+  //     qvel = U[-s, s) at k = D + dof (W = 2D)
+  //   REACHER, REACHERANGLE (reacher.py:157-160): qpos noise U[-.1, .1),
+  //     qvel U[-.005, .005), then the target's two draws at 2D, 2D + 1
+  //   PUSHER (pusher.py:178-195): default angles, qvel U[-.005, .005) on the
+  //     first D - 4 dofs (k = dof), the object's two draws at D - 4, D - 3
+  //   UR5E, FETCH (ur5e.py:41-46): default pose at rest, the target's two
+  //     draws at 0, 1;  GRASP (grasp.py:54-70): default pose at rest
+  const int kind = A.gen ? A.kind : 0;
+  int W = 2 * D;
+  float as = A.scale, vs = A.scale;
+  int nvel = D;
+  if (kind == BX_ENV_REACHER || kind == BX_ENV_REACHERANGLE) {
+    W = 2 * D + 2; as = .1f; vs = .005f;
+  } else if (kind == BX_ENV_PUSHER) {
+    W = D - 4 + 2; as = 0.f; vs = .005f; nvel = D - 4;
+  } else if (kind == BX_ENV_UR5E || kind == BX_ENV_FETCH) {
+    W = 2; as = 0.f; vs = 0.f; nvel = 0;
+  } else if (kind == BX_ENV_GRASP) {
+    W = 0; as = 0.f; vs = 0.f; nvel = 0;
+  }
+  const int voff = kind == BX_ENV_PUSHER ? 0 : D;  // pusher's qvel draws come first
   const uint64_t seed = A.seeds ? A.seeds[e] : A.seed;
-  const uint64_t g0 = A.seeds ? 0ull : (uint64_t)(A.env_offset + e) * (uint64_t)(2 * D);
+  const uint64_t g0 = A.seeds ? 0ull : (uint64_t)(A.env_offset + e) * (uint64_t)W;
   for (int f = 0; f < H.n_fk; f++) {
     int o = H.o_fk + f * FK_STRIDE;
     float a3[3], v3_[3];
     for (int l = 0; l < 3; l++) {
       int ix = c.i(o + FK_IDX + l);
       if (A.gen) {
-        a3[l] = ix >= 0 ? c.f(H.o_dangle + ix) + uniform_at(seed, g0 + ix, -A.scale, A.scale) : 0.f;
-        v3_[l] = ix >= 0 ? uniform_at(seed, g0 + D + ix, -A.scale, A.scale) : 0.f;
+        a3[l] = ix < 0 ? 0.f
+                : c.f(H.o_dangle + ix) + (as > 0.f ? uniform_at(seed, g0 + ix, -as, as) : 0.f);
+        v3_[l] = ix >= 0 && ix < nvel ? uniform_at(seed, g0 + voff + ix, -vs, vs) : 0.f;
       } else {
         a3[l] = ix >= 0 ? ja[ix] : 0.f;
         v3_[l] = ix >= 0 ? jv[ix] : 0.f;
@@ -4263,6 +4287,51 @@ __global__ void __launch_bounds__(64) default_qp_kernel(ResetArgs A) {
       q[b * 13 + 1] = q[b * 13 + 1] - zmin * 0.f;
       q[b * 13 + 2] = q[b * 13 + 2] - zmin * 1.f;
     }
+  }
+  // the bodies the env's reset places after default_qp (index_update of
+  // qp.pos, so after the lift): the reachers' target (reacher.py:212-221,
+  // reacherangle.py:102-113: radius .2 u, sqrt(u) for ReacherAngle), the
+  // pusher's object in its .17 disc, goal and table (pusher.py:181-201), the
+  // target envs' target on their ring (ur5e.py:117-125, fetch.py:124-134)
+  const float twopi = 3.14159265358979323846f * 2.f;
+  if (kind == BX_ENV_REACHER || kind == BX_ENV_REACHERANGLE) {
+    const float u0 = uniform_at(seed, g0 + 2 * D, 0.f, 1.f);
+    const float u1 = uniform_at(seed, g0 + 2 * D + 1, 0.f, 1.f);
+    const float dist = .2f * (kind == BX_ENV_REACHERANGLE ? sqrtf(u0) : u0);
+    const float an = twopi * u1;
+    float* t = q + (int)A.coef[0] * 13;
+    t[0] = dist * cosf(an);
+    t[1] = dist * sinf(an);
+    t[2] = .01f;
+  } else if (kind == BX_ENV_PUSHER) {
+    float x = uniform_at(seed, g0 + D - 4, -.3f, 0.f);
+    float y = uniform_at(seed, g0 + D - 3, -.2f, .2f);
+    const float nrm = sqrtf(x * x + y * y);
+    const float sc = nrm > .17f ? .17f / nrm : 1.f;
+    float* ob = q + (int)A.coef[1] * 13;
+    ob[0] = sc * x;
+    ob[1] = sc * y;
+    ob[2] = .05f;
+    float* gl = q + (int)A.coef[2] * 13;
+    gl[0] = .45f; gl[1] = .05f; gl[2] = .05f;
+    float* tb = q + (int)A.coef[3] * 13;
+    tb[0] = 0.f; tb[1] = 0.f; tb[2] = 0.f;
+  } else if (kind == BX_ENV_UR5E || kind == BX_ENV_FETCH) {
+    const float u0 = uniform_at(seed, g0, 0.f, 1.f), u1 = uniform_at(seed, g0 + 1, 0.f, 1.f);
+    const float rr = A.coef[2] + A.coef[3] * u0;
+    const float an = twopi * u1;
+    float* t = q + (int)A.coef[1] * 13;
+    t[0] = rr * cosf(an);
+    t[1] = rr * sinf(an);
+    t[2] = A.coef[4];
+  }
+  // the target envs' per-env stream (info['rng']): a hash of (seed, global
+  // env id), or of the env's own key
+  if (A.rng_out && (kind == BX_ENV_UR5E || kind == BX_ENV_FETCH || kind == BX_ENV_GRASP)) {
+    const uint64_t id = A.seeds ? 0ull : (uint64_t)(A.env_offset + e);
+    int64_t z = (int64_t)(id * 0x9E3779B97F4A7C15ull + (seed & 0x7FFFFFFFFFFFFFFFull));
+    z = (int64_t)((uint64_t)(z ^ (z >> 31)) * 0x94D049BB133111EBull);
+    A.rng_out[e] = (uint32_t)(z ^ (z >> 29));
   }
   for (int b = 0; b < N; b++) store_qp_global(A.out, e, b, q + b * 13);
 }

@@ -57,6 +57,10 @@ struct ResetArgs {
   int64_t env_offset;
   const uint64_t* seeds;
   float scale;
+  // gen = 1: the env kind's reset program (bx_env_reset) and its coef
+  int kind;
+  float coef[8];
+  uint32_t* rng_out;  // UR5E / FETCH / GRASP: the per-env streams (or null)
 };
 
 // SINGLE-mode step kernels (fast-reciprocal translation unit)

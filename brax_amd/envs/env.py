@@ -231,15 +231,17 @@ class PhysicsEnv(Env):
     return self.reset_noise_scale
 
   def reset_batch(self, rng, batch_size, env_offset=None):
-    """Batched `Env.reset` (e.g. `ant.py:198-220`) in one C call,
-    `bx_env_reset`: noise, default_qp, the reset-time Info and the
-    observation on the device.
+    """Batched `Env.reset` (e.g. `ant.py:198-220`, `reacher.py:156-174`,
+    `pusher.py:178-209`, `ur5e.py:41-58`) in one C call, `bx_env_reset`:
+    the env's reset draws, default_qp, the bodies its reset places, the
+    target envs' streams, the reset-time Info and the observation, on the
+    device.
 
-    `rng` is one key (2,) / int: env e draws its noise U[-s, s) from the
-    counter RNG keyed by (rng, global env id env_offset + e). A (B, 2) key
-    batch gives every env its own key (`VmapWrapper.reset`). Parity with JAX
-    threefry is unpinned; the reset itself is pinned through
-    `reset_from` with the same noise (`reset_noise`)."""
+    `rng` is one key (2,) / int: env e draws from the counter RNG keyed by
+    (rng, global env id env_offset + e). A (B, 2) key batch gives every env
+    its own key (`VmapWrapper.reset`). Parity with JAX threefry is unpinned
+    (SURVEY §8(c)); the reset itself is pinned through `reset_from` with the
+    same draws (`reset_noise`)."""
     B = int(batch_size)
     off = self.env_offset if env_offset is None else int(env_offset)
     dev = self.sys.device
@@ -264,13 +266,18 @@ class PhysicsEnv(Env):
     out.steps = base + 8 * B
     out.truncation = base + 12 * B
     out.metrics = met.data_ptr() if self.metric_keys else None
+    rng = None
+    if getattr(self, 'needs_rng', False):  # the target envs' per-env streams
+      rng = torch.empty((B,), dtype=torch.int32, device=dev)
+      out.rng = rng.data_ptr()
     p = self._params()
     _native.check(_native.lib().bx_env_reset(
         self.sys._h, C.byref(p), B, seed, off,
         None if seeds is None else C.c_void_p(seeds.data_ptr()), float(self._noise_scale()),
         C.byref(out), _stream(dev.index)))
     reward, done, _, _ = scal.unbind(0)
-    return State(qp=qp, obs=obs, reward=reward, done=done, metrics=self._metrics(met), info={})
+    return State(qp=qp, obs=obs, reward=reward, done=done, metrics=self._metrics(met),
+                 info={} if rng is None else {'rng': rng})
 
   def reset_noise(self, rng, batch_size, env_offset=None):
     """The (qpos, qvel) that `reset_batch(rng, batch_size)` adds up, drawn

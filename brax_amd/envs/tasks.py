@@ -12,11 +12,11 @@ BX_ENV_REACHER / REACHERANGLE / SWIMMER / PUSHER (`include/brax_amd.h`).
 * Pusher (`pusher.py:170-242`): rewards from the state before the step.
 
 Resets: the reachers draw joint noise and a target in a disc, the pusher
-places its object in a disc and fixes goal and table; these run as a
-default_qp kernel plus a position write and the kernel observation. Noise
-and targets come from the device counter RNG keyed by the reset key (JAX
-threefry parity unpinned); the reset itself is pinned through
-`reset_from`.
+places its object in a disc and fixes goal and table, the target envs place
+their target on a ring and start their per-env streams: all inside
+`bx_env_reset` (the reset kernel's per-kind programs), one C call. The draws
+come from the device counter RNG keyed by the reset key (JAX threefry parity
+unpinned); the reset itself is pinned through `reset_from`.
 """
 import ctypes as C
 import math
@@ -36,6 +36,13 @@ def _uniform(shape, seed, offset, lo, hi, device):
     _native.check(_native.lib().bx_uniform(C.c_void_p(out.data_ptr()), out.numel(), seed,
                                            offset, float(lo), float(hi), _stream(out.device.index)))
   return out
+
+
+def _slab(rng, batch_size, offset, width, lo, hi, device):
+  """The (B, W) draws U(seed, g * W + k, lo, hi) of global envs g = offset..
+  offset + B - 1, exactly as bx_env_reset's reset kernel draws them."""
+  seed = key_to_seed(rng)
+  return _uniform((batch_size, width), seed, offset * width, lo, hi, device)
 
 
 # ---------------------------------------------------------------- constants
@@ -71,10 +78,12 @@ def swimmer_coef(forward_reward_weight=1.0, ctrl_cost_weight=1e-4):
 
 
 def pusher_coef(body_index):
+  """Tip, object, goal (the step program) and table (the reset program)."""
   c = np.zeros(8, np.float64)
   c[0] = body_index['r_wrist_roll_link']
   c[1] = body_index['object']
   c[2] = body_index['goal']
+  c[3] = body_index['table']
   return c
 
 
@@ -112,24 +121,22 @@ class Reacher(_KernelTask):
                              angle=self.kind == 11)
     self._set_sizes()
 
-  def reset_batch(self, rng, batch_size, env_offset=None):
-    """reacher.py:172-186: default angles + U[-.1, .1), velocities
-    U[-.005, .005), a target at U[0, .2) (sqrt for ReacherAngle) x the unit
-    circle, z = .01; keyed by (rng, global env id)."""
-    B = int(batch_size)
+  def reset_draws(self, rng, batch_size, env_offset=None):
+    """The `reset_from` arguments `reset_batch(rng, batch_size)` builds on
+    the device (reacher.py:157-165, reacherangle.py:45-50, _random_target):
+    the same counter draws (W = 2D + 2 per env), the target formed on the
+    host."""
+    B, D, dev = int(batch_size), self.sys.num_joint_dof, self.sys.device
     off = self.env_offset if env_offset is None else int(env_offset)
-    seed = key_to_seed(rng)
-    D = self.sys.num_joint_dof
-    dev = self.sys.device
-    noise = _uniform((B, 2 * D + 2), seed, off * (2 * D + 2), 0., 1., dev)
-    qpos = self.sys.default_angle().reshape(1, -1) + (noise[:, :D] * .2 - .1)
-    qvel = noise[:, D:2 * D] * .01 - .005
-    u = noise[:, 2 * D:]
+    W = 2 * D + 2
+    qpos = self.sys.default_angle().reshape(1, -1) + _slab(rng, B, off, W, -.1, .1, dev)[:, :D]
+    qvel = _slab(rng, B, off, W, -.005, .005, dev)[:, D:2 * D]
+    u = _slab(rng, B, off, W, 0., 1., dev)[:, 2 * D:].double()
     dist = .2 * (torch.sqrt(u[:, 0]) if self.target_sqrt else u[:, 0])
     ang = math.pi * 2. * u[:, 1]
     target = torch.stack([dist * torch.cos(ang), dist * torch.sin(ang),
-                          torch.full_like(dist, .01)], -1)
-    return self.reset_from(qpos, qvel, target)
+                          torch.full_like(dist, .01)], -1).float()
+    return dict(joint_angle=qpos, joint_velocity=qvel, target=target)
 
   def reset_from(self, joint_angle, joint_velocity, target=None):
     qp = self.sys.default_qp(joint_angle=joint_angle, joint_velocity=joint_velocity)
@@ -187,25 +194,21 @@ class Pusher(_KernelTask):
     self.coef = pusher_coef(idx)
     self._set_sizes()
 
-  def reset_batch(self, rng, batch_size, env_offset=None):
-    """pusher.py:178-209: default angles; velocity noise U[-.005, .005) on
-    all but the last 4 dofs; the object at U[-.3, 0) x U[-.2, .2) scaled into
-    a .17 disc, 5 cm up; goal (.45, .05, .05); table at the origin."""
-    B = int(batch_size)
+  def reset_draws(self, rng, batch_size, env_offset=None):
+    """`reset_from` arguments of `reset_batch` (pusher.py:181-195): W = D - 2
+    draws per env, qvel on the first D - 4 dofs, the object's two."""
+    B, D, dev = int(batch_size), self.sys.num_joint_dof, self.sys.device
     off = self.env_offset if env_offset is None else int(env_offset)
-    seed = key_to_seed(rng)
-    D = self.sys.num_joint_dof
-    dev = self.sys.device
-    u = _uniform((B, D + 2), seed, off * (D + 2), 0., 1., dev)
+    W = D - 2
     qvel = torch.zeros((B, D), device=dev)
-    qvel[:, :D - 4] = u[:, :D - 4] * .01 - .005
-    cyl = torch.stack([-.3 + .3 * u[:, D - 4], -.2 + .4 * u[:, D - 3], torch.zeros_like(u[:, 0])],
-                      -1)
-    norm = torch.linalg.norm(cyl, dim=-1, keepdim=True)
-    scale = torch.where(norm > .17, .17 / norm, torch.ones_like(norm))
-    obj = scale * cyl + torch.tensor([0., 0., .05], device=dev)
+    qvel[:, :D - 4] = _slab(rng, B, off, W, -.005, .005, dev)[:, :D - 4]
+    x = _slab(rng, B, off, W, -.3, 0., dev)[:, D - 4].double()
+    y = _slab(rng, B, off, W, -.2, .2, dev)[:, D - 3].double()
+    norm = torch.sqrt(x * x + y * y)
+    sc = torch.where(norm > .17, .17 / norm, torch.ones_like(norm))
+    obj = torch.stack([sc * x, sc * y, torch.full_like(x, .05)], -1).float()
     qpos = self.sys.default_angle().reshape(1, -1).expand(B, -1)
-    return self.reset_from(qpos, qvel, object_pos=obj)
+    return dict(joint_angle=qpos, joint_velocity=qvel, object_pos=obj)
 
   def reset_from(self, joint_angle, joint_velocity, object_pos=None):
     """Reset state from explicit joint angles / velocities and the object's
@@ -254,21 +257,19 @@ class Ur5e(_KernelTask):
     self.coef = target_coef(self.sys.body.index, self.torso, *self.ring)
     self._set_sizes()
 
-  def reset_batch(self, rng, batch_size, env_offset=None):
-    """ur5e.py:59-75: the default pose, a target on the ring."""
-    B = int(batch_size)
+  def reset_draws(self, rng, batch_size, env_offset=None):
+    """`reset_from` arguments of `reset_batch` (ur5e.py:41-46,117-125): the
+    default pose at rest, the target's two draws per env on the ring."""
+    B, D, dev = int(batch_size), self.sys.num_joint_dof, self.sys.device
     off = self.env_offset if env_offset is None else int(env_offset)
-    seed = key_to_seed(rng)
-    u = _uniform((B, 2), seed, off * 2, 0., 1., self.sys.device)
+    u = _slab(rng, B, off, 2, 0., 1., dev).double()
     radius, distance, height = self.ring
     dist = radius + distance * u[:, 0]
     ang = math.pi * 2. * u[:, 1]
     target = torch.stack([dist * torch.cos(ang), dist * torch.sin(ang),
-                          torch.full_like(dist, height)], -1)
-    st = self.reset_from(self.sys.default_angle().reshape(1, -1).expand(B, -1),
-                         torch.zeros((B, self.sys.num_joint_dof), device=self.sys.device), target)
-    st.info['rng'] = rng_streams(seed, off, B, self.sys.device)
-    return st
+                          torch.full_like(dist, height)], -1).float()
+    return dict(joint_angle=self.sys.default_angle().reshape(1, -1).expand(B, -1),
+                joint_velocity=torch.zeros((B, D), device=dev), target=target)
 
   def reset_from(self, joint_angle, joint_velocity, target=None):
     qp = self.sys.default_qp(joint_angle=joint_angle, joint_velocity=joint_velocity)
@@ -342,18 +343,6 @@ class Grasp(_KernelTask):
     p = super()._params(opts, first_qp, first_obs)
     p.act_map = self.act_map.data_ptr() if hasattr(self, 'act_map') else None
     return p
-
-  def reset_batch(self, rng, batch_size, env_offset=None):
-    """grasp.py:54-70: the default pose at rest (the target stays at its
-    configured spot)."""
-    B = int(batch_size)
-    off = self.env_offset if env_offset is None else int(env_offset)
-    D = self.sys.num_joint_dof
-    dev = self.sys.device
-    st = self.reset_from(self.sys.default_angle().reshape(1, -1).expand(B, -1),
-                         torch.zeros((B, D), device=dev))
-    st.info['rng'] = rng_streams(key_to_seed(rng), off, B, dev)
-    return st
 
   def reset_from(self, joint_angle, joint_velocity):
     qp = self.sys.default_qp(joint_angle=joint_angle, joint_velocity=joint_velocity)

@@ -368,25 +368,38 @@ int bx_system_info(bx_system* sys, int64_t n_envs, const bx_qp* qp,
 int bx_env_sizes(bx_system* sys, const bx_env_params* env, int32_t* obs_size,
                  int32_t* n_metrics);
 
-/* Env.reset of the env kinds whose reset is symmetric joint noise (ANT,
- * HUMANOID, HALFCHEETAH, HUMANOID_STANDUP, HOPPER, WALKER2D, the pendulums,
- * ACROBOT, SWIMMER), batched, in two launches (ant.py:198-220,
- * humanoid.py:223-244, half_cheetah.py:164-180, humanoid_standup.py:216-230):
- * for env e (global id g = env_offset + e)
- *   qpos = default_angle + U[-s, s)  counter RNG (seed, g * 2D + k)
- *   qvel =                 U[-s, s)  counter RNG (seed, g * 2D + D + k)
- *   qp   = System.default_qp(qpos, qvel)       (system.py:112-242)
+/* Env.reset of every env kind, batched, in two launches (ant.py:198-220,
+ * humanoid.py:223-244, half_cheetah.py:164-180, humanoid_standup.py:216-230,
+ * reacher.py:156-174, reacherangle.py:44-60, pusher.py:178-209,
+ * ur5e.py:41-58, fetch.py:41-57, grasp.py:54-70). For env e (global id
+ * g = env_offset + e), with D = num_joint_dof and W draws per env, the k-th
+ * draw is the counter RNG at (seed, g * W + k):
+ *   default kinds (W = 2D, s = noise_scale):
+ *     qpos = default_angle + U[-s, s) (k = dof), qvel = U[-s, s) (k = D + dof)
+ *   REACHER, REACHERANGLE (W = 2D + 2): the same with U[-.1, .1) and
+ *     U[-.005, .005); the target (coef[0]) at (d cos a, d sin a, .01) with
+ *     d = .2 u (ReacherAngle .2 sqrt(u)) at k = 2D, a = 2 pi u at k = 2D + 1
+ *   PUSHER (W = D - 2): default angles, qvel U[-.005, .005) on the first
+ *     D - 4 dofs (k = dof); the object (coef[1]) at U[-.3, 0) x U[-.2, .2)
+ *     (k = D - 4, D - 3) scaled into a .17 disc, z = .05; the goal (coef[2])
+ *     at (.45, .05, .05); the table (coef[3]) at the origin
+ *   UR5E, FETCH (W = 2): the default pose at rest; the target (coef[1]) at
+ *     radius coef[2] + coef[3] u (k = 0), angle 2 pi u (k = 1), z = coef[4]
+ *   GRASP: the default pose at rest
+ *   qp   = System.default_qp(qpos, qvel) (system.py:112-242), then the
+ *          placed bodies' positions
  *   obs  = _get_obs(qp, System.info(qp), 0)    (system.py:327-340)
- *   reward = done = metrics = 0; steps = truncation = 0 when given.
- * D = num_joint_dof, s = noise_scale. Keying by global env id makes the
- * states independent of how a batch is sharded over GPUs.
- * env_seeds (device, n_envs uint64, may be NULL) gives every env its own key
- * instead, as `VmapWrapper.reset` over a (B, 2) key batch (wrappers.py:79-80):
- * env e then draws from (env_seeds[e], k) and (env_seeds[e], D + k). The JAX
- * threefry stream itself is parity-unpinned. The params'
- * first_qp / first_obs are not read. The reachers, pusher and the target envs
- * place bodies at reset: their Env.reset is bx_uniform + bx_system_default_qp
- * + the position writes + bx_env_observe (brax_amd/envs/tasks.py). */
+ *   reward = done = metrics = 0; steps = truncation = 0 when given;
+ *   UR5E, FETCH, GRASP: out->rng (required) = the env's stream, a hash of
+ *   (seed, g).
+ * noise_scale is read by the default kinds only (the others' ranges are
+ * fixed by the reference envs). Keying by global env id makes the states
+ * independent of how a batch is sharded over GPUs. env_seeds
+ * (device, n_envs uint64, may be NULL) gives every env its own key instead,
+ * as `VmapWrapper.reset` over a (B, 2) key batch (wrappers.py:79-80): env e
+ * then draws from (env_seeds[e], k) and hashes (env_seeds[e], 0) for its
+ * stream. The JAX threefry stream itself is parity-unpinned.
+ * The params' first_qp / first_obs are not read. */
 int bx_env_reset(bx_system* sys, const bx_env_params* env, int64_t n_envs, uint64_t seed,
                  int64_t env_offset, const uint64_t* env_seeds, float noise_scale,
                  const bx_env_state* out, void* stream);

@@ -24,7 +24,13 @@ ENV_KIND = {'none': 0, 'ant': 1, 'humanoid': 2, 'halfcheetah': 3, 'humanoidstand
 
 
 def build():
-  subprocess.run(['make', '-s', '-C', HERE], check=True)
+  """make, under a file lock: parallel test workers (pytest -n) would
+  otherwise rebuild the same objects concurrently."""
+  import fcntl
+  os.makedirs(os.path.join(HERE, '_build'), exist_ok=True)
+  with open(os.path.join(HERE, '_build', '.lock'), 'w') as lk:
+    fcntl.flock(lk, fcntl.LOCK_EX)
+    subprocess.run(['make', '-s', '-C', HERE], check=True)
 
 
 def _load():

@@ -122,3 +122,77 @@ def test_target_teleport_stream(dev, name):
   # targets that were not hit stay where the physics left them
   np.testing.assert_array_equal(tg[B // 2:], st.qp.pos[B // 2:, g].cpu().numpy())
   assert len(set(map(tuple, np.round(tg[:B // 2], 5)))) == B // 2  # distinct spots
+
+
+@pytest.mark.parametrize('name', ['reacher', 'reacherangle', 'pusher', 'ur5e', 'fetch', 'grasp'])
+def test_body_placing_reset_is_one_call(dev, name):
+  """`bx_env_reset` places the bodies these envs' resets place (reacher.py:
+  156-174, reacherangle.py:44-60, pusher.py:178-209, ur5e.py:41-58,
+  fetch.py:41-57, grasp.py:54-70) and starts the target envs' streams, in
+  the one C call: its state equals the explicit path (`reset_draws`: the
+  same counter draws at the same indices, placements formed on the host in
+  float64, then `reset_from`), the noise bit for bit."""
+  import ctypes as C
+  from brax_amd import abi, _native
+  from brax_amd.envs import tasks
+  from brax_amd.envs import env as env_mod
+  from brax_amd.system import _stream
+  from brax_amd import envs
+  env = envs.get_environment(name, device=dev)
+  B, off = 48, 100
+  key = np.array([3, 17], np.uint32)
+  st = env.reset_batch(key, B, env_offset=off)
+  if name == 'grasp':
+    D = env.sys.num_joint_dof
+    ref = env.reset_from(env.sys.default_angle().reshape(1, -1).expand(B, -1),
+                         torch.zeros((B, D), device=dev))
+  else:
+    ref = env.reset_from(**env.reset_draws(key, B, env_offset=off))
+  torch.cuda.synchronize()
+  for f in ('pos', 'rot', 'vel', 'ang'):
+    a, b = getattr(st.qp, f), getattr(ref.qp, f)
+    assert torch.allclose(a, b, atol=2e-6, rtol=0), (f, float((a - b).abs().max()))
+  # the joint noise is the same draw, bit for bit: rotations and velocities
+  # of the arm come from the same angles
+  assert torch.allclose(st.obs, ref.obs, atol=1e-5, rtol=1e-5)
+  assert float(st.reward.abs().max()) == 0 and float(st.done.abs().max()) == 0
+  if getattr(env, 'needs_rng', False):
+    want = tasks.rng_streams(env_mod.key_to_seed(key), off, B, dev)
+    assert torch.equal(st.info['rng'], want)
+    # the C ABI refuses a target env reset without the stream buffer
+    out = abi.BxEnvState()
+    qp, obs, scal, met = env._alloc(B)
+    out.qp = env_mod.qp_struct(qp, True)
+    out.obs, out.reward, out.done = obs.data_ptr(), scal.data_ptr(), scal.data_ptr() + 4 * B
+    out.metrics = met.data_ptr()
+    p = env._params()
+    rc = _native.lib().bx_env_reset(env.sys._h, C.byref(p), B, 1, 0, None, 0.1, C.byref(out),
+                                    _stream(dev.index))
+    assert rc != 0 and b'rng' in _native.lib().bx_last_error()
+
+
+@pytest.mark.parametrize('name', ['ant', 'reacher', 'pusher', 'ur5e', 'grasp'])
+def test_vmap_reset_uses_each_envs_key(dev, name):
+  """`VmapWrapper.reset` over a (B, 2) key batch (wrappers.py:79-80): env e
+  depends on key e only (its draws and, for the target envs, its stream),
+  equals a one-env reset from that key, and a repeated key repeats the env."""
+  from brax_amd import envs
+  from brax_amd.envs import wrappers
+  env = envs.get_environment(name, device=dev)
+  keys = np.stack([np.array([i, 3 * i + 1], np.uint32) for i in range(16)])
+  st = wrappers.VmapWrapper(env).reset(keys)
+  assert st.qp.pos.shape[0] == 16
+  for e in (0, 5, 15):
+    one = wrappers.VmapWrapper(env).reset(keys[e:e + 1])
+    assert torch.equal(one.qp.pos[0], st.qp.pos[e]) and torch.equal(one.obs[0], st.obs[e])
+    if 'rng' in st.info:
+      assert torch.equal(one.info['rng'][0], st.info['rng'][e])
+  keys2 = keys.copy()
+  keys2[3] = keys2[9]
+  st2 = wrappers.VmapWrapper(env).reset(keys2)
+  assert torch.equal(st2.qp.pos[3], st2.qp.pos[9]) and torch.equal(st2.obs[3], st2.obs[9])
+  if name != 'grasp':  # grasp's reset draws nothing but its stream
+    assert not torch.equal(st.qp.pos[3], st.qp.pos[9])
+  if 'rng' in st.info:
+    assert torch.equal(st2.info['rng'][3], st2.info['rng'][9])
+    assert not torch.equal(st.info['rng'][3], st.info['rng'][9])

@@ -61,25 +61,6 @@ def test_env_reset_matches_explicit_path(dev, name):
   assert torch.equal(one.qp.pos[0], st.qp.pos[7]) and torch.equal(one.obs[0], st.obs[7])
 
 
-def test_vmap_reset_uses_each_envs_key(dev):
-  """`VmapWrapper.reset` over a (B, 2) key batch: env e depends on key e only
-  (wrappers.py:79-80), and equals a single-env reset from that key."""
-  from brax_amd import envs
-  from brax_amd.envs import wrappers
-  env = envs.get_environment('ant', device=dev)
-  keys = np.stack([np.array([i, 3 * i + 1], np.uint32) for i in range(16)])
-  st = wrappers.VmapWrapper(env).reset(keys)
-  assert st.qp.pos.shape[0] == 16
-  assert not torch.equal(st.qp.rot[0], st.qp.rot[1])
-  for e in (0, 5, 15):
-    one = wrappers.VmapWrapper(env).reset(keys[e:e + 1])
-    assert torch.equal(one.qp.rot[0], st.qp.rot[e]) and torch.equal(one.obs[0], st.obs[e])
-  # the same key twice gives the same env
-  keys[3] = keys[9]
-  st2 = wrappers.VmapWrapper(env).reset(keys)
-  assert torch.equal(st2.qp.rot[3], st2.qp.rot[9])
-
-
 def test_ant_32768_shards_reproduce_one_batch(dev, oracle_lib):
   """BASELINE configs[3] (Ant, 32,768 envs over 8 GPUs), rehearsed on one
   GPU: 8 shards of 4,096 envs with env_offset = r * 4096 reset to, and step
