@@ -228,7 +228,9 @@ class PhysicsEnv(Env):
 
   # -------------------------------------------------------------- reset
   def _noise_scale(self):
-    return self.reset_noise_scale
+    # the default kinds' U[-s, s) reset noise; the body-placing kinds' reset
+    # ranges are fixed by their reference envs (bx_env_reset)
+    return getattr(self, 'reset_noise_scale', 0.0)
 
   def reset_batch(self, rng, batch_size, env_offset=None):
     """Batched `Env.reset` (e.g. `ant.py:198-220`, `reacher.py:156-174`,

@@ -70,6 +70,23 @@ def _reset_batch(env, rng, batch_size):
   return env.reset(rng)
 
 
+class _ScaledConfigSystem:
+  """EpisodeWrapper.sys (`wrappers.py:92-95`): the reference deep-copies the
+  env's System and multiplies its *config's* dt and substeps by
+  action_repeat ("for proper video speed"); the copy's integrator keeps the
+  original step. Here: the env's System, with a scaled copy of its config."""
+
+  def __init__(self, sys_, action_repeat):
+    import copy  # pylint: disable=import-outside-toplevel
+    self._sys = sys_
+    self.config = copy.deepcopy(sys_.config)
+    self.config.dt *= action_repeat
+    self.config.substeps *= action_repeat
+
+  def __getattr__(self, name):
+    return getattr(self._sys, name)
+
+
 class EpisodeWrapper(Wrapper):
   """`wrappers.py:83-120`: step counter, truncation and episode-length done."""
 
@@ -77,6 +94,8 @@ class EpisodeWrapper(Wrapper):
     super().__init__(env)
     self.episode_length = episode_length
     self.action_repeat = action_repeat
+    if hasattr(env, 'sys'):
+      self.sys = _ScaledConfigSystem(env.sys, action_repeat)
 
   def _add_counters(self, state):
     z = torch.zeros_like(torch.as_tensor(state.done))

@@ -534,11 +534,13 @@ class stable_top_k:
     self.jp.top_k = self.orig
 
 
-def wrapped_ant(n_envs=8, n_steps=6, episode_length=3):
-  """Episode + AutoReset wrapped Ant (`envs/__init__.py:74-92`)."""
+def wrapped_ant(n_envs=8, n_steps=6, episode_length=3, action_repeat=1):
+  """Episode + AutoReset wrapped Ant (`envs/__init__.py:74-92`); with
+  action_repeat > 1 the EpisodeWrapper scans that many env steps per step
+  and sums their rewards (`wrappers.py:105-120`)."""
   from brax import envs
-  env = envs.create('ant', episode_length=episode_length, auto_reset=True,
-                    batch_size=n_envs)
+  env = envs.create('ant', episode_length=episode_length, action_repeat=action_repeat,
+                    auto_reset=True, batch_size=n_envs)
   st = env.reset(np.array([7, 0], np.uint32))
   out = {k: [] for k in ('qp', 'obs', 'reward', 'done', 'steps', 'truncation')}
   out['first_qp'] = qp_pack(st.info['first_qp'])
@@ -560,6 +562,7 @@ def wrapped_ant(n_envs=8, n_steps=6, episode_length=3):
   r = {k: (np.stack(v) if isinstance(v, list) else v) for k, v in out.items()}
   r['action'] = acts
   r['episode_length'] = np.int32(episode_length)
+  r['action_repeat'] = np.int32(action_repeat)
   return r
 
 
@@ -730,6 +733,8 @@ def main():
       save(f'envtraj_{name}', env_traj(env, name, 8, 4))
   if want('wrap'):
     save('wrap_ant', wrapped_ant())
+  if want('wrap_ar2'):
+    save('wrap_ant_ar2', wrapped_ant(n_steps=6, episode_length=5, action_repeat=2))
   # physics-only rollouts of the other registered envs' systems (their pbd
   # configs): Thruster/Twister forces, frozen bodies, systems without contacts
   for mod, (B, T, aw) in ROBOTS.items():

@@ -226,13 +226,18 @@ def test_reset_vs_golden(dev, oracle_lib, name):
   assert normwise(obs[:, :n_state], T['reset_obs'][:, :n_state]).max() <= 1e-5
 
 
-def test_wrapped_rollout_vs_golden(dev):
+@pytest.mark.parametrize('name', ['wrap_ant', 'wrap_ant_ar2'])
+def test_wrapped_rollout_vs_golden(dev, name):
   """Fused Episode+AutoReset (one launch per step) vs the reference's wrapped
-  `envs.create('ant', episode_length=3, batch_size=8)` rollout."""
+  `envs.create('ant', episode_length=L, action_repeat=R, batch_size=8)`
+  rollout: R = 1, and R = 2 (the kernel's `reps` loop: two env steps per
+  launch, rewards summed, steps advanced by 2; wrappers.py:105-120)."""
   from brax_amd import envs
   from brax_amd.envs.env import State
-  T = golden('wrap_ant')
-  env = envs.create('ant', episode_length=int(T['episode_length']), batch_size=8, device=dev)
+  T = golden(name)
+  ar = int(T['action_repeat']) if 'action_repeat' in T else 1
+  env = envs.create('ant', episode_length=int(T['episode_length']), action_repeat=ar,
+                    batch_size=8, device=dev)
   first_qp = _to_qp(T['first_qp'], dev)
   first_obs = torch.as_tensor(T['first_obs'], dtype=torch.float32, device=dev)
   st = State(qp=_to_qp(T['qp'][0], dev),
@@ -248,9 +253,17 @@ def test_wrapped_rollout_vs_golden(dev):
       tol = 1e-5 if f in ('pos', 'rot') else 2e-4
       assert normwise(got[..., sl], T['qp'][t + 1][..., sl]).max() <= tol, (t, f)
     assert normwise(st.obs.cpu().numpy(), T['obs'][t + 1]).max() <= 2e-4
+    assert np.abs(st.reward.cpu().numpy() - T['reward'][t + 1]).max() <= 1e-4 * ar
     assert np.array_equal(st.done.cpu().numpy(), T['done'][t + 1])
     assert np.array_equal(st.info['steps'].cpu().numpy(), T['steps'][t + 1])
     assert np.array_equal(st.info['truncation'].cpu().numpy(), T['truncation'][t + 1])
+  if ar > 1:  # EpisodeWrapper.sys: the config's dt and substeps scaled (wrappers.py:92-95)
+    w = env
+    while not isinstance(w, __import__('brax_amd.envs.wrappers', fromlist=['x']).EpisodeWrapper):
+      w = w.env
+    assert w.sys.config.dt == pytest.approx(ar * env.unwrapped.sys.config.dt)
+    assert w.sys.config.substeps == ar * env.unwrapped.sys.config.substeps
+    assert w.sys.num_bodies == env.unwrapped.sys.num_bodies
 
 
 def test_full_batch_properties(dev, oracle_lib):

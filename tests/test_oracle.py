@@ -151,19 +151,27 @@ def test_closest_segment_kats(oracle_lib):
     np.testing.assert_allclose(b[0], eb, atol=1.5 * 10**-places)
 
 
-def test_wrapper_semantics(oracle_lib):
+@pytest.mark.parametrize('name', ['wrap_ant', 'wrap_ant_ar2'])
+def test_wrapper_semantics(oracle_lib, name):
   """Episode + AutoReset semantics (wrappers.py:105-148) restated in numpy on
-  top of the oracle's unwrapped env step, vs the reference's wrapped rollout."""
-  T = golden('wrap_ant')
+  top of the oracle's unwrapped env step, vs the reference's wrapped rollout;
+  wrap_ant_ar2: action_repeat 2 (the EpisodeWrapper scans two env steps per
+  step and sums their rewards; steps advance by 2)."""
+  T = golden(name)
   o = _oracle(oracle_lib, 'ant')
   ep = int(T['episode_length'])
+  ar = int(T['action_repeat']) if 'action_repeat' in T else 1
   qp, obs = T['qp'][0], T['obs'][0]
   done = T['done'][0]
   steps = T['steps'][0]
   for t in range(T['action'].shape[0]):
     steps = np.where(done != 0, 0.0, steps)
-    qp1, obs1, rew, d_in, _ = o.env_step('ant', qp, T['action'][t], 87, 10)
-    steps = steps + 1
+    q, rew = qp, 0.0
+    for _ in range(ar):
+      q, obs1, r, d_in, _ = o.env_step('ant', q, T['action'][t], 87, 10)
+      rew = rew + r
+    qp1 = q
+    steps = steps + ar
     done = np.where(steps >= ep, 1.0, d_in)
     trunc = np.where(steps >= ep, 1 - d_in, 0.0)
     sel = done != 0
