@@ -72,6 +72,8 @@ struct Builder {
 int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // A/B knob: BX_NO_JOINT_HALVES=1 keeps one lane per joint
   const bool jh_off = getenv("BX_NO_JOINT_HALVES") && atoi(getenv("BX_NO_JOINT_HALVES"));
+  // A/B switch: BX_NO_R2=1 keeps 17-32-row systems at 32 lanes
+  const bool r2_off = getenv("BX_NO_R2") && atoi(getenv("BX_NO_R2"));
   const int N = d->n_bodies, J = d->n_joints, K = d->n_actuators, R = d->n_rows, G = d->n_groups;
   if (N <= 0) return fail("descriptor has no bodies");
   if (d->dynamics_mode != BX_DYN_PBD && d->dynamics_mode != BX_DYN_LEGACY_SPRING)
@@ -411,11 +413,32 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   }
   H.const_words = (((r ? H.o_base : (int)B.w.size())) + 3) & ~3;
 
+  // the register-hoisted (SINGLE) kernels' shape limits, independent of the
+  // lane count: gather lists of <= 8 entries, <= 2 collider groups per body,
+  // the pbd step without culling or the extended contact functions
+  size_t mx = 0;
+  int max_groups = 0;
+  bool xcol = false;  // extended contact functions run in the item-loop kernel
+  for (int g = 0; g < G; g++) xcol |= d->col_fn[g] >= BX_COL_HEIGHTMAP;
+  for (int b = 0; b < N; b++) {
+    mx = std::max({mx, jl[b].size(), al[b].size(), cl[b].size()});
+    std::vector<int> gs;
+    for (int v : cl[b])
+      if (std::find(gs.begin(), gs.end(), v >> 24) == gs.end()) gs.push_back(v >> 24);
+    max_groups = std::max(max_groups, (int)gs.size());
+  }
+  const bool single_shape = mx <= 8 && max_groups <= 2 && H.n_nn == 0 &&
+                            d->dynamics_mode != BX_DYN_LEGACY_SPRING && !xcol;
   // per-env LDS layout
   int L = std::max({N, J, K, R, 1});
   // an env is one 16/32/64-lane segment of a wave; past 64 items (large
   // scenes) it spreads over a whole 128- or 256-thread workgroup
   L = L <= 16 ? 16 : L <= 32 ? 32 : L <= 64 ? 64 : L <= 128 ? 128 : 256;
+  // 17-32 contact rows and <= 16 bodies / joints / actuators: SINGLE mode at
+  // 16 lanes with two rows per lane (F_R2: rows l and l + 16), not 32 lanes
+  // for the rows alone (HalfCheetah, HumanoidStandup, Fetch)
+  const bool r2 = L == 32 && std::max({N, J, K}) <= 16 && R <= 32 && single_shape && !r2_off;
+  if (r2) L = 16;
   H.L = L;
   int off = 0;
   auto carve = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
@@ -461,22 +484,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // envs 64 words apart: with the odd-multiple record strides, the four
   // envs' records of one ds_read_b128 lane group land on distinct bank slots
   H.env_words = (off + 63) & ~63;
-  size_t mx = 0;
-  int max_groups = 0;
-  bool xcol = false;  // extended contact functions run in the item-loop kernel
-  for (int g = 0; g < G; g++) xcol |= d->col_fn[g] >= BX_COL_HEIGHTMAP;
   {
-    for (int b = 0; b < N; b++) {
-      mx = std::max({mx, jl[b].size(), al[b].size(), cl[b].size()});
-      std::vector<int> gs;
-      for (int v : cl[b])
-        if (std::find(gs.begin(), gs.end(), v >> 24) == gs.end()) gs.push_back(v >> 24);
-      max_groups = std::max(max_groups, (int)gs.size());
-    }
     // the register-hoisted kernel is the pbd step only; legacy_spring systems
     // run the item-loop kernel
-    H.single = (N <= L && J <= L && K <= L && R <= L && mx <= 8 && max_groups <= 2 &&
-                H.n_nn == 0 && !H.spring && !xcol) ? 1 : 0;
+    H.single = (N <= L && J <= L && K <= L && (R <= L || r2) && single_shape) ? 1 : 0;
     // MULTI mode: a pbd scene past one wave (256 threads per env), every
     // lane owning <= 1 body / joint / actuator / task and <= MULTI_MR rows
     size_t mxja = 0;
@@ -648,6 +659,9 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         uint32_t rw[32];
         row_words(l < R ? l : 0, rw);
         for (int k = 0; k < 32; k++) put(l, LI_ROW + k, rw[k]);
+        // F_R2: the lane's second row, l + 16
+        row_words(l + 16 < R ? l + 16 : 0, rw);
+        for (int k = 0; k < 32; k++) put(l, LI_ROW2 + k, rw[k]);
       }
       put_list(l, LI_JL, jl[b], hasB, (uint32_t)(2 * J));
       put_list(l, LI_AL, al[b], hasB, (uint32_t)(2 * K));
@@ -679,6 +693,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     // F_JH (joint halves, SINGLE mode at 16 lanes): <= 8 revolute joints, each
     // driven by the actuator of the same index
     if (H.single && L == 16 && J <= 8 && K <= 8 && H.act_same && !(f & 1) && !jh_off) f |= 128;
+    if (r2) f |= 256;  // F_R2: two contact rows per lane (SINGLE mode, 16 lanes)
     S->feat = f;
     S->fold = (H.act_same && K == J && J > 0 && !(f & 2)) ? 1 : 0;
   }

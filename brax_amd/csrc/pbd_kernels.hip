@@ -222,6 +222,10 @@ enum { F_G1 = 32 };
 // plane, capsule-mesh, box-box SAT), item-loop kernels only. F_GEN: every
 // feature, the item-loop kernels' general instantiation.
 enum { F_X = 64, F_GEN = F_ALL | F_X };
+// F_R2 (outside F_ALL, SINGLE mode at 16 lanes): 17-32 contact rows, lane l
+// owning rows l and l + 16 (its second row's constants from the lane image's
+// LI_ROW2 words)
+enum { F_R2 = 256 };
 template <int F> __device__ __forceinline__ bool is_rev(int type) {
   if constexpr ((F & F_SPH) == 0) return true; else return type == 1;
 }
@@ -299,7 +303,7 @@ __device__ __forceinline__ constexpr int lim_group(int l) {
 // neither: the reference's formulas
 template <int F>
 __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, q4& dpr,
-                            v3& dcp, q4& dcr, const JLim* JL = nullptr,
+                            v3& dcp, q4& dcr, bool useJL = false, JLim JL = JLim{},
                             const uint4* LI = nullptr) {
   // each body rotates three or four of the joint's vectors: one matrix each
   // in the SINGLE-mode TU (the item-loop / MULTI kernels keep rotate():
@@ -338,8 +342,8 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
     v3 axis_c = rc_(J.axc[0]);
     v3 dq1 = cross(axis, axis_c);
     v3 n1;
-    if (JL) {
-      n1 = hinge_turn(axis, ref_p, ref_c, *JL);
+    if (useJL) {
+      n1 = hinge_turn(axis, ref_p, ref_c, JL);
     } else if (LI) {
       n1 = hinge_turn(axis, ref_p, ref_c, ld_lim(LI, LIM_G0));
     } else {
@@ -1179,8 +1183,9 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
 // Torque/Angle.apply_reduced for actuator a (lane) -> aslot
 template <int F>
 __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, const Env& E,
-                                           const float* al, int a, const JLim* JL = nullptr,
-                                           const uint4* LI = nullptr, const v3* tqd = nullptr) {
+                                           const float* al, int a, bool useJL = false,
+                                           JLim JL = JLim{}, const uint4* LI = nullptr,
+                                           const v3* tqd = nullptr) {
   QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
   if (LI && is_torque<F>(A.type)) {
     // torque actuators on the lane image's limit rows: the angles
@@ -1224,15 +1229,15 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
     st_v3a(E.aslot + (E.nK + a) * ASLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
     return;
   }
-  if (JL && is_rev<F>(Jc.type) && is_torque<F>(A.type)) {
+  if (useJL && is_rev<F>(Jc.type) && is_torque<F>(A.type)) {
     // a revolute torque actuator needs its hinge angle only for the limit
     // cut: the test on pseudo-angles (no atan2)
     const v3 axis = rotate(Jc.axp[0], p.rot);
     const v3 ref_p = rotate(Jc.axp[2], p.rot), ref_c = rotate(Jc.axc[2], cq.rot);
     const float pa = pseudo_angle(dot(ref_p, ref_c), dot(cross(ref_p, ref_c), axis));
     float t = al[0] * A.strength * -1.f;
-    if (pa < JL->plo) t = 0.f;
-    if (pa > JL->phi) t = 0.f;
+    if (pa < JL.plo) t = 0.f;
+    if (pa > JL.phi) t = 0.f;
     const v3 tq = mk(0.f, 0.f, 0.f) + axis * t;
     st_v3a(E.aslot + a * ASLOT_STRIDE, mul(Jc.Ip, tq));
     st_v3a(E.aslot + (E.nK + a) * ASLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
@@ -2090,13 +2095,13 @@ __device__ __forceinline__ GList<M> load_glist(const Cst& c, int o_off, int o_l,
 
 template <int M>
 struct Hoist {
-  bool hasB, hasJ, hasA, hasR;
+  bool hasB, hasJ, hasA, hasR, hasR2;
   BodyC B;
   JointC J;
   JLim JL;
   JSide S;
   ActC A;
-  RowC R;
+  RowC R, R2;  // R2: F_R2's second row (lane + 16)
   GList<M> jl, al, cl;
 };
 
@@ -2105,7 +2110,7 @@ struct Hoist {
 // L2 round trip (the records' own layout needs three dependent ones: list
 // offsets -> entries, joint / row -> the bodies it references).
 // JH (joint halves): lanes j and j + 8 both hold joint j and actuator j.
-template <int M, bool JH>
+template <int M, bool JH, bool R2 = false>
 __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& H, int lane,
                                            Hoist<M>& X) {
   const int jx = JH ? (lane & 7) : lane;
@@ -2113,6 +2118,7 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   X.hasJ = jx < H.J;
   X.hasA = jx < H.K;
   X.hasR = lane < H.R;
+  X.hasR2 = R2 && lane + 16 < H.R;
   const uint4* im = reinterpret_cast<const uint4*>(blob + H.o_lane) + lane;
   uint32_t w[LANE_W];
   auto grab = [&](int o, int n) {
@@ -2127,6 +2133,7 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   grab(OJ, 48);
   grab(OA, 8);
   grab(LI_ROW, 32);
+  if constexpr (R2) grab(LI_ROW2, 32);
   grab(LI_JL, M);
   grab(LI_AL, M);
   grab(LI_CL, M);
@@ -2170,27 +2177,30 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
 #pragma unroll
   for (int k = 0; k < 3; k++) X.A.idx[k] = n(OA + LA_IDX + k);
   X.A.strength = f(OA + LA_STR);
-  RowC& R = X.R;
-  R.group = n(LI_ROW + LR_GROUP);
-  R.a = n(LI_ROW + LR_A);
-  R.b = n(LI_ROW + LR_B);
-  R.fn = n(LI_ROW + LR_FN);
-  R.oneway = n(LI_ROW + LR_OW);
-  R.a_pos = f3(LI_ROW + LR_APOS);
-  R.a_end = f3(LI_ROW + LR_AEND);
-  R.a_rad = f(LI_ROW + LR_ARAD);
-  R.b_pos = f3(LI_ROW + LR_BPOS);
-  R.b_end = f3(LI_ROW + LR_BEND);
-  R.b_rad = f(LI_ROW + LR_BRAD);
-  R.fric = f(LI_ROW + LR_FRIC);
-  R.elas = f(LI_ROW + LR_ELAS);
-  R.scale = f(LI_ROW + LR_SCALE);
-  R.thr = f(LI_ROW + LR_THR);
-  R.erp = f(LI_ROW + LR_ERP);
-  R.ma = f(LI_ROW + LR_MA);
-  R.mb = f(LI_ROW + LR_MB);
-  R.Ia = f3(LI_ROW + LR_IA);
-  R.Ib = f3(LI_ROW + LR_IB);
+  auto row = [&](int o, RowC& R) {
+    R.group = n(o + LR_GROUP);
+    R.a = n(o + LR_A);
+    R.b = n(o + LR_B);
+    R.fn = n(o + LR_FN);
+    R.oneway = n(o + LR_OW);
+    R.a_pos = f3(o + LR_APOS);
+    R.a_end = f3(o + LR_AEND);
+    R.a_rad = f(o + LR_ARAD);
+    R.b_pos = f3(o + LR_BPOS);
+    R.b_end = f3(o + LR_BEND);
+    R.b_rad = f(o + LR_BRAD);
+    R.fric = f(o + LR_FRIC);
+    R.elas = f(o + LR_ELAS);
+    R.scale = f(o + LR_SCALE);
+    R.thr = f(o + LR_THR);
+    R.erp = f(o + LR_ERP);
+    R.ma = f(o + LR_MA);
+    R.mb = f(o + LR_MB);
+    R.Ia = f3(o + LR_IA);
+    R.Ib = f3(o + LR_IB);
+  };
+  row(LI_ROW, X.R);
+  if constexpr (R2) row(LI_ROW2, X.R2);
   X.JL = JLim{f(OL + LL_PLO), f(OL + LL_PHI), f(OL + LL_CLO), f(OL + LL_SLO), f(OL + LL_CHI),
                f(OL + LL_SHI)};
   if constexpr (JH) {
@@ -2342,7 +2352,9 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   // 70.5 M env-steps/s): they read the rows from the lane image where they
   // test them (ld_lim), and take the pseudo-angle limit tests for the
   // spherical rows and torque cuts too (Humanoid 75.0 -> 78.9 M)
-  const JLim* JLP = (F & F_SPH) == 0 ? &X.JL : nullptr;
+  // (passed by value: a pointer into X kept the hoisted struct in scratch,
+  // 672-720 B per lane in every revolute kernel without joint halves)
+  constexpr bool JLH = (F & F_SPH) == 0;
   const uint4* LIP = (F & F_SPH) != 0 ? reinterpret_cast<const uint4*>(c.w + H.o_lane) + lane : nullptr;
   const int jx = lane & 7;         // JH: this lane's joint / actuator
   const bool child = lane >= 8;    // JH: this lane's side
@@ -2402,9 +2414,9 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         if (FOLD) {
           const JointC& Jc = X.J;
           const v3 tqd = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
-          act_torque<F>(X.J, A, E, al, lane, JLP, LIP, &tqd);
+          act_torque<F>(X.J, A, E, al, lane, JLH, X.JL, LIP, &tqd);
         } else if (H.act_same) {
-          act_torque<F>(X.J, A, E, al, lane, JLP, LIP);
+          act_torque<F>(X.J, A, E, al, lane, JLH, X.JL, LIP);
         } else {
           JointC Jc = load_joint(c, H, A.joint);
           act_torque<F>(Jc, A, E, al, lane);
@@ -2452,7 +2464,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
         q4 dpr, dcr;
-        joint_apply<F>(Jc, p, cq, dpp, dpr, dcp, dcr, JLP, LIP);
+        joint_apply<F>(Jc, p, cq, dpp, dpr, dcp, dcr, JLH, X.JL, LIP);
         st_slot(E.jslot + lane * SLOT_STRIDE, dpp, dpr, 0.f);
         st_slot(E.jslot + (E.nJ + lane) * SLOT_STRIDE, dcp, dcr, 0.f);
       }
@@ -2479,11 +2491,14 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       sync();
       BX_STAMP(3);
     }
-    // ---- collisions (system.py:288-313)
+    // ---- collisions (system.py:288-313): the lane's row (F_R2: rows lane
+    // and lane + 16), its contact kept in registers until the velocity pass
+    constexpr bool R2 = (F & F_R2) != 0;
     v3 cpos = mk(0.f, 0.f, 0.f), cn = mk(0.f, 0.f, 0.f);
     float pen = 0.f, dl = 0.f;
-    if (X.hasR) {
-      const RowC& R = X.R;
+    v3 cpos2 = mk(0.f, 0.f, 0.f), cn2 = mk(0.f, 0.f, 0.f);
+    float pen2 = 0.f, dl2 = 0.f;
+    auto pos_pass = [&](const RowC& R, int r, v3& cpos, v3& cn, float& pen, float& dl) {
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cvel;
       contact_gen<F>(R, a, b, cpos, cvel, cn, pen);
@@ -2495,13 +2510,17 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       v3 oap, obp;
       q4 oar, obr;
       dl = position_contact<F>(R, a, b, pap, par, pbp, pbr, cpos, cn, pen, oap, oar, obp, obr);
-      float* rd = E.rowd + lane * ROWD_STRIDE;
+      float* rd = E.rowd + r * ROWD_STRIDE;
       st4a(rd, f32x4{cpos.x, cpos.y, cpos.z, cn.x});
       st4a(rd + 4, f32x4{cn.y, cn.z, pen, dl});
-      st_slot(E.cslot + lane * SLOT_STRIDE, oap, oar,
+      st_slot(E.cslot + r * SLOT_STRIDE, oap, oar,
               (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f);
-      st_slot(E.cslot + (E.nR + lane) * SLOT_STRIDE, obp, obr,
+      st_slot(E.cslot + (E.nR + r) * SLOT_STRIDE, obp, obr,
               (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f);
+    };
+    if (X.hasR) pos_pass(X.R, lane, cpos, cn, pen, dl);
+    if constexpr (R2) {
+      if (X.hasR2) pos_pass(X.R2, lane + 16, cpos2, cn2, pen2, dl2);
     }
     sync();
     BX_STAMP(4);
@@ -2518,8 +2537,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     }
     sync();
     BX_STAMP(5);
-    if (X.hasR) {
-      const RowC& R = X.R;
+    auto vel_pass = [&](const RowC& R, int r, v3 cpos, v3 cn, float pen, float dl) {
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 rap, rav, raa, rbp, rbv, rba;
       ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
@@ -2527,10 +2545,14 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       v3 oav, oaa, obv, oba;
       velocity_contact<F>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos, cn, pen, dl, oav, oaa, obv,
                           oba);
-      st_slot(E.cslot + lane * SLOT_STRIDE, oav, q4{oaa.x, oaa.y, oaa.z, 0.f},
+      st_slot(E.cslot + r * SLOT_STRIDE, oav, q4{oaa.x, oaa.y, oaa.z, 0.f},
               (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f);
-      st_slot(E.cslot + (E.nR + lane) * SLOT_STRIDE, obv, q4{oba.x, oba.y, oba.z, 0.f},
+      st_slot(E.cslot + (E.nR + r) * SLOT_STRIDE, obv, q4{oba.x, oba.y, oba.z, 0.f},
               (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f);
+    };
+    if (X.hasR) vel_pass(X.R, lane, cpos, cn, pen, dl);
+    if constexpr (R2) {
+      if (X.hasR2) vel_pass(X.R2, lane + 16, cpos2, cn2, pen2, dl2);
     }
     sync();
     BX_STAMP(6);
@@ -3634,7 +3656,7 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
   zero_slots(E, H, lane);
   // SINGLE: the lane image's loads go out before the state's
   Hoist<M> X;
-  if constexpr (S) load_hoist<M, (F & F_JH) != 0>(A.blob, H, lane, X);
+  if constexpr (S) load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0>(A.blob, H, lane, X);
   for (int b = lane; b < H.N; b += L) {
     if (valid) {
       load_qp_global(A.qin, e, b, E.qp + b * QP_STRIDE);
@@ -3737,7 +3759,7 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
   // (never stored)
   const int64_t el = valid ? e : 0;
   Hoist<M> X;
-  if constexpr (S) load_hoist<M, (F & F_JH) != 0>(A.blob, H, lane, X);
+  if constexpr (S) load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0>(A.blob, H, lane, X);
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
   float done_in = A.in.done[el];
   float steps_in = A.in.steps ? A.in.steps[el] : 0.f;
@@ -4400,8 +4422,21 @@ static void launch_one(void (*k)(Args), dim3 grid, int tpb, size_t lds, hipStrea
     case F_CC | F_TW | F_G1 | F_JH: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW | F_JH, M>, grid, tpb, lds, s, a); break; \
     default: launch_one<ARGS>(KERNEL<16, 1, F_ALL, M>, grid, tpb, lds, s, a); break; \
   }
+// F_R2 systems (17-32 rows at 16 lanes): HalfCheetah (capsule-capsule,
+// two-way, joint halves), Fetch (box corners, one group), HumanoidStandup
+// (spherical, one group), else every feature
+#define BX_SINGLE16_R2(KERNEL, ARGS, M)                                             \
+  switch (feat & ~F_R2) {                                                           \
+    case F_CC | F_TW | F_JH:                                                        \
+    case F_CC | F_TW | F_G1 | F_JH: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW | F_JH | F_R2, M>, grid, tpb, lds, s, a); break; \
+    case F_G1: launch_one<ARGS>(KERNEL<16, 1, F_G1 | F_R2, M>, grid, tpb, lds, s, a); break; \
+    case F_SPH | F_G1: launch_one<ARGS>(KERNEL<16, 1, F_SPH | F_G1 | F_R2, M>, grid, tpb, lds, s, a); break; \
+    default: launch_one<ARGS>(KERNEL<16, 1, F_ALL | F_R2, M>, grid, tpb, lds, s, a); break; \
+  }
 #define BX_DISPATCH_SINGLE(KERNEL, ARGS)                                            \
-  if (L == 16) {                                                                    \
+  if (L == 16 && (feat & F_R2)) {                                                   \
+    if (gw <= 4) { BX_SINGLE16_R2(KERNEL, ARGS, 4) } else { BX_SINGLE16_R2(KERNEL, ARGS, 8) } \
+  } else if (L == 16) {                                                             \
     if (gw <= 4) { BX_SINGLE16(KERNEL, ARGS, 4) } else { BX_SINGLE16(KERNEL, ARGS, 8) } \
   } else if (L == 32) {                                                             \
     launch_one<ARGS>(KERNEL<32, 1, F_ALL, 8>, grid, tpb, lds, s, a);                \
@@ -4452,6 +4487,12 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
   if (fold && L == 16 && gw <= 4 && (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP) &&
       feat == (F_SPH | F_G1)) {
     launch_one<EnvArgs>(env_step_kernel<16, 1, F_SPH | F_G1, 4, EK_HUM>, grid, tpb, lds, s, a);
+    return hipGetLastError();
+  }
+  // HumanoidStandup: the Humanoid system lying down, 22 ground rows (F_R2)
+  if (fold && L == 16 && (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP) &&
+      feat == (F_SPH | F_G1 | F_R2)) {
+    launch_one<EnvArgs>(env_step_kernel<16, 1, F_SPH | F_G1 | F_R2, 8, EK_HUM>, grid, tpb, lds, s, a);
     return hipGetLastError();
   }
   BX_DISPATCH_SINGLE(env_step_kernel, EnvArgs)
