@@ -427,7 +427,15 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       if (std::find(gs.begin(), gs.end(), v >> 24) == gs.end()) gs.push_back(v >> 24);
     max_groups = std::max(max_groups, (int)gs.size());
   }
-  const bool single_shape = mx <= 8 && max_groups <= 2 && H.n_nn == 0 &&
+  // F_C16: a body's contact list may hold up to 16 entries (its joint and
+  // actuator lists <= 8), the SINGLE kernels then gather 16 contact slots
+  size_t mx_ja = 0, mx_c = 0;
+  for (int b = 0; b < N; b++) {
+    mx_ja = std::max({mx_ja, jl[b].size(), al[b].size()});
+    mx_c = std::max(mx_c, cl[b].size());
+  }
+  const bool c16 = mx_c > 8 && mx_c <= 16 && mx_ja <= 8;
+  const bool single_shape = (mx <= 8 || c16) && max_groups <= 2 && H.n_nn == 0 &&
                             d->dynamics_mode != BX_DYN_LEGACY_SPRING && !xcol;
   // per-env LDS layout
   int L = std::max({N, J, K, R, 1});
@@ -487,7 +495,8 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   {
     // the register-hoisted kernel is the pbd step only; legacy_spring systems
     // run the item-loop kernel
-    H.single = (N <= L && J <= L && K <= L && (R <= L || r2) && single_shape) ? 1 : 0;
+    H.single = (N <= L && J <= L && K <= L && (R <= L || r2) && single_shape &&
+                (mx <= 8 || L == 16)) ? 1 : 0;  // F_C16 kernels: 16 lanes
     // MULTI mode: a pbd scene past one wave (256 threads per env), every
     // lane owning <= 1 body / joint / actuator / task and <= MULTI_MR rows
     size_t mxja = 0;
@@ -556,6 +565,25 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // above, so its words are the same bits the item-loop kernels read; a lane
   // without an item of a kind gets item 0's record (as the kernels' clamped
   // index did), and zeros where the system has none of that kind
+  // F_R2: which rows each lane works. Rows of one contact function share a
+  // slot where they fit (HalfCheetah, Pusher: the plane rows in the first,
+  // the capsule-capsule rows in the second), so a pass runs one function per
+  // slot instead of both on every lane; otherwise rows l and l + 16
+  std::vector<int> slot1(16, -1), slot2(16, -1);
+  if (r2) {
+    std::vector<int> pl, other;
+    for (int x = 0; x < R; x++)
+      (d->col_fn[d->row_group[x]] == BX_COL_CAPSULE_PLANE ? pl : other).push_back(x);
+    if (!pl.empty() && !other.empty() && pl.size() <= 16 && other.size() <= 16) {
+      for (size_t i = 0; i < pl.size(); i++) slot1[i] = pl[i];
+      for (size_t i = 0; i < other.size(); i++) slot2[i] = other[i];
+    } else {
+      for (int l = 0; l < 16; l++) {
+        slot1[l] = l < R ? l : -1;
+        slot2[l] = l + 16 < R ? l + 16 : -1;
+      }
+    }
+  }
   if (H.single) {
     B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
     H.o_lane = B.alloc(LANE_W * LANE_IMG_LANES);
@@ -659,9 +687,16 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         uint32_t rw[32];
         row_words(l < R ? l : 0, rw);
         for (int k = 0; k < 32; k++) put(l, LI_ROW + k, rw[k]);
-        // F_R2: the lane's second row, l + 16
-        row_words(l + 16 < R ? l + 16 : 0, rw);
-        for (int k = 0; k < 32; k++) put(l, LI_ROW2 + k, rw[k]);
+        // F_R2: the lane's two rows (slot1[l], slot2[l])
+        if (r2 && l < 16) {
+          const int a = slot1[l], b2 = slot2[l];
+          row_words(a >= 0 ? a : 0, rw);
+          for (int k = 0; k < 32; k++) put(l, LI_ROW + k, rw[k]);
+          row_words(b2 >= 0 ? b2 : 0, rw);
+          for (int k = 0; k < 32; k++) put(l, LI_ROW2 + k, rw[k]);
+          put(l, LI_RIDX, (uint32_t)a);
+          put(l, LI_RIDX + 1, (uint32_t)b2);
+        }
       }
       put_list(l, LI_JL, jl[b], hasB, (uint32_t)(2 * J));
       put_list(l, LI_AL, al[b], hasB, (uint32_t)(2 * K));
@@ -670,6 +705,9 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       uint32_t cz = (uint32_t)(2 * R);
       if (hasB && !cl[b].empty()) cz |= (uint32_t)cl[b][0] & 0x7F000000u;
       put_list(l, LI_CL, cl[b], hasB, cz);
+      // F_C16: entries 8..15 of the contact list
+      for (int k = 0; k < 8; k++)
+        put(l, LI_CL2 + k, hasB && 8 + k < (int)cl[b].size() ? (uint32_t)cl[b][8 + k] : cz);
     }
   }
   H.total_words = (int)B.w.size();
@@ -678,7 +716,9 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   S->hdr = H;
   S->single_ok = H.single != 0;
   S->min_L = L;
-  S->gw = mx <= 4 ? 4 : 8;
+  // gather width of the joint / actuator lists (and the contact list, unless
+  // F_C16 gives it 16)
+  S->gw = (c16 ? mx_ja : mx) <= 4 ? 4 : 8;
   {
     int f = 0;
     for (int j = 0; j < J; j++) if (d->joint_type[j] != BX_JOINT_REVOLUTE) f |= 1;
@@ -694,6 +734,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     // driven by the actuator of the same index
     if (H.single && L == 16 && J <= 8 && K <= 8 && H.act_same && !(f & 1) && !jh_off) f |= 128;
     if (r2) f |= 256;  // F_R2: two contact rows per lane (SINGLE mode, 16 lanes)
+    if (H.single && c16) f |= 512;  // F_C16: 16-entry contact gather lists
     S->feat = f;
     S->fold = (H.act_same && K == J && J > 0 && !(f & 2)) ? 1 : 0;
   }

@@ -226,6 +226,12 @@ enum { F_X = 64, F_GEN = F_ALL | F_X };
 // owning rows l and l + 16 (its second row's constants from the lane image's
 // LI_ROW2 words)
 enum { F_R2 = 256 };
+// F_C16 (outside F_ALL, SINGLE mode): contact gather lists of up to 16
+// entries (Pusher's wrist: 15 rows), the joint / actuator lists <= M
+enum { F_C16 = 512 };
+template <int F, int M> __device__ __forceinline__ constexpr int cl_width() {
+  return (F & F_C16) ? 16 : M;
+}
 template <int F> __device__ __forceinline__ bool is_rev(int type) {
   if constexpr ((F & F_SPH) == 0) return true; else return type == 1;
 }
@@ -2093,16 +2099,18 @@ __device__ __forceinline__ GList<M> load_glist(const Cst& c, int o_off, int o_l,
   return g;
 }
 
-template <int M>
+template <int M, int MC = M>
 struct Hoist {
   bool hasB, hasJ, hasA, hasR, hasR2;
+  int r1, r2;  // the rows R and R2 (F_R2: from the lane image; else r1 = lane)
   BodyC B;
   JointC J;
   JLim JL;
   JSide S;
   ActC A;
-  RowC R, R2;  // R2: F_R2's second row (lane + 16)
-  GList<M> jl, al, cl;
+  RowC R, R2;  // R2: F_R2's second row
+  GList<M> jl, al;
+  GList<MC> cl;
 };
 
 // The lane's hoisted constants from the blob's lane image (pbd_layout.h
@@ -2110,15 +2118,17 @@ struct Hoist {
 // L2 round trip (the records' own layout needs three dependent ones: list
 // offsets -> entries, joint / row -> the bodies it references).
 // JH (joint halves): lanes j and j + 8 both hold joint j and actuator j.
-template <int M, bool JH, bool R2 = false>
+template <int M, bool JH, bool R2 = false, int MC = M>
 __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& H, int lane,
-                                           Hoist<M>& X) {
+                                           Hoist<M, MC>& X) {
   const int jx = JH ? (lane & 7) : lane;
   X.hasB = lane < H.N;
   X.hasJ = jx < H.J;
   X.hasA = jx < H.K;
   X.hasR = lane < H.R;
-  X.hasR2 = R2 && lane + 16 < H.R;
+  X.hasR2 = false;
+  X.r1 = lane;
+  X.r2 = -1;
   const uint4* im = reinterpret_cast<const uint4*>(blob + H.o_lane) + lane;
   uint32_t w[LANE_W];
   auto grab = [&](int o, int n) {
@@ -2133,10 +2143,14 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   grab(OJ, 48);
   grab(OA, 8);
   grab(LI_ROW, 32);
-  if constexpr (R2) grab(LI_ROW2, 32);
+  if constexpr (R2) {
+    grab(LI_ROW2, 32);
+    grab(LI_RIDX, 4);
+  }
   grab(LI_JL, M);
   grab(LI_AL, M);
-  grab(LI_CL, M);
+  grab(LI_CL, MC < 8 ? MC : 8);
+  if constexpr (MC > 8) grab(LI_CL2, 8);
   constexpr int OL = JH ? LI_JLIM_H : LI_JLIM;
   grab(OL, 8);
   if constexpr (JH) grab(LI_SIDE_H, 16);
@@ -2200,7 +2214,13 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
     R.Ib = f3(o + LR_IB);
   };
   row(LI_ROW, X.R);
-  if constexpr (R2) row(LI_ROW2, X.R2);
+  if constexpr (R2) {
+    row(LI_ROW2, X.R2);
+    X.r1 = n(LI_RIDX);
+    X.r2 = n(LI_RIDX + 1);
+    X.hasR = X.r1 >= 0;
+    X.hasR2 = X.r2 >= 0;
+  }
   X.JL = JLim{f(OL + LL_PLO), f(OL + LL_PHI), f(OL + LL_CLO), f(OL + LL_SLO), f(OL + LL_CHI),
                f(OL + LL_SHI)};
   if constexpr (JH) {
@@ -2216,8 +2236,9 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   for (int k = 0; k < M; k++) {
     X.jl.e[k] = n(LI_JL + k);
     X.al.e[k] = n(LI_AL + k);
-    X.cl.e[k] = n(LI_CL + k);
   }
+#pragma unroll
+  for (int k = 0; k < MC; k++) X.cl.e[k] = n(k < 8 ? LI_CL + k : LI_CL2 + k - 8);
 }
 
 template <int M>
@@ -2336,8 +2357,8 @@ __device__ unsigned long long bx_stamp_wave[4096][16];
 // System.step's Info reads.
 template <int L, int F, int M, bool FOLD = false>
 __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
-                                const float* act, int aw, const Hoist<M>& X, v3& icv, v3& ica,
-                                v3& iaa) {
+                                const float* act, int aw, const Hoist<M, cl_width<F, M>()>& X,
+                                v3& icv, v3& ica, v3& iaa) {
 #ifdef BX_STAMPS
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last;
@@ -2518,9 +2539,9 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       st_slot(E.cslot + (E.nR + r) * SLOT_STRIDE, obp, obr,
               (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f);
     };
-    if (X.hasR) pos_pass(X.R, lane, cpos, cn, pen, dl);
+    if (X.hasR) pos_pass(X.R, X.r1, cpos, cn, pen, dl);
     if constexpr (R2) {
-      if (X.hasR2) pos_pass(X.R2, lane + 16, cpos2, cn2, pen2, dl2);
+      if (X.hasR2) pos_pass(X.R2, X.r2, cpos2, cn2, pen2, dl2);
     }
     sync();
     BX_STAMP(4);
@@ -2550,9 +2571,9 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       st_slot(E.cslot + (E.nR + r) * SLOT_STRIDE, obv, q4{oba.x, oba.y, oba.z, 0.f},
               (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f);
     };
-    if (X.hasR) vel_pass(X.R, lane, cpos, cn, pen, dl);
+    if (X.hasR) vel_pass(X.R, X.r1, cpos, cn, pen, dl);
     if constexpr (R2) {
-      if (X.hasR2) vel_pass(X.R2, lane + 16, cpos2, cn2, pen2, dl2);
+      if (X.hasR2) vel_pass(X.R2, X.r2, cpos2, cn2, pen2, dl2);
     }
     sync();
     BX_STAMP(6);
@@ -3655,8 +3676,8 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
   Env E = carve(ebase + le * H.env_words, H, MU);
   zero_slots(E, H, lane);
   // SINGLE: the lane image's loads go out before the state's
-  Hoist<M> X;
-  if constexpr (S) load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0>(A.blob, H, lane, X);
+  Hoist<M, cl_width<F, M>()> X;
+  if constexpr (S) load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>()>(A.blob, H, lane, X);
   for (int b = lane; b < H.N; b += L) {
     if (valid) {
       load_qp_global(A.qin, e, b, E.qp + b * QP_STRIDE);
@@ -3758,8 +3779,8 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
   // first chunk of the action row; an invalid env's lanes read env 0's
   // (never stored)
   const int64_t el = valid ? e : 0;
-  Hoist<M> X;
-  if constexpr (S) load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0>(A.blob, H, lane, X);
+  Hoist<M, cl_width<F, M>()> X;
+  if constexpr (S) load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>()>(A.blob, H, lane, X);
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
   float done_in = A.in.done[el];
   float steps_in = A.in.steps ? A.in.steps[el] : 0.f;
@@ -4426,6 +4447,12 @@ static void launch_one(void (*k)(Args), dim3 grid, int tpb, size_t lds, hipStrea
 // two-way, joint halves), Fetch (box corners, one group), HumanoidStandup
 // (spherical, one group), else every feature
 #define BX_SINGLE16_R2(KERNEL, ARGS, M)                                             \
+  if (feat & F_C16) {                                                               \
+    if ((feat & ~(F_R2 | F_C16 | F_G1)) == (F_CC | F_TW | F_JH))                    \
+      launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW | F_JH | F_R2 | F_C16, M>, grid, tpb, lds, s, a); \
+    else                                                                            \
+      launch_one<ARGS>(KERNEL<16, 1, F_ALL | F_R2 | F_C16, M>, grid, tpb, lds, s, a); \
+  } else                                                                            \
   switch (feat & ~F_R2) {                                                           \
     case F_CC | F_TW | F_JH:                                                        \
     case F_CC | F_TW | F_G1 | F_JH: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW | F_JH | F_R2, M>, grid, tpb, lds, s, a); break; \
@@ -4436,6 +4463,9 @@ static void launch_one(void (*k)(Args), dim3 grid, int tpb, size_t lds, hipStrea
 #define BX_DISPATCH_SINGLE(KERNEL, ARGS)                                            \
   if (L == 16 && (feat & F_R2)) {                                                   \
     if (gw <= 4) { BX_SINGLE16_R2(KERNEL, ARGS, 4) } else { BX_SINGLE16_R2(KERNEL, ARGS, 8) } \
+  } else if (L == 16 && (feat & F_C16)) {                                           \
+    if (gw <= 4) launch_one<ARGS>(KERNEL<16, 1, F_ALL | F_C16, 4>, grid, tpb, lds, s, a); \
+    else launch_one<ARGS>(KERNEL<16, 1, F_ALL | F_C16, 8>, grid, tpb, lds, s, a);     \
   } else if (L == 16) {                                                             \
     if (gw <= 4) { BX_SINGLE16(KERNEL, ARGS, 4) } else { BX_SINGLE16(KERNEL, ARGS, 8) } \
   } else if (L == 32) {                                                             \

@@ -124,8 +124,10 @@ enum {
   LI_JLIM_H = 192,
   LI_SIDE_H = 200,  // joint halves: this lane's side of its joint (LS_*)
   LI_JLIM12 = 216,  // the lane's joint's limit rows 1 and 2 (LL_*, 8 words each; lane j -> joint j)
-  LI_ROW2 = 232,    // F_R2: the lane's second contact row, lane + 16 (LR_*)
-  LANE_W = 264
+  LI_ROW2 = 232,    // F_R2: the lane's second contact row (LR_*)
+  LI_RIDX = 264,    // F_R2: the indices of the lane's two rows (-1: none)
+  LI_CL2 = 268,     // F_C16: contact gather-list entries 8..15
+  LANE_W = 276
 };
 // a joint-halves lane's side (lanes 8-15: the child's): its anchor offset,
 // hinge axis and reference axis in its body's frame, that body's inverse
