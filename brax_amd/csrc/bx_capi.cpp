@@ -570,11 +570,16 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // the capsule-capsule rows in the second), so a pass runs one function per
   // slot instead of both on every lane; otherwise rows l and l + 16
   std::vector<int> slot1(16, -1), slot2(16, -1);
+  bool r2g = false;  // F_R2G: slot 1 one-way capsule-plane, slot 2 two-way capsule-capsule
   if (r2) {
     std::vector<int> pl, other;
     for (int x = 0; x < R; x++)
       (d->col_fn[d->row_group[x]] == BX_COL_CAPSULE_PLANE ? pl : other).push_back(x);
     if (!pl.empty() && !other.empty() && pl.size() <= 16 && other.size() <= 16) {
+      r2g = true;
+      for (int x : pl) r2g &= d->col_oneway[d->row_group[x]] != 0;
+      for (int x : other)
+        r2g &= d->col_fn[d->row_group[x]] == BX_COL_CAPSULE_CAPSULE && !d->col_oneway[d->row_group[x]];
       for (size_t i = 0; i < pl.size(); i++) slot1[i] = pl[i];
       for (size_t i = 0; i < other.size(); i++) slot2[i] = other[i];
     } else {
@@ -735,6 +740,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     if (H.single && L == 16 && J <= 8 && K <= 8 && H.act_same && !(f & 1) && !jh_off) f |= 128;
     if (r2) f |= 256;  // F_R2: two contact rows per lane (SINGLE mode, 16 lanes)
     if (H.single && c16) f |= 512;  // F_C16: 16-entry contact gather lists
+    if (r2g) f |= 1024;             // F_R2G: one contact function per row slot
     S->feat = f;
     S->fold = (H.act_same && K == J && J > 0 && !(f & 2)) ? 1 : 0;
   }

@@ -18,6 +18,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "pbd_launch.h"
 #include "pbd_layout.h"
 #include "pbd_math.h"
@@ -229,6 +231,10 @@ enum { F_R2 = 256 };
 // F_C16 (outside F_ALL, SINGLE mode): contact gather lists of up to 16
 // entries (Pusher's wrist: 15 rows), the joint / actuator lists <= M
 enum { F_C16 = 512 };
+// F_R2G (with F_R2): the host put every one-way capsule-plane row in the
+// lanes' first slot and every two-way capsule-capsule row in the second, so
+// each slot's passes are compiled for its one contact function
+enum { F_R2G = 1024 };
 template <int F, int M> __device__ __forceinline__ constexpr int cl_width() {
   return (F & F_C16) ? 16 : M;
 }
@@ -238,11 +244,16 @@ template <int F> __device__ __forceinline__ bool is_rev(int type) {
 template <int F> __device__ __forceinline__ bool is_torque(int type) {
   if constexpr ((F & F_ANGLE) == 0) return true; else return type == 0;
 }
+// F_CCO (kernel-internal): every row this code path sees is a two-way
+// capsule-capsule row (F_R2G's second slot)
+enum { F_CCO = 2048 };
 template <int F> __device__ __forceinline__ bool is_plane(int fn) {
-  if constexpr ((F & F_CC) == 0) return true; else return fn == 0;
+  if constexpr ((F & F_CCO) != 0) return false;
+  else if constexpr ((F & F_CC) == 0) return true; else return fn == 0;
 }
 template <int F> __device__ __forceinline__ bool is_oneway(int ow) {
-  if constexpr ((F & F_TW) == 0) return true; else return ow != 0;
+  if constexpr ((F & F_CCO) != 0) return false;
+  else if constexpr ((F & F_TW) == 0) return true; else return ow != 0;
 }
 
 // Joint.apply_angle_update (joints.py:130-152): the impulse p of an angular
@@ -2519,10 +2530,16 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     float pen = 0.f, dl = 0.f;
     v3 cpos2 = mk(0.f, 0.f, 0.f), cn2 = mk(0.f, 0.f, 0.f);
     float pen2 = 0.f, dl2 = 0.f;
-    auto pos_pass = [&](const RowC& R, int r, v3& cpos, v3& cn, float& pen, float& dl) {
+    // F_R2G: slot 1 holds only one-way capsule-plane rows, slot 2 only
+    // two-way capsule-capsule rows
+    constexpr bool RG = (F & F_R2G) != 0;
+    constexpr int F1 = RG ? (F & ~(F_CC | F_TW)) : F;
+    constexpr int F2 = RG ? (F | F_CCO) : F;
+    auto pos_pass = [&](auto fc, const RowC& R, int r, v3& cpos, v3& cn, float& pen, float& dl) {
+      constexpr int FS = decltype(fc)::value;
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cvel;
-      contact_gen<F>(R, a, b, cpos, cvel, cn, pen);
+      contact_gen<FS>(R, a, b, cpos, cvel, cn, pen);
       v3 pap, pbp;
       q4 par, pbr;
       float unused;
@@ -2530,7 +2547,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       ld_slot(E.prev + R.b * PREV_STRIDE, pbp, pbr, unused);
       v3 oap, obp;
       q4 oar, obr;
-      dl = position_contact<F>(R, a, b, pap, par, pbp, pbr, cpos, cn, pen, oap, oar, obp, obr);
+      dl = position_contact<FS>(R, a, b, pap, par, pbp, pbr, cpos, cn, pen, oap, oar, obp, obr);
       float* rd = E.rowd + r * ROWD_STRIDE;
       st4a(rd, f32x4{cpos.x, cpos.y, cpos.z, cn.x});
       st4a(rd + 4, f32x4{cn.y, cn.z, pen, dl});
@@ -2539,9 +2556,9 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       st_slot(E.cslot + (E.nR + r) * SLOT_STRIDE, obp, obr,
               (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f);
     };
-    if (X.hasR) pos_pass(X.R, X.r1, cpos, cn, pen, dl);
+    if (X.hasR) pos_pass(std::integral_constant<int, F1>{}, X.R, X.r1, cpos, cn, pen, dl);
     if constexpr (R2) {
-      if (X.hasR2) pos_pass(X.R2, X.r2, cpos2, cn2, pen2, dl2);
+      if (X.hasR2) pos_pass(std::integral_constant<int, F2>{}, X.R2, X.r2, cpos2, cn2, pen2, dl2);
     }
     sync();
     BX_STAMP(4);
@@ -2558,22 +2575,23 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     }
     sync();
     BX_STAMP(5);
-    auto vel_pass = [&](const RowC& R, int r, v3 cpos, v3 cn, float pen, float dl) {
+    auto vel_pass = [&](auto fc, const RowC& R, int r, v3 cpos, v3 cn, float pen, float dl) {
+      constexpr int FS = decltype(fc)::value;
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 rap, rav, raa, rbp, rbv, rba;
       ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
       ld_rb(E.rb + R.b * RB_STRIDE, rbp, rbv, rba);
       v3 oav, oaa, obv, oba;
-      velocity_contact<F>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos, cn, pen, dl, oav, oaa, obv,
-                          oba);
+      velocity_contact<FS>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos, cn, pen, dl, oav, oaa, obv,
+                           oba);
       st_slot(E.cslot + r * SLOT_STRIDE, oav, q4{oaa.x, oaa.y, oaa.z, 0.f},
               (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f);
       st_slot(E.cslot + (E.nR + r) * SLOT_STRIDE, obv, q4{oba.x, oba.y, oba.z, 0.f},
               (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f);
     };
-    if (X.hasR) vel_pass(X.R, X.r1, cpos, cn, pen, dl);
+    if (X.hasR) vel_pass(std::integral_constant<int, F1>{}, X.R, X.r1, cpos, cn, pen, dl);
     if constexpr (R2) {
-      if (X.hasR2) vel_pass(X.R2, X.r2, cpos2, cn2, pen2, dl2);
+      if (X.hasR2) vel_pass(std::integral_constant<int, F2>{}, X.R2, X.r2, cpos2, cn2, pen2, dl2);
     }
     sync();
     BX_STAMP(6);
@@ -4448,12 +4466,16 @@ static void launch_one(void (*k)(Args), dim3 grid, int tpb, size_t lds, hipStrea
 // (spherical, one group), else every feature
 #define BX_SINGLE16_R2(KERNEL, ARGS, M)                                             \
   if (feat & F_C16) {                                                               \
-    if ((feat & ~(F_R2 | F_C16 | F_G1)) == (F_CC | F_TW | F_JH))                    \
+    if ((feat & ~(F_R2 | F_C16 | F_G1 | F_R2G)) == (F_CC | F_TW | F_JH) && (feat & F_R2G)) \
+      launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW | F_JH | F_R2 | F_C16 | F_R2G, M>, grid, tpb, lds, s, a); \
+    else if ((feat & ~(F_R2 | F_C16 | F_G1 | F_R2G)) == (F_CC | F_TW | F_JH))      \
       launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW | F_JH | F_R2 | F_C16, M>, grid, tpb, lds, s, a); \
     else                                                                            \
       launch_one<ARGS>(KERNEL<16, 1, F_ALL | F_R2 | F_C16, M>, grid, tpb, lds, s, a); \
   } else                                                                            \
   switch (feat & ~F_R2) {                                                           \
+    case F_CC | F_TW | F_JH | F_R2G:                                                \
+    case F_CC | F_TW | F_G1 | F_JH | F_R2G: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW | F_JH | F_R2 | F_R2G, M>, grid, tpb, lds, s, a); break; \
     case F_CC | F_TW | F_JH:                                                        \
     case F_CC | F_TW | F_G1 | F_JH: launch_one<ARGS>(KERNEL<16, 1, F_CC | F_TW | F_JH | F_R2, M>, grid, tpb, lds, s, a); break; \
     case F_G1: launch_one<ARGS>(KERNEL<16, 1, F_G1 | F_R2, M>, grid, tpb, lds, s, a); break; \
