@@ -50,6 +50,9 @@ ANT_BYTES_PER_ENV_STEP = 1428
 # F_JH (one collider group per body, joint halves), gather width 4, the Ant
 # env program only (EK_ANT)
 ANT_KERNEL = 'bx::env_step_kernel<16, 1, 160, 4, 1>'
+# the same instantiation under its multi-step name: K-step open-loop rollout
+# launches (bx_env_rollout_packed)
+ANT_ROLLOUT_KERNEL = 'bx::env_rollout_kernel<16, 1, 160, 4, 1>'
 # Counted flops per Ant Env.step (reference numpy path).
 ANT_FLOPS_PER_ENV_STEP = 87382
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8 TB/s HBM3E
@@ -314,6 +317,37 @@ def kernel_train(env, state, act, n=200):
   return a.elapsed_time(b) / n
 
 
+def clone_state(st):
+  """A copy of a graph's output state that outlives the graph's memory pool."""
+  from brax_amd.base import PackedQP, packed_buffer
+  info = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in st.info.items()}
+  return st.replace(qp=PackedQP(packed_buffer(st.qp).clone()), obs=st.obs.clone(),
+                    reward=st.reward.clone(), done=st.done.clone(), info=info)
+
+
+def rollout_train(env, state, k, n=20):
+  """Per-step duration of the open-loop rollout kernel alone: `n`
+  back-to-back `bx_env_rollout_packed` launches of `k` steps (one fixed
+  action block, outputs to one buffer) bracketed by HIP events on their
+  stream, divided by n * k."""
+  from brax_amd.envs.rollout import rollout
+  B = state.qp.pos.shape[0]
+  acts = torch.rand((k, B, env.action_size), device=state.qp.pos.device) * 2 - 1
+  u = env.unwrapped
+  out = torch.empty((k * B * (u.sys.num_bodies * 16 + u.obs_size + 4 + len(u.metric_keys)),),
+                    device=state.qp.pos.device)
+  for _ in range(3):
+    rollout(env, state, acts, out=out)
+  torch.cuda.synchronize()
+  a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+  a.record()
+  for _ in range(n):
+    rollout(env, state, acts, out=out)
+  b.record()
+  torch.cuda.synchronize()
+  return a.elapsed_time(b) / (n * k)
+
+
 def src_sha1():
   """sha1 over the native sources and build files of libbrax_amd.so."""
   import hashlib
@@ -328,9 +362,10 @@ def src_sha1():
   return h.hexdigest()
 
 
-def _rocprof_avg(kernel):
+def _rocprof_avg(kernel, steps_per_launch=1):
   """The committed rocprof average of `kernel` (profiles/rocprof_latest.json),
-  when it was profiled from this exact library build."""
+  when it was profiled from this exact library build, scaled to launches of
+  `steps_per_launch` env steps (the profile records its own launches')."""
   import hashlib
   p = os.path.join(ROOT, 'profiles', 'rocprof_latest.json')
   if not os.path.exists(p):
@@ -345,8 +380,10 @@ def _rocprof_avg(kernel):
   # directories) the exact kernel sources and build flags it was built from
   if not k or (d.get('lib_sha1') != sha and d.get('src_sha1') != src_sha1()):
     return None
-  return {'avg_ms': k['avg_ns'] * 1e-6, 'calls': k.get('calls'), 'source': d.get('source'),
-          'lib_sha1': sha, 'sq': k.get('sq')}
+  per_step = k['avg_ns'] * 1e-6 / k.get('steps_per_launch', 1)
+  return {'avg_ms': per_step * steps_per_launch, 'avg_ms_per_step': per_step,
+          'profiled_steps_per_launch': k.get('steps_per_launch', 1), 'calls': k.get('calls'),
+          'source': d.get('source'), 'lib_sha1': sha, 'sq': k.get('sq')}
 
 
 def main():
@@ -413,7 +450,7 @@ def main():
     state = one_step(state, k)
   # the step kernel alone (its launch train also brings the clocks up before
   # the timed loops)
-  kern_ms = kernel_train(env, state, act)
+  kern_ms = single_ms = kernel_train(env, state, act)
   if exchange is not None:
     exchange.reset()
   torch.cuda.synchronize()
@@ -430,33 +467,21 @@ def main():
   elapsed = time.perf_counter() - t0
   eager_elapsed = elapsed
   eager_collectives = exchange.flushes if exchange is not None else 0
-  # the same loop replayed from a hipGraph: K steps per graph launch (one
-  # draw of the K action slabs, then K x (Env.step + the episodic sum)), the
-  # actions continuing the eager loop's (step, global env id) stream; see
-  # brax_amd/envs/graph.py
+  # the same loop replayed from hipGraphs, the actions continuing the eager
+  # loop's (step, global env id) stream: (1) StepGraph: K steps per graph
+  # launch (one draw of the K action slabs, then K x (Env.step + the episodic
+  # sum)); (2) RolloutGraph: the K steps as ONE open-loop rollout launch
+  # (bx_env_rollout_packed: the state stays on chip between steps, every
+  # step's outputs written; the reference's lax.scan of env.step) after the
+  # one draw. `value` is the faster loop that completed on every rank.
   from brax_amd.envs.graph import StepGraph
-  k0 = args.warmup + args.steps
-  graph_err = None
-  try:
-    g = StepGraph(env, state, K, seed=1, offset=bd.action_offset(rank, B, A, k0, world),
-                  step_stride=world * B * A,
-                  hook=None if exchange is None else (
-                      lambda st: exchange.accumulate(st.reward, st.done)))
-  except Exception as e:  # pylint: disable=broad-except
-    # a failed capture must not sink the run: every rank falls back to the
-    # eager loop's measurement, and the line says so
-    g, graph_err = None, f'{type(e).__name__}: {e}'
-  use_graph = g is not None
-  if dist is not None:
-    f = torch.tensor([int(use_graph)], dtype=torch.int32, device=dev)
-    dist.all_reduce(f, op=dist.ReduceOp.MIN)
-    use_graph = bool(f.item())
-  elapsed = eager_elapsed
-  collectives = eager_collectives
-  if use_graph:
-    # warm replays (the first replay of a fresh graph uploads it)
+  from brax_amd.envs.rollout import RolloutGraph
+
+  def timed_replays(g, advance_hook):
+    """Warm replays, then args.steps // K timed replays (barrier + sync on
+    both sides); the elapsed wall time and the collectives inside it."""
     for _ in range(max(args.warmup // K, 2)):
-      state = g.replay()
+      g.replay()
     if exchange is not None:
       exchange.reset()
     torch.cuda.synchronize()
@@ -465,35 +490,88 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps // K):
-      state = g.replay()
-      if exchange is not None:
-        exchange.advance(K)  # the RCCL all-gather once per period, on the host
+      g.replay()
+      if advance_hook is not None:
+        advance_hook(K)  # the RCCL all-gather once per period, on the host
     torch.cuda.synchronize()
     if dist is not None:
       dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    collectives = exchange.flushes if exchange is not None else 0
+    return time.perf_counter() - t0, (exchange.flushes if exchange is not None else 0)
+
+  def build(kind, st, k0):
+    try:
+      off = bd.action_offset(rank, B, A, k0, world)
+      if kind == 'step':
+        return StepGraph(env, st, K, seed=1, offset=off, step_stride=world * B * A,
+                         hook=None if exchange is None else (
+                             lambda s_: exchange.accumulate(s_.reward, s_.done))), None
+      return RolloutGraph(env, st, K, seed=1, offset=off, step_stride=world * B * A,
+                          hook=None if exchange is None else (
+                              lambda tr: exchange.accumulate_steps(tr.reward, tr.done))), None
+    except Exception as e:  # pylint: disable=broad-except
+      # a failed capture must not sink the run: every rank falls back, and
+      # the line says so
+      return None, f'{type(e).__name__}: {e}'
+
+  def agreed(ok):
+    if dist is None:
+      return ok
+    f = torch.tensor([int(ok)], dtype=torch.int32, device=dev)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN)
+    return bool(f.item())
+
+  adv = None if exchange is None else exchange.advance
+  loops = {'eager': (eager_elapsed, eager_collectives, None)}
+  k0 = args.warmup + args.steps
+  for kind in ('step', 'rollout'):
+    g, err = build(kind, state, k0)
+    if agreed(g is not None):
+      el, col = timed_replays(g, adv)
+      loops[kind] = (el, col, None)
+      k0 += (max(args.warmup // K, 2) + args.steps // K) * K
+      state = clone_state(g._res[0] if kind == 'rollout' else g._out)  # pylint: disable=protected-access
+    else:
+      loops[kind] = (None, 0, err)
+    del g
   if dist is not None:
-    t = torch.tensor([elapsed, eager_elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([loops[k][0] if loops[k][0] is not None else -1.0
+                      for k in ('eager', 'step', 'rollout')], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, eager_elapsed = (float(x) for x in t.tolist())
+    for k, v in zip(('eager', 'step', 'rollout'), t.tolist()):
+      loops[k] = (float(v) if v >= 0 else None,) + loops[k][1:]
+  best = min((k for k in loops if loops[k][0] is not None), key=lambda k: loops[k][0])
+  elapsed, collectives = loops[best][0], loops[best][1]
+  eager_elapsed = loops['eager'][0]
 
   total = B * world * args.steps
   value = total / elapsed
   if rank != 0:
     dist.destroy_process_group()
     return
-  bytes_per_launch = ANT_BYTES_PER_ENV_STEP * B
-  flops_per_launch = ANT_FLOPS_PER_ENV_STEP * B
+  # the dominant kernel of the timed loop: the K-step rollout kernel (one
+  # launch = K x B env-steps) or the single-step kernel (one launch = B
+  # env-steps); achieved = algorithmic flops (bytes) per launch / launch time
+  if best == 'rollout':
+    kname, spl = ANT_ROLLOUT_KERNEL, K
+    kern_ms = rollout_train(env, state, K) * K
+    kern_src = (f'HIP events over 20 back-to-back {K}-step bx_env_rollout_packed launches on '
+                'the launch stream (rollout_train)')
+  else:
+    kname, spl = ANT_KERNEL, 1
+    kern_src = ('HIP events over 200 back-to-back bx_env_step launches on the launch stream '
+                '(kernel_train)')
+  bytes_per_launch = ANT_BYTES_PER_ENV_STEP * B * spl
+  flops_per_launch = ANT_FLOPS_PER_ENV_STEP * B * spl
   tflops = flops_per_launch / (kern_ms * 1e-3) / 1e12
   achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
   # PMC traffic of THIS kernel instantiation (Ant: 16 lanes, SINGLE mode,
-  # feature mask F_G1, gather width 4)
+  # features F_G1 | F_JH, gather width 4), per env-step x the launch's steps
   tr = _traffic()
-  k = ((tr or {}).get('kernels') or {}).get(ANT_KERNEL)
-  traffic = k['hbm_bytes_per_launch'] if k and k.get('batch') == B else None
-  rp = _rocprof_avg(ANT_KERNEL)
+  k = ((tr or {}).get('kernels') or {}).get(kname)
+  traffic = (k['hbm_bytes_per_launch'] / k.get('steps_per_launch', 1) * spl
+             if k and k.get('batch') == B else None)
+  rp = _rocprof_avg(kname, spl)
   sq = (rp or {}).get('sq') or {}
   out = {
       'metric': 'env-steps/sec (Ant, 4096 envs/GPU)',
@@ -517,11 +595,14 @@ def main():
               'config with device-RNG joint noise keyed by global env id',
       'config': {'workload': 'Ant-v1 Env.step (10 PBD substeps + obs/reward + '
                              'Episode/AutoReset), envs.create(ant)',
-                 'launch': (f'hipGraph replays of {K} captured steps (one on-device draw of '
-                            f'the {K} action slabs, then per step the fused Env.step kernel + '
-                            'the episodic sum when N>1)' if use_graph
-                            else f'eager Python loop (graph capture failed: {graph_err})'),
+                 'launch': {
+                     'rollout': f'hipGraph replays of one on-device draw of {K} action slabs + '
+                                f'one {K}-step open-loop rollout launch (bx_env_rollout_packed)',
+                     'step': f'hipGraph replays of one on-device draw of {K} action slabs + {K} '
+                             'fused Env.step launches (+ the episodic sum per step when N>1)',
+                     'eager': 'a Python loop of bx_uniform + Env.step per step'}[best],
                  'envs_per_gpu': B, 'episode_length': 1000, 'substeps': 10,
+                 'steps_per_launch': K if best != 'eager' else 1,
                  'parallelism': f'env-shard x{world}',
                  'exchange_period': period if world > 1 else None},
       # RCCL all-gathers of the episodic (reward, done) sums inside the timed
@@ -533,9 +614,10 @@ def main():
       'roofline': {'bound': 'valu', 'achieved': tflops, 'peak': FP32_VALU_PEAK_TFLOPS,
                    'unit': 'TFLOP/s', 'frac': tflops / FP32_VALU_PEAK_TFLOPS,
                    'traffic': traffic,
-                   'kernel': ANT_KERNEL, 'kernel_ms': kern_ms,
-                   'kernel_ms_source': 'HIP events over 200 back-to-back bx_env_step launches '
-                                       'on the launch stream (kernel_train)',
+                   'kernel': kname, 'kernel_ms': kern_ms, 'steps_per_launch': spl,
+                   'kernel_ms_per_step': kern_ms / spl,
+                   'kernel_ms_source': kern_src,
+                   'single_step_kernel_ms': single_ms,
                    # the SQ issue view of the same kernel (committed counters of
                    # this library build): VALU instructions x 4 cycles / wave cycles
                    'valu_issue_frac': sq.get('valu_issue_frac'),
@@ -547,9 +629,12 @@ def main():
   }
   # the same steps from the plain Python loop (one Env.step call per step):
   # host-bound on a slow host, hence the graph above
-  out['eager_loop'] = {'value': total / eager_elapsed, 'unit': 'env-steps/s',
-                       'ms_per_step': eager_elapsed * 1e3 / args.steps,
-                       'collectives_in_timed_region': eager_collectives}
+  # every loop's rate (value is the fastest); a loop that failed says why
+  for kind, key in (('eager', 'eager_loop'), ('step', 'graph_loop'), ('rollout', 'rollout_loop')):
+    el, col, err = loops[kind]
+    out[key] = ({'value': total / el, 'unit': 'env-steps/s', 'ms_per_step': el * 1e3 / args.steps,
+                 'collectives_in_timed_region': col} if el is not None else {'error': err})
+  out['timed_loop'] = best
   out['secondary_configs'] = None if args.no_secondary else secondary_configs(dev)
   out['phase_roofline'] = (None if args.no_phases else
                            phase_bench(env.unwrapped.sys, dev, args.phase_envs))

@@ -45,6 +45,10 @@ _SIGS = {
     'bx_env_step_packed': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64, C.c_void_p,
                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
                             C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
+    'bx_env_rollout_packed': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64, C.c_int32,
+                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                               C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                               C.c_void_p], C.c_int),
     'bx_env_sizes': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.POINTER(C.c_int32),
                       C.POINTER(C.c_int32)], C.c_int),
     'bx_env_reset': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64, C.c_uint64, C.c_int64,

@@ -1014,9 +1014,12 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   return 0;
 }
 
-int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx_env_state* in,
-                const float* act, int64_t act_stride, int64_t act_width, const bx_env_state* out,
-                void* stream) {
+// bx_env_step over n_steps consecutive steps in one launch (bx_env_rollout_packed):
+// step t reads act + t * act_step and writes the out pointers + t * out_step
+static int env_step_impl(bx_system* S, const bx_env_params* env, int64_t n_envs,
+                         const bx_env_state* in, const float* act, int64_t act_stride,
+                         int64_t act_width, const bx_env_state* out, void* stream,
+                         int32_t n_steps, int64_t act_step, int64_t out_step, int64_t rng_step) {
   if (!S || !env || !in || !out) return fail("null argument");
   DEVICE_SCOPE(S);
   if (check_env(S, env)) return 1;
@@ -1044,6 +1047,10 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   a.act = act;
   a.act_stride = act_stride;
   a.act_width = act_width;
+  a.n_steps = n_steps;
+  a.act_step = act_step;
+  a.out_step = out_step;
+  a.rng_step = rng_step;
   if (S->mode == 1)
     HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a, S->fold));
   else if (S->mode == 3)  // MULTI-mode systems step envs with the item-loop kernel
@@ -1054,10 +1061,17 @@ int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx
   return 0;
 }
 
-int bx_env_step_packed(bx_system* S, const bx_env_params* env, int64_t n_envs,
-                       const float* qp_in, const float* done_in, const float* steps_in,
-                       const uint32_t* rng_in, const float* act, int64_t act_stride,
-                       int64_t act_width, float* out, uint32_t* rng_out, void* stream) {
+int bx_env_step(bx_system* S, const bx_env_params* env, int64_t n_envs, const bx_env_state* in,
+                const float* act, int64_t act_stride, int64_t act_width, const bx_env_state* out,
+                void* stream) {
+  return env_step_impl(S, env, n_envs, in, act, act_stride, act_width, out, stream, 1, 0, 0, 0);
+}
+
+static int env_step_packed(bx_system* S, const bx_env_params* env, int64_t n_envs, int32_t n_steps,
+                           const float* qp_in, const float* done_in, const float* steps_in,
+                           const uint32_t* rng_in, const float* act, int64_t act_stride,
+                           int64_t act_step, int64_t act_width, float* out, uint32_t* rng_out,
+                           void* stream) {
   if (!S || !env) return fail("null argument");
   if (n_envs <= 0) {
     if (check_env(S, env)) return 1;
@@ -1090,7 +1104,30 @@ int bx_env_step_packed(bx_system* S, const bx_env_params* env, int64_t n_envs,
   o.truncation = p + 3 * B;
   o.metrics = env->n_metrics > 0 ? p + 4 * B : nullptr;
   o.rng = rng_out;
-  return bx_env_step(S, env, n_envs, &in, act, act_stride, act_width, &o, stream);
+  // one step's output block: qp | obs | reward, done, steps, truncation | metrics
+  const int64_t block = B * (N * 16 + env->obs_size + 4 + env->n_metrics);
+  return env_step_impl(S, env, n_envs, &in, act, act_stride, act_width, &o, stream, n_steps,
+                       act_step, block, B);
+}
+
+int bx_env_step_packed(bx_system* S, const bx_env_params* env, int64_t n_envs,
+                       const float* qp_in, const float* done_in, const float* steps_in,
+                       const uint32_t* rng_in, const float* act, int64_t act_stride,
+                       int64_t act_width, float* out, uint32_t* rng_out, void* stream) {
+  return env_step_packed(S, env, n_envs, 1, qp_in, done_in, steps_in, rng_in, act, act_stride, 0,
+                         act_width, out, rng_out, stream);
+}
+
+int bx_env_rollout_packed(bx_system* S, const bx_env_params* env, int64_t n_envs, int32_t n_steps,
+                          const float* qp_in, const float* done_in, const float* steps_in,
+                          const uint32_t* rng_in, const float* act, int64_t act_stride,
+                          int64_t act_step_stride, int64_t act_width, float* out,
+                          uint32_t* rng_out, void* stream) {
+  if (n_steps < 0) return fail("negative n_steps");
+  if (n_steps == 0) return S && env ? check_env(S, env) : fail("null argument");
+  if (act_step_stride < 0) return fail("negative action step stride");
+  return env_step_packed(S, env, n_envs, n_steps, qp_in, done_in, steps_in, rng_in, act,
+                         act_stride, act_step_stride, act_width, out, rng_out, stream);
 }
 
 int bx_system_info(bx_system* S, int64_t n_envs, const bx_qp* qp, const bx_info* info, void* stream) {

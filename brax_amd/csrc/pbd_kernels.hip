@@ -3773,9 +3773,15 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
 
 
 
-// Env.step fused with EpisodeWrapper/AutoResetWrapper (wrappers.py:105-148)
+// Env.step fused with EpisodeWrapper/AutoResetWrapper (wrappers.py:105-148),
+// for A.n_steps consecutive steps (bx_env_rollout_packed; 1 for bx_env_step):
+// step t reads its action rows at act + t * act_step and writes its outputs at
+// the output pointers + t * out_step (the rng stream at + t * rng_step); its
+// input state is step t - 1's output, kept in LDS (the AutoReset select
+// reloads first_qp there), so the lane image, the state and the per-env
+// scalars are loaded once per launch, not once per step
 template <int L, int MODE, int F, int M, int EK = EK_ANY>
-__global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
+__device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   BX_KSTAMP_DECL
   extern __shared__ __attribute__((aligned(16))) float smem[];
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
@@ -3790,7 +3796,6 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
   zero_slots(E, H, lane);
   const bx_env_params& P = A.P;
   const int kind = P.kind;
-  const float* act = valid ? A.act + e * A.act_stride : nullptr;
   const int aw = (int)A.act_width;
   // every load first, with clamped (unconditional) addresses so their
   // latencies overlap: the lane image, the per-env scalars, the state and the
@@ -3803,6 +3808,8 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
   float done_in = A.in.done[el];
   float steps_in = A.in.steps ? A.in.steps[el] : 0.f;
   if (!valid) done_in = steps_in = 0.f;
+  // the target envs' per-env stream (advanced by one per env step)
+  uint32_t rng_c = (A.in.rng && valid) ? A.in.rng[e] : 0u;
   constexpr int C = L < 64 ? L : 64;  // action-row chunk: one element per lane
   const float* arow_g = A.act + el * A.act_stride;
   float a0 = 0.f;
@@ -3825,6 +3832,24 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
         for (int k = 0; k < 13; k++) s[k] = k == 3 ? 1.f : 0.f;
       }
     }
+  }
+  const int nst = A.n_steps > 1 ? A.n_steps : 1;
+  for (int t = 0; t < nst; t++) {
+  const float* act = valid ? A.act + e * A.act_stride + t * A.act_step : nullptr;
+  if (t > 0) {
+    arow_g = A.act + el * A.act_stride + t * A.act_step;
+    if (aw > 0 && lane < C) a0 = arow_g[lane < aw ? lane : aw - 1];
+  }
+  // this step's outputs
+  bx_env_state O = A.out;
+  if (t > 0) {
+    const int64_t os = t * A.out_step;
+    O.qp.pos.ptr += os; O.qp.rot.ptr += os; O.qp.vel.ptr += os; O.qp.ang.ptr += os;
+    O.obs += os; O.reward += os; O.done += os;
+    if (O.metrics) O.metrics += os;
+    if (O.steps) O.steps += os;
+    if (O.truncation) O.truncation += os;
+    if (O.rng) O.rng += t * A.rng_step;
   }
   // the action row through LDS: its first act_read words stay staged (arow:
   // every index an actuator or force reads, jp.take clipping into the row),
@@ -3849,7 +3874,7 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
   }
   esync<L>();
   float steps = 0.f;
-  if (valid && A.in.steps) steps = (P.auto_reset && done_in != 0.f) ? 0.f : steps_in;
+  if (valid && (A.in.steps || t > 0)) steps = (P.auto_reset && done_in != 0.f) ? 0.f : steps_in;
   float done = P.auto_reset ? 0.f : done_in;
   float reward_sum = 0.f;
   const int reps = P.episode_length > 0 ? (P.action_repeat > 0 ? P.action_repeat : 1) : 1;
@@ -3937,13 +3962,13 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
     // (its launch requires fold), so its observation takes the lane's
     // hoisted body, joint and actuator
     env_observe<L, EK>(c, H, E, lane, kind, P.obs_flags, P.obs_size, act, aw,
-                   valid ? A.out.obs + e * P.obs_size : nullptr, P.coef, S ? &X.J : nullptr,
+                   valid ? O.obs + e * P.obs_size : nullptr, P.coef, S ? &X.J : nullptr,
                    S ? &X.B : nullptr, (S && EK == EK_HUM) ? &X.A : nullptr);
     BX_KSTAMP(12);
     // reward / done / metrics (lane 0 of the env)
     if (lane == 0 && valid) {
       const float dt = H.dt;
-      float* m = A.out.metrics ? A.out.metrics + e * P.n_metrics : nullptr;
+      float* m = O.metrics ? O.metrics + e * P.n_metrics : nullptr;
       v3 p1 = ld3(E.qp);
       float reward = 0.f;
       if (KIND_IS(BX_ENV_ANT)) {
@@ -4083,8 +4108,8 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
         }
         // one draw per env step (action repeats included), as the reference
         // splits its key once per step
-        const uint32_t key = A.in.rng[e] + (uint32_t)rep;
-        if (rep == reps - 1) A.out.rng[e] = key + 1u;
+        const uint32_t key = rng_c + (uint32_t)rep;
+        if (rep == reps - 1) O.rng[e] = key + 1u;
         if (hit != 0.f) {
           float u0 = uniform_at(key, 0, 0.f, 1.f), u1 = uniform_at(key, 1, 0.f, 1.f);
           float rr = P.coef[2] + P.coef[3] * u0;
@@ -4121,8 +4146,8 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
         reward = mto + close + touch + 5.f * hit + mtt;
         // sorted: closeToObject, hits, movingObjectToTarget, movingToObject, touchingObject
         if (m) { m[0] = close; m[1] = hit; m[2] = mtt; m[3] = mto; m[4] = touch; }
-        const uint32_t key = A.in.rng[e] + (uint32_t)rep;
-        if (rep == reps - 1) A.out.rng[e] = key + 1u;
+        const uint32_t key = rng_c + (uint32_t)rep;
+        if (rep == reps - 1) O.rng[e] = key + 1u;
         if (hit != 0.f) {
           float u0 = uniform_at(key, 0, 0.f, 1.f), u1 = uniform_at(key, 1, 0.f, 1.f);
           float u2 = uniform_at(key, 2, 0.f, 1.f);
@@ -4152,7 +4177,6 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
     esync<L>();
   }
   BX_KSTAMP(13);
-  if (!valid) return;
   done = E.red[0];
   float trunc = 0.f;
   bool reset_now = false;
@@ -4164,26 +4188,52 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
     trunc = steps >= ep ? 1.f - d_inner : 0.f;
   }
   if (P.auto_reset) reset_now = done != 0.f;
-  if (lane == 0) {
-    A.out.reward[e] = reward_sum;
-    A.out.done[e] = done;
-    if (A.out.steps) A.out.steps[e] = steps;
-    if (A.out.truncation) A.out.truncation[e] = trunc;
-  }
-  if (reset_now) {
-    for (int b = lane; b < H.N; b += L) {
-      float tmp[13];
-      load_qp_global(P.first_qp, e, b, tmp);
-      store_qp_global(A.out.qp, e, b, tmp);
+  if (valid) {
+    if (lane == 0) {
+      O.reward[e] = reward_sum;
+      O.done[e] = done;
+      if (O.steps) O.steps[e] = steps;
+      if (O.truncation) O.truncation[e] = trunc;
     }
-    for (int i = lane; i < P.obs_size; i += L) A.out.obs[e * P.obs_size + i] = P.first_obs[e * P.obs_size + i];
-  } else {
-    for (int b = lane; b < H.N; b += L) store_qp_global(A.out.qp, e, b, E.qp + b * QP_STRIDE);
+    if (reset_now) {
+      for (int b = lane; b < H.N; b += L) {
+        float tmp[13];
+        load_qp_global(P.first_qp, e, b, tmp);
+        store_qp_global(O.qp, e, b, tmp);
+        // the next step starts from the reset state
+        if (t + 1 < nst) {
+          float* s = E.qp + b * QP_STRIDE;
+#pragma unroll
+          for (int k = 0; k < 13; k++) s[k] = tmp[k];
+        }
+      }
+      for (int i = lane; i < P.obs_size; i += L) O.obs[e * P.obs_size + i] = P.first_obs[e * P.obs_size + i];
+    } else {
+      for (int b = lane; b < H.N; b += L) store_qp_global(O.qp, e, b, E.qp + b * QP_STRIDE);
+    }
   }
+  // the next step's input scalars: this step's outputs
+  done_in = done;
+  steps_in = steps;
+  rng_c += (uint32_t)reps;
+  esync<L>();
+  }  // steps
   BX_KSTAMP(14);
 }
 
 
+
+template <int L, int MODE, int F, int M, int EK = EK_ANY>
+__global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
+  env_step_body<L, MODE, F, M, EK>(A);
+}
+// the same body under its own name for multi-step launches of the
+// benchmarked envs' kernels (bx_env_rollout_packed), so a profile tells
+// K-step launches from single steps
+template <int L, int MODE, int F, int M, int EK = EK_ANY>
+__global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_rollout_kernel(EnvArgs A) {
+  env_step_body<L, MODE, F, M, EK>(A);
+}
 
 // System.info contact part + optional Env._get_obs of the same state (reset)
 template <int L>
@@ -4533,12 +4583,18 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
   // (their kernels fold each joint's damping into its actuator's slot: fold
   // = every joint j has torque actuator j)
   if (fold && L == 16 && gw <= 4 && k == BX_ENV_ANT && feat == (F_G1 | F_JH)) {
-    launch_one<EnvArgs>(env_step_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
+    if (a.n_steps > 1)
+      launch_one<EnvArgs>(env_rollout_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
+    else
+      launch_one<EnvArgs>(env_step_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
     return hipGetLastError();
   }
   if (fold && L == 16 && gw <= 4 && (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP) &&
       feat == (F_SPH | F_G1)) {
-    launch_one<EnvArgs>(env_step_kernel<16, 1, F_SPH | F_G1, 4, EK_HUM>, grid, tpb, lds, s, a);
+    if (a.n_steps > 1)
+      launch_one<EnvArgs>(env_rollout_kernel<16, 1, F_SPH | F_G1, 4, EK_HUM>, grid, tpb, lds, s, a);
+    else
+      launch_one<EnvArgs>(env_step_kernel<16, 1, F_SPH | F_G1, 4, EK_HUM>, grid, tpb, lds, s, a);
     return hipGetLastError();
   }
   // HumanoidStandup: the Humanoid system lying down, 22 ground rows (F_R2)

@@ -22,6 +22,11 @@ struct EnvArgs {
   bx_env_state in, out;
   const float* act;
   int64_t act_stride, act_width;
+  // consecutive env steps per launch (bx_env_rollout_packed; <= 1: one step):
+  // step t's action rows at act + t * act_step, its outputs at the out
+  // pointers + t * out_step floats (rng + t * rng_step)
+  int32_t n_steps;
+  int64_t act_step, out_step, rng_step;
 };
 struct InfoArgs {
   const uint32_t* blob;

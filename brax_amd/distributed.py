@@ -85,6 +85,13 @@ class EpisodeExchange:
       self.acc[0].add_(reward.float())
       self.acc[1].add_(done.float())
 
+  def accumulate_steps(self, reward, done):
+    """A rollout's K steps at once: (K, B) rewards and dones summed over the
+    steps into the sums (the device half of K calls; the float sum's order
+    is torch's reduction, not step by step)."""
+    self.acc[0].add_(reward.sum(0))
+    self.acc[1].add_(done.sum(0))
+
   def reset(self):
     """Zeroes the sums and the step count (e.g. at the start of a timed
     region, so its exchange periods start there)."""

@@ -1,0 +1,234 @@
+"""Open-loop rollouts: K `Env.step`s in ONE kernel launch.
+
+The reference collects trajectories by scanning `env.step` under `jit`
+(`brax/training/acting.py:53-77`, `generate_unroll`: `jax.lax.scan` of
+`actor_step`); when the actions are known up front (random-action rollouts,
+replayed action sequences, the reference notebook's benchmark loop) the scan
+is open-loop. `rollout(env, state, actions)` runs that scan through
+`bx_env_rollout_packed`: one launch steps every env K times, the state held on
+chip between steps, and writes every step's complete output (state, obs,
+reward, done, episode counters, metrics, the target envs' streams) to HBM -
+bit for bit the outputs of K chained `env.step` calls
+(`tests/test_gpu_rollout.py`).
+"""
+import ctypes as C
+import dataclasses
+from typing import Any, Optional, Tuple
+
+import torch
+
+from brax_amd import _native
+from brax_amd.base import PackedQP, packed_buffer
+from brax_amd.envs.env import PhysicsEnv, State, Wrapper, _f32, _Metrics
+from brax_amd.system import _stream
+
+
+@dataclasses.dataclass(frozen=True)
+class Trajectory:
+  """Every step of a rollout, leading axis K (steps) then B (envs):
+  qp (K, B, N, 16) packed (pos 0:3, rot 3:7, vel 7:10, ang 10:13), obs
+  (K, B, O), reward / done / steps / truncation (K, B), metrics (K, B, M)
+  with `metric_keys` naming the columns, rng (K, B) for the target envs."""
+  qp: Any
+  obs: Any
+  reward: Any
+  done: Any
+  steps: Any
+  truncation: Any
+  metrics: Any
+  metric_keys: Tuple[str, ...]
+  rng: Optional[Any] = None
+
+
+def chain_options(env):
+  """The PhysicsEnv under a wrapper chain and the options the fused kernel
+  applies for it: EpisodeWrapper (episode_length, action_repeat),
+  AutoResetWrapper (auto_reset); Vector / Vmap wrappers pass through.
+  Other wrappers have no fused form: NotImplementedError."""
+  from brax_amd.envs import wrappers  # pylint: disable=import-outside-toplevel
+  opts = {}
+  w = env
+  while isinstance(w, Wrapper):
+    if isinstance(w, wrappers.EpisodeWrapper):
+      opts['episode_length'] = w.episode_length
+      opts['action_repeat'] = w.action_repeat
+    elif isinstance(w, wrappers.AutoResetWrapper):
+      opts['auto_reset'] = True
+    elif not isinstance(w, (wrappers.VectorWrapper, wrappers.VmapWrapper)):
+      raise NotImplementedError(f'{type(w).__name__} has no fused rollout')
+    w = w.env
+  if not isinstance(w, PhysicsEnv):
+    raise NotImplementedError(f'{type(w).__name__} is not a kernel env')
+  return w, opts
+
+
+def rollout(env, state: State, actions, out: Optional[torch.Tensor] = None
+            ) -> Tuple[State, Trajectory]:
+  """K consecutive `env.step(state, actions[t])` in one launch.
+
+  Args:
+    env: an env from `brax_amd.envs.create` (Episode / AutoReset / Vector
+      wrappers over a kernel env).
+    state: the state to start from (a batch of B envs).
+    actions: (K, B, A) float32 on the env's device (any strides with a
+      unit last-axis stride).
+    out: optional flat float32 buffer of K * B * (N*16 + O + 4 + M) floats
+      for the trajectory (reused across calls by graph captures).
+  Returns:
+    (the state after the K-th step, the Trajectory of all K steps); the
+    state's tensors are views into the trajectory's last step.
+  """
+  u, opts = chain_options(env)
+  dev = u.sys.device
+  qbuf = packed_buffer(state.qp)
+  if qbuf is None:
+    qbuf = torch.zeros(state.qp.pos.shape[:-1] + (16,), dtype=torch.float32, device=dev)
+    for lo, f in ((0, state.qp.pos), (3, state.qp.rot), (7, state.qp.vel), (10, state.qp.ang)):
+      qbuf[..., lo:lo + f.shape[-1]] = f
+  if qbuf.dtype != torch.float32 or not qbuf.is_cuda or not qbuf.is_contiguous():
+    qbuf = qbuf.contiguous().float()
+  B = qbuf.shape[0]
+  act = actions
+  if type(act) is not torch.Tensor or act.dtype != torch.float32 or not act.is_cuda:
+    act = torch.as_tensor(act, dtype=torch.float32, device=dev)
+  if act.dim() != 3 or act.shape[1] != B or act.shape[2] != u.action_size:
+    raise ValueError(f'actions {tuple(act.shape)} != (K, {B}, {u.action_size})')
+  if act.stride(-1) != 1:
+    act = act.contiguous()
+  K = act.shape[0]
+  auto = bool(opts.get('auto_reset'))
+  info_in = state.info
+  first_qp = info_in.get('first_qp') if auto else None
+  first_obs = info_in.get('first_obs') if auto else None
+  if auto and (first_qp is None or first_obs is None):
+    raise ValueError('AutoResetWrapper state lacks first_qp / first_obs')
+  p = u._cached_params(opts, first_qp, first_obs)  # pylint: disable=protected-access
+  done_in = _f32(state.done, dev)
+  steps_in = info_in.get('steps')
+  if steps_in is not None:
+    steps_in = _f32(steps_in, dev)
+  rng_in = info_in.get('rng')
+  if rng_in is None and getattr(u, 'needs_rng', False):
+    rng_in = torch.zeros((B,), dtype=torch.int32, device=dev)
+  N, O, M = u.sys.num_bodies, u.obs_size, len(u.metric_keys)
+  block = B * (N * 16 + O + 4 + M)
+  if out is None:
+    out = torch.empty((K * block,), dtype=torch.float32, device=dev)
+  elif out.numel() < K * block or out.dtype != torch.float32 or not out.is_contiguous():
+    raise ValueError(f'out must hold {K * block} contiguous float32')
+  rng_out = torch.empty((K, B), dtype=torch.int32, device=dev) if rng_in is not None else None
+  _native.check(_native.lib().bx_env_rollout_packed(
+      u.sys._h, C.byref(p), B, K, qbuf.data_ptr(), done_in.data_ptr(),  # pylint: disable=protected-access
+      None if steps_in is None else steps_in.data_ptr(),
+      None if rng_in is None else rng_in.data_ptr(), act.data_ptr(), act.stride(1),
+      act.stride(0), act.shape[2], out.data_ptr(),
+      None if rng_out is None else rng_out.data_ptr(), _stream(dev.index)))
+  blocks = out[:K * block].view(K, block)
+  q, obs, sc, met = torch.split(blocks, (B * N * 16, B * O, 4 * B, B * M), dim=1)
+  q = q.view(K, B, N, 16)
+  obs = obs.view(K, B, O)
+  sc = sc.view(K, 4, B)
+  met = met.view(K, B, M)
+  traj = Trajectory(qp=q, obs=obs, reward=sc[:, 0], done=sc[:, 1], steps=sc[:, 2],
+                    truncation=sc[:, 3], metrics=met, metric_keys=tuple(u.metric_keys),
+                    rng=rng_out)
+  info = dict(info_in)
+  if p.episode_length > 0:
+    info['steps'] = sc[K - 1, 2]
+    info['truncation'] = sc[K - 1, 3]
+  if rng_out is not None:
+    info['rng'] = rng_out[K - 1]
+  keys = u.metric_keys
+  m_in = state.metrics
+  extra = m_in.carried(keys) if type(m_in) is _Metrics else {
+      k: v for k, v in m_in.items() if k not in keys}
+  final = State(qp=PackedQP(q[K - 1]), obs=obs[K - 1], reward=sc[K - 1, 0], done=sc[K - 1, 1],
+                metrics=_Metrics(met[K - 1] if M else None, keys, extra), info=info)
+  return final, traj
+
+
+class RolloutGraph:
+  """`rollout` of K steps with on-device action draws, captured as one HIP
+  graph: per replay ONE `bx_uniform_slabs` launch draws the K action slabs
+  (slab t at `offset + (r * K + t) * step_stride`, the eager loop's
+  `bx_uniform` offsets, as `StepGraph` draws them), ONE
+  `bx_env_rollout_packed` launch steps every env K times, and the K-th state
+  is fed back into the graph's static inputs. `hook(traj)` (device work
+  only) is recorded after the rollout, e.g. the episodic (reward, done) sum
+  over the K steps. `replay()` returns (state after the K-th step,
+  trajectory), valid until the next replay."""
+
+  def __init__(self, env, state: State, k: int, seed: int = 1, offset: int = 0,
+               step_stride: Optional[int] = None, lo: float = -1.0, hi: float = 1.0,
+               hook=None):
+    from brax_amd.envs.graph import _static  # pylint: disable=import-outside-toplevel
+    if k < 1:
+      raise ValueError(f'k must be >= 1, got {k}')
+    u, _ = chain_options(env)
+    dev = u.sys.device
+    self.env, self.k, self.device = env, int(k), dev
+    buf = packed_buffer(state.qp)
+    B = (buf if buf is not None else state.qp.pos).shape[0]
+    A = env.action_size
+    stride = B * A if step_stride is None else int(step_stride)
+    if buf is None:
+      buf = torch.zeros(state.qp.pos.shape[:-1] + (16,), dtype=torch.float32, device=dev)
+      for lo_, f in ((0, state.qp.pos), (3, state.qp.rot), (7, state.qp.vel), (10, state.qp.ang)):
+        buf[..., lo_:lo_ + f.shape[-1]] = f
+    self._qp = _static(buf)
+    self._done = _static(state.done)
+    info = dict(state.info)
+    self._steps = _static(info.get('steps'))
+    rng = info.get('rng')
+    if rng is None and getattr(u, 'needs_rng', False):
+      rng = torch.zeros((B,), dtype=torch.int32, device=dev)
+    self._rng = _static(rng)
+    if self._steps is not None:
+      info['steps'] = self._steps
+    if self._rng is not None:
+      info['rng'] = self._rng
+    self._in = State(qp=PackedQP(self._qp), obs=state.obs, reward=state.reward,
+                     done=self._done, metrics=state.metrics, info=info)
+    self._acts = torch.empty((self.k, B, A), dtype=torch.float32, device=dev)
+    N, O, M = u.sys.num_bodies, u.obs_size, len(u.metric_keys)
+    self._out = torch.empty((self.k * B * (N * 16 + O + 4 + M),), dtype=torch.float32,
+                            device=dev)
+    self._epoch = torch.zeros((1,), dtype=torch.int64, device=dev)
+    lib = _native.lib()
+
+    def body(hook=hook):
+      _native.check(lib.bx_uniform_slabs(
+          C.c_void_p(self._acts.data_ptr()), B * A, self.k, seed, offset, stride,
+          C.c_void_p(self._epoch.data_ptr()), self.k * stride, lo, hi, _stream(dev.index)))
+      st, tr = rollout(env, self._in, self._acts, out=self._out)
+      if hook is not None:
+        hook(tr)
+      self._qp.copy_(packed_buffer(st.qp))
+      self._done.copy_(st.done)
+      if self._steps is not None:
+        self._steps.copy_(st.info['steps'])
+      if self._rng is not None:
+        self._rng.copy_(st.info['rng'])
+      self._epoch.add_(1)
+      return st, tr
+
+    with torch.cuda.device(dev):
+      statics = [t for t in (self._qp, self._done, self._steps, self._rng) if t is not None]
+      snap = [t.clone() for t in statics]
+      side = torch.cuda.Stream(dev)
+      side.wait_stream(torch.cuda.current_stream(dev))
+      with torch.cuda.stream(side):
+        body(hook=None)
+      torch.cuda.current_stream(dev).wait_stream(side)
+      for dst, src in zip(statics, snap):
+        dst.copy_(src)
+      self._epoch.zero_()
+      self.graph = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(self.graph, capture_error_mode='thread_local'):
+        self._res = body()
+      torch.cuda.current_stream(dev).synchronize()
+
+  def replay(self):
+    """Steps every env K steps forward; returns (state, trajectory)."""
+    self.graph.replay()
+    return self._res

@@ -353,6 +353,23 @@ int bx_env_step_packed(bx_system* sys, const bx_env_params* env, int64_t n_envs,
                        const uint32_t* rng_in, const float* act, int64_t act_stride,
                        int64_t act_width, float* out, uint32_t* rng_out, void* stream);
 
+/* n_steps consecutive bx_env_step_packed calls in ONE launch: an open-loop
+ * rollout (the reference's `jax.lax.scan` of `env.step`, e.g.
+ * training/acting.py:53-77 generate_unroll, with the actions known up front:
+ * random-action rollouts). Step t reads its action rows at act + t *
+ * act_step_stride (row stride act_stride) and writes its whole output - qp
+ * (B,N,16) | obs (B,O) | reward | done | steps | truncation (B each) |
+ * metrics (B,M) - as block t of `out` (block = B * (N*16 + O + 4 + M)
+ * floats), its rng stream (target envs) at rng_out + t * B; its input state
+ * is step t - 1's output (step 0: qp_in, done_in, steps_in, rng_in). Every
+ * step's outputs are bit-identical to the chained single-step calls; the
+ * state stays on chip between steps (ABI 9). */
+int bx_env_rollout_packed(bx_system* sys, const bx_env_params* env, int64_t n_envs,
+                          int32_t n_steps, const float* qp_in, const float* done_in,
+                          const float* steps_in, const uint32_t* rng_in, const float* act,
+                          int64_t act_stride, int64_t act_step_stride, int64_t act_width,
+                          float* out, uint32_t* rng_out, void* stream);
+
 /* Batched System.default_qp from per-env joint angles/velocities
  * (B, num_joint_dof) contiguous (system.py:112-242). */
 int bx_system_default_qp(bx_system* sys, int64_t n_envs,

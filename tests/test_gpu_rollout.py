@@ -1,0 +1,117 @@
+"""Open-loop rollouts (`brax_amd.envs.rollout.rollout`, one
+`bx_env_rollout_packed` launch for K steps) against K chained `env.step`
+calls on the same actions: every step's state, observation, reward, done,
+episode counters, metrics and per-env stream must be bit-identical, across
+auto-resets (short episodes), action repeats and every kernel family (the
+SINGLE kernels at one and two rows per lane, the item loops, the env
+programs with pre-step actions and per-env streams)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def dev():
+  assert torch.cuda.is_available(), 'GPU tests need a GPU'
+  return torch.device('cuda', 0)
+
+
+def _check(env, st0, acts):
+  from brax_amd.envs.rollout import rollout
+  final, tr = rollout(env, st0, acts)
+  st = st0
+  for t in range(acts.shape[0]):
+    st = env.step(st, acts[t])
+    q = torch.cat([st.qp.pos, st.qp.rot, st.qp.vel, st.qp.ang], -1)
+    assert torch.equal(tr.qp[t][..., :13], q), t
+    assert torch.equal(tr.obs[t], st.obs), t
+    assert torch.equal(tr.reward[t], st.reward), t
+    assert torch.equal(tr.done[t], st.done), t
+    if 'steps' in st.info:
+      assert torch.equal(tr.steps[t], st.info['steps']), t
+      assert torch.equal(tr.truncation[t], st.info['truncation']), t
+    for i, k in enumerate(tr.metric_keys):
+      assert torch.equal(tr.metrics[t][:, i], st.metrics[k]), (t, k)
+    if 'rng' in st.info:
+      assert torch.equal(tr.rng[t], st.info['rng']), t
+  assert torch.equal(final.qp.pos, st.qp.pos) and torch.equal(final.obs, st.obs)
+  assert torch.equal(final.done, st.done)
+  return tr
+
+
+@pytest.mark.parametrize('name,B,K,ep,ar', [
+    ('ant', 256, 12, 5, 1), ('ant', 64, 9, 4, 2), ('humanoid', 128, 10, 6, 1),
+    ('humanoidstandup', 64, 6, 4, 1), ('halfcheetah', 64, 8, 3, 1), ('pusher', 32, 5, 3, 1),
+    ('fetch', 64, 7, 3, 1), ('grasp', 32, 5, 3, 1), ('reacherangle', 64, 8, 3, 1),
+    ('swimmer', 64, 8, 3, 1), ('hopper', 64, 12, 4, 1), ('ur5e', 64, 6, 3, 2)])
+def test_rollout_matches_chained_steps(dev, name, B, K, ep, ar):
+  from brax_amd import envs
+  env = envs.create(name, batch_size=B, episode_length=ep, action_repeat=ar, auto_reset=True,
+                    device=dev)
+  st0 = env.reset(np.array([2, 9], np.uint32))
+  g = torch.Generator(device='cpu').manual_seed(4)
+  acts = (torch.rand((K, B, env.action_size), generator=g) * 2 - 1).to(dev)
+  tr = _check(env, st0, acts)
+  assert float(tr.done.sum()) > 0  # the episodes ended inside the rollout
+  torch.cuda.synchronize()
+
+
+def test_rollout_without_wrappers_and_strided_actions(dev):
+  """No Episode / AutoReset wrappers (the bare env), and a (K, B, A) view
+  with a padded row stride."""
+  from brax_amd import envs
+  env = envs.create('ant', batch_size=64, episode_length=None, auto_reset=False, device=dev)
+  st0 = env.reset(np.array([1, 1], np.uint32))
+  base = (torch.rand((6, 64, 10), device=dev) * 2 - 1)
+  acts = base[..., :8]
+  assert acts.stride(1) == 10
+  _check(env, st0, acts)
+
+
+def test_rollout_full_batch_ant(dev):
+  """BASELINE configs[1]'s batch: 4,096 Ant envs, 20 steps in one launch."""
+  from brax_amd import envs
+  env = envs.create('ant', batch_size=4096, episode_length=1000, auto_reset=True, device=dev)
+  st0 = env.reset(np.array([0, 0x5EED], np.uint32))
+  acts = torch.rand((20, 4096, 8), device=dev) * 2 - 1
+  _check(env, st0, acts)
+
+
+def test_rollout_graph_matches_eager_loop(dev):
+  """RolloutGraph replays (one slab draw + one rollout launch per K steps)
+  step on the eager loop's bits: bx_uniform at action_offset(rank, B, A,
+  step, world) per step, env.step per step (rank 1 of a world of 2)."""
+  import ctypes as C
+  from brax_amd import _native, envs
+  from brax_amd import distributed as bd
+  from brax_amd.envs.rollout import RolloutGraph
+  B, K, world, rank, k0 = 128, 5, 2, 1, 3
+  env = envs.create('ant', batch_size=B, episode_length=7, auto_reset=True, device=dev)
+  A = env.action_size
+  bd.shard_env(env, rank, B)
+  st0 = env.reset(np.array([0, 4], np.uint32))
+  acc = torch.zeros((2, B), device=dev)
+
+  def hook(tr):
+    acc[0].add_(tr.reward.sum(0))
+    acc[1].add_(tr.done.sum(0))
+  g = RolloutGraph(env, st0, K, seed=3, offset=bd.action_offset(rank, B, A, k0, world),
+                   step_stride=world * B * A, hook=hook)
+  for _ in range(2):
+    out, tr = g.replay()
+  act = torch.empty((B, A), dtype=torch.float32, device=dev)
+  st = st0
+  done_sum = torch.zeros((B,), device=dev)
+  for k in range(2 * K):
+    _native.check(_native.lib().bx_uniform(
+        C.c_void_p(act.data_ptr()), B * A, 3, bd.action_offset(rank, B, A, k0 + k, world),
+        -1.0, 1.0, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    st = env.step(st, act)
+    done_sum += st.done
+  torch.cuda.synchronize()
+  assert torch.equal(out.qp.pos, st.qp.pos) and torch.equal(out.obs, st.obs)
+  assert torch.equal(out.info['steps'], st.info['steps'])
+  assert torch.equal(tr.done[K - 1], st.done)
+  assert torch.equal(acc[1], done_sum)  # 0 / 1 sums are exact in any order

@@ -24,7 +24,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ENV_STEP_B = {
     'bx::env_step_kernel<16, 1, 160, 4, 1>': 1428,  # Ant: N=10, A=8, O=87
     'bx::env_step_kernel<16, 1, 33, 4, 2>': 2284,   # Humanoid: N=12, A=17, O=240
+    # the same per env-step, K steps per launch (bx_env_rollout_packed)
+    'bx::env_rollout_kernel<16, 1, 160, 4, 1>': 1428,
+    'bx::env_rollout_kernel<16, 1, 33, 4, 2>': 2284,
 }
+
+
+def rollout_steps(d):
+  """Env steps per rollout launch in the profiled bench run (its JSON line's
+  config.steps_per_launch), 1 if absent."""
+  try:
+    with open(d.rstrip('/') + '.trace.log') as f:
+      lines = [l for l in f if l.startswith('{')]
+    return int(json.loads(lines[-1])['config'].get('steps_per_launch', 1))
+  except (OSError, IndexError, KeyError, ValueError):
+    return 1
 PHASE_B = {'kinetic_kernel': 80 * 10, 'update_acc_kernel': 72 * 10, 'vproj_kernel': 96 * 10,
            'capsule_plane_kernel': 120 * 5}
 
@@ -85,6 +99,10 @@ def main():
   # per-kernel averages from the dispatch trace at the bench grid (the
   # --stats CSV copied above averages every grid of an instantiation)
   grids, stats = bench_grids(d)
+  K = rollout_steps(d)
+  for k in stats:
+    if 'env_rollout_kernel' in k:
+      stats[k]['steps_per_launch'] = K
   cnt, meta = counters(d, grids)
   res = {}
   for k, cs in cnt.items():
@@ -114,7 +132,9 @@ def main():
     base = k.split('::')[-1].split('<')[0]
     if k in ENV_STEP_B:
       ent['batch'] = e['grid'] // 64 * 4  # 16 lanes per env, 4 envs per 64-wide workgroup
-      ent['algorithmic_bytes_per_launch'] = ENV_STEP_B[k] * ent['batch']
+      spl = K if 'env_rollout_kernel' in k else 1
+      ent['steps_per_launch'] = spl
+      ent['algorithmic_bytes_per_launch'] = ENV_STEP_B[k] * ent['batch'] * spl
     elif base in PHASE_B:
       envs = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20  # bench --phase-envs
       ent['envs'] = envs
