@@ -63,6 +63,9 @@ REF_PUBLISHED = 895723.0
 # GRAPH_MAX steps (one replay, one action draw), else gcd(steps, GRAPH_STEPS)
 GRAPH_STEPS = 50
 GRAPH_MAX = 200
+# the timed loops, in order: the eager Python loop, StepGraph replays,
+# RolloutGraph replays, RolloutRunner (direct rollout launches)
+KINDS = ('eager', 'step', 'rollout', 'direct')
 
 
 def graph_steps(steps):
@@ -475,13 +478,14 @@ def main():
   # step's outputs written; the reference's lax.scan of env.step) after the
   # one draw. `value` is the faster loop that completed on every rank.
   from brax_amd.envs.graph import StepGraph
-  from brax_amd.envs.rollout import RolloutGraph
+  from brax_amd.envs.rollout import RolloutGraph, RolloutRunner
 
   def timed_replays(g, advance_hook):
     """Warm replays, then args.steps // K timed replays (barrier + sync on
     both sides); the elapsed wall time and the collectives inside it."""
+    fire = g.run if isinstance(g, RolloutRunner) else g.replay
     for _ in range(max(args.warmup // K, 2)):
-      g.replay()
+      fire()
     if exchange is not None:
       exchange.reset()
     torch.cuda.synchronize()
@@ -490,7 +494,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps // K):
-      g.replay()
+      fire()
       if advance_hook is not None:
         advance_hook(K)  # the RCCL all-gather once per period, on the host
     torch.cuda.synchronize()
@@ -506,9 +510,10 @@ def main():
         return StepGraph(env, st, K, seed=1, offset=off, step_stride=world * B * A,
                          hook=None if exchange is None else (
                              lambda s_: exchange.accumulate(s_.reward, s_.done))), None
-      return RolloutGraph(env, st, K, seed=1, offset=off, step_stride=world * B * A,
-                          hook=None if exchange is None else (
-                              lambda tr: exchange.accumulate_steps(tr.reward, tr.done))), None
+      cls = RolloutGraph if kind == 'rollout' else RolloutRunner
+      return cls(env, st, K, seed=1, offset=off, step_stride=world * B * A,
+                 hook=None if exchange is None else (
+                     lambda tr: exchange.accumulate_steps(tr.reward, tr.done))), None
     except Exception as e:  # pylint: disable=broad-except
       # a failed capture must not sink the run: every rank falls back, and
       # the line says so
@@ -524,21 +529,22 @@ def main():
   adv = None if exchange is None else exchange.advance
   loops = {'eager': (eager_elapsed, eager_collectives, None)}
   k0 = args.warmup + args.steps
-  for kind in ('step', 'rollout'):
+  for kind in KINDS[1:]:
     g, err = build(kind, state, k0)
     if agreed(g is not None):
       el, col = timed_replays(g, adv)
       loops[kind] = (el, col, None)
       k0 += (max(args.warmup // K, 2) + args.steps // K) * K
-      state = clone_state(g._res[0] if kind == 'rollout' else g._out)  # pylint: disable=protected-access
+      state = clone_state(g.state() if kind == 'direct' else  # pylint: disable=protected-access
+                          g._res[0] if kind == 'rollout' else g._out)
     else:
       loops[kind] = (None, 0, err)
     del g
   if dist is not None:
     t = torch.tensor([loops[k][0] if loops[k][0] is not None else -1.0
-                      for k in ('eager', 'step', 'rollout')], dtype=torch.float64, device=dev)
+                      for k in KINDS], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    for k, v in zip(('eager', 'step', 'rollout'), t.tolist()):
+    for k, v in zip(KINDS, t.tolist()):
       loops[k] = (float(v) if v >= 0 else None,) + loops[k][1:]
   best = min((k for k in loops if loops[k][0] is not None), key=lambda k: loops[k][0])
   elapsed, collectives = loops[best][0], loops[best][1]
@@ -552,7 +558,7 @@ def main():
   # the dominant kernel of the timed loop: the K-step rollout kernel (one
   # launch = K x B env-steps) or the single-step kernel (one launch = B
   # env-steps); achieved = algorithmic flops (bytes) per launch / launch time
-  if best == 'rollout':
+  if best in ('rollout', 'direct'):
     kname, spl = ANT_ROLLOUT_KERNEL, K
     kern_ms = rollout_train(env, state, K) * K
     kern_src = (f'HIP events over 20 back-to-back {K}-step bx_env_rollout_packed launches on '
@@ -598,6 +604,11 @@ def main():
                  'launch': {
                      'rollout': f'hipGraph replays of one on-device draw of {K} action slabs + '
                                 f'one {K}-step open-loop rollout launch (bx_env_rollout_packed)',
+                     'direct': f'per {K} steps: one on-device draw of {K} action slabs '
+                               f'(bx_uniform_slabs) + one {K}-step open-loop rollout launch '
+                               '(bx_env_rollout_packed), launched directly from prebuilt C '
+                               'arguments, the state read in place from the previous launch\'s '
+                               'last step (RolloutRunner)',
                      'step': f'hipGraph replays of one on-device draw of {K} action slabs + {K} '
                              'fused Env.step launches (+ the episodic sum per step when N>1)',
                      'eager': 'a Python loop of bx_uniform + Env.step per step'}[best],
@@ -630,7 +641,8 @@ def main():
   # the same steps from the plain Python loop (one Env.step call per step):
   # host-bound on a slow host, hence the graph above
   # every loop's rate (value is the fastest); a loop that failed says why
-  for kind, key in (('eager', 'eager_loop'), ('step', 'graph_loop'), ('rollout', 'rollout_loop')):
+  for kind, key in (('eager', 'eager_loop'), ('step', 'graph_loop'), ('rollout', 'rollout_loop'),
+                    ('direct', 'direct_loop')):
     el, col, err = loops[kind]
     out[key] = ({'value': total / el, 'unit': 'env-steps/s', 'ms_per_step': el * 1e3 / args.steps,
                  'collectives_in_timed_region': col} if el is not None else {'error': err})

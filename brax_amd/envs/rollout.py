@@ -232,3 +232,118 @@ class RolloutGraph:
     """Steps every env K steps forward; returns (state, trajectory)."""
     self.graph.replay()
     return self._res
+
+
+class RolloutRunner:
+  """Back-to-back open-loop rollouts of K steps with on-device action draws,
+  launched directly: per `run()` one `bx_uniform_slabs` launch (the K slabs
+  at the eager loop's `bx_uniform` offsets: chunk c's slab t at `offset +
+  (c * K + t) * step_stride`) and one `bx_env_rollout_packed` launch, their C
+  arguments built once. Two trajectory buffers alternate: chunk c reads its
+  input state from chunk c - 1's last step in place (no copies), so a run
+  costs two C calls of host time, on the caller's current stream. `hook(traj)` runs after each rollout (device
+  work, e.g. the episodic sums). `state()` is the state after the last run."""
+
+  def __init__(self, env, state: State, k: int, seed: int = 1, offset: int = 0,
+               step_stride: Optional[int] = None, lo: float = -1.0, hi: float = 1.0,
+               hook=None):
+    if k < 1:
+      raise ValueError(f'k must be >= 1, got {k}')
+    u, opts = chain_options(env)
+    dev = u.sys.device
+    self.env, self.k, self.device, self.hook = env, int(k), dev, hook
+    self._u = u
+    buf = packed_buffer(state.qp)
+    B = (buf if buf is not None else state.qp.pos).shape[0]
+    A = env.action_size
+    self.B, self.A = B, A
+    self.seed, self.offset, self.lo, self.hi = seed, int(offset), float(lo), float(hi)
+    self.stride = B * A if step_stride is None else int(step_stride)
+    N, O, M = u.sys.num_bodies, u.obs_size, len(u.metric_keys)
+    self.N, self.O, self.M = N, O, M
+    self.block = B * (N * 16 + O + 4 + M)
+    self._out = torch.empty((2, self.k * self.block), dtype=torch.float32, device=dev)
+    needs_rng = state.info.get('rng') is not None or getattr(u, 'needs_rng', False)
+    self._rng = torch.zeros((2, self.k, B), dtype=torch.int32, device=dev) if needs_rng else None
+    self._acts = torch.empty((self.k, B, A), dtype=torch.float32, device=dev)
+    auto = bool(opts.get('auto_reset'))
+    self._first = (state.info.get('first_qp'), state.info.get('first_obs')) if auto else (None, None)
+    if auto and None in self._first:
+      raise ValueError('AutoResetWrapper state lacks first_qp / first_obs')
+    self._p = u._params(opts, *self._first)  # pylint: disable=protected-access
+    self._has_steps = self._p.episode_length > 0
+    # the starting state goes into buffer 1's last step: chunk 0 reads it there
+    last = self._views(1)
+    if buf is None:
+      for lo_, f in ((0, state.qp.pos), (3, state.qp.rot), (7, state.qp.vel), (10, state.qp.ang)):
+        last['qp'][..., lo_:lo_ + f.shape[-1]] = f
+    else:
+      last['qp'].copy_(buf)
+    last['done'].copy_(torch.as_tensor(state.done, dtype=torch.float32, device=dev))
+    if state.info.get('steps') is not None:
+      last['steps'].copy_(torch.as_tensor(state.info['steps'], dtype=torch.float32, device=dev))
+    else:
+      last['steps'].zero_()
+    if self._rng is not None and state.info.get('rng') is not None:
+      self._rng[1, self.k - 1].copy_(state.info['rng'])
+    self._metrics_in = state.metrics
+    self._info_in = dict(state.info)
+    self._c = 0
+    self._cur = 1  # the buffer holding the latest trajectory
+    self._lib = _native.lib()
+
+  def _views(self, i):
+    K, B, N, O, M = self.k, self.B, self.N, self.O, self.M
+    blk = self._out[i].view(K, self.block)[K - 1]
+    q, obs, sc, met = torch.split(blk, (B * N * 16, B * O, 4 * B, B * M))
+    sc = sc.view(4, B)
+    return {'qp': q.view(B, N, 16), 'obs': obs.view(B, O), 'reward': sc[0], 'done': sc[1],
+            'steps': sc[2], 'truncation': sc[3], 'metrics': met.view(B, M)}
+
+  def run(self):
+    """Draws the next K action slabs and steps every env K steps."""
+    src, dst = self._cur, 1 - self._cur
+    K, B = self.k, self.B
+    _native.check(self._lib.bx_uniform_slabs(
+        C.c_void_p(self._acts.data_ptr()), B * self.A, K, self.seed,
+        self.offset + self._c * K * self.stride, self.stride, None, 0, self.lo, self.hi,
+        _stream(self.device.index)))
+    base = self._out[src].data_ptr() + 4 * (K - 1) * self.block
+    N, O = self.N, self.O
+    sc = base + 4 * B * (N * 16 + O)
+    rng_in = None if self._rng is None else self._rng[src, K - 1].data_ptr()
+    _native.check(self._lib.bx_env_rollout_packed(
+        self._u.sys._h, C.byref(self._p), B, K, base, sc + 4 * B,  # pylint: disable=protected-access
+        sc + 8 * B if self._has_steps else None, rng_in, self._acts.data_ptr(), self.A,
+        B * self.A, self.A, self._out[dst].data_ptr(),
+        None if self._rng is None else self._rng[dst].data_ptr(), _stream(self.device.index)))
+    self._cur = dst
+    self._c += 1
+    if self.hook is not None:
+      self.hook(self.trajectory())
+
+  def trajectory(self) -> Trajectory:
+    K, B, N, O, M = self.k, self.B, self.N, self.O, self.M
+    blocks = self._out[self._cur].view(K, self.block)
+    q, obs, sc, met = torch.split(blocks, (B * N * 16, B * O, 4 * B, B * M), dim=1)
+    sc = sc.view(K, 4, B)
+    return Trajectory(qp=q.view(K, B, N, 16), obs=obs.view(K, B, O), reward=sc[:, 0],
+                      done=sc[:, 1], steps=sc[:, 2], truncation=sc[:, 3],
+                      metrics=met.view(K, B, M), metric_keys=tuple(self._u.metric_keys),
+                      rng=None if self._rng is None else self._rng[self._cur])
+
+  def state(self) -> State:
+    """The state after the last run (views of the current trajectory)."""
+    v = self._views(self._cur)
+    info = dict(self._info_in)
+    if self._has_steps:
+      info['steps'] = v['steps']
+      info['truncation'] = v['truncation']
+    if self._rng is not None:
+      info['rng'] = self._rng[self._cur, self.k - 1]
+    keys = self._u.metric_keys
+    m_in = self._metrics_in
+    extra = m_in.carried(keys) if type(m_in) is _Metrics else {
+        k: v_ for k, v_ in m_in.items() if k not in keys}
+    return State(qp=PackedQP(v['qp']), obs=v['obs'], reward=v['reward'], done=v['done'],
+                 metrics=_Metrics(v['metrics'] if self.M else None, keys, extra), info=info)

@@ -79,14 +79,16 @@ def test_rollout_full_batch_ant(dev):
   _check(env, st0, acts)
 
 
-def test_rollout_graph_matches_eager_loop(dev):
-  """RolloutGraph replays (one slab draw + one rollout launch per K steps)
-  step on the eager loop's bits: bx_uniform at action_offset(rank, B, A,
-  step, world) per step, env.step per step (rank 1 of a world of 2)."""
+@pytest.mark.parametrize('runner', ['graph', 'direct'])
+def test_rollout_graph_matches_eager_loop(dev, runner):
+  """RolloutGraph replays and RolloutRunner runs (one slab draw + one
+  rollout launch per K steps) step on the eager loop's bits: bx_uniform at
+  action_offset(rank, B, A, step, world) per step, env.step per step (rank 1
+  of a world of 2)."""
   import ctypes as C
   from brax_amd import _native, envs
   from brax_amd import distributed as bd
-  from brax_amd.envs.rollout import RolloutGraph
+  from brax_amd.envs.rollout import RolloutGraph, RolloutRunner
   B, K, world, rank, k0 = 128, 5, 2, 1, 3
   env = envs.create('ant', batch_size=B, episode_length=7, auto_reset=True, device=dev)
   A = env.action_size
@@ -97,10 +99,17 @@ def test_rollout_graph_matches_eager_loop(dev):
   def hook(tr):
     acc[0].add_(tr.reward.sum(0))
     acc[1].add_(tr.done.sum(0))
-  g = RolloutGraph(env, st0, K, seed=3, offset=bd.action_offset(rank, B, A, k0, world),
-                   step_stride=world * B * A, hook=hook)
-  for _ in range(2):
-    out, tr = g.replay()
+  kw = dict(seed=3, offset=bd.action_offset(rank, B, A, k0, world), step_stride=world * B * A,
+            hook=hook)
+  if runner == 'graph':
+    g = RolloutGraph(env, st0, K, **kw)
+    for _ in range(2):
+      out, tr = g.replay()
+  else:
+    g = RolloutRunner(env, st0, K, **kw)
+    for _ in range(2):
+      g.run()
+    out, tr = g.state(), g.trajectory()
   act = torch.empty((B, A), dtype=torch.float32, device=dev)
   st = st0
   done_sum = torch.zeros((B,), device=dev)
