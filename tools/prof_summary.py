@@ -73,7 +73,7 @@ def bench_grids(d):
 def counters(d, grids):
   out = defaultdict(lambda: defaultdict(list))
   meta = {}
-  for sub in ('fetch', 'write', 'sq'):
+  for sub in ('fetch', 'write', 'sq', 'sq2'):
     p = os.path.join(d, sub, 'run_counter_collection.csv')
     if not os.path.exists(p):
       continue
@@ -156,10 +156,18 @@ def main():
     if k in stats and waves and 'SQ_INSTS_VALU' in c and 'SQ_WAVE_CYCLES' in c:
       valu = c['SQ_INSTS_VALU']['mean'] / waves
       cyc = 4 * c['SQ_WAVE_CYCLES']['mean'] / waves
+      wc = c['SQ_WAVE_CYCLES']['mean']
       stats[k]['sq'] = {'source': f'profiles/{tag}_counters.json', 'waves': waves,
                         'valu_insts_per_wave': valu,
                         'lds_insts_per_wave': c.get('SQ_INSTS_LDS', {}).get('mean', 0) / waves,
+                        'salu_insts_per_wave': c.get('SQ_INSTS_SALU', {}).get('mean', 0) / waves,
                         'cycles_per_wave': cyc, 'valu_issue_frac': 4 * valu / cyc}
+      # the stall split of the wave cycles (quad-cycle counters over quad-cycles)
+      for name, ctr in (('wait_any_frac', 'SQ_WAIT_ANY'), ('wait_inst_any_frac', 'SQ_WAIT_INST_ANY'),
+                        ('active_inst_any_frac', 'SQ_ACTIVE_INST_ANY'),
+                        ('wait_inst_lds_frac', 'SQ_WAIT_INST_LDS')):
+        if ctr in c:
+          stats[k]['sq'][name] = c[ctr]['mean'] / wc
   with open(os.path.join(prof, 'rocprof_latest.json'), 'w') as f:
     sys.path.insert(0, ROOT)
     from bench import src_sha1
