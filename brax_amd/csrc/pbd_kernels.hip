@@ -1480,6 +1480,16 @@ __device__ __forceinline__ unsigned seg_min_u32(unsigned v) {
   }
 }
 
+// the sum over each 16-lane row (one env at 16 lanes) in every lane of the
+// row: a row_ror butterfly (every lane of the wave must be active)
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, false));
+  return v;
+}
+
 // a candidate cell's selection key: (distance bits, row); distances are >= 0,
 // so their bit patterns order like the floats; a masked cell's sim is -inf,
 // its key (+inf's bits) sorts after every finite distance, ties in row =
@@ -2361,7 +2371,7 @@ __device__ unsigned long long bx_stamp_wave[4096][16];
 #define BX_KSTAMP(k) do {} while (0)
 #endif
 
-// FOLD (the Ant / Humanoid env kernels; the host checks that every joint j
+// FOLD (the Ant / Humanoid / HalfCheetah env kernels; the host checks that every joint j
 // has torque actuator j): each joint's damping torque is added into its
 // actuator's slot, so the body phase gathers one list instead of two. The
 // actuator slots then no longer hold the actuators alone, which only
@@ -2535,6 +2545,15 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     constexpr bool RG = (F & F_R2G) != 0;
     constexpr int F1 = RG ? (F & ~(F_CC | F_TW)) : F;
     constexpr int F2 = RG ? (F | F_CCO) : F;
+    // a row that does not penetrate (pen <= 0) has c >= 0 in the position
+    // pass (cm = 0) and sm = 0 in the velocity pass: its impulses are exact
+    // zeros. The passes with capsule-capsule code (pairs that rarely touch)
+    // skip that math for such rows, and a wave in which no row of the pass
+    // penetrates skips it whole (the branch's exec mask is empty); the
+    // plane passes (some foot of the wave's envs is down at almost every
+    // substep) keep the straight-line code
+    const v3 z3 = mk(0.f, 0.f, 0.f);
+    const q4 z4{0.f, 0.f, 0.f, 0.f};
     auto pos_pass = [&](auto fc, const RowC& R, int r, v3& cpos, v3& cn, float& pen, float& dl) {
       constexpr int FS = decltype(fc)::value;
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
@@ -2545,9 +2564,13 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       float unused;
       ld_slot(E.prev + R.a * PREV_STRIDE, pap, par, unused);
       ld_slot(E.prev + R.b * PREV_STRIDE, pbp, pbr, unused);
-      v3 oap, obp;
-      q4 oar, obr;
-      dl = position_contact<FS>(R, a, b, pap, par, pbp, pbr, cpos, cn, pen, oap, oar, obp, obr);
+      v3 oap = z3, obp = z3;
+      q4 oar = z4, obr = z4;
+      if (!((FS & F_CC) != 0) || pen > 0.f) {
+        dl = position_contact<FS>(R, a, b, pap, par, pbp, pbr, cpos, cn, pen, oap, oar, obp, obr);
+      } else {
+        dl = 0.f;
+      }
       float* rd = E.rowd + r * ROWD_STRIDE;
       st4a(rd, f32x4{cpos.x, cpos.y, cpos.z, cn.x});
       st4a(rd + 4, f32x4{cn.y, cn.z, pen, dl});
@@ -2581,9 +2604,10 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       v3 rap, rav, raa, rbp, rbv, rba;
       ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
       ld_rb(E.rb + R.b * RB_STRIDE, rbp, rbv, rba);
-      v3 oav, oaa, obv, oba;
-      velocity_contact<FS>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos, cn, pen, dl, oav, oaa, obv,
-                           oba);
+      v3 oav = z3, oaa = z3, obv = z3, oba = z3;
+      if (!((FS & F_CC) != 0) || pen > 0.f)
+        velocity_contact<FS>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos, cn, pen, dl, oav, oaa,
+                             obv, oba);
       st_slot(E.cslot + r * SLOT_STRIDE, oav, q4{oaa.x, oaa.y, oaa.z, 0.f},
               (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f);
       st_slot(E.cslot + (E.nR + r) * SLOT_STRIDE, obv, q4{oba.x, oba.y, oba.z, 0.f},
@@ -3232,13 +3256,14 @@ __device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3
 
 // observation element i of the env kind
 // env-program specialisation: the hot env kinds get step kernels holding
-// only their own env code (EK_ANT, EK_HUM: Humanoid and HumanoidStandup);
-// EK_ANY carries every kind, chosen at run time
-enum { EK_ANY = 0, EK_ANT = 1, EK_HUM = 2 };
+// only their own env code (EK_ANT, EK_HUM: Humanoid and HumanoidStandup,
+// EK_CHEETAH: HalfCheetah); EK_ANY carries every kind, chosen at run time
+enum { EK_ANY = 0, EK_ANT = 1, EK_HUM = 2, EK_CHEETAH = 3 };
 template <int EK>
 __device__ __forceinline__ constexpr bool ek_has(int k) {
   return EK == EK_ANY || (EK == EK_ANT && k == BX_ENV_ANT) ||
-         (EK == EK_HUM && (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP));
+         (EK == EK_HUM && (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP)) ||
+         (EK == EK_CHEETAH && k == BX_ENV_HALFCHEETAH);
 }
 #define KIND_IS(k) (ek_has<EK>(k) && kind == (k))
 
@@ -3861,6 +3886,13 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     float v = a0;
     if (i0 > 0 && lane < C) v = arow_g[i < aw ? i : aw - 1];
     if (i >= aw || !valid) v = 0.f;
+    if constexpr (EK == EK_ANT && L == 16) {
+      // the Ant kernel: the squares summed across the env's 16 lanes by DPP
+      // (a butterfly order instead of lane 0's serial one)
+      if (i < H.act_read) E.arow[i] = v;
+      sq += row_sum16(v * v);
+      continue;
+    }
     if (lane < C) {
       E.red[lane] = v;
       if (i < H.act_read) E.arow[i] = v;
@@ -3879,6 +3911,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   float reward_sum = 0.f;
   const int reps = P.episode_length > 0 ? (P.action_repeat > 0 ? P.action_repeat : 1) : 1;
   BX_KSTAMP(10);
+  v3 icv = mk(0.f, 0.f, 0.f);  // SINGLE: the lane's body's contact impulse sum
   for (int rep = 0; rep < reps; rep++) {
     v3 pos0 = ld3(E.qp);  // torso position before the step
     v3 com0 = mk(0.f, 0.f, 0.f);
@@ -3950,8 +3983,8 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     }
     esync<L>();
     if constexpr (S) {
-      v3 icv, ica, iaa;
-      pbd_step_single<L, F, M, EK == EK_ANT || EK == EK_HUM>(c, H, E, lane, valid, sact, saw, X, icv, ica, iaa);
+      v3 ica, iaa;
+      pbd_step_single<L, F, M, EK != EK_ANY>(c, H, E, lane, valid, sact, saw, X, icv, ica, iaa);
     } else if (H.spring) {
       spring_step<L, F>(c, H, E, lane, valid, sact, saw);
     } else {
@@ -3965,6 +3998,13 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
                    valid ? O.obs + e * P.obs_size : nullptr, P.coef, S ? &X.J : nullptr,
                    S ? &X.B : nullptr, (S && EK == EK_HUM) ? &X.A : nullptr);
     BX_KSTAMP(12);
+    // the Ant kernel's contact cost: each body lane's clipped squares, summed
+    // across the env's lanes by DPP
+    float ccs = 0.f;
+    if constexpr (S && EK == EK_ANT && L == 16) {
+      const v3 cv = mk(clip1(icv.x), clip1(icv.y), clip1(icv.z));
+      ccs = row_sum16(X.hasB ? cv.x * cv.x + cv.y * cv.y + cv.z * cv.z : 0.f);
+    }
     // reward / done / metrics (lane 0 of the env)
     if (lane == 0 && valid) {
       const float dt = H.dt;
@@ -3980,12 +4020,13 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
         bool term = P.coef[6] != 0.f;
         float hr = term ? P.coef[3] : P.coef[3] * healthy;
         float ctrl = P.coef[1] * sq;
-        float cs = 0.f;
-        for (int b = 0; b < H.N; b++)
-          for (int k = 0; k < 3; k++) {
-            float cv = clip1(E.acc[b * ACC_STRIDE + ACC_ICV + k]);
-            cs += cv * cv;
-          }
+        float cs = ccs;
+        if constexpr (!(S && EK == EK_ANT && L == 16))
+          for (int b = 0; b < H.N; b++)
+            for (int k = 0; k < 3; k++) {
+              float cv = clip1(E.acc[b * ACC_STRIDE + ACC_ICV + k]);
+              cs += cv * cv;
+            }
         float ccost = P.coef[2] * cs;
         reward = fwd + hr - ctrl - ccost;
         done = term ? 1.f - healthy : 0.f;
@@ -4595,6 +4636,16 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
       launch_one<EnvArgs>(env_rollout_kernel<16, 1, F_SPH | F_G1, 4, EK_HUM>, grid, tpb, lds, s, a);
     else
       launch_one<EnvArgs>(env_step_kernel<16, 1, F_SPH | F_G1, 4, EK_HUM>, grid, tpb, lds, s, a);
+    return hipGetLastError();
+  }
+  // HalfCheetah: 16 one-way ground rows in slot 1, the feet's capsule-capsule
+  // row in slot 2 (F_R2 | F_R2G), joint halves
+  constexpr int F_CHEETAH = F_CC | F_TW | F_JH | F_R2 | F_R2G;
+  if (fold && L == 16 && gw <= 4 && k == BX_ENV_HALFCHEETAH && (feat & ~F_G1) == F_CHEETAH) {
+    if (a.n_steps > 1)
+      launch_one<EnvArgs>(env_rollout_kernel<16, 1, F_CHEETAH, 4, EK_CHEETAH>, grid, tpb, lds, s, a);
+    else
+      launch_one<EnvArgs>(env_step_kernel<16, 1, F_CHEETAH, 4, EK_CHEETAH>, grid, tpb, lds, s, a);
     return hipGetLastError();
   }
   // HumanoidStandup: the Humanoid system lying down, 22 ground rows (F_R2)
