@@ -4268,6 +4268,21 @@ template <int L, int MODE, int F, int M, int EK = EK_ANY>
 __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
   env_step_body<L, MODE, F, M, EK>(A);
 }
+// the Ant step kernel held to 256 registers (2 waves per SIMD) for batches
+// past one wave per SIMD: at 4,096 envs the unbounded kernel's single wave
+// per SIMD is 7 % faster (29.8 vs 32.0 us), but at 32,768 envs (8 waves per
+// SIMD) it runs 8 residency rounds against this one's 4 (152 vs 219 M
+// env-steps/s, tools/ab_ant_waves.sh)
+template <int L, int MODE, int F, int M, int EK = EK_ANY>
+__global__ void __launch_bounds__(L > 64 ? L : 64) __attribute__((amdgpu_waves_per_eu(2)))
+env_step_wide_kernel(EnvArgs A) {
+  env_step_body<L, MODE, F, M, EK>(A);
+}
+template <int L, int MODE, int F, int M, int EK = EK_ANY>
+__global__ void __launch_bounds__(L > 64 ? L : 64) __attribute__((amdgpu_waves_per_eu(2)))
+env_rollout_wide_kernel(EnvArgs A) {
+  env_step_body<L, MODE, F, M, EK>(A);
+}
 // the same body under its own name for multi-step launches of the
 // benchmarked envs' kernels (bx_env_rollout_packed), so a profile tells
 // K-step launches from single steps
@@ -4523,6 +4538,20 @@ __global__ void uniform_slabs_kernel(float* out, int64_t slab_n, int64_t n, uint
 // ---------------------------------------------------------------------------
 namespace bx {
 
+// compute units of the current device (the launch runs under the system's
+// device scope), cached per device
+static int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 template <typename Args>
 static void launch_one(void (*k)(Args), dim3 grid, int tpb, size_t lds, hipStream_t s, const Args& a) {
   // tpb threads per workgroup (a multiple of L, <= 64): 64 / L envs share a
@@ -4624,8 +4653,14 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
   // (their kernels fold each joint's damping into its actuator's slot: fold
   // = every joint j has torque actuator j)
   if (fold && L == 16 && gw <= 4 && k == BX_ENV_ANT && feat == (F_G1 | F_JH)) {
-    if (a.n_steps > 1)
+    // past one wave per SIMD: the register-capped kernels
+    const bool wide = (int64_t)grid.x * (tpb / 64 > 0 ? tpb / 64 : 1) > 4 * (int64_t)cu_count();
+    if (a.n_steps > 1 && wide)
+      launch_one<EnvArgs>(env_rollout_wide_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
+    else if (a.n_steps > 1)
       launch_one<EnvArgs>(env_rollout_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
+    else if (wide)
+      launch_one<EnvArgs>(env_step_wide_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
     else
       launch_one<EnvArgs>(env_step_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
     return hipGetLastError();

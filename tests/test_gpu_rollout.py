@@ -124,3 +124,13 @@ def test_rollout_graph_matches_eager_loop(dev, runner):
   assert torch.equal(out.info['steps'], st.info['steps'])
   assert torch.equal(tr.done[K - 1], st.done)
   assert torch.equal(acc[1], done_sum)  # 0 / 1 sums are exact in any order
+
+
+def test_rollout_wide_batch_ant(dev):
+  """Past one wave per SIMD (16,384 envs: 4 waves per SIMD) the Ant step and
+  rollout launches take the register-capped kernels: the same bits."""
+  from brax_amd import envs
+  env = envs.create('ant', batch_size=16384, episode_length=1000, auto_reset=True, device=dev)
+  st0 = env.reset(np.array([0, 0x5EED], np.uint32))
+  acts = torch.rand((4, 16384, 8), device=dev) * 2 - 1
+  _check(env, st0, acts)
