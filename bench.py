@@ -137,6 +137,12 @@ def cpu_baseline(batch, min_seconds=10.0, max_steps=100000):
   return {'value': B * steps / dt, 'unit': 'env-steps/s', 'cores': threads, 'kind': 'port',
           'nproc': cpu['nproc'], 'allowed_cpus': cpu['allowed_cpus'], 'cpu_model': cpu['model'],
           'omp_num_threads': os.environ.get('OMP_NUM_THREADS'),
+          # the box's CPU share is OMP_NUM_THREADS (the operator's setting);
+          # nproc counts the whole shared host
+          'per_core': B * steps / dt / max(threads, 1),
+          # the reference's own JAX-CPU floor for this env
+          'reference_cpu_floor': {'value': 990.0, 'unit': 'env-steps/s',
+                                  'source': 'brax/tests/env_test.py:27,75 (Ant, B=128, lax.scan of 1,000 zero-action steps, > 0.99 x 1000 SPS)'},
           'sample': f'Ant, {B} envs x {steps} env-steps ({dt:.1f} s), float32 C '
                     f'restatement (oracle/pbd_oracle.c), {threads} OpenMP threads '
                     f'(nproc {cpu["nproc"]}, {cpu["allowed_cpus"]} CPUs allowed, '
