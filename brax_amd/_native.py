@@ -49,6 +49,10 @@ _SIGS = {
                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
                                C.c_void_p], C.c_int),
+    'bx_env_rollout_random': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64, C.c_int32,
+                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                               C.c_uint64, C.c_uint64, C.c_float, C.c_float, C.c_int64,
+                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     'bx_env_sizes': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.POINTER(C.c_int32),
                       C.POINTER(C.c_int32)], C.c_int),
     'bx_env_reset': ([C.c_void_p, C.POINTER(abi.BxEnvParams), C.c_int64, C.c_uint64, C.c_int64,

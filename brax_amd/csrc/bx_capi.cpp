@@ -1016,16 +1016,35 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
 
 // bx_env_step over n_steps consecutive steps in one launch (bx_env_rollout_packed):
 // step t reads act + t * act_step and writes the out pointers + t * out_step
+struct DrawSpec {  // bx_env_rollout_random's on-device action draws
+  uint64_t seed, offset, step;
+  float lo, hi;
+  float* act_out;
+};
+static int check_draw(const bx_system* S, const bx_env_params* env, int64_t act_width) {
+  if (act_width <= 0) return fail("on-device draws need act_width >= 1");
+  // env programs that read the raw action row themselves (the pre-step
+  // action maps, the humanoid qfrc observation)
+  const int k = env->kind;
+  if (k == BX_ENV_REACHERANGLE || k == BX_ENV_SWIMMER || k == BX_ENV_GRASP ||
+      k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP)
+    return fail("this env kind's program reads the action row itself: draw with bx_uniform_slabs");
+  if (act_width > S->hdr.act_read)
+    return fail("on-device draws stage the whole action row: act_width exceeds the row the system stages");
+  return 0;
+}
+
 static int env_step_impl(bx_system* S, const bx_env_params* env, int64_t n_envs,
                          const bx_env_state* in, const float* act, int64_t act_stride,
                          int64_t act_width, const bx_env_state* out, void* stream,
-                         int32_t n_steps, int64_t act_step, int64_t out_step, int64_t rng_step) {
+                         int32_t n_steps, int64_t act_step, int64_t out_step, int64_t rng_step,
+                         const DrawSpec* draw = nullptr) {
   if (!S || !env || !in || !out) return fail("null argument");
   DEVICE_SCOPE(S);
   if (check_env(S, env)) return 1;
   // an empty batch is a no-op (its buffers, the action included, may be null)
   if (n_envs <= 0) return n_envs == 0 ? 0 : fail("negative n_envs");
-  if (check_act(S, act, act_stride, act_width)) return 1;
+  if (draw ? check_draw(S, env, act_width) : check_act(S, act, act_stride, act_width)) return 1;
   if (!qp_ok(in->qp) || !qp_ok(out->qp)) return fail("null qp field");
   if (!in->done || !out->done || !out->reward || !out->obs) return fail("null env buffer");
   if (env->auto_reset && (!qp_ok(env->first_qp) || !env->first_obs))
@@ -1051,6 +1070,15 @@ static int env_step_impl(bx_system* S, const bx_env_params* env, int64_t n_envs,
   a.act_step = act_step;
   a.out_step = out_step;
   a.rng_step = rng_step;
+  if (draw) {
+    a.draw = 1;
+    a.draw_seed = draw->seed;
+    a.draw_offset = draw->offset;
+    a.draw_step = draw->step;
+    a.draw_lo = draw->lo;
+    a.draw_hi = draw->hi;
+    a.act_out = draw->act_out;
+  }
   if (S->mode == 1)
     HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a, S->fold));
   else if (S->mode == 3)  // MULTI-mode systems step envs with the item-loop kernel
@@ -1071,7 +1099,7 @@ static int env_step_packed(bx_system* S, const bx_env_params* env, int64_t n_env
                            const float* qp_in, const float* done_in, const float* steps_in,
                            const uint32_t* rng_in, const float* act, int64_t act_stride,
                            int64_t act_step, int64_t act_width, float* out, uint32_t* rng_out,
-                           void* stream) {
+                           void* stream, const DrawSpec* draw = nullptr) {
   if (!S || !env) return fail("null argument");
   if (n_envs <= 0) {
     if (check_env(S, env)) return 1;
@@ -1107,7 +1135,7 @@ static int env_step_packed(bx_system* S, const bx_env_params* env, int64_t n_env
   // one step's output block: qp | obs | reward, done, steps, truncation | metrics
   const int64_t block = B * (N * 16 + env->obs_size + 4 + env->n_metrics);
   return env_step_impl(S, env, n_envs, &in, act, act_stride, act_width, &o, stream, n_steps,
-                       act_step, block, B);
+                       act_step, block, B, draw);
 }
 
 int bx_env_step_packed(bx_system* S, const bx_env_params* env, int64_t n_envs,
@@ -1128,6 +1156,20 @@ int bx_env_rollout_packed(bx_system* S, const bx_env_params* env, int64_t n_envs
   if (act_step_stride < 0) return fail("negative action step stride");
   return env_step_packed(S, env, n_envs, n_steps, qp_in, done_in, steps_in, rng_in, act,
                          act_stride, act_step_stride, act_width, out, rng_out, stream);
+}
+
+int bx_env_rollout_random(bx_system* S, const bx_env_params* env, int64_t n_envs, int32_t n_steps,
+                          const float* qp_in, const float* done_in, const float* steps_in,
+                          const uint32_t* rng_in, uint64_t seed, uint64_t offset,
+                          uint64_t step_stride, float lo, float hi, int64_t act_width,
+                          float* act_out, float* out, uint32_t* rng_out, void* stream) {
+  if (!S || !env) return fail("null argument");
+  if (n_steps < 0) return fail("negative n_steps");
+  if (check_env(S, env) || check_draw(S, env, act_width)) return 1;
+  if (n_steps == 0) return 0;
+  const DrawSpec d{seed, offset, step_stride, lo, hi, act_out};
+  return env_step_packed(S, env, n_envs, n_steps, qp_in, done_in, steps_in, rng_in, nullptr, 0, 0,
+                         act_width, out, rng_out, stream, &d);
 }
 
 int bx_system_info(bx_system* S, int64_t n_envs, const bx_qp* qp, const bx_info* info, void* stream) {

@@ -3836,9 +3836,17 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   // the target envs' per-env stream (advanced by one per env step)
   uint32_t rng_c = (A.in.rng && valid) ? A.in.rng[e] : 0u;
   constexpr int C = L < 64 ? L : 64;  // action-row chunk: one element per lane
-  const float* arow_g = A.act + el * A.act_stride;
+  // on-device draws: the action row from the counter RNG, staged in LDS whole
+  // (the host checks act_width <= act_read)
+  const bool drw = A.draw != 0;
+  auto draw_at = [&](int t, int i) {
+    return uniform_at(A.draw_seed,
+                      A.draw_offset + (uint64_t)t * A.draw_step + (uint64_t)el * (uint64_t)aw + (uint64_t)i,
+                      A.draw_lo, A.draw_hi);
+  };
+  const float* arow_g = drw ? nullptr : A.act + el * A.act_stride;
   float a0 = 0.f;
-  if (aw > 0 && lane < C) a0 = arow_g[lane < aw ? lane : aw - 1];
+  if (aw > 0 && lane < C) a0 = drw ? draw_at(0, lane < aw ? lane : aw - 1) : arow_g[lane < aw ? lane : aw - 1];
   if constexpr (S) {
     // N <= L: the lane's body
     float qv[13];
@@ -3860,10 +3868,16 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   }
   const int nst = A.n_steps > 1 ? A.n_steps : 1;
   for (int t = 0; t < nst; t++) {
-  const float* act = valid ? A.act + e * A.act_stride + t * A.act_step : nullptr;
+  // (draw mode: the env programs that read the raw row are refused on the
+  // host; physics reads the staged row)
+  const float* act = (valid && !drw) ? A.act + e * A.act_stride + t * A.act_step : nullptr;
   if (t > 0) {
-    arow_g = A.act + el * A.act_stride + t * A.act_step;
-    if (aw > 0 && lane < C) a0 = arow_g[lane < aw ? lane : aw - 1];
+    if (drw) {
+      if (aw > 0 && lane < C) a0 = draw_at(t, lane < aw ? lane : aw - 1);
+    } else {
+      arow_g = A.act + el * A.act_stride + t * A.act_step;
+      if (aw > 0 && lane < C) a0 = arow_g[lane < aw ? lane : aw - 1];
+    }
   }
   // this step's outputs
   bx_env_state O = A.out;
@@ -3884,8 +3898,9 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   for (int i0 = 0; i0 < aw; i0 += C) {
     const int i = i0 + lane;
     float v = a0;
-    if (i0 > 0 && lane < C) v = arow_g[i < aw ? i : aw - 1];
+    if (i0 > 0 && lane < C) v = drw ? draw_at(t, i < aw ? i : aw - 1) : arow_g[i < aw ? i : aw - 1];
     if (i >= aw || !valid) v = 0.f;
+    if (drw && A.act_out && valid && lane < C && i < aw) A.act_out[((int64_t)t * A.n_envs + e) * aw + i] = v;
     if constexpr (EK == EK_ANT && L == 16) {
       // the Ant kernel: the squares summed across the env's 16 lanes by DPP
       // (a butterfly order instead of lane 0's serial one)

@@ -27,6 +27,14 @@ struct EnvArgs {
   // pointers + t * out_step floats (rng + t * rng_step)
   int32_t n_steps;
   int64_t act_step, out_step, rng_step;
+  // on-device action draws (bx_env_rollout_random; draw = 0: read act): step
+  // t's action a of env e is uniform_at(draw_seed, draw_offset + t * draw_step
+  // + e * act_width + a, draw_lo, draw_hi), the same bits as bx_uniform_slabs;
+  // recorded at act_out[(t * n_envs + e) * act_width + a] when act_out is set
+  int32_t draw;
+  uint64_t draw_seed, draw_offset, draw_step;
+  float draw_lo, draw_hi;
+  float* act_out;
 };
 struct InfoArgs {
   const uint32_t* blob;

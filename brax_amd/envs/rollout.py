@@ -236,13 +236,17 @@ class RolloutGraph:
 
 class RolloutRunner:
   """Back-to-back open-loop rollouts of K steps with on-device action draws,
-  launched directly: per `run()` one `bx_uniform_slabs` launch (the K slabs
-  at the eager loop's `bx_uniform` offsets: chunk c's slab t at `offset +
-  (c * K + t) * step_stride`) and one `bx_env_rollout_packed` launch, their C
-  arguments built once. Two trajectory buffers alternate: chunk c reads its
-  input state from chunk c - 1's last step in place (no copies), so a run
-  costs two C calls of host time, on the caller's current stream. `hook(traj)` runs after each rollout (device
-  work, e.g. the episodic sums). `state()` is the state after the last run."""
+  launched directly: per `run()` ONE `bx_env_rollout_random` launch that
+  draws each step's actions inside the kernel (the K slabs at the eager
+  loop's `bx_uniform` offsets: chunk c's slab t at `offset + (c * K + t) *
+  step_stride`, recorded in `actions()`) and steps every env K times; for a
+  system whose staged action row is narrower than the env's action (`draw`
+  False), one `bx_uniform_slabs` launch and one `bx_env_rollout_packed`
+  launch instead. Two trajectory buffers alternate: chunk c reads its input
+  state from chunk c - 1's last step in place (no copies); one C call of host
+  time per run, on the caller's current stream. `hook(traj)` runs after each
+  rollout (device work, e.g. the episodic sums). `state()` is the state after
+  the last run."""
 
   def __init__(self, env, state: State, k: int, seed: int = 1, offset: int = 0,
                step_stride: Optional[int] = None, lo: float = -1.0, hi: float = 1.0,
@@ -291,6 +295,11 @@ class RolloutRunner:
     self._c = 0
     self._cur = 1  # the buffer holding the latest trajectory
     self._lib = _native.lib()
+    # one-launch draws when the system stages the whole action row (probed
+    # with a zero-step call: argument checks only)
+    self.draw = self._lib.bx_env_rollout_random(
+        self._u.sys._h, C.byref(self._p), B, 0, None, None, None, None, 0, 0, 0,  # pylint: disable=protected-access
+        0.0, 1.0, A, None, None, None, None) == 0
 
   def _views(self, i):
     K, B, N, O, M = self.k, self.B, self.N, self.O, self.M
@@ -304,23 +313,35 @@ class RolloutRunner:
     """Draws the next K action slabs and steps every env K steps."""
     src, dst = self._cur, 1 - self._cur
     K, B = self.k, self.B
-    _native.check(self._lib.bx_uniform_slabs(
-        C.c_void_p(self._acts.data_ptr()), B * self.A, K, self.seed,
-        self.offset + self._c * K * self.stride, self.stride, None, 0, self.lo, self.hi,
-        _stream(self.device.index)))
+    off = self.offset + self._c * K * self.stride
+    stream = _stream(self.device.index)
     base = self._out[src].data_ptr() + 4 * (K - 1) * self.block
     N, O = self.N, self.O
     sc = base + 4 * B * (N * 16 + O)
     rng_in = None if self._rng is None else self._rng[src, K - 1].data_ptr()
-    _native.check(self._lib.bx_env_rollout_packed(
-        self._u.sys._h, C.byref(self._p), B, K, base, sc + 4 * B,  # pylint: disable=protected-access
-        sc + 8 * B if self._has_steps else None, rng_in, self._acts.data_ptr(), self.A,
-        B * self.A, self.A, self._out[dst].data_ptr(),
-        None if self._rng is None else self._rng[dst].data_ptr(), _stream(self.device.index)))
+    rng_out = None if self._rng is None else self._rng[dst].data_ptr()
+    steps_in = sc + 8 * B if self._has_steps else None
+    if self.draw:
+      _native.check(self._lib.bx_env_rollout_random(
+          self._u.sys._h, C.byref(self._p), B, K, base, sc + 4 * B, steps_in, rng_in,  # pylint: disable=protected-access
+          self.seed, off, self.stride, self.lo, self.hi, self.A, self._acts.data_ptr(),
+          self._out[dst].data_ptr(), rng_out, stream))
+    else:
+      _native.check(self._lib.bx_uniform_slabs(
+          C.c_void_p(self._acts.data_ptr()), B * self.A, K, self.seed, off, self.stride, None, 0,
+          self.lo, self.hi, stream))
+      _native.check(self._lib.bx_env_rollout_packed(
+          self._u.sys._h, C.byref(self._p), B, K, base, sc + 4 * B, steps_in, rng_in,  # pylint: disable=protected-access
+          self._acts.data_ptr(), self.A, B * self.A, self.A, self._out[dst].data_ptr(), rng_out,
+          stream))
     self._cur = dst
     self._c += 1
     if self.hook is not None:
       self.hook(self.trajectory())
+
+  def actions(self):
+    """The last run's (K, B, A) actions."""
+    return self._acts
 
   def trajectory(self) -> Trajectory:
     K, B, N, O, M = self.k, self.B, self.N, self.O, self.M

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 9
+#define BX_ABI_VERSION 10
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
 enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
@@ -369,6 +369,27 @@ int bx_env_rollout_packed(bx_system* sys, const bx_env_params* env, int64_t n_en
                           const float* steps_in, const uint32_t* rng_in, const float* act,
                           int64_t act_stride, int64_t act_step_stride, int64_t act_width,
                           float* out, uint32_t* rng_out, void* stream);
+
+/* bx_env_rollout_packed with the actions drawn on the device inside the same
+ * launch: the reference's random-action rollout, a `lax.scan` of `env.step`
+ * on `jax.random.uniform` actions (notebooks/environments.ipynb:386-423, the
+ * published benchmark loop; the scan of training/acting.py:53-77). Step t's
+ * action a of env e is uniform_at(seed, offset + t * step_stride +
+ * e * act_width + a) in [lo, hi): the same bits bx_uniform_slabs(act, B * A,
+ * K, seed, offset, step_stride, NULL, 0, lo, hi) writes, so this equals that
+ * draw followed by bx_env_rollout_packed on its slabs. act_out (optional,
+ * (K, n_envs, act_width) contiguous) records the drawn actions. The whole
+ * action row is staged on chip: act_width must not exceed the widest row the
+ * system reads (every env's own action size fits). Env kinds whose program
+ * reads the raw row itself (ReacherAngle, Swimmer, Grasp, Humanoid,
+ * HumanoidStandup) are refused: draw with bx_uniform_slabs. n_steps = 0
+ * only checks the arguments (ABI 10). */
+int bx_env_rollout_random(bx_system* sys, const bx_env_params* env, int64_t n_envs,
+                          int32_t n_steps, const float* qp_in, const float* done_in,
+                          const float* steps_in, const uint32_t* rng_in, uint64_t seed,
+                          uint64_t offset, uint64_t step_stride, float lo, float hi,
+                          int64_t act_width, float* act_out, float* out, uint32_t* rng_out,
+                          void* stream);
 
 /* Batched System.default_qp from per-env joint angles/velocities
  * (B, num_joint_dof) contiguous (system.py:112-242). */

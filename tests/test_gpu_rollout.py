@@ -163,3 +163,38 @@ def test_env_speed_like_reference(dev, name):
     sps.append(B * T / (time.time() - t))
     assert bool(torch.all(st.done != 0))
   assert float(np.mean(sps)) > 1000 * 0.99
+
+
+@pytest.mark.parametrize('name', ['ant', 'halfcheetah', 'hopper', 'fetch', 'pusher', 'ur5e',
+                                  'humanoid', 'grasp'])
+def test_rollout_random_equals_slabs_then_rollout(dev, name):
+  """bx_env_rollout_random (the actions drawn inside the rollout launch) is
+  bit for bit bx_uniform_slabs followed by bx_env_rollout_packed on the
+  slabs, and records the same actions; the kinds whose env program reads the
+  raw action row are refused, and RolloutRunner falls back to the two
+  launches for them."""
+  import ctypes as C
+  from brax_amd import _native, envs
+  from brax_amd.envs.rollout import RolloutRunner, rollout
+  B, K = 64, 6
+  env = envs.create(name, batch_size=B, episode_length=4, auto_reset=True, device=dev)
+  A = env.action_size
+  st0 = env.reset(np.array([3, 1], np.uint32))
+  seed, off, stride = 5, 1000, 3 * B * A
+  runner = RolloutRunner(env, st0, K, seed=seed, offset=off, step_stride=stride)
+  assert runner.draw == (name not in ('humanoid', 'grasp'))
+  runner.run()
+  acts = torch.empty((K, B, A), dtype=torch.float32, device=dev)
+  _native.check(_native.lib().bx_uniform_slabs(
+      C.c_void_p(acts.data_ptr()), B * A, K, seed, off, stride, None, 0, -1.0, 1.0,
+      C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+  final, tr = rollout(env, st0, acts)
+  got = runner.trajectory()
+  torch.cuda.synchronize()
+  assert torch.equal(runner.actions(), acts)
+  assert torch.equal(got.qp[..., :13], tr.qp[..., :13])
+  assert torch.equal(got.obs, tr.obs) and torch.equal(got.reward, tr.reward)
+  assert torch.equal(got.done, tr.done) and torch.equal(got.steps, tr.steps)
+  if tr.rng is not None:
+    assert torch.equal(got.rng, tr.rng)
+  assert torch.equal(runner.state().obs, final.obs)
