@@ -63,6 +63,8 @@ REF_PUBLISHED = 895723.0
 # GRAPH_MAX steps (one replay, one action draw), else gcd(steps, GRAPH_STEPS)
 GRAPH_STEPS = 50
 GRAPH_MAX = 200
+# least warm-up of each replayed loop, seconds of its own work
+WARM_S = 0.02
 # the timed loops, in order: the eager Python loop, StepGraph replays,
 # RolloutGraph replays, RolloutRunner (direct rollout launches)
 KINDS = ('eager', 'step', 'rollout', 'direct')
@@ -488,10 +490,22 @@ def main():
 
   def timed_replays(g, advance_hook):
     """Warm replays, then args.steps // K timed replays (barrier + sync on
-    both sides); the elapsed wall time and the collectives inside it."""
+    both sides); the elapsed wall time, the collectives inside it and the
+    warm replays run. The warm-up is max(warmup // K, 2) replays, extended
+    to WARM_S of the loop's own work: the GPU's clock ramps over ~10 ms of
+    load (a 20-step rollout launch runs 506 us cold, 471 us warm in one
+    rocprof trace), so the timed region starts at the steady state."""
     fire = g.run if isinstance(g, RolloutRunner) else g.replay
-    for _ in range(max(args.warmup // K, 2)):
+    n_warm = max(args.warmup // K, 2)
+    t_w = time.perf_counter()
+    for _ in range(n_warm):
       fire()
+    torch.cuda.synchronize()
+    per = (time.perf_counter() - t_w) / n_warm
+    extra = max(0, math.ceil((WARM_S - per * n_warm) / max(per, 1e-6)))
+    for _ in range(extra):
+      fire()
+    n_warm += extra
     if exchange is not None:
       exchange.reset()
     torch.cuda.synchronize()
@@ -507,7 +521,7 @@ def main():
     if dist is not None:
       dist.barrier()
     torch.cuda.synchronize()
-    return time.perf_counter() - t0, (exchange.flushes if exchange is not None else 0)
+    return time.perf_counter() - t0, (exchange.flushes if exchange is not None else 0), n_warm
 
   def build(kind, st, k0):
     try:
@@ -538,9 +552,9 @@ def main():
   for kind in KINDS[1:]:
     g, err = build(kind, state, k0)
     if agreed(g is not None):
-      el, col = timed_replays(g, adv)
+      el, col, n_warm = timed_replays(g, adv)
       loops[kind] = (el, col, None)
-      k0 += (max(args.warmup // K, 2) + args.steps // K) * K
+      k0 += (n_warm + args.steps // K) * K
       state = clone_state(g.state() if kind == 'direct' else  # pylint: disable=protected-access
                           g._res[0] if kind == 'rollout' else g._out)
     else:
@@ -653,6 +667,8 @@ def main():
     out[key] = ({'value': total / el, 'unit': 'env-steps/s', 'ms_per_step': el * 1e3 / args.steps,
                  'collectives_in_timed_region': col} if el is not None else {'error': err})
   out['timed_loop'] = best
+  out['warmup_policy'] = (f'{args.warmup} warm-up steps; each replayed loop warms on >= '
+                          f'{WARM_S * 1e3:.0f} ms of its own untimed replays (steady-state clocks)')
   out['secondary_configs'] = None if args.no_secondary else secondary_configs(dev)
   out['phase_roofline'] = (None if args.no_phases else
                            phase_bench(env.unwrapped.sys, dev, args.phase_envs))
