@@ -243,7 +243,16 @@ def secondary_configs(dev, steps=50):
   out['humanoid_4096_graph'] = {'value': B * (steps // 10) * 10 / wall, 'unit': 'env-steps/s',
                                 'ms_per_step': wall * 1e3 / (steps // 10 * 10),
                                 'actions': 'drawn on the device every step'}
-  del env, st, g
+  # the same through K-step rollout launches (RolloutRunner; the Humanoid
+  # program reads the raw action row, so one slab draw + one rollout per K)
+  from brax_amd.envs.rollout import RolloutRunner
+  r = RolloutRunner(env, st[0], 50, seed=3)
+  wall, gpu = _time(r.run, max(steps // 50, 1), 2)
+  n_r = max(steps // 50, 1) * 50
+  out['humanoid_4096_rollout'] = {'value': B * n_r / wall, 'unit': 'env-steps/s',
+                                  'ms_per_step': wall * 1e3 / n_r, 'gpu_ms_per_step': gpu * 1e3 / n_r,
+                                  'actions': 'drawn on the device every step (50 per launch)'}
+  del env, st, g, r
   # configs[3]'s global batch (32,768 Ant envs) on ONE GPU: what one rank of
   # the 8-GPU run would hold if the whole batch sat on a single card.
   Bg = 32768
@@ -256,7 +265,13 @@ def secondary_configs(dev, steps=50):
   wall, gpu = _time(gstep, steps, 5)
   out['ant_32768_one_gpu'] = {'value': Bg * steps / wall, 'unit': 'env-steps/s',
                               'ms_per_step': wall * 1e3 / steps, 'gpu_ms_per_step': gpu * 1e3 / steps}
-  del env, st
+  r = RolloutRunner(env, st[0], 50, seed=3)
+  wall, gpu = _time(r.run, max(steps // 50, 1), 2)
+  out['ant_32768_one_gpu_rollout'] = {'value': Bg * n_r / wall, 'unit': 'env-steps/s',
+                                      'ms_per_step': wall * 1e3 / n_r,
+                                      'gpu_ms_per_step': gpu * 1e3 / n_r,
+                                      'actions': 'drawn inside the rollout launch (50 steps)'}
+  del env, st, r
   for cutoff in (0, 36):
     cfg = ant_mountain_config(4)
     cfg.collider_cutoff = cutoff

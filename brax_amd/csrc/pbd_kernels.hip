@@ -3042,10 +3042,15 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       float unused;
       ld_slot(E.prev + R.a * PREV_STRIDE, pap, par, unused);
       ld_slot(E.prev + R.b * PREV_STRIDE, pbp, pbr, unused);
-      v3 oap, obp;
-      q4 oar, obr;
-      dl[m] = position_contact<F>(R, a, b, pap, par, pbp, pbr, cpos[m], cn[m], pen[m], oap, oar, obp,
-                                  obr);
+      // a row that does not penetrate has exact-zero impulses in both passes
+      // (cm = 0, sm = 0): its math is skipped, by the whole wave when none of
+      // its rows of this iteration penetrates (most near capsule pairs)
+      v3 oap = mk(0.f, 0.f, 0.f), obp = mk(0.f, 0.f, 0.f);
+      q4 oar{0.f, 0.f, 0.f, 0.f}, obr{0.f, 0.f, 0.f, 0.f};
+      dl[m] = 0.f;
+      if (pen[m] > 0.f)
+        dl[m] = position_contact<F>(R, a, b, pap, par, pbp, pbr, cpos[m], cn[m], pen[m], oap, oar,
+                                    obp, obr);
       st_slot(E.cslot + r * MSLOT_STRIDE, oap, oar,
               (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f);
       if (!is_oneway<F>(R.oneway))
@@ -3081,9 +3086,10 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       v3 rap, rav, raa, rbp, rbv, rba;
       ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
       ld_rb(E.rb + R.b * RB_STRIDE, rbp, rbv, rba);
-      v3 oav, oaa, obv, oba;
-      velocity_contact<F>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos[m], cn[m], pen[m], dl[m],
-                          oav, oaa, obv, oba);
+      v3 oav = mk(0.f, 0.f, 0.f), oaa = oav, obv = oav, oba = oav;
+      if (pen[m] > 0.f)
+        velocity_contact<F>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos[m], cn[m], pen[m], dl[m],
+                            oav, oaa, obv, oba);
       st_slot(E.cslot + r * MSLOT_STRIDE, oav, q4{oaa.x, oaa.y, oaa.z, 0.f},
               (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f);
       if (!is_oneway<F>(R.oneway))
