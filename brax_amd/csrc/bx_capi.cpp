@@ -1349,6 +1349,7 @@ int bx_phase_capsule_plane(bx_system* S, int64_t n_envs, int64_t plane, const fl
 
 int bx_debug_stamps(unsigned long long* out, int reset) {
   // bit 1 of reset selects the MULTI-mode stamps (BX_MSTAMPS build)
+  // bit 2: the per-workgroup sums (4096 x 16 entries) instead of the totals
   if (reset & 2) HIP_OK(debug_mstamps(out, reset & 1));
   else HIP_OK(debug_stamps(out, reset));
   return 0;

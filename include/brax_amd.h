@@ -502,7 +502,8 @@ int bx_phase_capsule_plane(bx_system* sys, int64_t n_envs, int64_t plane, const 
 
 /* Diagnostic builds only (-DBX_STAMPS): per-phase s_memtime cycle sums of the
  * single-mode step, [0..9] phases, [15] samples; with reset bit 1 set, the
- * MULTI-mode step's (-DBX_MSTAMPS), [0..10]. Fails on product builds. */
+ * MULTI-mode step's (-DBX_MSTAMPS), [0..10]; with bit 2 set (single-mode),
+ * the per-workgroup sums, 4096 x 16 entries. Fails on product builds. */
 int bx_debug_stamps(unsigned long long* out16, int reset);
 
 /* Multi-rank episodic exchange is done over RCCL by the host (torch.distributed);

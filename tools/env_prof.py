@@ -21,12 +21,16 @@ def main():
   ap.add_argument('name')
   ap.add_argument('--batch', type=int, default=4096)
   ap.add_argument('--steps', type=int, default=20)
+  ap.add_argument('--block', type=int, default=0, help='threads per workgroup (A/B)')
   args = ap.parse_args()
   warnings.filterwarnings('ignore')
   from brax_amd import envs
   dev = torch.device('cuda', 0)
   B = args.batch
   env = envs.create(args.name, batch_size=B, episode_length=1000, auto_reset=True, device=dev)
+  if args.block:
+    from brax_amd import _native
+    _native.check(_native.lib().bx_system_set_block(env.unwrapped.sys._h, args.block))
   st = env.reset(np.array([0, 1], np.uint32))
   act = torch.rand((B, env.action_size), device=dev) * 2 - 1
   for _ in range(5):
