@@ -282,26 +282,14 @@ __device__ __forceinline__ v3 turn(v3 v, v3 axis, float c, float s) {
 // limits (math.signed_angle, joints.py:170-176): (cos, sin) is (x, y) /
 // |(x, y)| inside the limits, the limit's own outside; the test on
 // pseudo-angles. Neither atan2 nor the half-angle sincos is evaluated.
-// pseudo_angle(x, y) < p and > p without the division: with r = |x| + |y|,
-// 1 - x / r < p is x > (1 - p) r for y >= 0, x / r - 1 < p is x < (1 + p) r
-// below (and (0, 0) -> 0 as pseudo_angle); the same test up to the rounding
-// band of the boundary
-__device__ __forceinline__ bool pa_below(float x, float y, float p) {
-  const float r = fabsf(x) + fabsf(y);
-  return r > 0.f ? (y >= 0.f ? x > (1.f - p) * r : x < (1.f + p) * r) : 0.f < p;
-}
-__device__ __forceinline__ bool pa_above(float x, float y, float p) {
-  const float r = fabsf(x) + fabsf(y);
-  return r > 0.f ? (y >= 0.f ? x < (1.f - p) * r : x > (1.f + p) * r) : 0.f > p;
-}
 __device__ __forceinline__ v3 hinge_turn(v3 axis, v3 ref_p, v3 ref_c, const JLim& JL) {
   const float y = dot(cross(ref_p, ref_c), axis), x = dot(ref_p, ref_c);
-  const bool below = pa_below(x, y, JL.plo), above = pa_above(x, y, JL.phi);
+  const float pa = pseudo_angle(x, y);
   const float r2 = x * x + y * y;
   const float ri = r2 > 0.f ? rsqrtf(r2) : 0.f;
   float cph = r2 > 0.f ? x * ri : 1.f, sph = y * ri;
-  cph = below ? JL.clo : (above ? JL.chi : cph);
-  sph = below ? JL.slo : (above ? JL.shi : sph);
+  cph = pa < JL.plo ? JL.clo : (pa > JL.phi ? JL.chi : cph);
+  sph = pa < JL.plo ? JL.slo : (pa > JL.phi ? JL.shi : sph);
   return turn(ref_p, axis, cph, sph);
 }
 
@@ -1343,10 +1331,8 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   float wm = 1.f / m + dot(cr, mul(I, cr));
   float wp = xh(wm);
   float dl = -cc / (wm + wp + 1e-6f);
-  // dpo = sp (sg dl n) / m and the lever impulse sp (ro x dl n) = (sp dl) (ro x n):
-  // the side's constants folded (sg / m, loop-invariant), one cross product
-  const float spdl = J.sp * dl;
-  dpo = (spdl * (sg / m)) * n;
+  v3 pv = dl * n;
+  dpo = J.sp * ((sg * pv) / m);
   // the two angular constraints (axis alignment, limited hinge angle)
   v3 u0 = mrot(Mo, S.ax0);
   v3 u2 = mrot(Mo, S.ax2);
@@ -1362,8 +1348,8 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   // the side's rotation update is linear in the angular impulse: the
   // position constraint's and both angle constraints' add up before the one
   // quaternion product (joints.py:150-152, 190-195)
-  const v3 P = spdl * cr + J.sa * (pm + po);
-  dro = vec_quat_mul(mul((sg * 0.5f) * I, P), o.rot);
+  const v3 P = J.sp * cross(ro, pv) + J.sa * (pm + po);
+  dro = (sg * 0.5f) * vec_quat_mul(mul(I, P), o.rot);
 }
 
 // Actuator.apply_reduced (actuators.py:52-112) for a revolute joint, one side
@@ -1379,10 +1365,11 @@ __device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL
   float t;
   if (is_torque<F>(A.type)) {
     // the torque is cut outside the limits: the hinge angle's limit test on
-    // pseudo-angles (no atan2, no division)
-    const float x = dot(ref_p, ref_c), y = dot(cross(ref_p, ref_c), axis);
+    // pseudo-angles (no atan2)
+    const float pa = pseudo_angle(dot(ref_p, ref_c), dot(cross(ref_p, ref_c), axis));
     t = al[0] * A.strength * -1.f;
-    if (pa_below(x, y, JL.plo) || pa_above(x, y, JL.phi)) t = 0.f;
+    if (pa < JL.plo) t = 0.f;
+    if (pa > JL.phi) t = 0.f;
   } else {
     float ang = signed_angle(axis, ref_p, ref_c);
     float tgt = clampf(al[0] * 3.14159265358979323846f / 180.f, Jc.lim[0], Jc.lim[1]);
@@ -1392,9 +1379,8 @@ __device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL
   float sgp = is_torque<F>(A.type) ? 1.f : -1.f;
   // parent: sgp * Ip tq, child: -sgp * Ic tq (the side's sign times its inertia)
   float* slot = E.aslot + (child ? E.nK + a : a) * ASLOT_STRIDE;
-  // (the side's sign folded into its inertia, loop-invariant)
-  if (tqd) st_v3a(slot, mul(S.sg * S.I, sgp * tq + *tqd));  // + the joint's damping (FOLD)
-  else st_v3a(slot, mul((sgp * S.sg) * S.I, tq));
+  if (tqd) st_v3a(slot, S.sg * mul(S.I, sgp * tq + *tqd));  // + the joint's damping (FOLD)
+  else st_v3a(slot, (sgp * S.sg) * mul(S.I, tq));
 }
 
 // ---------------------------------------------------------------------------
