@@ -3829,7 +3829,13 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
 // input state is step t - 1's output, kept in LDS (the AutoReset select
 // reloads first_qp there), so the lane image, the state and the per-env
 // scalars are loaded once per launch, not once per step
-template <int L, int MODE, int F, int M, int EK = EK_ANY>
+// PK (the K-step rollout kernels, launched only on the packed layout of
+// bx_env_rollout_packed / _random): step t's outputs are one block at
+// out.qp.pos.ptr + t * out_step (qp (B, N, 16) | obs (B, O) | reward, done,
+// steps, truncation (4, B) | metrics (B, M)), so the step derives every
+// output pointer from that base instead of carrying eleven strided fields
+// across the step loop (uniform registers the kernel otherwise spills)
+template <int L, int MODE, int F, int M, int EK = EK_ANY, bool PK = false>
 __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   BX_KSTAMP_DECL
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -3904,16 +3910,42 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     }
   }
   // this step's outputs
-  bx_env_state O = A.out;
-  if (t > 0) {
-    const int64_t os = t * A.out_step;
-    O.qp.pos.ptr += os; O.qp.rot.ptr += os; O.qp.vel.ptr += os; O.qp.ang.ptr += os;
-    O.obs += os; O.reward += os; O.done += os;
-    if (O.metrics) O.metrics += os;
-    if (O.steps) O.steps += os;
-    if (O.truncation) O.truncation += os;
-    if (O.rng) O.rng += t * A.rng_step;
+  bx_env_state O;
+  float* blk = nullptr;  // PK: this step's output block
+  if constexpr (PK) {
+    const int64_t B = A.n_envs;
+    blk = A.out.qp.pos.ptr + t * A.out_step;
+    O.obs = blk + B * H.N * 16;
+    O.reward = O.obs + B * P.obs_size;
+    O.done = O.reward + B;
+    O.steps = O.reward + 2 * B;
+    O.truncation = O.reward + 3 * B;
+    O.metrics = P.n_metrics > 0 ? O.reward + 4 * B : nullptr;
+    O.rng = A.out.rng ? A.out.rng + t * A.rng_step : nullptr;
+  } else {
+    O = A.out;
+    if (t > 0) {
+      const int64_t os = t * A.out_step;
+      O.qp.pos.ptr += os; O.qp.rot.ptr += os; O.qp.vel.ptr += os; O.qp.ang.ptr += os;
+      O.obs += os; O.reward += os; O.done += os;
+      if (O.metrics) O.metrics += os;
+      if (O.steps) O.steps += os;
+      if (O.truncation) O.truncation += os;
+      if (O.rng) O.rng += t * A.rng_step;
+    }
   }
+  // body b's output record
+  auto store_out_qp = [&](int b, const float* src) {
+    if constexpr (PK) {
+      float* d = blk + (e * H.N + b) * 16;  // dword-aligned at any batch
+      st4a(d, f32x4{src[0], src[1], src[2], src[3]});
+      st4a(d + 4, f32x4{src[4], src[5], src[6], src[7]});
+      st4a(d + 8, f32x4{src[8], src[9], src[10], src[11]});
+      d[12] = src[12];
+    } else {
+      store_qp_global(O.qp, e, b, src);
+    }
+  };
   // the action row through LDS: its first act_read words stay staged (arow:
   // every index an actuator or force reads, jp.take clipping into the row),
   // and lane 0 sums the ctrl cost's squares in the reference's order (the
@@ -4279,7 +4311,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
       for (int b = lane; b < H.N; b += L) {
         float tmp[13];
         load_qp_global(P.first_qp, e, b, tmp);
-        store_qp_global(O.qp, e, b, tmp);
+        store_out_qp(b, tmp);
         // the next step starts from the reset state
         if (t + 1 < nst) {
           float* s = E.qp + b * QP_STRIDE;
@@ -4289,7 +4321,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
       }
       for (int i = lane; i < P.obs_size; i += L) O.obs[e * P.obs_size + i] = P.first_obs[e * P.obs_size + i];
     } else {
-      for (int b = lane; b < H.N; b += L) store_qp_global(O.qp, e, b, E.qp + b * QP_STRIDE);
+      for (int b = lane; b < H.N; b += L) store_out_qp(b, E.qp + b * QP_STRIDE);
     }
   }
   // the next step's input scalars: this step's outputs
@@ -4320,14 +4352,14 @@ env_step_wide_kernel(EnvArgs A) {
 template <int L, int MODE, int F, int M, int EK = EK_ANY>
 __global__ void __launch_bounds__(L > 64 ? L : 64) __attribute__((amdgpu_waves_per_eu(2)))
 env_rollout_wide_kernel(EnvArgs A) {
-  env_step_body<L, MODE, F, M, EK>(A);
+  env_step_body<L, MODE, F, M, EK, true>(A);
 }
 // the same body under its own name for multi-step launches of the
 // benchmarked envs' kernels (bx_env_rollout_packed), so a profile tells
 // K-step launches from single steps
 template <int L, int MODE, int F, int M, int EK = EK_ANY>
 __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_rollout_kernel(EnvArgs A) {
-  env_step_body<L, MODE, F, M, EK>(A);
+  env_step_body<L, MODE, F, M, EK, true>(A);
 }
 
 // System.info contact part + optional Env._get_obs of the same state (reset)
