@@ -30,6 +30,7 @@ always holds at least one collective (`collectives_in_timed_region`). Prints
 ONE JSON line on rank 0.
 """
 import argparse
+import gc
 import json
 import math
 import os
@@ -483,6 +484,8 @@ def main():
   if dist is not None:
     dist.barrier()
   torch.cuda.synchronize()
+  gc.collect()
+  gc.disable()  # no collector pause inside a timed region
   t0 = time.perf_counter()
   for k in range(args.steps):
     state = one_step(state, args.warmup + k)
@@ -491,6 +494,7 @@ def main():
     dist.barrier()
   torch.cuda.synchronize()
   elapsed = time.perf_counter() - t0
+  gc.enable()
   eager_elapsed = elapsed
   eager_collectives = exchange.flushes if exchange is not None else 0
   # the same loop replayed from hipGraphs, the actions continuing the eager
@@ -527,6 +531,8 @@ def main():
     if dist is not None:
       dist.barrier()
     torch.cuda.synchronize()
+    gc.collect()
+    gc.disable()  # no collector pause inside a timed region
     t0 = time.perf_counter()
     for _ in range(args.steps // K):
       fire()
@@ -536,7 +542,9 @@ def main():
     if dist is not None:
       dist.barrier()
     torch.cuda.synchronize()
-    return time.perf_counter() - t0, (exchange.flushes if exchange is not None else 0), n_warm
+    el = time.perf_counter() - t0
+    gc.enable()
+    return el, (exchange.flushes if exchange is not None else 0), n_warm
 
   def build(kind, st, k0):
     try:
