@@ -489,14 +489,19 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   off = tail;
   H.l_rowd = carve(R * ROWD_STRIDE);
   H.l_cslot = carve((2 * R + 1) * SLOT_STRIDE);
+  // SINGLE mode: the spherical kernels' joint limit rows, staged from the
+  // lane image once per launch (6 16-byte groups per lane, LIM_SLOTS; sized
+  // for this system's L, which bx_system_set_variant keeps)
+  const bool single_fit = N <= L && J <= L && K <= L && (R <= L || r2) && single_shape &&
+                          (mx <= 8 || L == 16);
+  H.l_jlim = single_fit ? carve(24 * L) : 0;
   // envs 64 words apart: with the odd-multiple record strides, the four
   // envs' records of one ds_read_b128 lane group land on distinct bank slots
   H.env_words = (off + 63) & ~63;
   {
     // the register-hoisted kernel is the pbd step only; legacy_spring systems
     // run the item-loop kernel
-    H.single = (N <= L && J <= L && K <= L && (R <= L || r2) && single_shape &&
-                (mx <= 8 || L == 16)) ? 1 : 0;  // F_C16 kernels: 16 lanes
+    H.single = single_fit ? 1 : 0;  // F_C16 kernels: 16 lanes
     // MULTI mode: a pbd scene past one wave (256 threads per env), every
     // lane owning <= 1 body / joint / actuator / task and <= MULTI_MR rows
     size_t mxja = 0;
@@ -947,8 +952,8 @@ int bx_system_set_variant(bx_system* S, int lanes, int mode) {
   if (lanes != 16 && lanes != 32 && lanes != 64 && lanes != 128 && lanes != 256)
     return fail("lanes must be 16, 32, 64, 128 or 256");
   if (mode < 0 || mode > 3) return fail("mode must be 0 (global), 1 (single), 2 (lds) or 3 (multi)");
-  if (mode == 1 && (!S->single_ok || lanes < S->min_L || lanes > 64))
-    return fail("system does not fit the single-item-per-lane kernel");
+  if (mode == 1 && (!S->single_ok || lanes < S->min_L || lanes > 64 || lanes > S->hdr.L))
+    return fail("system does not fit the single-item-per-lane kernel at that width");
   if (mode == 3 && (!S->multi_ok || lanes != 256))
     return fail("system does not fit the MULTI-mode kernel (256 lanes)");
   int old_L = S->L, old_m = S->mode, old_t = S->tpb;

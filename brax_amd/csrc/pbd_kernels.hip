@@ -86,6 +86,7 @@ struct Env {
   float* arow;   // the env's action row, its first act_read words (env step)
   float* nnl;    // NearNeighbors per-wave pick lists (nnl_words)
   int* nearl;    // MULTI: the pass's near rows, then per-wave counts
+  uint4* jlim;   // SINGLE spherical kernels: the lanes' limit rows, [6][L] groups
 };
 
 __device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -293,21 +294,25 @@ __device__ __forceinline__ v3 hinge_turn(v3 axis, v3 ref_p, v3 ref_c, const JLim
   return turn(ref_p, axis, cph, sph);
 }
 
-// A limit row (LL_*) from this lane's lane image, fetched where it is used:
-// the spherical kernels have no registers to hold three rows over the step.
-// li: the lane's first 16-byte group; g: the row's group (LIM_G*). The empty
-// asm makes every use a fresh L2 read rather than a hoisted register copy.
-enum { LIM_G0 = LI_JLIM / 4, LIM_G1 = LI_JLIM12 / 4, LIM_G2 = LI_JLIM12 / 4 + 2 };
+// A limit row (LL_*) of this lane's joint, read where it is used: the
+// spherical kernels have no registers to hold three rows over the step. The
+// rows are staged once per launch from the lane image (groups LI_JLIM / 4,
+// + 1 and LI_JLIM12 / 4 .. + 3) into LDS as 6 slots of L lanes (stage_lim):
+// li = the lane's slot-0 group, g = the row's first slot (LIM_G*). The empty
+// asm keeps every use a fresh LDS read rather than a hoisted register copy.
+enum { LIM_G0 = 0, LIM_G1 = 2, LIM_G2 = 4, LIM_SLOTS = 6 };
+template <int L>
 __device__ __forceinline__ JLim ld_lim(const uint4* li, int g) {
   asm volatile("" : "+s"(g));
-  const uint4 a = li[g * LANE_IMG_LANES], b = li[(g + 1) * LANE_IMG_LANES];
+  const uint4 a = li[g * L], b = li[(g + 1) * L];
   return JLim{__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z),
               __uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y)};
 }
 // the limit cut of a torque actuator needs only the pseudo-angles
+template <int L>
 __device__ __forceinline__ float2 ld_lim_p(const uint4* li, int g) {
   asm volatile("" : "+s"(g));
-  const uint4 a = li[g * LANE_IMG_LANES];
+  const uint4 a = li[g * L];
   return make_float2(__uint_as_float(a.x), __uint_as_float(a.y));
 }
 __device__ __forceinline__ constexpr int lim_group(int l) {
@@ -318,7 +323,7 @@ __device__ __forceinline__ constexpr int lim_group(int l) {
 // revolute hinge turn without atan2 / sincos; LI (no JL): the lane image
 // whose limit rows the revolute and spherical limits read the same way;
 // neither: the reference's formulas
-template <int F>
+template <int F, int LS = 16>
 __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, q4& dpr,
                             v3& dcp, q4& dcr, bool useJL = false, JLim JL = JLim{},
                             const uint4* LI = nullptr) {
@@ -362,7 +367,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
     if (useJL) {
       n1 = hinge_turn(axis, ref_p, ref_c, JL);
     } else if (LI) {
-      n1 = hinge_turn(axis, ref_p, ref_c, ld_lim(LI, LIM_G0));
+      n1 = hinge_turn(axis, ref_p, ref_c, ld_lim<LS>(LI, LIM_G0));
     } else {
       float psi = signed_angle(axis, ref_p, ref_c);
       float ph = clampf(psi, J.lim[0], J.lim[1]);
@@ -390,7 +395,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
         // limit_angle on pseudo-angles: inside the limits the row's impulse
         // is zero whatever the angle, outside n1 is turned by the limit's
         // own (cos, sin); neither atan2 nor sincos
-        const JLim L = ld_lim(LI, lim_group(l));
+        const JLim L = ld_lim<LS>(LI, lim_group(l));
         const float y = dot(cross(n1v[l], n2v[l]), nv[l]), x = dot(n1v[l], n2v[l]);
         const float pa = pseudo_angle(x, y);
         const bool below = pa < L.plo, above = pa > L.phi;
@@ -1198,7 +1203,7 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
 }
 
 // Torque/Angle.apply_reduced for actuator a (lane) -> aslot
-template <int F>
+template <int F, int LS = 16>
 __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, const Env& E,
                                            const float* al, int a, bool useJL = false,
                                            JLim JL = JLim{}, const uint4* LI = nullptr,
@@ -1213,7 +1218,7 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
       const v3 axis = rotate(Jc.axp[0], p.rot);
       const v3 ref_p = rotate(Jc.axp[2], p.rot), ref_c = rotate(Jc.axc[2], cq.rot);
       const float pa = pseudo_angle(dot(ref_p, ref_c), dot(cross(ref_p, ref_c), axis));
-      const float2 L = ld_lim_p(LI, LIM_G0);
+      const float2 L = ld_lim_p<LS>(LI, LIM_G0);
       tq = mk(0.f, 0.f, 0.f) + axis * ((pa < L.x || pa > L.y) ? 0.f : t0);
     } else {
       // Spherical.axis_angle (joints.py:388-415): psi, theta = +-acos(cb)
@@ -1236,7 +1241,7 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
       tq = mk(0.f, 0.f, 0.f);
 #pragma unroll
       for (int l = 0; l < 3; l++) {
-        const float2 L = ld_lim_p(LI, lim_group(l));
+        const float2 L = ld_lim_p<LS>(LI, lim_group(l));
         const float t = al[l] * A.strength * -1.f;
         tq = tq + axes[l] * ((pa[l] < L.x || pa[l] > L.y) ? 0.f : t);
       }
@@ -1413,6 +1418,7 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi =
   E.xact = al16(base + H.l_xact);
   E.arow = al16(base + H.l_arow);
   E.nnl = al16(base + H.l_nnl);
+  E.jlim = reinterpret_cast<uint4*>(al16(base + H.l_jlim));
   if (multi) {
     // MULTI: 8-word contact slots and task partials; no row-data region (the
     // row's contact stays in its lane's registers); the task partials double
@@ -2262,6 +2268,20 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   for (int k = 0; k < MC; k++) X.cl.e[k] = n(k < 8 ? LI_CL + k : LI_CL2 + k - 8);
 }
 
+// the spherical SINGLE kernels' limit rows into LDS, once per launch (see
+// ld_lim): 6 independent 16-byte loads per lane from the lane image
+template <int L, int F>
+__device__ __forceinline__ void stage_lim(const uint32_t* blob, const BlobHdr& H, const Env& E,
+                                          int lane) {
+  if constexpr ((F & F_SPH) != 0) {
+    const uint4* im = reinterpret_cast<const uint4*>(blob + H.o_lane) + lane;
+    constexpr int G[LIM_SLOTS] = {LI_JLIM / 4, LI_JLIM / 4 + 1, LI_JLIM12 / 4, LI_JLIM12 / 4 + 1,
+                                  LI_JLIM12 / 4 + 2, LI_JLIM12 / 4 + 3};
+#pragma unroll
+    for (int k = 0; k < LIM_SLOTS; k++) E.jlim[k * L + lane] = im[G[k] * LANE_IMG_LANES];
+  }
+}
+
 template <int M>
 __device__ __forceinline__ v3 gsum3(const GList<M>& g, const float* base, int stride) {
   v3 s = mk(0.f, 0.f, 0.f);
@@ -2400,7 +2420,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   // (passed by value: a pointer into X kept the hoisted struct in scratch,
   // 672-720 B per lane in every revolute kernel without joint halves)
   constexpr bool JLH = (F & F_SPH) == 0;
-  const uint4* LIP = (F & F_SPH) != 0 ? reinterpret_cast<const uint4*>(c.w + H.o_lane) + lane : nullptr;
+  const uint4* LIP = (F & F_SPH) != 0 ? E.jlim + lane : nullptr;  // staged by stage_lim
   const int jx = lane & 7;         // JH: this lane's joint / actuator
   const bool child = lane >= 8;    // JH: this lane's side
   float* myqp = E.qp + lane * QP_STRIDE;
@@ -2459,9 +2479,9 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         if (FOLD) {
           const JointC& Jc = X.J;
           const v3 tqd = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
-          act_torque<F>(X.J, A, E, al, lane, JLH, X.JL, LIP, &tqd);
+          act_torque<F, L>(X.J, A, E, al, lane, JLH, X.JL, LIP, &tqd);
         } else if (H.act_same) {
-          act_torque<F>(X.J, A, E, al, lane, JLH, X.JL, LIP);
+          act_torque<F, L>(X.J, A, E, al, lane, JLH, X.JL, LIP);
         } else {
           JointC Jc = load_joint(c, H, A.joint);
           act_torque<F>(Jc, A, E, al, lane);
@@ -2509,7 +2529,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
         q4 dpr, dcr;
-        joint_apply<F>(Jc, p, cq, dpp, dpr, dcp, dcr, JLH, X.JL, LIP);
+        joint_apply<F, L>(Jc, p, cq, dpp, dpr, dcp, dcr, JLH, X.JL, LIP);
         st_slot(E.jslot + lane * SLOT_STRIDE, dpp, dpr, 0.f);
         st_slot(E.jslot + (E.nJ + lane) * SLOT_STRIDE, dcp, dcr, 0.f);
       }
@@ -3744,7 +3764,10 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
   zero_slots(E, H, lane);
   // SINGLE: the lane image's loads go out before the state's
   Hoist<M, cl_width<F, M>()> X;
-  if constexpr (S) load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>()>(A.blob, H, lane, X);
+  if constexpr (S) {
+    load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>()>(A.blob, H, lane, X);
+    stage_lim<L, F>(A.blob, H, E, lane);
+  }
   for (int b = lane; b < H.N; b += L) {
     if (valid) {
       load_qp_global(A.qin, e, b, E.qp + b * QP_STRIDE);
@@ -3858,7 +3881,10 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   // (never stored)
   const int64_t el = valid ? e : 0;
   Hoist<M, cl_width<F, M>()> X;
-  if constexpr (S) load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>()>(A.blob, H, lane, X);
+  if constexpr (S) {
+    load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>()>(A.blob, H, lane, X);
+    stage_lim<L, F>(A.blob, H, E, lane);
+  }
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
   float done_in = A.in.done[el];
   float steps_in = A.in.steps ? A.in.steps[el] : 0.f;

@@ -100,6 +100,7 @@ struct BlobHdr {
   int32_t o_rimg;                    // MULTI mode: the row image (32 resolved words per row, LR_*)
   int32_t o_bimg;                    // MULTI mode: the rows' broad-phase bounds (BI_*), 0 = none
   int32_t l_near;                    // LDS (MULTI): the pass's near rows (R) + per-wave counts (16)
+  int32_t l_jlim;                    // LDS (SINGLE, spherical kernels): each lane's joint limit rows
 };
 
 // SINGLE-mode lane image: for each of 64 lanes, every constant the
