@@ -69,6 +69,29 @@ struct Builder {
   void i(int o, int x) { w[o] = (uint32_t)x; }
 };
 
+// the system's feature mask (F_* of pbd_kernels.hip: what its joints,
+// actuators, colliders and layout need), which picks its step kernels
+static int system_feat(const bx_desc* d, const BlobHdr& H, int L, int J, int K, int G,
+                       int max_groups, bool xcol, bool jh_off, bool r2, bool c16, bool r2g) {
+  int f = 0;
+  for (int j = 0; j < J; j++) if (d->joint_type[j] != BX_JOINT_REVOLUTE) f |= 1;
+  for (int a = 0; a < K; a++) if (d->act_type[a] != BX_ACT_TORQUE) f |= 2;
+  for (int g = 0; g < G; g++) {
+    if (d->col_fn[g] != BX_COL_CAPSULE_PLANE) f |= 4;
+    if (!d->col_oneway[g]) f |= 8;
+  }
+  if (d->n_forces > 0) f |= 16;
+  if (max_groups <= 1) f |= 32;  // F_G1: one collider group per body
+  if (xcol) f |= 64;             // F_X: extended contact functions
+  // F_JH (joint halves, SINGLE mode at 16 lanes): <= 8 revolute joints, each
+  // driven by the actuator of the same index
+  if (H.single && L == 16 && J <= 8 && K <= 8 && H.act_same && !(f & 1) && !jh_off) f |= 128;
+  if (r2) f |= 256;  // F_R2: two contact rows per lane (SINGLE mode, 16 lanes)
+  if (H.single && c16) f |= 512;  // F_C16: 16-entry contact gather lists
+  if (r2g) f |= 1024;             // F_R2G: one contact function per row slot
+  return f;
+}
+
 int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // A/B knob: BX_NO_JOINT_HALVES=1 keeps one lane per joint
   const bool jh_off = getenv("BX_NO_JOINT_HALVES") && atoi(getenv("BX_NO_JOINT_HALVES"));
@@ -494,7 +517,9 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // for this system's L, which bx_system_set_variant keeps)
   const bool single_fit = N <= L && J <= L && K <= L && (R <= L || r2) && single_shape &&
                           (mx <= 8 || L == 16);
-  H.l_jlim = single_fit ? carve(24 * L) : 0;
+  // (carved below, once the features say the system's SINGLE kernel reads it)
+  const int jlim_at = off;
+  H.l_jlim = 0;
   // envs 64 words apart: with the odd-multiple record strides, the four
   // envs' records of one ds_read_b128 lane group land on distinct bank slots
   H.env_words = (off + 63) & ~63;
@@ -720,6 +745,17 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         put(l, LI_CL2 + k, hasB && 8 + k < (int)cl[b].size() ? (uint32_t)cl[b][8 + k] : cz);
     }
   }
+  // the SINGLE kernel this system launches reads its joints' limit rows
+  // from LDS when its feature set carries spherical joints (F_SPH; the
+  // all-features instantiations too): carve the rows' region then (6
+  // 16-byte groups per lane), not otherwise (Ant keeps its LDS footprint:
+  // 32 envs per CU for the 2-wave kernels at 32,768 envs)
+  if (H.single && (single_kernel_feat(L, system_feat(d, H, L, J, K, G, max_groups, xcol, jh_off, r2,
+                                                     c16, r2g),
+                                      (c16 ? mx_ja : mx) <= 4 ? 4 : 8) & 1)) {
+    H.l_jlim = jlim_at;
+    H.env_words = (jlim_at + 24 * L + 63) & ~63;
+  }
   H.total_words = (int)B.w.size();
   std::memcpy(B.w.data(), &H, sizeof(BlobHdr));
 
@@ -730,22 +766,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // F_C16 gives it 16)
   S->gw = (c16 ? mx_ja : mx) <= 4 ? 4 : 8;
   {
-    int f = 0;
-    for (int j = 0; j < J; j++) if (d->joint_type[j] != BX_JOINT_REVOLUTE) f |= 1;
-    for (int a = 0; a < K; a++) if (d->act_type[a] != BX_ACT_TORQUE) f |= 2;
-    for (int g = 0; g < G; g++) {
-      if (d->col_fn[g] != BX_COL_CAPSULE_PLANE) f |= 4;
-      if (!d->col_oneway[g]) f |= 8;
-    }
-    if (d->n_forces > 0) f |= 16;
-    if (max_groups <= 1) f |= 32;  // F_G1: one collider group per body
-    if (xcol) f |= 64;             // F_X: extended contact functions
-    // F_JH (joint halves, SINGLE mode at 16 lanes): <= 8 revolute joints, each
-    // driven by the actuator of the same index
-    if (H.single && L == 16 && J <= 8 && K <= 8 && H.act_same && !(f & 1) && !jh_off) f |= 128;
-    if (r2) f |= 256;  // F_R2: two contact rows per lane (SINGLE mode, 16 lanes)
-    if (H.single && c16) f |= 512;  // F_C16: 16-entry contact gather lists
-    if (r2g) f |= 1024;             // F_R2G: one contact function per row slot
+    const int f = system_feat(d, H, L, J, K, G, max_groups, xcol, jh_off, r2, c16, r2g);
     S->feat = f;
     S->fold = (H.act_same && K == J && J > 0 && !(f & 2)) ? 1 : 0;
   }

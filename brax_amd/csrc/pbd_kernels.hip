@@ -4741,6 +4741,27 @@ hipError_t launch_system_step_single(int L, int feat, int gw, int tpb, int64_t n
   BX_DISPATCH_SINGLE(system_step_kernel, StepArgs)
   return hipGetLastError();
 }
+// single_kernel_feat: BX_DISPATCH_SINGLE run over a host-side probe that
+// records the instantiation's F instead of launching it (the same decision)
+struct ProbeArgs {
+  int* out;
+};
+template <int PL, int PMODE, int PF, int PM>
+void probe_kernel(ProbeArgs a) { *a.out = PF; }
+template <>
+void launch_one<ProbeArgs>(void (*k)(ProbeArgs), dim3, int, size_t, hipStream_t, const ProbeArgs& a) {
+  k(a);
+}
+int single_kernel_feat(int L, int feat, int gw) {
+  int f = -1;
+  const ProbeArgs a{&f};
+  const dim3 grid(1);
+  const int tpb = 64;
+  const size_t lds = 0;
+  hipStream_t s = nullptr;
+  BX_DISPATCH_SINGLE(probe_kernel, ProbeArgs)
+  return f;
+}
 hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
                                   hipStream_t s, const EnvArgs& a, int fold) {
   const int epb = tpb / L;

@@ -98,6 +98,10 @@ hipError_t launch_uniform_slabs(float* out, int64_t slab_n, int64_t n_slabs, uin
                                 uint64_t epoch_stride, float lo, float hi, hipStream_t s);
 
 hipError_t debug_stamps(unsigned long long* out, int reset);
+// the feature mask F of the SINGLE-mode kernel BX_DISPATCH_SINGLE picks for
+// (lanes, system features, gather width): its bit 1 (F_SPH) says whether it
+// reads the LDS-staged joint limit rows
+int single_kernel_feat(int L, int feat, int gw);
 hipError_t debug_mstamps(unsigned long long* out, int reset);  // MULTI mode (item-loop TU)
 hipError_t launch_phase(int which, const uint32_t* blob, int N, int64_t B, int64_t plane,
                         const float* in, float* out, const float* aux, int64_t aux_plane,
