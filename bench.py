@@ -50,7 +50,7 @@ ANT_BYTES_PER_ENV_STEP = 1428
 # rocprof name of the Ant env step: 16 lanes, SINGLE mode, features F_G1 |
 # F_JH (one collider group per body, joint halves), gather width 4, the Ant
 # env program only (EK_ANT)
-ANT_KERNEL = 'bx::env_step_kernel<16, 1, 160, 4, 1>'
+ANT_KERNEL = 'bx::env_step_packed_kernel<16, 1, 160, 4, 1>'
 # the same instantiation under its multi-step name: K-step open-loop rollout
 # launches (bx_env_rollout_packed)
 ANT_ROLLOUT_KERNEL = 'bx::env_rollout_kernel<16, 1, 160, 4, 1>'
@@ -305,40 +305,34 @@ def _traffic():
 
 def kernel_train(env, state, act, n=200):
   """Duration of the fused env-step kernel alone: `n` back-to-back
-  `bx_env_step` launches (fixed input state and action, ping-pong free: in and
-  out never alias) bracketed by HIP events on the stream they run on. The span
-  covers the launches and their inter-kernel gaps, never host work, so it
-  cannot exceed a timed step."""
+  `bx_env_step_packed` launches (Env.step's call; fixed input state and
+  action, in and out never alias) bracketed by HIP events on the stream they
+  run on. The span covers the launches and their inter-kernel gaps, never
+  host work, so it cannot exceed a timed step."""
   import ctypes as C
-  from brax_amd import _native, abi
-  from brax_amd.system import _stream, qp_struct
+  from brax_amd import _native
+  from brax_amd.base import packed_buffer
+  from brax_amd.system import _stream
   u = env.unwrapped
   dev = u.sys.device
-  B = state.qp.pos.shape[0]
-  qp, obs, scal, met = u._alloc(B)  # pylint: disable=protected-access
+  qb = packed_buffer(state.qp)
+  B = qb.shape[0]
+  N, O, M = u.sys.num_bodies, u.obs_size, len(u.metric_keys)
+  out = torch.empty((B * (N * 16 + O + 4 + M),), dtype=torch.float32, device=dev)
   p = u._params({'episode_length': 1000, 'action_repeat': 1, 'auto_reset': True},  # pylint: disable=protected-access
                 state.info['first_qp'], state.info['first_obs'])
-  sin = abi.BxEnvState()
-  sin.qp = qp_struct(state.qp, True)
-  sin.done = state.done.data_ptr()
-  sin.steps = state.info['steps'].data_ptr()
-  sout = abi.BxEnvState()
-  sout.qp = qp_struct(qp, True)
-  sout.obs = obs.data_ptr()
-  base = scal.data_ptr()
-  sout.reward, sout.done, sout.steps, sout.truncation = base, base + 4 * B, base + 8 * B, base + 12 * B
-  sout.metrics = met.data_ptr()
   lib = _native.lib()
   stream = _stream(dev.index)
-  args = (u.sys._h, C.byref(p), B, C.byref(sin), C.c_void_p(act.data_ptr()), act.stride(0),  # pylint: disable=protected-access
-          act.shape[1], C.byref(sout), stream)
+  args = (u.sys._h, C.byref(p), B, qb.data_ptr(), state.done.data_ptr(),  # pylint: disable=protected-access
+          state.info['steps'].data_ptr(), None, C.c_void_p(act.data_ptr()), act.stride(0),
+          act.shape[1], out.data_ptr(), None, stream)
   for _ in range(10):
-    _native.check(lib.bx_env_step(*args))
+    _native.check(lib.bx_env_step_packed(*args))
   torch.cuda.synchronize()
   a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
   a.record()
   for _ in range(n):
-    lib.bx_env_step(*args)
+    lib.bx_env_step_packed(*args)
   b.record()
   torch.cuda.synchronize()
   return a.elapsed_time(b) / n
@@ -608,8 +602,8 @@ def main():
                 'the launch stream (rollout_train)')
   else:
     kname, spl = ANT_KERNEL, 1
-    kern_src = ('HIP events over 200 back-to-back bx_env_step launches on the launch stream '
-                '(kernel_train)')
+    kern_src = ('HIP events over 200 back-to-back bx_env_step_packed launches on the launch '
+                'stream (kernel_train)')
   bytes_per_launch = ANT_BYTES_PER_ENV_STEP * B * spl
   flops_per_launch = ANT_FLOPS_PER_ENV_STEP * B * spl
   tflops = flops_per_launch / (kern_ms * 1e-3) / 1e12

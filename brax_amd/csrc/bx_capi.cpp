@@ -1064,7 +1064,7 @@ static int env_step_impl(bx_system* S, const bx_env_params* env, int64_t n_envs,
                          const bx_env_state* in, const float* act, int64_t act_stride,
                          int64_t act_width, const bx_env_state* out, void* stream,
                          int32_t n_steps, int64_t act_step, int64_t out_step, int64_t rng_step,
-                         const DrawSpec* draw = nullptr) {
+                         const DrawSpec* draw = nullptr, bool packed = false) {
   if (!S || !env || !in || !out) return fail("null argument");
   DEVICE_SCOPE(S);
   if (check_env(S, env)) return 1;
@@ -1096,6 +1096,7 @@ static int env_step_impl(bx_system* S, const bx_env_params* env, int64_t n_envs,
   a.act_step = act_step;
   a.out_step = out_step;
   a.rng_step = rng_step;
+  a.packed = packed ? 1 : 0;
   if (draw) {
     a.draw = 1;
     a.draw_seed = draw->seed;
@@ -1161,7 +1162,7 @@ static int env_step_packed(bx_system* S, const bx_env_params* env, int64_t n_env
   // one step's output block: qp | obs | reward, done, steps, truncation | metrics
   const int64_t block = B * (N * 16 + env->obs_size + 4 + env->n_metrics);
   return env_step_impl(S, env, n_envs, &in, act, act_stride, act_width, &o, stream, n_steps,
-                       act_step, block, B, draw);
+                       act_step, block, B, draw, true);
 }
 
 int bx_env_step_packed(bx_system* S, const bx_env_params* env, int64_t n_envs,

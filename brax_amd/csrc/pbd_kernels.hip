@@ -4365,6 +4365,12 @@ template <int L, int MODE, int F, int M, int EK = EK_ANY>
 __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(EnvArgs A) {
   env_step_body<L, MODE, F, M, EK>(A);
 }
+// one step on the packed layout (bx_env_step_packed: Env.step's host path)
+// through the PK body, under its own name (the benchmarked envs' kernels)
+template <int L, int MODE, int F, int M, int EK = EK_ANY>
+__global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_packed_kernel(EnvArgs A) {
+  env_step_body<L, MODE, F, M, EK, true>(A);
+}
 // the Ant step kernel held to 256 registers (2 waves per SIMD) for batches
 // past one wave per SIMD: at 4,096 envs the unbounded kernel's single wave
 // per SIMD is 7 % faster (29.8 vs 32.0 us), but at 32,768 envs (8 waves per
@@ -4773,12 +4779,15 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
   if (fold && L == 16 && gw <= 4 && k == BX_ENV_ANT && feat == (F_G1 | F_JH)) {
     // past one wave per SIMD: the register-capped kernels
     const bool wide = (int64_t)grid.x * (tpb / 64 > 0 ? tpb / 64 : 1) > 4 * (int64_t)cu_count();
-    if (a.n_steps > 1 && wide)
+    // (a packed single step at a wide batch takes the wide rollout kernel)
+    if ((a.n_steps > 1 || a.packed) && wide)
       launch_one<EnvArgs>(env_rollout_wide_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
     else if (a.n_steps > 1)
       launch_one<EnvArgs>(env_rollout_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
     else if (wide)
       launch_one<EnvArgs>(env_step_wide_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
+    else if (a.packed)
+      launch_one<EnvArgs>(env_step_packed_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
     else
       launch_one<EnvArgs>(env_step_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
     return hipGetLastError();
@@ -4787,6 +4796,8 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
       feat == (F_SPH | F_G1)) {
     if (a.n_steps > 1)
       launch_one<EnvArgs>(env_rollout_kernel<16, 1, F_SPH | F_G1, 4, EK_HUM>, grid, tpb, lds, s, a);
+    else if (a.packed)
+      launch_one<EnvArgs>(env_step_packed_kernel<16, 1, F_SPH | F_G1, 4, EK_HUM>, grid, tpb, lds, s, a);
     else
       launch_one<EnvArgs>(env_step_kernel<16, 1, F_SPH | F_G1, 4, EK_HUM>, grid, tpb, lds, s, a);
     return hipGetLastError();
@@ -4797,6 +4808,8 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
   if (fold && L == 16 && gw <= 4 && k == BX_ENV_HALFCHEETAH && (feat & ~F_G1) == F_CHEETAH) {
     if (a.n_steps > 1)
       launch_one<EnvArgs>(env_rollout_kernel<16, 1, F_CHEETAH, 4, EK_CHEETAH>, grid, tpb, lds, s, a);
+    else if (a.packed)
+      launch_one<EnvArgs>(env_step_packed_kernel<16, 1, F_CHEETAH, 4, EK_CHEETAH>, grid, tpb, lds, s, a);
     else
       launch_one<EnvArgs>(env_step_kernel<16, 1, F_CHEETAH, 4, EK_CHEETAH>, grid, tpb, lds, s, a);
     return hipGetLastError();

@@ -32,6 +32,7 @@ struct EnvArgs {
   // + e * act_width + a, draw_lo, draw_hi), the same bits as bx_uniform_slabs;
   // recorded at act_out[(t * n_envs + e) * act_width + a] when act_out is set
   int32_t draw;
+  int32_t packed;  // the outputs are the packed block layout (bx_env_*_packed / rollouts)
   uint64_t draw_seed, draw_offset, draw_step;
   float draw_lo, draw_hi;
   float* act_out;

@@ -34,5 +34,5 @@ def test_traffic_carries_algorithmic_bytes_per_env_kernel():
     t = json.load(f)['kernels']
   ant = t[bench.ANT_KERNEL]
   assert ant['algorithmic_bytes_per_launch'] == bench.ANT_BYTES_PER_ENV_STEP * 4096
-  hum = t['bx::env_step_kernel<16, 1, 33, 4, 2>']
+  hum = t['bx::env_step_packed_kernel<16, 1, 33, 4, 2>']
   assert hum['algorithmic_bytes_per_launch'] == 2284 * 4096

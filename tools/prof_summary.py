@@ -24,6 +24,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ENV_STEP_B = {
     'bx::env_step_kernel<16, 1, 160, 4, 1>': 1428,  # Ant: N=10, A=8, O=87
     'bx::env_step_kernel<16, 1, 33, 4, 2>': 2284,   # Humanoid: N=12, A=17, O=240
+    # Env.step's packed-layout single step (bx_env_step_packed)
+    'bx::env_step_packed_kernel<16, 1, 160, 4, 1>': 1428,
+    'bx::env_step_packed_kernel<16, 1, 33, 4, 2>': 2284,
     # the same per env-step, K steps per launch (bx_env_rollout_packed)
     'bx::env_rollout_kernel<16, 1, 160, 4, 1>': 1428,
     'bx::env_rollout_kernel<16, 1, 33, 4, 2>': 2284,
