@@ -469,6 +469,12 @@ def main():
 
   for k in range(args.warmup):
     state = one_step(state, k)
+  # no collector pause inside a timed region; collected BEFORE the warm-up
+  # work: a collection between the warm-up and t0 idles the GPU for
+  # milliseconds, its clock drops, and a short timed region (the driver's
+  # 20 steps are ONE rollout launch) runs on the ramp
+  gc.collect()
+  gc.disable()
   # the step kernel alone (its launch train also brings the clocks up before
   # the timed loops)
   kern_ms = single_ms = kernel_train(env, state, act)
@@ -478,8 +484,6 @@ def main():
   if dist is not None:
     dist.barrier()
   torch.cuda.synchronize()
-  gc.collect()
-  gc.disable()  # no collector pause inside a timed region
   t0 = time.perf_counter()
   for k in range(args.steps):
     state = one_step(state, args.warmup + k)
@@ -509,6 +513,8 @@ def main():
     load (a 20-step rollout launch runs 506 us cold, 471 us warm in one
     rocprof trace), so the timed region starts at the steady state."""
     fire = g.run if isinstance(g, RolloutRunner) else g.replay
+    gc.collect()  # before the warm replays (see the eager loop)
+    gc.disable()
     n_warm = max(args.warmup // K, 2)
     t_w = time.perf_counter()
     for _ in range(n_warm):
@@ -525,8 +531,6 @@ def main():
     if dist is not None:
       dist.barrier()
     torch.cuda.synchronize()
-    gc.collect()
-    gc.disable()  # no collector pause inside a timed region
     t0 = time.perf_counter()
     for _ in range(args.steps // K):
       fire()

@@ -54,9 +54,30 @@ def main():
       torch.cuda.synchronize()
       walls.append((time.perf_counter() - t0) * 1e6)
     w = float(np.median(walls))
+    # the same one-launch region after the GPU idled (a host pause of 5 ms,
+    # e.g. a garbage collection between warm-up and t0): the clock drops
+    idle = []
+    for _ in range(10):
+      for _ in range(3):
+        r.run()
+      torch.cuda.synchronize()
+      time.sleep(0.005)
+      t0 = time.perf_counter()
+      r.run()
+      torch.cuda.synchronize()
+      idle.append((time.perf_counter() - t0) * 1e6)
+    # host time of one run() call (ctypes + the C entry point + the launch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(20):
+      r.run()
+    host = (time.perf_counter() - t0) * 1e6 / 20
+    torch.cuda.synchronize()
     rows.append({'K': K, 'gpu_us_per_launch': gpu_us, 'gpu_us_per_step': gpu_us / K,
                  'wall_us_one_launch': w, 'wall_us_per_step': w / K,
-                 'wall_minus_gpu_us': w - gpu_us})
+                 'wall_minus_gpu_us': w - gpu_us,
+                 'wall_us_one_launch_after_5ms_idle': float(np.median(idle)),
+                 'host_us_per_run_call': host})
     print(json.dumps(rows[-1]), flush=True)
     del r
   # least-squares fit of the back-to-back GPU time: per-step + fixed
