@@ -52,6 +52,7 @@ struct bx_system {
   bool single_ok = false;
   bool multi_ok = false;  // MODE_MULTI (3): large pbd scenes, 256 threads per env
   int fold = 0;     // every joint j has torque actuator j (the Ant / Humanoid env kernels)
+  int jb = 0;       // the joint-halves env kernels may own body copies (JB, build_blob)
   size_t lds_env = 0;    // bytes per block for the per-env kernels
   size_t lds_reset = 0;  // bytes per block for default_qp
 };
@@ -683,17 +684,27 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     auto put_list = [&](int lane, int base, const std::vector<int>& v, bool has, uint32_t zero) {
       for (int k = 0; k < 8; k++) put(lane, base + k, has && k < (int)v.size() ? (uint32_t)v[k] : zero);
     };
+    // a body's record: mass, inverse inertia, pos / rot / quat masks
+    auto put_body = [&](int lane, int base, int b) {
+      const uint32_t* s = &B.w[H.o_body + b * BODY_STRIDE];
+      put(lane, base, s[BODY_MASS]);
+      for (int k = 0; k < 3; k++) {
+        put(lane, base + 1 + k, s[BODY_I + k]);
+        put(lane, base + 4 + k, s[BODY_PM + k]);
+        put(lane, base + 7 + k, s[BODY_RM + k]);
+      }
+      for (int k = 0; k < 4; k++) put(lane, base + 10 + k, s[BODY_QM + k]);
+    };
+    // joint halves: lane m's side body (the parent of joint m & 7 on lanes
+    // 0-7 of each 16, the child on 8-15)
+    auto side_body = [&](int m) {
+      const uint32_t* s = &B.w[H.o_joint + ((m & 7) < J ? (m & 7) : 0) * JOINT_STRIDE];
+      return (int)s[(m & 8) ? J_BC : J_BP];
+    };
     for (int l = 0; l < LANE_IMG_LANES; l++) {
       const bool hasB = l < N;
       const int b = hasB ? l : 0;
-      const uint32_t* s = &B.w[H.o_body + b * BODY_STRIDE];
-      put(l, LI_BODY, s[BODY_MASS]);
-      for (int k = 0; k < 3; k++) {
-        put(l, LI_BODY + 1 + k, s[BODY_I + k]);
-        put(l, LI_BODY + 4 + k, s[BODY_PM + k]);
-        put(l, LI_BODY + 7 + k, s[BODY_RM + k]);
-      }
-      for (int k = 0; k < 4; k++) put(l, LI_BODY + 10 + k, s[BODY_QM + k]);
+      put_body(l, LI_BODY, b);
       put_joint(l, LI_JOINT, l < J ? l : 0);
       put_act(l, LI_ACT, l < K ? l : 0);
       put_joint(l, LI_JOINT_H, (l & 7) < J ? (l & 7) : 0);
@@ -716,6 +727,19 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         put(l, LI_SIDE_H + LS_M, bw[BODY_MASS]);
         put(l, LI_SIDE_H + LS_SG, fbits(child ? -1.0 : 1.0));
         put(l, LI_SIDE_H + LS_BODY, (uint32_t)body);
+        // JB: the side body's record and gather lists; LS_OWN on the lowest
+        // lane of the 16 whose side is that body
+        const bool hasS = (l & 7) < J;
+        bool own = hasS;
+        for (int m = l & ~15; m < l; m++)
+          if ((m & 7) < J && side_body(m) == body) own = false;
+        put(l, LI_SIDE_H + LS_OWN, own ? 1u : 0u);
+        put_body(l, LI_BODY_J, body);
+        put_list(l, LI_JL_J, jl[body], hasS, (uint32_t)(2 * J));
+        put_list(l, LI_AL_J, al[body], hasS, (uint32_t)(2 * K));
+        uint32_t czj = (uint32_t)(2 * R);
+        if (hasS && !cl[body].empty()) czj |= (uint32_t)cl[body][0] & 0x7F000000u;
+        put_list(l, LI_CL_J, cl[body], hasS, czj);
       }
       put_act(l, LI_ACT_H, (l & 7) < K ? (l & 7) : 0);
       if (R > 0) {
@@ -769,6 +793,29 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     const int f = system_feat(d, H, L, J, K, G, max_groups, xcol, jh_off, r2, c16, r2g);
     S->feat = f;
     S->fold = (H.act_same && K == J && J > 0 && !(f & 2)) ? 1 : 0;
+    // JB (the Ant / HalfCheetah env kernels: joint halves own body copies):
+    // every body on no joint side must be frozen in all dimensions (position,
+    // rotation and the quaternion's vector part masks zero) and touch
+    // contact rows only as the plane side of one-way rows (its record then
+    // never changes and its contact sums are zeros); no forces (they index
+    // bodies by lane)
+    bool jb = S->fold && (f & 128) && !(f & 16) && L == 16;
+    std::vector<char> side(N, 0);
+    for (int j = 0; j < J; j++) side[d->joint_body_p[j]] = side[d->joint_body_c[j]] = 1;
+    for (int b = 0; b < N && jb; b++) {
+      if (side[b]) continue;
+      const uint32_t* bw = &B.w[H.o_body + b * BODY_STRIDE];
+      for (int k = 0; k < 3; k++)
+        jb = jb && bw[BODY_PM + k] == fbits(0.0) && bw[BODY_RM + k] == fbits(0.0);
+      // (the reference's quaternion mask keeps w at 1 for a frozen rotation:
+      // integrators.py's [0] + frozen.rotation; the w update is an exact zero)
+      for (int k = 1; k < 4; k++) jb = jb && bw[BODY_QM + k] == fbits(0.0);
+    }
+    for (int x = 0; x < R && jb; x++) {
+      if (!side[d->row_body_a[x]]) jb = false;
+      if (!side[d->row_body_b[x]] && !d->col_oneway[d->row_group[x]]) jb = false;
+    }
+    S->jb = jb ? 1 : 0;
   }
   // the MULTI kernel is instantiated for the lean feature set (revolute,
   // torque, capsule-plane / capsule-capsule, no forces)
@@ -1107,7 +1154,8 @@ static int env_step_impl(bx_system* S, const bx_env_params* env, int64_t n_envs,
     a.act_out = draw->act_out;
   }
   if (S->mode == 1)
-    HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a, S->fold));
+    HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a,
+                                  S->fold ? (1 | (S->jb ? 2 : 0)) : 0));
   else if (S->mode == 3)  // MULTI-mode systems step envs with the item-loop kernel
     HIP_OK(launch_env_step_generic(S->L, 0, S->feat, S->tpb, n_envs,
                                    (size_t)S->hdr.env_words * 4, as_stream(stream), a));

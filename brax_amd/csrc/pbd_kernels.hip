@@ -2129,6 +2129,7 @@ __device__ __forceinline__ GList<M> load_glist(const Cst& c, int o_off, int o_l,
 template <int M, int MC = M>
 struct Hoist {
   bool hasB, hasJ, hasA, hasR, hasR2;
+  bool own;   // the lane's body counts in per-body sums (JB: one copy per body)
   int r1, r2;  // the rows R and R2 (F_R2: from the lane image; else r1 = lane)
   BodyC B;
   JointC J;
@@ -2145,11 +2146,14 @@ struct Hoist {
 // L2 round trip (the records' own layout needs three dependent ones: list
 // offsets -> entries, joint / row -> the bodies it references).
 // JH (joint halves): lanes j and j + 8 both hold joint j and actuator j.
-template <int M, bool JH, bool R2 = false, int MC = M>
+// JB (JH, the Ant / HalfCheetah env kernels): the lane's body is its side's
+// (parent of joint j on lane j, child on lane j + 8), a copy per side lane
+template <int M, bool JH, bool R2 = false, int MC = M, bool JB = false>
 __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& H, int lane,
                                            Hoist<M, MC>& X) {
+  static_assert(!JB || (JH && MC <= 8), "JB: joint halves, <= 8 contact entries");
   const int jx = JH ? (lane & 7) : lane;
-  X.hasB = lane < H.N;
+  X.hasB = JB ? jx < H.J : lane < H.N;
   X.hasJ = jx < H.J;
   X.hasA = jx < H.K;
   X.hasR = lane < H.R;
@@ -2166,7 +2170,9 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
     }
   };
   constexpr int OJ = JH ? LI_JOINT_H : LI_JOINT, OA = JH ? LI_ACT_H : LI_ACT;
-  grab(LI_BODY, 16);
+  constexpr int OB = JB ? LI_BODY_J : LI_BODY, OJL = JB ? LI_JL_J : LI_JL,
+                OAL = JB ? LI_AL_J : LI_AL, OCL = JB ? LI_CL_J : LI_CL;
+  grab(OB, 16);
   grab(OJ, 48);
   grab(OA, 8);
   grab(LI_ROW, 32);
@@ -2174,9 +2180,9 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
     grab(LI_ROW2, 32);
     grab(LI_RIDX, 4);
   }
-  grab(LI_JL, M);
-  grab(LI_AL, M);
-  grab(LI_CL, MC < 8 ? MC : 8);
+  grab(OJL, M);
+  grab(OAL, M);
+  grab(OCL, MC < 8 ? MC : 8);
   if constexpr (MC > 8) grab(LI_CL2, 8);
   constexpr int OL = JH ? LI_JLIM_H : LI_JLIM;
   grab(OL, 8);
@@ -2184,11 +2190,11 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   auto f = [&](int i) { return __uint_as_float(w[i]); };
   auto f3 = [&](int i) { return mk(f(i), f(i + 1), f(i + 2)); };
   auto n = [&](int i) { return (int)w[i]; };
-  X.B.mass = f(LI_BODY);
-  X.B.I = f3(LI_BODY + 1);
-  X.B.pm = f3(LI_BODY + 4);
-  X.B.rm = f3(LI_BODY + 7);
-  X.B.qm = q4{f(LI_BODY + 10), f(LI_BODY + 11), f(LI_BODY + 12), f(LI_BODY + 13)};
+  X.B.mass = f(OB);
+  X.B.I = f3(OB + 1);
+  X.B.pm = f3(OB + 4);
+  X.B.rm = f3(OB + 7);
+  X.B.qm = q4{f(OB + 10), f(OB + 11), f(OB + 12), f(OB + 13)};
   JointC& J = X.J;
   J.type = n(OJ + LJ_TYPE);
   J.bp = n(OJ + LJ_BP);
@@ -2259,13 +2265,14 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
     X.S.sg = f(LI_SIDE_H + LS_SG);
     X.S.body = n(LI_SIDE_H + LS_BODY);
   }
+  X.own = JB ? (X.hasB && n(LI_SIDE_H + LS_OWN) != 0) : X.hasB;
 #pragma unroll
   for (int k = 0; k < M; k++) {
-    X.jl.e[k] = n(LI_JL + k);
-    X.al.e[k] = n(LI_AL + k);
+    X.jl.e[k] = n(OJL + k);
+    X.al.e[k] = n(OAL + k);
   }
 #pragma unroll
-  for (int k = 0; k < MC; k++) X.cl.e[k] = n(k < 8 ? LI_CL + k : LI_CL2 + k - 8);
+  for (int k = 0; k < MC; k++) X.cl.e[k] = n(k < 8 ? OCL + k : LI_CL2 + k - 8);
 }
 
 // the spherical SINGLE kernels' limit rows into LDS, once per launch (see
@@ -2423,9 +2430,37 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   const uint4* LIP = (F & F_SPH) != 0 ? E.jlim + lane : nullptr;  // staged by stage_lim
   const int jx = lane & 7;         // JH: this lane's joint / actuator
   const bool child = lane >= 8;    // JH: this lane's side
-  float* myqp = E.qp + lane * QP_STRIDE;
+  // JB (the Ant / HalfCheetah env kernels: joint halves, damping folded):
+  // the lane's body is its side's, every side lane updating its own copy
+  // with the same instructions and inputs (the side body's constants and
+  // gather lists), so the copies stay bit-identical and the actuator and
+  // joint phases read the state from registers, not from the LDS record the
+  // previous phase wrote; the records are written where the contact passes,
+  // the observation and the outputs read them (by every copy: same-address
+  // writes of equal values; one writing copy per body measured slower).
+  // Bodies on no joint side are frozen (checked on the host) and keep their
+  // loaded record
+  constexpr bool JB = FOLD && JH;
+  const int bi = JB ? X.S.body : lane;  // the lane's body
+  float* myqp = E.qp + bi * QP_STRIDE;
   QP q;
   if (X.hasB) q = ldqp(myqp);
+  if constexpr (JB) {
+    // the records of bodies on no joint side (frozen, on the plane side of
+    // one-way rows only: checked on the host) as their own lanes would leave
+    // them: the previous-substep slot at their (unchanging) pose, zero contact
+    // sums; the side bodies' copies overwrite their own records below
+    if (lane < H.N) {
+      const float* r = E.qp + lane * QP_STRIDE;
+      const QP o = ldqp(r);
+      st_slot(E.prev + lane * PREV_STRIDE, o.pos, o.rot, 0.f);
+      st_rb(E.rb + lane * RB_STRIDE, o.pos, o.vel, o.ang);
+      float* acc = E.acc + lane * ACC_STRIDE;
+      st3(acc + ACC_ICV, mk(0.f, 0.f, 0.f));
+      st3(acc + ACC_ICA, mk(0.f, 0.f, 0.f));
+      st3(acc + ACC_IAA, mk(0.f, 0.f, 0.f));
+    }
+  }
   icv = mk(0.f, 0.f, 0.f);
   ica = mk(0.f, 0.f, 0.f);
   iaa = mk(0.f, 0.f, 0.f);
@@ -2455,12 +2490,18 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     for (int sub = 0; sub < 2; sub++) {
       ppos = q.pos;
       prot = q.rot;
-      if (sub == 1 && X.hasB) st_slot(E.prev + lane * PREV_STRIDE, ppos, prot, 0.f);
+      if (sub == 1 && X.hasB) st_slot(E.prev + bi * PREV_STRIDE, ppos, prot, 0.f);
       // actuators + damping (actuator a drives joint a when H.act_same)
       if constexpr (JH) {
         // one side of joint / actuator jx per lane (act_same, checked on the host)
         const int jb = X.S.body;
-        if constexpr (FOLD) {
+        if constexpr (JB) {
+          // the partner lane holds the joint's other body
+          const JointC& Jc = X.J;
+          const v3 oa = xh3(q.ang);
+          const v3 tqd = -1.f * Jc.damping * (sel3(child, oa, q.ang) - sel3(child, q.ang, oa));
+          if (X.hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, q.rot, &tqd);
+        } else if constexpr (FOLD) {
           const JointC& Jc = X.J;
           const v3 tqd = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
           if (X.hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE), &tqd);
@@ -2510,7 +2551,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
         q4 r = q.rot + quat_mul(hq, q.rot);
         q.rot = (FOLD && JH) ? qnormalize_bare(r) : qnormalize(r);  // Ant env kernel: bare sqrt
-        stqp(myqp, q);
+        if (!JB) stqp(myqp, q);  // JB: the joint phase takes the lane's copy
         dpa_last = dpa;
       }
       sync();
@@ -2518,7 +2559,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       if constexpr (JH) {
         if (X.hasJ) {
           const JointC& Jc = X.J;
-          QP o = ldqp(E.qp + X.S.body * QP_STRIDE);
+          const QP o = JB ? q : ldqp(E.qp + X.S.body * QP_STRIDE);
           v3 dpo;
           q4 dro;
           joint_apply_half(Jc, X.JL, X.S, child, o, dpo, dro);
@@ -2551,7 +2592,8 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                    q.rot.z + dr.z * X.B.qm.z};
         if (sub == 0) vproj(q, ppos, prot, X.B, h, FOLD && JH);
-        stqp(myqp, q);
+        // JB: the record is read next by the contact passes (after sub 1)
+        if (!JB || sub == 1) stqp(myqp, q);
       }
       sync();
       BX_STAMP(3);
@@ -2630,7 +2672,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       q.pos = q.pos + mul(dp, X.B.pm);
       q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                  q.rot.z + dr.z * X.B.qm.z};
-      st_rb(E.rb + lane * RB_STRIDE, q.pos, q.vel, q.ang);
+      st_rb(E.rb + bi * RB_STRIDE, q.pos, q.vel, q.ang);
       vproj(q, ppos, prot, X.B, h, FOLD && JH);
       stqp(myqp, q);
     }
@@ -2673,7 +2715,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     BX_STAMP(7);
   }
   if (X.hasB) {
-    float* acc = E.acc + lane * ACC_STRIDE;
+    float* acc = E.acc + bi * ACC_STRIDE;
     st3(acc + ACC_ICV, icv);
     st3(acc + ACC_ICA, ica);
     st3(acc + ACC_IAA, iaa);
@@ -3882,7 +3924,9 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   const int64_t el = valid ? e : 0;
   Hoist<M, cl_width<F, M>()> X;
   if constexpr (S) {
-    load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>()>(A.blob, H, lane, X);
+    // JB: the env-program kernels with joint halves (pbd_step_single's FOLD && JH)
+    load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>(),
+               (F & F_JH) != 0 && EK != EK_ANY>(A.blob, H, lane, X);
     stage_lim<L, F>(A.blob, H, E, lane);
   }
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
@@ -4100,7 +4144,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     float ccs = 0.f;
     if constexpr (S && EK == EK_ANT && L == 16) {
       const v3 cv = mk(clip1(icv.x), clip1(icv.y), clip1(icv.z));
-      ccs = row_sum16(X.hasB ? cv.x * cv.x + cv.y * cv.y + cv.z * cv.z : 0.f);
+      ccs = row_sum16(X.own ? cv.x * cv.x + cv.y * cv.y + cv.z * cv.z : 0.f);
     }
     // reward / done / metrics (lane 0 of the env)
     if (lane == 0 && valid) {
@@ -4775,8 +4819,10 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
   // the benchmarked envs get kernels holding only their own env program
   const int k = a.P.kind;
   // (their kernels fold each joint's damping into its actuator's slot: fold
-  // = every joint j has torque actuator j)
-  if (fold && L == 16 && gw <= 4 && k == BX_ENV_ANT && feat == (F_G1 | F_JH)) {
+  // bit 0 = every joint j has torque actuator j; the joint-halves kernels
+  // also give each side lane its body's copy: bit 1 = the system allows it)
+  const bool jb = (fold & 2) != 0;
+  if (fold && jb && L == 16 && gw <= 4 && k == BX_ENV_ANT && feat == (F_G1 | F_JH)) {
     // past one wave per SIMD: the register-capped kernels
     const bool wide = (int64_t)grid.x * (tpb / 64 > 0 ? tpb / 64 : 1) > 4 * (int64_t)cu_count();
     // (a packed single step at a wide batch takes the wide rollout kernel)
@@ -4805,7 +4851,7 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
   // HalfCheetah: 16 one-way ground rows in slot 1, the feet's capsule-capsule
   // row in slot 2 (F_R2 | F_R2G), joint halves
   constexpr int F_CHEETAH = F_CC | F_TW | F_JH | F_R2 | F_R2G;
-  if (fold && L == 16 && gw <= 4 && k == BX_ENV_HALFCHEETAH && (feat & ~F_G1) == F_CHEETAH) {
+  if (fold && jb && L == 16 && gw <= 4 && k == BX_ENV_HALFCHEETAH && (feat & ~F_G1) == F_CHEETAH) {
     if (a.n_steps > 1)
       launch_one<EnvArgs>(env_rollout_kernel<16, 1, F_CHEETAH, 4, EK_CHEETAH>, grid, tpb, lds, s, a);
     else if (a.packed)

@@ -128,12 +128,20 @@ enum {
   LI_ROW2 = 232,    // F_R2: the lane's second contact row (LR_*)
   LI_RIDX = 264,    // F_R2: the indices of the lane's two rows (-1: none)
   LI_CL2 = 268,     // F_C16: contact gather-list entries 8..15
-  LANE_W = 276
+  // JB (joint halves own body copies, the Ant / HalfCheetah env kernels): the
+  // body record and gather lists of the lane's SIDE body (LS_BODY)
+  LI_BODY_J = 276,
+  LI_JL_J = 292,
+  LI_AL_J = 300,
+  LI_CL_J = 308,
+  LANE_W = 316
 };
 // a joint-halves lane's side (lanes 8-15: the child's): its anchor offset,
 // hinge axis and reference axis in its body's frame, that body's inverse
-// inertia and mass, the side's sign (+1 parent, -1 child) and the body
-enum { LS_OFF = 0, LS_AX0 = 3, LS_AX2 = 6, LS_I = 9, LS_M = 12, LS_SG = 13, LS_BODY = 14 };
+// inertia and mass, the side's sign (+1 parent, -1 child) and the body;
+// LS_OWN: 1 on the lowest lane whose side is that body (JB: the copy that
+// counts in per-body sums)
+enum { LS_OFF = 0, LS_AX0 = 3, LS_AX2 = 6, LS_I = 9, LS_M = 12, LS_SG = 13, LS_BODY = 14, LS_OWN = 15 };
 // a limit row [lo, hi] as the SINGLE-mode kernels test it: the
 // pseudo-angles of the limits (a monotone stand-in for atan2 over (-pi, pi],
 // +-3 past +-pi) and their cosines / sines

@@ -1,4 +1,4 @@
-"""Diagnostic: one library build's Ant / Humanoid rollouts (4096 envs, 20
+"""Diagnostic: one library build's Ant / Humanoid / HalfCheetah rollouts (4096 envs, 20
 steps, fixed seeds) saved for a bitwise comparison between builds.
 
   BRAX_AMD_LIB=<lib> python tools/bitcmp.py save <out.npz>
@@ -17,7 +17,7 @@ def save(path):
   from brax_amd import envs
   dev = torch.device('cuda', 0)
   out = {}
-  for name in ('ant', 'humanoid'):
+  for name in ('ant', 'humanoid', 'halfcheetah'):
     env = envs.create(name, batch_size=4096, episode_length=1000, auto_reset=True, device=dev)
     st = env.reset(np.array([0, 7], np.uint32))
     g = torch.Generator(dev).manual_seed(3)
