@@ -488,9 +488,9 @@ def main():
   for k in range(args.steps):
     state = one_step(state, args.warmup + k)
   torch.cuda.synchronize()
-  if dist is not None:
+  if dist is not None:  # (one rank: the synchronisation above is the bracket)
     dist.barrier()
-  torch.cuda.synchronize()
+    torch.cuda.synchronize()
   elapsed = time.perf_counter() - t0
   gc.enable()
   eager_elapsed = elapsed
@@ -537,9 +537,9 @@ def main():
       if advance_hook is not None:
         advance_hook(K)  # the RCCL all-gather once per period, on the host
     torch.cuda.synchronize()
-    if dist is not None:
+    if dist is not None:  # (one rank: the synchronisation above is the bracket)
       dist.barrier()
-    torch.cuda.synchronize()
+      torch.cuda.synchronize()
     el = time.perf_counter() - t0
     gc.enable()
     return el, (exchange.flushes if exchange is not None else 0), n_warm
