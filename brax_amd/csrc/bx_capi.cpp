@@ -799,7 +799,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     // contact rows only as the plane side of one-way rows (its record then
     // never changes and its contact sums are zeros); no forces (they index
     // bodies by lane)
-    bool jb = S->fold && (f & 128) && !(f & 16) && L == 16;
+    // (BX_NO_JB=1: off, the Ant / HalfCheetah kinds then take the all-kinds
+    // kernel; the GPU tests run that fallback against the goldens too)
+    const bool jb_off = getenv("BX_NO_JB") && atoi(getenv("BX_NO_JB"));
+    bool jb = S->fold && (f & 128) && !(f & 16) && L == 16 && !jb_off;
     std::vector<char> side(N, 0);
     for (int j = 0; j < J; j++) side[d->joint_body_p[j]] = side[d->joint_body_c[j]] = 1;
     for (int b = 0; b < N && jb; b++) {
