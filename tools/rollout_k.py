@@ -6,7 +6,7 @@ torch.cuda.synchronize() (what a one-launch timed region sees), so the
 launch's cost splits into K x per-step + a fixed part (prologue, slowest-wave
 tail, launch and completion latency).
 
-    python tools/rollout_k.py [K ...]
+    python tools/rollout_k.py [--spin] [K ...]
 """
 import json
 import os
@@ -15,6 +15,13 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+SPIN = '--spin' in sys.argv
+if SPIN:
+  # hipDeviceScheduleSpin (1) before the context exists: host waits spin
+  import ctypes
+  sys.argv.remove('--spin')
+  print('hipSetDeviceFlags(spin) ->', ctypes.CDLL('libamdhip64.so').hipSetDeviceFlags(ctypes.c_uint(1)))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
