@@ -116,10 +116,14 @@ class EpisodeExchange:
   def flush(self):
     """All-gathers the sums since the last exchange, resets them and returns
     the gathered (world, 2, B) sums (a fresh tensor per flush)."""
-    if self._nccl:
-      out = torch.empty_like(self.out)
-      dist.all_gather_into_tensor(out, self.acc, group=self.group)
-    else:
+    if self._nccl or self.acc.device.type == 'cpu':
+      # one all_gather_into_tensor into the ranks' sums concatenated along
+      # dim 0: RCCL's call on the device, and the same call on gloo with host
+      # tensors, which is how the CPU tests run this path
+      flat = torch.empty((self.world * 2, self.B), dtype=self.acc.dtype, device=self.acc.device)
+      dist.all_gather_into_tensor(flat, self.acc, group=self.group)
+      out = flat.view(self.world, 2, self.B)
+    else:  # gloo with device tensors (the one-GPU rehearsal of the N-rank bench)
       parts = list(torch.empty_like(self.out).unbind(0))
       dist.all_gather(parts, self.acc.clone(), group=self.group)
       out = torch.stack(parts)
