@@ -1,21 +1,25 @@
 """Benchmark: env-steps/sec of Ant at 4096 envs per GPU (BASELINE.json).
 
 One step = a fresh (B, 8) slab of synthetic U[-1,1] actions drawn on the
-device by the counter RNG (`bx_uniform`, the reference's published loop draws
-one per step, notebooks/environments.ipynb:386-423) + one `Env.step` of
-`envs.create('ant', batch_size=B, episode_length=1000, auto_reset=True)`,
-i.e. ONE fused kernel launch doing 10 PBD substeps + observation + reward +
-Episode/AutoReset. Inputs are resident in HBM.
+device by the counter RNG (keyed by step and global env id; the reference's
+published loop draws one per step, notebooks/environments.ipynb:386-423) + one
+`Env.step` of `envs.create('ant', batch_size=B, episode_length=1000,
+auto_reset=True)`: 10 PBD substeps + observation + reward + Episode/AutoReset.
+Inputs are resident in HBM.
 
-The timed loop runs twice: first as a plain Python loop (reported as
-`eager_loop`), then as replays of a hipGraph holding K of those steps (K =
-steps up to 200, else gcd(steps, 50); `brax_amd.envs.graph.StepGraph`): per
-replay ONE launch draws the K action slabs (each bit-identical to the eager
-loop's draw of that step, offset advanced by a device epoch counter), then K
-fused Env.step kernels. `value` is the graph loop: on a slow host the Python
-loop's ~20 us per step otherwise leaves the GPU idle between 29 us kernels.
-Before the timed loops, a 200-launch train of the step kernel alone
-(`roofline.kernel_ms`) and warm graph replays bring the clocks up.
+`value` is the `direct` loop, by design: `RolloutRunner`, ONE
+`bx_env_rollout_random` launch per K steps (K = steps up to 200, else
+gcd(steps, 50)) that draws each step's actions inside the kernel and steps
+every env K times, the state read in place from the previous launch's last
+step (the reference's lax.scan of env.step with the random actions drawn in
+the loop). The other loops are reported beside it for the record:
+`eager_loop` (Python: bx_uniform + Env.step per step), `graph_loop`
+(StepGraph: a hipGraph of one draw + K Env.step launches: the closed-loop
+per-step path) and `rollout_loop` (RolloutGraph: a hipGraph of one draw + one
+bx_env_rollout_packed launch). Only if the direct loop cannot run is `value`
+taken from the next loop in that order, and `timed_loop` says which.
+`roofline.kernel_ms` times the headline loop's own launch (back-to-back
+RolloutRunner.run() calls bracketed by HIP events on their stream).
 
     python bench.py [--gpus N --steps K --warmup W --batch B]
     torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU)
@@ -77,7 +81,10 @@ def graph_steps(steps):
 
 def _dist():
   ws = int(os.environ.get('WORLD_SIZE', '1'))
-  if ws > 1:
+  # BX_DIST_FORCE=1: the process group (and the episodic RCCL exchange) even
+  # at world size 1, e.g. `torchrun --nproc-per-node 1`: the one-GPU box then
+  # executes the N-GPU run's collective path on RCCL
+  if ws > 1 or os.environ.get('BX_DIST_FORCE') == '1':
     import torch.distributed as dist
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -285,12 +292,21 @@ def secondary_configs(dev, steps=50):
 
     def mstep():
       qp[0], _ = sys_.step(qp[0], a)
+
+    def mstep_noinfo():
+      qp[0], _ = sys_.step(qp[0], a, info=False)
     n = max(steps // 5, 5)
     wall, gpu = _time(mstep, n, 2)
     out[f'mountain4_2048_cutoff{cutoff}'] = {
         'value': Bm * n / wall, 'unit': 'env-steps/s (System.step)',
         'ms_per_step': wall * 1e3 / n, 'gpu_ms_per_step': gpu * 1e3 / n,
         'contact_rows': sys_.num_rows, 'lanes_per_env': sys_.lanes}
+    # the same steps without Info (System.step(..., info=False): the state
+    # only, as jit drops the Info a caller ignores)
+    wall, gpu = _time(mstep_noinfo, n, 2)
+    out[f'mountain4_2048_cutoff{cutoff}_noinfo'] = {
+        'value': Bm * n / wall, 'unit': 'env-steps/s (System.step, no Info)',
+        'ms_per_step': wall * 1e3 / n, 'gpu_ms_per_step': gpu * 1e3 / n}
   return out
 
 
@@ -346,27 +362,24 @@ def clone_state(st):
                     reward=st.reward.clone(), done=st.done.clone(), info=info)
 
 
-def rollout_train(env, state, k, n=20):
-  """Per-step duration of the open-loop rollout kernel alone: `n`
-  back-to-back `bx_env_rollout_packed` launches of `k` steps (one fixed
-  action block, outputs to one buffer) bracketed by HIP events on their
-  stream, divided by n * k."""
-  from brax_amd.envs.rollout import rollout
-  B = state.qp.pos.shape[0]
-  acts = torch.rand((k, B, env.action_size), device=state.qp.pos.device) * 2 - 1
-  u = env.unwrapped
-  out = torch.empty((k * B * (u.sys.num_bodies * 16 + u.obs_size + 4 + len(u.metric_keys)),),
-                    device=state.qp.pos.device)
+def runner_train(env, state, k, n=20):
+  """Per-step duration of the headline loop's own launch: `n` back-to-back
+  `RolloutRunner.run()` calls of `k` steps (one `bx_env_rollout_random`
+  launch each, the actions drawn inside it, each launch reading the previous
+  one's last step in place) bracketed by HIP events on the stream they run on,
+  divided by n * k. Returns (ms per step, the runner's `draw`)."""
+  from brax_amd.envs.rollout import RolloutRunner
+  r = RolloutRunner(env, state, k, seed=1)
   for _ in range(3):
-    rollout(env, state, acts, out=out)
+    r.run()
   torch.cuda.synchronize()
   a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
   a.record()
   for _ in range(n):
-    rollout(env, state, acts, out=out)
+    r.run()
   b.record()
   torch.cuda.synchronize()
-  return a.elapsed_time(b) / (n * k)
+  return a.elapsed_time(b) / (n * k), r.draw
 
 
 def src_sha1():
@@ -455,7 +468,7 @@ def main():
   # timed step count when shorter, so every timed region holds >= 1 collective
   K = graph_steps(args.steps)
   period = bd.exchange_period(1000, args.steps, K)
-  exchange = bd.EpisodeExchange(B, dev, every=period) if world > 1 else None
+  exchange = bd.EpisodeExchange(B, dev, every=period) if dist is not None else None
 
   def one_step(st, k):
     # the step's action slab, keyed by (step, global env id): drawn on the
@@ -587,7 +600,8 @@ def main():
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     for k, v in zip(KINDS, t.tolist()):
       loops[k] = (float(v) if v >= 0 else None,) + loops[k][1:]
-  best = min((k for k in loops if loops[k][0] is not None), key=lambda k: loops[k][0])
+  # the headline is the direct loop by design; another loop only if it failed
+  best = next(k for k in ('direct', 'rollout', 'step', 'eager') if loops[k][0] is not None)
   elapsed, collectives = loops[best][0], loops[best][1]
   eager_elapsed = loops['eager'][0]
 
@@ -599,11 +613,14 @@ def main():
   # the dominant kernel of the timed loop: the K-step rollout kernel (one
   # launch = K x B env-steps) or the single-step kernel (one launch = B
   # env-steps); achieved = algorithmic flops (bytes) per launch / launch time
+  direct_draw = None
   if best in ('rollout', 'direct'):
     kname, spl = ANT_ROLLOUT_KERNEL, K
-    kern_ms = rollout_train(env, state, K) * K
-    kern_src = (f'HIP events over 20 back-to-back {K}-step bx_env_rollout_packed launches on '
-                'the launch stream (rollout_train)')
+    ms_step, direct_draw = runner_train(env, state, K)
+    kern_ms = ms_step * K
+    kern_src = (f'HIP events over 20 back-to-back {K}-step RolloutRunner.run() launches '
+                f'({"bx_env_rollout_random: actions drawn inside the launch" if direct_draw else "bx_uniform_slabs + bx_env_rollout_packed"}) '
+                'on the launch stream (runner_train): the headline loop\'s own launch')
   else:
     kname, spl = ANT_KERNEL, 1
     kern_src = ('HIP events over 200 back-to-back bx_env_step_packed launches on the launch '
@@ -645,18 +662,23 @@ def main():
                  'launch': {
                      'rollout': f'hipGraph replays of one on-device draw of {K} action slabs + '
                                 f'one {K}-step open-loop rollout launch (bx_env_rollout_packed)',
-                     'direct': f'per {K} steps: one on-device draw of {K} action slabs '
-                               f'(bx_uniform_slabs) + one {K}-step open-loop rollout launch '
-                               '(bx_env_rollout_packed), launched directly from prebuilt C '
-                               'arguments, the state read in place from the previous launch\'s '
-                               'last step (RolloutRunner)',
+                     'direct': (f'per {K} steps: ONE {K}-step open-loop rollout launch that '
+                                'draws each step\'s actions inside the kernel '
+                                '(bx_env_rollout_random), launched directly from prebuilt C '
+                                'arguments, the state read in place from the previous launch\'s '
+                                'last step (RolloutRunner)' if direct_draw else
+                                f'per {K} steps: one on-device draw of {K} action slabs '
+                                f'(bx_uniform_slabs) + one {K}-step open-loop rollout launch '
+                                '(bx_env_rollout_packed), launched directly from prebuilt C '
+                                'arguments (RolloutRunner)'),
                      'step': f'hipGraph replays of one on-device draw of {K} action slabs + {K} '
                              'fused Env.step launches (+ the episodic sum per step when N>1)',
                      'eager': 'a Python loop of bx_uniform + Env.step per step'}[best],
                  'envs_per_gpu': B, 'episode_length': 1000, 'substeps': 10,
                  'steps_per_launch': K if best != 'eager' else 1,
                  'parallelism': f'env-shard x{world}',
-                 'exchange_period': period if world > 1 else None},
+                 'exchange_period': period if exchange is not None else None,
+                 'dist_backend': dist.get_backend() if dist is not None else None},
       # RCCL all-gathers of the episodic (reward, done) sums inside the timed
       # region (0 at N = 1: there is no collective on one GPU)
       'collectives_in_timed_region': collectives,
@@ -688,6 +710,8 @@ def main():
     out[key] = ({'value': total / el, 'unit': 'env-steps/s', 'ms_per_step': el * 1e3 / args.steps,
                  'collectives_in_timed_region': col} if el is not None else {'error': err})
   out['timed_loop'] = best
+  out['timed_loop_policy'] = ('the direct loop by design (RolloutRunner); rollout, step, eager '
+                              'only when it could not run')
   out['warmup_policy'] = (f'{args.warmup} warm-up steps; each replayed loop warms on >= '
                           f'{WARM_S * 1e3:.0f} ms of its own untimed replays (steady-state clocks)')
   out['secondary_configs'] = None if args.no_secondary else secondary_configs(dev)

@@ -2392,6 +2392,17 @@ __device__ unsigned long long bx_stamp_wave[4096][16];
     if ((k) == 14 && threadIdx.x == 0)                                             \
       for (int _i = 0; _i < 5; _i++) bx_stamp_wave[blockIdx.x & 4095][10 + _i] += kst_acc[_i]; \
   } while (0)
+#elif defined(BX_PHASE_MARKS)
+// static per-phase instruction mix (diagnostic, tools/phase_mix.py): the
+// stamp points as assembly comments the scheduler does not move code across
+#define BX_STAMP(k)                                                                \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    asm volatile(";BXPHASE " #k ::: "memory");                                     \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+  } while (0)
+#define BX_KSTAMP_DECL
+#define BX_KSTAMP(k) BX_STAMP(k)
 #else
 #define BX_STAMP(k) do {} while (0)
 #define BX_KSTAMP_DECL
@@ -2915,6 +2926,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
 #endif
   const float h = H.h;
   const v3 g = mk(H.gx, H.gy, H.gz);
+  const bool info_rows = io.pos || io.normal || io.pen || io.cell;
   float* myqp = E.qp + lane * QP_STRIDE;
   QP q;
   if (X.hasB) q = ldqp(myqp);
@@ -3046,8 +3058,11 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
 #if defined(BX_MULTI_HOIST_ROWS)
     const bool bph = false;
 #else
-    // (culled scenes skip it: NearNeighbors already keeps only near cells)
-    const bool bph = H.o_bimg != 0 && H.n_nn == 0 && it + 1 < H.substeps / 2;
+    // (culled scenes skip it: NearNeighbors already keeps only near cells).
+    // Without contact-row Info (System.step(..., info=False): no caller
+    // reads the rows) the last pass takes it too: its far rows' Info is never
+    // written
+    const bool bph = H.o_bimg != 0 && H.n_nn == 0 && (it + 1 < H.substeps / 2 || !info_rows);
 #endif
     int nwork = nact;
     if (bph) {
@@ -3196,7 +3211,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
     BX_MSTAMP(8);
   }
   // Info contact rows of the last position pass (system.py:36-43)
-  if (valid) {
+  if (valid && info_rows) {
 #pragma unroll
     for (int m = 0; m < MR; m++) {
 #if defined(BX_MULTI_HOIST_ROWS)

@@ -85,11 +85,11 @@ def rollout(env, state: State, actions, out: Optional[torch.Tensor] = None
     qbuf = torch.zeros(state.qp.pos.shape[:-1] + (16,), dtype=torch.float32, device=dev)
     for lo, f in ((0, state.qp.pos), (3, state.qp.rot), (7, state.qp.vel), (10, state.qp.ang)):
       qbuf[..., lo:lo + f.shape[-1]] = f
-  if qbuf.dtype != torch.float32 or not qbuf.is_cuda or not qbuf.is_contiguous():
-    qbuf = qbuf.contiguous().float()
+  if qbuf.dtype != torch.float32 or qbuf.device != dev or not qbuf.is_contiguous():
+    qbuf = qbuf.to(dev, torch.float32).contiguous()
   B = qbuf.shape[0]
   act = actions
-  if type(act) is not torch.Tensor or act.dtype != torch.float32 or not act.is_cuda:
+  if type(act) is not torch.Tensor or act.dtype != torch.float32 or act.device != dev:
     act = torch.as_tensor(act, dtype=torch.float32, device=dev)
   if act.dim() != 3 or act.shape[1] != B or act.shape[2] != u.action_size:
     raise ValueError(f'actions {tuple(act.shape)} != (K, {B}, {u.action_size})')
@@ -114,8 +114,9 @@ def rollout(env, state: State, actions, out: Optional[torch.Tensor] = None
   block = B * (N * 16 + O + 4 + M)
   if out is None:
     out = torch.empty((K * block,), dtype=torch.float32, device=dev)
-  elif out.numel() < K * block or out.dtype != torch.float32 or not out.is_contiguous():
-    raise ValueError(f'out must hold {K * block} contiguous float32')
+  elif (out.numel() < K * block or out.dtype != torch.float32 or not out.is_contiguous()
+        or out.device != dev):
+    raise ValueError(f'out must hold {K * block} contiguous float32 on {dev}')
   rng_out = torch.empty((K, B), dtype=torch.int32, device=dev) if rng_in is not None else None
   _native.check(_native.lib().bx_env_rollout_packed(
       u.sys._h, C.byref(p), B, K, qbuf.data_ptr(), done_in.data_ptr(),  # pylint: disable=protected-access

@@ -235,13 +235,27 @@ class System:
         _stream(self.device.index)))
     return out if batched else out[0]
 
-  def step(self, qp: QP, act):
-    """`System.step` (system.py:244-325): (QP, act) -> (QP, Info)."""
+  def step(self, qp: QP, act, info: bool = True):
+    """`System.step` (system.py:244-325): (QP, act) -> (QP, Info).
+
+    info=False: (QP, None) -- the step without its Info outputs (the per-body
+    contact / actuator sums and the per-row contact_pos / normal /
+    penetration), for callers that read only the state, as XLA drops Info
+    under jit when the caller ignores it. The state is the same bits; the
+    large-scene kernel also skips the contact math of far capsule pairs on
+    the step's last collision pass (their rows would only feed Info)."""
     batched = qp.pos.dim() == 3
     B = qp.pos.shape[0] if batched else 1
     act = self._act(act, B)
     lead = (B,) if batched else ()
     out = self._new_qp(lead)
+    if not info:
+      qi = qp_struct(qp, batched)
+      qo = qp_struct(out, batched)
+      _native.check(_native.lib().bx_system_step(
+          self._h, B, C.byref(qi), C.c_void_p(act.data_ptr()), act.stride(0), act.shape[1],
+          C.byref(qo), None, _stream(self.device.index)))
+      return out, None
     N, R = self.num_bodies, self.num_contacts
     spring = int(self.desc.get('dynamics_mode', 0)) == abi.DYN_LEGACY_SPRING
     cbuf = torch.empty(lead + (N, 18 if spring else 12), dtype=torch.float32, device=self.device)

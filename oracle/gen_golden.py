@@ -534,6 +534,36 @@ class stable_top_k:
     self.jp.top_k = self.orig
 
 
+class jit_index_update:
+  """jumpy.index_update (`jumpy.py:161-167`) with jit's scatter semantics:
+  under jit `x.at[idx].set(y)` drops the index tuples that fall outside x
+  (XLA scatter), where the numpy path raises IndexError. NearNeighbors sets its
+  allowed cells with BODY indices into the (U, U) candidate matrix
+  (`colliders.py:63-67`); in Ant Mountain(2+) the last ants' bodies index past
+  U, so only the jit semantics construct the scene. Used for mountain4nn."""
+
+  def __enter__(self):
+    from brax import jumpy
+    self.jp, self.orig = jumpy, jumpy.index_update
+
+    def index_update(x, idx, y):
+      if jumpy._which_np(x, idx, y) is not np or not isinstance(idx, tuple):  # pylint: disable=protected-access
+        return self.orig(x, idx, y)
+      shape = np.shape(x)
+      ii = [np.asarray(i) for i in idx]
+      keep = np.ones(np.broadcast(*ii).shape, bool)
+      for i, n in zip(ii, shape):
+        keep &= (i >= -n) & (i < n)
+      x = np.copy(x)
+      x[tuple(np.broadcast_to(i, keep.shape)[keep] for i in ii)] = y
+      return x
+    jumpy.index_update = index_update
+    return self
+
+  def __exit__(self, *exc):
+    self.jp.index_update = self.orig
+
+
 def wrapped_ant(n_envs=8, n_steps=6, episode_length=3, action_repeat=1):
   """Episode + AutoReset wrapped Ant (`envs/__init__.py:74-92`); with
   action_repeat > 1 the EpisodeWrapper scans that many env steps per step
@@ -751,6 +781,15 @@ def main():
     s = ant_mountain_sys(1, cutoff=9)
     save('desc_mountain1nn', dump_desc(s))
     save('traj_mountain1nn', sys_traj(s, 'mountain1nn', s.default_qp(), 4, 4, 1.0, 8))
+  # BASELINE configs[4]'s culled leg: Ant Mountain(4), cutoff 36 (9 per ant,
+  # `notebooks/multiagent.ipynb:87-115`), the scene the MULTI kernel runs;
+  # jit's scatter for the out-of-range allowed cells, jax.lax.top_k's tie order
+  if want('mountain4nn'):
+    with jit_index_update():
+      s = ant_mountain_sys(4, cutoff=36)
+    save('desc_mountain4nn', dump_desc(s))
+    with stable_top_k():
+      save('traj_mountain4nn', sys_traj(s, 'mountain4nn', s.default_qp(), 4, 3, 1.0, 32))
   # short-horizon twins of the reference's long physics-test scenes: the same
   # bodies at the Ant's dt 0.05 / 10 substeps, from `burn` zero-action steps
   # past default_qp (falling into contact), 8 steps recorded, so the fp32

@@ -165,7 +165,7 @@ def config_for(name):
   if name == 'twin_cull':
     from oracle import scenes
     return cfgmod.parse(scenes.TWIN_CULL_CONFIG)
-  if name in ('mountain1nn', 'mountain2nn'):
+  if name in ('mountain1nn', 'mountain2nn', 'mountain4nn'):
     n = int(name[len('mountain')])
     cfg = ant_mountain_config(n)
     cfg.collider_cutoff = 9 * n

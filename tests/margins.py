@@ -10,10 +10,11 @@ import os
 _MARGINS = []
 
 
-def record_margin(field, measured, tol):
+def record_margin(field, measured, tol, **extra):
+  """`extra`: e.g. `n`, the samples the gate covered."""
   test = os.environ.get('PYTEST_CURRENT_TEST', '?').split(' ')[0]
   _MARGINS.append({'test': test, 'field': field, 'measured': measured, 'tol': tol,
-                   'ratio': measured / tol if tol > 0 else None})
+                   'ratio': measured / tol if tol > 0 else None, **extra})
 
 
 def write(path):
@@ -27,4 +28,8 @@ def write(path):
   rows = sorted(worst.values(), key=lambda m: -(m['ratio'] or 0))
   os.makedirs(os.path.dirname(path), exist_ok=True)
   with open(path, 'w') as f:
-    json.dump({'n_gates': len(_MARGINS), 'worst_per_test_field': rows}, f, indent=1)
+    # the gates whose bound exceeds 1e-2 (Brax's own fp32 off by > 5e-3 on
+    # their samples): the ill-conditioned groups and the reset-lift obs
+    wide = [m for m in rows if m['tol'] > 1e-2]
+    json.dump({'n_gates': len(_MARGINS), 'n_wide_gates': len(wide), 'wide_gates': wide,
+               'worst_per_test_field': rows}, f, indent=1)

@@ -7,7 +7,7 @@ from tests.conftest import golden
 from tests.helpers import (CAPSULES, NN_MASKED, POINTS, ROBOTS, SPRING_ENVS, SPRING_ROBOTS, XCOL, compiled,
                            config_for)
 
-NAMES = (['ant', 'humanoid', 'halfcheetah', 'humanoidstandup', 'mountain1', 'mountain2', 'mountain4', 'mountain1nn']
+NAMES = (['ant', 'humanoid', 'halfcheetah', 'humanoidstandup', 'mountain1', 'mountain2', 'mountain4', 'mountain1nn', 'mountain4nn']
          + ROBOTS + CAPSULES + NN_MASKED + POINTS + SPRING_ENVS + SPRING_ROBOTS + XCOL)
 
 

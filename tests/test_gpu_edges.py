@@ -104,3 +104,29 @@ def test_scene_past_lds_is_refused(dev):
   from brax_amd.envs.mountain import ant_mountain_config
   with pytest.raises((NativeError, ValueError), match='LDS|too many|large'):
     brax_amd.System(ant_mountain_config(32), device=dev)
+
+
+@pytest.mark.parametrize('name,cutoff', [('ant', 0), ('humanoid', 0), ('mountain4', 0),
+                                         ('mountain4', 36), ('capsule_cull', 0)])
+def test_step_without_info_is_the_same_state(dev, name, cutoff):
+  """`System.step(qp, act, info=False)` (no Info outputs: the large-scene
+  kernel also skips far capsule pairs on its last collision pass, whose rows
+  only feed Info) steps to the bits of the full step, for the SINGLE,
+  item-loop and MULTI kernels."""
+  import brax_amd
+  cfg = config_for(name)
+  if cutoff:
+    cfg.collider_cutoff = cutoff
+  sys_ = brax_amd.System(cfg, device=dev)
+  B = 64
+  q0 = sys_.default_qp()
+  qp = brax_amd.QP(*(t.unsqueeze(0).expand((B,) + t.shape).contiguous()
+                     for t in (q0.pos, q0.rot, q0.vel, q0.ang)))
+  g = torch.Generator(dev).manual_seed(4)
+  for _ in range(3):
+    act = torch.rand((B, max(sys_.action_size, 1)), device=dev, generator=g) * 2 - 1
+    a, info = sys_.step(qp, act)
+    b, none = sys_.step(qp, act, info=False)
+    assert info is not None and none is None
+    _same(a, b)
+    qp = a

@@ -152,8 +152,17 @@ def test_body_placing_reset_is_one_call(dev, name):
   for f in ('pos', 'rot', 'vel', 'ang'):
     a, b = getattr(st.qp, f), getattr(ref.qp, f)
     assert torch.allclose(a, b, atol=2e-6, rtol=1e-6), (f, float((a - b).abs().max()))
-  # the joint noise is the same draw, bit for bit: rotations and velocities
-  # of the arm come from the same angles
+  # the joint noise is the same draw, bit for bit: every body the reset does
+  # not place (the joint tree's, from the same angles through the same
+  # default_qp kernel) is bit-identical; only the placements, formed on the
+  # host in float64 on the explicit path, may differ by rounding
+  from tests.helpers import reset_bodies
+  placed = {env.sys._body_index[b] for b in reset_bodies(name)}  # pylint: disable=protected-access
+  assert placed or name == 'grasp'
+  keep = [b for b in range(env.sys.num_bodies) if b not in placed]
+  for f in ('pos', 'rot', 'vel', 'ang'):
+    a, b = getattr(st.qp, f)[:, keep], getattr(ref.qp, f)[:, keep]
+    assert torch.equal(a, b), (f, float((a - b).abs().max()))
   assert torch.allclose(st.obs, ref.obs, atol=1e-5, rtol=1e-5)
   assert float(st.reward.abs().max()) == 0 and float(st.done.abs().max()) == 0
   if getattr(env, 'needs_rng', False):

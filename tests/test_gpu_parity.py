@@ -33,7 +33,7 @@ ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
 # 400-10,000 substeps per step, resting contacts at their gates) have an O(1)
 # fp32 envelope, so a state gate there tests nothing: they stay KATs below,
 # and their short-horizon twins (SHORT_SCENES) carry the trajectory gates
-SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + NN_MASKED
+SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn', 'mountain4nn'] + ROBOTS + NN_MASKED
             + [p for p in POINTS if not p.startswith('box')] + SPRING_ROBOTS + XCOL + SHORT_SCENES)
 POS_TOL = 1e-5
 
@@ -59,13 +59,33 @@ def _to_qp(a, dev):
   return qp_from_numpy(a, dev)
 
 
-def _gate(got, ref, e32, field):
+WIDE = 1e-2  # a sample whose own bound 2 x E32 exceeds this is ill-conditioned
+
+
+def _gate(got, ref, e32, field, split=True):
+  """max(1e-5, 2 x E32) over a group of envs, E32 the largest fp32 error of
+  Brax's own algorithm over the group's samples. With `split`, the envs are
+  two groups: the well-conditioned ones (2 x E32_i <= 1e-2) against the
+  bound of their own group, the ill-conditioned ones (a contact flipping on
+  rounding: Brax's own fp32 is off by > 5e-3 there) against theirs, recorded
+  as `<field>:illcond`. (Until round 3 one group held every env, so one
+  ill-conditioned env loosened the gate of all; the split only tightens it.)
+  Without `split` (the reset lift's discontinuity: any env may flip), one
+  group."""
   nw = normwise(got, ref)
-  tol = max(POS_TOL, 2.0 * float(np.max(e32)))
-  record_margin(field, float(nw.max()), tol)
+  e32 = np.broadcast_to(np.asarray(e32, np.float64), nw.shape)
   assert np.all(np.isfinite(got)), field
-  assert nw.max() <= tol, f'{field}: normwise {nw.max():.3e} > tol {tol:.3e}'
-  return nw.max(), tol
+  ill = (2.0 * e32 > WIDE) if split else np.zeros(nw.shape, bool)
+  worst = (0.0, POS_TOL)
+  for sel, name in ((~ill, field), (ill, field + ':illcond')):
+    if not sel.any():
+      continue
+    tol = max(POS_TOL, 2.0 * float(e32[sel].max()))
+    m = float(nw[sel].max())
+    record_margin(name, m, tol, n=int(sel.sum()))
+    assert m <= tol, f'{name}: normwise {m:.3e} > tol {tol:.3e} ({int(sel.sum())} envs)'
+    worst = max(worst, (m, tol))
+  return worst
 
 
 class Envelope:
@@ -225,7 +245,7 @@ def test_reset_vs_golden(dev, oracle_lib, name):
   obs32 = o32.env_obs(env_kind(name), q32, o32.system_info(q32), np.zeros((B, o32.A)),
                       T['obs'].shape[-1], obs_flags=obs_flags(name), coef=env.coef)
   obs = st.obs.cpu().numpy()
-  _gate(obs, T['reset_obs'], normwise(obs32, T['reset_obs']), 'obs')
+  _gate(obs, T['reset_obs'], normwise(obs32, T['reset_obs']), 'obs', split=False)
   n_state = (1 + 4 + 2 * meta['num_joint_dof'] + 6 + 2 * obs_flags(name)
              if env_kind(name) == 'ant' else obs.shape[-1])
   assert normwise(obs[:, :n_state], T['reset_obs'][:, :n_state]).max() <= 1e-5
@@ -454,7 +474,9 @@ def nn_cells_check(cells, ref_sel, sim, tol_rel=1e-5):
 
 
 @pytest.mark.parametrize('name,variant', [('mountain1nn', None), ('mountain1nn', 'itemloop'),
-                                          ('mountain1nn', 'multi'), ('capsule_cull_s', None),
+                                          ('mountain1nn', 'multi'), ('mountain4nn', None),
+                                          ('mountain4nn', 'multi'), ('mountain4nn', 'itemloop'),
+                                          ('capsule_cull_s', None),
                                           ('twin_cull', None), ('twin_cull', 'multi')])
 def test_near_neighbors_cells_vs_reference(dev, name, variant):
   """NearNeighbors.update's top_k (colliders.py:71-85) is index work: the

@@ -14,7 +14,7 @@ from tests.helpers import (CAPSULES, NN_MASKED, SHORT_SCENES, ENVTRAJ_KERNEL, PO
                            compiled, env_kind, obs_flags)
 
 ENV_TRAJ = ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'] + SPRING_ENVS
-SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn'] + ROBOTS + CAPSULES + NN_MASKED + POINTS
+SYS_TRAJ = (['mountain1', 'mountain2', 'mountain4', 'mountain1nn', 'mountain4nn'] + ROBOTS + CAPSULES + NN_MASKED + POINTS
             + SPRING_ROBOTS + XCOL + SHORT_SCENES)
 
 

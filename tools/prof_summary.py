@@ -61,12 +61,26 @@ def bench_grids(d):
   with open(p) as f:
     for r in csv.DictReader(f):
       k = short(r['Kernel_Name'])
-      n[k][int(r['Grid_Size_X'])].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+      # the total grid (the counter passes report X * Y * Z; the phase
+      # kernels launch 2-D grids)
+      g = int(r['Grid_Size_X']) * int(r.get('Grid_Size_Y') or 1) * int(r.get('Grid_Size_Z') or 1)
+      n[k][g].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
   grids, stats = {}, {}
   for k, by in n.items():
     g = max(by, key=lambda x: len(by[x]))
     grids[k] = g
     stats[k] = {'calls': len(by[g]), 'avg_ns': sum(by[g]) / len(by[g]), 'grid': g}
+    if 'rollout' in k:
+      # a rollout kernel runs K-step launches and (Env.step on a wide batch)
+      # one-step launches: split the durations at 4x the shortest, so each
+      # average covers launches of one length
+      d = sorted(by[g])
+      long_ = [x for x in d if x > 4 * d[0]]
+      if long_:
+        short_ = [x for x in d if x <= 4 * d[0]]
+        stats[k].update({'calls': len(long_), 'avg_ns': sum(long_) / len(long_),
+                         'one_step_launches': {'calls': len(short_),
+                                               'avg_ns': sum(short_) / len(short_)}})
     other = {str(x): {'calls': len(v), 'avg_ns': sum(v) / len(v)} for x, v in by.items() if x != g}
     if other:
       stats[k]['other_grids'] = other
@@ -106,6 +120,8 @@ def main():
   for k in stats:
     if 'env_rollout_kernel' in k:
       stats[k]['steps_per_launch'] = K
+    elif 'env_rollout_wide_kernel' in k:
+      stats[k]['steps_per_launch'] = 50  # bench.py secondary_configs: 50-step rollouts
   cnt, meta = counters(d, grids)
   res = {}
   for k, cs in cnt.items():
