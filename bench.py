@@ -12,7 +12,12 @@ Inputs are resident in HBM.
 gcd(steps, 50)) that draws each step's actions inside the kernel and steps
 every env K times, the state read in place from the previous launch's last
 step (the reference's lax.scan of env.step with the random actions drawn in
-the loop). The other loops are reported beside it for the record:
+the loop). Its timed region (barrier + synchronisation on both sides,
+exactly `--steps` steps) runs `--repeats` times (default 5) and `value` is the
+median region: at the driver's 20 steps a region is ONE launch, and a lone
+launch or clock hiccup would move a single sample by several percent (every
+sample is in `timed_regions`). The other loops are reported beside it for the
+record:
 `eager_loop` (Python: bx_uniform + Env.step per step), `graph_loop`
 (StepGraph: a hipGraph of one draw + K Env.step launches: the closed-loop
 per-step path) and `rollout_loop` (RolloutGraph: a hipGraph of one draw + one
@@ -300,7 +305,8 @@ def secondary_configs(dev, steps=50):
     out[f'mountain4_2048_cutoff{cutoff}'] = {
         'value': Bm * n / wall, 'unit': 'env-steps/s (System.step)',
         'ms_per_step': wall * 1e3 / n, 'gpu_ms_per_step': gpu * 1e3 / n,
-        'contact_rows': sys_.num_rows, 'lanes_per_env': sys_.lanes}
+        'contact_rows': sys_.num_rows, 'lanes_per_env': sys_.lanes,
+        'lds_bytes_per_env': sys_.lds_bytes, 'envs_per_cu': (160 * 1024) // max(sys_.lds_bytes, 1)}
     # the same steps without Info (System.step(..., info=False): the state
     # only, as jit drops the Info a caller ignores)
     wall, gpu = _time(mstep_noinfo, n, 2)
@@ -432,6 +438,8 @@ def main():
   ap.add_argument('--phase-envs', type=int, default=1 << 20)
   ap.add_argument('--no-secondary', action='store_true',
                   help='skip the Humanoid / Ant Mountain legs')
+  ap.add_argument('--repeats', type=int, default=5,
+                  help='timed regions of the direct (headline) loop; value = their median')
   ap.add_argument('--generic', action='store_true',
                   help='force the generic item-loop kernel variant (A/B)')
   ap.add_argument('--block', type=int, default=0,
@@ -518,10 +526,11 @@ def main():
   from brax_amd.envs.graph import StepGraph
   from brax_amd.envs.rollout import RolloutGraph, RolloutRunner
 
-  def timed_replays(g, advance_hook):
-    """Warm replays, then args.steps // K timed replays (barrier + sync on
-    both sides); the elapsed wall time, the collectives inside it and the
-    warm replays run. The warm-up is max(warmup // K, 2) replays, extended
+  def timed_replays(g, advance_hook, repeats=1):
+    """Warm replays, then `repeats` timed regions of args.steps // K replays
+    each (barrier + sync on both sides of every region); the elapsed wall
+    time of each region, the collectives inside each and the replays run
+    untimed + timed. The warm-up is max(warmup // K, 2) replays, extended
     to WARM_S of the loop's own work: the GPU's clock ramps over ~10 ms of
     load (a 20-step rollout launch runs 506 us cold, 471 us warm in one
     rocprof trace), so the timed region starts at the steady state."""
@@ -538,24 +547,27 @@ def main():
     for _ in range(extra):
       fire()
     n_warm += extra
-    if exchange is not None:
-      exchange.reset()
-    torch.cuda.synchronize()
-    if dist is not None:
-      dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps // K):
-      fire()
-      if advance_hook is not None:
-        advance_hook(K)  # the RCCL all-gather once per period, on the host
-    torch.cuda.synchronize()
-    if dist is not None:  # (one rank: the synchronisation above is the bracket)
-      dist.barrier()
+    els, cols = [], []
+    for _ in range(repeats):
+      if exchange is not None:
+        exchange.reset()
       torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+      if dist is not None:
+        dist.barrier()
+      torch.cuda.synchronize()
+      t0 = time.perf_counter()
+      for _ in range(args.steps // K):
+        fire()
+        if advance_hook is not None:
+          advance_hook(K)  # the RCCL all-gather once per period, on the host
+      torch.cuda.synchronize()
+      if dist is not None:  # (one rank: the synchronisation above is the bracket)
+        dist.barrier()
+        torch.cuda.synchronize()
+      els.append(time.perf_counter() - t0)
+      cols.append(exchange.flushes if exchange is not None else 0)
     gc.enable()
-    return el, (exchange.flushes if exchange is not None else 0), n_warm
+    return els, min(cols), n_warm + (repeats - 1) * (args.steps // K)
 
   def build(kind, st, k0):
     try:
@@ -581,25 +593,39 @@ def main():
     return bool(f.item())
 
   adv = None if exchange is None else exchange.advance
-  loops = {'eager': (eager_elapsed, eager_collectives, None)}
+  # per loop: the timed regions' elapsed times (the direct loop's timed
+  # region runs `--repeats` times; the others once), collectives, error
+  R = max(int(args.repeats), 1)
+  loops = {'eager': ([eager_elapsed], eager_collectives, None)}
   k0 = args.warmup + args.steps
   for kind in KINDS[1:]:
     g, err = build(kind, state, k0)
     if agreed(g is not None):
-      el, col, n_warm = timed_replays(g, adv)
-      loops[kind] = (el, col, None)
-      k0 += (n_warm + args.steps // K) * K
+      els, col, n_run = timed_replays(g, adv, R if kind == 'direct' else 1)
+      loops[kind] = (els, col, None)
+      k0 += (n_run + args.steps // K) * K
       state = clone_state(g.state() if kind == 'direct' else  # pylint: disable=protected-access
                           g._res[0] if kind == 'rollout' else g._out)
     else:
       loops[kind] = (None, 0, err)
     del g
   if dist is not None:
-    t = torch.tensor([loops[k][0] if loops[k][0] is not None else -1.0
-                      for k in KINDS], dtype=torch.float64, device=dev)
+    # each region's time is its slowest rank's
+    t = torch.tensor([loops[k][0][i] if loops[k][0] is not None else -1.0
+                      for k in KINDS for i in range(R if k == 'direct' else 1)],
+                     dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    for k, v in zip(KINDS, t.tolist()):
-      loops[k] = (float(v) if v >= 0 else None,) + loops[k][1:]
+    v = t.tolist()
+    for k in KINDS:
+      n = R if k == 'direct' else 1
+      part, v = v[:n], v[n:]
+      loops[k] = ((part if part[0] >= 0 else None),) + loops[k][1:]
+  # a loop's time: the median of its timed regions (one region but the
+  # direct loop's; its region is one K-step launch at the driver's 20 steps,
+  # so a single launch or clock hiccup would move a lone sample by several %)
+  samples = {k: loops[k][0] for k in KINDS}
+  loops = {k: ((float(np.median(e)) if e is not None else None),) + loops[k][1:]
+           for k, e in ((k, loops[k][0]) for k in KINDS)}
   # the headline is the direct loop by design; another loop only if it failed
   best = next(k for k in ('direct', 'rollout', 'step', 'eager') if loops[k][0] is not None)
   elapsed, collectives = loops[best][0], loops[best][1]
@@ -710,6 +736,9 @@ def main():
     out[key] = ({'value': total / el, 'unit': 'env-steps/s', 'ms_per_step': el * 1e3 / args.steps,
                  'collectives_in_timed_region': col} if el is not None else {'error': err})
   out['timed_loop'] = best
+  out['timed_regions'] = {'repeats': len(samples[best]) if samples[best] else 0,
+                          'ms_per_step': [e * 1e3 / args.steps for e in (samples[best] or [])],
+                          'statistic': 'median'}
   out['timed_loop_policy'] = ('the direct loop by design (RolloutRunner); rollout, step, eager '
                               'only when it could not run')
   out['warmup_policy'] = (f'{args.warmup} warm-up steps; each replayed loop warms on >= '

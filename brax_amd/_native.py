@@ -33,6 +33,7 @@ _SIGS = {
                           C.POINTER(C.c_void_p)], C.c_int),
     'bx_system_destroy': ([C.c_void_p], C.c_int),
     'bx_system_lanes': ([C.c_void_p], C.c_int),
+    'bx_system_lds_bytes': ([C.c_void_p], C.c_int),
     'bx_system_set_single': ([C.c_void_p, C.c_int], C.c_int),
     'bx_system_set_variant': ([C.c_void_p, C.c_int, C.c_int], C.c_int),
     'bx_system_set_block': ([C.c_void_p, C.c_int], C.c_int),

@@ -351,7 +351,17 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   put_lists(al, H.o_al_off, H.o_al);
   put_lists(cl, H.o_cl_off, H.o_cl);
   // MULTI-mode gather tasks: each body's contact list cut, per collider group,
-  // into runs of <= TASK_W slots (same order); a body's tasks in list order
+  // into runs of <= TASK_W slots (same order); a body's tasks in list order.
+  // MULTI slots: row x's a side is slot x, a two-way row's b side slot R +
+  // its two-way rank (one-way rows have none), then the zero slot
+  std::vector<int> mb(R, -1);
+  int n_tw = 0;
+  for (int x = 0; x < R; x++)
+    if (!d->col_oneway[d->row_group[x]]) mb[x] = R + n_tw++;
+  H.m_zero = R + n_tw;
+  for (int x = 0; x < R; x++)
+    if (mb[x] < 0) mb[x] = H.m_zero;
+  auto mslot_of = [&](int s) { return s < R ? s : mb[s - R]; };
   std::vector<std::vector<int>> task_e;  // slot indices
   std::vector<std::vector<int>> btask(N);  // task | group << 24
   int max_btask = 0;
@@ -361,7 +371,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       const int g = cl[b][i] >> 24;
       std::vector<int> t;
       while (i < cl[b].size() && (cl[b][i] >> 24) == g && (int)t.size() < TASK_W)
-        t.push_back(cl[b][i++] & 0xFFFFFF);
+        t.push_back(mslot_of(cl[b][i++] & 0xFFFFFF));
       btask[b].push_back((int)task_e.size() | (g << 24));
       task_e.push_back(t);
     }
@@ -371,7 +381,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.o_task = B.alloc(H.T * TASK_W);
   for (int t = 0; t < H.T; t++)
     for (int k = 0; k < TASK_W; k++)
-      B.i(H.o_task + t * TASK_W + k, k < (int)task_e[t].size() ? task_e[t][k] : 2 * R);
+      B.i(H.o_task + t * TASK_W + k, k < (int)task_e[t].size() ? task_e[t][k] : H.m_zero);
   H.o_btask = B.alloc(N * BTASK_W);
   for (int b = 0; b < N; b++) {
     // padding: the zero task (index T, a zero partial) in the last group
@@ -481,19 +491,11 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.l_jslot = carve((2 * J + 1) * SLOT_STRIDE);
   H.l_aslot = carve((2 * K + 1) * ASLOT_STRIDE);
   H.l_acc = carve(N * ACC_STRIDE);
-  H.l_ract = carve(R);
-  H.l_alist = carve(H.info_rows);
-  H.l_ang = carve(2 * D);
+  // NearNeighbors ranks and the active-row list: culled scenes only (the
+  // SINGLE kernels never cull; MULTI's all-pairs scenes need the room)
+  H.l_ract = carve(H.n_nn ? R : 0);
+  H.l_alist = carve(H.n_nn ? H.info_rows : 0);
   H.l_red = carve(64);
-  // env programs' System.step action (swimmer: + drag, grasp: 3 palm actions)
-  H.xact_words = std::max(16, (d->action_size + 12 + 3) & ~3);
-  H.l_xact = carve(H.xact_words);
-  // the action row staged by the env step: every index an actuator or force
-  // reads (jp.take clips into the row, so no read lands past these words)
-  H.act_read = std::max(d->action_size, 1);
-  for (int k = 0; k < 3 * K; k++) H.act_read = std::max(H.act_read, d->act_index[k] + 1);
-  for (int k = 0; k < 3 * d->n_forces; k++) H.act_read = std::max(H.act_read, d->force_index[k] + 1);
-  H.l_arow = carve(H.act_read);
   // NearNeighbors: each wave's sorted picks (64-bit keys) when an env spans
   // up to 4 waves
   {
@@ -502,13 +504,30 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     H.nnl_words = 2 * 4 * max_cut;
     H.l_nnl = carve(H.nnl_words);
   }
+  // the MULTI (System.step only) tail starts here, over the env step's regions
+  const int tail_m = off;
+  // env-step regions: joint angles, the env programs' System.step action
+  // (swimmer: + drag, grasp: 3 palm actions), the staged action row (every
+  // index an actuator or force reads: jp.take clips into the row, so no read
+  // lands past these words)
+  H.l_ang = carve(2 * D);
+  H.xact_words = std::max(16, (d->action_size + 12 + 3) & ~3);
+  H.l_xact = carve(H.xact_words);
+  H.act_read = std::max(d->action_size, 1);
+  for (int k = 0; k < 3 * K; k++) H.act_read = std::max(H.act_read, d->act_index[k] + 1);
+  for (int k = 0; k < 3 * d->n_forces; k++) H.act_read = std::max(H.act_read, d->force_index[k] + 1);
+  H.l_arow = carve(H.act_read);
   // the contact regions form each mode's tail: the item-loop / SINGLE
   // kernels keep per-row data and 12-word slots, MULTI mode keeps the row data
-  // in registers and needs 8-word slots plus the task partials
+  // in registers and needs 6-word slots plus the task partials
   const int tail = off;
-  H.l_mslot = carve((2 * R + 1) * MSLOT_STRIDE);
-  H.l_tslot = carve((H.T + 1) * MSLOT_STRIDE);
-  H.l_near = carve(R + 16);
+  off = tail_m;
+  H.l_mslot = carve((H.m_zero + 1) * MSLOT_STRIDE);
+  H.l_tslot = carve((H.T + 1) * TSLOT_STRIDE);
+  // the broad phase's near-row list (16-bit) and per-wave counts: all-pairs
+  // scenes only (culled scenes skip the broad phase)
+  H.l_near = carve(H.n_nn ? 0 : (R + 1) / 2);
+  H.l_nearc = carve(H.n_nn ? 0 : 16);
   H.env_words_m = (off + 63) & ~63;
   off = tail;
   H.l_rowd = carve(R * ROWD_STRIDE);
@@ -565,6 +584,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     uint32_t rw[32];
     for (int x = 0; x < R; x++) {
       row_words(x, rw);
+      rw[LR_MBSLOT] = (uint32_t)mb[x];
       for (int k = 0; k < 32; k++) B.w[H.o_rimg + ((k / 4) * R + x) * 4 + k % 4] = rw[k];
     }
     // broad-phase bounds (BI_*): reach = |a_end| + |b_end| + radii in double,
@@ -585,6 +605,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       bw[BI_B] = (uint32_t)d->row_body_b[x];
       std::memcpy(&bw[BI_REACH], &rf, 4);
       bw[BI_SKIP] = d->col_fn[g] == BX_COL_CAPSULE_CAPSULE ? 1u : 0u;
+      bw[BI_BSLOT] = (uint32_t)mb[x];
       for (int k = 0; k < 3; k++) {
         bw[BI_APOS + k] = fbits(d->row_a_pos[3 * x + k]);
         bw[BI_BPOS + k] = fbits(d->row_b_pos[3 * x + k]);
@@ -1010,6 +1031,7 @@ int bx_system_destroy(bx_system* S) {
 }
 
 int bx_system_lanes(bx_system* S) { return S ? S->L : 0; }
+int bx_system_lds_bytes(bx_system* S) { return S ? (int)step_lds(S) : 0; }
 
 int bx_system_set_single(bx_system* S, int on) {
   if (!S) return fail("null system");

@@ -79,13 +79,14 @@ struct Env {
   int* ract;     // R: NearNeighbors rank of the row this step, -1 = culled
   int* alist;    // info_rows: the step's active rows in Info order
   int sstride;   // contact slot stride: SLOT_STRIDE, or MSLOT_STRIDE in MULTI mode
-  float* tslot;  // MULTI mode: (T + 1) x MSLOT_STRIDE gather-task partials, zero last
+  float* tslot;  // MULTI mode: (T + 1) x TSLOT_STRIDE gather-task partials, zero last
   float* nd;     // NearNeighbors candidate distances, stride nds (scratch, before the substeps)
   int nds;
   float* xact;   // the action an env program hands System.step (xact_words)
   float* arow;   // the env's action row, its first act_read words (env step)
   float* nnl;    // NearNeighbors per-wave pick lists (nnl_words)
-  int* nearl;    // MULTI: the pass's near rows, then per-wave counts
+  uint16_t* nearl;  // MULTI: the pass's near rows
+  int* nearc;       // MULTI: the broad phase's per-wave counts
   uint4* jlim;   // SINGLE spherical kernels: the lanes' limit rows, [6][L] groups
 };
 
@@ -551,6 +552,7 @@ __device__ __forceinline__ void body_forces(const Cst& c, const BlobHdr& H, int 
 
 struct RowC {
   int group, a, b, fn, oneway;
+  int bslot;  // MULTI row image: the b side's contact slot
   v3 a_pos, a_end, b_pos, b_end;
   float a_rad, b_rad, fric, elas, scale, thr, erp;
   float ma, mb;
@@ -575,6 +577,7 @@ __device__ __forceinline__ RowC load_row(const Cst& c, const BlobHdr& H, int r) 
   x.scale = c.f(o + R_SCALE);
   x.thr = c.f(o + R_THR);
   x.erp = c.f(o + R_ERP);
+  x.bslot = -1;  // (the MULTI kernel's rows come from the row image)
   int oa = H.o_body + x.a * BODY_STRIDE, ob = H.o_body + x.b * BODY_STRIDE;
   x.ma = c.f(oa + BODY_MASS);
   x.mb = c.f(ob + BODY_MASS);
@@ -1034,7 +1037,11 @@ __device__ __forceinline__ void contact_gen_x(const Cst& c, const BlobHdr& H, in
 }
 
 // One/TwoWay._position_contact (colliders.py:306-377, 495-580)
-template <int F>
+// RAWL (the MULTI kernel): oar / obr carry, in x, y, z, each side's angular
+// impulse before the body's quaternion product (w = 0): the body forms
+// 0.5 vec_quat_mul(I L, rot) once from its rows' summed L, as the update is
+// linear in L (the reference's per-row quaternions, summed, are the same)
+template <int F, bool RAWL = false>
 __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, const QP& b, const v3& ao_pos,
                                   const q4& ao_rot, const v3& bo_pos, const q4& bo_rot, v3 cpos,
                                   v3 n, float cpen, v3& oap, q4& oar, v3& obp, q4& obr) {
@@ -1064,7 +1071,12 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
     // one quaternion update for their sum (both linear in the impulse)
     pv = pv + dlt * n2 * sm * cm;
     oap = sc * (pv / R.ma);
-    oar = sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
+    if constexpr (RAWL) {
+      const v3 L = sc * cross(pp, pv);
+      oar = q4{0.f, L.x, L.y, L.z};
+    } else {
+      oar = sc * (0.5f * vec_quat_mul(mul(R.Ia, cross(pp, pv)), a.rot));
+    }
     obp = mk(0.f, 0.f, 0.f);
     obr = q4{0.f, 0.f, 0.f, 0.f};
     return dl * cm;
@@ -1100,9 +1112,15 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
   const v3 pt = dlt * n2 * sm * cm;
   const v3 ps = pv + pt;
   oap = sc * (ps / R.ma);
-  oar = sc * (0.5f * vec_quat_mul(mul(R.Ia, la + cross(pp, pt)), a.rot));
   obp = sc * (-ps / R.mb);
-  obr = sc * (-0.5f * vec_quat_mul(mul(R.Ib, lb + cross(pc, pt)), b.rot));
+  if constexpr (RAWL) {
+    const v3 La = sc * (la + cross(pp, pt)), Lb = -sc * (lb + cross(pc, pt));
+    oar = q4{0.f, La.x, La.y, La.z};
+    obr = q4{0.f, Lb.x, Lb.y, Lb.z};
+  } else {
+    oar = sc * (0.5f * vec_quat_mul(mul(R.Ia, la + cross(pp, pt)), a.rot));
+    obr = sc * (-0.5f * vec_quat_mul(mul(R.Ib, lb + cross(pc, pt)), b.rot));
+  }
   return dl;
 }
 
@@ -1420,13 +1438,14 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi =
   E.nnl = al16(base + H.l_nnl);
   E.jlim = reinterpret_cast<uint4*>(al16(base + H.l_jlim));
   if (multi) {
-    // MULTI: 8-word contact slots and task partials; no row-data region (the
+    // MULTI: 6-word contact slots, 8-word task partials; no row-data region (the
     // row's contact stays in its lane's registers); the task partials double
     // as NearNeighbors scratch before the substeps
     E.rowd = nullptr;
     E.cslot = al16(base + H.l_mslot);
     E.tslot = al16(base + H.l_tslot);
-    E.nearl = reinterpret_cast<int*>(base + H.l_near);
+    E.nearl = reinterpret_cast<uint16_t*>(base + H.l_near);
+    E.nearc = reinterpret_cast<int*>(base + H.l_nearc);
     E.sstride = MSLOT_STRIDE;
     E.nd = E.tslot;
     E.nds = 1;
@@ -1453,8 +1472,16 @@ __device__ __forceinline__ void esync() {
   if constexpr (L > 64) __syncthreads(); else sync();
 }
 
-// a culled row's slots: no update, not counted
-__device__ __forceinline__ void zero_row_slots(const Env& E, int r) {
+// a culled row's slots: no update, not counted (MULTI: 6-word slots, the b
+// side at the row image's compact slot index)
+__device__ __forceinline__ void zero_row_slots(const Cst& c, const BlobHdr& H, const Env& E, int r) {
+  if (E.tslot) {
+    float* sa = E.cslot + r * MSLOT_STRIDE;
+    const int b = c.i(H.o_rimg + ((LR_MBSLOT / 4) * H.R + r) * 4 + LR_MBSLOT % 4);
+    float* sb = E.cslot + b * MSLOT_STRIDE;
+    for (int k = 0; k < MSLOT_STRIDE; k++) { sa[k] = 0.f; sb[k] = 0.f; }
+    return;
+  }
   float* sa = E.cslot + r * E.sstride;
   float* sb = E.cslot + (E.nR + r) * E.sstride;
   for (int k = 0; k < 8; k++) { sa[k] = 0.f; sb[k] = 0.f; }
@@ -1534,7 +1561,7 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
     const int og = H.o_group + c.i(H.o_row + r * ROW_STRIDE + R_GROUP) * GROUP_STRIDE;
     if (c.i(og + G_CUT)) {
       E.ract[r] = -1;
-      zero_row_slots(E, r);
+      zero_row_slots(c, H, E, r);
     } else {
       E.ract[r] = 0;
       E.alist[c.i(og + G_INFO) + r - c.i(og + G_R0)] = r;
@@ -1675,9 +1702,9 @@ __device__ __forceinline__ int row_info(const Cst& c, const BlobHdr& H, const En
 __device__ __forceinline__ void zero_slots(const Env& E, const BlobHdr& H, int lane) {
   if (lane < SLOT_STRIDE) {
     E.jslot[2 * H.J * SLOT_STRIDE + lane] = 0.f;
-    if (lane < E.sstride) E.cslot[2 * H.R * E.sstride + lane] = 0.f;
+    if (lane < E.sstride) E.cslot[(E.tslot ? H.m_zero : 2 * H.R) * E.sstride + lane] = 0.f;
     if (lane < ASLOT_STRIDE) E.aslot[2 * H.K * ASLOT_STRIDE + lane] = 0.f;
-    if (E.tslot && lane < MSLOT_STRIDE) E.tslot[H.T * MSLOT_STRIDE + lane] = 0.f;
+    if (E.tslot && lane < TSLOT_STRIDE) E.tslot[H.T * TSLOT_STRIDE + lane] = 0.f;
   }
 }
 
@@ -2800,7 +2827,8 @@ __device__ __forceinline__ RowC load_row_img(const Cst& c, const BlobHdr& H, int
   x.elas = f(LR_ELAS);
   x.scale = f(LR_SCALE);
   x.thr = f(LR_THR);
-  x.erp = f(LR_ERP);
+  x.bslot = (int)w[LR_MBSLOT];  // (the MULTI image carries no erp)
+  x.erp = 0.f;
   x.ma = f(LR_MA);
   x.mb = f(LR_MB);
   x.Ia = f3(LR_IA);
@@ -2825,7 +2853,7 @@ __device__ __forceinline__ void load_hoist_multi(const Cst& c, const BlobHdr& H,
   X.al = load_glist<MAXG>(c, H.o_al_off, H.o_al, b, X.hasB, 2 * H.K);
   const bool hasT = lane < H.T;
 #pragma unroll
-  for (int k = 0; k < TASK_W; k++) X.te[k] = hasT ? c.i(H.o_task + lane * TASK_W + k) : 2 * H.R;
+  for (int k = 0; k < TASK_W; k++) X.te[k] = hasT ? c.i(H.o_task + lane * TASK_W + k) : H.m_zero;
 #pragma unroll
   for (int k = 0; k < BTASK_W; k++) X.bt[k] = X.hasB ? c.i(H.o_btask + b * BTASK_W + k) : H.T;
   if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? lane : 0);
@@ -2834,61 +2862,76 @@ __device__ __forceinline__ void load_hoist_multi(const Cst& c, const BlobHdr& H,
 #pragma unroll
   for (int m = 0; m < MR; m++) {
     const int r = lane + m * L;
-    X.R[m] = load_row(c, H, r < H.R ? r : 0);
+    const int rr = r < H.R ? r : 0;
+    X.R[m] = load_row(c, H, rr);
+    X.R[m].bslot = c.i(H.o_rimg + ((LR_MBSLOT / 4) * H.R + rr) * 4 + LR_MBSLOT % 4);
   }
 #endif
 }
 
-// phase 1: the lane's task partial, its slots summed in list order
+// a MULTI contact slot: the linear part, the angular part (3 + 3 words; slot
+// k at 24 k bytes, so 8-byte accesses)
+__device__ __forceinline__ void st_mslot(float* s, v3 a, v3 l) {
+  float2* p = reinterpret_cast<float2*>(__builtin_assume_aligned(s, 8));
+  p[0] = float2{a.x, a.y};
+  p[1] = float2{a.z, l.x};
+  p[2] = float2{l.y, l.z};
+}
+__device__ __forceinline__ void ld_mslot(const float* s, v3& a, v3& l) {
+  const float2* p = reinterpret_cast<const float2*>(__builtin_assume_aligned(s, 8));
+  const float2 x = p[0], y = p[1], z = p[2];
+  a = mk(x.x, x.y, y.x);
+  l = mk(y.y, z.x, z.y);
+}
+
+// phase 1: the lane's task partial, its slots summed in list order; a slot
+// counts when its linear part is nonzero (the reference's any(dq_pos) /
+// any(dp_vel) per row, colliders.py:187-195,231-239)
 __device__ __forceinline__ void task_sum(const int* te, const float* ms, float* out) {
-  v3 a = mk(0.f, 0.f, 0.f);
-  q4 r{0.f, 0.f, 0.f, 0.f};
+  v3 a = mk(0.f, 0.f, 0.f), l = mk(0.f, 0.f, 0.f);
   float n = 0.f;
 #pragma unroll
   for (int k = 0; k < TASK_W; k++) {
-    v3 v;
-    q4 q;
-    float f;
-    ld_slot(ms + te[k] * MSLOT_STRIDE, v, q, f);
+    v3 v, w;
+    ld_mslot(ms + te[k] * MSLOT_STRIDE, v, w);
     a = a + v;
-    r = r + q;
-    n += f;
+    l = l + w;
+    n += (v.x != 0.f || v.y != 0.f || v.z != 0.f) ? 1.f : 0.f;
   }
-  st_slot(out, a, r, n);
+  st4a(out, f32x4{a.x, a.y, a.z, l.x});
+  st4a(out + 4, f32x4{l.y, l.z, n, 0.f});
 }
 
-// phase 2: sum over the body's groups of (group's partials) / (eps + count)
+// phase 2: sum over the body's groups of (group's partials) / (eps + count):
+// the linear part a and the angular part l
 __device__ __forceinline__ void body_combine(const int* bt, const float* ts, float eps, v3& a,
-                                             q4& r) {
+                                             v3& l) {
   a = mk(0.f, 0.f, 0.f);
-  r = q4{0.f, 0.f, 0.f, 0.f};
-  v3 ga = mk(0.f, 0.f, 0.f);
-  q4 gr{0.f, 0.f, 0.f, 0.f};
+  l = mk(0.f, 0.f, 0.f);
+  v3 ga = mk(0.f, 0.f, 0.f), gl = mk(0.f, 0.f, 0.f);
   float gn = 0.f;
   int g = bt[0] >> 24;
 #pragma unroll
   for (int k = 0; k < BTASK_W; k++) {
-    v3 v;
-    q4 q;
-    float f;
-    ld_slot(ts + (bt[k] & 0xFFFFFF) * MSLOT_STRIDE, v, q, f);
+    const float* t = ts + (bt[k] & 0xFFFFFF) * TSLOT_STRIDE;
+    const f32x4 t0 = ld4a(t), t1 = ld4a(t + 4);
     const int gk = bt[k] >> 24;
     if (gk != g) {
       const float d = eps + gn;
       a = a + ga / d;
-      r = q4{r.w + gr.w / d, r.x + gr.x / d, r.y + gr.y / d, r.z + gr.z / d};
+      l = l + gl / d;
       ga = mk(0.f, 0.f, 0.f);
-      gr = q4{0.f, 0.f, 0.f, 0.f};
+      gl = mk(0.f, 0.f, 0.f);
       gn = 0.f;
       g = gk;
     }
-    ga = ga + v;
-    gr = gr + q;
-    gn += f;
+    ga = ga + mk(t0[0], t0[1], t0[2]);
+    gl = gl + mk(t0[3], t1[0], t1[1]);
+    gn += t1[2];
   }
   const float d = eps + gn;
   a = a + ga / d;
-  r = q4{r.w + gr.w / d, r.x + gr.x / d, r.y + gr.y / d, r.z + gr.z / d};
+  l = l + gl / d;
 }
 
 // info: the env's Info contact rows (contact_pos 3, normal 3, penetration),
@@ -3068,7 +3111,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
     if (bph) {
       constexpr int NWV = L / 64;
       const int wv = lane >> 6;
-      int* cnt = E.nearl + H.R;
+      int* cnt = E.nearc;
       bool nr[MR];
       int rr[MR], rk[MR];
 #pragma unroll
@@ -3091,11 +3134,10 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
             near = !(norm(cb - ca) > __uint_as_float(g0.z) + 1e-4f);
           }
           if (!near) {
-            const f32x4 z{0.f, 0.f, 0.f, 0.f};
-            st4a(E.cslot + r * MSLOT_STRIDE, z);
-            st4a(E.cslot + r * MSLOT_STRIDE + 4, z);
-            st4a(E.cslot + (H.R + r) * MSLOT_STRIDE, z);
-            st4a(E.cslot + (H.R + r) * MSLOT_STRIDE + 4, z);
+            // (a one-way row's b slot is the zero slot: zeros again)
+            const v3 z = mk(0.f, 0.f, 0.f);
+            st_mslot(E.cslot + r * MSLOT_STRIDE, z, z);
+            st_mslot(E.cslot + (int)g1.w * MSLOT_STRIDE, z, z);
           }
         }
         nr[m] = near;
@@ -3116,7 +3158,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
           before += w2 < wv ? k : 0;
           mt += k;
         }
-        if (nr[m]) E.nearl[total + before + rk[m]] = rr[m];
+        if (nr[m]) E.nearl[total + before + rk[m]] = (uint16_t)rr[m];
         total += mt;
       }
       nwork = total;
@@ -3144,23 +3186,22 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       q4 oar{0.f, 0.f, 0.f, 0.f}, obr{0.f, 0.f, 0.f, 0.f};
       dl[m] = 0.f;
       if (pen[m] > 0.f)
-        dl[m] = position_contact<F>(R, a, b, pap, par, pbp, pbr, cpos[m], cn[m], pen[m], oap, oar,
-                                    obp, obr);
-      st_slot(E.cslot + r * MSLOT_STRIDE, oap, oar,
-              (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f);
+        dl[m] = position_contact<F, true>(R, a, b, pap, par, pbp, pbr, cpos[m], cn[m], pen[m], oap,
+                                          oar, obp, obr);
+      st_mslot(E.cslot + r * MSLOT_STRIDE, oap, mk(oar.x, oar.y, oar.z));
       if (!is_oneway<F>(R.oneway))
-        st_slot(E.cslot + (H.R + r) * MSLOT_STRIDE, obp, obr,
-                (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f);
+        st_mslot(E.cslot + R.bslot * MSLOT_STRIDE, obp, mk(obr.x, obr.y, obr.z));
     }
     esync<L>();
     BX_MSTAMP(4);
-    if (lane < H.T) task_sum(X.te, E.cslot, E.tslot + lane * MSLOT_STRIDE);
+    if (lane < H.T) task_sum(X.te, E.cslot, E.tslot + lane * TSLOT_STRIDE);
     esync<L>();
     BX_MSTAMP(5);
     if (X.hasB) {
-      v3 dp;
-      q4 dr;
-      body_combine(X.bt, E.tslot, 1e-6f, dp, dr);
+      v3 dp, dl;
+      body_combine(X.bt, E.tslot, 1e-6f, dp, dl);
+      // the body's one quaternion product of its summed angular impulses
+      const q4 dr = 0.5f * vec_quat_mul(mul(X.B.I, dl), q.rot);
       q.pos = q.pos + mul(dp, X.B.pm);
       q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                  q.rot.z + dr.z * X.B.qm.z};
@@ -3185,21 +3226,16 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       if (pen[m] > 0.f)
         velocity_contact<F>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos[m], cn[m], pen[m], dl[m],
                             oav, oaa, obv, oba);
-      st_slot(E.cslot + r * MSLOT_STRIDE, oav, q4{oaa.x, oaa.y, oaa.z, 0.f},
-              (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f);
-      if (!is_oneway<F>(R.oneway))
-        st_slot(E.cslot + (H.R + r) * MSLOT_STRIDE, obv, q4{oba.x, oba.y, oba.z, 0.f},
-                (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f);
+      st_mslot(E.cslot + r * MSLOT_STRIDE, oav, oaa);
+      if (!is_oneway<F>(R.oneway)) st_mslot(E.cslot + R.bslot * MSLOT_STRIDE, obv, oba);
     }
     esync<L>();
     BX_MSTAMP(7);
-    if (lane < H.T) task_sum(X.te, E.cslot, E.tslot + lane * MSLOT_STRIDE);
+    if (lane < H.T) task_sum(X.te, E.cslot, E.tslot + lane * TSLOT_STRIDE);
     esync<L>();
     if (X.hasB) {
-      v3 dv;
-      q4 da;
-      body_combine(X.bt, E.tslot, 1e-6f, dv, da);
-      v3 dav = mk(da.w, da.x, da.y);
+      v3 dv, dav;
+      body_combine(X.bt, E.tslot, 1e-6f, dv, dav);
       q.vel = mul(q.vel + dv, X.B.pm);
       q.ang = mul(q.ang + dav, X.B.rm);
       stqp(myqp, q);
@@ -3259,7 +3295,7 @@ __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane)
   if (H.n_nn) nn_select<L>(c, H, E, lane);
   for (int r = lane; r < Rn; r += L) {
     if (!row_active(H, E, r)) {
-      zero_row_slots(E, r);
+      zero_row_slots(c, H, E, r);
       continue;
     }
     RowC R = load_row(c, H, r);

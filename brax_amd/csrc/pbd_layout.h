@@ -90,7 +90,7 @@ struct BlobHdr {
   // MULTI mode (large pbd scenes): gather tasks and the mode's LDS tail
   int32_t multi;                     // the system fits the MULTI-mode kernel
   int32_t T, o_task, o_btask;        // tasks: TASK_W slot indices each; per body BTASK_W task refs
-  int32_t l_mslot, l_tslot;          // LDS: 8-word contact slots (2R+1), task partials (T+1)
+  int32_t l_mslot, l_tslot;          // LDS: 6-word contact slots (R + two-way + 1), task partials (T+1)
   int32_t env_words_m;               // per-env LDS words in MULTI mode
   int32_t l_xact;                    // LDS: the action an env program hands System.step
   int32_t xact_words;
@@ -99,8 +99,10 @@ struct BlobHdr {
   int32_t l_nnl, nnl_words;          // LDS: NearNeighbors per-wave pick lists (envs over several waves)
   int32_t o_rimg;                    // MULTI mode: the row image (32 resolved words per row, LR_*)
   int32_t o_bimg;                    // MULTI mode: the rows' broad-phase bounds (BI_*), 0 = none
-  int32_t l_near;                    // LDS (MULTI): the pass's near rows (R) + per-wave counts (16)
+  int32_t l_near;                    // LDS (MULTI, all-pairs scenes): the pass's near rows (R, 16-bit)
   int32_t l_jlim;                    // LDS (SINGLE, spherical kernels): each lane's joint limit rows
+  int32_t m_zero;                    // MULTI: the zero contact slot (R + two-way rows)
+  int32_t l_nearc;                   // LDS (MULTI): the broad phase's per-wave counts (16)
 };
 
 // SINGLE-mode lane image: for each of 64 lanes, every constant the
@@ -158,14 +160,26 @@ enum {
   LR_SCALE = 21, LR_THR = 22, LR_ERP = 23, LR_MA = 24, LR_MB = 25, LR_IA = 26, LR_IB = 29  // 32
 };
 // MULTI-mode gather tasks: a task sums <= TASK_W contact slots of one body and
-// collider group; a body adds <= BTASK_W task partials (ref = task | group << 24)
-enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 8, MULTI_MR = 4 };
+// collider group; a body adds <= BTASK_W task partials (ref = task | group << 24).
+// MULTI contact slots are 6 words: the linear part (position or velocity
+// change, 3) and the angular part (3: the position pass's angular impulse
+// before the body's one quaternion product, the velocity pass's angular
+// velocity change); the count is the linear part's any-nonzero, formed where
+// the task sums. Slot r is row r's a side; a two-way row's b side is slot R +
+// its two-way rank (LR_MBSLOT / BI_BSLOT), then one zero slot (m_zero). Task
+// partials: 8 words (the two sums, the count).
+enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 6, TSLOT_STRIDE = 8, MULTI_MR = 4 };
+// the MULTI row image's b-side slot word (the impulse model's erp, which the
+// MULTI pbd passes never read, is not carried there)
+enum { LR_MBSLOT = LR_ERP };
 // MULTI-mode broad phase: per row, 16-byte group g of row r at
 // o_bimg + (g * R + r) * 4: (body a, body b, reach, may_skip), (a's centre
 // offset, 0), (b's centre offset, 0). A capsule-capsule row whose capsule
 // centres lie farther apart than reach (half segments + radii, rounded up)
 // cannot penetrate, and its position / velocity updates are exact zeros.
-enum { BI_A = 0, BI_B = 1, BI_REACH = 2, BI_SKIP = 3, BI_APOS = 4, BI_BPOS = 8, BI_WORDS = 12 };
+// BI_BSLOT: the row's b-side slot (two-way rows; one-way rows: the zero slot).
+enum { BI_A = 0, BI_B = 1, BI_REACH = 2, BI_SKIP = 3, BI_APOS = 4, BI_BSLOT = 7, BI_BPOS = 8,
+       BI_WORDS = 12 };
 enum { HULL_STRIDE = 114, HULL_V = 0, HULL_F = 24, HULL_N = 96 };
 
 }  // namespace bx

@@ -146,6 +146,11 @@ class System:
     self._default_h = {0: self._h}  # one handle per config.defaults index used
     self.lanes = _native.lib().bx_system_lanes(self._h)
 
+  @property
+  def lds_bytes(self):
+    """LDS bytes per workgroup of the System.step kernel (bx_system_lds_bytes)."""
+    return _native.lib().bx_system_lds_bytes(self._h)
+
   def _create(self, reset_desc):
     cd, keep = abi.make_desc(self.desc)
     rd, keep_r = abi.make_reset_desc(reset_desc, self.num_joint_dof)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 10
+#define BX_ABI_VERSION 11
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
 enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
@@ -306,6 +306,12 @@ int bx_system_destroy(bx_system* sys);
 /* Threads that own one env in this system's step kernels: 16/32/64 lanes of
  * one wavefront, or a whole 128/256-thread workgroup for large scenes. */
 int bx_system_lanes(bx_system* sys);
+
+/* LDS bytes per workgroup of this system's System.step kernel (the current
+ * variant): with 160 KB per CU it sets how many envs a CU holds at once (the
+ * large-scene kernel runs one env per 256-thread workgroup). A diagnostic
+ * query; 0 for a null handle. */
+int bx_system_lds_bytes(bx_system* sys);
 
 /* Select the register-hoisted kernel variant (default when the system fits:
  * every lane owns <= 1 body/joint/actuator/contact row) or the generic

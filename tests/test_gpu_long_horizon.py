@@ -20,7 +20,8 @@ chaotically, so the gate is on distributions, per env:
 * terminations (done without truncation) per env-step: two proportions
   within 3 standard errors;
 * divergence, over each env's first episode: the steps until the median
-  per-env position error between the two paths passes 1e-4 must be at least
+  per-env position error between the two paths passes 1e-4 (1e-5 where
+  Brax's own two roundings stay below 1e-4 inside the window) must be at least
   half of what separates Brax's own two fp32 roundings (the oracle's plain
   and FMA-contracted float32 builds) on the same inputs, and the median
   ratio of the two error curves at most 4, and the exponential growth rate
@@ -192,7 +193,17 @@ def test_long_horizon_statistics(dev, oracle_lib, name):
   keep = np.arange(Td)[:, None] < first_done[None, :]
   med_hip = divergence_curve(pos_h[:Td], pos_o32, keep)
   med_fma = divergence_curve(pos_fma, pos_o32, keep)
-  div_hip, div_fma = divergence_step(med_hip), divergence_step(med_fma)
+  # the divergence threshold: 1e-4, or 1e-5 where the yardstick stays below
+  # 1e-4 inside the first-episode window (Humanoid: ~52-step episodes), so
+  # the gate always compares two crossings
+  thresh = 1e-4
+  if divergence_step(med_fma, thresh) > Td:
+    thresh = 1e-5
+  div_hip, div_fma = divergence_step(med_hip, thresh), divergence_step(med_fma, thresh)
+  # the ratio of the two curves at the window's end (the last step both are
+  # defined on)
+  last = np.nonzero(np.isfinite(med_hip) & np.isfinite(med_fma) & (med_fma > 0))[0]
+  ratio_end = float(med_hip[last[-1]] / med_fma[last[-1]]) if last.size else None
   # the drift ratio where both curves are defined and above the first
   # step's rounding floor
   both = np.isfinite(med_hip) & np.isfinite(med_fma) & (med_fma > 0) & (med_hip > 0)
@@ -212,8 +223,11 @@ def test_long_horizon_statistics(dev, oracle_lib, name):
            'return': compare(rh, ro), 'episode_length_mean': compare(lh, lo),
            'x_velocity_mean': compare(xh, xo),
            'terminations': {'hip': th, 'oracle': to},
-           'divergence_steps_to_1e-4': {'hip_vs_f32': div_hip, 'f32fma_vs_f32': div_fma},
+           'divergence_threshold': thresh,
+           'divergence_steps': {'hip_vs_f32': div_hip, 'f32fma_vs_f32': div_fma},
            'drift_ratio_hip_over_f32fma': ratio,
+           'drift_ratio_at_window_end': ratio_end,
+           'window_end_step': int(last[-1]) + 1 if last.size else None,
            'growth_log10_per_step': {'hip_vs_f32': slope_hip, 'f32fma_vs_f32': slope_fma},
            'median_pos_err_hip_vs_f32': [None if np.isnan(x) else float(x) for x in med_hip[:100]],
            'median_pos_err_f32fma_vs_f32': [None if np.isnan(x) else float(x) for x in med_fma[:100]]}
@@ -237,7 +251,7 @@ def test_long_horizon_statistics(dev, oracle_lib, name):
     assert s['z'] < 3.0, (k, s)
     assert s['ks'] < s['ks_crit'], (k, s)
   assert stats['terminations']['z'] < 3.0, stats['terminations']
-  if div_fma <= Td:  # the yardstick crosses 1e-4 inside the first-episode window
-    assert div_hip >= 0.5 * div_fma, stats['divergence_steps_to_1e-4']
+  assert div_fma <= Td, ('the yardstick never crosses the divergence threshold', stats)
+  assert div_hip >= 0.5 * div_fma, stats['divergence_steps']
   assert ratio <= 4.0, ratio
   assert slope_hip <= 1.5 * max(slope_fma, 1e-3), stats['growth_log10_per_step']

@@ -9,11 +9,12 @@ stamp points as `;BXPHASE k` comments, code not scheduled across them):
 
 Every instruction is attributed to the phase whose mark ENDS its stretch of
 code (the next `;BXPHASE` in program order), with the loop depth LLVM
-annotates on its basic block; the per-step dynamic estimate multiplies each
-stretch by the trip count of its depth (the `--trips` per depth, default the
-Ant rollout kernel's: depth 1 = steps (1 per step), depth 2 = scan
-iterations per step (5), depth 3 = substeps per iteration... as LLVM nests
-them: see the printed table, which keeps depth apart).
+annotates on its basic block. A loop's block laid out past the loop's marks
+(its stretch ends at a mark outside the loop) goes to the loop body's last
+phase. Per loop depth the totals are exact; the per-phase split follows the
+layout. Per env step (the Ant rollout kernel): depth 4 = the substep loop (10
+trips), depth 3 = the collision part of a substep pair (5), depths 1-2 once
+(tools/lane_use.py TRIPS).
 
 Instruction classes: VALU arithmetic (fma / mul / add), transcendental,
 compare / select, DPP lane moves, SGPR-lane moves (readlane / writelane:
@@ -71,6 +72,7 @@ def parse(path, sym):
   pending = []  # (depth, class) since the last mark
   out = defaultdict(Counter)  # (phase, depth) -> class counts
   depth = 0
+  marks_at = defaultdict(list)  # loop depth -> the marks seen at that depth
   for l in lines[start + 1:]:
     if l.startswith('.Lfunc_end'):
       break
@@ -81,8 +83,15 @@ def parse(path, sym):
     s = l.strip()
     m = re.match(r';\s*BXPHASE (\d+)', s)
     if m:
+      marks_at[depth].append(int(m.group(1)))
       for d, c in pending:
-        out[(m.group(1), d)][c] += 1
+        # a loop's block that LLVM laid out past the loop's marks (the mark
+        # ending the stretch sits at a shallower depth) is the loop body's
+        # last phase: the one ending at the loop's highest mark
+        ph = m.group(1)
+        if d > depth and marks_at.get(d):
+          ph = str(max(marks_at[d]))
+        out[(ph, d)][c] += 1
       pending = []
       continue
     if not s or s.startswith((';', '.')):
