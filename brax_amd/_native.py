@@ -34,6 +34,8 @@ _SIGS = {
     'bx_system_destroy': ([C.c_void_p], C.c_int),
     'bx_system_lanes': ([C.c_void_p], C.c_int),
     'bx_system_lds_bytes': ([C.c_void_p], C.c_int),
+    'bx_system_plan': ([C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                        C.POINTER(C.c_int32)], C.c_int),
     'bx_system_set_single': ([C.c_void_p, C.c_int], C.c_int),
     'bx_system_set_variant': ([C.c_void_p, C.c_int, C.c_int], C.c_int),
     'bx_system_set_block': ([C.c_void_p, C.c_int], C.c_int),

@@ -1030,6 +1030,18 @@ int bx_system_destroy(bx_system* S) {
   return 0;
 }
 
+// the host half of bx_system_create: the kernel plan of a descriptor (no device)
+int bx_system_plan(const bx_desc* desc, const bx_reset_desc* reset, int32_t* mode,
+                   int32_t* lanes, int32_t* lds_bytes) {
+  if (!desc || !mode || !lanes || !lds_bytes) return fail("null argument");
+  bx_system S;
+  if (int rc = build_blob(desc, reset, &S)) return rc;
+  *mode = S.mode;
+  *lanes = S.L;
+  *lds_bytes = (int32_t)step_lds(&S);
+  return 0;
+}
+
 int bx_system_lanes(bx_system* S) { return S ? S->L : 0; }
 int bx_system_lds_bytes(bx_system* S) { return S ? (int)step_lds(S) : 0; }
 

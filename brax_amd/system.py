@@ -151,6 +151,25 @@ class System:
     """LDS bytes per workgroup of the System.step kernel (bx_system_lds_bytes)."""
     return _native.lib().bx_system_lds_bytes(self._h)
 
+  @staticmethod
+  def plan(config):
+    """The kernel plan `config` compiles to, on the host without a device
+    (bx_system_plan): {'mode': 1 SINGLE / 3 MULTI / 0 item loops, 'lanes':
+    threads per env, 'lds_bytes': the System.step kernel's LDS per workgroup,
+    'envs_per_cu_by_lds': what 160 KB of LDS holds}."""
+    vc, desc, meta = compiler.compile_system(config)
+    rdesc = compiler.compile_reset(vc, meta['body_index'])
+    cd, keep = abi.make_desc(desc)
+    rd, keep_r = abi.make_reset_desc(rdesc, meta['num_joint_dof'])
+    mode, lanes, lds = C.c_int32(), C.c_int32(), C.c_int32()
+    _native.check(_native.lib().bx_system_plan(C.byref(cd), C.byref(rd), C.byref(mode),
+                                               C.byref(lanes), C.byref(lds)))
+    del keep, keep_r
+    per_wg = lds.value
+    envs_per_wg = max(64 // lanes.value, 1)
+    return {'mode': mode.value, 'lanes': lanes.value, 'lds_bytes': per_wg,
+            'envs_per_cu_by_lds': (160 * 1024 // per_wg) * envs_per_wg if per_wg else None}
+
   def _create(self, reset_desc):
     cd, keep = abi.make_desc(self.desc)
     rd, keep_r = abi.make_reset_desc(reset_desc, self.num_joint_dof)

@@ -307,6 +307,14 @@ int bx_system_destroy(bx_system* sys);
  * one wavefront, or a whole 128/256-thread workgroup for large scenes. */
 int bx_system_lanes(bx_system* sys);
 
+/* The host half of bx_system_create, without a device: the kernel plan the
+ * descriptor compiles to -- mode (1 SINGLE: register-hoisted, one env per
+ * 16/32/64 lanes; 3 MULTI: one env per 256-thread workgroup; 0 item loops),
+ * threads per env, and the System.step kernel's LDS bytes per workgroup
+ * (160 KB per CU / that = envs a CU holds at once). */
+int bx_system_plan(const bx_desc* desc, const bx_reset_desc* reset, int32_t* mode,
+                   int32_t* lanes, int32_t* lds_bytes);
+
 /* LDS bytes per workgroup of this system's System.step kernel (the current
  * variant): with 160 KB per CU it sets how many envs a CU holds at once (the
  * large-scene kernel runs one env per 256-thread workgroup). A diagnostic

@@ -1,0 +1,39 @@
+"""The kernel plan each system compiles to, on the host (bx_system_plan: the
+host half of bx_system_create, no device): which step kernel runs it and the
+LDS its workgroup needs, i.e. how many envs a CU holds at once."""
+import pytest
+
+from brax_amd.system import System
+from tests.helpers import config_for
+
+LDS_CU = 160 * 1024  # MI355X LDS per CU
+
+
+@pytest.mark.parametrize('name', ['ant', 'humanoid', 'halfcheetah', 'humanoidstandup'])
+def test_env_systems_run_the_register_hoisted_kernel(name):
+  p = System.plan(config_for(name))
+  assert p['mode'] == 1 and p['lanes'] == 16, p
+  # four envs per one-wave workgroup
+  assert 0 < p['lds_bytes'] <= LDS_CU // 4, p
+
+
+@pytest.mark.parametrize('cutoff', [0, 36])
+def test_ant_mountain4_fits_three_envs_per_cu(cutoff):
+  """BASELINE configs[4]: Ant Mountain(4) runs the large-scene kernel (one env
+  per 256-thread workgroup) with 6-word contact slots and b slots for the
+  630 two-way rows only, so three envs share a CU's LDS (two until round 3:
+  73.7 KB per env); 2,048 envs then take 3 residency rounds instead of 4."""
+  cfg = config_for('mountain4')
+  cfg.collider_cutoff = cutoff
+  p = System.plan(cfg)
+  assert p['mode'] == 3 and p['lanes'] == 256, p
+  assert p['lds_bytes'] * 3 <= LDS_CU, p
+  assert p['envs_per_cu_by_lds'] == 3, p
+
+
+def test_plan_refuses_a_null_descriptor():
+  import ctypes as C
+  from brax_amd import _native
+  v = C.c_int32()
+  rc = _native.lib().bx_system_plan(None, None, C.byref(v), C.byref(v), C.byref(v))
+  assert rc != 0 and b'null' in _native.lib().bx_last_error()
