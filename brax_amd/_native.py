@@ -33,6 +33,7 @@ _SIGS = {
                           C.POINTER(C.c_void_p)], C.c_int),
     'bx_system_destroy': ([C.c_void_p], C.c_int),
     'bx_system_lanes': ([C.c_void_p], C.c_int),
+    'bx_system_env_lanes': ([C.c_void_p], C.c_int),
     'bx_system_lds_bytes': ([C.c_void_p], C.c_int),
     'bx_system_plan': ([C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                         C.POINTER(C.c_int32)], C.c_int),
@@ -74,6 +75,7 @@ _SIGS = {
     'bx_phase_capsule_plane': ([C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
                                 C.c_int64, C.c_void_p], C.c_int),
     'bx_debug_stamps': ([C.POINTER(C.c_ulonglong), C.c_int], C.c_int),
+    'bx_debug_partner': ([C.c_void_p, C.c_int, C.c_void_p], C.c_int),
     'bx_uniform': ([C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_float, C.c_float,
                     C.c_void_p], C.c_int),
     'bx_uniform_epoch': ([C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_void_p,

@@ -53,6 +53,7 @@ struct bx_system {
   bool multi_ok = false;  // MODE_MULTI (3): large pbd scenes, 256 threads per env
   int fold = 0;     // every joint j has torque actuator j (the Ant / Humanoid env kernels)
   int jb = 0;       // the joint-halves env kernels may own body copies (JB, build_blob)
+  int sh = 0;       // the spherical joint halves at 32 lanes (the Humanoid env kernels)
   size_t lds_env = 0;    // bytes per block for the per-env kernels
   size_t lds_reset = 0;  // bytes per block for default_qp
 };
@@ -557,6 +558,45 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     for (int a = 0; a < K; a++)
       if (d->act_joint[a] != a) H.act_same = 0;
   }
+  // JB's body conditions (the env kernels whose joint-halves lanes own body
+  // copies): every body on no joint side is frozen in all dimensions
+  // (position, rotation and the quaternion's vector part masks zero) and
+  // touches contact rows only as the plane side of one-way rows (its record
+  // then never changes and its contact sums are zeros)
+  auto jb_bodies_ok = [&]() {
+    std::vector<char> side(N, 0);
+    for (int j = 0; j < J; j++) side[d->joint_body_p[j]] = side[d->joint_body_c[j]] = 1;
+    for (int b = 0; b < N; b++) {
+      if (side[b]) continue;
+      const uint32_t* bw = &B.w[H.o_body + b * BODY_STRIDE];
+      for (int k = 0; k < 3; k++)
+        if (bw[BODY_PM + k] != fbits(0.0) || bw[BODY_RM + k] != fbits(0.0)) return false;
+      // (the reference's quaternion mask keeps w at 1 for a frozen rotation:
+      // integrators.py's [0] + frozen.rotation; the w update is an exact zero)
+      for (int k = 1; k < 4; k++)
+        if (bw[BODY_QM + k] != fbits(0.0)) return false;
+    }
+    for (int x = 0; x < R; x++) {
+      if (!side[d->row_body_a[x]]) return false;
+      if (!side[d->row_body_b[x]] && !d->col_oneway[d->row_group[x]]) return false;
+    }
+    return true;
+  };
+  // the spherical joint halves (the Humanoid env kernels at 32 lanes per env,
+  // pbd_kernels.hip joint_apply_half_sph): spherical joints only, each driven
+  // by the torque actuator of its index, <= 16 of them, one collider group of
+  // one-way capsule-plane rows, <= 16 rows at one per lane, gather lists <= 4,
+  // no forces, JB's body conditions. The lane image's joint-halves regions
+  // then map lane l to joint l & 15 and side l & 16 (the revolute halves: l & 7,
+  // l & 8). A/B knob BX_SPH_HALVES=0: off
+  bool sh = !(getenv("BX_SPH_HALVES") && atoi(getenv("BX_SPH_HALVES")) == 0) && H.single && L == 16 &&
+            !r2 && !c16 && mx <= 4 && max_groups <= 1 && J > 0 && J <= 16 && K == J && H.act_same &&
+            d->n_forces == 0;
+  for (int j = 0; j < J && sh; j++) sh = d->joint_type[j] == BX_JOINT_SPHERICAL;
+  for (int a = 0; a < K && sh; a++) sh = d->act_type[a] == BX_ACT_TORQUE;
+  for (int g = 0; g < G && sh; g++) sh = d->col_fn[g] == BX_COL_CAPSULE_PLANE && d->col_oneway[g];
+  sh = sh && jb_bodies_ok();
+  const int HB = sh ? 16 : 8;  // the joint halves' half width (lanes per side)
   // a contact row's 32 resolved words (LR_*): its record's geometry and
   // constants with the masses / inverse inertias of the bodies it names
   auto row_words = [&](int x, uint32_t* out) {
@@ -717,10 +757,12 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       for (int k = 0; k < 4; k++) put(lane, base + 10 + k, s[BODY_QM + k]);
     };
     // joint halves: lane m's side body (the parent of joint m & 7 on lanes
-    // 0-7 of each 16, the child on 8-15)
+    // 0-7 of each 16, the child on 8-15; the spherical halves: m & 15 on
+    // lanes 0-15 of each 32, the child on 16-31)
     auto side_body = [&](int m) {
-      const uint32_t* s = &B.w[H.o_joint + ((m & 7) < J ? (m & 7) : 0) * JOINT_STRIDE];
-      return (int)s[(m & 8) ? J_BC : J_BP];
+      const int j = m & (HB - 1);
+      const uint32_t* s = &B.w[H.o_joint + (j < J ? j : 0) * JOINT_STRIDE];
+      return (int)s[(m & HB) ? J_BC : J_BP];
     };
     for (int l = 0; l < LANE_IMG_LANES; l++) {
       const bool hasB = l < N;
@@ -728,15 +770,21 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       put_body(l, LI_BODY, b);
       put_joint(l, LI_JOINT, l < J ? l : 0);
       put_act(l, LI_ACT, l < K ? l : 0);
-      put_joint(l, LI_JOINT_H, (l & 7) < J ? (l & 7) : 0);
-      put_lim(l, LI_JLIM, l < J ? l : 0, 0);
-      put_lim(l, LI_JLIM12, l < J ? l : 0, 1);
-      put_lim(l, LI_JLIM12 + 8, l < J ? l : 0, 2);
-      put_lim(l, LI_JLIM_H, (l & 7) < J ? (l & 7) : 0, 0);
+      const int jh = l & (HB - 1);  // the lane's joint-halves joint
+      put_joint(l, LI_JOINT_H, jh < J ? jh : 0);
+      // the staged limit rows (stage_lim): lane l -> joint l; the spherical
+      // halves' child lanes l >= 16 -> joint l & 15 (no other kernel reads a
+      // joint there: lanes past J hold none)
+      const int jl_ = sh ? (l & 15) : l;
+      put_lim(l, LI_JLIM, jl_ < J ? jl_ : 0, 0);
+      put_lim(l, LI_JLIM12, jl_ < J ? jl_ : 0, 1);
+      put_lim(l, LI_JLIM12 + 8, jl_ < J ? jl_ : 0, 2);
+      put_lim(l, LI_JLIM_H, jh < J ? jh : 0, 0);
       if (J > 0) {
-        // the joint-halves side: the parent's on lanes 0-7, the child's on 8-15
-        const bool child = (l & 8) != 0;
-        const uint32_t* s = &B.w[H.o_joint + ((l & 7) < J ? (l & 7) : 0) * JOINT_STRIDE];
+        // the joint-halves side: the parent's on lanes 0-7, the child's on
+        // 8-15 (the spherical halves: 0-15, 16-31)
+        const bool child = (l & HB) != 0;
+        const uint32_t* s = &B.w[H.o_joint + (jh < J ? jh : 0) * JOINT_STRIDE];
         const int body = (int)s[child ? J_BC : J_BP];
         const uint32_t* bw = &B.w[H.o_body + body * BODY_STRIDE];
         for (int k = 0; k < 3; k++) {
@@ -744,16 +792,18 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
           put(l, LI_SIDE_H + LS_AX0 + k, s[(child ? J_AXC : J_AXP) + k]);
           put(l, LI_SIDE_H + LS_AX2 + k, s[(child ? J_AXC : J_AXP) + 6 + k]);
           put(l, LI_SIDE_H + LS_I + k, bw[BODY_I + k]);
+          put(l, LI_SIDE_AX1 + k, s[(child ? J_AXC : J_AXP) + 3 + k]);
         }
         put(l, LI_SIDE_H + LS_M, bw[BODY_MASS]);
         put(l, LI_SIDE_H + LS_SG, fbits(child ? -1.0 : 1.0));
         put(l, LI_SIDE_H + LS_BODY, (uint32_t)body);
         // JB: the side body's record and gather lists; LS_OWN on the lowest
-        // lane of the 16 whose side is that body
-        const bool hasS = (l & 7) < J;
+        // lane of the env's (16, or 32 for the spherical halves) whose side
+        // is that body
+        const bool hasS = jh < J;
         bool own = hasS;
-        for (int m = l & ~15; m < l; m++)
-          if ((m & 7) < J && side_body(m) == body) own = false;
+        for (int m = l & ~(2 * HB - 1); m < l; m++)
+          if ((m & (HB - 1)) < J && side_body(m) == body) own = false;
         put(l, LI_SIDE_H + LS_OWN, own ? 1u : 0u);
         put_body(l, LI_BODY_J, body);
         put_list(l, LI_JL_J, jl[body], hasS, (uint32_t)(2 * J));
@@ -762,7 +812,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         if (hasS && !cl[body].empty()) czj |= (uint32_t)cl[body][0] & 0x7F000000u;
         put_list(l, LI_CL_J, cl[body], hasS, czj);
       }
-      put_act(l, LI_ACT_H, (l & 7) < K ? (l & 7) : 0);
+      put_act(l, LI_ACT_H, jh < K ? jh : 0);
       if (R > 0) {
         uint32_t rw[32];
         row_words(l < R ? l : 0, rw);
@@ -799,7 +849,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
                                                      c16, r2g),
                                       (c16 ? mx_ja : mx) <= 4 ? 4 : 8) & 1)) {
     H.l_jlim = jlim_at;
-    H.env_words = (jlim_at + 24 * L + 63) & ~63;
+    H.env_words = (jlim_at + 24 * (sh ? 32 : L) + 63) & ~63;  // the spherical halves: 32 lanes
   }
   H.total_words = (int)B.w.size();
   std::memcpy(B.w.data(), &H, sizeof(BlobHdr));
@@ -815,31 +865,15 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     S->feat = f;
     S->fold = (H.act_same && K == J && J > 0 && !(f & 2)) ? 1 : 0;
     // JB (the Ant / HalfCheetah env kernels: joint halves own body copies):
-    // every body on no joint side must be frozen in all dimensions (position,
-    // rotation and the quaternion's vector part masks zero) and touch
-    // contact rows only as the plane side of one-way rows (its record then
-    // never changes and its contact sums are zeros); no forces (they index
-    // bodies by lane)
+    // JB's body conditions (jb_bodies_ok) and no forces (they index bodies
+    // by lane)
     // (BX_NO_JB=1: off, the Ant / HalfCheetah kinds then take the all-kinds
     // kernel; the GPU tests run that fallback against the goldens too)
     const bool jb_off = getenv("BX_NO_JB") && atoi(getenv("BX_NO_JB"));
-    bool jb = S->fold && (f & 128) && !(f & 16) && L == 16 && !jb_off;
-    std::vector<char> side(N, 0);
-    for (int j = 0; j < J; j++) side[d->joint_body_p[j]] = side[d->joint_body_c[j]] = 1;
-    for (int b = 0; b < N && jb; b++) {
-      if (side[b]) continue;
-      const uint32_t* bw = &B.w[H.o_body + b * BODY_STRIDE];
-      for (int k = 0; k < 3; k++)
-        jb = jb && bw[BODY_PM + k] == fbits(0.0) && bw[BODY_RM + k] == fbits(0.0);
-      // (the reference's quaternion mask keeps w at 1 for a frozen rotation:
-      // integrators.py's [0] + frozen.rotation; the w update is an exact zero)
-      for (int k = 1; k < 4; k++) jb = jb && bw[BODY_QM + k] == fbits(0.0);
-    }
-    for (int x = 0; x < R && jb; x++) {
-      if (!side[d->row_body_a[x]]) jb = false;
-      if (!side[d->row_body_b[x]] && !d->col_oneway[d->row_group[x]]) jb = false;
-    }
+    const bool jb = S->fold && (f & 128) && !(f & 16) && L == 16 && !jb_off && jb_bodies_ok();
     S->jb = jb ? 1 : 0;
+    // the spherical halves (the Humanoid env kernels at 32 lanes)
+    S->sh = (sh && S->fold && f == (1 | 32)) ? 1 : 0;
   }
   // the MULTI kernel is instantiated for the lean feature set (revolute,
   // torque, capsule-plane / capsule-capsule, no forces)
@@ -1043,6 +1077,11 @@ int bx_system_plan(const bx_desc* desc, const bx_reset_desc* reset, int32_t* mod
 }
 
 int bx_system_lanes(bx_system* S) { return S ? S->L : 0; }
+// (the spherical halves run when the system's SINGLE kernel is the default
+// one: bx_system_set_variant to other lanes or modes leaves them out)
+int bx_system_env_lanes(bx_system* S) {
+  return S ? ((S->sh && S->mode == 1 && S->L == 16 && S->tpb >= 32) ? 32 : S->L) : 0;
+}
 int bx_system_lds_bytes(bx_system* S) { return S ? (int)step_lds(S) : 0; }
 
 int bx_system_set_single(bx_system* S, int on) {
@@ -1192,7 +1231,7 @@ static int env_step_impl(bx_system* S, const bx_env_params* env, int64_t n_envs,
   }
   if (S->mode == 1)
     HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a,
-                                  S->fold ? (1 | (S->jb ? 2 : 0)) : 0));
+                                  S->fold ? (1 | (S->jb ? 2 : 0) | (S->sh ? 4 : 0)) : 0));
   else if (S->mode == 3)  // MULTI-mode systems step envs with the item-loop kernel
     HIP_OK(launch_env_step_generic(S->L, 0, S->feat, S->tpb, n_envs,
                                    (size_t)S->hdr.env_words * 4, as_stream(stream), a));
@@ -1456,6 +1495,13 @@ int bx_phase_capsule_plane(bx_system* S, int64_t n_envs, int64_t plane, const fl
   if (!aligned16(in) || !aligned16(out)) return fail("SoA bases must be 16-byte aligned");
   if (R == 0) return 0;
   HIP_OK(launch_capsule_plane(S->blob, (int)R, n_envs, plane, in, out, out_plane, as_stream(stream)));
+  return 0;
+}
+
+int bx_debug_partner(float* out64, int lanes, void* stream) {
+  if (!out64) return fail("null argument");
+  if (lanes != 16 && lanes != 32) return fail("lanes must be 16 or 32");
+  HIP_OK(debug_partner(out64, lanes, as_stream(stream)));
   return 0;
 }
 

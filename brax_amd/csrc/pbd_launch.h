@@ -99,6 +99,7 @@ hipError_t launch_uniform_slabs(float* out, int64_t slab_n, int64_t n_slabs, uin
                                 uint64_t epoch_stride, float lo, float hi, hipStream_t s);
 
 hipError_t debug_stamps(unsigned long long* out, int reset);
+hipError_t debug_partner(float* out64, int lanes, hipStream_t s);
 // the feature mask F of the SINGLE-mode kernel BX_DISPATCH_SINGLE picks for
 // (lanes, system features, gather width): its bit 1 (F_SPH) says whether it
 // reads the LDS-staged joint limit rows

@@ -147,6 +147,13 @@ class System:
     self.lanes = _native.lib().bx_system_lanes(self._h)
 
   @property
+  def env_lanes(self):
+    """Threads per env of the Env.step / rollout kernels (bx_system_env_lanes):
+    32 where the env kernels split each joint over two lanes (the spherical
+    joint halves, Humanoid), else `lanes`."""
+    return _native.lib().bx_system_env_lanes(self._h)
+
+  @property
   def lds_bytes(self):
     """LDS bytes per workgroup of the System.step kernel (bx_system_lds_bytes)."""
     return _native.lib().bx_system_lds_bytes(self._h)

@@ -60,6 +60,7 @@ def _to_qp(a, dev):
 
 
 WIDE = 1e-2  # a sample whose own bound 2 x E32 exceeds this is ill-conditioned
+NEAR_TOL = 1e-3  # the ill-conditioned envs: distance to the nearest fp32 realisation (recorded)
 
 
 def _gate(got, ref, e32, field, split=True):
@@ -73,6 +74,7 @@ def _gate(got, ref, e32, field, split=True):
   Without `split` (the reset lift's discontinuity: any env may flip), one
   group."""
   nw = normwise(got, ref)
+  samples = getattr(e32, 'samples', None)
   e32 = np.broadcast_to(np.asarray(e32, np.float64), nw.shape)
   assert np.all(np.isfinite(got)), field
   ill = (2.0 * e32 > WIDE) if split else np.zeros(nw.shape, bool)
@@ -85,6 +87,15 @@ def _gate(got, ref, e32, field, split=True):
     record_margin(name, m, tol, n=int(sel.sum()))
     assert m <= tol, f'{name}: normwise {m:.3e} > tol {tol:.3e} ({int(sel.sum())} envs)'
     worst = max(worst, (m, tol))
+  if samples is not None and ill.any():
+    # an ill-conditioned env's branch (which contacts fire) is a coin toss
+    # under fp32 rounding: its distance to the NEAREST of Brax's fp32
+    # realisations (the envelope's runs) says whether the HIP result is one of
+    # them up to rounding on its branch (recorded, not asserted yet)
+    near = np.min([normwise(got, np.asarray(v)) for v in samples], axis=0)
+    near = np.broadcast_to(near, nw.shape)
+    record_margin(field + ':illcond_nearest', float(near[ill].max()), NEAR_TOL,
+                  n=int(ill.sum()), asserted=False)
   return worst
 
 
@@ -124,8 +135,15 @@ def _make_env(name, dev, **kw):
   return envs.get_environment(env_kind(name), device=dev, **kw)
 
 
+class _E32(np.ndarray):
+  """E32 per env, carrying the fp32 realisations it was taken over."""
+  samples = None
+
+
 def _env_err(vals, ref):
-  return np.max([normwise(v, ref) for v in vals], axis=0)
+  e = np.asarray(np.max([normwise(v, ref) for v in vals], axis=0), np.float64).view(_E32)
+  e.samples = vals
+  return e
 
 
 @pytest.mark.parametrize('name', ENV_TRAJ + SYS_TRAJ + [r + ':generic' for r in ROBOTS])
