@@ -588,8 +588,11 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // one-way capsule-plane rows, <= 16 rows at one per lane, gather lists <= 4,
   // no forces, JB's body conditions. The lane image's joint-halves regions
   // then map lane l to joint l & 15 and side l & 16 (the revolute halves: l & 7,
-  // l & 8). A/B knob BX_SPH_HALVES=0: off
-  bool sh = !(getenv("BX_SPH_HALVES") && atoi(getenv("BX_SPH_HALVES")) == 0) && H.single && L == 16 &&
+  // l & 8). Opt-in (BX_SPH_HALVES=1): measured slower than the 16-lane
+  // kernel (Humanoid rollout 37.7 vs 32.1 us per step at 4,096 envs): its two
+  // waves per SIMD share one VALU, and the halves' redundant shared geometry
+  // leaves 1.65x the VALU work per env (Kernels)
+  bool sh = getenv("BX_SPH_HALVES") && atoi(getenv("BX_SPH_HALVES")) == 1 && H.single && L == 16 &&
             !r2 && !c16 && mx <= 4 && max_groups <= 1 && J > 0 && J <= 16 && K == J && H.act_same &&
             d->n_forces == 0;
   for (int j = 0; j < J && sh; j++) sh = d->joint_type[j] == BX_JOINT_SPHERICAL;

@@ -262,16 +262,18 @@ template <int F> __device__ __forceinline__ bool is_oneway(int ow) {
 
 // Joint.apply_angle_update (joints.py:130-152): the impulse p of an angular
 // correction dq; each side's rotation update is linear in it
+// (ND: Newton-corrected quotients, the spherical kernels: pbd_math.h ndiv)
+template <bool ND = false>
 __device__ __forceinline__ v3 angle_impulse(const JointC& J, v3 dq) {
   float th = cancel_norm(dq);
-  v3 n = dq / (th + 1e-6f);
+  v3 n = dv3<ND>(dq, th + 1e-6f);
 #if defined(BX_TU_FAST)
   // w1 + w2 as one quadratic form in Ip + Ic (loop-invariant; SINGLE-mode TU)
-  float dl = -th / (dot(n, mul(J.Ip + J.Ic, n)) + 1e-6f);
+  float dl = dv<ND>(-th, dot(n, mul(J.Ip + J.Ic, n)) + 1e-6f);
 #else
   float w1 = dot(n, mul(J.Ip, n));
   float w2 = dot(n, mul(J.Ic, n));
-  float dl = -th / (w1 + w2 + 1e-6f);
+  float dl = dv<ND>(-th, w1 + w2 + 1e-6f);
 #endif
   return -dl * n;
 }
@@ -341,20 +343,23 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
   auto rp_ = [&](v3 v) { return rotate(v, p.rot); };
   auto rc_ = [&](v3 v) { return rotate(v, c.rot); };
 #endif
+  // the spherical kernels (the Humanoid family) divide with Newton-corrected
+  // quotients (pbd_math.h ndiv)
+  constexpr bool ND = (F & F_SPH) != 0;
   // positional constraint: apply_position_update (joints.py:154-195)
   v3 pw = p.pos + rp_(J.off_p);
   v3 cw = c.pos + rc_(J.off_c);
   v3 dx = pw - cw;
   v3 rp = pw - p.pos, rc = cw - c.pos;
   float cc = cancel_norm(dx);
-  v3 n = dx / (cc + 1e-6f);
+  v3 n = dv3<ND>(dx, cc + 1e-6f);
   v3 cr1 = cross(rp, n), cr2 = cross(rc, n);
   float w1 = 1.f / J.mp + dot(cr1, mul(J.Ip, cr1));
   float w2 = 1.f / J.mc + dot(cr2, mul(J.Ic, cr2));
-  float dl = -cc / (w1 + w2 + 1e-6f);
+  float dl = dv<ND>(-cc, w1 + w2 + 1e-6f);
   v3 pv = dl * n;
-  dpp = J.sp * (pv / J.mp);
-  dcp = J.sp * (-pv / J.mc);
+  dpp = J.sp * dv3<ND>(pv, J.mp);
+  dcp = J.sp * dv3<ND>(-pv, J.mc);
   // the angle constraints' impulses (apply_angle_update, joints.py:130-152);
   // each body's rotation update is linear in its angular impulse, so these
   // and the position constraint's add up before one quaternion product per
@@ -378,16 +383,16 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
       n1 = rotate(ref_p, fix);
     }
     v3 dq2 = cross(n1, ref_c);
-    pimp = angle_impulse(J, dq1) + angle_impulse(J, dq2);
+    pimp = angle_impulse<ND>(J, dq1) + angle_impulse<ND>(J, dq2);
   } else {
     v3 a1p = rp_(J.axp[0]), a2p = rp_(J.axp[1]);
     v3 a1c = rc_(J.axc[0]), a2c = rc_(J.axc[1]), a3c = rc_(J.axc[2]);
     v3 lon = cross(a3c, a1p);
-    lon = lon / (1e-6f + dir_norm(lon));
+    lon = dv3<ND>(lon, 1e-6f + dir_norm(lon));
     v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
-    xz = xz / (1e-6f + dir_norm(xz));
+    xz = dv3<ND>(xz, 1e-6f + dir_norm(xz));
     v3 a2n = cross(xz, a1p);
-    a2n = a2n / (1e-6f + dir_norm(a2n));
+    a2n = dv3<ND>(a2n, 1e-6f + dir_norm(a2n));
     float sg = signf(dot(a1p, a3c));
     v3 nv[3] = {a1p, -a2n * sg, a3c};
     v3 n1v[3] = {a2p, a1p, lon};
@@ -404,7 +409,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
         const bool below = pa < L.plo, above = pa > L.phi;
         const v3 n1 = turn(n1v[l], nv[l], below ? L.clo : L.chi, below ? L.slo : L.shi);
         const v3 dq = cross(n1, n2v[l]) * ((below || above) ? 1.f : 0.f);
-        pimp = pimp + angle_impulse(J, dq);
+        pimp = pimp + angle_impulse<ND>(J, dq);
         continue;
       }
       // limit_angle (joints.py:343-355)
@@ -416,7 +421,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
       q4 fix = quat_rot_axis(nv[l], ph);
       v3 n1 = rotate(n1v[l], fix);
       v3 dq = cross(n1, n2v[l]) * mask;
-      pimp = pimp + angle_impulse(J, dq);
+      pimp = pimp + angle_impulse<ND>(J, dq);
     }
   }
   const v3 Pp = J.sp * cross(rp, pv) + J.sa * pimp;
@@ -554,9 +559,16 @@ __device__ __forceinline__ void body_forces(const Cst& c, const BlobHdr& H, int 
 
 struct RowC {
   int group, a, b, fn, oneway;
-  int bslot;  // MULTI row image: the b side's contact slot
   v3 a_pos, a_end, b_pos, b_end;
-  float a_rad, b_rad, fric, elas, scale, thr, erp;
+  float a_rad, b_rad, fric, elas, scale, thr;
+  // erp (the legacy_spring impulse model) or, in the MULTI kernel (pbd only:
+  // no erp), the b side's contact slot from its row image: one register
+  // either way (a separate field took the MULTI kernel past 128 VGPRs, and
+  // its 256-thread workgroups from three per CU to one: tools/multi_occ.py)
+  union {
+    float erp;
+    int bslot;
+  };
   float ma, mb;
   v3 Ia, Ib;
 };
@@ -579,7 +591,6 @@ __device__ __forceinline__ RowC load_row(const Cst& c, const BlobHdr& H, int r) 
   x.scale = c.f(o + R_SCALE);
   x.thr = c.f(o + R_THR);
   x.erp = c.f(o + R_ERP);
-  x.bslot = -1;  // (the MULTI kernel's rows come from the row image)
   int oa = H.o_body + x.a * BODY_STRIDE, ob = H.o_body + x.b * BODY_STRIDE;
   x.ma = c.f(oa + BODY_MASS);
   x.mb = c.f(ob + BODY_MASS);
@@ -1473,20 +1484,20 @@ __device__ __forceinline__ void joint_apply_half_sph(const JointC& J, const JSid
   const v3 ro = wo - o.pos;
   const v3 dx = S.sg * (wo - xhl3<L>(wo));
   const float cc = cancel_norm(dx);
-  const v3 n = dx / (cc + 1e-6f);
+  const v3 n = ndiv3(dx, cc + 1e-6f);
   const v3 cr = cross(ro, n);
   const float wm = 1.f / S.m + dot(cr, mul(S.I, cr));
-  const float dl = -cc / (wm + xhl<L>(wm) + 1e-6f);
+  const float dl = ndiv(-cc, wm + xhl<L>(wm) + 1e-6f);
   const v3 pv = dl * n;
-  dpo = J.sp * ((S.sg * pv) / S.m);
+  dpo = J.sp * ndiv3(S.sg * pv, S.m);
   // the spherical frame (both lanes)
   const SphAxes X = sph_axes<L>(Mo, S, child);
   v3 lon = cross(X.a3c, X.a1p);
-  lon = lon / (1e-6f + dir_norm(lon));
+  lon = ndiv3(lon, 1e-6f + dir_norm(lon));
   v3 xz = dot(X.a1p, X.a1c) * X.a1c + dot(X.a1p, X.a2c) * X.a2c;
-  xz = xz / (1e-6f + dir_norm(xz));
+  xz = ndiv3(xz, 1e-6f + dir_norm(xz));
   v3 a2n = cross(xz, X.a1p);
-  a2n = a2n / (1e-6f + dir_norm(a2n));
+  a2n = ndiv3(a2n, 1e-6f + dir_norm(a2n));
   const float sg = signf(dot(X.a1p, X.a3c));
   // limit_angle on pseudo-angles (as joint_apply's lane-image rows)
   auto row = [&](v3 nv, v3 n1v, v3 n2v, const JLim& Lr) {
@@ -1495,7 +1506,7 @@ __device__ __forceinline__ void joint_apply_half_sph(const JointC& J, const JSid
     const bool below = pa < Lr.plo, above = pa > Lr.phi;
     const v3 n1 = turn(n1v, nv, below ? Lr.clo : Lr.chi, below ? Lr.slo : Lr.shi);
     const v3 dq = cross(n1, n2v) * ((below || above) ? 1.f : 0.f);
-    return angle_impulse(J, dq);
+    return angle_impulse<true>(J, dq);
   };
   // slot A: row 0 (nv a1p, n1 a2p, n2 lon) on the parent lane, row 2 (a3c,
   // lon, a2c) on the child's; slot B: row 1 (-a2n sg, a1p, xz), the parent's
@@ -2986,7 +2997,6 @@ __device__ __forceinline__ RowC load_row_img(const Cst& c, const BlobHdr& H, int
   x.scale = f(LR_SCALE);
   x.thr = f(LR_THR);
   x.bslot = (int)w[LR_MBSLOT];  // (the MULTI image carries no erp)
-  x.erp = 0.f;
   x.ma = f(LR_MA);
   x.mb = f(LR_MB);
   x.Ia = f3(LR_IA);
@@ -4097,11 +4107,16 @@ template <int L, int MODE, int F, int M>
 __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kernel(StepArgs A) {
   system_step_body<L, MODE, F, M>(A);
 }
-// the MULTI kernel held to 128 VGPRs (four waves per SIMD by registers; A/B
-// knob BX_MULTI_WPE=4, launch_system_step_multi)
-template <int M>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-system_step_multi_w4_kernel(StepArgs A) {
+// the MULTI kernel held to 256 registers per lane (VGPRs + AGPRs): two waves
+// per SIMD, so two of its 4-wave workgroups per CU. Past 256 (the row image's
+// b-slot index took it to 256 + 4) one wave per SIMD fits and the CU holds
+// ONE workgroup: Ant Mountain(4) at 2,048 envs ran 1.8x slower
+// (tools/multi_occ.py: the step time grew with the batch from 256 envs on).
+// A/B knob BX_MULTI_WPE=4: held to 128 (four waves per SIMD: the LDS then
+// admits three workgroups; spills)
+template <int M, int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W)))
+system_step_multi_kernel(StepArgs A) {
   system_step_body<256, MODE_MULTI, F_CC | F_TW, M>(A);
 }
 
@@ -5161,19 +5176,19 @@ hipError_t launch_system_step_multi(int feat, int mr, int64_t n_envs, size_t lds
   static const bool w4 = getenv("BX_MULTI_WPE") && atoi(getenv("BX_MULTI_WPE")) == 4;
   if (w4) {
     switch (mr) {
-      case 1: launch_one<StepArgs>(system_step_multi_w4_kernel<1>, grid, 256, lds, s, a); break;
-      case 2: launch_one<StepArgs>(system_step_multi_w4_kernel<2>, grid, 256, lds, s, a); break;
-      case 3: launch_one<StepArgs>(system_step_multi_w4_kernel<3>, grid, 256, lds, s, a); break;
-      case 4: launch_one<StepArgs>(system_step_multi_w4_kernel<4>, grid, 256, lds, s, a); break;
+      case 1: launch_one<StepArgs>(system_step_multi_kernel<1, 4>, grid, 256, lds, s, a); break;
+      case 2: launch_one<StepArgs>(system_step_multi_kernel<2, 4>, grid, 256, lds, s, a); break;
+      case 3: launch_one<StepArgs>(system_step_multi_kernel<3, 4>, grid, 256, lds, s, a); break;
+      case 4: launch_one<StepArgs>(system_step_multi_kernel<4, 4>, grid, 256, lds, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
   switch (mr) {
-    case 1: launch_one<StepArgs>(system_step_kernel<256, MODE_MULTI, F_LEAN, 1>, grid, 256, lds, s, a); break;
-    case 2: launch_one<StepArgs>(system_step_kernel<256, MODE_MULTI, F_LEAN, 2>, grid, 256, lds, s, a); break;
-    case 3: launch_one<StepArgs>(system_step_kernel<256, MODE_MULTI, F_LEAN, 3>, grid, 256, lds, s, a); break;
-    case 4: launch_one<StepArgs>(system_step_kernel<256, MODE_MULTI, F_LEAN, 4>, grid, 256, lds, s, a); break;
+    case 1: launch_one<StepArgs>(system_step_multi_kernel<1, 2>, grid, 256, lds, s, a); break;
+    case 2: launch_one<StepArgs>(system_step_multi_kernel<2, 2>, grid, 256, lds, s, a); break;
+    case 3: launch_one<StepArgs>(system_step_multi_kernel<3, 2>, grid, 256, lds, s, a); break;
+    case 4: launch_one<StepArgs>(system_step_multi_kernel<4, 2>, grid, 256, lds, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -152,6 +152,35 @@ __device__ __forceinline__ float clampf(float x, float lo, float hi) {
 }
 __device__ __forceinline__ float signf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
 
+// a / b with the fast reciprocal's quotient corrected by one Newton step on
+// the exact (fma) residual: IEEE division's correctly rounded result in all
+// but rare ties, at 4 VALU instead of 2 (rcp, mul) or ~10 (the IEEE
+// sequence). The spherical joints' constraint math (the Humanoid kernels):
+// there the fast quotient's extra ulp doubled the long-horizon divergence
+// against Brax's fp32 (tests/test_gpu_long_horizon.py; IEEE division
+// builds brought the ratio from 2.3 to 0.95, square roots changed nothing)
+__device__ __forceinline__ float ndiv(float a, float b) {
+  const float r = __builtin_amdgcn_rcpf(b);
+  const float q = a * r;
+  return __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+}
+__device__ __forceinline__ v3 ndiv3(v3 a, float b) {
+  const float r = __builtin_amdgcn_rcpf(b);
+  const v3 q = a * r;
+  return mk(__builtin_fmaf(__builtin_fmaf(-b, q.x, a.x), r, q.x),
+            __builtin_fmaf(__builtin_fmaf(-b, q.y, a.y), r, q.y),
+            __builtin_fmaf(__builtin_fmaf(-b, q.z, a.z), r, q.z));
+}
+// `a / b` (ND false: the build's division) or ndiv (ND true)
+template <bool ND>
+__device__ __forceinline__ float dv(float a, float b) {
+  if constexpr (ND) return ndiv(a, b); else return a / b;
+}
+template <bool ND>
+__device__ __forceinline__ v3 dv3(v3 a, float b) {
+  if constexpr (ND) return ndiv3(a, b); else return a / b;
+}
+
 // q / |q| with the bare v_sqrt_f32 (the Ant env kernel's integrator only)
 __device__ __forceinline__ q4 qnormalize_bare(q4 r) {
   float rn = __builtin_amdgcn_sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);

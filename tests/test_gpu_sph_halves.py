@@ -1,9 +1,11 @@
-"""The spherical joint halves (the Humanoid env kernels at 32 lanes per env:
-pbd_kernels.hip joint_apply_half_sph / act_torque_half_sph): the partner
-exchange on its own, and the 32-lane kernels against the 16-lane kernel they
-replace, bit for bit (BX_SPH_HALVES=0 builds a system without them). The
-16-lane kernel itself is held to the reference by test_gpu_parity's Humanoid
-goldens, which the default (32-lane) env kernels run too.
+"""The spherical joint halves (opt-in, BX_SPH_HALVES=1: the Humanoid env
+kernels at 32 lanes per env, pbd_kernels.hip joint_apply_half_sph /
+act_torque_half_sph; measured slower than the default 16-lane kernel): the
+partner exchange on its own, the 32-lane kernels' K-step rollout launch bit
+for bit against their own chained steps, and both against the 16-lane kernel
+(which test_gpu_parity holds to the reference's goldens) within rounding:
+the two compile the same arithmetic to differently contracted FMAs (the
+first steps from reset differ by ~4e-9).
 """
 import ctypes as C
 import os
@@ -47,18 +49,23 @@ def _env(name, B, halves, dev):
       os.environ['BX_SPH_HALVES'] = old
 
 
-def _same(a, b, t):
+def _close(a, b, t, tol):
+  """Every field within `tol` relative to its magnitude; done flags equal."""
   for x, y in ((a.qp.pos, b.qp.pos), (a.qp.rot, b.qp.rot), (a.qp.vel, b.qp.vel),
-               (a.qp.ang, b.qp.ang), (a.obs, b.obs), (a.reward, b.reward), (a.done, b.done)):
-    assert torch.equal(x, y), (t, float((x - y).abs().max()))
+               (a.qp.ang, b.qp.ang), (a.obs, b.obs), (a.reward, b.reward)):
+    err = float((x - y).abs().max() / y.abs().max().clamp(min=1.0))
+    assert err <= tol, (t, err)
+  assert torch.equal(a.done, b.done), t
 
 
 def test_env_lanes(dev):
-  """Humanoid's env kernels take the halves; Ant, HalfCheetah and
-  HumanoidStandup (its 22 ground rows: two per lane at 16 lanes) do not."""
+  """Humanoid's env kernels take the halves when asked; by default, and for
+  Ant, HalfCheetah and HumanoidStandup (its 22 ground rows: two per lane at
+  16 lanes) never."""
   from brax_amd import envs
   assert _env('humanoid', 8, True, dev).unwrapped.sys.env_lanes == 32
   assert _env('humanoid', 8, False, dev).unwrapped.sys.env_lanes == 16
+  assert envs.create('humanoid', batch_size=8, device=dev).unwrapped.sys.env_lanes == 16
   for name in ('ant', 'halfcheetah', 'humanoidstandup'):
     s = envs.create(name, batch_size=8, device=dev).unwrapped.sys
     assert s.env_lanes == s.lanes == 16, name
@@ -67,23 +74,27 @@ def test_env_lanes(dev):
 @pytest.mark.parametrize('B', [1, 255, 4096])
 def test_halves_match_the_16_lane_kernel(dev, B):
   """Env.step (one launch per step, Episode + AutoReset: the episodes end
-  inside the run) and a K-step rollout launch: every output bit-identical
-  to the 16-lane kernel's, at an odd batch (a half-filled last wave) too."""
+  inside the run) against the 16-lane kernel within rounding, at an odd batch
+  (a half-filled last wave) too; then a K-step rollout launch of the halves
+  bit for bit against their own chained Env.step launches."""
   from brax_amd.envs.rollout import rollout
   on, off = _env('humanoid', B, True, dev), _env('humanoid', B, False, dev)
   assert on.unwrapped.sys.env_lanes == 32 and off.unwrapped.sys.env_lanes == 16
   a, b = on.reset(np.array([4, 2], np.uint32)), off.reset(np.array([4, 2], np.uint32))
-  _same(a, b, 'reset')
+  _close(a, b, 'reset', 0.0)
   g = torch.Generator(device='cpu').manual_seed(B)
-  steps = 12 if B < 4096 else 4
-  for t in range(steps):
+  for t in range(6):  # (the episodes are 7 steps: none ends here)
     act = (torch.rand((B, on.action_size), generator=g) * 2 - 1).to(dev)
     a, b = on.step(a, act), off.step(b, act)
-    _same(a, b, t)
-  assert B == 4096 or float(a.done.sum()) > 0
+    _close(a, b, t, 1e-5)
   acts = (torch.rand((10, B, on.action_size), generator=g) * 2 - 1).to(dev)
-  fa, ta = rollout(on, a, acts)
-  fb, tb = rollout(off, b, acts)
-  assert torch.equal(ta.qp, tb.qp) and torch.equal(ta.obs, tb.obs)
-  assert torch.equal(ta.reward, tb.reward) and torch.equal(ta.done, tb.done)
-  _same(fa, fb, 'rollout')
+  final, tr = rollout(on, a, acts)
+  st = a
+  for t in range(acts.shape[0]):
+    st = on.step(st, acts[t])
+    q = torch.cat([st.qp.pos, st.qp.rot, st.qp.vel, st.qp.ang], -1)
+    assert torch.equal(tr.qp[t][..., :13], q), t
+    assert torch.equal(tr.obs[t], st.obs) and torch.equal(tr.reward[t], st.reward), t
+    assert torch.equal(tr.done[t], st.done), t
+  assert float(tr.done.sum()) > 0  # the episodes ended inside the rollout
+  assert torch.equal(final.qp.pos, st.qp.pos) and torch.equal(final.obs, st.obs)
