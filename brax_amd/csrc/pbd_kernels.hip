@@ -265,6 +265,7 @@ template <int F> __device__ __forceinline__ bool is_oneway(int ow) {
 // (ND: Newton-corrected quotients, the spherical kernels: pbd_math.h ndiv)
 template <bool ND = false>
 __device__ __forceinline__ v3 angle_impulse(const JointC& J, v3 dq) {
+  BX_IEEE_IN_JOINT
   float th = cancel_norm(dq);
   v3 n = dv3<ND>(dq, th + 1e-6f);
 #if defined(BX_TU_FAST)
@@ -333,6 +334,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
                             v3& dcp, q4& dcr, bool useJL = false, JLim JL = JLim{},
                             const uint4* LI = nullptr) {
   // each body rotates three or four of the joint's vectors: one matrix each
+  BX_IEEE_IN_JOINT
   // in the SINGLE-mode TU (the item-loop / MULTI kernels keep rotate():
   // their culled Mountain scene sits closer to its gate)
 #if defined(BX_TU_FAST)
@@ -354,8 +356,8 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
   float cc = cancel_norm(dx);
   v3 n = dv3<ND>(dx, cc + 1e-6f);
   v3 cr1 = cross(rp, n), cr2 = cross(rc, n);
-  float w1 = 1.f / J.mp + dot(cr1, mul(J.Ip, cr1));
-  float w2 = 1.f / J.mc + dot(cr2, mul(J.Ic, cr2));
+  float w1 = BX_INV(J.mp) + dot(cr1, mul(J.Ip, cr1));
+  float w2 = BX_INV(J.mc) + dot(cr2, mul(J.Ic, cr2));
   float dl = dv<ND>(-cc, w1 + w2 + 1e-6f);
   v3 pv = dl * n;
   dpp = J.sp * dv3<ND>(pv, J.mp);
@@ -640,6 +642,7 @@ template <int F>
 __device__ __forceinline__ void contact_gen(const RowC& R, const QP& a, const QP& b, v3& pos, v3& vel, v3& n,
                             float& pen) {
   if (is_plane<F>(R.fn)) {
+  BX_IEEE_IN_CONTACT
     v3 e = a.pos + rotate(R.a_end, a.rot);
     n = rotate(mk(0.f, 0.f, 1.f), b.rot);
     pos = e - n * R.a_rad;
@@ -1058,6 +1061,7 @@ template <int F, bool RAWL = false>
 __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, const QP& b, const v3& ao_pos,
                                   const q4& ao_rot, const v3& bo_pos, const q4& bo_rot, v3 cpos,
                                   v3 n, float cpen, v3& oap, q4& oar, v3& obp, q4& obr) {
+  BX_IEEE_IN_CONTACT
   float sc = R.scale;
   if (is_oneway<F>(R.oneway)) {
     v3 pp = cpos, pc = cpos + n * cpen;
@@ -1065,7 +1069,7 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
     pp = pp - a.pos;
     float c = dot(dx, n);
     v3 cr1 = cross(pp, n);
-    float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
+    float w1 = BX_INV(R.ma) + dot(cr1, mul(R.Ia, cr1));
     float dl = -c / (w1 + 1e-6f);
     float cm = c < 0.f ? 1.f : 0.f;
     v3 pv = dl * n * cm;
@@ -1077,13 +1081,13 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
     float c2 = cancel_norm(dt);
     v3 n2 = dt / (c2 + 1e-6f);
     cr1 = cross(pp, n2);
-    w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
+    w1 = BX_INV(R.ma) + dot(cr1, mul(R.Ia, cr1));
     float dlt = -c2 / (w1 + 0.f);
     float sm = fabsf(dlt) < fabsf(R.fric * dl) ? 1.f : 0.f;
     // the normal and friction impulses share the lever arm: one position and
     // one quaternion update for their sum (both linear in the impulse)
     pv = pv + dlt * n2 * sm * cm;
-    oap = sc * (pv / R.ma);
+    oap = sc * BX_DIVM(pv, R.ma);
     if constexpr (RAWL) {
       const v3 L = sc * cross(pp, pv);
       oar = q4{0.f, L.x, L.y, L.z};
@@ -1098,8 +1102,8 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
   v3 pc = cpos + n * cpen / 2.f - b.pos;
   float c = -cpen;
   v3 cr1 = cross(pp, n), cr2 = cross(pc, n);
-  float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
-  float w2 = 1.f / R.mb + dot(cr2, mul(R.Ib, cr2));
+  float w1 = BX_INV(R.ma) + dot(cr1, mul(R.Ia, cr1));
+  float w2 = BX_INV(R.mb) + dot(cr2, mul(R.Ib, cr2));
   float dl = -c / (w1 + w2 + 1e-6f);
   float cm = c < 0.f ? 1.f : 0.f;
   v3 pv = dl * n * cm;
@@ -1118,14 +1122,14 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
   v3 n2 = dt / (c2 + 1e-6f);
   cr1 = cross(pp, n2);
   cr2 = cross(pc, n2);
-  w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
-  w2 = 1.f / R.mb + dot(cr2, mul(R.Ib, cr2));
+  w1 = BX_INV(R.ma) + dot(cr1, mul(R.Ia, cr1));
+  w2 = BX_INV(R.mb) + dot(cr2, mul(R.Ib, cr2));
   float dlt = -c2 / (w1 + w2);
   float sm = fabsf(dlt) < fabsf(dl) ? 1.f : 0.f;
   const v3 pt = dlt * n2 * sm * cm;
   const v3 ps = pv + pt;
-  oap = sc * (ps / R.ma);
-  obp = sc * (-ps / R.mb);
+  oap = sc * BX_DIVM(ps, R.ma);
+  obp = sc * BX_DIVM(-ps, R.mb);
   if constexpr (RAWL) {
     const v3 La = sc * (la + cross(pp, pt)), Lb = -sc * (lb + cross(pc, pt));
     oar = q4{0.f, La.x, La.y, La.z};
@@ -1143,6 +1147,7 @@ template <int F>
 __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const QP& a, const QP& b, v3 aop,
                                  v3 aov, v3 aoa, v3 bop, v3 bov, v3 boa, v3 cpos, v3 n, float cpen,
                                  float dlam, v3& oav, v3& oaa, v3& obv, v3& oba) {
+  BX_IEEE_IN_CONTACT
   v3 ra = cpos - a.pos, rb = cpos - b.pos;
   v3 rv = is_oneway<F>(R.oneway) ? a.vel + cross(a.ang, ra)
                    : (a.vel + cross(a.ang, ra)) - (b.vel + cross(b.ang, rb));
@@ -1156,12 +1161,12 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
   v3 pdyn;
   if (is_oneway<F>(R.oneway)) {
     v3 aw = cross(ra, vtd);
-    float w = 1.f / R.ma + dot(aw, aw);
+    float w = BX_INV(R.ma) + dot(aw, aw);
     pdyn = dvel / (w + 1e-6f);
   } else {
     v3 a1 = cross(ra, vtd), a2 = cross(rb, vtd);
-    float w1 = 1.f / R.ma + dot(a1, mul(R.Ia, a1));
-    float w2 = 1.f / R.mb + dot(a2, mul(R.Ib, a2));
+    float w1 = BX_INV(R.ma) + dot(a1, mul(R.Ia, a1));
+    float w2 = BX_INV(R.mb) + dot(a2, mul(R.Ib, a2));
     pdyn = dvel / (w1 + w2 + 1e-6f);
   }
   v3 rvo = is_oneway<F>(R.oneway) ? aov + cross(aoa, cpos - aop)
@@ -1174,25 +1179,25 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
   float c = cancel_norm(dvr);
   v3 n2 = dvr / (c + 1e-6f);
   v3 cr1 = cross(pp, n2);
-  float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
+  float w1 = BX_INV(R.ma) + dot(cr1, mul(R.Ia, cr1));
   float dlr;
   if (is_oneway<F>(R.oneway)) {
     dlr = c / (w1 + 1e-6f);
   } else {
     v3 cr2 = cross(pc, n2);
-    float w2 = 1.f / R.mb + dot(cr2, mul(R.Ib, cr2));
+    float w2 = BX_INV(R.mb) + dot(cr2, mul(R.Ib, cr2));
     dlr = c / (w1 + w2 + 1e-6f);
   }
   float sm = cpen > 0.f ? 1.f : 0.f;
   float sink = is_oneway<F>(R.oneway) ? (vno <= -R.thr ? 1.f : 0.f) : (vno <= 0.f ? 1.f : 0.f);
   v3 pv = (dlr * n2 * sink + pdyn) * sm;
-  oav = pv / R.ma;
+  oav = BX_DIVM(pv, R.ma);
   oaa = cross(mul(R.Ia, ra), pv);
   if (is_oneway<F>(R.oneway)) {
     obv = mk(0.f, 0.f, 0.f);
     oba = mk(0.f, 0.f, 0.f);
   } else {
-    obv = -pv / R.mb;
+    obv = BX_DIVM(-pv, R.mb);
     oba = cross(mul(R.Ib, rb), -pv);
   }
 }
@@ -1208,10 +1213,10 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
   v3 x1 = cross(mul(R.Ia, cross(rpa, n)), rpa);
   float denom;
   if (is_oneway<F>(R.oneway)) {
-    denom = 1.f / R.ma + dot(n, x1);
+    denom = BX_INV(R.ma) + dot(n, x1);
   } else {
     v3 x2 = cross(mul(R.Ib, cross(rpb, n)), rpb);
-    denom = 1.f / R.ma + 1.f / R.mb + dot(n, x1 + x2);
+    denom = BX_INV(R.ma) + BX_INV(R.mb) + dot(n, x1 + x2);
   }
   float imp = (-1.f * (1.f + R.elas) * nv + bv) / denom;
   v3 vd = cvel - nv * n;
@@ -1239,6 +1244,7 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
                                            const float* al, int a, bool useJL = false,
                                            JLim JL = JLim{}, const uint4* LI = nullptr,
                                            const v3* tqd = nullptr) {
+  BX_IEEE_IN_JOINT
   QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
   if (LI && is_torque<F>(A.type)) {
     // torque actuators on the lane image's limit rows: the angles
@@ -1366,7 +1372,7 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   float cc = cancel_norm(dx);
   v3 n = dx / (cc + 1e-6f);
   v3 cr = cross(ro, n);
-  float wm = 1.f / m + dot(cr, mul(I, cr));
+  float wm = BX_INV(m) + dot(cr, mul(I, cr));
   float wp = xh(wm);
   float dl = -cc / (wm + wp + 1e-6f);
   v3 pv = dl * n;
@@ -1486,7 +1492,7 @@ __device__ __forceinline__ void joint_apply_half_sph(const JointC& J, const JSid
   const float cc = cancel_norm(dx);
   const v3 n = ndiv3(dx, cc + 1e-6f);
   const v3 cr = cross(ro, n);
-  const float wm = 1.f / S.m + dot(cr, mul(S.I, cr));
+  const float wm = BX_INV(S.m) + dot(cr, mul(S.I, cr));
   const float dl = ndiv(-cc, wm + xhl<L>(wm) + 1e-6f);
   const v3 pv = dl * n;
   dpo = J.sp * ndiv3(S.sg * pv, S.m);
@@ -1999,9 +2005,9 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
           v3 ppos = ld3(pv);
           q4 prot = ld4(pv + 3);
           q4 nr = qnormalize(q.rot);
-          q.vel = mul((q.pos - ppos) / h, B.pm);
+          q.vel = mul(BX_DIVH(q.pos - ppos, h), B.pm);
           q4 dq = quat_mul(nr, quat_inv(prot));
-          v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
+          v3 a = BX_DIVH(2.f * mk(dq.x, dq.y, dq.z), h);
           float scl = dq.w >= 0.f ? 1.f : -1.f;
           q.ang = mul(mul(scl * B.rm, a), B.rm);
           q.rot = nr;
@@ -2068,9 +2074,9 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       v3 ppos = ld3(pv);
       q4 prot = ld4(pv + 3);
       q4 nr = qnormalize(q.rot);
-      q.vel = mul((q.pos - ppos) / h, B.pm);
+      q.vel = mul(BX_DIVH(q.pos - ppos, h), B.pm);
       q4 dq = quat_mul(nr, quat_inv(prot));
-      v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
+      v3 a = BX_DIVH(2.f * mk(dq.x, dq.y, dq.z), h);
       float scl = dq.w >= 0.f ? 1.f : -1.f;
       q.ang = mul(mul(scl * B.rm, a), B.rm);
       q.rot = nr;
@@ -2486,6 +2492,7 @@ __device__ __forceinline__ v3 gsum3(const GList<M>& g, const float* base, int st
 template <bool G1, int M>
 __device__ __forceinline__ void gsum_contact(const GList<M>& g, const float* cslot, float eps,
                                              v3& a, q4& r, bool rot4) {
+  BX_IEEE_IN_CONTACT
   if constexpr (G1) {
     // one group: the two-group form below with its second accumulator all
     // exact zeros (0 / eps = 0, x + 0 = x), so the same bits at half the work
@@ -2538,10 +2545,11 @@ __device__ __forceinline__ void gsum_contact(const GList<M>& g, const float* csl
 // Euler.velocity_projection (integrators.py:122-146) on one body
 __device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, float h,
                                       bool bare = false) {
+  BX_IEEE_IN_BODY
   q4 nr = bare ? qnormalize_bare(q.rot) : qnormalize(q.rot);
-  q.vel = mul((q.pos - ppos) / h, B.pm);
+  q.vel = mul(BX_DIVH(q.pos - ppos, h), B.pm);
   q4 dq = quat_mul(nr, quat_inv(prot));
-  v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
+  v3 a = BX_DIVH(2.f * mk(dq.x, dq.y, dq.z), h);
   float scl = dq.w >= 0.f ? 1.f : -1.f;
   q.ang = mul(mul(scl * B.rm, a), B.rm);
   q.rot = nr;
@@ -4112,8 +4120,8 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
 // b-slot index took it to 256 + 4) one wave per SIMD fits and the CU holds
 // ONE workgroup: Ant Mountain(4) at 2,048 envs ran 1.8x slower
 // (tools/multi_occ.py: the step time grew with the batch from 256 envs on).
-// A/B knob BX_MULTI_WPE=4: held to 128 (four waves per SIMD: the LDS then
-// admits three workgroups; spills)
+// A/B knob BX_MULTI_WPE=3 / 4: held to 168 / 128 (three / four waves per
+// SIMD: the LDS then admits three workgroups per CU; both spill)
 template <int M, int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W)))
 system_step_multi_kernel(StepArgs A) {
@@ -5173,13 +5181,17 @@ hipError_t launch_system_step_multi(int feat, int mr, int64_t n_envs, size_t lds
                                     const StepArgs& a) {
   if ((feat & (F_SPH | F_ANGLE | F_FORCE | F_X)) != 0) return hipErrorInvalidValue;
   dim3 grid((unsigned)n_envs);
-  static const bool w4 = getenv("BX_MULTI_WPE") && atoi(getenv("BX_MULTI_WPE")) == 4;
-  if (w4) {
-    switch (mr) {
-      case 1: launch_one<StepArgs>(system_step_multi_kernel<1, 4>, grid, 256, lds, s, a); break;
-      case 2: launch_one<StepArgs>(system_step_multi_kernel<2, 4>, grid, 256, lds, s, a); break;
-      case 3: launch_one<StepArgs>(system_step_multi_kernel<3, 4>, grid, 256, lds, s, a); break;
-      case 4: launch_one<StepArgs>(system_step_multi_kernel<4, 4>, grid, 256, lds, s, a); break;
+  static const int wpe = getenv("BX_MULTI_WPE") ? atoi(getenv("BX_MULTI_WPE")) : 2;
+  if (wpe == 3 || wpe == 4) {
+    switch (mr * 8 + wpe) {
+      case 1 * 8 + 3: launch_one<StepArgs>(system_step_multi_kernel<1, 3>, grid, 256, lds, s, a); break;
+      case 2 * 8 + 3: launch_one<StepArgs>(system_step_multi_kernel<2, 3>, grid, 256, lds, s, a); break;
+      case 3 * 8 + 3: launch_one<StepArgs>(system_step_multi_kernel<3, 3>, grid, 256, lds, s, a); break;
+      case 4 * 8 + 3: launch_one<StepArgs>(system_step_multi_kernel<4, 3>, grid, 256, lds, s, a); break;
+      case 1 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<1, 4>, grid, 256, lds, s, a); break;
+      case 2 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<2, 4>, grid, 256, lds, s, a); break;
+      case 3 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<3, 4>, grid, 256, lds, s, a); break;
+      case 4 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<4, 4>, grid, 256, lds, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -137,21 +137,6 @@ __device__ __forceinline__ q4 quat_inv(q4 q) { return {q.w, -q.x, -q.y, -q.z}; }
 __device__ __forceinline__ float signed_angle(v3 axis, v3 ref_p, v3 ref_c) {
   return atan2f(dot(cross(ref_p, ref_c), axis), dot(ref_p, ref_c));
 }
-// A monotone stand-in for atan2(y, x) over (-pi, pi]: 1 - x / (|x| + |y|)
-// for y >= 0, x / (|x| + |y|) - 1 below, (0, 0) -> 0 as atan2(0, 0). Comparing
-// it with a limit's pseudo-angle decides `atan2(y, x) < limit` without the
-// transcendental (the two differ only inside the rounding band of the
-// boundary, where fp32 atan2 and the float64 reference differ too).
-__device__ __forceinline__ float pseudo_angle(float x, float y) {
-  const float r = fabsf(x) + fabsf(y);
-  const float t = r > 0.f ? x / r : 1.f;
-  return y >= 0.f ? 1.f - t : t - 1.f;
-}
-__device__ __forceinline__ float clampf(float x, float lo, float hi) {
-  return x < lo ? lo : (x > hi ? hi : x);
-}
-__device__ __forceinline__ float signf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
-
 // a / b with the fast reciprocal's quotient corrected by one Newton step on
 // the exact (fma) residual: IEEE division's correctly rounded result in all
 // but rare ties, at 4 VALU instead of 2 (rcp, mul) or ~10 (the IEEE
@@ -171,6 +156,41 @@ __device__ __forceinline__ v3 ndiv3(v3 a, float b) {
             __builtin_fmaf(__builtin_fmaf(-b, q.y, a.y), r, q.y),
             __builtin_fmaf(__builtin_fmaf(-b, q.z, a.z), r, q.z));
 }
+// diagnostic A/B (tools/gpu_drift_ab.sh): IEEE division inside one group of
+// functions (the contacts, the body integration, the joints and actuators)
+#if defined(BX_IEEE_CONTACT)
+#define BX_IEEE_IN_CONTACT _Pragma("clang fp reciprocal(off)")
+#else
+#define BX_IEEE_IN_CONTACT
+#endif
+#if defined(BX_IEEE_BODY)
+#define BX_IEEE_IN_BODY _Pragma("clang fp reciprocal(off)")
+#else
+#define BX_IEEE_IN_BODY
+#endif
+#if defined(BX_IEEE_JOINT)
+#define BX_IEEE_IN_JOINT _Pragma("clang fp reciprocal(off)")
+#else
+#define BX_IEEE_IN_JOINT
+#endif
+
+// quotients by the step's constants (the substep h, the bodies' masses):
+// the fast reciprocal of a constant is off by up to 1 ulp the SAME way every
+// substep (1 / h = 533.33 for Humanoid's h; Ant's 200 is exact), a
+// systematic bias rather than rounding noise (diagnostic A/B macros
+// BX_ND_H / BX_ND_M, tools/gpu_drift_ab.sh)
+#if defined(BX_ND_H)
+#define BX_DIVH(a, h) ndiv3((a), (h))
+#else
+#define BX_DIVH(a, h) ((a) / (h))
+#endif
+#if defined(BX_ND_M)
+#define BX_INV(m) ndiv(1.f, (m))
+#define BX_DIVM(a, m) ndiv3((a), (m))
+#else
+#define BX_INV(m) (1.f / (m))
+#define BX_DIVM(a, m) ((a) / (m))
+#endif
 // `a / b` (ND false: the build's division) or ndiv (ND true)
 template <bool ND>
 __device__ __forceinline__ float dv(float a, float b) {
@@ -181,13 +201,35 @@ __device__ __forceinline__ v3 dv3(v3 a, float b) {
   if constexpr (ND) return ndiv3(a, b); else return a / b;
 }
 
+// A monotone stand-in for atan2(y, x) over (-pi, pi]: 1 - x / (|x| + |y|)
+// for y >= 0, x / (|x| + |y|) - 1 below, (0, 0) -> 0 as atan2(0, 0). Comparing
+// it with a limit's pseudo-angle decides `atan2(y, x) < limit` without the
+// transcendental (the two differ only inside the rounding band of the
+// boundary, where fp32 atan2 and the float64 reference differ too).
+__device__ __forceinline__ float pseudo_angle(float x, float y) {
+  BX_IEEE_IN_JOINT
+  const float r = fabsf(x) + fabsf(y);
+#if defined(BX_ND_PSEUDO)
+  const float t = r > 0.f ? ndiv(x, r) : 1.f;  // (diagnostic build: tools/gpu_drift_ab.sh)
+#else
+  const float t = r > 0.f ? x / r : 1.f;
+#endif
+  return y >= 0.f ? 1.f - t : t - 1.f;
+}
+__device__ __forceinline__ float clampf(float x, float lo, float hi) {
+  return x < lo ? lo : (x > hi ? hi : x);
+}
+__device__ __forceinline__ float signf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
+
 // q / |q| with the bare v_sqrt_f32 (the Ant env kernel's integrator only)
 __device__ __forceinline__ q4 qnormalize_bare(q4 r) {
+  BX_IEEE_IN_BODY
   float rn = __builtin_amdgcn_sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
   return {r.w / rn, r.x / rn, r.y / rn, r.z / rn};
 }
 // q / |q| (integrators.py:67, 133)
 __device__ __forceinline__ q4 qnormalize(q4 r) {
+  BX_IEEE_IN_BODY
   float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
   return {r.w / rn, r.x / rn, r.y / rn, r.z / rn};
 }

@@ -200,14 +200,19 @@ def test_system_step_vs_golden(dev, oracle_lib, name):
     _gate(pen, ref_pen, _env_err(o_pen, ref_pen), 'pen')
 
 
-@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS + ENVTRAJ_KERNEL + ['ant:nojb', 'halfcheetah:nojb'])
+@pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS + ENVTRAJ_KERNEL +
+                         ['ant:nojb', 'halfcheetah:nojb', 'humanoid:sph'])
 def test_env_step_vs_golden(dev, oracle_lib, name, monkeypatch):
   name, _, variant = name.partition(':')
   if variant == 'nojb':
     # the all-kinds kernel the Ant / HalfCheetah kinds fall back to when their
     # system does not allow the body copies of their own kernels (BX_NO_JB)
     monkeypatch.setenv('BX_NO_JB', '1')
+  if variant == 'sph':
+    # the opt-in spherical joint halves (32 lanes per env)
+    monkeypatch.setenv('BX_SPH_HALVES', '1')
   env = _make_env(name, dev)
+  assert variant != 'sph' or env.unwrapped.sys.env_lanes == 32
   T = golden(env_golden(name))
   env32 = Envelope(oracle_lib, name)
   fl = obs_flags(name)
