@@ -262,19 +262,17 @@ template <int F> __device__ __forceinline__ bool is_oneway(int ow) {
 
 // Joint.apply_angle_update (joints.py:130-152): the impulse p of an angular
 // correction dq; each side's rotation update is linear in it
-// (ND: Newton-corrected quotients, the spherical kernels: pbd_math.h ndiv)
-template <bool ND = false>
 __device__ __forceinline__ v3 angle_impulse(const JointC& J, v3 dq) {
   BX_IEEE_IN_JOINT
   float th = cancel_norm(dq);
-  v3 n = dv3<ND>(dq, th + 1e-6f);
+  v3 n = dq / (th + 1e-6f);
 #if defined(BX_TU_FAST)
   // w1 + w2 as one quadratic form in Ip + Ic (loop-invariant; SINGLE-mode TU)
-  float dl = dv<ND>(-th, dot(n, mul(J.Ip + J.Ic, n)) + 1e-6f);
+  float dl = -th / (dot(n, mul(J.Ip + J.Ic, n)) + 1e-6f);
 #else
   float w1 = dot(n, mul(J.Ip, n));
   float w2 = dot(n, mul(J.Ic, n));
-  float dl = dv<ND>(-th, w1 + w2 + 1e-6f);
+  float dl = -th / (w1 + w2 + 1e-6f);
 #endif
   return -dl * n;
 }
@@ -345,23 +343,20 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
   auto rp_ = [&](v3 v) { return rotate(v, p.rot); };
   auto rc_ = [&](v3 v) { return rotate(v, c.rot); };
 #endif
-  // the spherical kernels (the Humanoid family) divide with Newton-corrected
-  // quotients (pbd_math.h ndiv)
-  constexpr bool ND = (F & F_SPH) != 0;
   // positional constraint: apply_position_update (joints.py:154-195)
   v3 pw = p.pos + rp_(J.off_p);
   v3 cw = c.pos + rc_(J.off_c);
   v3 dx = pw - cw;
   v3 rp = pw - p.pos, rc = cw - c.pos;
   float cc = cancel_norm(dx);
-  v3 n = dv3<ND>(dx, cc + 1e-6f);
+  v3 n = dx / (cc + 1e-6f);
   v3 cr1 = cross(rp, n), cr2 = cross(rc, n);
-  float w1 = BX_INV(J.mp) + dot(cr1, mul(J.Ip, cr1));
-  float w2 = BX_INV(J.mc) + dot(cr2, mul(J.Ic, cr2));
-  float dl = dv<ND>(-cc, w1 + w2 + 1e-6f);
+  float w1 = 1.f / J.mp + dot(cr1, mul(J.Ip, cr1));
+  float w2 = 1.f / J.mc + dot(cr2, mul(J.Ic, cr2));
+  float dl = -cc / (w1 + w2 + 1e-6f);
   v3 pv = dl * n;
-  dpp = J.sp * dv3<ND>(pv, J.mp);
-  dcp = J.sp * dv3<ND>(-pv, J.mc);
+  dpp = J.sp * (pv / J.mp);
+  dcp = J.sp * (-pv / J.mc);
   // the angle constraints' impulses (apply_angle_update, joints.py:130-152);
   // each body's rotation update is linear in its angular impulse, so these
   // and the position constraint's add up before one quaternion product per
@@ -385,16 +380,16 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
       n1 = rotate(ref_p, fix);
     }
     v3 dq2 = cross(n1, ref_c);
-    pimp = angle_impulse<ND>(J, dq1) + angle_impulse<ND>(J, dq2);
+    pimp = angle_impulse(J, dq1) + angle_impulse(J, dq2);
   } else {
     v3 a1p = rp_(J.axp[0]), a2p = rp_(J.axp[1]);
     v3 a1c = rc_(J.axc[0]), a2c = rc_(J.axc[1]), a3c = rc_(J.axc[2]);
     v3 lon = cross(a3c, a1p);
-    lon = dv3<ND>(lon, 1e-6f + dir_norm(lon));
+    lon = lon / (1e-6f + dir_norm(lon));
     v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
-    xz = dv3<ND>(xz, 1e-6f + dir_norm(xz));
+    xz = xz / (1e-6f + dir_norm(xz));
     v3 a2n = cross(xz, a1p);
-    a2n = dv3<ND>(a2n, 1e-6f + dir_norm(a2n));
+    a2n = a2n / (1e-6f + dir_norm(a2n));
     float sg = signf(dot(a1p, a3c));
     v3 nv[3] = {a1p, -a2n * sg, a3c};
     v3 n1v[3] = {a2p, a1p, lon};
@@ -411,7 +406,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
         const bool below = pa < L.plo, above = pa > L.phi;
         const v3 n1 = turn(n1v[l], nv[l], below ? L.clo : L.chi, below ? L.slo : L.shi);
         const v3 dq = cross(n1, n2v[l]) * ((below || above) ? 1.f : 0.f);
-        pimp = pimp + angle_impulse<ND>(J, dq);
+        pimp = pimp + angle_impulse(J, dq);
         continue;
       }
       // limit_angle (joints.py:343-355)
@@ -423,7 +418,7 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
       q4 fix = quat_rot_axis(nv[l], ph);
       v3 n1 = rotate(n1v[l], fix);
       v3 dq = cross(n1, n2v[l]) * mask;
-      pimp = pimp + angle_impulse<ND>(J, dq);
+      pimp = pimp + angle_impulse(J, dq);
     }
   }
   const v3 Pp = J.sp * cross(rp, pv) + J.sa * pimp;
@@ -1069,7 +1064,7 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
     pp = pp - a.pos;
     float c = dot(dx, n);
     v3 cr1 = cross(pp, n);
-    float w1 = BX_INV(R.ma) + dot(cr1, mul(R.Ia, cr1));
+    float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
     float dl = -c / (w1 + 1e-6f);
     float cm = c < 0.f ? 1.f : 0.f;
     v3 pv = dl * n * cm;
@@ -1081,13 +1076,13 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
     float c2 = cancel_norm(dt);
     v3 n2 = dt / (c2 + 1e-6f);
     cr1 = cross(pp, n2);
-    w1 = BX_INV(R.ma) + dot(cr1, mul(R.Ia, cr1));
+    w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
     float dlt = -c2 / (w1 + 0.f);
     float sm = fabsf(dlt) < fabsf(R.fric * dl) ? 1.f : 0.f;
     // the normal and friction impulses share the lever arm: one position and
     // one quaternion update for their sum (both linear in the impulse)
     pv = pv + dlt * n2 * sm * cm;
-    oap = sc * BX_DIVM(pv, R.ma);
+    oap = sc * (pv / R.ma);
     if constexpr (RAWL) {
       const v3 L = sc * cross(pp, pv);
       oar = q4{0.f, L.x, L.y, L.z};
@@ -1102,8 +1097,8 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
   v3 pc = cpos + n * cpen / 2.f - b.pos;
   float c = -cpen;
   v3 cr1 = cross(pp, n), cr2 = cross(pc, n);
-  float w1 = BX_INV(R.ma) + dot(cr1, mul(R.Ia, cr1));
-  float w2 = BX_INV(R.mb) + dot(cr2, mul(R.Ib, cr2));
+  float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
+  float w2 = 1.f / R.mb + dot(cr2, mul(R.Ib, cr2));
   float dl = -c / (w1 + w2 + 1e-6f);
   float cm = c < 0.f ? 1.f : 0.f;
   v3 pv = dl * n * cm;
@@ -1122,14 +1117,14 @@ __device__ __forceinline__ float position_contact(const RowC& R, const QP& a, co
   v3 n2 = dt / (c2 + 1e-6f);
   cr1 = cross(pp, n2);
   cr2 = cross(pc, n2);
-  w1 = BX_INV(R.ma) + dot(cr1, mul(R.Ia, cr1));
-  w2 = BX_INV(R.mb) + dot(cr2, mul(R.Ib, cr2));
+  w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
+  w2 = 1.f / R.mb + dot(cr2, mul(R.Ib, cr2));
   float dlt = -c2 / (w1 + w2);
   float sm = fabsf(dlt) < fabsf(dl) ? 1.f : 0.f;
   const v3 pt = dlt * n2 * sm * cm;
   const v3 ps = pv + pt;
-  oap = sc * BX_DIVM(ps, R.ma);
-  obp = sc * BX_DIVM(-ps, R.mb);
+  oap = sc * (ps / R.ma);
+  obp = sc * (-ps / R.mb);
   if constexpr (RAWL) {
     const v3 La = sc * (la + cross(pp, pt)), Lb = -sc * (lb + cross(pc, pt));
     oar = q4{0.f, La.x, La.y, La.z};
@@ -1161,12 +1156,12 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
   v3 pdyn;
   if (is_oneway<F>(R.oneway)) {
     v3 aw = cross(ra, vtd);
-    float w = BX_INV(R.ma) + dot(aw, aw);
+    float w = 1.f / R.ma + dot(aw, aw);
     pdyn = dvel / (w + 1e-6f);
   } else {
     v3 a1 = cross(ra, vtd), a2 = cross(rb, vtd);
-    float w1 = BX_INV(R.ma) + dot(a1, mul(R.Ia, a1));
-    float w2 = BX_INV(R.mb) + dot(a2, mul(R.Ib, a2));
+    float w1 = 1.f / R.ma + dot(a1, mul(R.Ia, a1));
+    float w2 = 1.f / R.mb + dot(a2, mul(R.Ib, a2));
     pdyn = dvel / (w1 + w2 + 1e-6f);
   }
   v3 rvo = is_oneway<F>(R.oneway) ? aov + cross(aoa, cpos - aop)
@@ -1179,25 +1174,25 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
   float c = cancel_norm(dvr);
   v3 n2 = dvr / (c + 1e-6f);
   v3 cr1 = cross(pp, n2);
-  float w1 = BX_INV(R.ma) + dot(cr1, mul(R.Ia, cr1));
+  float w1 = 1.f / R.ma + dot(cr1, mul(R.Ia, cr1));
   float dlr;
   if (is_oneway<F>(R.oneway)) {
     dlr = c / (w1 + 1e-6f);
   } else {
     v3 cr2 = cross(pc, n2);
-    float w2 = BX_INV(R.mb) + dot(cr2, mul(R.Ib, cr2));
+    float w2 = 1.f / R.mb + dot(cr2, mul(R.Ib, cr2));
     dlr = c / (w1 + w2 + 1e-6f);
   }
   float sm = cpen > 0.f ? 1.f : 0.f;
   float sink = is_oneway<F>(R.oneway) ? (vno <= -R.thr ? 1.f : 0.f) : (vno <= 0.f ? 1.f : 0.f);
   v3 pv = (dlr * n2 * sink + pdyn) * sm;
-  oav = BX_DIVM(pv, R.ma);
+  oav = pv / R.ma;
   oaa = cross(mul(R.Ia, ra), pv);
   if (is_oneway<F>(R.oneway)) {
     obv = mk(0.f, 0.f, 0.f);
     oba = mk(0.f, 0.f, 0.f);
   } else {
-    obv = BX_DIVM(-pv, R.mb);
+    obv = -pv / R.mb;
     oba = cross(mul(R.Ib, rb), -pv);
   }
 }
@@ -1213,10 +1208,10 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
   v3 x1 = cross(mul(R.Ia, cross(rpa, n)), rpa);
   float denom;
   if (is_oneway<F>(R.oneway)) {
-    denom = BX_INV(R.ma) + dot(n, x1);
+    denom = 1.f / R.ma + dot(n, x1);
   } else {
     v3 x2 = cross(mul(R.Ib, cross(rpb, n)), rpb);
-    denom = BX_INV(R.ma) + BX_INV(R.mb) + dot(n, x1 + x2);
+    denom = 1.f / R.ma + 1.f / R.mb + dot(n, x1 + x2);
   }
   float imp = (-1.f * (1.f + R.elas) * nv + bv) / denom;
   v3 vd = cvel - nv * n;
@@ -1372,7 +1367,7 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   float cc = cancel_norm(dx);
   v3 n = dx / (cc + 1e-6f);
   v3 cr = cross(ro, n);
-  float wm = BX_INV(m) + dot(cr, mul(I, cr));
+  float wm = 1.f / m + dot(cr, mul(I, cr));
   float wp = xh(wm);
   float dl = -cc / (wm + wp + 1e-6f);
   v3 pv = dl * n;
@@ -1490,20 +1485,20 @@ __device__ __forceinline__ void joint_apply_half_sph(const JointC& J, const JSid
   const v3 ro = wo - o.pos;
   const v3 dx = S.sg * (wo - xhl3<L>(wo));
   const float cc = cancel_norm(dx);
-  const v3 n = ndiv3(dx, cc + 1e-6f);
+  const v3 n = dx / (cc + 1e-6f);
   const v3 cr = cross(ro, n);
-  const float wm = BX_INV(S.m) + dot(cr, mul(S.I, cr));
-  const float dl = ndiv(-cc, wm + xhl<L>(wm) + 1e-6f);
+  const float wm = 1.f / S.m + dot(cr, mul(S.I, cr));
+  const float dl = -cc / (wm + xhl<L>(wm) + 1e-6f);
   const v3 pv = dl * n;
-  dpo = J.sp * ndiv3(S.sg * pv, S.m);
+  dpo = J.sp * ((S.sg * pv) / S.m);
   // the spherical frame (both lanes)
   const SphAxes X = sph_axes<L>(Mo, S, child);
   v3 lon = cross(X.a3c, X.a1p);
-  lon = ndiv3(lon, 1e-6f + dir_norm(lon));
+  lon = lon / (1e-6f + dir_norm(lon));
   v3 xz = dot(X.a1p, X.a1c) * X.a1c + dot(X.a1p, X.a2c) * X.a2c;
-  xz = ndiv3(xz, 1e-6f + dir_norm(xz));
+  xz = xz / (1e-6f + dir_norm(xz));
   v3 a2n = cross(xz, X.a1p);
-  a2n = ndiv3(a2n, 1e-6f + dir_norm(a2n));
+  a2n = a2n / (1e-6f + dir_norm(a2n));
   const float sg = signf(dot(X.a1p, X.a3c));
   // limit_angle on pseudo-angles (as joint_apply's lane-image rows)
   auto row = [&](v3 nv, v3 n1v, v3 n2v, const JLim& Lr) {
@@ -1512,7 +1507,7 @@ __device__ __forceinline__ void joint_apply_half_sph(const JointC& J, const JSid
     const bool below = pa < Lr.plo, above = pa > Lr.phi;
     const v3 n1 = turn(n1v, nv, below ? Lr.clo : Lr.chi, below ? Lr.slo : Lr.shi);
     const v3 dq = cross(n1, n2v) * ((below || above) ? 1.f : 0.f);
-    return angle_impulse<true>(J, dq);
+    return angle_impulse(J, dq);
   };
   // slot A: row 0 (nv a1p, n1 a2p, n2 lon) on the parent lane, row 2 (a3c,
   // lon, a2c) on the child's; slot B: row 1 (-a2n sg, a1p, xz), the parent's
@@ -2005,9 +2000,9 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
           v3 ppos = ld3(pv);
           q4 prot = ld4(pv + 3);
           q4 nr = qnormalize(q.rot);
-          q.vel = mul(BX_DIVH(q.pos - ppos, h), B.pm);
+          q.vel = mul(ndiv3(q.pos - ppos, h), B.pm);
           q4 dq = quat_mul(nr, quat_inv(prot));
-          v3 a = BX_DIVH(2.f * mk(dq.x, dq.y, dq.z), h);
+          v3 a = ndiv3(2.f * mk(dq.x, dq.y, dq.z), h);
           float scl = dq.w >= 0.f ? 1.f : -1.f;
           q.ang = mul(mul(scl * B.rm, a), B.rm);
           q.rot = nr;
@@ -2074,9 +2069,9 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       v3 ppos = ld3(pv);
       q4 prot = ld4(pv + 3);
       q4 nr = qnormalize(q.rot);
-      q.vel = mul(BX_DIVH(q.pos - ppos, h), B.pm);
+      q.vel = mul(ndiv3(q.pos - ppos, h), B.pm);
       q4 dq = quat_mul(nr, quat_inv(prot));
-      v3 a = BX_DIVH(2.f * mk(dq.x, dq.y, dq.z), h);
+      v3 a = ndiv3(2.f * mk(dq.x, dq.y, dq.z), h);
       float scl = dq.w >= 0.f ? 1.f : -1.f;
       q.ang = mul(mul(scl * B.rm, a), B.rm);
       q.rot = nr;
@@ -2547,9 +2542,11 @@ __device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, f
                                       bool bare = false) {
   BX_IEEE_IN_BODY
   q4 nr = bare ? qnormalize_bare(q.rot) : qnormalize(q.rot);
-  q.vel = mul(BX_DIVH(q.pos - ppos, h), B.pm);
+  // (the quotients by h Newton-corrected, as qnormalize's; the Ant env
+  // kernel's bare path keeps the fast ones: its 1 / h = 200 is exact)
+  q.vel = mul(bare ? (q.pos - ppos) / h : ndiv3(q.pos - ppos, h), B.pm);
   q4 dq = quat_mul(nr, quat_inv(prot));
-  v3 a = BX_DIVH(2.f * mk(dq.x, dq.y, dq.z), h);
+  v3 a = bare ? 2.f * mk(dq.x, dq.y, dq.z) / h : ndiv3(2.f * mk(dq.x, dq.y, dq.z), h);
   float scl = dq.w >= 0.f ? 1.f : -1.f;
   q.ang = mul(mul(scl * B.rm, a), B.rm);
   q.rot = nr;

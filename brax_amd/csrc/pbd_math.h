@@ -139,11 +139,8 @@ __device__ __forceinline__ float signed_angle(v3 axis, v3 ref_p, v3 ref_c) {
 }
 // a / b with the fast reciprocal's quotient corrected by one Newton step on
 // the exact (fma) residual: IEEE division's correctly rounded result in all
-// but rare ties, at 4 VALU instead of 2 (rcp, mul) or ~10 (the IEEE
-// sequence). The spherical joints' constraint math (the Humanoid kernels):
-// there the fast quotient's extra ulp doubled the long-horizon divergence
-// against Brax's fp32 (tests/test_gpu_long_horizon.py; IEEE division
-// builds brought the ratio from 2.3 to 0.95, square roots changed nothing)
+// but rare ties, at 4 VALU instead of 2 (rcp, mul) or ~6-10 (the IEEE
+// sequence); the body integration's quotients (qnormalize, vproj)
 __device__ __forceinline__ float ndiv(float a, float b) {
   const float r = __builtin_amdgcn_rcpf(b);
   const float q = a * r;
@@ -174,32 +171,6 @@ __device__ __forceinline__ v3 ndiv3(v3 a, float b) {
 #define BX_IEEE_IN_JOINT
 #endif
 
-// quotients by the step's constants (the substep h, the bodies' masses):
-// the fast reciprocal of a constant is off by up to 1 ulp the SAME way every
-// substep (1 / h = 533.33 for Humanoid's h; Ant's 200 is exact), a
-// systematic bias rather than rounding noise (diagnostic A/B macros
-// BX_ND_H / BX_ND_M, tools/gpu_drift_ab.sh)
-#if defined(BX_ND_H)
-#define BX_DIVH(a, h) ndiv3((a), (h))
-#else
-#define BX_DIVH(a, h) ((a) / (h))
-#endif
-#if defined(BX_ND_M)
-#define BX_INV(m) ndiv(1.f, (m))
-#define BX_DIVM(a, m) ndiv3((a), (m))
-#else
-#define BX_INV(m) (1.f / (m))
-#define BX_DIVM(a, m) ((a) / (m))
-#endif
-// `a / b` (ND false: the build's division) or ndiv (ND true)
-template <bool ND>
-__device__ __forceinline__ float dv(float a, float b) {
-  if constexpr (ND) return ndiv(a, b); else return a / b;
-}
-template <bool ND>
-__device__ __forceinline__ v3 dv3(v3 a, float b) {
-  if constexpr (ND) return ndiv3(a, b); else return a / b;
-}
 
 // A monotone stand-in for atan2(y, x) over (-pi, pi]: 1 - x / (|x| + |y|)
 // for y >= 0, x / (|x| + |y|) - 1 below, (0, 0) -> 0 as atan2(0, 0). Comparing
@@ -209,11 +180,7 @@ __device__ __forceinline__ v3 dv3(v3 a, float b) {
 __device__ __forceinline__ float pseudo_angle(float x, float y) {
   BX_IEEE_IN_JOINT
   const float r = fabsf(x) + fabsf(y);
-#if defined(BX_ND_PSEUDO)
-  const float t = r > 0.f ? ndiv(x, r) : 1.f;  // (diagnostic build: tools/gpu_drift_ab.sh)
-#else
   const float t = r > 0.f ? x / r : 1.f;
-#endif
   return y >= 0.f ? 1.f - t : t - 1.f;
 }
 __device__ __forceinline__ float clampf(float x, float lo, float hi) {
@@ -228,10 +195,21 @@ __device__ __forceinline__ q4 qnormalize_bare(q4 r) {
   return {r.w / rn, r.x / rn, r.y / rn, r.z / rn};
 }
 // q / |q| (integrators.py:67, 133)
+// (the quotients Newton-corrected: the fast reciprocal's extra ulp here, the
+// same way at every substep, left each quaternion's norm off 1 by a bias and
+// doubled Humanoid's long-horizon divergence from Brax's fp32; IEEE division
+// in the body integration alone took the ratio from 2.5 to 1.0 in the A/B of
+// tools/gpu_drift_ab.sh, none in the joints, contacts, pseudo-angles or
+// constant quotients did)
 __device__ __forceinline__ q4 qnormalize(q4 r) {
   BX_IEEE_IN_BODY
   float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
-  return {r.w / rn, r.x / rn, r.y / rn, r.z / rn};
+  const float ri = __builtin_amdgcn_rcpf(rn);
+  auto one = [&](float x) {
+    const float q = x * ri;
+    return __builtin_fmaf(__builtin_fmaf(-rn, q, x), ri, q);
+  };
+  return {one(r.w), one(r.x), one(r.y), one(r.z)};
 }
 
 }  // namespace bx
