@@ -2000,9 +2000,9 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
           v3 ppos = ld3(pv);
           q4 prot = ld4(pv + 3);
           q4 nr = qnormalize(q.rot);
-          q.vel = mul(ndiv3(q.pos - ppos, h), B.pm);
+          q.vel = mul((q.pos - ppos) / h, B.pm);
           q4 dq = quat_mul(nr, quat_inv(prot));
-          v3 a = ndiv3(2.f * mk(dq.x, dq.y, dq.z), h);
+          v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
           float scl = dq.w >= 0.f ? 1.f : -1.f;
           q.ang = mul(mul(scl * B.rm, a), B.rm);
           q.rot = nr;
@@ -2069,9 +2069,9 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       v3 ppos = ld3(pv);
       q4 prot = ld4(pv + 3);
       q4 nr = qnormalize(q.rot);
-      q.vel = mul(ndiv3(q.pos - ppos, h), B.pm);
+      q.vel = mul((q.pos - ppos) / h, B.pm);
       q4 dq = quat_mul(nr, quat_inv(prot));
-      v3 a = ndiv3(2.f * mk(dq.x, dq.y, dq.z), h);
+      v3 a = 2.f * mk(dq.x, dq.y, dq.z) / h;
       float scl = dq.w >= 0.f ? 1.f : -1.f;
       q.ang = mul(mul(scl * B.rm, a), B.rm);
       q.rot = nr;
@@ -2544,9 +2544,16 @@ __device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, f
   q4 nr = bare ? qnormalize_bare(q.rot) : qnormalize(q.rot);
   // (the quotients by h Newton-corrected, as qnormalize's; the Ant env
   // kernel's bare path keeps the fast ones: its 1 / h = 200 is exact)
-  q.vel = mul(bare ? (q.pos - ppos) / h : ndiv3(q.pos - ppos, h), B.pm);
+  // (the SINGLE-mode TU's non-bare path: Newton-corrected quotients, pbd_math.h
+  // qnormalize)
+#if defined(BX_TU_FAST)
+  const bool nd = !bare;
+#else
+  const bool nd = false;
+#endif
+  q.vel = mul(nd ? ndiv3(q.pos - ppos, h) : (q.pos - ppos) / h, B.pm);
   q4 dq = quat_mul(nr, quat_inv(prot));
-  v3 a = bare ? 2.f * mk(dq.x, dq.y, dq.z) / h : ndiv3(2.f * mk(dq.x, dq.y, dq.z), h);
+  v3 a = nd ? ndiv3(2.f * mk(dq.x, dq.y, dq.z), h) : 2.f * mk(dq.x, dq.y, dq.z) / h;
   float scl = dq.w >= 0.f ? 1.f : -1.f;
   q.ang = mul(mul(scl * B.rm, a), B.rm);
   q.rot = nr;
