@@ -291,7 +291,9 @@ __device__ __forceinline__ v3 hinge_turn(v3 axis, v3 ref_p, v3 ref_c, const JLim
   const float y = dot(cross(ref_p, ref_c), axis), x = dot(ref_p, ref_c);
   const float pa = pseudo_angle(x, y);
   const float r2 = x * x + y * y;
-  const float ri = r2 > 0.f ? rsqrtf(r2) : 0.f;
+  // (v_rsq_f32 itself: rsqrtf's denormal-input rescaling is dead for r2 of
+  // unit vectors' dot products; the same bits for every normal r2)
+  const float ri = r2 > 0.f ? __builtin_amdgcn_rsqf(r2) : 0.f;
   float cph = r2 > 0.f ? x * ri : 1.f, sph = y * ri;
   cph = pa < JL.plo ? JL.clo : (pa > JL.phi ? JL.chi : cph);
   sph = pa < JL.plo ? JL.slo : (pa > JL.phi ? JL.shi : sph);
@@ -1339,8 +1341,10 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
 enum { F_JH = 128 };
 
 // the partner half's value: lane ^ 8 within the env's 16-lane row
+// (bound_ctrl set: a row rotation has no invalid source lane, so the `old`
+// operand is dead and needs no zeroing v_mov before each exchange)
 __device__ __forceinline__ float xh(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, true));
 }
 __device__ __forceinline__ v3 xh3(v3 v) { return mk(xh(v.x), xh(v.y), xh(v.z)); }
 __device__ __forceinline__ v3 sel3(bool s, v3 a, v3 b) {
@@ -1650,10 +1654,10 @@ __device__ __forceinline__ void zero_row_slots(const Cst& c, const BlobHdr& H, c
 // broadcasts measured slower: 31.7k vs 28.7k cycles of picks per step.)
 template <int W>
 __device__ __forceinline__ unsigned seg_min_u32(unsigned v) {
-  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
-  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
-  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false));  // row_ror:2
-  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, false));  // row_ror:1
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, true));  // row_ror:8
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, true));  // row_ror:4
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, true));  // row_ror:2
+  v = min(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, true));  // row_ror:1
   if constexpr (W == 16) {
     return v;
   } else {
@@ -1669,10 +1673,10 @@ __device__ __forceinline__ unsigned seg_min_u32(unsigned v) {
 // the sum over each 16-lane row (one env at 16 lanes) in every lane of the
 // row: a row_ror butterfly (every lane of the wave must be active)
 __device__ __forceinline__ float row_sum16(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, false));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, true));
   return v;
 }
 

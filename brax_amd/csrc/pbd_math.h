@@ -34,9 +34,14 @@ __device__ __forceinline__ float norm(v3 a) { return sqrtf(dot(a, a)); }
 // (1 ulp) turns normalised vectors' unit dot products into 1 - ulp, and
 // acos near 1 magnifies that to 3.5e-4 rad (spherical joint angles at their
 // reference offset, physics_legacy_test.py:494-552; measured)
+// (the three |x_i| <= 1e-8 tests as one: the largest |x_i| against 1e-8, a
+// v_max3_f32 with |.| modifiers and one compare instead of three compares
+// and two mask ANDs)
+__device__ __forceinline__ bool near_zero3(v3 a) {
+  return fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fabsf(a.z)) <= 1e-8f;
+}
 __device__ __forceinline__ float safe_norm(v3 a) {
-  bool z = fabsf(a.x) <= 1e-8f && fabsf(a.y) <= 1e-8f && fabsf(a.z) <= 1e-8f;
-  return z ? 0.f : norm(a);
+  return near_zero3(a) ? 0.f : norm(a);
 }
 
 // safe_norm with the bare v_sqrt_f32 (<= 1 ulp) in the SINGLE-mode TU, for
@@ -47,8 +52,7 @@ __device__ __forceinline__ float safe_norm(v3 a) {
 // impulses, whose clamps against the norm move by the same ulp)
 __device__ __forceinline__ float cancel_norm(v3 a) {
 #if defined(BX_TU_FAST) && !defined(BX_IEEE_CANCEL_NORM)
-  bool z = fabsf(a.x) <= 1e-8f && fabsf(a.y) <= 1e-8f && fabsf(a.z) <= 1e-8f;
-  return z ? 0.f : __builtin_amdgcn_sqrtf(dot(a, a));
+  return near_zero3(a) ? 0.f : __builtin_amdgcn_sqrtf(dot(a, a));
 #else
   return safe_norm(a);
 #endif
