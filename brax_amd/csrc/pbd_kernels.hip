@@ -2036,9 +2036,9 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       float* sa = E.cslot + r * SLOT_STRIDE;
       float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
       st3(sa, oap); st4(sa + 3, oar);
-      sa[7] = (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f;
+      sa[7] = nonzero3(oap);
       st3(sb, obp); st4(sb + 3, obr);
-      sb[7] = (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f;
+      sb[7] = nonzero3(obp);
     }
     esync<L>();
     for (int b = lane; b < N; b += L) {
@@ -2096,9 +2096,9 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       float* sa = E.cslot + r * SLOT_STRIDE;
       float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
       st3(sa, oav); st3(sa + 3, oaa);
-      sa[7] = (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f;
+      sa[7] = nonzero3(oav);
       st3(sb, obv); st3(sb + 3, oba);
-      sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
+      sb[7] = nonzero3(obv);
     }
     esync<L>();
     for (int b = lane; b < N; b += L) {
@@ -2152,9 +2152,9 @@ __device__ void impulse_rows(const Cst& c, const BlobHdr& H, const Env& E, int l
     float* sa = E.cslot + r * SLOT_STRIDE;
     float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
     st3(sa, oav); st3(sa + 3, oaa);
-    sa[7] = (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f;
+    sa[7] = nonzero3(oav);
     st3(sb, obv); st3(sb + 3, oba);
-    sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
+    sb[7] = nonzero3(obv);
   }
 }
 
@@ -2616,10 +2616,16 @@ __device__ unsigned long long bx_stamp_wave[4096][16];
 // NOINFO (the env kernels, which write no Info): a capsule-capsule row whose
 // capsule centres lie farther apart than its reach cannot penetrate, and is
 // left out of the capsule-capsule pass before the segment-segment test
-template <int L, int F, int M, bool FOLD = false, bool NOINFO = false>
+// FULL: every lane has a joint side, an actuator and a body copy, the `has`
+// tests compile-time true. (Tried for the Ant kernel, 16 lanes = 8 joints x 2
+// sides: 190 fewer SALU per step, no faster — a wave's SALU issue hides
+// behind its VALU — and the merged blocks contract differently; unused.)
+template <int L, int F, int M, bool FOLD = false, bool NOINFO = false, bool FULL = false>
 __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
                                 const float* act, int aw, const Hoist<M, cl_width<F, M>()>& X,
                                 v3& icv, v3& ica, v3& iaa) {
+  static_assert(!FULL || ((F & F_JH) != 0 && L == 16), "FULL: the 16-lane joint halves");
+  const bool hasB = FULL || X.hasB, hasJ = FULL || X.hasJ, hasA = FULL || X.hasA;
 #ifdef BX_STAMPS
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last;
@@ -2662,7 +2668,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   const int bi = JB ? X.S.body : lane;  // the lane's body
   float* myqp = E.qp + bi * QP_STRIDE;
   QP q;
-  if (X.hasB) q = ldqp(myqp);
+  if (hasB) q = ldqp(myqp);
   if constexpr (JB) {
     // the records of bodies on no joint side (frozen, on the plane side of
     // one-way rows only: checked on the host) as their own lanes would leave
@@ -2684,7 +2690,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   iaa = mk(0.f, 0.f, 0.f);
   // action values of the lane's actuator (constant over the step)
   float al[3] = {0.f, 0.f, 0.f};
-  if (X.hasA && valid) {
+  if (hasA && valid) {
 #pragma unroll
     for (int l = 0; l < 3; l++) {
       int ai = X.A.idx[l];
@@ -2694,7 +2700,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   // dp_f of the lane's body: constant over the step (depends on the action only)
   v3 fv = mk(0.f, 0.f, 0.f), fa = mk(0.f, 0.f, 0.f);
   if constexpr ((F & F_FORCE) != 0) {
-    if (X.hasB) body_forces(c, H, lane, act, aw, valid, fv, fa);
+    if (hasB) body_forces(c, H, lane, act, aw, valid, fv, fa);
   }
   for (int it = 0; it < H.substeps / 2; it++) {
     v3 ppos = q.pos;
@@ -2708,7 +2714,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     for (int sub = 0; sub < 2; sub++) {
       ppos = q.pos;
       prot = q.rot;
-      if (sub == 1 && X.hasB) st_slot(E.prev + bi * PREV_STRIDE, ppos, prot, 0.f);
+      if (sub == 1 && hasB) st_slot(E.prev + bi * PREV_STRIDE, ppos, prot, 0.f);
       // actuators + damping (actuator a drives joint a when H.act_same)
       if constexpr (JH) {
         // one side of joint / actuator jx per lane (act_same, checked on the host)
@@ -2719,25 +2725,25 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
           const v3 oa = xhl3<L>(q.ang);
           const v3 tqd = -1.f * Jc.damping * (sel3(child, oa, q.ang) - sel3(child, q.ang, oa));
           if constexpr (SH) {
-            if (X.hasA) act_torque_half_sph<L>(X.S, X.A, E, al, jx, child, q.rot, LIP, tqd);
+            if (hasA) act_torque_half_sph<L>(X.S, X.A, E, al, jx, child, q.rot, LIP, tqd);
           } else {
-            if (X.hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, q.rot, &tqd);
+            if (hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, q.rot, &tqd);
           }
         } else if constexpr (FOLD) {
           const JointC& Jc = X.J;
           const v3 tqd = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
-          if (X.hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE), &tqd);
+          if (hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE), &tqd);
         } else {
-        if (X.hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE));
+        if (hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, ld_rot(E.qp + jb * QP_STRIDE));
         }
-        if (!FOLD && X.hasJ) {
+        if (!FOLD && hasJ) {
           const JointC& Jc = X.J;
           v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
           // parent: Ip tq, child: -Ic tq
           st_v3a(E.jslot + (child ? E.nJ + jx : jx) * SLOT_STRIDE, X.S.sg * mul(X.S.I, tq));
         }
       } else {
-      if (X.hasA) {
+      if (hasA) {
         const ActC& A = X.A;
         if (FOLD) {
           const JointC& Jc = X.J;
@@ -2750,7 +2756,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
           act_torque<F>(Jc, A, E, al, lane);
         }
       }
-      if (!FOLD && X.hasJ) {
+      if (!FOLD && hasJ) {
         const JointC& Jc = X.J;
         v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
         st_v3a(E.jslot + lane * SLOT_STRIDE, mul(Jc.Ip, tq));
@@ -2759,7 +2765,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       }
       sync();
       BX_STAMP(0);
-      if (X.hasB) {
+      if (hasB) {
         v3 dpa = gsum3(X.al, E.aslot, ASLOT_STRIDE);
         v3 dpj = FOLD ? mk(0.f, 0.f, 0.f) : gsum3(X.jl, E.jslot, SLOT_STRIDE);
         v3 vel = H.vexp * q.vel;
@@ -2779,7 +2785,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       sync();
       BX_STAMP(1);
       if constexpr (JH) {
-        if (X.hasJ) {
+        if (hasJ) {
           const JointC& Jc = X.J;
           const QP o = JB ? q : ldqp(E.qp + X.S.body * QP_STRIDE);
           v3 dpo;
@@ -2788,7 +2794,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
           else joint_apply_half(Jc, X.JL, X.S, child, o, dpo, dro);
           st_slot(E.jslot + (child ? E.nJ + jx : jx) * SLOT_STRIDE, dpo, dro, 0.f);
         }
-      } else if (X.hasJ) {
+      } else if (hasJ) {
         const JointC& Jc = X.J;
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
@@ -2799,7 +2805,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       }
       sync();
       BX_STAMP(2);
-      if (X.hasB) {
+      if (hasB) {
         v3 dp = mk(0.f, 0.f, 0.f);
         q4 dr{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2878,9 +2884,9 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       st4a(rd, f32x4{cpos.x, cpos.y, cpos.z, cn.x});
       st4a(rd + 4, f32x4{cn.y, cn.z, pen, dl});
       st_slot(E.cslot + r * SLOT_STRIDE, oap, oar,
-              (oap.x != 0.f || oap.y != 0.f || oap.z != 0.f) ? 1.f : 0.f);
+              nonzero3(oap));
       st_slot(E.cslot + (E.nR + r) * SLOT_STRIDE, obp, obr,
-              (obp.x != 0.f || obp.y != 0.f || obp.z != 0.f) ? 1.f : 0.f);
+              nonzero3(obp));
     };
     if (X.hasR) pos_pass(std::integral_constant<int, F1>{}, X.R, X.r1, cpos, cn, pen, dl);
     if constexpr (R2) {
@@ -2888,7 +2894,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     }
     sync();
     BX_STAMP(4);
-    if (X.hasB) {
+    if (hasB) {
       v3 dp;
       q4 dr;
       gsum_contact<(F & F_G1) != 0>(X.cl, E.cslot, 1e-6f, dp, dr, true);
@@ -2912,9 +2918,9 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         velocity_contact<FS>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos, cn, pen, dl, oav, oaa,
                              obv, oba);
       st_slot(E.cslot + r * SLOT_STRIDE, oav, q4{oaa.x, oaa.y, oaa.z, 0.f},
-              (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f);
+              nonzero3(oav));
       st_slot(E.cslot + (E.nR + r) * SLOT_STRIDE, obv, q4{oba.x, oba.y, oba.z, 0.f},
-              (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f);
+              nonzero3(obv));
     };
     if (X.hasR) vel_pass(std::integral_constant<int, F1>{}, X.R, X.r1, cpos, cn, pen, dl);
     if constexpr (R2) {
@@ -2922,7 +2928,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     }
     sync();
     BX_STAMP(6);
-    if (X.hasB) {
+    if (hasB) {
       v3 dv;
       q4 da;
       gsum_contact<(F & F_G1) != 0>(X.cl, E.cslot, 1e-6f, dv, da, false);
@@ -2937,7 +2943,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     sync();
     BX_STAMP(7);
   }
-  if (X.hasB) {
+  if (hasB) {
     float* acc = E.acc + bi * ACC_STRIDE;
     st3(acc + ACC_ICV, icv);
     st3(acc + ACC_ICA, ica);
@@ -3080,7 +3086,7 @@ __device__ __forceinline__ void task_sum(const int* te, const float* ms, float* 
     ld_mslot(ms + te[k] * MSLOT_STRIDE, v, w);
     a = a + v;
     l = l + w;
-    n += (v.x != 0.f || v.y != 0.f || v.z != 0.f) ? 1.f : 0.f;
+    n += nonzero3(v);
   }
   st4a(out, f32x4{a.x, a.y, a.z, l.x});
   st4a(out + 4, f32x4{l.y, l.z, n, 0.f});
@@ -3492,9 +3498,9 @@ __device__ void pbd_info(const Cst& c, const BlobHdr& H, const Env& E, int lane)
     float* sa = E.cslot + r * SLOT_STRIDE;
     float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
     st3(sa, oav); st3(sa + 3, oaa);
-    sa[7] = (oav.x != 0.f || oav.y != 0.f || oav.z != 0.f) ? 1.f : 0.f;
+    sa[7] = nonzero3(oav);
     st3(sb, obv); st3(sb + 3, oba);
-    sb[7] = (obv.x != 0.f || obv.y != 0.f || obv.z != 0.f) ? 1.f : 0.f;
+    sb[7] = nonzero3(obv);
   }
   esync<L>();
   for (int b = lane; b < N; b += L) {

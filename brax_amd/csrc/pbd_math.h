@@ -40,6 +40,11 @@ __device__ __forceinline__ float norm(v3 a) { return sqrtf(dot(a, a)); }
 __device__ __forceinline__ bool near_zero3(v3 a) {
   return fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fabsf(a.z)) <= 1e-8f;
 }
+// 1 when any component is nonzero (a slot's contact count): the largest |x_i|
+// against 0, as near_zero3
+__device__ __forceinline__ float nonzero3(v3 a) {
+  return fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fabsf(a.z)) != 0.f ? 1.f : 0.f;
+}
 __device__ __forceinline__ float safe_norm(v3 a) {
   return near_zero3(a) ? 0.f : norm(a);
 }
