@@ -15,4 +15,6 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 150 python -u tools/sph_ab.py > gpurun_out/sph_ab_$TAG.log 2>&1; ok $?
 bash tools/run_prof.sh $TAG || exit 7
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench20_$TAG.log 2>&1 || exit 8
+# against the previous build, when one is staged (brax_amd/_lib_prev)
+if [ -f brax_amd/_lib_prev/libbrax_amd.so ]; then bash tools/gpu_ab_prev.sh ab_$TAG || exit 9; fi
 exit $rc
