@@ -190,11 +190,6 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.gx = (float)d->gravity[0]; H.gy = (float)d->gravity[1]; H.gz = (float)d->gravity[2];
 
   H.o_body = B.alloc(N * BODY_STRIDE);
-  // the frozen masks are 0 / 1 (1 - frozen, system.py / integrators.py): the
-  // step kernels rely on it (a mask applied twice is applied once)
-  for (int k = 0; k < 3 * N; k++)
-    if ((d->pos_mask[k] != 0.0 && d->pos_mask[k] != 1.0) || (d->rot_mask[k] != 0.0 && d->rot_mask[k] != 1.0))
-      return fail("body position / rotation masks must be 0 or 1 (frozen flags)");
   for (int b = 0; b < N; b++) {
     int o = H.o_body + b * BODY_STRIDE;
     B.f(o + BODY_MASS, d->body_mass[b]);

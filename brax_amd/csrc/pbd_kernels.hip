@@ -177,9 +177,6 @@ struct JointC {
 struct JSide {
   v3 off, ax0, ax2, I;
   v3 ax1;  // the spherical halves' second axis
-  // sg * I (exact: sg = +-1): the revolute halves apply the side's sign and
-  // inverse inertia in one product (the same bits, 3-10 fewer VALU per call)
-  v3 sgI;
   float m, sg;
   int body;
 };
@@ -1360,10 +1357,8 @@ __device__ __forceinline__ v3 sel3(bool s, v3 a, v3 b) {
 __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL, const JSide& S,
                                                  bool child, const QP& o, v3& dpo, q4& dro) {
   const float sg = S.sg;
+  const v3 I = S.I;
   const float m = S.m;
-  // (sg * I: the sign and the inverse inertia in one factor, exactly; 0.5 sg I
-  // likewise for the rotation update, a power-of-two scaling)
-  const v3 sgI = S.sgI, hsgI = 0.5f * S.sgI;
   // this side's three vectors through one rotation matrix
   const RotM Mo = rot_matrix(o.rot);
   // positional constraint
@@ -1376,11 +1371,11 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   float cc = cancel_norm(dx);
   v3 n = dx / (cc + 1e-6f);
   v3 cr = cross(ro, n);
-  float wm = 1.f / m + sg * dot(cr, mul(sgI, cr));  // (sg (cr . sg I cr): cr . I cr exactly)
+  float wm = 1.f / m + dot(cr, mul(I, cr));
   float wp = xh(wm);
   float dl = -cc / (wm + wp + 1e-6f);
   v3 pv = dl * n;
-  dpo = J.sp * (pv * (sg * (1.f / m)));  // ((sg pv) / m, the fast quotient's bits)
+  dpo = J.sp * ((sg * pv) / m);
   // the two angular constraints (axis alignment, limited hinge angle)
   v3 u0 = mrot(Mo, S.ax0);
   v3 u2 = mrot(Mo, S.ax2);
@@ -1397,7 +1392,7 @@ __device__ __forceinline__ void joint_apply_half(const JointC& J, const JLim& JL
   // position constraint's and both angle constraints' add up before the one
   // quaternion product (joints.py:150-152, 190-195)
   const v3 P = J.sp * cross(ro, pv) + J.sa * (pm + po);
-  dro = vec_quat_mul(mul(hsgI, P), o.rot);
+  dro = (sg * 0.5f) * vec_quat_mul(mul(I, P), o.rot);
 }
 
 // Actuator.apply_reduced (actuators.py:52-112) for a revolute joint, one side
@@ -1427,8 +1422,8 @@ __device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL
   float sgp = is_torque<F>(A.type) ? 1.f : -1.f;
   // parent: sgp * Ip tq, child: -sgp * Ic tq (the side's sign times its inertia)
   float* slot = E.aslot + (child ? E.nK + a : a) * ASLOT_STRIDE;
-  if (tqd) st_v3a(slot, mul(S.sgI, sgp * tq + *tqd));  // + the joint's damping (FOLD)
-  else st_v3a(slot, sgp * mul(S.sgI, tq));
+  if (tqd) st_v3a(slot, S.sg * mul(S.I, sgp * tq + *tqd));  // + the joint's damping (FOLD)
+  else st_v3a(slot, (sgp * S.sg) * mul(S.I, tq));
 }
 
 // ---------------------------------------------------------------------------
@@ -1626,6 +1621,16 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi =
 // ds_write sees it without draining lgkmcnt. Only the compiler must not move
 // or forward memory accesses across the boundary.
 __device__ __forceinline__ void sync() { asm volatile("" ::: "memory"); }
+// pbd_step_single's phase boundaries (A/B knob -DBX_NOSYNC_SINGLE: none; the
+// compiler's own alias analysis then keeps every LDS store before the loads
+// that may read it, the gather indices being runtime values, and the machine
+// scheduler may overlap one phase's tail with the next's independent work,
+// which an inline-asm boundary forbids)
+__device__ __forceinline__ void phase_sync() {
+#if !defined(BX_NOSYNC_SINGLE)
+  sync();
+#endif
+}
 // An env spread over L > 64 threads (large scenes: 128 or 256 threads = 2-4
 // waves of one workgroup, one env per workgroup) needs a real workgroup
 // barrier at each phase boundary; within one wave the compiler fence above.
@@ -2455,7 +2460,6 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
     X.S.I = f3(LI_SIDE_H + LS_I);
     X.S.m = f(LI_SIDE_H + LS_M);
     X.S.sg = f(LI_SIDE_H + LS_SG);
-    X.S.sgI = X.S.sg * X.S.I;
     X.S.body = n(LI_SIDE_H + LS_BODY);
     X.S.ax1 = HALF == 16 ? f3(LI_SIDE_AX1) : mk(0.f, 0.f, 0.f);
   }
@@ -2565,7 +2569,7 @@ __device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, f
   q4 dq = quat_mul(nr, quat_inv(prot));
   v3 a = nd ? ndiv3(2.f * mk(dq.x, dq.y, dq.z), h) : 2.f * mk(dq.x, dq.y, dq.z) / h;
   float scl = dq.w >= 0.f ? 1.f : -1.f;
-  q.ang = mul(scl * B.rm, a);  // (the reference's second rot mask: identity here, 0 / 1 masks)
+  q.ang = mul(mul(scl * B.rm, a), B.rm);
   q.rot = nr;
 }
 
@@ -2746,7 +2750,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
           const JointC& Jc = X.J;
           v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
           // parent: Ip tq, child: -Ic tq
-          st_v3a(E.jslot + (child ? E.nJ + jx : jx) * SLOT_STRIDE, mul(X.S.sgI, tq));
+          st_v3a(E.jslot + (child ? E.nJ + jx : jx) * SLOT_STRIDE, X.S.sg * mul(X.S.I, tq));
         }
       } else {
       if (hasA) {
@@ -2769,7 +2773,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         st_v3a(E.jslot + (E.nJ + lane) * SLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
       }
       }
-      sync();
+      phase_sync();
       BX_STAMP(0);
       if (hasB) {
         v3 dpa = gsum3(X.al, E.aslot, ASLOT_STRIDE);
@@ -2780,19 +2784,15 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         v3 an = H.aexp * q.ang;
         an = an + ((dpa + fa) + dpj) * h;
         q.ang = mul(an, X.B.rm);
-        // the reference masks q.vel * h and q.ang again (integrators.py:73-80);
-        // with 0 / 1 masks (checked on the host) the second mask is the
-        // identity on the already masked values, and (x * 0.5) * h is
-        // x * (0.5 * h) exactly: the same bits, 9 fewer VALU per substep
-        q.pos = q.pos + q.vel * h;
-        const v3 am = q.ang;
-        q4 hq = q4{0.f, am.x, am.y, am.z} * (0.5f * h);
+        q.pos = q.pos + mul(q.vel * h, X.B.pm);
+        v3 am = mul(q.ang, X.B.rm);
+        q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
         q4 r = q.rot + quat_mul(hq, q.rot);
         q.rot = (JB && !SH) ? qnormalize_bare(r) : qnormalize(r);  // Ant env kernel: bare sqrt
         if (!JB) stqp(myqp, q);  // JB: the joint phase takes the lane's copy
         dpa_last = dpa;
       }
-      sync();
+      phase_sync();
       BX_STAMP(1);
       if constexpr (JH) {
         if (hasJ) {
@@ -2813,7 +2813,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         st_slot(E.jslot + lane * SLOT_STRIDE, dpp, dpr, 0.f);
         st_slot(E.jslot + (E.nJ + lane) * SLOT_STRIDE, dcp, dcr, 0.f);
       }
-      sync();
+      phase_sync();
       BX_STAMP(2);
       if (hasB) {
         v3 dp = mk(0.f, 0.f, 0.f);
@@ -2834,7 +2834,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         // JB: the record is read next by the contact passes (after sub 1)
         if (!JB || sub == 1) stqp(myqp, q);
       }
-      sync();
+      phase_sync();
       BX_STAMP(3);
     }
     // ---- collisions (system.py:288-313): the lane's row (F_R2: rows lane
@@ -2902,7 +2902,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     if constexpr (R2) {
       if (X.hasR2) pos_pass(std::integral_constant<int, F2>{}, X.R2, X.r2, cpos2, cn2, pen2, dl2);
     }
-    sync();
+    phase_sync();
     BX_STAMP(4);
     if (hasB) {
       v3 dp;
@@ -2915,7 +2915,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       vproj(q, ppos, prot, X.B, h, JB && !SH);
       stqp(myqp, q);
     }
-    sync();
+    phase_sync();
     BX_STAMP(5);
     auto vel_pass = [&](auto fc, const RowC& R, int r, v3 cpos, v3 cn, float pen, float dl) {
       constexpr int FS = decltype(fc)::value;
@@ -2936,7 +2936,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     if constexpr (R2) {
       if (X.hasR2) vel_pass(std::integral_constant<int, F2>{}, X.R2, X.r2, cpos2, cn2, pen2, dl2);
     }
-    sync();
+    phase_sync();
     BX_STAMP(6);
     if (hasB) {
       v3 dv;
@@ -2950,7 +2950,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       ica = ica + dav;
       iaa = iaa + dpa_last;
     }
-    sync();
+    phase_sync();
     BX_STAMP(7);
   }
   if (hasB) {
@@ -2959,7 +2959,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     st3(acc + ACC_ICA, ica);
     st3(acc + ACC_IAA, iaa);
   }
-  sync();
+  phase_sync();
   BX_STAMP(9);
 #ifdef BX_STAMPS
   if (threadIdx.x == 0) {

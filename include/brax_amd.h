@@ -88,8 +88,8 @@ typedef struct bx_desc {
   /* bodies */
   const double* body_mass;         /* [N] */
   const double* body_inv_inertia;  /* [N,3]  (inverse, body-frame diagonal) */
-  const double* pos_mask;          /* [N,3] 1 - frozen position: 0 or 1 */
-  const double* rot_mask;          /* [N,3] 1 - frozen rotation: 0 or 1 */
+  const double* pos_mask;          /* [N,3] */
+  const double* rot_mask;          /* [N,3] */
   const double* quat_mask;         /* [N,4] */
   /* joints, in application order (grouped by dof like joints.get) */
   const int32_t* joint_type;       /* [J] BX_JOINT_* */
