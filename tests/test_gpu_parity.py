@@ -92,10 +92,22 @@ def _gate(got, ref, e32, field, split=True):
     # under fp32 rounding: its distance to the NEAREST of Brax's fp32
     # realisations (the envelope's runs) says whether the HIP result is one of
     # them up to rounding on its branch (recorded, not asserted yet)
-    near = np.min([normwise(got, np.asarray(v)) for v in samples], axis=0)
-    near = np.broadcast_to(near, nw.shape)
-    record_margin(field + ':illcond_nearest', float(near[ill].max()), NEAR_TOL,
-                  n=int(ill.sum()), asserted=False)
+    S = [np.asarray(v) for v in samples]
+    near = np.broadcast_to(np.min([normwise(got, v) for v in S], axis=0), nw.shape)
+    # the realisations' own spread: for each, its distance to the nearest
+    # OTHER one; the largest of those per env (how far apart Brax's fp32
+    # runs land from each other)
+    nn = np.zeros(nw.shape)
+    for i, a in enumerate(S):
+      d = np.full(nw.shape, np.inf)
+      for j, b in enumerate(S):
+        if i != j:
+          d = np.minimum(d, np.broadcast_to(normwise(a, b), nw.shape))
+      nn = np.maximum(nn, d)
+    tol_e = np.maximum(POS_TOL, 2.0 * nn)
+    k = int(np.argmax(np.where(ill, near / tol_e, -1.0)))
+    record_margin(field + ':illcond_nearest', float(near.flat[k]), float(tol_e.flat[k]),
+                  n=int(ill.sum()), asserted=False, envelope_tol=float(2.0 * e32.flat[k]))
   return worst
 
 
