@@ -60,7 +60,7 @@ def _to_qp(a, dev):
 
 
 WIDE = 1e-2  # a sample whose own bound 2 x E32 exceeds this is ill-conditioned
-NEAR_TOL = 1e-3  # the ill-conditioned envs: distance to the nearest fp32 realisation (recorded)
+NEAR_TOL = 1e-3  # the ill-conditioned envs: floor of the nearest-realisation bound
 
 
 def _gate(got, ref, e32, field, split=True):
@@ -84,19 +84,22 @@ def _gate(got, ref, e32, field, split=True):
       continue
     tol = max(POS_TOL, 2.0 * float(e32[sel].max()))
     m = float(nw[sel].max())
-    record_margin(name, m, tol, n=int(sel.sum()))
+    # the ill-conditioned group's envelope bound (> 1e-2 by definition) is
+    # Brax-vs-Brax branch distance; the binding gate for those envs is the
+    # nearest-realisation one below
+    record_margin(name, m, tol, n=int(sel.sum()), **({'role': 'envelope'} if name.endswith(':illcond') else {}))
     assert m <= tol, f'{name}: normwise {m:.3e} > tol {tol:.3e} ({int(sel.sum())} envs)'
     worst = max(worst, (m, tol))
-  if samples is not None and ill.any():
+  if ill.any():
     # an ill-conditioned env's branch (which contacts fire) is a coin toss
-    # under fp32 rounding: its distance to the NEAREST of Brax's fp32
-    # realisations (the envelope's runs) says whether the HIP result is one of
-    # them up to rounding on its branch (recorded, not asserted yet)
+    # under fp32 rounding, so its gate is the distance to the NEAREST of
+    # Brax's fp32 realisations (the envelope's runs): the HIP result must be
+    # one of them up to rounding on its branch. The bound: twice the
+    # realisations' own spread (for each, its distance to the nearest OTHER
+    # one; the largest of those per env), floored at NEAR_TOL, capped at WIDE.
+    assert samples is not None, f'{field}: an ill-conditioned gate needs the fp32 realisations'
     S = [np.asarray(v) for v in samples]
     near = np.broadcast_to(np.min([normwise(got, v) for v in S], axis=0), nw.shape)
-    # the realisations' own spread: for each, its distance to the nearest
-    # OTHER one; the largest of those per env (how far apart Brax's fp32
-    # runs land from each other)
     nn = np.zeros(nw.shape)
     for i, a in enumerate(S):
       d = np.full(nw.shape, np.inf)
@@ -104,10 +107,11 @@ def _gate(got, ref, e32, field, split=True):
         if i != j:
           d = np.minimum(d, np.broadcast_to(normwise(a, b), nw.shape))
       nn = np.maximum(nn, d)
-    tol_e = np.maximum(POS_TOL, 2.0 * nn)
+    tol_e = np.clip(2.0 * nn, NEAR_TOL, WIDE)
     k = int(np.argmax(np.where(ill, near / tol_e, -1.0)))
-    record_margin(field + ':illcond_nearest', float(near.flat[k]), float(tol_e.flat[k]),
-                  n=int(ill.sum()), asserted=False, envelope_tol=float(2.0 * e32.flat[k]))
+    m, tol = float(near.flat[k]), float(tol_e.flat[k])
+    record_margin(field + ':illcond_nearest', m, tol, n=int(ill.sum()), envelope_tol=float(2.0 * e32.flat[k]))
+    assert m <= tol, f'{field}:illcond_nearest: {m:.3e} from the nearest fp32 realisation > tol {tol:.3e}'
   return worst
 
 

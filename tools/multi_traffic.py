@@ -2,13 +2,17 @@
 Info (diagnostic, for rocprofv3 PMC passes): 30 steps of one mode only, so a
 counter pass sees one kind of launch.
 
-    python tools/multi_traffic.py [info|noinfo] [cutoff]
+    python tools/multi_traffic.py [info|noinfo] [cutoff] [save.npz]
+
+With a third argument the final state is saved (a bitwise A/B of two builds:
+BRAX_AMD_LIB selects the library).
 """
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import brax_amd  # noqa: E402
@@ -31,6 +35,8 @@ def main():
     qp = sys_.step(qp, act, info=info)[0]
   torch.cuda.synchronize()
   print('mode', 'info' if info else 'noinfo', 'cutoff', cutoff, 'envs', B, 'rows', sys_.num_rows, flush=True)
+  if len(sys.argv) > 3:
+    np.savez(sys.argv[3], **{k: getattr(qp, k).cpu().numpy() for k in ('pos', 'rot', 'vel', 'ang')})
 
 
 if __name__ == '__main__':
