@@ -107,6 +107,89 @@ def _dist():
   return None, 0, 1, 0
 
 
+def rank_plan(gpus, environ):
+  """What `bench.py --gpus N` does in a process with environment `environ`:
+  ('run', None) when it is a rank of an N-process world (or N = 1 alone);
+  ('spawn', None) when N > 1 and no launcher set WORLD_SIZE, so this parent
+  must start the N ranks itself; ('refuse', why) when the world a launcher
+  made disagrees with --gpus (the line would name the wrong experiment)."""
+  if gpus < 1:
+    return 'refuse', f'--gpus {gpus}: need at least one GPU'
+  ws = environ.get('WORLD_SIZE')
+  if ws is None:
+    return ('spawn', None) if gpus > 1 else ('run', None)
+  if int(ws) != gpus:
+    return 'refuse', (f'--gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks: '
+                      'run with --gpus equal to the world size')
+  return 'run', None
+
+
+def rank_env(environ, rank, world, port):
+  """The environment of rank `rank` of a `world`-process run started by
+  `spawn_ranks` (torchrun's variables, one process per local GPU)."""
+  e = dict(environ)
+  e.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+           LOCAL_WORLD_SIZE=str(world), GROUP_RANK='0', MASTER_ADDR='127.0.0.1',
+           MASTER_PORT=str(port))
+  return e
+
+
+def spawn_ranks(gpus, argv, script=None):
+  """`python bench.py --gpus N` without a launcher: start N fresh rank
+  processes of this script (one per GPU, torchrun's environment) BEFORE this
+  parent touches the GPU, wait for all of them, and return the first failing
+  rank's exit status (the others are stopped then, since they would wait at a
+  barrier forever). Rank 0 prints the JSON line. (`script`: another program
+  in the ranks' place, for the CPU test of this contract.)"""
+  import signal
+  import socket
+  import subprocess
+  backend = os.environ.get('BX_DIST_BACKEND', 'nccl')
+  if backend == 'nccl':
+    have = torch.cuda.device_count()  # counts devices without initialising HIP
+    if have < gpus:
+      print(f'bench.py: --gpus {gpus} but {have} GPUs are visible', file=sys.stderr)
+      return 2
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  procs = [subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv),
+                            env=rank_env(os.environ, r, gpus, port))
+           for r in range(gpus)]
+
+  def stop(*_):
+    for q in procs:  # our own children, by PID
+      if q.poll() is None:
+        q.terminate()
+  # a launcher that stops this parent stops its ranks too
+  prev = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+  try:
+    return _wait_ranks(procs, stop)
+  finally:
+    signal.signal(signal.SIGTERM, prev)
+
+
+def _wait_ranks(procs, stop):
+  rc, t_stop = 0, None
+  live = list(procs)
+  while live:
+    for p in list(live):
+      code = p.poll()
+      if code is None:
+        continue
+      live.remove(p)
+      if code != 0 and rc == 0:
+        rc = code if code > 0 else 128 - code
+        stop()
+        t_stop = time.monotonic()
+    if t_stop is not None and live and time.monotonic() - t_stop > 15:
+      for q in live:
+        q.kill()
+      t_stop = None
+    time.sleep(0.05)
+  return rc
+
+
 def host_cpu():
   """This host's CPU: `nproc`, the CPUs this process may run on, and the
   /proc/cpuinfo model name."""
@@ -306,7 +389,11 @@ def secondary_configs(dev, steps=50):
         'value': Bm * n / wall, 'unit': 'env-steps/s (System.step)',
         'ms_per_step': wall * 1e3 / n, 'gpu_ms_per_step': gpu * 1e3 / n,
         'contact_rows': sys_.num_rows, 'lanes_per_env': sys_.lanes,
-        'lds_bytes_per_env': sys_.lds_bytes, 'envs_per_cu': (160 * 1024) // max(sys_.lds_bytes, 1)}
+        'lds_bytes_per_env': sys_.lds_bytes,
+        'envs_per_cu_by_lds': (160 * 1024) // max(sys_.lds_bytes, 1),
+        # the MULTI kernel holds 256 registers (two waves per SIMD): two
+        # 4-wave workgroups per CU run, whatever the LDS would admit
+        'envs_per_cu_by_registers': 2 if sys_.lanes == 256 else None}
     # the same steps without Info (System.step(..., info=False): the state
     # only, as jit drops the Info a caller ignores)
     wall, gpu = _time(mstep_noinfo, n, 2)
@@ -420,9 +507,15 @@ def _rocprof_avg(kernel, steps_per_launch=1):
   # directories) the exact kernel sources and build flags it was built from
   if not k or (d.get('lib_sha1') != sha and d.get('src_sha1') != src_sha1()):
     return None
-  per_step = k['avg_ns'] * 1e-6 / k.get('steps_per_launch', 1)
-  return {'avg_ms': per_step * steps_per_launch, 'avg_ms_per_step': per_step,
-          'profiled_steps_per_launch': k.get('steps_per_launch', 1), 'calls': k.get('calls'),
+  spl = k.get('steps_per_launch', 1)
+  per_step = k['avg_ns'] * 1e-6 / spl
+  # the profiled launch as measured, and the same rate scaled to this run's
+  # launch length (labelled apart: a 50-step launch profiled at 1.03 ms is
+  # 0.41 ms scaled to 20 steps, not a 0.41 ms 50-step launch)
+  return {'profiled_launch_ms': k['avg_ns'] * 1e-6, 'profiled_steps_per_launch': spl,
+          'avg_ms_per_step': per_step,
+          'scaled_to_steps_per_launch': steps_per_launch,
+          'scaled_launch_ms': per_step * steps_per_launch, 'calls': k.get('calls'),
           'source': d.get('source'), 'lib_sha1': sha, 'sq': k.get('sq')}
 
 
@@ -448,6 +541,12 @@ def main():
                   help='lanes,mode kernel variant (mode 0 global, 1 single, 2 lds)')
   args = ap.parse_args()
 
+  plan, why = rank_plan(args.gpus, os.environ)
+  if plan == 'refuse':
+    print(f'bench.py: {why}', file=sys.stderr)
+    sys.exit(2)
+  if plan == 'spawn':
+    sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
   dist, rank, world, local = _dist()
   dev = torch.device('cuda', local)
   torch.cuda.set_device(dev)

@@ -12,7 +12,7 @@ i32p = C.POINTER(C.c_int32)
 f64p = C.POINTER(C.c_double)
 f32p = C.POINTER(C.c_float)
 
-ABI_VERSION = 12  # include/brax_amd.h BX_ABI_VERSION
+ABI_VERSION = 13  # include/brax_amd.h BX_ABI_VERSION
 
 _DESC_FIELDS = [
     ('n_bodies', C.c_int32), ('n_joints', C.c_int32), ('n_actuators', C.c_int32),

@@ -53,7 +53,6 @@ struct bx_system {
   bool multi_ok = false;  // MODE_MULTI (3): large pbd scenes, 256 threads per env
   int fold = 0;     // every joint j has torque actuator j (the Ant / Humanoid env kernels)
   int jb = 0;       // the joint-halves env kernels may own body copies (JB, build_blob)
-  int sh = 0;       // the spherical joint halves at 32 lanes (the Humanoid env kernels)
   size_t lds_env = 0;    // bytes per block for the per-env kernels
   size_t lds_reset = 0;  // bytes per block for default_qp
 };
@@ -582,24 +581,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     }
     return true;
   };
-  // the spherical joint halves (the Humanoid env kernels at 32 lanes per env,
-  // pbd_kernels.hip joint_apply_half_sph): spherical joints only, each driven
-  // by the torque actuator of its index, <= 16 of them, one collider group of
-  // one-way capsule-plane rows, <= 16 rows at one per lane, gather lists <= 4,
-  // no forces, JB's body conditions. The lane image's joint-halves regions
-  // then map lane l to joint l & 15 and side l & 16 (the revolute halves: l & 7,
-  // l & 8). Opt-in (BX_SPH_HALVES=1): measured slower than the 16-lane
-  // kernel (Humanoid rollout 37.7 vs 32.1 us per step at 4,096 envs): its two
-  // waves per SIMD share one VALU, and the halves' redundant shared geometry
-  // leaves 1.65x the VALU work per env (Kernels)
-  bool sh = getenv("BX_SPH_HALVES") && atoi(getenv("BX_SPH_HALVES")) == 1 && H.single && L == 16 &&
-            !r2 && !c16 && mx <= 4 && max_groups <= 1 && J > 0 && J <= 16 && K == J && H.act_same &&
-            d->n_forces == 0;
-  for (int j = 0; j < J && sh; j++) sh = d->joint_type[j] == BX_JOINT_SPHERICAL;
-  for (int a = 0; a < K && sh; a++) sh = d->act_type[a] == BX_ACT_TORQUE;
-  for (int g = 0; g < G && sh; g++) sh = d->col_fn[g] == BX_COL_CAPSULE_PLANE && d->col_oneway[g];
-  sh = sh && jb_bodies_ok();
-  const int HB = sh ? 16 : 8;  // the joint halves' half width (lanes per side)
+  const int HB = 8;  // the joint halves' half width (lanes per side)
   // a contact row's 32 resolved words (LR_*): its record's geometry and
   // constants with the masses / inverse inertias of the bodies it names
   auto row_words = [&](int x, uint32_t* out) {
@@ -760,8 +742,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       for (int k = 0; k < 4; k++) put(lane, base + 10 + k, s[BODY_QM + k]);
     };
     // joint halves: lane m's side body (the parent of joint m & 7 on lanes
-    // 0-7 of each 16, the child on 8-15; the spherical halves: m & 15 on
-    // lanes 0-15 of each 32, the child on 16-31)
+    // 0-7 of each 16, the child on 8-15)
     auto side_body = [&](int m) {
       const int j = m & (HB - 1);
       const uint32_t* s = &B.w[H.o_joint + (j < J ? j : 0) * JOINT_STRIDE];
@@ -775,17 +756,14 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       put_act(l, LI_ACT, l < K ? l : 0);
       const int jh = l & (HB - 1);  // the lane's joint-halves joint
       put_joint(l, LI_JOINT_H, jh < J ? jh : 0);
-      // the staged limit rows (stage_lim): lane l -> joint l; the spherical
-      // halves' child lanes l >= 16 -> joint l & 15 (no other kernel reads a
-      // joint there: lanes past J hold none)
-      const int jl_ = sh ? (l & 15) : l;
-      put_lim(l, LI_JLIM, jl_ < J ? jl_ : 0, 0);
-      put_lim(l, LI_JLIM12, jl_ < J ? jl_ : 0, 1);
-      put_lim(l, LI_JLIM12 + 8, jl_ < J ? jl_ : 0, 2);
+      // the staged limit rows (stage_lim): lane l -> joint l
+      put_lim(l, LI_JLIM, l < J ? l : 0, 0);
+      put_lim(l, LI_JLIM12, l < J ? l : 0, 1);
+      put_lim(l, LI_JLIM12 + 8, l < J ? l : 0, 2);
       put_lim(l, LI_JLIM_H, jh < J ? jh : 0, 0);
       if (J > 0) {
         // the joint-halves side: the parent's on lanes 0-7, the child's on
-        // 8-15 (the spherical halves: 0-15, 16-31)
+        // 8-15
         const bool child = (l & HB) != 0;
         const uint32_t* s = &B.w[H.o_joint + (jh < J ? jh : 0) * JOINT_STRIDE];
         const int body = (int)s[child ? J_BC : J_BP];
@@ -795,14 +773,12 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
           put(l, LI_SIDE_H + LS_AX0 + k, s[(child ? J_AXC : J_AXP) + k]);
           put(l, LI_SIDE_H + LS_AX2 + k, s[(child ? J_AXC : J_AXP) + 6 + k]);
           put(l, LI_SIDE_H + LS_I + k, bw[BODY_I + k]);
-          put(l, LI_SIDE_AX1 + k, s[(child ? J_AXC : J_AXP) + 3 + k]);
         }
         put(l, LI_SIDE_H + LS_M, bw[BODY_MASS]);
         put(l, LI_SIDE_H + LS_SG, fbits(child ? -1.0 : 1.0));
         put(l, LI_SIDE_H + LS_BODY, (uint32_t)body);
         // JB: the side body's record and gather lists; LS_OWN on the lowest
-        // lane of the env's (16, or 32 for the spherical halves) whose side
-        // is that body
+        // lane of the env's 16 whose side is that body
         const bool hasS = jh < J;
         bool own = hasS;
         for (int m = l & ~(2 * HB - 1); m < l; m++)
@@ -852,7 +828,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
                                                      c16, r2g),
                                       (c16 ? mx_ja : mx) <= 4 ? 4 : 8) & 1)) {
     H.l_jlim = jlim_at;
-    H.env_words = (jlim_at + 24 * (sh ? 32 : L) + 63) & ~63;  // the spherical halves: 32 lanes
+    H.env_words = (jlim_at + 24 * L + 63) & ~63;
   }
   H.total_words = (int)B.w.size();
   std::memcpy(B.w.data(), &H, sizeof(BlobHdr));
@@ -875,8 +851,6 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     const bool jb_off = getenv("BX_NO_JB") && atoi(getenv("BX_NO_JB"));
     const bool jb = S->fold && (f & 128) && !(f & 16) && L == 16 && !jb_off && jb_bodies_ok();
     S->jb = jb ? 1 : 0;
-    // the spherical halves (the Humanoid env kernels at 32 lanes)
-    S->sh = (sh && S->fold && f == (1 | 32)) ? 1 : 0;
   }
   // the MULTI kernel is instantiated for the lean feature set (revolute,
   // torque, capsule-plane / capsule-capsule, no forces)
@@ -1080,10 +1054,8 @@ int bx_system_plan(const bx_desc* desc, const bx_reset_desc* reset, int32_t* mod
 }
 
 int bx_system_lanes(bx_system* S) { return S ? S->L : 0; }
-// (the spherical halves run when the system's SINGLE kernel is the default
-// one: bx_system_set_variant to other lanes or modes leaves them out)
 int bx_system_env_lanes(bx_system* S) {
-  return S ? ((S->sh && S->mode == 1 && S->L == 16 && S->tpb >= 32) ? 32 : S->L) : 0;
+  return S ? S->L : 0;
 }
 int bx_system_lds_bytes(bx_system* S) { return S ? (int)step_lds(S) : 0; }
 
@@ -1234,7 +1206,7 @@ static int env_step_impl(bx_system* S, const bx_env_params* env, int64_t n_envs,
   }
   if (S->mode == 1)
     HIP_OK(launch_env_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a,
-                                  S->fold ? (1 | (S->jb ? 2 : 0) | (S->sh ? 4 : 0)) : 0));
+                                  S->fold ? (1 | (S->jb ? 2 : 0)) : 0));
   else if (S->mode == 3)  // MULTI-mode systems step envs with the item-loop kernel
     HIP_OK(launch_env_step_generic(S->L, 0, S->feat, S->tpb, n_envs,
                                    (size_t)S->hdr.env_words * 4, as_stream(stream), a));
@@ -1503,7 +1475,7 @@ int bx_phase_capsule_plane(bx_system* S, int64_t n_envs, int64_t plane, const fl
 
 int bx_debug_partner(float* out64, int lanes, void* stream) {
   if (!out64) return fail("null argument");
-  if (lanes != 16 && lanes != 32) return fail("lanes must be 16 or 32");
+  if (lanes != 16) return fail("lanes must be 16 (the revolute joint halves' exchange)");
   HIP_OK(debug_partner(out64, lanes, as_stream(stream)));
   return 0;
 }

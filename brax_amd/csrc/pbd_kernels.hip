@@ -176,7 +176,6 @@ struct JointC {
 // per-substep code selects no constants by side
 struct JSide {
   v3 off, ax0, ax2, I;
-  v3 ax1;  // the spherical halves' second axis
   float m, sg;
   int body;
 };
@@ -1427,143 +1426,6 @@ __device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL
 }
 
 // ---------------------------------------------------------------------------
-// spherical joint halves (F_SPH | F_JH at 32 lanes per env: the Humanoid env
-// kernels): lane j works the parent side of joint j and lane j + 16 its child
-// side, each with its own copy of its side's body (JB). A lane rotates only
-// its own body's axes (one rotation matrix) and trades them with its partner;
-// the geometry both sides share (the position constraint's direction and
-// effective masses, the spherical frame lon / xz / a2n, the three limit
-// tests) is computed on both lanes, the three limit rows' impulses split two
-// (the parent lane: rows 0 and 1) to one (the child lane: row 2), and each
-// lane forms only its own body's rotation update. The operations and their
-// order are the 16-lane kernel's (joint_apply / act_torque on the lane
-// image), so the two kernels' results are bit-identical.
-// ---------------------------------------------------------------------------
-// the partner half's value (lane ^ L / 2 within the env): a DPP row rotation
-// at 16 lanes; at 32, v_permlane16_swap exchanges rows 0 / 1 (2 / 3) of a
-// register and each lane keeps the row it does not hold
-template <int L>
-__device__ __forceinline__ float xhl(float v) {
-  if constexpr (L == 16) {
-    return xh(v);
-  } else {
-    static_assert(L == 32, "joint halves: 16 or 32 lanes per env");
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
-  }
-}
-template <int L>
-__device__ __forceinline__ v3 xhl3(v3 v) { return mk(xhl<L>(v.x), xhl<L>(v.y), xhl<L>(v.z)); }
-
-// the five world axes of a spherical joint (a1p, a2p of the parent; a1c, a2c,
-// a3c of the child) from this side's three and the partner's
-struct SphAxes {
-  v3 a1p, a2p, a1c, a2c, a3c;
-};
-template <int L>
-__device__ __forceinline__ SphAxes sph_axes(const RotM& Mo, const JSide& S, bool child) {
-  const v3 u0 = mrot(Mo, S.ax0), u1 = mrot(Mo, S.ax1), u2 = mrot(Mo, S.ax2);
-  const v3 t0 = xhl3<L>(u0), t1 = xhl3<L>(u1), t2 = xhl3<L>(u2);
-  return SphAxes{sel3(child, t0, u0), sel3(child, t1, u1), sel3(child, u0, t0), sel3(child, u1, t1),
-                 sel3(child, u2, t2)};
-}
-
-// a limit row whose slot group depends on the lane (the spherical halves'
-// first row slot: row 0 on the parent lane, row 2 on the child's)
-template <int L>
-__device__ __forceinline__ JLim ld_lim_v(const uint4* li, int g) {
-  const uint4 a = li[g * L], b = li[(g + 1) * L];
-  return JLim{__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z),
-              __uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y)};
-}
-
-// Spherical.apply_reduced (joints.py:332-386) with the position constraint
-// (joints.py:154-195), one side: o is this side's body; returns its dp, dq
-template <int L>
-__device__ __forceinline__ void joint_apply_half_sph(const JointC& J, const JSide& S, bool child,
-                                                     const uint4* LI, const QP& o, v3& dpo, q4& dro) {
-  const RotM Mo = rot_matrix(o.rot);
-  // positional constraint (as joint_apply_half: the parent's anchor minus
-  // the child's on both lanes, the effective masses added in either order)
-  const v3 wo = o.pos + mrot(Mo, S.off);
-  const v3 ro = wo - o.pos;
-  const v3 dx = S.sg * (wo - xhl3<L>(wo));
-  const float cc = cancel_norm(dx);
-  const v3 n = dx / (cc + 1e-6f);
-  const v3 cr = cross(ro, n);
-  const float wm = 1.f / S.m + dot(cr, mul(S.I, cr));
-  const float dl = -cc / (wm + xhl<L>(wm) + 1e-6f);
-  const v3 pv = dl * n;
-  dpo = J.sp * ((S.sg * pv) / S.m);
-  // the spherical frame (both lanes)
-  const SphAxes X = sph_axes<L>(Mo, S, child);
-  v3 lon = cross(X.a3c, X.a1p);
-  lon = lon / (1e-6f + dir_norm(lon));
-  v3 xz = dot(X.a1p, X.a1c) * X.a1c + dot(X.a1p, X.a2c) * X.a2c;
-  xz = xz / (1e-6f + dir_norm(xz));
-  v3 a2n = cross(xz, X.a1p);
-  a2n = a2n / (1e-6f + dir_norm(a2n));
-  const float sg = signf(dot(X.a1p, X.a3c));
-  // limit_angle on pseudo-angles (as joint_apply's lane-image rows)
-  auto row = [&](v3 nv, v3 n1v, v3 n2v, const JLim& Lr) {
-    const float y = dot(cross(n1v, n2v), nv), x = dot(n1v, n2v);
-    const float pa = pseudo_angle(x, y);
-    const bool below = pa < Lr.plo, above = pa > Lr.phi;
-    const v3 n1 = turn(n1v, nv, below ? Lr.clo : Lr.chi, below ? Lr.slo : Lr.shi);
-    const v3 dq = cross(n1, n2v) * ((below || above) ? 1.f : 0.f);
-    return angle_impulse(J, dq);
-  };
-  // slot A: row 0 (nv a1p, n1 a2p, n2 lon) on the parent lane, row 2 (a3c,
-  // lon, a2c) on the child's; slot B: row 1 (-a2n sg, a1p, xz), the parent's
-  const v3 iA = row(sel3(child, X.a3c, X.a1p), sel3(child, lon, X.a2p), sel3(child, X.a2c, lon),
-                    ld_lim_v<L>(LI, child ? LIM_G2 : LIM_G0));
-  const v3 iB = row(-a2n * sg, X.a1p, xz, ld_lim<L>(LI, LIM_G1));
-  // pimp = ((0 + row 0) + row 1) + row 2 on both lanes: the parent sends its
-  // partial sum, the child its row 2
-  const v3 p01 = (mk(0.f, 0.f, 0.f) + iA) + iB;
-  const v3 got = xhl3<L>(sel3(child, iA, p01));
-  const v3 pimp = sel3(child, got, p01) + sel3(child, iA, got);
-  const v3 P = J.sp * cross(ro, pv) + J.sa * pimp;
-  dro = (S.sg * 0.5f) * vec_quat_mul(mul(S.I, P), o.rot);
-}
-
-// Actuator.apply_reduced (actuators.py:52-112), a torque actuator on a
-// spherical joint, one side; tqd: the joint's damping torque (FOLD)
-template <int L>
-__device__ __forceinline__ void act_torque_half_sph(const JSide& S, const ActC& A, const Env& E,
-                                                    const float* al, int a, bool child, const q4& ro,
-                                                    const uint4* LI, const v3& tqd) {
-  const SphAxes X = sph_axes<L>(rot_matrix(ro), S, child);
-  // Spherical.axis_angle's three angles on pseudo-angles (act_torque)
-  const v3 lon = cross(X.a3c, X.a1p);
-  const v3 xz = dot(X.a1p, X.a1c) * X.a1c + dot(X.a1p, X.a2c) * X.a2c;
-  const float xb = dot(xz, X.a1p), r2 = dot(xz, xz);
-  const float sg = signf(dot(X.a1p, X.a3c));
-  const float yb = r2 > 0.f ? sg * __builtin_amdgcn_sqrtf(fmaxf(r2 - xb * xb, 0.f)) : sg;
-  // psi (pa[0]) and phi (pa[2]) have one form, pseudo_angle(v . lon,
-  // (v x lon) . w): the parent lane takes psi's (v, w) = (a2p, a1p), the
-  // child phi's (a2c, -a3c), and they trade the results
-  const v3 pv = sel3(child, X.a2c, X.a2p), pw = sel3(child, -X.a3c, X.a1p);
-  const float pm = pseudo_angle(dot(pv, lon), dot(cross(pv, lon), pw));
-  const float po = xhl<L>(pm);
-  float pa[3];
-  pa[0] = child ? po : pm;
-  pa[1] = pseudo_angle(sg == 0.f ? 1.f : xb, yb);
-  pa[2] = child ? pm : po;
-  const v3 axes[3] = {X.a1p, X.a2c, X.a3c};
-  v3 tq = mk(0.f, 0.f, 0.f);
-#pragma unroll
-  for (int l = 0; l < 3; l++) {
-    const float2 Lr = ld_lim_p<L>(LI, lim_group(l));
-    const float t = al[l] * A.strength * -1.f;
-    tq = tq + axes[l] * ((pa[l] < Lr.x || pa[l] > Lr.y) ? 0.f : t);
-  }
-  tq = tq + tqd;
-  // parent: Ip tq, child: -Ic tq
-  st_v3a(E.aslot + (child ? E.nK + a : a) * ASLOT_STRIDE, S.sg * mul(S.I, tq));
-}
-
-// ---------------------------------------------------------------------------
 // per-env LDS carving
 // ---------------------------------------------------------------------------
 // every LDS region starts 16-byte aligned (offsets are multiples of 4 words,
@@ -2339,16 +2201,15 @@ struct Hoist {
 // LI_*): every load independent and unconditional, so the whole set costs one
 // L2 round trip (the records' own layout needs three dependent ones: list
 // offsets -> entries, joint / row -> the bodies it references).
-// JH (joint halves): lanes j and j + HALF both hold joint j and actuator j
-// (HALF 8 at 16 lanes per env; the spherical halves: 16 at 32 lanes).
-// JB (JH, the Ant / HalfCheetah / Humanoid env kernels): the lane's body is
-// its side's (parent of joint j on lane j, child on lane j + HALF), a copy
-// per side lane
-template <int M, bool JH, bool R2 = false, int MC = M, bool JB = false, int HALF = 8>
+// JH (joint halves): lanes j and j + 8 of an env's 16 both hold joint j and
+// actuator j. JB (JH, the Ant / HalfCheetah env kernels): the lane's body is
+// its side's (parent of joint j on lane j, child on lane j + 8), a copy per
+// side lane
+template <int M, bool JH, bool R2 = false, int MC = M, bool JB = false>
 __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& H, int lane,
                                            Hoist<M, MC>& X) {
   static_assert(!JB || (JH && MC <= 8), "JB: joint halves, <= 8 contact entries");
-  const int jx = JH ? (lane & (HALF - 1)) : lane;
+  const int jx = JH ? (lane & 7) : lane;
   X.hasB = JB ? jx < H.J : lane < H.N;
   X.hasJ = jx < H.J;
   X.hasA = jx < H.K;
@@ -2383,7 +2244,6 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   constexpr int OL = JH ? LI_JLIM_H : LI_JLIM;
   grab(OL, 8);
   if constexpr (JH) grab(LI_SIDE_H, 16);
-  if constexpr (JH && HALF == 16) grab(LI_SIDE_AX1, 4);
   auto f = [&](int i) { return __uint_as_float(w[i]); };
   auto f3 = [&](int i) { return mk(f(i), f(i + 1), f(i + 2)); };
   auto n = [&](int i) { return (int)w[i]; };
@@ -2461,7 +2321,6 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
     X.S.m = f(LI_SIDE_H + LS_M);
     X.S.sg = f(LI_SIDE_H + LS_SG);
     X.S.body = n(LI_SIDE_H + LS_BODY);
-    X.S.ax1 = HALF == 16 ? f3(LI_SIDE_AX1) : mk(0.f, 0.f, 0.f);
   }
   X.own = JB ? (X.hasB && n(LI_SIDE_H + LS_OWN) != 0) : X.hasB;
 #pragma unroll
@@ -2654,15 +2513,11 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   // 672-720 B per lane in every revolute kernel without joint halves)
   constexpr bool JLH = (F & F_SPH) == 0;
   const uint4* LIP = (F & F_SPH) != 0 ? E.jlim + lane : nullptr;  // staged by stage_lim
-  // JH: this lane's joint / actuator and its side (lanes j and j + HALF:
-  // 8 at 16 lanes per env, 16 for the spherical halves at 32)
-  constexpr int HALF = L == 32 ? 16 : 8;
-  const int jx = lane & (HALF - 1);
-  const bool child = (lane & HALF) != 0;
-  // SH: the spherical halves (bit-identical to the 16-lane kernel: IEEE
-  // normalisation as there, not the Ant kernel's bare square root)
-  constexpr bool SH = JH && (F & F_SPH) != 0;
-  static_assert(!JH || L == 16 || (SH && L == 32), "joint halves: revolute at 16 lanes, spherical at 32");
+  // JH: this lane's joint / actuator and its side (lanes j and j + 8 of the
+  // env's 16)
+  const int jx = lane & 7;
+  const bool child = (lane & 8) != 0;
+  static_assert(!JH || (L == 16 && (F & F_SPH) == 0), "joint halves: revolute joints at 16 lanes");
   // JB (the Ant / HalfCheetah env kernels: joint halves, damping folded):
   // the lane's body is its side's, every side lane updating its own copy
   // with the same instructions and inputs (the side body's constants and
@@ -2674,7 +2529,6 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   // Bodies on no joint side are frozen (checked on the host) and keep their
   // loaded record
   constexpr bool JB = FOLD && JH;
-  static_assert(!SH || JB, "the spherical halves: the env kernels' body copies");
   const int bi = JB ? X.S.body : lane;  // the lane's body
   float* myqp = E.qp + bi * QP_STRIDE;
   QP q;
@@ -2732,13 +2586,9 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         if constexpr (JB) {
           // the partner lane holds the joint's other body
           const JointC& Jc = X.J;
-          const v3 oa = xhl3<L>(q.ang);
+          const v3 oa = xh3(q.ang);
           const v3 tqd = -1.f * Jc.damping * (sel3(child, oa, q.ang) - sel3(child, q.ang, oa));
-          if constexpr (SH) {
-            if (hasA) act_torque_half_sph<L>(X.S, X.A, E, al, jx, child, q.rot, LIP, tqd);
-          } else {
-            if (hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, q.rot, &tqd);
-          }
+          if (hasA) act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, jx, child, q.rot, &tqd);
         } else if constexpr (FOLD) {
           const JointC& Jc = X.J;
           const v3 tqd = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
@@ -2788,7 +2638,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         v3 am = mul(q.ang, X.B.rm);
         q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
         q4 r = q.rot + quat_mul(hq, q.rot);
-        q.rot = (JB && !SH) ? qnormalize_bare(r) : qnormalize(r);  // Ant env kernel: bare sqrt
+        q.rot = JB ? qnormalize_bare(r) : qnormalize(r);  // Ant env kernel: bare sqrt
         if (!JB) stqp(myqp, q);  // JB: the joint phase takes the lane's copy
         dpa_last = dpa;
       }
@@ -2800,8 +2650,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
           const QP o = JB ? q : ldqp(E.qp + X.S.body * QP_STRIDE);
           v3 dpo;
           q4 dro;
-          if constexpr (SH) joint_apply_half_sph<L>(Jc, X.S, child, LIP, o, dpo, dro);
-          else joint_apply_half(Jc, X.JL, X.S, child, o, dpo, dro);
+          joint_apply_half(Jc, X.JL, X.S, child, o, dpo, dro);
           st_slot(E.jslot + (child ? E.nJ + jx : jx) * SLOT_STRIDE, dpo, dro, 0.f);
         }
       } else if (hasJ) {
@@ -2830,7 +2679,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         q.pos = q.pos + mul(dp, X.B.pm);
         q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                    q.rot.z + dr.z * X.B.qm.z};
-        if (sub == 0) vproj(q, ppos, prot, X.B, h, JB && !SH);
+        if (sub == 0) vproj(q, ppos, prot, X.B, h, JB);
         // JB: the record is read next by the contact passes (after sub 1)
         if (!JB || sub == 1) stqp(myqp, q);
       }
@@ -2912,7 +2761,7 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                  q.rot.z + dr.z * X.B.qm.z};
       st_rb(E.rb + bi * RB_STRIDE, q.pos, q.vel, q.ang);
-      vproj(q, ppos, prot, X.B, h, JB && !SH);
+      vproj(q, ppos, prot, X.B, h, JB);
       stqp(myqp, q);
     }
     phase_sync();
@@ -4193,7 +4042,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   if constexpr (S) {
     // JB: the env-program kernels with joint halves (pbd_step_single's FOLD && JH)
     load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>(),
-               (F & F_JH) != 0 && EK != EK_ANY, L == 32 ? 16 : 8>(A.blob, H, lane, X);
+               (F & F_JH) != 0 && EK != EK_ANY>(A.blob, H, lane, X);
     stage_lim<L, F>(A.blob, H, E, lane);
   }
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
@@ -5107,22 +4956,6 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
       launch_one<EnvArgs>(env_step_kernel<16, 1, F_G1 | F_JH, 4, EK_ANT>, grid, tpb, lds, s, a);
     return hipGetLastError();
   }
-  // the spherical joint halves (fold bit 2: the system allows them): 32
-  // lanes per env, lanes j and j + 16 the two sides of joint j, two envs per
-  // wave (twice the waves of the 16-lane kernel for one batch)
-  if ((fold & 4) && L == 16 && gw <= 4 && tpb >= 32 &&
-      (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP) && feat == (F_SPH | F_G1)) {
-    constexpr int FH = F_SPH | F_G1 | F_JH;
-    const int e32 = tpb / 32;
-    const dim3 g32((unsigned)((n_envs + e32 - 1) / e32));
-    const size_t lds32 = lds / (size_t)epb * (size_t)e32;  // the env blocks of e32 envs
-    // (the register-capped kernels: two waves per SIMD, the point of 32 lanes)
-    if (a.n_steps > 1 || a.packed)
-      launch_one<EnvArgs>(env_rollout_wide_kernel<32, 1, FH, 4, EK_HUM>, g32, tpb, lds32, s, a);
-    else
-      launch_one<EnvArgs>(env_step_wide_kernel<32, 1, FH, 4, EK_HUM>, g32, tpb, lds32, s, a);
-    return hipGetLastError();
-  }
   if (fold && L == 16 && gw <= 4 && (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP) &&
       feat == (F_SPH | F_G1)) {
     if (a.n_steps > 1)
@@ -5157,7 +4990,7 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
 // the joint halves' partner exchange alone (bx_debug_partner)
 __global__ void __launch_bounds__(64) partner_kernel(float* out, int lanes) {
   const float v = (float)threadIdx.x;
-  out[threadIdx.x] = lanes == 32 ? xhl<32>(v) : xhl<16>(v);
+  out[threadIdx.x] = lanes == 16 ? xh(v) : v;
 }
 hipError_t debug_partner(float* out64, int lanes, hipStream_t s) {
   hipLaunchKernelGGL(partner_kernel, dim3(1), dim3(64), 0, s, out64, lanes);

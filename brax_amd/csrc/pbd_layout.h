@@ -136,13 +136,9 @@ enum {
   LI_JL_J = 292,
   LI_AL_J = 300,
   LI_CL_J = 308,
-  // spherical joint halves (32 lanes per env): the side's second axis (LS_*
-  // continued: ax1 3, pad 1)
-  LI_SIDE_AX1 = 316,
-  LANE_W = 320
+  LANE_W = 316
 };
-// a joint-halves lane's side (lanes 8-15 of 16: the child's; the spherical
-// halves at 32 lanes: lanes 16-31): its anchor offset,
+// a joint-halves lane's side (lanes 8-15 of 16: the child's): its anchor offset,
 // hinge axis and reference axis in its body's frame, that body's inverse
 // inertia and mass, the side's sign (+1 parent, -1 child) and the body;
 // LS_OWN: 1 on the lowest lane whose side is that body (JB: the copy that

@@ -210,8 +210,8 @@ class EvalWrapper(Wrapper):
 
 # ---------------------------------------------------------------------------
 # gym-API adapters (`wrappers.py:206-337`) -- gym itself is not a dependency:
-# spaces are plain Box descriptions; outputs stay device tensors (the role of
-# the reference's JaxToTorchWrapper DLPack hop, `to_torch.py:28-64`).
+# spaces are plain Box descriptions; outputs stay device tensors (the torch
+# side, the reference's JaxToTorchWrapper, is `brax_amd.envs.to_torch`).
 # ---------------------------------------------------------------------------
 
 @dataclasses.dataclass(frozen=True)
@@ -285,30 +285,3 @@ class VectorGymWrapper(GymWrapper):
     self.single_action_space = self.action_space
     self.observation_space = _box(env.observation_size, np.inf, self.num_envs)
     self.action_space = _box(env.action_size, 1.0, self.num_envs)
-
-
-class TorchWrapper:
-  """`to_torch.py:28-64` (JaxToTorchWrapper): outputs as torch tensors on
-  `device`; brax_amd outputs already are device tensors, so this only moves
-  them when another device is asked for."""
-
-  def __init__(self, env, device=None):
-    self.env = env
-    self.device = device
-
-  def __getattr__(self, name):
-    return getattr(self.env, name)
-
-  def _t(self, x):
-    if isinstance(x, dict):
-      return {k: self._t(v) for k, v in x.items()}
-    if isinstance(x, torch.Tensor) and self.device is not None:
-      return x.to(self.device)
-    return x
-
-  def reset(self):
-    return self._t(self.env.reset())
-
-  def step(self, action):
-    obs, reward, done, info = self.env.step(action)
-    return self._t(obs), self._t(reward), self._t(done), self._t(info)

@@ -149,8 +149,7 @@ class System:
   @property
   def env_lanes(self):
     """Threads per env of the Env.step / rollout kernels (bx_system_env_lanes):
-    32 where the env kernels split each joint over two lanes (the spherical
-    joint halves, Humanoid), else `lanes`."""
+    the step kernels' `lanes`."""
     return _native.lib().bx_system_env_lanes(self._h)
 
   @property
@@ -163,7 +162,10 @@ class System:
     """The kernel plan `config` compiles to, on the host without a device
     (bx_system_plan): {'mode': 1 SINGLE / 3 MULTI / 0 item loops, 'lanes':
     threads per env, 'lds_bytes': the System.step kernel's LDS per workgroup,
-    'envs_per_cu_by_lds': what 160 KB of LDS holds}."""
+    'envs_per_cu_by_lds': what 160 KB of LDS holds, 'envs_per_cu_by_registers':
+    what the register file holds (MULTI: the kernel is built for two waves per
+    SIMD, 256 registers, so two 4-wave workgroups; None where not fixed by the
+    build), 'envs_per_cu': the smaller of the two, i.e. what runs}."""
     vc, desc, meta = compiler.compile_system(config)
     rdesc = compiler.compile_reset(vc, meta['body_index'])
     cd, keep = abi.make_desc(desc)
@@ -174,8 +176,13 @@ class System:
     del keep, keep_r
     per_wg = lds.value
     envs_per_wg = max(64 // lanes.value, 1)
+    by_lds = (160 * 1024 // per_wg) * envs_per_wg if per_wg else None
+    # system_step_multi_kernel<M, 2>: amdgpu_waves_per_eu(2) (pbd_kernels.hip)
+    by_regs = 2 if mode.value == 3 else None
+    runs = min(x for x in (by_lds, by_regs) if x is not None) if (by_lds or by_regs) else None
     return {'mode': mode.value, 'lanes': lanes.value, 'lds_bytes': per_wg,
-            'envs_per_cu_by_lds': (160 * 1024 // per_wg) * envs_per_wg if per_wg else None}
+            'envs_per_cu_by_lds': by_lds, 'envs_per_cu_by_registers': by_regs,
+            'envs_per_cu': runs}
 
   def _create(self, reset_desc):
     cd, keep = abi.make_desc(self.desc)

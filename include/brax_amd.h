@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BX_ABI_VERSION 12
+#define BX_ABI_VERSION 13
 
 /* joint kinds, actuator kinds, contact functions (descriptor enums) */
 enum { BX_JOINT_REVOLUTE = 1, BX_JOINT_UNIVERSAL = 2, BX_JOINT_SPHERICAL = 3 };
@@ -308,8 +308,8 @@ int bx_system_destroy(bx_system* sys);
 int bx_system_lanes(bx_system* sys);
 
 /* Threads per env of this system's Env.step / rollout kernels (bx_env_step,
- * bx_env_rollout_*): the step kernels' lanes, or 32 where the env kernels
- * work each joint with two lanes (the spherical joint halves: Humanoid). */
+ * bx_env_rollout_*): the step kernels' lanes. (ABI 12's opt-in 32-lane
+ * spherical joint halves measured slower and were removed in ABI 13.) */
 int bx_system_env_lanes(bx_system* sys);
 
 /* The host half of bx_system_create, without a device: the kernel plan the
@@ -525,10 +525,10 @@ int bx_phase_capsule_plane(bx_system* sys, int64_t n_envs, int64_t plane, const 
  * the per-workgroup sums, 4096 x 16 entries. Fails on product builds. */
 int bx_debug_stamps(unsigned long long* out16, int reset);
 
-/* The joint halves' partner exchange on its own (diagnostic): one wavefront
- * writes out64[l] = the value lane l receives from its partner lane
- * (l ^ lanes / 2 within each env of `lanes` = 16 or 32 threads) when every
- * lane offers its own index. */
+/* The revolute joint halves' partner exchange on its own (diagnostic): one
+ * wavefront writes out64[l] = the value lane l receives from its partner lane
+ * (l ^ 8 within each env of `lanes` = 16 threads) when every lane offers its
+ * own index. */
 int bx_debug_partner(float* out64, int lanes, void* stream);
 
 /* Multi-rank episodic exchange is done over RCCL by the host (torch.distributed);

@@ -596,6 +596,62 @@ def wrapped_ant(n_envs=8, n_steps=6, episode_length=3, action_repeat=1):
   return r
 
 
+def gym_ant(n_envs=8, n_steps=6, episode_length=3):
+  """The reference's gym path: `envs.create_gym_env('ant', batch_size=B,
+  episode_length=L)` (`envs/__init__.py:118-130`) -> VectorGymWrapper, whose
+  jitted step returns (obs, reward, done, info = {**state.metrics,
+  **state.info}) (`wrappers.py:311-314`); JaxToTorchWrapper (`to_torch.py:
+  28-64`) only converts those leaves. Records every leaf of every step's
+  return and the wrapped state the steps start from (`_state` after reset:
+  the reset key is parity-unpinned, so the build starts from these arrays).
+  jax.jit and jax.random.PRNGKey are absent offline: during this call jit is
+  the identity (the numpy backend runs the same function eagerly) and
+  PRNGKey(seed) is the (2,) uint32 key layout [0, seed]."""
+  import types
+  import jax
+  from brax import envs
+  saved = {k: getattr(jax, k, None) for k in ('jit', 'random')}
+  jax.jit = lambda fun, **_: fun
+  jax.random = types.SimpleNamespace(PRNGKey=lambda seed: np.array([0, seed], np.uint32))
+  try:
+    g = envs.create_gym_env('ant', batch_size=n_envs, seed=5, episode_length=episode_length)
+    g.reset()
+    st = g._state  # pylint: disable=protected-access
+    out = {'qp0': qp_pack(st.qp), 'obs0': np.asarray(st.obs),
+           'reward0': np.asarray(st.reward, np.float64), 'done0': np.asarray(st.done, np.float64),
+           'first_qp': qp_pack(st.info['first_qp']), 'first_obs': np.asarray(st.info['first_obs']),
+           'steps0': np.asarray(st.info['steps'], np.float64),
+           'truncation0': np.asarray(st.info['truncation'], np.float64)}
+    acts = np.stack([np.random.default_rng(40_000 + t).uniform(-1, 1, (n_envs, 8))
+                     for t in range(n_steps)])
+    rec = {}
+    keys = None
+    for t in range(n_steps):
+      obs, reward, done, info = g.step(acts[t])
+      if keys is None:
+        keys = sorted(info)
+      assert sorted(info) == keys
+      rec.setdefault('obs', []).append(np.asarray(obs))
+      rec.setdefault('reward', []).append(np.asarray(reward, np.float64))
+      rec.setdefault('done', []).append(np.asarray(done, np.float64))
+      rec.setdefault('qp', []).append(qp_pack(g._state.qp))  # pylint: disable=protected-access
+      for k in keys:
+        v = info[k]
+        v = qp_pack(v) if k == 'first_qp' else np.asarray(v, np.float64)
+        rec.setdefault('info_' + k, []).append(v)
+  finally:
+    for k, v in saved.items():
+      if v is None:
+        delattr(jax, k)
+      else:
+        setattr(jax, k, v)
+  out.update({k: np.stack(v) for k, v in rec.items()})
+  out['action'] = acts
+  out['info_keys'] = np.array(keys)
+  out['episode_length'] = np.int32(episode_length)
+  return out
+
+
 def kats():
   """Known answers: the reference's own geometry/math functions."""
   from brax import math as bm
@@ -683,8 +739,8 @@ def main():
   args = ap.parse_args()
   _setup()
   if args.desc_only:
-    global env_traj, sys_traj, wrapped_ant, kats  # pylint: disable=global-statement
-    env_traj = sys_traj = wrapped_ant = kats = lambda *a, **k: None  # noqa: E731
+    global env_traj, sys_traj, wrapped_ant, kats, gym_ant  # pylint: disable=global-statement
+    env_traj = sys_traj = wrapped_ant = kats = gym_ant = lambda *a, **k: None  # noqa: E731
   os.makedirs(OUT, exist_ok=True)
   from brax import envs
   from brax.envs import ant as ant_mod
@@ -765,6 +821,8 @@ def main():
     save('wrap_ant', wrapped_ant())
   if want('wrap_ar2'):
     save('wrap_ant_ar2', wrapped_ant(n_steps=6, episode_length=5, action_repeat=2))
+  if want('gym_ant'):
+    save('gym_ant', gym_ant())
   # physics-only rollouts of the other registered envs' systems (their pbd
   # configs): Thruster/Twister forces, frozen bodies, systems without contacts
   for mod, (B, T, aw) in ROBOTS.items():

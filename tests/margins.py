@@ -8,13 +8,32 @@ import json
 import os
 
 _MARGINS = []
+_RATIOS = {}
 
 
-def record_margin(field, measured, tol, **extra):
-  """`extra`: e.g. `n`, the samples the gate covered."""
+def record_margin(field, measured, tol, ratios=None, **extra):
+  """`extra`: e.g. `n`, the samples the gate covered. `ratios`: every env's
+  measured / bound of a per-env gate (pooled per test and field over the
+  test's steps into the ratio table)."""
   test = os.environ.get('PYTEST_CURRENT_TEST', '?').split(' ')[0]
   _MARGINS.append({'test': test, 'field': field, 'measured': measured, 'tol': tol,
                    'ratio': measured / tol if tol > 0 else None, **extra})
+  if ratios is not None:
+    _RATIOS.setdefault((test, field), []).extend(ratios)
+
+
+def ratio_table():
+  """Per (test, field): the per-env ratios HIP_i / max(1e-5, 2 E32_i) pooled
+  over the test's steps: n, p50, p99, max, and how many exceed 1 / 0.9."""
+  import numpy as np
+  rows = []
+  for (test, field), r in _RATIOS.items():
+    a = np.asarray(r, np.float64)
+    rows.append({'test': test, 'field': field, 'n': int(a.size),
+                 'p50': float(np.percentile(a, 50)), 'p99': float(np.percentile(a, 99)),
+                 'max': float(a.max()), 'over_1': int((a > 1).sum()),
+                 'over_0.9': int((a > 0.9).sum())})
+  return sorted(rows, key=lambda m: -m['max'])
 
 
 def write(path):
@@ -34,5 +53,12 @@ def write(path):
     # envs' binding gate is `:illcond_nearest` (<= 1e-2 by construction)
     wide = [m for m in rows if m['tol'] > 1e-2 and m.get('role') != 'envelope']
     env = [m for m in rows if m.get('role') == 'envelope']
+    table = ratio_table()
     json.dump({'n_gates': len(_MARGINS), 'n_wide_gates': len(wide), 'wide_gates': wide,
-               'envelope_gates': env, 'worst_per_test_field': rows}, f, indent=1)
+               'envelope_gates': env,
+               'per_env_ratio_table': table,
+               'per_env_over_1': sum(t['over_1'] for t in table),
+               'per_env_over_0.9': sum(t['over_0.9'] for t in table),
+               'envelope_realisations_per_env': 2 * (1 + int(os.environ.get('BX_ENVELOPE_N', '32'))),
+               'worst_per_test_field': [{k: v for k, v in m.items() if k != 'ratios'}
+                                        for m in rows]}, f, indent=1)

@@ -36,3 +36,55 @@ def test_traffic_carries_algorithmic_bytes_per_env_kernel():
   assert ant['algorithmic_bytes_per_launch'] == bench.ANT_BYTES_PER_ENV_STEP * 4096
   hum = t['bx::env_step_packed_kernel<16, 1, 33, 4, 2>']
   assert hum['algorithmic_bytes_per_launch'] == 2284 * 4096
+
+
+def test_rank_plan_follows_gpus_and_the_launcher():
+  """`--gpus N` is the experiment the line names: alone it spawns N ranks, a
+  launcher's world must match it, and N = 1 runs in place."""
+  assert bench.rank_plan(1, {}) == ('run', None)
+  assert bench.rank_plan(8, {}) == ('spawn', None)
+  assert bench.rank_plan(2, {'WORLD_SIZE': '2'}) == ('run', None)
+  assert bench.rank_plan(1, {'WORLD_SIZE': '1'}) == ('run', None)
+  for gpus, env in ((8, {'WORLD_SIZE': '1'}), (1, {'WORLD_SIZE': '4'}), (0, {})):
+    plan, why = bench.rank_plan(gpus, env)
+    assert plan == 'refuse' and why
+
+
+def test_rank_env_is_torchruns():
+  e = bench.rank_env({'X': '1'}, 3, 8, 29999)
+  assert (e['RANK'], e['LOCAL_RANK'], e['WORLD_SIZE'], e['MASTER_ADDR'], e['MASTER_PORT'],
+          e['X']) == ('3', '3', '8', '127.0.0.1', '29999', '1')
+
+
+def _script(tmp_path, body):
+  p = tmp_path / 'rank.py'
+  p.write_text('import os, sys, time\n' + body)
+  return str(p)
+
+
+def test_spawn_ranks_starts_n_ranks(tmp_path, monkeypatch):
+  monkeypatch.setenv('BX_DIST_BACKEND', 'gloo')
+  out = tmp_path / 'seen'
+  out.mkdir()
+  s = _script(tmp_path, f"open(os.path.join({str(out)!r}, os.environ['RANK']), 'w').write("
+                        "os.environ['WORLD_SIZE'] + ' ' + ' '.join(sys.argv[1:]))\n")
+  assert bench.spawn_ranks(3, ['--gpus', '3'], script=s) == 0
+  assert sorted(os.listdir(out)) == ['0', '1', '2']
+  assert (out / '2').read_text() == '3 --gpus 3'
+
+
+def test_spawn_ranks_fails_when_a_rank_fails(tmp_path, monkeypatch):
+  """A failing rank fails the run, and the ranks left waiting (as at a
+  barrier) are stopped instead of hanging the parent."""
+  monkeypatch.setenv('BX_DIST_BACKEND', 'gloo')
+  s = _script(tmp_path, "sys.exit(3) if os.environ['RANK'] == '1' else time.sleep(600)\n")
+  import time
+  t0 = time.monotonic()
+  assert bench.spawn_ranks(2, [], script=s) == 3
+  assert time.monotonic() - t0 < 60
+
+
+def test_spawn_ranks_refuses_more_rccl_ranks_than_gpus(monkeypatch):
+  monkeypatch.delenv('BX_DIST_BACKEND', raising=False)
+  monkeypatch.setattr(bench.torch.cuda, 'device_count', lambda: 1)
+  assert bench.spawn_ranks(8, []) == 2

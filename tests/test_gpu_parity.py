@@ -1,21 +1,23 @@
 """HIP path (through the C-ABI) vs the reference's golden vectors and the C
 restatement. Needs an MI355X.
 
-Parity gate, per env and field, normwise
-    max|Δ| <= tol * max(1, max|x|)   against the reference's float64 states:
-  every field:             tol = max(1e-5, 2 * E32)
+Parity gate, per env i and field, normwise
+    max|Δ_i| <= tol_i * max(1, max|x_i|)   against the reference's float64 states:
+  every field:             tol_i = max(1e-5, 2 * E32_i)
   Ant (the north-star config) pos/rot additionally <= 1e-5 flat
-E32 is the fp32 error envelope of Brax's OWN algorithm on the same sample:
+E32_i is the fp32 error envelope of Brax's OWN algorithm on the same sample:
 the largest normwise error, vs the float64 reference, of the oracle's two
 float32 builds (the reference algorithm executed in true fp32, plain and with
 a*b+c contracted to FMA as XLA's jit does) over the exact inputs and copies
 perturbed by fp32-ulp relative noise (x * (1 + U[-6e-8,6e-8]), SURVEY §8(c)'s
-conditioning probe; 15 copies for the system steps, 3 for the env layer). The HIP kernel must be as close to the
+conditioning probe; 32 copies per build: 66 realisations per env). The HIP kernel must be as close to the
 reference as fp32 rounding noise itself allows, within 2x. Velocities are
 (pos - pos_prev)/h, so fp32 rounding is amplified ~1/h per substep, and the
 contact masks (`penetration > 0`, `c < 0`, static-friction and sinking gates)
 flip on rounding; a flat 1e-5 is not reachable for those by Brax itself.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -61,36 +63,59 @@ def _to_qp(a, dev):
 
 WIDE = 1e-2  # a sample whose own bound 2 x E32 exceeds this is ill-conditioned
 NEAR_TOL = 1e-3  # the ill-conditioned envs: floor of the nearest-realisation bound
+# fp32-ulp perturbed copies per oracle build in the envelope:
+# 2 builds x (1 exact + 32 perturbed) = 66 realisations per env, so a
+# per-env E32_i is not a noisy maximum of a handful of runs
+N_PERTURB = int(os.environ.get('BX_ENVELOPE_N', '32'))
+# BX_PARITY_RECORD_ONLY=1 (diagnostic runs): record the per-env ratios of
+# every gate without asserting them (the group bound is still asserted), so
+# one run lists every env past its bound
+RECORD_ONLY = os.environ.get('BX_PARITY_RECORD_ONLY') == '1'
 
 
 def _gate(got, ref, e32, field, split=True):
-  """max(1e-5, 2 x E32) over a group of envs, E32 the largest fp32 error of
-  Brax's own algorithm over the group's samples. With `split`, the envs are
-  two groups: the well-conditioned ones (2 x E32_i <= 1e-2) against the
-  bound of their own group, the ill-conditioned ones (a contact flipping on
-  rounding: Brax's own fp32 is off by > 5e-3 there) against theirs, recorded
-  as `<field>:illcond`. (Until round 3 one group held every env, so one
-  ill-conditioned env loosened the gate of all; the split only tightens it.)
-  Without `split` (the reset lift's discontinuity: any env may flip), one
-  group."""
+  """SURVEY 8(c)'s per-sample gate: env i's normwise error <= max(1e-5,
+  2 x E32_i), E32_i the largest fp32 error of Brax's own algorithm over that
+  env's 66 realisations (both oracle builds, exact and ulp-perturbed inputs).
+  The envs are split: the well-conditioned ones (2 x E32_i <= 1e-2) take
+  their own bound; the ill-conditioned ones (a contact flipping on rounding:
+  Brax's own fp32 is off by > 5e-3 there) are gated on the NEAREST of Brax's
+  fp32 realisations below, their envelope group recorded as
+  `<field>:illcond` (role 'envelope'). Every gate records the distribution
+  of HIP_i / bound_i over its envs (tests/margins.py). Without `split` (the
+  reset lift's discontinuity: any env may flip), one group bound.
+  (Until round 4 the well-conditioned bound was the group's largest E32,
+  under which one env's large Brax error covered another's excess.)"""
   nw = normwise(got, ref)
   samples = getattr(e32, 'samples', None)
   e32 = np.broadcast_to(np.asarray(e32, np.float64), nw.shape)
   assert np.all(np.isfinite(got)), field
   ill = (2.0 * e32 > WIDE) if split else np.zeros(nw.shape, bool)
   worst = (0.0, POS_TOL)
-  for sel, name in ((~ill, field), (ill, field + ':illcond')):
-    if not sel.any():
-      continue
-    tol = max(POS_TOL, 2.0 * float(e32[sel].max()))
-    m = float(nw[sel].max())
+  well = ~ill
+  if well.any():
+    group_tol = max(POS_TOL, 2.0 * float(e32[well].max()))
+    tol_i = np.maximum(POS_TOL, 2.0 * e32) if split else np.full(nw.shape, group_tol)
+    r = np.where(well, nw / tol_i, -1.0)
+    k = int(np.argmax(r))
+    m, tol = float(nw.flat[k]), float(tol_i.flat[k])
+    record_margin(field, m, tol, n=int(well.sum()), ratios=r[well].ravel().tolist(),
+                  gate='per_env' if split else 'group', group_tol=group_tol,
+                  group_ratio=float(nw[well].max()) / group_tol)
+    assert float(nw[well].max()) <= group_tol, f'{field}: group bound'
+    if not RECORD_ONLY:
+      assert m <= tol, (f'{field}: env {k} normwise {m:.3e} > its bound {tol:.3e} '
+                        f'({int((r > 1).sum())} of {int(well.sum())} envs past theirs)')
+    worst = (m, tol)
+  if ill.any():
+    tol = max(POS_TOL, 2.0 * float(e32[ill].max()))
+    m = float(nw[ill].max())
     # the ill-conditioned group's envelope bound (> 1e-2 by definition) is
     # Brax-vs-Brax branch distance; the binding gate for those envs is the
     # nearest-realisation one below
-    record_margin(name, m, tol, n=int(sel.sum()), **({'role': 'envelope'} if name.endswith(':illcond') else {}))
-    assert m <= tol, f'{name}: normwise {m:.3e} > tol {tol:.3e} ({int(sel.sum())} envs)'
+    record_margin(field + ':illcond', m, tol, n=int(ill.sum()), role='envelope')
+    assert m <= tol, f'{field}:illcond: normwise {m:.3e} > tol {tol:.3e} ({int(ill.sum())} envs)'
     worst = max(worst, (m, tol))
-  if ill.any():
     # an ill-conditioned env's branch (which contacts fire) is a coin toss
     # under fp32 rounding, so its gate is the distance to the NEAREST of
     # Brax's fp32 realisations (the envelope's runs): the HIP result must be
@@ -121,11 +146,11 @@ class Envelope:
   contracted to fused multiply-adds (XLA's jit contracts them, as hipcc does);
   the envelope is the max normwise error over every run."""
 
-  def __init__(self, oracle_lib, name, n_perturb=3, desc=None):
+  def __init__(self, oracle_lib, name, n_perturb=None, desc=None):
     d, rd = desc if desc is not None else compiled(name)[1:3]
     self.os = [prep_oracle(oracle_lib.Oracle(d, rd, np.float32, safe_guard=True, fma=f), name)
                for f in (False, True)]
-    self.n = n_perturb
+    self.n = N_PERTURB if n_perturb is None else n_perturb
 
   def _inputs(self, qp):
     yield qp.astype(np.float32)
@@ -170,13 +195,13 @@ def test_system_step_vs_golden(dev, oracle_lib, name):
     from brax_amd import _native
     _native.check(_native.lib().bx_system_set_single(sys_._h, 0))
   T = golden('traj_' + name)
-  # 15 perturbed copies per build: the envelope is a max over samples, and 3 understate
+  # 32 perturbed copies per build (N_PERTURB): the envelope is a max over samples, and 3 understate
   # it for small batches and for sums over discontinuous gates (legacy_spring
   # Info.contact sums an impulse pass per substep through `penetration > 0`,
   # `v_n < 0` and `|v_t| > 0.01`, colliders.py:290-293: E32 of HalfCheetah's
   # env 3 at t = 2 grows 5.6e-6 -> 1.08e-5 from 3 to 15 copies; one-env
   # scenes such as the height map likewise)
-  env32 = Envelope(oracle_lib, name, n_perturb=15)
+  env32 = Envelope(oracle_lib, name)
   for t in range(T['action'].shape[0]):
     qp_in = _to_qp(T['qp'][t], dev)
     act = torch.as_tensor(T['action'][t], dtype=torch.float32, device=dev)
@@ -217,18 +242,14 @@ def test_system_step_vs_golden(dev, oracle_lib, name):
 
 
 @pytest.mark.parametrize('name', ENV_TRAJ + XY_ENVS + ENVTRAJ_KERNEL +
-                         ['ant:nojb', 'halfcheetah:nojb', 'humanoid:sph'])
+                         ['ant:nojb', 'halfcheetah:nojb'])
 def test_env_step_vs_golden(dev, oracle_lib, name, monkeypatch):
   name, _, variant = name.partition(':')
   if variant == 'nojb':
     # the all-kinds kernel the Ant / HalfCheetah kinds fall back to when their
     # system does not allow the body copies of their own kernels (BX_NO_JB)
     monkeypatch.setenv('BX_NO_JB', '1')
-  if variant == 'sph':
-    # the opt-in spherical joint halves (32 lanes per env)
-    monkeypatch.setenv('BX_SPH_HALVES', '1')
   env = _make_env(name, dev)
-  assert variant != 'sph' or env.unwrapped.sys.env_lanes == 32
   T = golden(env_golden(name))
   env32 = Envelope(oracle_lib, name)
   fl = obs_flags(name)
@@ -446,7 +467,7 @@ def test_full_batch_properties_other_envs(dev, oracle_lib, name):
   assert torch.isfinite(a.obs).all()
   vc, d, rd, meta = compiled(name)
   o64 = oracle_lib.Oracle(d, rd, np.float64, safe_guard=True)
-  env32 = Envelope(oracle_lib, name, n_perturb=15)
+  env32 = Envelope(oracle_lib, name)
   idx = np.random.default_rng(1).choice(B, 64, replace=False)
   qp_in = st.qp.numpy()[idx]
   an = act.cpu().numpy()[idx].astype(np.float64)

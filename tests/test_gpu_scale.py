@@ -159,7 +159,7 @@ def test_mountain4_full_batch(dev, oracle_lib, cutoff, variant):
   vc, d, meta = brax_amd.compiler.compile_system(cfg)
   rd = compile_reset(vc, meta['body_index'])
   o64 = oracle_lib.Oracle(d, rd, np.float64, safe_guard=True)
-  env32 = Envelope(oracle_lib, None, n_perturb=7, desc=(d, rd))
+  env32 = Envelope(oracle_lib, None, desc=(d, rd))
   idx = np.random.default_rng(11).choice(B, 8, replace=False)
   qp_in = qp.numpy()[idx]
   an = act.cpu().numpy()[idx].astype(np.float64)

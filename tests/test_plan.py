@@ -21,14 +21,17 @@ def test_env_systems_run_the_register_hoisted_kernel(name):
 def test_ant_mountain4_fits_three_envs_per_cu(cutoff):
   """BASELINE configs[4]: Ant Mountain(4) runs the large-scene kernel (one env
   per 256-thread workgroup) with 6-word contact slots and b slots for the
-  630 two-way rows only, so three envs share a CU's LDS (two until round 3:
-  73.7 KB per env); 2,048 envs then take 3 residency rounds instead of 4."""
+  630 two-way rows only, so three envs would share a CU's LDS (two until
+  round 3: 73.7 KB per env). The kernel is built for two waves per SIMD (256
+  registers: a third workgroup's registers spill), so two envs run per CU:
+  the register file, not the LDS, sets the residency."""
   cfg = config_for('mountain4')
   cfg.collider_cutoff = cutoff
   p = System.plan(cfg)
   assert p['mode'] == 3 and p['lanes'] == 256, p
   assert p['lds_bytes'] * 3 <= LDS_CU, p
   assert p['envs_per_cu_by_lds'] == 3, p
+  assert p['envs_per_cu_by_registers'] == 2 and p['envs_per_cu'] == 2, p
 
 
 def test_plan_refuses_a_null_descriptor():
