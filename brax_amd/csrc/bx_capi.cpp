@@ -36,6 +36,22 @@ uint32_t fbits(double x) {
   return u;
 }
 
+// a joint limit l (radians, as the record holds it in float) as the kernels
+// test it (pbd_layout.h LL_*): its pseudo-angle (pbd_math.h pseudo_angle, a
+// monotone stand-in for atan2 over (-pi, pi]; +-3 at or past +-pi, where no
+// angle is out of range) and its cosine / sine, in double
+void limit_trig(float lf, double* p, double* c, double* s) {
+  const double l = lf;
+  *c = std::cos(l);
+  *s = std::sin(l);
+  if (l <= -M_PI) *p = -3.0;
+  else if (l >= M_PI) *p = 3.0;
+  else {
+    const double r = std::fabs(*c) + std::fabs(*s), t = r > 0 ? *c / r : 1.0;
+    *p = *s >= 0 ? 1.0 - t : t - 1.0;
+  }
+}
+
 }  // namespace
 
 struct bx_system {
@@ -227,6 +243,19 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       B.f(o + J_AXC + k, d->joint_axis_c[9 * j + k]);
     }
     for (int k = 0; k < 6; k++) B.f(o + J_LIM + k, d->joint_limit[6 * j + k]);
+    // the limit rows' pseudo-angles and cos / sin (J_JLIM, LL_*), from the
+    // radians just stored as float
+    for (int row = 0; row < 3; row++)
+      for (int side = 0; side < 2; side++) {
+        float lf;
+        std::memcpy(&lf, &B.w[o + J_LIM + 2 * row + side], 4);
+        double p, c, sn;
+        limit_trig(lf, &p, &c, &sn);
+        const int r = o + J_JLIM + 8 * row;
+        B.f(r + (side ? LL_PHI : LL_PLO), p);
+        B.f(r + (side ? LL_CHI : LL_CLO), c);
+        B.f(r + (side ? LL_SHI : LL_SLO), sn);
+      }
     if (d->dynamics_mode == BX_DYN_LEGACY_SPRING) {
       B.f(o + J_STIFF, d->joint_stiffness[j]);
       B.f(o + J_SDAMP, d->joint_spring_damping[j]);
@@ -605,12 +634,32 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // and pass instead of record -> referenced body)
   if (H.multi && R > 0) {
     B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
-    H.o_rimg = B.alloc(32 * R);
+    H.o_rimg = B.alloc(MG_WORDS * R);
+    H.o_rphys = B.alloc(MP_WORDS * R);
     uint32_t rw[32];
     for (int x = 0; x < R; x++) {
       row_words(x, rw);
-      rw[LR_MBSLOT] = (uint32_t)mb[x];
-      for (int k = 0; k < 32; k++) B.w[H.o_rimg + ((k / 4) * R + x) * 4 + k % 4] = rw[k];
+      uint32_t g[MG_WORDS], p[MP_WORDS];
+      g[MG_AB] = (rw[LR_A] & 0xFFFFu) | (rw[LR_B] << 16);
+      g[MG_META] = (rw[LR_FN] & 0xFFu) | ((rw[LR_OW] & 0xFFu) << 8) | ((uint32_t)mb[x] << 16);
+      for (int k = 0; k < 3; k++) {
+        g[MG_APOS + k] = rw[LR_APOS + k];
+        g[MG_AEND + k] = rw[LR_AEND + k];
+        g[MG_BPOS + k] = rw[LR_BPOS + k];
+        g[MG_BEND + k] = rw[LR_BEND + k];
+        p[MP_IA + k] = rw[LR_IA + k];
+        p[MP_IB + k] = rw[LR_IB + k];
+      }
+      g[MG_ARAD] = rw[LR_ARAD];
+      g[MG_BRAD] = rw[LR_BRAD];
+      p[MP_FRIC] = rw[LR_FRIC];
+      p[MP_ELAS] = rw[LR_ELAS];
+      p[MP_SCALE] = rw[LR_SCALE];
+      p[MP_THR] = rw[LR_THR];
+      p[MP_MA] = rw[LR_MA];
+      p[MP_MB] = rw[LR_MB];
+      for (int k = 0; k < MG_WORDS; k++) B.w[H.o_rimg + ((k / 4) * R + x) * 4 + k % 4] = g[k];
+      for (int k = 0; k < MP_WORDS; k++) B.w[H.o_rphys + ((k / 4) * R + x) * 4 + k % 4] = p[k];
     }
     // broad-phase bounds (BI_*): reach = |a_end| + |b_end| + radii in double,
     // rounded up to float
@@ -702,22 +751,8 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     // from the radians the record holds, in double
     auto put_lim = [&](int lane, int base, int j, int row) {
       if (J == 0) return;
-      const uint32_t* s = &B.w[H.o_joint + j * JOINT_STRIDE];
-      for (int side = 0; side < 2; side++) {
-        float lf;
-        std::memcpy(&lf, &s[J_LIM + 2 * row + side], 4);
-        const double l = lf, c = std::cos(l), sn = std::sin(l);
-        double p;
-        if (l <= -M_PI) p = -3.0;
-        else if (l >= M_PI) p = 3.0;
-        else {
-          const double r = std::fabs(c) + std::fabs(sn), t = r > 0 ? c / r : 1.0;
-          p = sn >= 0 ? 1.0 - t : t - 1.0;
-        }
-        put(lane, base + (side ? LL_PHI : LL_PLO), fbits(p));
-        put(lane, base + (side ? LL_CHI : LL_CLO), fbits(c));
-        put(lane, base + (side ? LL_SHI : LL_SLO), fbits(sn));
-      }
+      const uint32_t* s = &B.w[H.o_joint + j * JOINT_STRIDE + J_JLIM + 8 * row];
+      for (int k = 0; k < 6; k++) put(lane, base + k, s[k]);
     };
     auto put_act = [&](int lane, int base, int a) {
       if (K == 0) return;

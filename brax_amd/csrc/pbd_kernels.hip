@@ -323,15 +323,27 @@ __device__ __forceinline__ float2 ld_lim_p(const uint4* li, int g) {
 __device__ __forceinline__ constexpr int lim_group(int l) {
   return l == 0 ? LIM_G0 : (l == 1 ? LIM_G1 : LIM_G2);
 }
+// limit row `row` of a joint from its record (J_JLIM: the item-loop kernels)
+__device__ __forceinline__ JLim rec_lim(const uint32_t* jrec, int row) {
+  const uint32_t* r = jrec + J_JLIM + 8 * row;
+  return JLim{__uint_as_float(r[LL_PLO]), __uint_as_float(r[LL_PHI]), __uint_as_float(r[LL_CLO]),
+              __uint_as_float(r[LL_SLO]), __uint_as_float(r[LL_CHI]), __uint_as_float(r[LL_SHI])};
+}
 
 // JL: the hoisted kernels' limit row (pseudo-angles, cos / sin): the
 // revolute hinge turn without atan2 / sincos; LI (no JL): the lane image
 // whose limit rows the revolute and spherical limits read the same way;
-// neither: the reference's formulas
+// JREC (the item-loop kernels): the joint's record, whose J_JLIM rows they
+// read the same way; none: the reference's formulas (the MULTI kernel).
+// The atan2-free forms are also the more accurate: (cos, sin) of the hinge
+// angle straight from (x, y) / |(x, y)|, where atan2, the half-angle sincos
+// and the quaternion turn each add their ulps (the item-loop kernels' hinge
+// ran 1.3-1.7x Brax's own per-env fp32 error on Acrobot / Reacher / the
+// double pendulum before, tests/test_gpu_parity.py per-env gate)
 template <int F, int LS = 16>
 __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const QP& c, v3& dpp, q4& dpr,
                             v3& dcp, q4& dcr, bool useJL = false, JLim JL = JLim{},
-                            const uint4* LI = nullptr) {
+                            const uint4* LI = nullptr, const uint32_t* JREC = nullptr) {
   // each body rotates three or four of the joint's vectors: one matrix each
   BX_IEEE_IN_JOINT
   // in the SINGLE-mode TU (the item-loop / MULTI kernels keep rotate():
@@ -374,6 +386,8 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
       n1 = hinge_turn(axis, ref_p, ref_c, JL);
     } else if (LI) {
       n1 = hinge_turn(axis, ref_p, ref_c, ld_lim<LS>(LI, LIM_G0));
+    } else if (JREC) {
+      n1 = hinge_turn(axis, ref_p, ref_c, rec_lim(JREC, 0));
     } else {
       float psi = signed_angle(axis, ref_p, ref_c);
       float ph = clampf(psi, J.lim[0], J.lim[1]);
@@ -397,11 +411,11 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
     v3 n2v[3] = {lon, xz, a2c};
 #pragma unroll
     for (int l = 0; l < 3; l++) {
-      if (LI) {
+      if (LI || JREC) {
         // limit_angle on pseudo-angles: inside the limits the row's impulse
         // is zero whatever the angle, outside n1 is turned by the limit's
         // own (cos, sin); neither atan2 nor sincos
-        const JLim L = ld_lim<LS>(LI, lim_group(l));
+        const JLim L = LI ? ld_lim<LS>(LI, lim_group(l)) : rec_lim(JREC, l);
         const float y = dot(cross(n1v[l], n2v[l]), nv[l]), x = dot(n1v[l], n2v[l]);
         const float pa = pseudo_angle(x, y);
         const bool below = pa < L.plo, above = pa > L.phi;
@@ -440,11 +454,16 @@ __device__ __forceinline__ int axis_angle(const JointC& J, const QP& p, const QP
   }
   v3 a1p = rotate(J.axp[0], p.rot), a2p = rotate(J.axp[1], p.rot);
   v3 a1c = rotate(J.axc[0], c.rot), a2c = rotate(J.axc[1], c.rot), a3c = rotate(J.axc[2], c.rot);
+  // (the normalisations' quotients correctly rounded, ndiv3: theta =
+  // acos(cb) near cb = 1 turns the fast reciprocal's extra ulp in xz into
+  // 1e-5-scale angle errors, which legacy_spring Grasp's stiff Angle
+  // actuators and limit springs on its 2-dof thumb joints carried to 2.3x
+  // Brax's own fp32 error, tests/test_gpu_parity.py per-env gate)
   v3 lon = cross(a3c, a1p);
-  lon = lon / (1e-10f + safe_norm(lon));
+  lon = ndiv3(lon, 1e-10f + safe_norm(lon));
   float psi = signed_angle(a1p, a2p, lon);
   v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
-  xz = xz / (1e-10f + safe_norm(xz));
+  xz = ndiv3(xz, 1e-10f + safe_norm(xz));
   float cb = dot(xz, a1p);
   float theta = acosf(clampf(cb, -1.f, 1.f)) * signf(dot(a1p, a3c));
   float phi = signed_angle(-a3c, a2c, lon);
@@ -472,6 +491,7 @@ __device__ __forceinline__ SpringC load_spring(const Cst& c, const BlobHdr& H, i
 __device__ __forceinline__ void spring_joint_apply(const JointC& J, const SpringC& S, const QP& p,
                                                    const QP& c, v3& dvp, v3& dap, v3& dvc,
                                                    v3& dac) {
+  BX_IEEE_IN_SPRING
   // QP.to_world (base.py:110-124)
   v3 op = rotate(J.off_p, p.rot), oc = rotate(J.off_c, c.rot);
   v3 pos_p = p.pos + op, vel_p = p.vel + cross(p.ang, op);
@@ -1203,6 +1223,7 @@ __device__ __forceinline__ void velocity_contact(const RowC& R, float h, const Q
 template <int F>
 __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos, v3 cvel, v3 n,
                                 float cpen, v3& oav, v3& oaa, v3& obv, v3& oba) {
+  BX_IEEE_IN_SPRING
   v3 rpa = cpos - a.pos, rpb = cpos - b.pos;
   float bv = R.erp * cpen;
   float nv = dot(n, cvel);
@@ -1313,7 +1334,7 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
         if (ang[l] < Jc.lim[2 * l]) t = 0.f;
         if (ang[l] > Jc.lim[2 * l + 1]) t = 0.f;
       } else {
-        float tgt = clampf(al[l] * 3.14159265358979323846f / 180.f, Jc.lim[2 * l], Jc.lim[2 * l + 1]);
+        float tgt = clampf(deg_to_rad(al[l]), Jc.lim[2 * l], Jc.lim[2 * l + 1]);
         t = (tgt - ang[l]) * A.strength;
       }
       tq = tq + axes[l] * t;
@@ -1414,7 +1435,7 @@ __device__ __forceinline__ void act_torque_half(const JointC& Jc, const JLim& JL
     if (pa > JL.phi) t = 0.f;
   } else {
     float ang = signed_angle(axis, ref_p, ref_c);
-    float tgt = clampf(al[0] * 3.14159265358979323846f / 180.f, Jc.lim[0], Jc.lim[1]);
+    float tgt = clampf(deg_to_rad(al[0]), Jc.lim[0], Jc.lim[1]);
     t = (tgt - ang) * A.strength;
   }
   v3 tq = mk(0.f, 0.f, 0.f) + axis * t;
@@ -1506,7 +1527,7 @@ __device__ __forceinline__ void esync() {
 __device__ __forceinline__ void zero_row_slots(const Cst& c, const BlobHdr& H, const Env& E, int r) {
   if (E.tslot) {
     float* sa = E.cslot + r * MSLOT_STRIDE;
-    const int b = c.i(H.o_rimg + ((LR_MBSLOT / 4) * H.R + r) * 4 + LR_MBSLOT % 4);
+    const int b = (int)((uint32_t)c.i(H.o_rimg + ((MG_META / 4) * H.R + r) * 4 + MG_META % 4) >> 16);
     float* sb = E.cslot + b * MSLOT_STRIDE;
     for (int k = 0; k < MSLOT_STRIDE; k++) { sa[k] = 0.f; sb[k] = 0.f; }
     return;
@@ -1848,7 +1869,8 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), q = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
         q4 dpr, dcr;
-        joint_apply<F>(Jc, p, q, dpp, dpr, dcp, dcr);
+        joint_apply<F>(Jc, p, q, dpp, dpr, dcp, dcr, false, JLim{}, nullptr,
+                       c.w + H.o_joint + j * JOINT_STRIDE);
         float* sp = E.jslot + j * SLOT_STRIDE;
         float* sc = E.jslot + (E.nJ + j) * SLOT_STRIDE;
         st3(sp, dpp); st4(sp + 3, dpr);
@@ -2034,6 +2056,7 @@ __device__ void impulse_rows(const Cst& c, const BlobHdr& H, const Env& E, int l
 // and divided by (eps + #non-zero rows), groups added in order
 __device__ __forceinline__ void contact_reduce(const Cst& c, const BlobHdr& H, const Env& E, int b,
                                                float eps, v3& dv, v3& da) {
+  BX_IEEE_IN_SPRING
   dv = mk(0.f, 0.f, 0.f);
   da = mk(0.f, 0.f, 0.f);
   int i = c.i(H.o_cl_off + b), e = c.i(H.o_cl_off + b + 1);
@@ -2412,18 +2435,14 @@ __device__ __forceinline__ void gsum_contact(const GList<M>& g, const float* csl
 
 // Euler.velocity_projection (integrators.py:122-146) on one body
 __device__ __forceinline__ void vproj(QP& q, v3 ppos, q4 prot, const BodyC& B, float h,
-                                      bool bare = false) {
+                                      bool bare = false, bool fast = false) {
   BX_IEEE_IN_BODY
-  q4 nr = bare ? qnormalize_bare(q.rot) : qnormalize(q.rot);
+  q4 nr = bare ? qnormalize_bare(q.rot) : qnormalize(q.rot, fast);
   // (the quotients by h Newton-corrected, as qnormalize's; the Ant env
   // kernel's bare path keeps the fast ones: its 1 / h = 200 is exact)
-  // (the SINGLE-mode TU's non-bare path: Newton-corrected quotients, pbd_math.h
-  // qnormalize)
-#if defined(BX_TU_FAST)
-  const bool nd = !bare;
-#else
-  const bool nd = false;
-#endif
+  // (every non-bare path, both translation units: Newton-corrected
+  // quotients, pbd_math.h qnormalize)
+  const bool nd = !bare && !fast;  // (fast: the MULTI kernel, pbd_math.h qnormalize)
   q.vel = mul(nd ? ndiv3(q.pos - ppos, h) : (q.pos - ppos) / h, B.pm);
   q4 dq = quat_mul(nr, quat_inv(prot));
   v3 a = nd ? ndiv3(2.f * mk(dq.x, dq.y, dq.z), h) : 2.f * mk(dq.x, dq.y, dq.z) / h;
@@ -2445,9 +2464,11 @@ __device__ unsigned long long bx_stamp_wave[4096][16];
     st_acc[k] += _t - st_last;                                                     \
     st_last = _t;                                                                  \
   } while (0)
-// kernel-level stamps (env_step_kernel): slots 10..14
+// kernel-level stamps (env_step_kernel): slots 10..14; with BX_PSTAMPS the
+// prologue's parts too (slots 5..9, BX_KSTAMP(5..9); the pbd phases' slots
+// 0..9 are then not written)
 #define BX_KSTAMP_DECL                                                             \
-  unsigned long long kst_last, kst_acc[5] = {0, 0, 0, 0, 0};                       \
+  unsigned long long kst_last, kst_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};       \
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(kst_last)::"memory");
 #define BX_KSTAMP(k)                                                               \
   do {                                                                             \
@@ -2455,11 +2476,18 @@ __device__ unsigned long long bx_stamp_wave[4096][16];
     unsigned long long _t;                                                         \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
     __builtin_amdgcn_sched_barrier(0);                                             \
-    kst_acc[(k) - 10] += _t - kst_last;                                            \
+    kst_acc[(k) - 5] += _t - kst_last;                                             \
     kst_last = _t;                                                                 \
     if ((k) == 14 && threadIdx.x == 0)                                             \
-      for (int _i = 0; _i < 5; _i++) bx_stamp_wave[blockIdx.x & 4095][10 + _i] += kst_acc[_i]; \
+      for (int _i = BX_KSLOT0; _i < 10; _i++) bx_stamp_wave[blockIdx.x & 4095][5 + _i] += kst_acc[_i]; \
   } while (0)
+#if defined(BX_PSTAMPS)
+#define BX_KSLOT0 0
+#define BX_PSTAMP(k) BX_KSTAMP(k)
+#else
+#define BX_KSLOT0 5
+#define BX_PSTAMP(k) do {} while (0)
+#endif
 #elif defined(BX_PHASE_MARKS)
 // static per-phase instruction mix (diagnostic, tools/phase_mix.py): the
 // stamp points as assembly comments the scheduler does not move code across
@@ -2471,10 +2499,12 @@ __device__ unsigned long long bx_stamp_wave[4096][16];
   } while (0)
 #define BX_KSTAMP_DECL
 #define BX_KSTAMP(k) BX_STAMP(k)
+#define BX_PSTAMP(k) do {} while (0)
 #else
 #define BX_STAMP(k) do {} while (0)
 #define BX_KSTAMP_DECL
 #define BX_KSTAMP(k) do {} while (0)
+#define BX_PSTAMP(k) do {} while (0)
 #endif
 
 // FOLD (the Ant / Humanoid / HalfCheetah env kernels; the host checks that every joint j
@@ -2812,8 +2842,10 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   BX_STAMP(9);
 #ifdef BX_STAMPS
   if (threadIdx.x == 0) {
+#if !defined(BX_PSTAMPS)
 #pragma unroll
     for (int k = 0; k < 10; k++) bx_stamp_wave[blockIdx.x & 4095][k] += st_acc[k];
+#endif
     bx_stamp_wave[blockIdx.x & 4095][15] += 1ull;
   }
 #endif
@@ -2849,46 +2881,43 @@ struct HoistM {
 // hides those loads. Measured (Ant Mountain(4), 2048 envs, rows per lane 3):
 // 0.44 ms per step, against 0.68 ms with the rows hoisted into registers
 // (BX_MULTI_HOIST_ROWS: 256 VGPRs + 78 AGPRs, one wave per SIMD).
-// row r's constants from the MULTI row image (bx_capi.cpp): eight
-// independent 16-byte loads, consecutive rows' groups adjacent
-__device__ __forceinline__ RowC load_row_img(const Cst& c, const BlobHdr& H, int r) {
+// row r's geometry from the MULTI row image (bx_capi.cpp, pbd_layout.h MG_*):
+// four independent 16-byte loads, consecutive rows' groups adjacent; what
+// contact_gen reads and the slot word. The impulse constants (MP_*, three
+// loads) complete the record for the position pass; the velocity pass reads
+// neither part for a row that does not penetrate (it stores exact zeros from
+// the slot word the position pass kept). 7 loads per near row and pass where
+// the 32-word record took 8 on both passes
+__device__ __forceinline__ RowC load_row_geo(const Cst& c, const BlobHdr& H, int r) {
   const uint4* im = reinterpret_cast<const uint4*>(c.w + H.o_rimg) + r;
-  uint32_t w[32];
-#pragma unroll
-  for (int g = 0; g < 8; g++) {
-    const uint4 v = im[g * H.R];
-    w[4 * g] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
-  }
-  auto f = [&](int i) { return __uint_as_float(w[i]); };
-  auto f3 = [&](int i) { return mk(f(i), f(i + 1), f(i + 2)); };
+  const uint4 g0 = im[0], g1 = im[H.R], g2 = im[2 * H.R], g3 = im[3 * H.R];
   RowC x;
-  x.group = (int)w[LR_GROUP];
-  x.a = (int)w[LR_A];
-  x.b = (int)w[LR_B];
-  x.fn = (int)w[LR_FN];
-  x.oneway = (int)w[LR_OW];
-  x.a_pos = f3(LR_APOS);
-  x.a_end = f3(LR_AEND);
-  x.a_rad = f(LR_ARAD);
-  x.b_pos = f3(LR_BPOS);
-  x.b_end = f3(LR_BEND);
-  x.b_rad = f(LR_BRAD);
-  x.fric = f(LR_FRIC);
-  x.elas = f(LR_ELAS);
-  x.scale = f(LR_SCALE);
-  x.thr = f(LR_THR);
-  x.bslot = (int)w[LR_MBSLOT];  // (the MULTI image carries no erp)
-  x.ma = f(LR_MA);
-  x.mb = f(LR_MB);
-  x.Ia = f3(LR_IA);
-  x.Ib = f3(LR_IB);
+  x.group = 0;  // (no MULTI pass reads the group)
+  x.a = (int)(g0.x & 0xFFFFu);
+  x.b = (int)(g0.x >> 16);
+  x.fn = (int)(g0.y & 0xFFu);
+  x.oneway = (int)((g0.y >> 8) & 0xFFu);
+  x.bslot = (int)(g0.y >> 16);  // (the MULTI image carries no erp)
+  x.a_pos = mk(__uint_as_float(g0.z), __uint_as_float(g0.w), __uint_as_float(g1.x));
+  x.a_end = mk(__uint_as_float(g1.y), __uint_as_float(g1.z), __uint_as_float(g1.w));
+  x.a_rad = __uint_as_float(g2.x);
+  x.b_pos = mk(__uint_as_float(g2.y), __uint_as_float(g2.z), __uint_as_float(g2.w));
+  x.b_end = mk(__uint_as_float(g3.x), __uint_as_float(g3.y), __uint_as_float(g3.z));
+  x.b_rad = __uint_as_float(g3.w);
   return x;
 }
-#if defined(BX_MULTI_HOIST_ROWS)
-#define BX_MULTI_ROW(R, m, r) const RowC& R = X.R[m]
-#else
-#define BX_MULTI_ROW(R, m, r) const RowC R = load_row_img(c, H, r)
-#endif
+__device__ __forceinline__ void load_row_phys(const Cst& c, const BlobHdr& H, int r, RowC& x) {
+  const uint4* im = reinterpret_cast<const uint4*>(c.w + H.o_rphys) + r;
+  const uint4 p0 = im[0], p1 = im[H.R], p2 = im[2 * H.R];
+  x.fric = __uint_as_float(p0.x);
+  x.elas = __uint_as_float(p0.y);
+  x.scale = __uint_as_float(p0.z);
+  x.thr = __uint_as_float(p0.w);
+  x.ma = __uint_as_float(p1.x);
+  x.mb = __uint_as_float(p1.y);
+  x.Ia = mk(__uint_as_float(p1.z), __uint_as_float(p1.w), __uint_as_float(p2.x));
+  x.Ib = mk(__uint_as_float(p2.y), __uint_as_float(p2.z), __uint_as_float(p2.w));
+}
 
 template <int L, int MR>
 __device__ __forceinline__ void load_hoist_multi(const Cst& c, const BlobHdr& H, int lane,
@@ -2913,7 +2942,7 @@ __device__ __forceinline__ void load_hoist_multi(const Cst& c, const BlobHdr& H,
     const int r = lane + m * L;
     const int rr = r < H.R ? r : 0;
     X.R[m] = load_row(c, H, rr);
-    X.R[m].bslot = c.i(H.o_rimg + ((LR_MBSLOT / 4) * H.R + rr) * 4 + LR_MBSLOT % 4);
+    X.R[m].bslot = (int)((uint32_t)c.i(H.o_rimg + ((MG_META / 4) * H.R + rr) * 4 + MG_META % 4) >> 16);
   }
 #endif
 }
@@ -3051,15 +3080,18 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
 #define BX_MULTI_RX(x) (H.n_nn ? E.alist[x] : (x))
 #define BX_MULTI_SKIP(x, r) ((x) >= nact)
 #endif
-  // the row's contact between the position and velocity passes
+  // the row's contact between the position and velocity passes, and its
+  // slot word (one-way flag, b-side slot) for the velocity pass's stores
   v3 cpos[MR], cn[MR];
   float pen[MR], dl[MR];
+  int meta[MR];
 #pragma unroll
   for (int m = 0; m < MR; m++) {
     cpos[m] = mk(0.f, 0.f, 0.f);
     cn[m] = mk(0.f, 0.f, 0.f);
     pen[m] = 0.f;
     dl[m] = 0.f;
+    meta[m] = 0;
   }
   for (int it = 0; it < H.substeps / 2; it++) {
     v3 ppos = q.pos;
@@ -3101,7 +3133,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
         v3 am = mul(q.ang, X.B.rm);
         q4 hq = (q4{0.f, am.x, am.y, am.z} * 0.5f) * h;
         q4 r = q.rot + quat_mul(hq, q.rot);
-        q.rot = qnormalize(r);
+        q.rot = qnormalize(r, true);
         stqp(myqp, q);
         dpa_last = dpa;
       }
@@ -3135,7 +3167,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
         q.pos = q.pos + mul(dp, X.B.pm);
         q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                    q.rot.z + dr.z * X.B.qm.z};
-        if (sub == 0) vproj(q, ppos, prot, X.B, h);
+        if (sub == 0) vproj(q, ppos, prot, X.B, h, false, true);
         stqp(myqp, q);
       }
       esync<L>();
@@ -3219,10 +3251,19 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       const int x = lane + m * L;
       const int r = x < nwork ? (bph ? E.nearl[x] : BX_MULTI_RX(x)) : 0;
       if (bph ? x >= nwork : BX_MULTI_SKIP(x, r)) continue;
-      BX_MULTI_ROW(R, m, r);
+#if defined(BX_MULTI_HOIST_ROWS)
+      const RowC& R = X.R[m];
+#else
+      // (both parts issued together: the impulse constants loaded behind
+      // contact_gen, for penetrating rows only, exposed their latency there
+      // and measured 1.5 % slower)
+      RowC R = load_row_geo(c, H, r);
+      load_row_phys(c, H, r, R);
+#endif
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cvel;
       contact_gen<F>(R, a, b, cpos[m], cvel, cn[m], pen[m]);
+      meta[m] = (R.oneway & 0xFF) | (R.bslot << 16);
       v3 pap, pbp;
       q4 par, pbr;
       float unused;
@@ -3234,9 +3275,10 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       v3 oap = mk(0.f, 0.f, 0.f), obp = mk(0.f, 0.f, 0.f);
       q4 oar{0.f, 0.f, 0.f, 0.f}, obr{0.f, 0.f, 0.f, 0.f};
       dl[m] = 0.f;
-      if (pen[m] > 0.f)
+      if (pen[m] > 0.f) {
         dl[m] = position_contact<F, true>(R, a, b, pap, par, pbp, pbr, cpos[m], cn[m], pen[m], oap,
                                           oar, obp, obr);
+      }
       st_mslot(E.cslot + r * MSLOT_STRIDE, oap, mk(oar.x, oar.y, oar.z));
       if (!is_oneway<F>(R.oneway))
         st_mslot(E.cslot + R.bslot * MSLOT_STRIDE, obp, mk(obr.x, obr.y, obr.z));
@@ -3255,7 +3297,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       q.rot = q4{q.rot.w + dr.w * X.B.qm.w, q.rot.x + dr.x * X.B.qm.x, q.rot.y + dr.y * X.B.qm.y,
                  q.rot.z + dr.z * X.B.qm.z};
       st_rb(E.rb + lane * RB_STRIDE, q.pos, q.vel, q.ang);
-      vproj(q, ppos, prot, X.B, h);
+      vproj(q, ppos, prot, X.B, h, false, true);
       stqp(myqp, q);
     }
     esync<L>();
@@ -3266,17 +3308,25 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       const int x = lane + m * L;
       const int r = x < nwork ? (bph ? E.nearl[x] : BX_MULTI_RX(x)) : 0;
       if (bph ? x >= nwork : BX_MULTI_SKIP(x, r)) continue;
-      BX_MULTI_ROW(R, m, r);
-      QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
-      v3 rap, rav, raa, rbp, rbv, rba;
-      ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
-      ld_rb(E.rb + R.b * RB_STRIDE, rbp, rbv, rba);
+      // a row that does not penetrate stores exact zeros (sm = 0,
+      // colliders.py:584-658): no constants read, no state gathered
       v3 oav = mk(0.f, 0.f, 0.f), oaa = oav, obv = oav, oba = oav;
-      if (pen[m] > 0.f)
+      if (pen[m] > 0.f) {
+#if defined(BX_MULTI_HOIST_ROWS)
+        const RowC& R = X.R[m];
+#else
+        RowC R = load_row_geo(c, H, r);
+        load_row_phys(c, H, r, R);
+#endif
+        QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+        v3 rap, rav, raa, rbp, rbv, rba;
+        ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
+        ld_rb(E.rb + R.b * RB_STRIDE, rbp, rbv, rba);
         velocity_contact<F>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos[m], cn[m], pen[m], dl[m],
                             oav, oaa, obv, oba);
+      }
       st_mslot(E.cslot + r * MSLOT_STRIDE, oav, oaa);
-      if (!is_oneway<F>(R.oneway)) st_mslot(E.cslot + R.bslot * MSLOT_STRIDE, obv, oba);
+      if (!is_oneway<F>(meta[m] & 0xFF)) st_mslot(E.cslot + (meta[m] >> 16) * MSLOT_STRIDE, obv, oba);
     }
     esync<L>();
     BX_MSTAMP(7);
@@ -4030,6 +4080,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   const bool valid = e < A.n_envs;
   Env E = carve(ebase + le * H.env_words, H);
   zero_slots(E, H, lane);
+  BX_PSTAMP(5);
   const bx_env_params& P = A.P;
   const int kind = P.kind;
   const int aw = (int)A.act_width;
@@ -4045,6 +4096,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
                (F & F_JH) != 0 && EK != EK_ANY>(A.blob, H, lane, X);
     stage_lim<L, F>(A.blob, H, E, lane);
   }
+  BX_PSTAMP(6);
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
   float done_in = A.in.done[el];
   float steps_in = A.in.steps ? A.in.steps[el] : 0.f;
@@ -4063,6 +4115,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   const float* arow_g = drw ? nullptr : A.act + el * A.act_stride;
   float a0 = 0.f;
   if (aw > 0 && lane < C) a0 = drw ? draw_at(0, lane < aw ? lane : aw - 1) : arow_g[lane < aw ? lane : aw - 1];
+  BX_PSTAMP(7);
   if constexpr (S) {
     // N <= L: the lane's body
     float qv[13];
@@ -4082,6 +4135,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
       }
     }
   }
+  BX_PSTAMP(8);
   const int nst = A.n_steps > 1 ? A.n_steps : 1;
   for (int t = 0; t < nst; t++) {
   // (draw mode: the env programs that read the raw row are refused on the

@@ -17,11 +17,15 @@ enum {
   BODY_MASS = 0, BODY_I = 2, BODY_PM = 5, BODY_RM = 8, BODY_QM = 11,
 };
 enum {
-  JOINT_STRIDE = 48,
+  JOINT_STRIDE = 72,
   J_TYPE = 0, J_BP = 1, J_BC = 2, J_FREE = 3, J_DOF = 4, J_ANGLE_OFF = 5, J_NANGLES = 6,
   J_DAMP = 7, J_SP = 8, J_SA = 9, J_OFFP = 10, J_OFFC = 13, J_AXP = 16, J_AXC = 25, J_LIM = 34,
   // legacy_spring joints (spring_joints.py:57-67)
   J_STIFF = 40, J_SDAMP = 41, J_LSTR = 42,
+  // the three limit rows as the kernels test them (LL_*, 8 words each): the
+  // item-loop kernels' atan2-free hinge and limit rows read them here, the
+  // SINGLE kernels from the lane image (LI_JLIM, LI_JLIM12)
+  J_JLIM = 48,
 };
 enum { ACT_STRIDE = 8, A_TYPE = 0, A_JOINT = 1, A_IDX = 2, A_STR = 5 };
 // collider groups: NearNeighbors cutoff (0 = Pairs), row range, Info base
@@ -103,6 +107,7 @@ struct BlobHdr {
   int32_t l_jlim;                    // LDS (SINGLE, spherical kernels): each lane's joint limit rows
   int32_t m_zero;                    // MULTI: the zero contact slot (R + two-way rows)
   int32_t l_nearc;                   // LDS (MULTI): the broad phase's per-wave counts (16)
+  int32_t o_rphys;                   // MULTI mode: the rows' impulse constants (MP_*)
 };
 
 // SINGLE-mode lane image: for each of 64 lanes, every constant the
@@ -169,9 +174,18 @@ enum {
 // its two-way rank (LR_MBSLOT / BI_BSLOT), then one zero slot (m_zero). Task
 // partials: 8 words (the two sums, the count).
 enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 6, TSLOT_STRIDE = 8, MULTI_MR = 4 };
-// the MULTI row image's b-side slot word (the impulse model's erp, which the
-// MULTI pbd passes never read, is not carried there)
-enum { LR_MBSLOT = LR_ERP };
+// the MULTI row image, in two parts (bx_capi.cpp), 16-byte group g of row r
+// at o + (g * R + r) * 4: the geometry (MG_*, 4 groups), which every near
+// row's contact_gen reads in the position pass, and the impulse constants
+// (MP_*, 3 groups), which only a penetrating row's impulses read (its
+// position and velocity passes); a row that does not penetrate stores exact
+// zeros from its geometry's slot word alone. MG_AB: body a | body b << 16;
+// MG_META: contact function | one-way << 8 | the b side's contact slot << 16
+// (two-way rows: R + the row's two-way rank; one-way rows: the zero slot)
+enum { MG_AB = 0, MG_META = 1, MG_APOS = 2, MG_AEND = 5, MG_ARAD = 8, MG_BPOS = 9, MG_BEND = 12,
+       MG_BRAD = 15, MG_WORDS = 16 };
+enum { MP_FRIC = 0, MP_ELAS = 1, MP_SCALE = 2, MP_THR = 3, MP_MA = 4, MP_MB = 5, MP_IA = 6, MP_IB = 9,
+       MP_WORDS = 12 };
 // MULTI-mode broad phase: per row, 16-byte group g of row r at
 // o_bimg + (g * R + r) * 4: (body a, body b, reach, may_skip), (a's centre
 // offset, 0), (b's centre offset, 0). A capsule-capsule row whose capsule

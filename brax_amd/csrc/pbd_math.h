@@ -179,6 +179,12 @@ __device__ __forceinline__ v3 ndiv3(v3 a, float b) {
 #else
 #define BX_IEEE_IN_JOINT
 #endif
+// IEEE division in the legacy_spring step's impulse functions (the spring
+// joints, the impulse contacts and their (1e-8 + count) reduction), always:
+// with the build's fast reciprocal, legacy_spring Grasp ran 1.17x its per-env
+// bound (2 x Brax's own fp32 error) and 0.6x under IEEE division; its stiff
+// springs amplify the quotients' extra ulp (tests/test_gpu_parity.py)
+#define BX_IEEE_IN_SPRING _Pragma("clang fp reciprocal(off)")
 
 
 // A monotone stand-in for atan2(y, x) over (-pi, pi]: 1 - x / (|x| + |y|)
@@ -191,6 +197,16 @@ __device__ __forceinline__ float pseudo_angle(float x, float y) {
   const float r = fabsf(x) + fabsf(y);
   const float t = r > 0.f ? x / r : 1.f;
   return y >= 0.f ? 1.f - t : t - 1.f;
+}
+// the Angle actuator's target act * pi / 180 (actuators.py:75-91), divided
+// as jnp divides (correctly rounded), not through the build's fast
+// reciprocal: the quotient is the same in every fp32 realisation of Brax (no
+// state perturbation reaches it), so its extra ulp is a systematic error
+// that Brax's fp32 envelope does not cover (legacy_spring Grasp ran 1.17x
+// its per-env bound through its stiff Angle actuators)
+__device__ __forceinline__ float deg_to_rad(float a) {
+  _Pragma("clang fp reciprocal(off)")
+  return a * 3.14159265358979323846f / 180.f;
 }
 __device__ __forceinline__ float clampf(float x, float lo, float hi) {
   return x < lo ? lo : (x > hi ? hi : x);
@@ -210,22 +226,23 @@ __device__ __forceinline__ q4 qnormalize_bare(q4 r) {
 // in the body integration alone took the ratio from 2.5 to 1.0 in the A/B of
 // tools/gpu_drift_ab.sh, none in the joints, contacts, pseudo-angles or
 // constant quotients did)
-__device__ __forceinline__ q4 qnormalize(q4 r) {
+// (every kernel but the MULTI one since round 5. `fast`: the build's fast
+// quotients, the MULTI kernel's choice by measurement: on Ant Mountain its
+// per-env parity ratios are the same either way (largest 0.51 fast vs 0.50
+// Newton over 46 gates, tests/test_gpu_parity.py) and the Newton steps cost
+// it 2 % (331 vs 325 us per 2,048-env step, tools/multi_ab.sh); the item
+// loops need them: with fast quotients their per-env gate failed on legacy
+// Grasp / Swimmer and the pendulums)
+__device__ __forceinline__ q4 qnormalize(q4 r, bool fast = false) {
   BX_IEEE_IN_BODY
   float rn = sqrtf(r.w * r.w + r.x * r.x + r.y * r.y + r.z * r.z);
-#if defined(BX_TU_FAST)
+  if (fast) return {r.w / rn, r.x / rn, r.y / rn, r.z / rn};
   const float ri = __builtin_amdgcn_rcpf(rn);
   auto one = [&](float x) {
     const float q = x * ri;
     return __builtin_fmaf(__builtin_fmaf(-rn, q, x), ri, q);
   };
   return {one(r.w), one(r.x), one(r.y), one(r.z)};
-#else
-  // (the item-loop / MULTI TU keeps the build's division: its parity gates
-  // were measured on it, and the Newton form moved the item-loop inverted
-  // pendulum's ang past its 2 x E32 bound, 1.79e-5 against 1.17e-5)
-  return {r.w / rn, r.x / rn, r.y / rn, r.z / rn};
-#endif
 }
 
 }  // namespace bx

@@ -130,3 +130,22 @@ def test_step_without_info_is_the_same_state(dev, name, cutoff):
     assert info is not None and none is None
     _same(a, b)
     qp = a
+  # mid-trajectory: the golden rollout's last state per env, each copy's
+  # positions / velocities perturbed, so capsule pairs cross the broad
+  # phase's reach (in both directions) on the last collision pass, the one
+  # info=False also culls
+  from tests.conftest import golden
+  T = golden('traj_' + name)['qp'][-1]
+  rng = np.random.default_rng(5)
+  q = np.repeat(T, (B + T.shape[0] - 1) // T.shape[0], axis=0)[:B].copy()
+  q[..., 0:3] += rng.uniform(-0.02, 0.02, q[..., 0:3].shape)
+  q[..., 7:10] += rng.uniform(-0.5, 0.5, q[..., 7:10].shape)
+  q[..., 10:13] += rng.uniform(-1.0, 1.0, q[..., 10:13].shape)
+  from brax_amd.base import qp_from_numpy
+  qp = qp_from_numpy(q, dev)
+  for _ in range(6):
+    act = torch.rand((B, max(sys_.action_size, 1)), device=dev, generator=g) * 2 - 1
+    a, _ = sys_.step(qp, act)
+    b, _ = sys_.step(qp, act, info=False)
+    _same(a, b)
+    qp = a

@@ -3,9 +3,9 @@
 stepped through the C-ABI vs the golden `gym_ant` that
 `oracle/gen_golden.py:gym_ant` records from the reference's VectorGymWrapper
 (`wrappers.py:311-314`: obs, reward, done and info = {**state.metrics,
-**state.info}, every leaf, every step). Both start from the reference's
-wrapped state after reset (the reset key itself is parity-unpinned: threefry
-is absent offline). Episode length 3 puts truncation, the done-driven
+**state.info}, every leaf, every step). Every step starts from the
+reference's wrapped state before it (after reset: the reset key itself is
+parity-unpinned, threefry being absent offline). Episode length 3 puts truncation, the done-driven
 AutoReset select and the step-counter reset inside the 6 steps.
 
 Gates: the per-env envelope gate of tests/test_gpu_parity.py on obs, qp,
@@ -46,11 +46,21 @@ def test_vector_gym_step_vs_reference(dev, oracle_lib):
   assert g.num_envs == B and g.action_space.shape == (B, 8)
   assert g.single_observation_space.shape == (87,)
   f32 = lambda a: torch.as_tensor(a, dtype=torch.float32, device=dev)  # noqa: E731
-  first_qp = _qp(T['first_qp'], dev)
-  g.env._state = State(  # pylint: disable=protected-access
-      qp=_qp(T['qp0'], dev), obs=f32(T['obs0']), reward=f32(T['reward0']), done=f32(T['done0']),
-      metrics={}, info={'first_qp': first_qp, 'first_obs': f32(T['first_obs']),
-                        'steps': f32(T['steps0']), 'truncation': f32(T['truncation0'])})
+
+  def wrapped_state(t):
+    """The reference's wrapped state before step t: after reset (t = 0) or
+    after its step t - 1 (each step then starts from the reference's own
+    state: the gym path's reward is (x1 - x0) / dt, which would amplify a
+    chained fp32 drift of the state 20x)."""
+    if t == 0:
+      q, o, r, d, st, tr = (T['qp0'], T['obs0'], T['reward0'], T['done0'], T['steps0'],
+                            T['truncation0'])
+    else:
+      q, o, r, d = T['qp'][t - 1], T['obs'][t - 1], T['reward'][t - 1], T['done'][t - 1]
+      st, tr = T['info_steps'][t - 1], T['info_truncation'][t - 1]
+    return State(qp=_qp(q, dev), obs=f32(o), reward=f32(r), done=f32(d), metrics={},
+                 info={'first_qp': _qp(T['first_qp'], dev), 'first_obs': f32(T['first_obs']),
+                       'steps': f32(st), 'truncation': f32(tr)})
   inner = g.env._env.unwrapped  # pylint: disable=protected-access
   keys = [str(k) for k in T['info_keys']]
   mkeys = list(inner.metric_keys)
@@ -58,6 +68,7 @@ def test_vector_gym_step_vs_reference(dev, oracle_lib):
                                  if k not in ('first_qp', 'first_obs', 'steps', 'truncation'))
   env32 = Envelope(oracle_lib, 'ant')
   for t in range(T['action'].shape[0]):
+    g.env._state = wrapped_state(t)  # pylint: disable=protected-access
     # numpy actions in (the gym caller's), converted by the wrapper's action()
     obs, reward, done, info = g.step(T['action'][t].astype(np.float32))
     torch.cuda.synchronize()

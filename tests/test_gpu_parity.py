@@ -73,6 +73,20 @@ N_PERTURB = int(os.environ.get('BX_ENVELOPE_N', '32'))
 RECORD_ONLY = os.environ.get('BX_PARITY_RECORD_ONLY') == '1'
 
 
+def _dump_failure(field, got, ref, samples):
+  """A per-env gate past its bound: the HIP output, the reference and Brax's
+  fp32 realisations to gpurun_out/gate_fail_<test>_<field>.npz, for the
+  offline search of the element and phase that carry the excess."""
+  import re
+  test = os.environ.get('PYTEST_CURRENT_TEST', '?').split(' ')[0]
+  name = re.sub(r'[^A-Za-z0-9_.-]+', '_', test.split('::')[-1]) + '_' + field
+  d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'gpurun_out')
+  os.makedirs(d, exist_ok=True)
+  np.savez_compressed(os.path.join(d, f'gate_fail_{name}.npz'), got=np.asarray(got),
+                      ref=np.asarray(ref),
+                      samples=np.asarray([np.asarray(v) for v in (samples or [])]))
+
+
 def _gate(got, ref, e32, field, split=True):
   """SURVEY 8(c)'s per-sample gate: env i's normwise error <= max(1e-5,
   2 x E32_i), E32_i the largest fp32 error of Brax's own algorithm over that
@@ -103,6 +117,8 @@ def _gate(got, ref, e32, field, split=True):
                   gate='per_env' if split else 'group', group_tol=group_tol,
                   group_ratio=float(nw[well].max()) / group_tol)
     assert float(nw[well].max()) <= group_tol, f'{field}: group bound'
+    if m > tol:
+      _dump_failure(field, got, ref, samples)
     if not RECORD_ONLY:
       assert m <= tol, (f'{field}: env {k} normwise {m:.3e} > its bound {tol:.3e} '
                         f'({int((r > 1).sum())} of {int(well.sum())} envs past theirs)')
