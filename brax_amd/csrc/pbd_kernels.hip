@@ -409,21 +409,32 @@ __device__ __forceinline__ void joint_apply(const JointC& J, const QP& p, const 
     v3 nv[3] = {a1p, -a2n * sg, a3c};
     v3 n1v[3] = {a2p, a1p, lon};
     v3 n2v[3] = {lon, xz, a2c};
+    if (LI || JREC) {
+      // limit_angle on pseudo-angles: inside the limits the row's impulse is
+      // zero whatever the angle, outside n1 is turned by the limit's own
+      // (cos, sin); neither atan2 nor sincos. The three rows' limits are
+      // read first (one burst: each lane-image read is a scheduling fence,
+      // ld_lim), so the three independent row chains interleave; their
+      // impulses are summed in the reference's row order (Humanoid rollout
+      // 32.0 -> 31.5 us per step, Env.step 42.3 -> 41.6, tools/env_ab.sh)
+      JLim Lr[3];
 #pragma unroll
-    for (int l = 0; l < 3; l++) {
-      if (LI || JREC) {
-        // limit_angle on pseudo-angles: inside the limits the row's impulse
-        // is zero whatever the angle, outside n1 is turned by the limit's
-        // own (cos, sin); neither atan2 nor sincos
-        const JLim L = LI ? ld_lim<LS>(LI, lim_group(l)) : rec_lim(JREC, l);
+      for (int l = 0; l < 3; l++) Lr[l] = LI ? ld_lim<LS>(LI, lim_group(l)) : rec_lim(JREC, l);
+      v3 imp[3];
+#pragma unroll
+      for (int l = 0; l < 3; l++) {
+        const JLim& L = Lr[l];
         const float y = dot(cross(n1v[l], n2v[l]), nv[l]), x = dot(n1v[l], n2v[l]);
         const float pa = pseudo_angle(x, y);
         const bool below = pa < L.plo, above = pa > L.phi;
         const v3 n1 = turn(n1v[l], nv[l], below ? L.clo : L.chi, below ? L.slo : L.shi);
         const v3 dq = cross(n1, n2v[l]) * ((below || above) ? 1.f : 0.f);
-        pimp = pimp + angle_impulse(J, dq);
-        continue;
+        imp[l] = angle_impulse(J, dq);
       }
+      pimp = ((pimp + imp[0]) + imp[1]) + imp[2];
+    }
+#pragma unroll
+    for (int l = 0; l < 3 && !(LI || JREC); l++) {
       // limit_angle (joints.py:343-355)
       float ph = signed_angle(nv[l], n1v[l], n2v[l]);
       float lo = J.lim[2 * l], hi = J.lim[2 * l + 1];
@@ -1295,11 +1306,13 @@ __device__ __forceinline__ void act_torque(const JointC& Jc, const ActC& A, cons
       pa[2] = pseudo_angle(dot(a2c, lon), dot(cross(a2c, lon), -a3c));
       const v3 axes[3] = {a1p, a2c, a3c};
       tq = mk(0.f, 0.f, 0.f);
+      float2 Lp[3];
+#pragma unroll
+      for (int l = 0; l < 3; l++) Lp[l] = ld_lim_p<LS>(LI, lim_group(l));
 #pragma unroll
       for (int l = 0; l < 3; l++) {
-        const float2 L = ld_lim_p<LS>(LI, lim_group(l));
         const float t = al[l] * A.strength * -1.f;
-        tq = tq + axes[l] * ((pa[l] < L.x || pa[l] > L.y) ? 0.f : t);
+        tq = tq + axes[l] * ((pa[l] < Lp[l].x || pa[l] > Lp[l].y) ? 0.f : t);
       }
     }
     if (tqd) tq = tq + *tqd;  // + the joint's damping (FOLD)
@@ -3478,9 +3491,28 @@ __device__ __forceinline__ float euler_y(const float* q) {
 }
 
 // Humanoid center of mass over bodies [:-1] (humanoid.py:336-338) -> red[32..35]
-__device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3& com, float& msum) {
+// hb (SINGLE mode, 16 lanes, N <= 16): each lane's hoisted body, so body b's
+// mass is wave lane b's (every env of the wave has the same bodies), read
+// without a load; the loop then has a fixed trip count whose qp reads issue
+// together instead of one dependent constant load per body. Same sum order;
+// the masked tail adds 0 * pos, which leaves acc and m unchanged.
+__device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3& com, float& msum,
+                             const BodyC* hb = nullptr) {
   v3 acc = mk(0.f, 0.f, 0.f);
   float m = 0.f;
+  if (hb) {
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+      const bool in = b < H.N - 1;
+      const float mb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hb->mass), b));
+      const float w = in ? mb : 0.f;
+      acc = acc + w * ld3(qp + (in ? b : 0) * QP_STRIDE);
+      m += w;
+    }
+    com = acc / m;
+    msum = m;
+    return;
+  }
   for (int b = 0; b < H.N - 1; b++) {
     float mb = c.f(H.o_body + b * BODY_STRIDE + BODY_MASS);
     acc = acc + mb * ld3(qp + b * QP_STRIDE);
@@ -3789,7 +3821,7 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
   if ((KIND_IS(BX_ENV_HUMANOID) || KIND_IS(BX_ENV_HUMANOID_STANDUP)) && lane == 0) {
     v3 com;
     float msum;
-    humanoid_com(c, H, E.qp, com, msum);
+    humanoid_com(c, H, E.qp, com, msum, L == 16 ? hbody : nullptr);
     st3(E.red + 32, com);
     E.red[35] = msum;
   }
@@ -4227,7 +4259,9 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     v3 pos0 = ld3(E.qp);  // torso position before the step
     v3 com0 = mk(0.f, 0.f, 0.f);
     float msum = 0.f;
-    if (KIND_IS(BX_ENV_HUMANOID) || KIND_IS(BX_ENV_SWIMMER)) humanoid_com(c, H, E.qp, com0, msum);
+    if (KIND_IS(BX_ENV_HUMANOID) || KIND_IS(BX_ENV_SWIMMER))
+      humanoid_com(c, H, E.qp, com0, msum,
+                   (S && EK == EK_HUM && (F & F_JH) == 0) ? &X.B : nullptr);
     // the target envs' torso before the step (red words 36..38)
     if ((KIND_IS(BX_ENV_UR5E) || KIND_IS(BX_ENV_FETCH)) && lane == 0)
       st3(E.red + 36, ld3(E.qp + (int)P.coef[0] * QP_STRIDE));

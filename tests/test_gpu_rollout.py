@@ -198,3 +198,34 @@ def test_rollout_random_equals_slabs_then_rollout(dev, name):
   if tr.rng is not None:
     assert torch.equal(got.rng, tr.rng)
   assert torch.equal(runner.state().obs, final.obs)
+
+
+def test_strided_autoreset_target(dev):
+  """An AutoReset target (info['first_qp']) given as four separate
+  (B, N, 3|4) tensors instead of the packed layout (the kernels read it
+  through its bx_qp strides): the same bits as the packed target, for K-step
+  rollouts and single steps."""
+  import brax_amd
+  from brax_amd import envs
+  from brax_amd.envs.rollout import rollout
+  env = envs.create('ant', batch_size=64, episode_length=3, auto_reset=True, device=dev)
+  st0 = env.reset(np.array([3, 5], np.uint32))
+  fq = st0.info['first_qp']
+  strided = brax_amd.QP(pos=fq.pos.contiguous(), rot=fq.rot.contiguous(),
+                        vel=fq.vel.contiguous(), ang=fq.ang.contiguous())
+  st1 = st0.replace(info={**st0.info, 'first_qp': strided})
+  g = torch.Generator(device='cpu').manual_seed(6)
+  acts = (torch.rand((8, 64, 8), generator=g) * 2 - 1).to(dev)
+  fa, ta = rollout(env, st0, acts)
+  fb, tb = rollout(env, st1, acts)
+  assert float(ta.done.sum()) > 0  # the AutoReset select ran
+  # (the packed records' three pad words are never written)
+  for x, y in ((ta.qp[..., :13], tb.qp[..., :13]), (ta.obs, tb.obs), (ta.reward, tb.reward),
+               (ta.done, tb.done),
+               (ta.steps, tb.steps), (ta.metrics, tb.metrics)):
+    assert torch.equal(x, y)
+  a, b = st0, st1
+  for t in range(4):
+    a, b = env.step(a, acts[t]), env.step(b, acts[t])
+    assert torch.equal(a.qp.pos, b.qp.pos) and torch.equal(a.obs, b.obs)
+    assert torch.equal(a.done, b.done)

@@ -1,0 +1,8 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${1:-r05i}
+for n in _lib _lib_prev; do
+  echo "== $n"
+  BRAX_AMD_LIB=brax_amd/$n/libbrax_amd.so timeout -k 10 200 python tools/diag_rollout_graph.py 2>&1 | grep -v amdgpu.ids || exit 2
+done
