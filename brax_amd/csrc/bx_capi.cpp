@@ -3,8 +3,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -533,6 +535,28 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     H.nnl_words = 2 * 4 * max_cut;
     H.l_nnl = carve(H.nnl_words);
   }
+  // the MULTI broad phase's capsule centres: the distinct (body, offset)
+  // pairs of the capsule-capsule rows' two capsules (the bits the per-row
+  // centres rotate), placed in the world once per pass for every row naming them
+  std::map<std::array<uint32_t, 4>, int> cen_ix;
+  std::vector<std::array<uint32_t, 4>> cens;
+  std::vector<int> row_cen(2 * R, 0);
+  for (int x = 0; x < R; x++) {
+    if (d->col_fn[d->row_group[x]] != BX_COL_CAPSULE_CAPSULE) continue;
+    for (int side = 0; side < 2; side++) {
+      const int body = side ? d->row_body_b[x] : d->row_body_a[x];
+      const double* o = side ? &d->row_b_pos[3 * x] : &d->row_a_pos[3 * x];
+      const std::array<uint32_t, 4> k{(uint32_t)body, fbits(o[0]), fbits(o[1]), fbits(o[2])};
+      auto it = cen_ix.find(k);
+      if (it == cen_ix.end()) {
+        it = cen_ix.emplace(k, (int)cens.size()).first;
+        cens.push_back(k);
+      }
+      row_cen[2 * x + side] = it->second;
+    }
+  }
+  if (cens.size() > 0xFFFF) return fail("too many broad-phase capsule centres");
+  H.n_cen = (int)cens.size();
   // the MULTI (System.step only) tail starts here, over the env step's regions
   const int tail_m = off;
   // env-step regions: joint angles, the env programs' System.step action
@@ -557,6 +581,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // scenes only (culled scenes skip the broad phase)
   H.l_near = carve(H.n_nn ? 0 : (R + 1) / 2);
   H.l_nearc = carve(H.n_nn ? 0 : 16);
+  // the broad phase's row bounds and centres (constants, then world), staged
+  // once per launch
+  H.l_bimg = carve(H.n_nn ? 0 : BI_WORDS * R);
+  H.l_cen = carve(H.n_nn ? 0 : 8 * H.n_cen);
   H.env_words_m = (off + 63) & ~63;
   off = tail;
   H.l_rowd = carve(R * ROWD_STRIDE);
@@ -663,7 +691,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     }
     // broad-phase bounds (BI_*): reach = |a_end| + |b_end| + radii in double,
     // rounded up to float
-    H.o_bimg = B.alloc(BI_WORDS * R);
+    std::vector<uint32_t> bimg(BI_WORDS * R, 0u);
     for (int x = 0; x < R; x++) {
       const int g = d->row_group[x];
       double reach = d->row_a_radius[x] + d->row_b_radius[x];
@@ -674,18 +702,18 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       }
       reach += std::sqrt(ea) + std::sqrt(eb);
       const float rf = std::nextafter((float)reach, 3.0e38f);
-      uint32_t bw[BI_WORDS] = {0};
-      bw[BI_A] = (uint32_t)d->row_body_a[x];
-      bw[BI_B] = (uint32_t)d->row_body_b[x];
+      uint32_t* bw = &bimg[BI_WORDS * x];
+      const bool skip = d->col_fn[g] == BX_COL_CAPSULE_CAPSULE;
+      if (skip) bw[BI_CEN] = (uint32_t)row_cen[2 * x] | ((uint32_t)row_cen[2 * x + 1] << 16);
       std::memcpy(&bw[BI_REACH], &rf, 4);
-      bw[BI_SKIP] = d->col_fn[g] == BX_COL_CAPSULE_CAPSULE ? 1u : 0u;
+      bw[BI_SKIP] = skip ? 1u : 0u;
       bw[BI_BSLOT] = (uint32_t)mb[x];
-      for (int k = 0; k < 3; k++) {
-        bw[BI_APOS + k] = fbits(d->row_a_pos[3 * x + k]);
-        bw[BI_BPOS + k] = fbits(d->row_b_pos[3 * x + k]);
-      }
-      for (int k = 0; k < BI_WORDS; k++) B.w[H.o_bimg + ((k / 4) * R + x) * 4 + k % 4] = bw[k];
     }
+    H.o_bimg = B.alloc(BI_WORDS * R);
+    for (int k = 0; k < BI_WORDS * R; k++) B.w[H.o_bimg + k] = bimg[k];
+    H.o_cen = B.alloc(4 * H.n_cen);
+    for (int k = 0; k < H.n_cen; k++)
+      for (int i = 0; i < 4; i++) B.w[H.o_cen + 4 * k + i] = cens[k][i];
   }
   // the SINGLE-mode lane image (pbd_layout.h LI_*): copies of the records
   // above, so its words are the same bits the item-loop kernels read; a lane

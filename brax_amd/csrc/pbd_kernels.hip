@@ -88,6 +88,8 @@ struct Env {
   float* nnl;    // NearNeighbors per-wave pick lists (nnl_words)
   uint16_t* nearl;  // MULTI: the pass's near rows
   int* nearc;       // MULTI: the broad phase's per-wave counts
+  uint4* bimg;      // MULTI: the rows' broad-phase bounds (BI_*), staged per launch
+  uint4* cen;       // MULTI: the capsule centres' (body, offset), then their world points
   uint4* jlim;   // SINGLE spherical kernels: the lanes' limit rows, [6][L] groups
 };
 
@@ -1499,6 +1501,8 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi =
     E.tslot = al16(base + H.l_tslot);
     E.nearl = reinterpret_cast<uint16_t*>(base + H.l_near);
     E.nearc = reinterpret_cast<int*>(base + H.l_nearc);
+    E.bimg = reinterpret_cast<uint4*>(al16(base + H.l_bimg));
+    E.cen = reinterpret_cast<uint4*>(al16(base + H.l_cen));
     E.sstride = MSLOT_STRIDE;
     E.nd = E.tslot;
     E.nds = 1;
@@ -3054,7 +3058,7 @@ template <int L, int F, int MR>
 __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
                                const float* act, int aw, const HoistM<MR>& X, RowInfoOut io) {
 #ifdef BX_MSTAMPS
-  unsigned long long ms_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ms_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long ms_last;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ms_last)::"memory");
 #endif
@@ -3206,6 +3210,16 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       constexpr int NWV = L / 64;
       const int wv = lane >> 6;
       int* cnt = E.nearc;
+      // the capsule centres in the world, once for every row naming them
+      uint4* cw = E.cen + H.n_cen;
+      for (int k = lane; k < H.n_cen; k += L) {
+        const uint4 cc = E.cen[k];
+        const float* qb = E.qp + (int)cc.x * QP_STRIDE;
+        const v3 p = ld3(qb) + rotate(mk(__uint_as_float(cc.y), __uint_as_float(cc.z),
+                                         __uint_as_float(cc.w)), ld_rot(qb));
+        cw[k] = make_uint4(__float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(p.z), 0u);
+      }
+      esync<L>();
       bool nr[MR];
       int rr[MR], rk[MR];
 #pragma unroll
@@ -3214,24 +3228,20 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
         const int r = x < nact ? BX_MULTI_RX(x) : -1;
         bool near = false;
         if (r >= 0) {
-          const uint4* bi = reinterpret_cast<const uint4*>(c.w + H.o_bimg) + r;
-          const uint4 g0 = bi[0], g1 = bi[H.R], g2 = bi[2 * H.R];
-          near = g0.w == 0u;
+          const uint4 g0 = E.bimg[r];
+          near = g0.z == 0u;
           if (!near) {
-            const float* qa = E.qp + (int)g0.x * QP_STRIDE;
-            const float* qb = E.qp + (int)g0.y * QP_STRIDE;
-            const v3 ca = ld3(qa) + rotate(mk(__uint_as_float(g1.x), __uint_as_float(g1.y),
-                                              __uint_as_float(g1.z)), ld_rot(qa));
-            const v3 cb = ld3(qb) + rotate(mk(__uint_as_float(g2.x), __uint_as_float(g2.y),
-                                              __uint_as_float(g2.z)), ld_rot(qb));
+            const uint4 a4 = cw[g0.x & 0xFFFFu], b4 = cw[g0.x >> 16];
+            const v3 ca = mk(__uint_as_float(a4.x), __uint_as_float(a4.y), __uint_as_float(a4.z));
+            const v3 cb = mk(__uint_as_float(b4.x), __uint_as_float(b4.y), __uint_as_float(b4.z));
             // + 1e-4: far above the fp32 error of the centres
-            near = !(norm(cb - ca) > __uint_as_float(g0.z) + 1e-4f);
+            near = !(norm(cb - ca) > __uint_as_float(g0.y) + 1e-4f);
           }
           if (!near) {
             // (a one-way row's b slot is the zero slot: zeros again)
             const v3 z = mk(0.f, 0.f, 0.f);
             st_mslot(E.cslot + r * MSLOT_STRIDE, z, z);
-            st_mslot(E.cslot + (int)g1.w * MSLOT_STRIDE, z, z);
+            st_mslot(E.cslot + (int)g0.w * MSLOT_STRIDE, z, z);
           }
         }
         nr[m] = near;
@@ -3257,7 +3267,12 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       }
       nwork = total;
       esync<L>();
+#ifdef BX_MSTAMPS
+      ms_acc[12] += (unsigned long long)nwork;
+      ms_acc[13] += 1ull;
+#endif
     }
+    BX_MSTAMP(11);
     // Collider.position_apply (colliders.py:198-240): the lane's rows
 #pragma unroll
     for (int m = 0; m < MR; m++) {
@@ -3391,7 +3406,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
 #ifdef BX_MSTAMPS
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int k = 0; k < 11; k++) bx_mstamp_wave[blockIdx.x & 4095][k] += ms_acc[k];
+    for (int k = 0; k < 14; k++) bx_mstamp_wave[blockIdx.x & 4095][k] += ms_acc[k];
     bx_mstamp_wave[blockIdx.x & 4095][15] += 1ull;
   }
 #endif
@@ -4005,6 +4020,13 @@ __device__ __forceinline__ void system_step_body(const StepArgs& A) {
     // M = contact rows per lane
     HoistM<M> X;
     load_hoist_multi<L, M>(c, H, lane, X);
+    // the broad phase's constants into LDS, read by every pass
+    if (H.o_bimg != 0 && H.n_nn == 0) {
+      const uint4* bg = reinterpret_cast<const uint4*>(c.w + H.o_bimg);
+      for (int r = lane; r < H.R; r += L) E.bimg[r] = bg[r];
+      const uint4* cg = reinterpret_cast<const uint4*>(c.w + H.o_cen);
+      for (int k = lane; k < H.n_cen; k += L) E.cen[k] = cg[k];
+    }
     const int64_t ro = valid ? e * H.info_rows : 0;
     RowInfoOut io{A.info.contact_pos ? A.info.contact_pos + ro * 3 : nullptr,
                   A.info.contact_normal ? A.info.contact_normal + ro * 3 : nullptr,

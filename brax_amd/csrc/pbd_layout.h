@@ -108,6 +108,8 @@ struct BlobHdr {
   int32_t m_zero;                    // MULTI: the zero contact slot (R + two-way rows)
   int32_t l_nearc;                   // LDS (MULTI): the broad phase's per-wave counts (16)
   int32_t o_rphys;                   // MULTI mode: the rows' impulse constants (MP_*)
+  int32_t n_cen, o_cen;              // MULTI broad phase: the capsule centres (body, offset)
+  int32_t l_bimg, l_cen;             // LDS (MULTI broad phase): the rows' bounds, the centres
 };
 
 // SINGLE-mode lane image: for each of 64 lanes, every constant the
@@ -186,14 +188,17 @@ enum { MG_AB = 0, MG_META = 1, MG_APOS = 2, MG_AEND = 5, MG_ARAD = 8, MG_BPOS = 
        MG_BRAD = 15, MG_WORDS = 16 };
 enum { MP_FRIC = 0, MP_ELAS = 1, MP_SCALE = 2, MP_THR = 3, MP_MA = 4, MP_MB = 5, MP_IA = 6, MP_IB = 9,
        MP_WORDS = 12 };
-// MULTI-mode broad phase: per row, 16-byte group g of row r at
-// o_bimg + (g * R + r) * 4: (body a, body b, reach, may_skip), (a's centre
-// offset, 0), (b's centre offset, 0). A capsule-capsule row whose capsule
-// centres lie farther apart than reach (half segments + radii, rounded up)
-// cannot penetrate, and its position / velocity updates are exact zeros.
-// BI_BSLOT: the row's b-side slot (two-way rows; one-way rows: the zero slot).
-enum { BI_A = 0, BI_B = 1, BI_REACH = 2, BI_SKIP = 3, BI_APOS = 4, BI_BSLOT = 7, BI_BPOS = 8,
-       BI_WORDS = 12 };
+// MULTI-mode broad phase: per row one 16-byte group at o_bimg + 4 r (staged
+// in LDS at l_bimg once per launch): (centre a | centre b << 16, reach,
+// may_skip, b slot). A capsule-capsule row whose capsule centres lie farther
+// apart than reach (half segments + radii, rounded up) cannot penetrate, and
+// its position / velocity updates are exact zeros. The centres are the
+// distinct (body, offset) pairs of the rows' capsules, 16 bytes each at
+// o_cen + 4 k: (body, offset xyz), staged at l_cen; each broad-phase pass
+// places them in the world once (l_cen + 4 n_cen + 4 k) for every row that
+// names them. BI_BSLOT: the row's b-side slot (two-way rows; one-way rows:
+// the zero slot).
+enum { BI_CEN = 0, BI_REACH = 1, BI_SKIP = 2, BI_BSLOT = 3, BI_WORDS = 4 };
 enum { HULL_STRIDE = 114, HULL_V = 0, HULL_F = 24, HULL_N = 96 };
 
 }  // namespace bx

@@ -31,10 +31,12 @@ for k in range(30):
   qp, _ = sys_.step(qp, a)
 torch.cuda.synchronize()
 _native.check(lib.bx_debug_stamps(buf, 2))
-v = np.array(buf[:11], dtype=np.float64)
+v = np.array(buf[:12], dtype=np.float64)
 n = max(buf[15], 1)
 names = ['act+damp', 'body acc', 'joint', 'body pos(+vproj)', 'contact pos rows', 'task sum (pos)',
-         'body combine pos', 'contact vel rows', 'task sum + body (vel)', 'nn select', 'tail']
+         'body combine pos', 'contact vel rows', 'task sum + body (vel)', 'nn select', 'tail',
+         'broad phase']
+print('near rows per broad-phase pass', buf[12] / max(buf[13], 1), 'passes/wg-step', buf[13] / n)
 tot = v.sum()
 print('cutoff', cut, 'samples', n, 'cycles/wave0/step', tot / n)
 for i, nm in enumerate(names):
