@@ -743,53 +743,97 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       }
     }
   }
+  // records in the lane images' layouts, each word through put(lane, word,
+  // value): a joint (LJ_*, with its bodies' masses / inverse inertias), its
+  // limit row `row` (LL_*: pseudo-angles and cos / sin, from J_JLIM), an
+  // actuator (LA_*), a joint-halves side (LS_* but LS_OWN; returns the body)
+  auto img_joint = [&](auto&& put, int lane, int base, int j) {
+    if (J == 0) return;
+    const uint32_t* s = &B.w[H.o_joint + j * JOINT_STRIDE];
+    const int bp = (int)s[J_BP], bc = (int)s[J_BC];
+    const uint32_t* p = &B.w[H.o_body + bp * BODY_STRIDE];
+    const uint32_t* c = &B.w[H.o_body + bc * BODY_STRIDE];
+    const int ints[6] = {J_TYPE, J_BP, J_BC, J_FREE, J_ANGLE_OFF, J_NANGLES};
+    for (int k = 0; k < 6; k++) put(lane, base + k, s[ints[k]]);
+    put(lane, base + LJ_DAMP, s[J_DAMP]);
+    put(lane, base + LJ_SP, s[J_SP]);
+    put(lane, base + LJ_SA, s[J_SA]);
+    for (int k = 0; k < 3; k++) {
+      put(lane, base + LJ_OFFP + k, s[J_OFFP + k]);
+      put(lane, base + LJ_OFFC + k, s[J_OFFC + k]);
+      put(lane, base + LJ_IP + k, p[BODY_I + k]);
+      put(lane, base + LJ_IC + k, c[BODY_I + k]);
+    }
+    for (int k = 0; k < 9; k++) {
+      put(lane, base + LJ_AXP + k, s[J_AXP + k]);
+      put(lane, base + LJ_AXC + k, s[J_AXC + k]);
+    }
+    for (int k = 0; k < 6; k++) put(lane, base + LJ_LIM + k, s[J_LIM + k]);
+    put(lane, base + LJ_DOF, s[J_DOF]);
+    put(lane, base + LJ_MP, p[BODY_MASS]);
+    put(lane, base + LJ_MC, c[BODY_MASS]);
+  };
+  auto img_lim = [&](auto&& put, int lane, int base, int j, int row) {
+    if (J == 0) return;
+    const uint32_t* s = &B.w[H.o_joint + j * JOINT_STRIDE + J_JLIM + 8 * row];
+    for (int k = 0; k < 6; k++) put(lane, base + k, s[k]);
+  };
+  auto img_act = [&](auto&& put, int lane, int base, int a) {
+    if (K == 0) return;
+    const uint32_t* s = &B.w[H.o_act + a * ACT_STRIDE];
+    put(lane, base + LA_TYPE, s[A_TYPE]);
+    put(lane, base + LA_JOINT, s[A_JOINT]);
+    for (int k = 0; k < 3; k++) put(lane, base + LA_IDX + k, s[A_IDX + k]);
+    put(lane, base + LA_STR, s[A_STR]);
+  };
+  auto img_side = [&](auto&& put, int lane, int base, int j, bool child) {
+    const uint32_t* s = &B.w[H.o_joint + j * JOINT_STRIDE];
+    const int body = (int)s[child ? J_BC : J_BP];
+    const uint32_t* bw = &B.w[H.o_body + body * BODY_STRIDE];
+    for (int k = 0; k < 3; k++) {
+      put(lane, base + LS_OFF + k, s[(child ? J_OFFC : J_OFFP) + k]);
+      put(lane, base + LS_AX0 + k, s[(child ? J_AXC : J_AXP) + k]);
+      put(lane, base + LS_AX2 + k, s[(child ? J_AXC : J_AXP) + 6 + k]);
+      put(lane, base + LS_I + k, bw[BODY_I + k]);
+    }
+    put(lane, base + LS_M, bw[BODY_MASS]);
+    put(lane, base + LS_SG, fbits(child ? -1.0 : 1.0));
+    put(lane, base + LS_BODY, (uint32_t)body);
+    return body;
+  };
+  // the MULTI kernel's joint halves (MJ_*): revolute joints each driven by
+  // the torque actuator of its index, <= 128 joints (16 lanes per 8)
+  {
+    bool ok = H.multi && J > 0 && J <= 128 && K == J && H.act_same;
+    for (int j = 0; j < J; j++) ok = ok && d->joint_type[j] == BX_JOINT_REVOLUTE;
+    for (int a = 0; a < K; a++) ok = ok && d->act_type[a] == BX_ACT_TORQUE;
+    const bool off = getenv("BX_NO_MULTI_JH") && atoi(getenv("BX_NO_MULTI_JH"));
+    H.mjh = ok && !off ? 1 : 0;
+  }
+  if (H.mjh) {
+    B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
+    H.o_mjh = B.alloc(MJ_W * MJ_LANES);
+    auto putm = [&](int lane, int w, uint32_t v) {
+      B.w[H.o_mjh + (w / 4) * 4 * MJ_LANES + 4 * lane + w % 4] = v;
+    };
+    for (int l = 0; l < MJ_LANES; l++) {
+      const int jx = (l >> 4) * 8 + (l & 7);
+      const int j = jx < J ? jx : 0;
+      img_joint(putm, l, MJ_JOINT, j);
+      img_act(putm, l, MJ_ACT, j);
+      img_lim(putm, l, MJ_JLIM, j, 0);
+      img_side(putm, l, MJ_SIDE, j, (l & 8) != 0);
+    }
+  }
   if (H.single) {
     B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
     H.o_lane = B.alloc(LANE_W * LANE_IMG_LANES);
     auto put = [&](int lane, int w, uint32_t v) {
       B.w[H.o_lane + (w / 4) * 4 * LANE_IMG_LANES + 4 * lane + w % 4] = v;
     };
-    auto put_joint = [&](int lane, int base, int j) {
-      if (J == 0) return;
-      const uint32_t* s = &B.w[H.o_joint + j * JOINT_STRIDE];
-      const int bp = (int)s[J_BP], bc = (int)s[J_BC];
-      const uint32_t* p = &B.w[H.o_body + bp * BODY_STRIDE];
-      const uint32_t* c = &B.w[H.o_body + bc * BODY_STRIDE];
-      const int ints[6] = {J_TYPE, J_BP, J_BC, J_FREE, J_ANGLE_OFF, J_NANGLES};
-      for (int k = 0; k < 6; k++) put(lane, base + k, s[ints[k]]);
-      put(lane, base + LJ_DAMP, s[J_DAMP]);
-      put(lane, base + LJ_SP, s[J_SP]);
-      put(lane, base + LJ_SA, s[J_SA]);
-      for (int k = 0; k < 3; k++) {
-        put(lane, base + LJ_OFFP + k, s[J_OFFP + k]);
-        put(lane, base + LJ_OFFC + k, s[J_OFFC + k]);
-        put(lane, base + LJ_IP + k, p[BODY_I + k]);
-        put(lane, base + LJ_IC + k, c[BODY_I + k]);
-      }
-      for (int k = 0; k < 9; k++) {
-        put(lane, base + LJ_AXP + k, s[J_AXP + k]);
-        put(lane, base + LJ_AXC + k, s[J_AXC + k]);
-      }
-      for (int k = 0; k < 6; k++) put(lane, base + LJ_LIM + k, s[J_LIM + k]);
-      put(lane, base + LJ_DOF, s[J_DOF]);
-      put(lane, base + LJ_MP, p[BODY_MASS]);
-      put(lane, base + LJ_MC, c[BODY_MASS]);
-    };
-    // the limit row's pseudo-angles (kernels' pseudo_angle) and cos / sin,
-    // from the radians the record holds, in double
-    auto put_lim = [&](int lane, int base, int j, int row) {
-      if (J == 0) return;
-      const uint32_t* s = &B.w[H.o_joint + j * JOINT_STRIDE + J_JLIM + 8 * row];
-      for (int k = 0; k < 6; k++) put(lane, base + k, s[k]);
-    };
-    auto put_act = [&](int lane, int base, int a) {
-      if (K == 0) return;
-      const uint32_t* s = &B.w[H.o_act + a * ACT_STRIDE];
-      put(lane, base + LA_TYPE, s[A_TYPE]);
-      put(lane, base + LA_JOINT, s[A_JOINT]);
-      for (int k = 0; k < 3; k++) put(lane, base + LA_IDX + k, s[A_IDX + k]);
-      put(lane, base + LA_STR, s[A_STR]);
-    };
+    auto put_joint = [&](int lane, int base, int j) { img_joint(put, lane, base, j); };
+    auto put_lim = [&](int lane, int base, int j, int row) { img_lim(put, lane, base, j, row); };
+    auto put_act = [&](int lane, int base, int a) { img_act(put, lane, base, a); };
     auto put_list = [&](int lane, int base, const std::vector<int>& v, bool has, uint32_t zero) {
       for (int k = 0; k < 8; k++) put(lane, base + k, has && k < (int)v.size() ? (uint32_t)v[k] : zero);
     };
@@ -828,18 +872,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         // the joint-halves side: the parent's on lanes 0-7, the child's on
         // 8-15
         const bool child = (l & HB) != 0;
-        const uint32_t* s = &B.w[H.o_joint + (jh < J ? jh : 0) * JOINT_STRIDE];
-        const int body = (int)s[child ? J_BC : J_BP];
-        const uint32_t* bw = &B.w[H.o_body + body * BODY_STRIDE];
-        for (int k = 0; k < 3; k++) {
-          put(l, LI_SIDE_H + LS_OFF + k, s[(child ? J_OFFC : J_OFFP) + k]);
-          put(l, LI_SIDE_H + LS_AX0 + k, s[(child ? J_AXC : J_AXP) + k]);
-          put(l, LI_SIDE_H + LS_AX2 + k, s[(child ? J_AXC : J_AXP) + 6 + k]);
-          put(l, LI_SIDE_H + LS_I + k, bw[BODY_I + k]);
-        }
-        put(l, LI_SIDE_H + LS_M, bw[BODY_MASS]);
-        put(l, LI_SIDE_H + LS_SG, fbits(child ? -1.0 : 1.0));
-        put(l, LI_SIDE_H + LS_BODY, (uint32_t)body);
+        const int body = img_side(put, l, LI_SIDE_H, jh < J ? jh : 0, child);
         // JB: the side body's record and gather lists; LS_OWN on the lowest
         // lane of the env's 16 whose side is that body
         const bool hasS = jh < J;
@@ -1195,7 +1228,8 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   if (S->mode == 1)
     HIP_OK(launch_system_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   else if (S->mode == 3)
-    HIP_OK(launch_system_step_multi(S->feat, (S->hdr.R + 255) / 256, n_envs, step_lds(S), as_stream(stream), a));
+    HIP_OK(launch_system_step_multi(S->feat | (S->hdr.mjh ? 128 : 0), (S->hdr.R + 255) / 256, n_envs,
+                                    step_lds(S), as_stream(stream), a));
   else
     HIP_OK(launch_system_step_generic(S->L, S->mode, S->feat, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   return 0;

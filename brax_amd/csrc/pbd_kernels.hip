@@ -2884,8 +2884,10 @@ template <int MR>
 struct HoistM {
   bool hasB, hasJ, hasA;
   BodyC B;
-  JointC J;
+  JointC J;  // joint halves (MJH): the lane's joint side's joint
   ActC A;
+  JSide S;   // MJH: the lane's side, its joint's first limit row
+  JLim JL;
   GList<MAXG> jl, al;
   int te[TASK_W];   // the lane's task: contact slot indices (padding: the zero slot)
   int bt[BTASK_W];  // the lane's body: task | group << 24 (padding: the zero task)
@@ -2936,7 +2938,66 @@ __device__ __forceinline__ void load_row_phys(const Cst& c, const BlobHdr& H, in
   x.Ib = mk(__uint_as_float(p2.y), __uint_as_float(p2.z), __uint_as_float(p2.w));
 }
 
-template <int L, int MR>
+// MJH: the lane's joint side from the MULTI joint-halves image (MJ_*, 20
+// independent 16-byte loads), parsed as the SINGLE lane image's records
+template <int MR>
+__device__ __forceinline__ void load_mjh(const Cst& c, const BlobHdr& H, int lane, HoistM<MR>& X) {
+  const int jx = ((lane >> 4) << 3) + (lane & 7);
+  X.hasJ = jx < H.J;
+  X.hasA = jx < H.K;
+  const uint4* im = reinterpret_cast<const uint4*>(c.w + H.o_mjh) + lane;
+  uint32_t w[MJ_W];
+#pragma unroll
+  for (int g = 0; g < MJ_W / 4; g++) {
+    const uint4 v = im[g * MJ_LANES];
+    w[4 * g] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+  }
+  auto f = [&](int i) { return __uint_as_float(w[i]); };
+  auto f3 = [&](int i) { return mk(f(i), f(i + 1), f(i + 2)); };
+  auto n = [&](int i) { return (int)w[i]; };
+  JointC& J = X.J;
+  constexpr int OJ = MJ_JOINT;
+  J.type = n(OJ + LJ_TYPE);
+  J.bp = n(OJ + LJ_BP);
+  J.bc = n(OJ + LJ_BC);
+  J.free = n(OJ + LJ_FREE);
+  J.angle_off = n(OJ + LJ_AOFF);
+  J.n_angles = n(OJ + LJ_NANG);
+  J.dof = n(OJ + LJ_DOF);
+  J.damping = f(OJ + LJ_DAMP);
+  J.sp = f(OJ + LJ_SP);
+  J.sa = f(OJ + LJ_SA);
+  J.off_p = f3(OJ + LJ_OFFP);
+  J.off_c = f3(OJ + LJ_OFFC);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    J.axp[k] = f3(OJ + LJ_AXP + 3 * k);
+    J.axc[k] = f3(OJ + LJ_AXC + 3 * k);
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++) J.lim[k] = f(OJ + LJ_LIM + k);
+  J.mp = f(OJ + LJ_MP);
+  J.mc = f(OJ + LJ_MC);
+  J.Ip = f3(OJ + LJ_IP);
+  J.Ic = f3(OJ + LJ_IC);
+  X.A.type = n(MJ_ACT + LA_TYPE);
+  X.A.joint = n(MJ_ACT + LA_JOINT);
+#pragma unroll
+  for (int k = 0; k < 3; k++) X.A.idx[k] = n(MJ_ACT + LA_IDX + k);
+  X.A.strength = f(MJ_ACT + LA_STR);
+  constexpr int OL = MJ_JLIM;
+  X.JL = JLim{f(OL + LL_PLO), f(OL + LL_PHI), f(OL + LL_CLO), f(OL + LL_SLO), f(OL + LL_CHI),
+              f(OL + LL_SHI)};
+  X.S.off = f3(MJ_SIDE + LS_OFF);
+  X.S.ax0 = f3(MJ_SIDE + LS_AX0);
+  X.S.ax2 = f3(MJ_SIDE + LS_AX2);
+  X.S.I = f3(MJ_SIDE + LS_I);
+  X.S.m = f(MJ_SIDE + LS_M);
+  X.S.sg = f(MJ_SIDE + LS_SG);
+  X.S.body = n(MJ_SIDE + LS_BODY);
+}
+
+template <int L, int MR, bool MJH = false>
 __device__ __forceinline__ void load_hoist_multi(const Cst& c, const BlobHdr& H, int lane,
                                                  HoistM<MR>& X) {
   X.hasB = lane < H.N;
@@ -2951,8 +3012,12 @@ __device__ __forceinline__ void load_hoist_multi(const Cst& c, const BlobHdr& H,
   for (int k = 0; k < TASK_W; k++) X.te[k] = hasT ? c.i(H.o_task + lane * TASK_W + k) : H.m_zero;
 #pragma unroll
   for (int k = 0; k < BTASK_W; k++) X.bt[k] = X.hasB ? c.i(H.o_btask + b * BTASK_W + k) : H.T;
-  if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? lane : 0);
-  if (H.K > 0) X.A = load_act(c, H, X.hasA ? lane : 0);
+  if constexpr (MJH) {
+    load_mjh<MR>(c, H, lane, X);
+  } else {
+    if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? lane : 0);
+    if (H.K > 0) X.A = load_act(c, H, X.hasA ? lane : 0);
+  }
 #if defined(BX_MULTI_HOIST_ROWS)
 #pragma unroll
   for (int m = 0; m < MR; m++) {
@@ -3064,6 +3129,10 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
 #endif
   const float h = H.h;
   const v3 g = mk(H.gx, H.gy, H.gz);
+  // MJH (the joint halves, F_JH): the lane's joint jx and side
+  constexpr bool MJH = (F & F_JH) != 0;
+  const int mjx = ((lane >> 4) << 3) + (lane & 7);
+  const bool mchild = (lane & 8) != 0;
   const bool info_rows = io.pos || io.normal || io.pen || io.cell;
   float* myqp = E.qp + lane * QP_STRIDE;
   QP q;
@@ -3120,6 +3189,18 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       prot = q.rot;
       if (sub == 1 && X.hasB) st_slot(E.prev + lane * PREV_STRIDE, ppos, prot, 0.f);
       // actuators (actuators.py:52-112) + joint damping (joints.py:103-128)
+      if constexpr (MJH) {
+        // one side of joint / actuator jx per lane: the side's damping torque
+        // into its joint slot (parent: Ip tq, child: -Ic tq), its actuator
+        // torque into its actuator slot
+        if (X.hasJ) {
+          const JointC& Jc = X.J;
+          const v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
+          st_v3a(E.jslot + (mchild ? E.nJ + mjx : mjx) * SLOT_STRIDE, X.S.sg * mul(X.S.I, tq));
+          if (X.hasA)
+            act_torque_half<F>(X.J, X.JL, X.S, X.A, E, al, mjx, mchild, ld_rot(E.qp + X.S.body * QP_STRIDE));
+        }
+      } else {
       if (X.hasA) {
         if (H.act_same) {
           act_torque<F>(X.J, X.A, E, al, lane);
@@ -3133,6 +3214,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
         v3 tq = -1.f * Jc.damping * (ld_ang(E.qp + Jc.bp * QP_STRIDE) - ld_ang(E.qp + Jc.bc * QP_STRIDE));
         st_v3a(E.jslot + lane * SLOT_STRIDE, mul(Jc.Ip, tq));
         st_v3a(E.jslot + (E.nJ + lane) * SLOT_STRIDE, -1.f * mul(Jc.Ic, tq));
+      }
       }
       esync<L>();
       BX_MSTAMP(0);
@@ -3157,7 +3239,15 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       esync<L>();
       BX_MSTAMP(1);
       // Joint.apply (joints.py:79-100)
-      if (X.hasJ) {
+      if constexpr (MJH) {
+        if (X.hasJ) {
+          const QP o = ldqp(E.qp + X.S.body * QP_STRIDE);
+          v3 dpo;
+          q4 dro;
+          joint_apply_half(X.J, X.JL, X.S, mchild, o, dpo, dro);
+          st_slot(E.jslot + (mchild ? E.nJ + mjx : mjx) * SLOT_STRIDE, dpo, dro, 0.f);
+        }
+      } else if (X.hasJ) {
         const JointC& Jc = X.J;
         QP p = ldqp(E.qp + Jc.bp * QP_STRIDE), cq = ldqp(E.qp + Jc.bc * QP_STRIDE);
         v3 dpp, dcp;
@@ -4019,7 +4109,7 @@ __device__ __forceinline__ void system_step_body(const StepArgs& A) {
   if constexpr (MU) {
     // M = contact rows per lane
     HoistM<M> X;
-    load_hoist_multi<L, M>(c, H, lane, X);
+    load_hoist_multi<L, M, (F & F_JH) != 0>(c, H, lane, X);
     // the broad phase's constants into LDS, read by every pass
     if (H.o_bimg != 0 && H.n_nn == 0) {
       const uint4* bg = reinterpret_cast<const uint4*>(c.w + H.o_bimg);
@@ -4099,10 +4189,10 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
 // (tools/multi_occ.py: the step time grew with the batch from 256 envs on).
 // A/B knob BX_MULTI_WPE=3 / 4: held to 168 / 128 (three / four waves per
 // SIMD: the LDS then admits three workgroups per CU; both spill)
-template <int M, int W>
+template <int M, int W, int JH = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W)))
 system_step_multi_kernel(StepArgs A) {
-  system_step_body<256, MODE_MULTI, F_CC | F_TW, M>(A);
+  system_step_body<256, MODE_MULTI, F_CC | F_TW | JH, M>(A);
 }
 
 
@@ -5159,6 +5249,17 @@ hipError_t launch_system_step_multi(int feat, int mr, int64_t n_envs, size_t lds
       case 2 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<2, 4>, grid, 256, lds, s, a); break;
       case 3 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<3, 4>, grid, 256, lds, s, a); break;
       case 4 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<4, 4>, grid, 256, lds, s, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if ((feat & F_JH) != 0) {
+    // the joint halves (H.mjh: revolute joints, torque actuators of the same index)
+    switch (mr) {
+      case 1: launch_one<StepArgs>(system_step_multi_kernel<1, 2, F_JH>, grid, 256, lds, s, a); break;
+      case 2: launch_one<StepArgs>(system_step_multi_kernel<2, 2, F_JH>, grid, 256, lds, s, a); break;
+      case 3: launch_one<StepArgs>(system_step_multi_kernel<3, 2, F_JH>, grid, 256, lds, s, a); break;
+      case 4: launch_one<StepArgs>(system_step_multi_kernel<4, 2, F_JH>, grid, 256, lds, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -110,6 +110,7 @@ struct BlobHdr {
   int32_t o_rphys;                   // MULTI mode: the rows' impulse constants (MP_*)
   int32_t n_cen, o_cen;              // MULTI broad phase: the capsule centres (body, offset)
   int32_t l_bimg, l_cen;             // LDS (MULTI broad phase): the rows' bounds, the centres
+  int32_t mjh, o_mjh;                // MULTI joint halves: the image (MJ_*) of lane l's joint side
 };
 
 // SINGLE-mode lane image: for each of 64 lanes, every constant the
@@ -145,6 +146,12 @@ enum {
   LI_CL_J = 308,
   LANE_W = 316
 };
+// MULTI-mode joint halves: lane l works side (l & 8: child) of joint
+// (l >> 4) * 8 + (l & 7) and that joint's actuator, the Ant kernel's halves
+// in every 16-lane row of the env's 256; word w of lane l at o_mjh +
+// (w / 4) * 4 * 256 + 4 * l + w % 4: the joint (LJ_*), the actuator (LA_*),
+// the first limit row (LL_*), the side (LS_*)
+enum { MJ_JOINT = 0, MJ_ACT = 48, MJ_JLIM = 56, MJ_SIDE = 64, MJ_W = 80, MJ_LANES = 256 };
 // a joint-halves lane's side (lanes 8-15 of 16: the child's): its anchor offset,
 // hinge axis and reference axis in its body's frame, that body's inverse
 // inertia and mass, the side's sign (+1 parent, -1 child) and the body;
