@@ -536,13 +536,16 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     H.l_nnl = carve(H.nnl_words);
   }
   // the MULTI broad phase's capsule centres: the distinct (body, offset)
-  // pairs of the capsule-capsule rows' two capsules (the bits the per-row
-  // centres rotate), placed in the world once per pass for every row naming them
+  // pairs of the capsule-capsule rows' and the culled groups' rows' two
+  // collidables (the bits the per-row centres rotate), placed in the world
+  // once per pass (culled scenes: once per step, for the NearNeighbors keys)
+  // for every row naming them
   std::map<std::array<uint32_t, 4>, int> cen_ix;
   std::vector<std::array<uint32_t, 4>> cens;
   std::vector<int> row_cen(2 * R, 0);
   for (int x = 0; x < R; x++) {
-    if (d->col_fn[d->row_group[x]] != BX_COL_CAPSULE_CAPSULE) continue;
+    const int g = d->row_group[x];
+    if (d->col_fn[g] != BX_COL_CAPSULE_CAPSULE && d->col_cutoff[g] == 0) continue;
     for (int side = 0; side < 2; side++) {
       const int body = side ? d->row_body_b[x] : d->row_body_a[x];
       const double* o = side ? &d->row_b_pos[3 * x] : &d->row_a_pos[3 * x];
@@ -583,8 +586,8 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.l_nearc = carve(H.n_nn ? 0 : 16);
   // the broad phase's row bounds and centres (constants, then world), staged
   // once per launch
-  H.l_bimg = carve(H.n_nn ? 0 : BI_WORDS * R);
-  H.l_cen = carve(H.n_nn ? 0 : 8 * H.n_cen);
+  H.l_bimg = carve(BI_WORDS * R);
+  H.l_cen = carve(8 * H.n_cen);
   H.env_words_m = (off + 63) & ~63;
   off = tail;
   H.l_rowd = carve(R * ROWD_STRIDE);
@@ -704,9 +707,17 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       const float rf = std::nextafter((float)reach, 3.0e38f);
       uint32_t* bw = &bimg[BI_WORDS * x];
       const bool skip = d->col_fn[g] == BX_COL_CAPSULE_CAPSULE;
-      if (skip) bw[BI_CEN] = (uint32_t)row_cen[2 * x] | ((uint32_t)row_cen[2 * x + 1] << 16);
+      const bool cull = d->col_cutoff[g] != 0;
+      if (skip || cull) bw[BI_CEN] = (uint32_t)row_cen[2 * x] | ((uint32_t)row_cen[2 * x + 1] << 16);
       std::memcpy(&bw[BI_REACH], &rf, 4);
-      bw[BI_SKIP] = skip ? 1u : 0u;
+      uint32_t fl = (skip ? BIF_SKIP : 0u) | (cull ? BIF_CULL : 0u) |
+                    (d->row_nn_masked && d->row_nn_masked[x] ? BIF_MASK : 0u);
+      if (!cull) {
+        // the unculled row's Info index (its group's first Info row + its offset)
+        const int og = H.o_group + g * GROUP_STRIDE;
+        fl |= (uint32_t)((int)B.w[og + G_INFO] + x - (int)B.w[og + G_R0]) << BIF_INFO_SHIFT;
+      }
+      bw[BI_FLAGS] = fl;
       bw[BI_BSLOT] = (uint32_t)mb[x];
     }
     H.o_bimg = B.alloc(BI_WORDS * R);

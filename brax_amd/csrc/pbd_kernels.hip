@@ -150,6 +150,21 @@ __device__ __forceinline__ v3 ld_v3a(const float* s) {
   return mk(a.x, a.y, a.z);
 }
 // qp_right_before records (RB_STRIDE): pos, vel, ang in 3 x b128
+// a MULTI contact slot: the linear part, the angular part (3 + 3 words; slot
+// k at 24 k bytes, so 8-byte accesses)
+__device__ __forceinline__ void st_mslot(float* s, v3 a, v3 l) {
+  float2* p = reinterpret_cast<float2*>(__builtin_assume_aligned(s, 8));
+  p[0] = float2{a.x, a.y};
+  p[1] = float2{a.z, l.x};
+  p[2] = float2{l.y, l.z};
+}
+__device__ __forceinline__ void ld_mslot(const float* s, v3& a, v3& l) {
+  const float2* p = reinterpret_cast<const float2*>(__builtin_assume_aligned(s, 8));
+  const float2 x = p[0], y = p[1], z = p[2];
+  a = mk(x.x, x.y, y.x);
+  l = mk(y.y, z.x, z.y);
+}
+
 __device__ __forceinline__ void st_rb(float* s, v3 p, v3 v, v3 a) {
   st4a(s, f32x4{p.x, p.y, p.z, v.x});
   st4a(s + 4, f32x4{v.y, v.z, a.x, a.y});
@@ -1590,6 +1605,22 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
+// v of lane ^ d within the wave (d = 1, 2, 4, 8 by DPP: quad permutes, row
+// shifts, the row rotation; 16, 32 by ds_bpermute)
+__device__ __forceinline__ unsigned lane_xor(unsigned v, int d) {
+  switch (d) {
+    case 1: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);   // quad_perm 1,0,3,2
+    case 2: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);   // quad_perm 2,3,0,1
+    case 4: {
+      const unsigned up = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, true);  // row_shl:4
+      const unsigned dn = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+      return (threadIdx.x & 4) ? dn : up;
+    }
+    case 8: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, true);  // row_ror:8
+    default: return (unsigned)__shfl_xor((int)v, d, 64);
+  }
+}
+
 // a candidate cell's selection key: (distance bits, row); distances are >= 0,
 // so their bit patterns order like the floats; a masked cell's sim is -inf,
 // its key (+inf's bits) sorts after every finite distance, ties in row =
@@ -1620,10 +1651,68 @@ __device__ __forceinline__ unsigned long long nn_key(const Cst& c, const BlobHdr
 // with several, each wave's sorted list goes to LDS and every listed key
 // counts the smaller keys of the other lists (its rank in the union).
 // Groups with more than NK candidates per lane take the serial pick.
+// MULTI: the centres (E.cen: n_cen (body, offset) words) placed in the world
+// from the env's current qp, at E.cen + n_cen (the caller syncs)
 template <int L>
-__device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane) {
+__device__ __forceinline__ void place_centres(const BlobHdr& H, const Env& E, int lane) {
+  uint4* cw = E.cen + H.n_cen;
+  for (int k = lane; k < H.n_cen; k += L) {
+    const uint4 cc = E.cen[k];
+    const float* qb = E.qp + (int)cc.x * QP_STRIDE;
+    const v3 p = ld3(qb) + rotate(mk(__uint_as_float(cc.y), __uint_as_float(cc.z),
+                                     __uint_as_float(cc.w)), ld_rot(qb));
+    cw[k] = make_uint4(__float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(p.z), 0u);
+  }
+}
+// a row's collidable-centre distance from the placed centres (nn_key's and
+// the broad phase's, same bits)
+__device__ __forceinline__ float centre_dist(const Env& E, const BlobHdr& H, unsigned pair) {
+  const uint4* cw = E.cen + H.n_cen;
+  const uint4 a4 = cw[pair & 0xFFFFu], b4 = cw[pair >> 16];
+  const v3 ca = mk(__uint_as_float(a4.x), __uint_as_float(a4.y), __uint_as_float(a4.z));
+  const v3 cb = mk(__uint_as_float(b4.x), __uint_as_float(b4.y), __uint_as_float(b4.z));
+  return norm(cb - ca);
+}
+
+#ifdef BX_MSTAMPS
+// (diagnostic: the MULTI stamps build splits the picks' phases into slots
+// 12-14 of the caller's accumulators)
+#define BX_NSTAMP(k)                                                               \
+  do {                                                                             \
+    if (nsa) {                                                                     \
+      __builtin_amdgcn_sched_barrier(0);                                           \
+      unsigned long long _t;                                                       \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");   \
+      __builtin_amdgcn_sched_barrier(0);                                           \
+      nsa[k] += _t - *nsl;                                                         \
+      *nsl = _t;                                                                   \
+    }                                                                              \
+  } while (0)
+#else
+#define BX_NSTAMP(k) do {} while (0)
+#endif
+// MT (the MULTI kernel): each row's group flags, Info index and centre pair
+// from the LDS-staged bounds (E.bimg), the keys' distances from the centres
+// placed this step (place_centres, before the call): no dependent L2 reads
+template <int L, bool MT = false>
+__device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane,
+                          unsigned long long* nsa = nullptr, unsigned long long* nsl = nullptr) {
   // Pairs rows are always active (rank 0) at their fixed Info index; culled
   // rows start unselected with empty (zero, uncounted) slots
+  if constexpr (MT) {
+    for (int r = lane; r < H.R; r += L) {
+      const uint4 g0 = E.bimg[r];
+      if (g0.z & BIF_CULL) {
+        E.ract[r] = -1;
+        const v3 z = mk(0.f, 0.f, 0.f);
+        st_mslot(E.cslot + r * MSLOT_STRIDE, z, z);
+        st_mslot(E.cslot + (int)g0.w * MSLOT_STRIDE, z, z);
+      } else {
+        E.ract[r] = 0;
+        E.alist[g0.z >> BIF_INFO_SHIFT] = r;
+      }
+    }
+  } else
   for (int r = lane; r < H.R; r += L) {
     const int og = H.o_group + c.i(H.o_row + r * ROW_STRIDE + R_GROUP) * GROUP_STRIDE;
     if (c.i(og + G_CUT)) {
@@ -1635,6 +1724,7 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
     }
   }
   esync<L>();
+  BX_NSTAMP(14);
   constexpr int W = L < 64 ? L : 64;  // the env's lanes in one wave
   constexpr int NW = L / W;           // the env's waves
   constexpr int NK = 4;               // candidates per lane held in registers
@@ -1650,7 +1740,17 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
 #pragma unroll
       for (int i = 0; i < NK; i++) {
         const int r = r0 + lane + i * L;
-        k[i] = r < r1 ? nn_key(c, H, E, r) : ~0ull;
+        if constexpr (MT) {
+          if (r < r1) {
+            const uint4 g0 = E.bimg[r];
+            const unsigned d = (g0.z & BIF_MASK) ? 0x7F800000u : __float_as_uint(centre_dist(E, H, g0.x));
+            k[i] = ((unsigned long long)d << 32) | (unsigned)r;
+          } else {
+            k[i] = ~0ull;
+          }
+        } else {
+          k[i] = r < r1 ? nn_key(c, H, E, r) : ~0ull;
+        }
       }
       // sorting network on the lane's keys
       auto cs = [](unsigned long long& a, unsigned long long& b) {
@@ -1659,7 +1759,50 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
         b = hi;
       };
       cs(k[0], k[1]); cs(k[2], k[3]); cs(k[0], k[2]); cs(k[1], k[3]); cs(k[1], k[2]);
+      BX_NSTAMP(12);
       unsigned long long* lst = reinterpret_cast<unsigned long long*>(E.nnl);
+      if constexpr (NW > 1) {
+        // each wave's 4 x 64 keys sorted ascending by a bitonic network
+        // (element 4 wl + q in lane wl's k[q]): the lane's sorted four are
+        // the size-4 blocks (odd lanes' reversed: descending), then per block
+        // size the lane-exchange strides (>= 4 elements: lane ^ stride / 4,
+        // two 32-bit lane swizzles per key) and the in-lane strides 2, 1.
+        // The union's order is the picks' (distance, then row: the 64-bit
+        // key); its first `cut` keys are the wave's list.
+        static_assert(NW == 1 || (W == 64 && NK == 4), "bitonic lists: 4 keys x 64 lanes");
+        if (wl & 1) {
+          const unsigned long long t0 = k[0], t1 = k[1];
+          k[0] = k[3]; k[1] = k[2]; k[2] = t1; k[3] = t0;
+        }
+        auto ced = [](unsigned long long& a, unsigned long long& b, bool up) {
+          const bool sw = up ? (b < a) : (a < b);
+          const unsigned long long x = a;
+          a = sw ? b : a;
+          b = sw ? x : b;
+        };
+#pragma unroll
+        for (int size = 8; size <= 256; size <<= 1) {
+          const bool up = ((wl * 4) & size) == 0;
+#pragma unroll
+          for (int d = size >> 3; d >= 1; d >>= 1) {
+            const bool keep_min = ((wl & d) == 0) == up;
+#pragma unroll
+            for (int q = 0; q < NK; q++) {
+              const unsigned lo = lane_xor((unsigned)k[q], d);
+              const unsigned hi = lane_xor((unsigned)(k[q] >> 32), d);
+              const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+              k[q] = keep_min ? (o < k[q] ? o : k[q]) : (o < k[q] ? k[q] : o);
+            }
+          }
+          ced(k[0], k[2], up); ced(k[1], k[3], up);
+          ced(k[0], k[1], up); ced(k[2], k[3], up);
+        }
+#pragma unroll
+        for (int q = 0; q < NK; q++)
+          if (4 * wl + q < cut) lst[wv * cut + 4 * wl + q] = k[q];
+        // (a cut past the wave's 256 keys: the rest of its list is empty)
+        for (int i = NK * W + wl; i < cut; i += W) lst[wv * cut + i] = ~0ull;
+      } else
       for (int kk = 0; kk < cut; kk++) {
         const unsigned long long cur = k[0];
         const unsigned hi = (unsigned)(cur >> 32), lo = (unsigned)cur;
@@ -1681,6 +1824,7 @@ __device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane
       }
       if constexpr (NW > 1) {
         esync<L>();
+        BX_NSTAMP(13);
         for (int t = lane; t < NW * cut; t += L) {
           const int w = t / cut, i = t % cut;
           const unsigned long long key = lst[t];
@@ -3029,21 +3173,6 @@ __device__ __forceinline__ void load_hoist_multi(const Cst& c, const BlobHdr& H,
 #endif
 }
 
-// a MULTI contact slot: the linear part, the angular part (3 + 3 words; slot
-// k at 24 k bytes, so 8-byte accesses)
-__device__ __forceinline__ void st_mslot(float* s, v3 a, v3 l) {
-  float2* p = reinterpret_cast<float2*>(__builtin_assume_aligned(s, 8));
-  p[0] = float2{a.x, a.y};
-  p[1] = float2{a.z, l.x};
-  p[2] = float2{l.y, l.z};
-}
-__device__ __forceinline__ void ld_mslot(const float* s, v3& a, v3& l) {
-  const float2* p = reinterpret_cast<const float2*>(__builtin_assume_aligned(s, 8));
-  const float2 x = p[0], y = p[1], z = p[2];
-  a = mk(x.x, x.y, y.x);
-  l = mk(y.y, z.x, z.y);
-}
-
 // phase 1: the lane's task partial, its slots summed in list order; a slot
 // counts when its linear part is nonzero (the reference's any(dq_pos) /
 // any(dp_vel) per row, colliders.py:187-195,231-239)
@@ -3123,7 +3252,7 @@ template <int L, int F, int MR>
 __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
                                const float* act, int aw, const HoistM<MR>& X, RowInfoOut io) {
 #ifdef BX_MSTAMPS
-  unsigned long long ms_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ms_acc[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long ms_last;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ms_last)::"memory");
 #endif
@@ -3152,7 +3281,15 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
   }
   // NearNeighbors.update once per step (system.py:320-321): ranks in E.ract,
   // culled rows' slots zeroed (their lanes skip them below)
-  if (H.n_nn) nn_select<L>(c, H, E, lane);
+  if (H.n_nn) {
+    place_centres<L>(H, E, lane);
+    esync<L>();
+#ifdef BX_MSTAMPS
+    nn_select<L, true>(c, H, E, lane, ms_acc, &ms_last);
+#else
+    nn_select<L, true>(c, H, E, lane);
+#endif
+  }
   BX_MSTAMP(9);
   // the lane's rows: the m-th is active row x = lane + m * L in Info order
   // (the culled scenes' selected rows compacted: E.alist), so lanes past
@@ -3301,14 +3438,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       const int wv = lane >> 6;
       int* cnt = E.nearc;
       // the capsule centres in the world, once for every row naming them
-      uint4* cw = E.cen + H.n_cen;
-      for (int k = lane; k < H.n_cen; k += L) {
-        const uint4 cc = E.cen[k];
-        const float* qb = E.qp + (int)cc.x * QP_STRIDE;
-        const v3 p = ld3(qb) + rotate(mk(__uint_as_float(cc.y), __uint_as_float(cc.z),
-                                         __uint_as_float(cc.w)), ld_rot(qb));
-        cw[k] = make_uint4(__float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(p.z), 0u);
-      }
+      place_centres<L>(H, E, lane);
       esync<L>();
       bool nr[MR];
       int rr[MR], rk[MR];
@@ -3319,13 +3449,10 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
         bool near = false;
         if (r >= 0) {
           const uint4 g0 = E.bimg[r];
-          near = g0.z == 0u;
+          near = (g0.z & BIF_SKIP) == 0u;
           if (!near) {
-            const uint4 a4 = cw[g0.x & 0xFFFFu], b4 = cw[g0.x >> 16];
-            const v3 ca = mk(__uint_as_float(a4.x), __uint_as_float(a4.y), __uint_as_float(a4.z));
-            const v3 cb = mk(__uint_as_float(b4.x), __uint_as_float(b4.y), __uint_as_float(b4.z));
             // + 1e-4: far above the fp32 error of the centres
-            near = !(norm(cb - ca) > __uint_as_float(g0.y) + 1e-4f);
+            near = !(centre_dist(E, H, g0.x) > __uint_as_float(g0.y) + 1e-4f);
           }
           if (!near) {
             // (a one-way row's b slot is the zero slot: zeros again)
@@ -3496,7 +3623,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
 #ifdef BX_MSTAMPS
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int k = 0; k < 14; k++) bx_mstamp_wave[blockIdx.x & 4095][k] += ms_acc[k];
+    for (int k = 0; k < 15; k++) bx_mstamp_wave[blockIdx.x & 4095][k] += ms_acc[k];
     bx_mstamp_wave[blockIdx.x & 4095][15] += 1ull;
   }
 #endif
@@ -4110,8 +4237,8 @@ __device__ __forceinline__ void system_step_body(const StepArgs& A) {
     // M = contact rows per lane
     HoistM<M> X;
     load_hoist_multi<L, M, (F & F_JH) != 0>(c, H, lane, X);
-    // the broad phase's constants into LDS, read by every pass
-    if (H.o_bimg != 0 && H.n_nn == 0) {
+    // the broad phase's / NearNeighbors' constants into LDS, read by every pass
+    if (H.o_bimg != 0) {
       const uint4* bg = reinterpret_cast<const uint4*>(c.w + H.o_bimg);
       for (int r = lane; r < H.R; r += L) E.bimg[r] = bg[r];
       const uint4* cg = reinterpret_cast<const uint4*>(c.w + H.o_cen);

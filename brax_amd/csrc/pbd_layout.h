@@ -197,7 +197,7 @@ enum { MP_FRIC = 0, MP_ELAS = 1, MP_SCALE = 2, MP_THR = 3, MP_MA = 4, MP_MB = 5,
        MP_WORDS = 12 };
 // MULTI-mode broad phase: per row one 16-byte group at o_bimg + 4 r (staged
 // in LDS at l_bimg once per launch): (centre a | centre b << 16, reach,
-// may_skip, b slot). A capsule-capsule row whose capsule centres lie farther
+// flags, b slot). A capsule-capsule row whose capsule centres lie farther
 // apart than reach (half segments + radii, rounded up) cannot penetrate, and
 // its position / velocity updates are exact zeros. The centres are the
 // distinct (body, offset) pairs of the rows' capsules, 16 bytes each at
@@ -205,7 +205,12 @@ enum { MP_FRIC = 0, MP_ELAS = 1, MP_SCALE = 2, MP_THR = 3, MP_MA = 4, MP_MB = 5,
 // places them in the world once (l_cen + 4 n_cen + 4 k) for every row that
 // names them. BI_BSLOT: the row's b-side slot (two-way rows; one-way rows:
 // the zero slot).
-enum { BI_CEN = 0, BI_REACH = 1, BI_SKIP = 2, BI_BSLOT = 3, BI_WORDS = 4 };
+// BI_FLAGS: bit 0 may_skip (capsule-capsule), bit 1 the row's group is
+// culled (NearNeighbors), bit 2 a masked cell (R_NNMASK), bits 8.. a row of
+// an unculled group: its Info index. Culled scenes (no broad phase) stage the
+// same image: their NearNeighbors keys take the centres too.
+enum { BI_CEN = 0, BI_REACH = 1, BI_FLAGS = 2, BI_BSLOT = 3, BI_WORDS = 4 };
+enum { BIF_SKIP = 1, BIF_CULL = 2, BIF_MASK = 4, BIF_INFO_SHIFT = 8 };
 enum { HULL_STRIDE = 114, HULL_V = 0, HULL_F = 24, HULL_N = 96 };
 
 }  // namespace bx

@@ -26,13 +26,14 @@ def test_ant_mountain4_runs_two_envs_per_cu(cutoff):
   the register file sets the residency. With all pairs (cutoff 0) the broad
   phase's row bounds and capsule centres sit in LDS too (round 5: 16 bytes per
   row, staged once per launch), which the second workgroup's share still
-  holds; the culled scene (cutoff 36) has no broad phase and would fit three."""
+  holds; the culled scene (cutoff 36) stages the same image for its
+  NearNeighbors keys (two by either count too)."""
   cfg = config_for('mountain4')
   cfg.collider_cutoff = cutoff
   p = System.plan(cfg)
   assert p['mode'] == 3 and p['lanes'] == 256, p
   assert p['lds_bytes'] * 2 <= LDS_CU, p
-  assert p['envs_per_cu_by_lds'] == (2 if cutoff == 0 else 3), p
+  assert p['envs_per_cu_by_lds'] == 2, p
   assert p['envs_per_cu_by_registers'] == 2 and p['envs_per_cu'] == 2, p
 
 
