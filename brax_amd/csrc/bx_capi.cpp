@@ -535,21 +535,26 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     H.nnl_words = 2 * 4 * max_cut;
     H.l_nnl = carve(H.nnl_words);
   }
-  // the MULTI broad phase's capsule centres: the distinct (body, offset)
-  // pairs of the capsule-capsule rows' and the culled groups' rows' two
-  // collidables (the bits the per-row centres rotate), placed in the world
-  // once per pass (culled scenes: once per step, for the NearNeighbors keys)
-  // for every row naming them
-  std::map<std::array<uint32_t, 4>, int> cen_ix;
-  std::vector<std::array<uint32_t, 4>> cens;
+  // the MULTI kernel's row tables: the rows' collidables as the distinct
+  // (body, offset, end, radius) records, whose centres the broad phase and
+  // the NearNeighbors keys place in the world once per pass (culled scenes:
+  // once per step) for every row naming them, and from which the contact
+  // passes assemble a row's geometry in LDS
+  std::map<std::array<uint32_t, 8>, int> cen_ix;
+  std::vector<std::array<uint32_t, 8>> cens;
   std::vector<int> row_cen(2 * R, 0);
+  // and the rows' impulse constants as the distinct (friction, elasticity,
+  // scale, velocity threshold) materials
+  std::map<std::array<uint32_t, 4>, int> mat_ix;
+  std::vector<std::array<uint32_t, 4>> mats;
+  std::vector<int> row_mat(R, 0);
   for (int x = 0; x < R; x++) {
-    const int g = d->row_group[x];
-    if (d->col_fn[g] != BX_COL_CAPSULE_CAPSULE && d->col_cutoff[g] == 0) continue;
+    // (the row record's words: the bits the row image carried)
+    const uint32_t* w = &B.w[H.o_row + x * ROW_STRIDE];
     for (int side = 0; side < 2; side++) {
-      const int body = side ? d->row_body_b[x] : d->row_body_a[x];
-      const double* o = side ? &d->row_b_pos[3 * x] : &d->row_a_pos[3 * x];
-      const std::array<uint32_t, 4> k{(uint32_t)body, fbits(o[0]), fbits(o[1]), fbits(o[2])};
+      const int o = side ? R_BPOS : R_APOS, oe = side ? R_BEND : R_AEND, orr = side ? R_BRAD : R_ARAD;
+      const std::array<uint32_t, 8> k{w[side ? R_B : R_A], w[o], w[o + 1], w[o + 2],
+                                      w[oe], w[oe + 1], w[oe + 2], w[orr]};
       auto it = cen_ix.find(k);
       if (it == cen_ix.end()) {
         it = cen_ix.emplace(k, (int)cens.size()).first;
@@ -557,9 +562,18 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       }
       row_cen[2 * x + side] = it->second;
     }
+    const std::array<uint32_t, 4> m{w[R_FRIC], w[R_ELAS], w[R_SCALE], w[R_THR]};
+    auto it = mat_ix.find(m);
+    if (it == mat_ix.end()) {
+      it = mat_ix.emplace(m, (int)mats.size()).first;
+      mats.push_back(m);
+    }
+    row_mat[x] = it->second;
   }
-  if (cens.size() > 0xFFFF) return fail("too many broad-phase capsule centres");
+  if (cens.size() > 0xFFFF || mats.size() > 0xFF || R > 0xFFFF)
+    return fail("too many collidables, materials or rows for the MULTI row tables");
   H.n_cen = (int)cens.size();
+  H.n_mat = (int)mats.size();
   // the MULTI (System.step only) tail starts here, over the env step's regions
   const int tail_m = off;
   // env-step regions: joint angles, the env programs' System.step action
@@ -587,7 +601,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // the broad phase's row bounds and centres (constants, then world), staged
   // once per launch
   H.l_bimg = carve(BI_WORDS * R);
-  H.l_cen = carve(8 * H.n_cen);
+  H.l_cen = carve(4 * (3 * H.n_cen + H.n_mat + N));
   H.env_words_m = (off + 63) & ~63;
   off = tail;
   H.l_rowd = carve(R * ROWD_STRIDE);
@@ -660,38 +674,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       out[LR_IB + k] = pb[BODY_I + k];
     }
   };
-  // the MULTI-mode row image: every row's resolved words, 16-byte group g of
-  // row r at o_rimg + (g * R + r) * 4 (one round of independent loads per row
-  // and pass instead of record -> referenced body)
+  // the MULTI kernel's row tables (BI_*: bounds / flags per row; collidables,
+  // materials and bodies after them)
   if (H.multi && R > 0) {
     B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
-    H.o_rimg = B.alloc(MG_WORDS * R);
-    H.o_rphys = B.alloc(MP_WORDS * R);
-    uint32_t rw[32];
-    for (int x = 0; x < R; x++) {
-      row_words(x, rw);
-      uint32_t g[MG_WORDS], p[MP_WORDS];
-      g[MG_AB] = (rw[LR_A] & 0xFFFFu) | (rw[LR_B] << 16);
-      g[MG_META] = (rw[LR_FN] & 0xFFu) | ((rw[LR_OW] & 0xFFu) << 8) | ((uint32_t)mb[x] << 16);
-      for (int k = 0; k < 3; k++) {
-        g[MG_APOS + k] = rw[LR_APOS + k];
-        g[MG_AEND + k] = rw[LR_AEND + k];
-        g[MG_BPOS + k] = rw[LR_BPOS + k];
-        g[MG_BEND + k] = rw[LR_BEND + k];
-        p[MP_IA + k] = rw[LR_IA + k];
-        p[MP_IB + k] = rw[LR_IB + k];
-      }
-      g[MG_ARAD] = rw[LR_ARAD];
-      g[MG_BRAD] = rw[LR_BRAD];
-      p[MP_FRIC] = rw[LR_FRIC];
-      p[MP_ELAS] = rw[LR_ELAS];
-      p[MP_SCALE] = rw[LR_SCALE];
-      p[MP_THR] = rw[LR_THR];
-      p[MP_MA] = rw[LR_MA];
-      p[MP_MB] = rw[LR_MB];
-      for (int k = 0; k < MG_WORDS; k++) B.w[H.o_rimg + ((k / 4) * R + x) * 4 + k % 4] = g[k];
-      for (int k = 0; k < MP_WORDS; k++) B.w[H.o_rphys + ((k / 4) * R + x) * 4 + k % 4] = p[k];
-    }
     // broad-phase bounds (BI_*): reach = |a_end| + |b_end| + radii in double,
     // rounded up to float
     std::vector<uint32_t> bimg(BI_WORDS * R, 0u);
@@ -708,10 +694,12 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       uint32_t* bw = &bimg[BI_WORDS * x];
       const bool skip = d->col_fn[g] == BX_COL_CAPSULE_CAPSULE;
       const bool cull = d->col_cutoff[g] != 0;
-      if (skip || cull) bw[BI_CEN] = (uint32_t)row_cen[2 * x] | ((uint32_t)row_cen[2 * x + 1] << 16);
+      bw[BI_CEN] = (uint32_t)row_cen[2 * x] | ((uint32_t)row_cen[2 * x + 1] << 16);
       std::memcpy(&bw[BI_REACH], &rf, 4);
       uint32_t fl = (skip ? BIF_SKIP : 0u) | (cull ? BIF_CULL : 0u) |
-                    (d->row_nn_masked && d->row_nn_masked[x] ? BIF_MASK : 0u);
+                    (d->row_nn_masked && d->row_nn_masked[x] ? BIF_MASK : 0u) |
+                    (d->col_oneway[g] ? BIF_OW : 0u) | ((uint32_t)d->col_fn[g] << BIF_FN_SHIFT) |
+                    ((uint32_t)row_mat[x] << BIF_MAT_SHIFT);
       if (!cull) {
         // the unculled row's Info index (its group's first Info row + its offset)
         const int og = H.o_group + g * GROUP_STRIDE;
@@ -722,9 +710,17 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     }
     H.o_bimg = B.alloc(BI_WORDS * R);
     for (int k = 0; k < BI_WORDS * R; k++) B.w[H.o_bimg + k] = bimg[k];
-    H.o_cen = B.alloc(4 * H.n_cen);
+    H.o_cen = B.alloc(8 * H.n_cen + 4 * H.n_mat + 4 * N);
     for (int k = 0; k < H.n_cen; k++)
-      for (int i = 0; i < 4; i++) B.w[H.o_cen + 4 * k + i] = cens[k][i];
+      for (int i = 0; i < 8; i++) B.w[H.o_cen + 8 * k + i] = cens[k][i];
+    const int o_mat = H.o_cen + 8 * H.n_cen, o_bod = o_mat + 4 * H.n_mat;
+    for (int k = 0; k < H.n_mat; k++)
+      for (int i = 0; i < 4; i++) B.w[o_mat + 4 * k + i] = mats[k][i];
+    // the bodies' (mass, inverse inertia), the rows' ma / Ia / mb / Ib
+    for (int b = 0; b < N; b++) {
+      B.w[o_bod + 4 * b] = B.w[H.o_body + b * BODY_STRIDE + BODY_MASS];
+      for (int i = 0; i < 3; i++) B.w[o_bod + 4 * b + 1 + i] = B.w[H.o_body + b * BODY_STRIDE + BODY_I + i];
+    }
   }
   // the SINGLE-mode lane image (pbd_layout.h LI_*): copies of the records
   // above, so its words are the same bits the item-loop kernels read; a lane
@@ -814,14 +810,15 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   };
   // the MULTI kernel's joint halves (MJ_*): revolute joints each driven by
   // the torque actuator of its index, <= 128 joints (16 lanes per 8)
+  bool mjh = false;
   {
     bool ok = H.multi && J > 0 && J <= 128 && K == J && H.act_same;
     for (int j = 0; j < J; j++) ok = ok && d->joint_type[j] == BX_JOINT_REVOLUTE;
     for (int a = 0; a < K; a++) ok = ok && d->act_type[a] == BX_ACT_TORQUE;
     const bool off = getenv("BX_NO_MULTI_JH") && atoi(getenv("BX_NO_MULTI_JH"));
-    H.mjh = ok && !off ? 1 : 0;
+    mjh = ok && !off;
   }
-  if (H.mjh) {
+  if (mjh) {
     B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
     H.o_mjh = B.alloc(MJ_W * MJ_LANES);
     auto putm = [&](int lane, int w, uint32_t v) {
@@ -1239,7 +1236,7 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   if (S->mode == 1)
     HIP_OK(launch_system_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   else if (S->mode == 3)
-    HIP_OK(launch_system_step_multi(S->feat | (S->hdr.mjh ? 128 : 0), (S->hdr.R + 255) / 256, n_envs,
+    HIP_OK(launch_system_step_multi(S->feat | (S->hdr.o_mjh ? 128 : 0), (S->hdr.R + 255) / 256, n_envs,
                                     step_lds(S), as_stream(stream), a));
   else
     HIP_OK(launch_system_step_generic(S->L, S->mode, S->feat, S->tpb, n_envs, step_lds(S), as_stream(stream), a));

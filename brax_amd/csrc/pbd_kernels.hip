@@ -88,8 +88,10 @@ struct Env {
   float* nnl;    // NearNeighbors per-wave pick lists (nnl_words)
   uint16_t* nearl;  // MULTI: the pass's near rows
   int* nearc;       // MULTI: the broad phase's per-wave counts
-  uint4* bimg;      // MULTI: the rows' broad-phase bounds (BI_*), staged per launch
-  uint4* cen;       // MULTI: the capsule centres' (body, offset), then their world points
+  uint4* bimg;      // MULTI: the rows' bounds / flags (BI_*), staged per launch
+  uint4* cen;       // MULTI: the collidables (2 groups each)
+  uint4* mat;       // MULTI: the materials (fric, elas, scale, thr)
+  uint4* bod;       // MULTI: the bodies' (mass, inverse inertia), then the placed centres
   uint4* jlim;   // SINGLE spherical kernels: the lanes' limit rows, [6][L] groups
 };
 
@@ -1518,6 +1520,8 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi =
     E.nearc = reinterpret_cast<int*>(base + H.l_nearc);
     E.bimg = reinterpret_cast<uint4*>(al16(base + H.l_bimg));
     E.cen = reinterpret_cast<uint4*>(al16(base + H.l_cen));
+    E.mat = E.cen + 2 * H.n_cen;
+    E.bod = E.mat + H.n_mat;
     E.sstride = MSLOT_STRIDE;
     E.nd = E.tslot;
     E.nds = 1;
@@ -1554,16 +1558,9 @@ __device__ __forceinline__ void esync() {
   if constexpr (L > 64) __syncthreads(); else sync();
 }
 
-// a culled row's slots: no update, not counted (MULTI: 6-word slots, the b
-// side at the row image's compact slot index)
+// a culled row's slots: no update, not counted (the item-loop kernels; the
+// MULTI kernel's NearNeighbors zeroes its 6-word slots from its row tables)
 __device__ __forceinline__ void zero_row_slots(const Cst& c, const BlobHdr& H, const Env& E, int r) {
-  if (E.tslot) {
-    float* sa = E.cslot + r * MSLOT_STRIDE;
-    const int b = (int)((uint32_t)c.i(H.o_rimg + ((MG_META / 4) * H.R + r) * 4 + MG_META % 4) >> 16);
-    float* sb = E.cslot + b * MSLOT_STRIDE;
-    for (int k = 0; k < MSLOT_STRIDE; k++) { sa[k] = 0.f; sb[k] = 0.f; }
-    return;
-  }
   float* sa = E.cslot + r * E.sstride;
   float* sb = E.cslot + (E.nR + r) * E.sstride;
   for (int k = 0; k < 8; k++) { sa[k] = 0.f; sb[k] = 0.f; }
@@ -1651,13 +1648,14 @@ __device__ __forceinline__ unsigned long long nn_key(const Cst& c, const BlobHdr
 // with several, each wave's sorted list goes to LDS and every listed key
 // counts the smaller keys of the other lists (its rank in the union).
 // Groups with more than NK candidates per lane take the serial pick.
-// MULTI: the centres (E.cen: n_cen (body, offset) words) placed in the world
-// from the env's current qp, at E.cen + n_cen (the caller syncs)
+// MULTI: the collidables' centres (E.cen: n_cen (body, offset | end, radius)
+// records) placed in the world from the env's current qp, after the bodies'
+// table (the caller syncs)
 template <int L>
 __device__ __forceinline__ void place_centres(const BlobHdr& H, const Env& E, int lane) {
-  uint4* cw = E.cen + H.n_cen;
+  uint4* cw = E.bod + H.N;
   for (int k = lane; k < H.n_cen; k += L) {
-    const uint4 cc = E.cen[k];
+    const uint4 cc = E.cen[2 * k];
     const float* qb = E.qp + (int)cc.x * QP_STRIDE;
     const v3 p = ld3(qb) + rotate(mk(__uint_as_float(cc.y), __uint_as_float(cc.z),
                                      __uint_as_float(cc.w)), ld_rot(qb));
@@ -1667,11 +1665,44 @@ __device__ __forceinline__ void place_centres(const BlobHdr& H, const Env& E, in
 // a row's collidable-centre distance from the placed centres (nn_key's and
 // the broad phase's, same bits)
 __device__ __forceinline__ float centre_dist(const Env& E, const BlobHdr& H, unsigned pair) {
-  const uint4* cw = E.cen + H.n_cen;
+  const uint4* cw = E.bod + H.N;
   const uint4 a4 = cw[pair & 0xFFFFu], b4 = cw[pair >> 16];
   const v3 ca = mk(__uint_as_float(a4.x), __uint_as_float(a4.y), __uint_as_float(a4.z));
   const v3 cb = mk(__uint_as_float(b4.x), __uint_as_float(b4.y), __uint_as_float(b4.z));
   return norm(cb - ca);
+}
+
+// MULTI: contact row r's record from the LDS tables (its flags / b slot, its
+// two collidables, their bodies' masses and inverse inertias, its
+// material): the words the row image held, with no L2 read
+__device__ __forceinline__ RowC row_from_lds(const Env& E, int r) {
+  const uint4 g0 = E.bimg[r];
+  const uint4 a0 = E.cen[2 * (g0.x & 0xFFFFu)], a1 = E.cen[2 * (g0.x & 0xFFFFu) + 1];
+  const uint4 b0 = E.cen[2 * (g0.x >> 16)], b1 = E.cen[2 * (g0.x >> 16) + 1];
+  const uint4 mt = E.mat[(g0.z >> BIF_MAT_SHIFT) & 0xFFu];
+  RowC x;
+  x.group = 0;  // (no MULTI pass reads the group)
+  x.a = (int)a0.x;
+  x.b = (int)b0.x;
+  x.fn = (int)((g0.z >> BIF_FN_SHIFT) & 0xFu);
+  x.oneway = (g0.z & BIF_OW) ? 1 : 0;
+  x.bslot = (int)g0.w;
+  x.a_pos = mk(__uint_as_float(a0.y), __uint_as_float(a0.z), __uint_as_float(a0.w));
+  x.a_end = mk(__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z));
+  x.a_rad = __uint_as_float(a1.w);
+  x.b_pos = mk(__uint_as_float(b0.y), __uint_as_float(b0.z), __uint_as_float(b0.w));
+  x.b_end = mk(__uint_as_float(b1.x), __uint_as_float(b1.y), __uint_as_float(b1.z));
+  x.b_rad = __uint_as_float(b1.w);
+  x.fric = __uint_as_float(mt.x);
+  x.elas = __uint_as_float(mt.y);
+  x.scale = __uint_as_float(mt.z);
+  x.thr = __uint_as_float(mt.w);
+  const uint4 ba = E.bod[x.a], bb = E.bod[x.b];
+  x.ma = __uint_as_float(ba.x);
+  x.mb = __uint_as_float(bb.x);
+  x.Ia = mk(__uint_as_float(ba.y), __uint_as_float(ba.z), __uint_as_float(ba.w));
+  x.Ib = mk(__uint_as_float(bb.y), __uint_as_float(bb.z), __uint_as_float(bb.w));
+  return x;
 }
 
 #ifdef BX_MSTAMPS
@@ -1694,8 +1725,10 @@ __device__ __forceinline__ float centre_dist(const Env& E, const BlobHdr& H, uns
 // MT (the MULTI kernel): each row's group flags, Info index and centre pair
 // from the LDS-staged bounds (E.bimg), the keys' distances from the centres
 // placed this step (place_centres, before the call): no dependent L2 reads
+// (always inlined: a call would take the caller's header by reference and
+// put the whole struct in scratch, reloaded in every phase of the MULTI loop)
 template <int L, bool MT = false>
-__device__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane,
+__device__ __forceinline__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane,
                           unsigned long long* nsa = nullptr, unsigned long long* nsl = nullptr) {
   // Pairs rows are always active (rank 0) at their fixed Info index; culled
   // rows start unselected with empty (zero, uncounted) slots
@@ -3035,53 +3068,7 @@ struct HoistM {
   GList<MAXG> jl, al;
   int te[TASK_W];   // the lane's task: contact slot indices (padding: the zero slot)
   int bt[BTASK_W];  // the lane's body: task | group << 24 (padding: the zero task)
-#if defined(BX_MULTI_HOIST_ROWS)
-  RowC R[MR];
-#endif
 };
-// a lane's m-th row constants, read from the L2-resident blob at each pass:
-// at <= 256 VGPRs the kernel runs two waves per SIMD (two envs per CU), which
-// hides those loads. Measured (Ant Mountain(4), 2048 envs, rows per lane 3):
-// 0.44 ms per step, against 0.68 ms with the rows hoisted into registers
-// (BX_MULTI_HOIST_ROWS: 256 VGPRs + 78 AGPRs, one wave per SIMD).
-// row r's geometry from the MULTI row image (bx_capi.cpp, pbd_layout.h MG_*):
-// four independent 16-byte loads, consecutive rows' groups adjacent; what
-// contact_gen reads and the slot word. The impulse constants (MP_*, three
-// loads) complete the record for the position pass; the velocity pass reads
-// neither part for a row that does not penetrate (it stores exact zeros from
-// the slot word the position pass kept). 7 loads per near row and pass where
-// the 32-word record took 8 on both passes
-__device__ __forceinline__ RowC load_row_geo(const Cst& c, const BlobHdr& H, int r) {
-  const uint4* im = reinterpret_cast<const uint4*>(c.w + H.o_rimg) + r;
-  const uint4 g0 = im[0], g1 = im[H.R], g2 = im[2 * H.R], g3 = im[3 * H.R];
-  RowC x;
-  x.group = 0;  // (no MULTI pass reads the group)
-  x.a = (int)(g0.x & 0xFFFFu);
-  x.b = (int)(g0.x >> 16);
-  x.fn = (int)(g0.y & 0xFFu);
-  x.oneway = (int)((g0.y >> 8) & 0xFFu);
-  x.bslot = (int)(g0.y >> 16);  // (the MULTI image carries no erp)
-  x.a_pos = mk(__uint_as_float(g0.z), __uint_as_float(g0.w), __uint_as_float(g1.x));
-  x.a_end = mk(__uint_as_float(g1.y), __uint_as_float(g1.z), __uint_as_float(g1.w));
-  x.a_rad = __uint_as_float(g2.x);
-  x.b_pos = mk(__uint_as_float(g2.y), __uint_as_float(g2.z), __uint_as_float(g2.w));
-  x.b_end = mk(__uint_as_float(g3.x), __uint_as_float(g3.y), __uint_as_float(g3.z));
-  x.b_rad = __uint_as_float(g3.w);
-  return x;
-}
-__device__ __forceinline__ void load_row_phys(const Cst& c, const BlobHdr& H, int r, RowC& x) {
-  const uint4* im = reinterpret_cast<const uint4*>(c.w + H.o_rphys) + r;
-  const uint4 p0 = im[0], p1 = im[H.R], p2 = im[2 * H.R];
-  x.fric = __uint_as_float(p0.x);
-  x.elas = __uint_as_float(p0.y);
-  x.scale = __uint_as_float(p0.z);
-  x.thr = __uint_as_float(p0.w);
-  x.ma = __uint_as_float(p1.x);
-  x.mb = __uint_as_float(p1.y);
-  x.Ia = mk(__uint_as_float(p1.z), __uint_as_float(p1.w), __uint_as_float(p2.x));
-  x.Ib = mk(__uint_as_float(p2.y), __uint_as_float(p2.z), __uint_as_float(p2.w));
-}
-
 // MJH: the lane's joint side from the MULTI joint-halves image (MJ_*, 20
 // independent 16-byte loads), parsed as the SINGLE lane image's records
 template <int MR>
@@ -3162,15 +3149,6 @@ __device__ __forceinline__ void load_hoist_multi(const Cst& c, const BlobHdr& H,
     if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? lane : 0);
     if (H.K > 0) X.A = load_act(c, H, X.hasA ? lane : 0);
   }
-#if defined(BX_MULTI_HOIST_ROWS)
-#pragma unroll
-  for (int m = 0; m < MR; m++) {
-    const int r = lane + m * L;
-    const int rr = r < H.R ? r : 0;
-    X.R[m] = load_row(c, H, rr);
-    X.R[m].bslot = (int)((uint32_t)c.i(H.o_rimg + ((MG_META / 4) * H.R + rr) * 4 + MG_META % 4) >> 16);
-  }
-#endif
 }
 
 // phase 1: the lane's task partial, its slots summed in list order; a slot
@@ -3294,15 +3272,9 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
   // the lane's rows: the m-th is active row x = lane + m * L in Info order
   // (the culled scenes' selected rows compacted: E.alist), so lanes past
   // the active count, and whole waves, skip the contact passes
-#if defined(BX_MULTI_HOIST_ROWS)
-  const int nact = H.R;  // hoisted rows are fixed per lane: no compaction
-#define BX_MULTI_RX(x) (x)
-#define BX_MULTI_SKIP(x, r) ((x) >= H.R || !row_active(H, E, r))
-#else
   const int nact = H.n_nn ? H.info_rows : H.R;
 #define BX_MULTI_RX(x) (H.n_nn ? E.alist[x] : (x))
 #define BX_MULTI_SKIP(x, r) ((x) >= nact)
-#endif
   // the row's contact between the position and velocity passes, and its
   // slot word (one-way flag, b-side slot) for the velocity pass's stores
   v3 cpos[MR], cn[MR];
@@ -3423,15 +3395,11 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
     // reach cannot penetrate, so both its passes' updates are exact zeros;
     // its slots are zeroed here and the pair left out of both passes. The
     // near rows are listed in (m, wave, lane) order (E.nearl).
-#if defined(BX_MULTI_HOIST_ROWS)
-    const bool bph = false;
-#else
     // (culled scenes skip it: NearNeighbors already keeps only near cells).
     // Without contact-row Info (System.step(..., info=False): no caller
     // reads the rows) the last pass takes it too: its far rows' Info is never
     // written
     const bool bph = H.o_bimg != 0 && H.n_nn == 0 && (it + 1 < H.substeps / 2 || !info_rows);
-#endif
     int nwork = nact;
     if (bph) {
       constexpr int NWV = L / 64;
@@ -3496,15 +3464,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       const int x = lane + m * L;
       const int r = x < nwork ? (bph ? E.nearl[x] : BX_MULTI_RX(x)) : 0;
       if (bph ? x >= nwork : BX_MULTI_SKIP(x, r)) continue;
-#if defined(BX_MULTI_HOIST_ROWS)
-      const RowC& R = X.R[m];
-#else
-      // (both parts issued together: the impulse constants loaded behind
-      // contact_gen, for penetrating rows only, exposed their latency there
-      // and measured 1.5 % slower)
-      RowC R = load_row_geo(c, H, r);
-      load_row_phys(c, H, r, R);
-#endif
+      RowC R = row_from_lds(E, r);
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 cvel;
       contact_gen<F>(R, a, b, cpos[m], cvel, cn[m], pen[m]);
@@ -3557,12 +3517,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       // colliders.py:584-658): no constants read, no state gathered
       v3 oav = mk(0.f, 0.f, 0.f), oaa = oav, obv = oav, oba = oav;
       if (pen[m] > 0.f) {
-#if defined(BX_MULTI_HOIST_ROWS)
-        const RowC& R = X.R[m];
-#else
-        RowC R = load_row_geo(c, H, r);
-        load_row_phys(c, H, r, R);
-#endif
+        RowC R = row_from_lds(E, r);
         QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
         v3 rap, rav, raa, rbp, rbv, rba;
         ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
@@ -3594,16 +3549,9 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
   if (valid && info_rows) {
 #pragma unroll
     for (int m = 0; m < MR; m++) {
-#if defined(BX_MULTI_HOIST_ROWS)
-      const int r = lane + m * L;
-      if (r >= H.R) continue;
-      const int x = row_info(c, H, E, r);
-      if (x < 0) continue;
-#else
       const int x = lane + m * L;
       if (x >= nact) continue;
       const int r = BX_MULTI_RX(x);
-#endif
       if (io.pos) st3(io.pos + x * 3, cpos[m]);
       if (io.normal) st3(io.normal + x * 3, cn[m]);
       if (io.pen) io.pen[x] = pen[m];
@@ -4242,7 +4190,7 @@ __device__ __forceinline__ void system_step_body(const StepArgs& A) {
       const uint4* bg = reinterpret_cast<const uint4*>(c.w + H.o_bimg);
       for (int r = lane; r < H.R; r += L) E.bimg[r] = bg[r];
       const uint4* cg = reinterpret_cast<const uint4*>(c.w + H.o_cen);
-      for (int k = lane; k < H.n_cen; k += L) E.cen[k] = cg[k];
+      for (int k = lane; k < 2 * H.n_cen + H.n_mat + H.N; k += L) E.cen[k] = cg[k];
     }
     const int64_t ro = valid ? e * H.info_rows : 0;
     RowInfoOut io{A.info.contact_pos ? A.info.contact_pos + ro * 3 : nullptr,

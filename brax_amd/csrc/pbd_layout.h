@@ -101,16 +101,15 @@ struct BlobHdr {
   int32_t o_lane;                    // SINGLE mode: the lane image (below); 0 = none
   int32_t l_arow, act_read;          // LDS: the env's action row, the words any step reads
   int32_t l_nnl, nnl_words;          // LDS: NearNeighbors per-wave pick lists (envs over several waves)
-  int32_t o_rimg;                    // MULTI mode: the row image (32 resolved words per row, LR_*)
   int32_t o_bimg;                    // MULTI mode: the rows' broad-phase bounds (BI_*), 0 = none
   int32_t l_near;                    // LDS (MULTI, all-pairs scenes): the pass's near rows (R, 16-bit)
   int32_t l_jlim;                    // LDS (SINGLE, spherical kernels): each lane's joint limit rows
   int32_t m_zero;                    // MULTI: the zero contact slot (R + two-way rows)
   int32_t l_nearc;                   // LDS (MULTI): the broad phase's per-wave counts (16)
-  int32_t o_rphys;                   // MULTI mode: the rows' impulse constants (MP_*)
   int32_t n_cen, o_cen;              // MULTI broad phase: the capsule centres (body, offset)
   int32_t l_bimg, l_cen;             // LDS (MULTI broad phase): the rows' bounds, the centres
-  int32_t mjh, o_mjh;                // MULTI joint halves: the image (MJ_*) of lane l's joint side
+  int32_t o_mjh;                     // MULTI joint halves: the image (MJ_*) of lane l's joint side, 0 = none
+  int32_t n_mat;                     // MULTI row tables: materials (after the collidables, o_cen / l_cen)
 };
 
 // SINGLE-mode lane image: for each of 64 lanes, every constant the
@@ -183,18 +182,6 @@ enum {
 // its two-way rank (LR_MBSLOT / BI_BSLOT), then one zero slot (m_zero). Task
 // partials: 8 words (the two sums, the count).
 enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 6, TSLOT_STRIDE = 8, MULTI_MR = 4 };
-// the MULTI row image, in two parts (bx_capi.cpp), 16-byte group g of row r
-// at o + (g * R + r) * 4: the geometry (MG_*, 4 groups), which every near
-// row's contact_gen reads in the position pass, and the impulse constants
-// (MP_*, 3 groups), which only a penetrating row's impulses read (its
-// position and velocity passes); a row that does not penetrate stores exact
-// zeros from its geometry's slot word alone. MG_AB: body a | body b << 16;
-// MG_META: contact function | one-way << 8 | the b side's contact slot << 16
-// (two-way rows: R + the row's two-way rank; one-way rows: the zero slot)
-enum { MG_AB = 0, MG_META = 1, MG_APOS = 2, MG_AEND = 5, MG_ARAD = 8, MG_BPOS = 9, MG_BEND = 12,
-       MG_BRAD = 15, MG_WORDS = 16 };
-enum { MP_FRIC = 0, MP_ELAS = 1, MP_SCALE = 2, MP_THR = 3, MP_MA = 4, MP_MB = 5, MP_IA = 6, MP_IB = 9,
-       MP_WORDS = 12 };
 // MULTI-mode broad phase: per row one 16-byte group at o_bimg + 4 r (staged
 // in LDS at l_bimg once per launch): (centre a | centre b << 16, reach,
 // flags, b slot). A capsule-capsule row whose capsule centres lie farther
@@ -206,11 +193,19 @@ enum { MP_FRIC = 0, MP_ELAS = 1, MP_SCALE = 2, MP_THR = 3, MP_MA = 4, MP_MB = 5,
 // names them. BI_BSLOT: the row's b-side slot (two-way rows; one-way rows:
 // the zero slot).
 // BI_FLAGS: bit 0 may_skip (capsule-capsule), bit 1 the row's group is
-// culled (NearNeighbors), bit 2 a masked cell (R_NNMASK), bits 8.. a row of
-// an unculled group: its Info index. Culled scenes (no broad phase) stage the
-// same image: their NearNeighbors keys take the centres too.
+// culled (NearNeighbors), bit 2 a masked cell (R_NNMASK), bit 3 one-way,
+// bits 4-7 the contact function, 8-15 the material, 16.. a row of an
+// unculled group: its Info index. BI_CEN names the row's two collidables.
+// The row tables at o_cen (uint4 units, staged at l_cen once per launch):
+// 2 n_cen collidable groups ((body, offset), (end, radius)), n_mat materials
+// (friction, elasticity, scale, velocity threshold), N bodies (mass, inverse
+// inertia); in LDS then n_cen placed centres. Every MULTI contact pass
+// assembles its rows' records from them (row_from_lds), the broad phase and
+// the NearNeighbors keys take the placed centres (culled scenes, which have
+// no broad phase, stage the same tables).
 enum { BI_CEN = 0, BI_REACH = 1, BI_FLAGS = 2, BI_BSLOT = 3, BI_WORDS = 4 };
-enum { BIF_SKIP = 1, BIF_CULL = 2, BIF_MASK = 4, BIF_INFO_SHIFT = 8 };
+enum { BIF_SKIP = 1, BIF_CULL = 2, BIF_MASK = 4, BIF_OW = 8, BIF_FN_SHIFT = 4, BIF_MAT_SHIFT = 8,
+       BIF_INFO_SHIFT = 16 };
 enum { HULL_STRIDE = 114, HULL_V = 0, HULL_F = 24, HULL_N = 96 };
 
 }  // namespace bx
