@@ -3671,22 +3671,23 @@ __device__ __forceinline__ float euler_y(const float* q) {
 }
 
 // Humanoid center of mass over bodies [:-1] (humanoid.py:336-338) -> red[32..35]
-// hb (SINGLE mode, 16 lanes, N <= 16): each lane's hoisted body, so body b's
-// mass is wave lane b's (every env of the wave has the same bodies), read
-// without a load; the loop then has a fixed trip count whose qp reads issue
-// together instead of one dependent constant load per body. Same sum order;
-// the masked tail adds 0 * pos, which leaves acc and m unchanged.
+// n16 (SINGLE mode: N <= 16): a fixed trip count, so the bodies' masses
+// (uniform scalar loads) and qp reads issue together instead of one
+// dependent load per body; same sum order, the masked tail adds 0 * pos,
+// which leaves acc and m unchanged. (Not the lanes' hoisted masses through
+// readlane: the call sits in a lane-0 branch, where a spilled mass is
+// restored for the active lanes only.)
 __device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3& com, float& msum,
-                             const BodyC* hb = nullptr) {
+                             bool n16 = false) {
   v3 acc = mk(0.f, 0.f, 0.f);
   float m = 0.f;
-  if (hb) {
+  if (n16) {
 #pragma unroll
     for (int b = 0; b < 16; b++) {
       const bool in = b < H.N - 1;
-      const float mb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hb->mass), b));
-      const float w = in ? mb : 0.f;
-      acc = acc + w * ld3(qp + (in ? b : 0) * QP_STRIDE);
+      const int bb = in ? b : 0;
+      const float w = in ? c.f(H.o_body + bb * BODY_STRIDE + BODY_MASS) : 0.f;
+      acc = acc + w * ld3(qp + bb * QP_STRIDE);
       m += w;
     }
     com = acc / m;
@@ -4001,7 +4002,7 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
   if ((KIND_IS(BX_ENV_HUMANOID) || KIND_IS(BX_ENV_HUMANOID_STANDUP)) && lane == 0) {
     v3 com;
     float msum;
-    humanoid_com(c, H, E.qp, com, msum, L == 16 ? hbody : nullptr);
+    humanoid_com(c, H, E.qp, com, msum, L == 16 && hbody != nullptr);
     st3(E.red + 32, com);
     E.red[35] = msum;
   }
@@ -4447,8 +4448,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     v3 com0 = mk(0.f, 0.f, 0.f);
     float msum = 0.f;
     if (KIND_IS(BX_ENV_HUMANOID) || KIND_IS(BX_ENV_SWIMMER))
-      humanoid_com(c, H, E.qp, com0, msum,
-                   (S && EK == EK_HUM && (F & F_JH) == 0) ? &X.B : nullptr);
+      humanoid_com(c, H, E.qp, com0, msum, S && EK == EK_HUM && (F & F_JH) == 0);
     // the target envs' torso before the step (red words 36..38)
     if ((KIND_IS(BX_ENV_UR5E) || KIND_IS(BX_ENV_FETCH)) && lane == 0)
       st3(E.red + 36, ld3(E.qp + (int)P.coef[0] * QP_STRIDE));
