@@ -570,10 +570,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     }
     row_mat[x] = it->second;
   }
-  if (cens.size() > 0xFFFF || mats.size() > 0xFF || R > 0xFFFF)
-    return fail("too many collidables, materials or rows for the MULTI row tables");
-  H.n_cen = (int)cens.size();
-  H.n_mat = (int)mats.size();
+  // (past these sizes the scene takes the item-loop kernels: no MULTI tables)
+  const bool mtab_ok = cens.size() <= 0xFFFF && mats.size() <= 0xFF && R <= 0xFFFF;
+  H.n_cen = mtab_ok ? (int)cens.size() : 0;
+  H.n_mat = mtab_ok ? (int)mats.size() : 0;
   // the MULTI (System.step only) tail starts here, over the env step's regions
   const int tail_m = off;
   // env-step regions: joint angles, the env programs' System.step action
@@ -625,8 +625,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     // lane owning <= 1 body / joint / actuator / task and <= MULTI_MR rows
     size_t mxja = 0;
     for (int b = 0; b < N; b++) mxja = std::max({mxja, jl[b].size(), al[b].size()});
+    // (and its LDS tail within one workgroup's 160 KB)
     H.multi = (!H.single && L > 64 && !H.spring && !xcol && N <= 256 && J <= 256 && K <= 256 &&
-               H.T <= 256 && R <= MULTI_MR * 256 && mxja <= 8 && max_btask <= BTASK_W) ? 1 : 0;
+               H.T <= 256 && R <= MULTI_MR * 256 && mxja <= 8 && max_btask <= BTASK_W && mtab_ok &&
+               (size_t)H.env_words_m * 4 <= 160 * 1024) ? 1 : 0;
     H.act_same = 1;
     for (int a = 0; a < K; a++)
       if (d->act_joint[a] != a) H.act_same = 0;

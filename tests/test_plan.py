@@ -43,3 +43,25 @@ def test_plan_refuses_a_null_descriptor():
   v = C.c_int32()
   rc = _native.lib().bx_system_plan(None, None, C.byref(v), C.byref(v), C.byref(v))
   assert rc != 0 and b'null' in _native.lib().bx_last_error()
+
+
+def test_mountain4_with_many_materials_takes_the_item_loops():
+  """The MULTI kernel assembles rows from LDS tables with <= 255 distinct
+  (friction, elasticity, scale, threshold) materials; a scene with more
+  (here every row its own friction) takes the item-loop kernels instead of
+  failing to build."""
+  import ctypes as C
+  import numpy as np
+  from brax_amd import _native, abi, compiler
+  cfg = config_for('mountain4')
+  vc, desc, meta = compiler.compile_system(cfg)
+  rdesc = compiler.compile_reset(vc, meta['body_index'])
+  n = len(desc['row_friction'])
+  desc['row_friction'] = np.linspace(0.5, 1.5, n)
+  cd, keep = abi.make_desc(desc)
+  rd, keep_r = abi.make_reset_desc(rdesc, meta['num_joint_dof'])
+  mode, lanes, lds = C.c_int32(), C.c_int32(), C.c_int32()
+  _native.check(_native.lib().bx_system_plan(C.byref(cd), C.byref(rd), C.byref(mode),
+                                             C.byref(lanes), C.byref(lds)))
+  del keep, keep_r
+  assert mode.value == 0, (mode.value, lanes.value, lds.value)
