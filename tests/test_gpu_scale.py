@@ -121,14 +121,16 @@ def test_ant_32768_shards_reproduce_one_batch(dev, oracle_lib):
 
 
 @pytest.mark.parametrize('variant', ['multi', 'itemloop'])
-@pytest.mark.parametrize('cutoff', [0, 36])
+@pytest.mark.parametrize('cutoff', [0, 36, 300])
 def test_mountain4_full_batch(dev, oracle_lib, cutoff, variant):
   """BASELINE configs[4]: Ant Mountain(4) System.step at 2,048 envs
   (37 bodies, 630 capsule-capsule + 72 capsule-plane rows; NearNeighbors
   cutoff 36 as published): determinism, batch independence, unit
   quaternions and parity with the fp64 oracle on sampled envs. Both large-
   scene kernels: MULTI (the default: 256 threads per env, gather tasks) and
-  the item loops at 256 threads per env."""
+  the item loops at 256 threads per env. Cutoff 300 keeps more cells than
+  one wave's 256 candidate keys: the NearNeighbors lists past a wave's
+  sorted keys are empty (the bitonic lists' padding)."""
   import brax_amd
   from brax_amd import _native
   from tests.test_gpu_parity import Envelope, _env_err, _gate
