@@ -38,3 +38,25 @@ def test_abi_version_and_error_path():
   h = ctypes.c_void_p()
   rc = lib.bx_system_create(None, None, 0, ctypes.byref(h))
   assert rc != 0 and b'null' in lib.bx_last_error()
+
+
+def test_missing_library_fails_loudly(tmp_path):
+  """No CPU fallback: with the HIP library absent, the product path raises
+  NativeError at its first native call instead of computing anything."""
+  import subprocess
+  import sys
+  code = ('import brax_amd, sys\n'
+          'from brax_amd._native import NativeError\n'
+          'from brax_amd.system import System\n'
+          'from tests.helpers import config_for\n'
+          'try:\n'
+          '  System.plan(config_for("ant"))\n'
+          'except NativeError as e:\n'
+          '  print("raised", e)\n'
+          '  sys.exit(0)\n'
+          'sys.exit(3)\n')
+  env = dict(os.environ, BRAX_AMD_LIB=str(tmp_path / 'absent' / 'libbrax_amd.so'))
+  r = subprocess.run([sys.executable, '-c', code], cwd=ROOT, env=env, capture_output=True,
+                     text=True, timeout=120)
+  assert r.returncode == 0, r.stdout + r.stderr
+  assert 'raised' in r.stdout
