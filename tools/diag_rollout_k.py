@@ -30,12 +30,14 @@ def main():
   env = envs.create('ant', batch_size=4096, episode_length=1000, auto_reset=True, device=dev)
   st = env.reset(np.array([0, 7], np.uint32))
   out = {}
-  for K in (1, 5, 20):
+  ks = [int(k) for k in sys.argv[1:]] or [1, 5, 20]
+  for K in ks:
     acts = torch.rand((K, 4096, 8), device=dev) * 2 - 1
     buf = torch.empty((K * 4096 * (160 + 87 + 4 + 10),), device=dev)
     out[f'given K={K}'] = timed(lambda: rollout(env, st, acts, out=buf)) / K
     r = RolloutRunner(env, st, K, seed=3)
     out[f'drawn K={K}'] = timed(r.run) / K
+    out[f'drawn K={K} launch'] = out[f'drawn K={K}'] * K
   print(os.environ.get('BRAX_AMD_LIB', '_lib'), {k: round(v, 2) for k, v in out.items()}, flush=True)
 
 
