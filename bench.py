@@ -134,6 +134,40 @@ def rank_env(environ, rank, world, port):
   return e
 
 
+def _count_list(v):
+  return len([x for x in v.split(',') if x.strip() != ''])
+
+
+def visible_gpus(environ, topology='/sys/class/kfd/kfd/topology/nodes'):
+  """GPUs this process would see, without touching HIP: the device lists of
+  HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES (indices into what
+  ROCR_VISIBLE_DEVICES leaves), else ROCR_VISIBLE_DEVICES, else the GPU nodes
+  of the KFD topology (sysfs text; a node with SIMDs is a GPU, CPU nodes have
+  none). None when neither says."""
+  rocr = environ.get('ROCR_VISIBLE_DEVICES')
+  for k in ('HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES'):
+    v = environ.get(k)
+    if v is not None:
+      n = _count_list(v)
+      return min(n, _count_list(rocr)) if rocr is not None else n
+  if rocr is not None:
+    return _count_list(rocr)
+  try:
+    nodes = os.listdir(topology)
+  except OSError:
+    return None
+  n = 0
+  for d in nodes:
+    try:
+      with open(os.path.join(topology, d, 'properties')) as f:
+        props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+    except OSError:
+      continue
+    if int(props.get('simd_count', '0')) > 0:
+      n += 1
+  return n
+
+
 def spawn_ranks(gpus, argv, script=None):
   """`python bench.py --gpus N` without a launcher: start N fresh rank
   processes of this script (one per GPU, torchrun's environment) BEFORE this
@@ -146,9 +180,12 @@ def spawn_ranks(gpus, argv, script=None):
   import subprocess
   backend = os.environ.get('BX_DIST_BACKEND', 'nccl')
   if backend == 'nccl':
-    have = torch.cuda.device_count()  # counts devices without initialising HIP
-    if have < gpus:
-      print(f'bench.py: --gpus {gpus} but {have} GPUs are visible', file=sys.stderr)
+    # counted from the environment / the KFD topology: no HIP call in this
+    # parent (torch.cuda.device_count() falls back to hipGetDeviceCount when
+    # amdsmi is unavailable, which would initialise HIP before the ranks start)
+    have = visible_gpus(os.environ)
+    if have is not None and have < gpus:
+      print(f'bench.py: --gpus {gpus} but {have} GPUs visible', file=sys.stderr)
       return 2
   with socket.socket() as s:
     s.bind(('127.0.0.1', 0))
@@ -165,6 +202,17 @@ def spawn_ranks(gpus, argv, script=None):
   prev = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
   try:
     return _wait_ranks(procs, stop)
+  except BaseException:
+    # KeyboardInterrupt / SystemExit / an error while waiting: no rank is
+    # left running (a rank blocked at a barrier would hold its GPU)
+    stop()
+    for q in procs:
+      try:
+        q.wait(timeout=15)
+      except subprocess.TimeoutExpired:
+        q.kill()
+        q.wait()
+    raise
   finally:
     signal.signal(signal.SIGTERM, prev)
 

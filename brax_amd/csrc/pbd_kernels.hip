@@ -495,7 +495,7 @@ __device__ __forceinline__ int axis_angle(const JointC& J, const QP& p, const QP
   v3 xz = dot(a1p, a1c) * a1c + dot(a1p, a2c) * a2c;
   xz = ndiv3(xz, 1e-10f + safe_norm(xz));
   float cb = dot(xz, a1p);
-  float theta = acosf(clampf(cb, -1.f, 1.f)) * signf(dot(a1p, a3c));
+  float theta = acosf(clampf(cb, -1.f, 1.f)) * signf(dot(a1p, a3c)) + nan_of(cb);
   float phi = signed_angle(-a3c, a2c, lon);
   axes[0] = a1p; axes[1] = a2c; axes[2] = a3c;
   ang[0] = psi; ang[1] = theta; ang[2] = phi;
@@ -704,7 +704,9 @@ __device__ __forceinline__ void contact_gen(const RowC& R, const QP& a, const QP
   v3 pv = ba - bb;
   float dist = safe_norm(pv);
   n = pv / (1e-6f + dist);
-  pen = R.a_rad + R.b_rad - dist;
+  // (+ NaN for NaN segments: jnp's safe_norm is NaN there, allclose(NaN, 0)
+  // being False; the finite-math near-zero test would return 0)
+  pen = R.a_rad + R.b_rad - dist + nan_of(dot(pv, pv));
   pos = (ba + bb) / 2.f;
   vel = (a.vel + cross(a.ang, pos - a.pos)) - (b.vel + cross(b.ang, pos - b.pos));
 }
@@ -1270,7 +1272,7 @@ __device__ void impulse_contact(const RowC& R, const QP& a, const QP& b, v3 cpos
   float vdn = safe_norm(vd);
   float impd = fminf(vdn / denom, R.fric * imp);
   v3 dird = vd / (1e-6f + vdn);
-  float an = (cpen > 0.f && nv < 0.f && imp > 0.f) ? 1.f : 0.f;
+  float an = (cpen > 0.f && nv < 0.f && imp > 0.f) ? 1.f : nan_of(cpen);
   float ad = an * (vdn > 0.01f ? 1.f : 0.f);
   v3 J = imp * n, Jd = -impd * dird;
   oav = (J / R.ma) * an + (Jd / R.ma) * ad;
@@ -2119,6 +2121,14 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       q4 oar, obr;
       float dl = position_contact<F>(R, a, b, ld3(pa), ld4(pa + 3), ld3(pb), ld4(pb + 3), cpos, n, pen,
                                   oap, oar, obp, obr);
+      if (is_nan(pen)) {
+        // a NaN contact's impulses are NaN on both sides (the reference's
+        // masked products, colliders.py:332-333: NaN * 0)
+        const float pz = nan_of(pen);
+        oap = obp = mk(pz, pz, pz);
+        oar = obr = q4{pz, pz, pz, pz};
+        dl = pz;
+      }
       float* rd = E.rowd + r * ROWD_STRIDE;
       st3(rd, cpos); st3(rd + 3, n); rd[6] = pen; rd[7] = dl;
       float* sa = E.cslot + r * SLOT_STRIDE;
@@ -2181,6 +2191,10 @@ __device__ void pbd_step(const Cst& c, const BlobHdr& H, const Env& E, int lane,
       v3 oav, oaa, obv, oba;
       velocity_contact<F>(R, h, a, b, ld3(ra), ld3(ra + 3), ld3(ra + 6), ld3(rbb), ld3(rbb + 3),
                        ld3(rbb + 6), ld3(rd), ld3(rd + 3), rd[6], rd[7], oav, oaa, obv, oba);
+      if (is_nan(rd[6])) {
+        const float pz = nan_of(rd[6]);
+        oav = oaa = obv = oba = mk(pz, pz, pz);
+      }
       float* sa = E.cslot + r * SLOT_STRIDE;
       float* sb = E.cslot + (E.nR + r) * SLOT_STRIDE;
       st3(sa, oav); st3(sa + 3, oaa);
@@ -2942,7 +2956,8 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
         const v3 d = (a.pos + rotate(R.a_pos, a.rot)) - (b.pos + rotate(R.b_pos, b.rot));
         const float reach =
             (norm(R.a_end) + norm(R.b_end) + R.a_rad + R.b_rad) * 1.00001f + 1e-4f;
-        far = dot(d, d) > reach * reach;
+        const float dd = dot(d, d);
+        far = dd > reach * reach && !is_nan(dd);
       }
       if (far) {
         cpos = z3;
@@ -2958,7 +2973,14 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       ld_slot(E.prev + R.b * PREV_STRIDE, pbp, pbr, unused);
       v3 oap = z3, obp = z3;
       q4 oar = z4, obr = z4;
-      if (!((FS & F_CC) != 0) || pen > 0.f) {
+      if ((FS & F_CC) != 0 && is_nan(pen)) {
+        // a NaN contact's impulses are NaN on both sides (the reference's
+        // masked products, colliders.py:332-333: NaN * 0)
+        const float pz = nan_of(pen);
+        oap = obp = mk(pz, pz, pz);
+        oar = obr = q4{pz, pz, pz, pz};
+        dl = pz;
+      } else if (!((FS & F_CC) != 0) || pen > 0.f) {
         dl = position_contact<FS>(R, a, b, pap, par, pbp, pbr, cpos, cn, pen, oap, oar, obp, obr);
       } else {
         dl = 0.f;
@@ -2997,9 +3019,13 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
       ld_rb(E.rb + R.b * RB_STRIDE, rbp, rbv, rba);
       v3 oav = z3, oaa = z3, obv = z3, oba = z3;
-      if (!((FS & F_CC) != 0) || pen > 0.f)
+      if ((FS & F_CC) != 0 && is_nan(pen)) {
+        const float pz = nan_of(pen);
+        oav = oaa = obv = oba = mk(pz, pz, pz);
+      } else if (!((FS & F_CC) != 0) || pen > 0.f) {
         velocity_contact<FS>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos, cn, pen, dl, oav, oaa,
                              obv, oba);
+      }
       st_slot(E.cslot + r * SLOT_STRIDE, oav, q4{oaa.x, oaa.y, oaa.z, 0.f},
               nonzero3(oav));
       st_slot(E.cslot + (E.nR + r) * SLOT_STRIDE, obv, q4{oba.x, oba.y, oba.z, 0.f},
@@ -3027,6 +3053,19 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     BX_STAMP(7);
   }
   if (hasB) {
+    // a NaN body's contact Info is NaN when it has contact rows: its rows'
+    // masked impulses were NaN (colliders.py:332-333, 440-442: NaN * 0; the
+    // straight-line plane passes above fold the masks to selects, so the
+    // slots carried zeros). A body's state is NaN at the end of the step
+    // exactly when a contact pass of the step saw it NaN (a one-way row's
+    // contact is its body's; the two-way passes carry NaN rows explicitly)
+    if ((X.cl.e[0] & 0xFFFFFF) != 2 * H.R) {
+      const float pz = nan_of(((q.pos.x + q.pos.y) + (q.pos.z + q.rot.w)) +
+                              ((q.rot.x + q.rot.y) + (q.rot.z + q.vel.x)) +
+                              ((q.vel.y + q.vel.z) + (q.ang.x + q.ang.y)) + q.ang.z);
+      icv = icv + mk(pz, pz, pz);
+      ica = ica + mk(pz, pz, pz);
+    }
     float* acc = E.acc + bi * ACC_STRIDE;
     st3(acc + ACC_ICV, icv);
     st3(acc + ACC_ICA, ica);
@@ -3420,7 +3459,8 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
           near = (g0.z & BIF_SKIP) == 0u;
           if (!near) {
             // + 1e-4: far above the fp32 error of the centres
-            near = !(centre_dist(E, H, g0.x) > __uint_as_float(g0.y) + 1e-4f);
+            const float cd = centre_dist(E, H, g0.x);
+            near = !(cd > __uint_as_float(g0.y) + 1e-4f) || is_nan(cd);
           }
           if (!near) {
             // (a one-way row's b slot is the zero slot: zeros again)
@@ -3480,7 +3520,14 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       v3 oap = mk(0.f, 0.f, 0.f), obp = mk(0.f, 0.f, 0.f);
       q4 oar{0.f, 0.f, 0.f, 0.f}, obr{0.f, 0.f, 0.f, 0.f};
       dl[m] = 0.f;
-      if (pen[m] > 0.f) {
+      if (is_nan(pen[m])) {
+        // a NaN contact's impulses are NaN on both sides (the reference's
+        // masked products, colliders.py:332-333: NaN * 0)
+        const float pz = nan_of(pen[m]);
+        oap = obp = mk(pz, pz, pz);
+        oar = obr = q4{pz, pz, pz, pz};
+        dl[m] = pz;
+      } else if (pen[m] > 0.f) {
         dl[m] = position_contact<F, true>(R, a, b, pap, par, pbp, pbr, cpos[m], cn[m], pen[m], oap,
                                           oar, obp, obr);
       }
@@ -3516,7 +3563,10 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       // a row that does not penetrate stores exact zeros (sm = 0,
       // colliders.py:584-658): no constants read, no state gathered
       v3 oav = mk(0.f, 0.f, 0.f), oaa = oav, obv = oav, oba = oav;
-      if (pen[m] > 0.f) {
+      if (is_nan(pen[m])) {
+        const float pz = nan_of(pen[m]);
+        oav = oaa = obv = oba = mk(pz, pz, pz);
+      } else if (pen[m] > 0.f) {
         RowC R = row_from_lds(E, r);
         QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
         v3 rap, rav, raa, rbp, rbv, rba;
@@ -3656,7 +3706,7 @@ __device__ void joint_angles(const Cst& c, const BlobHdr& H, const Env& E, int l
   }
 }
 
-__device__ __forceinline__ float clip1(float x) { return clampf(x, -1.f, 1.f); }
+__device__ __forceinline__ float clip1(float x) { return clampn(x, -1.f, 1.f); }
 
 // math.quat_to_euler(q)[2] (math.py:80-91) of a QP record's rot (w, x, y, z)
 __device__ __forceinline__ float euler_z(const float* q) {
@@ -3667,7 +3717,7 @@ __device__ __forceinline__ float euler_z(const float* q) {
 // math.quat_to_euler(q)[1] (math.py:80-91): asin(clip(2 q1 q3 + 2 q0 q2))
 // of a QP record's rot (w, x, y, z)
 __device__ __forceinline__ float euler_y(const float* q) {
-  return asinf(clampf(2.f * q[1] * q[3] + 2.f * q[0] * q[2], -1.f, 1.f));
+  return asinf(clampn(2.f * q[1] * q[3] + 2.f * q[0] * q[2], -1.f, 1.f));
 }
 
 // Humanoid center of mass over bodies [:-1] (humanoid.py:336-338) -> red[32..35]
@@ -4192,6 +4242,9 @@ __device__ __forceinline__ void system_step_body(const StepArgs& A) {
       for (int r = lane; r < H.R; r += L) E.bimg[r] = bg[r];
       const uint4* cg = reinterpret_cast<const uint4*>(c.w + H.o_cen);
       for (int k = lane; k < 2 * H.n_cen + H.n_mat + H.N; k += L) E.cen[k] = cg[k];
+      // lane k's first read (place_centres: E.cen[2k]) is another wave's
+      // write: no pass reads the tables before every wave has staged them
+      esync<L>();
     }
     const int64_t ro = valid ? e * H.info_rows : 0;
     RowInfoOut io{A.info.contact_pos ? A.info.contact_pos + ro * 3 : nullptr,
@@ -4549,8 +4602,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
         v3 vel = (p1 - pos0) / dt;
         float fwd = vel.x;
         float z = p1.z;
-        float healthy = z < P.coef[4] ? 0.f : 1.f;
-        healthy = z > P.coef[5] ? 0.f : healthy;
+        float healthy = in_range_or_nan(z, P.coef[4], P.coef[5]) ? 1.f : 0.f;
         bool term = P.coef[6] != 0.f;
         float hr = term ? P.coef[3] : P.coef[3] * healthy;
         float ctrl = P.coef[1] * sq;
@@ -4579,8 +4631,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
         v3 v = (com1 - com0) / dt;
         float fwd = P.coef[0] * v.x;
         float z = p1.z;
-        float healthy = z < P.coef[4] ? 0.f : 1.f;
-        healthy = z > P.coef[5] ? 0.f : healthy;
+        float healthy = in_range_or_nan(z, P.coef[4], P.coef[5]) ? 1.f : 0.f;
         bool term = P.coef[6] != 0.f;
         float hr = term ? P.coef[3] : P.coef[3] * healthy;
         float ctrl = P.coef[1] * sq;
@@ -4596,10 +4647,8 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
         float fwd = P.coef[0] * xv;
         float ay = euler_y(E.qp + 3);
         float z = p1.z;
-        float healthy = z < P.coef[3] ? 0.f : 1.f;
-        healthy = z > P.coef[4] ? 0.f : healthy;
-        healthy = ay > P.coef[6] ? 0.f : healthy;
-        healthy = ay < P.coef[5] ? 0.f : healthy;
+        float healthy = in_range_or_nan(z, P.coef[3], P.coef[4]) &&
+                        in_range_or_nan(ay, P.coef[5], P.coef[6]) ? 1.f : 0.f;
         bool term = P.coef[7] != 0.f;
         float hr = term ? P.coef[2] : P.coef[2] * healthy;
         float ctrl = P.coef[1] * sq;
@@ -4609,7 +4658,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
         if (m) { m[0] = -ctrl; m[1] = fwd; m[2] = hr; m[3] = p1.x; m[4] = xv; }
       } else if (KIND_IS(BX_ENV_INVERTED_PENDULUM)) {
         reward = 1.f;
-        done = fabsf(E.ang[0]) > .2f ? 1.f : 0.f;  // |obs[1]| > .2
+        done = fabsf(E.ang[0]) > .2f && !is_nan(E.ang[0]) ? 1.f : 0.f;  // |obs[1]| > .2
       } else if (KIND_IS(BX_ENV_INVERTED_DOUBLE_PENDULUM)) {
         // the pole tip (body 2's (0, 0, .3)) in the world
         const float* q2 = E.qp + 2 * QP_STRIDE;
@@ -4619,7 +4668,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
         float v1 = E.ang[H.D], v2 = E.ang[H.D + 1];
         float velp = 1e-3f * (v1 * v1) + 5e-3f * (v2 * v2);
         reward = 10.f - dist - velp;
-        done = y <= 1.f ? 1.f : 0.f;
+        done = y <= 1.f && !is_nan(y) ? 1.f : 0.f;
       } else if (KIND_IS(BX_ENV_ACROBOT)) {
         float a0 = E.ang[0], a1 = E.ang[1], w0 = E.ang[H.D], w1 = E.ang[H.D + 1];
         float dist = a0 * a0 + a1 * a1;

@@ -211,6 +211,36 @@ __device__ __forceinline__ float deg_to_rad(float a) {
 __device__ __forceinline__ float clampf(float x, float lo, float hi) {
   return x < lo ? lo : (x > hi ? hi : x);
 }
+
+// NaN semantics under the finite-math build (`step` never
+// raises, NaN / Inf propagate). The build assumes no NaN in any value it
+// computed, so `x != x`, `isnan` and `x * (c ? 1 : 0)` fold to false / a
+// select; the tests below see x through an empty asm (an opaque copy), so
+// the compiler cannot know it is not NaN, and test its bits.
+__device__ __forceinline__ bool is_nan(float x) {
+  asm("" : "+v"(x));
+  return (__float_as_uint(x) & 0x7fffffffu) > 0x7f800000u;
+}
+// 0, or a quiet NaN when x is NaN (itself opaque, so no NaN-free assumption
+// removes it). The reference multiplies its contact impulses by 0 / 1 masks
+// (`p = dlambda * n * coll_mask`, colliders.py:332-333; `* apply_n`,
+// `* sm`): NaN * 0 is NaN, so a NaN contact's impulse is NaN where the mask
+// is 0. The kernels write those masks as `c ? 1 : nan_of(pen)`.
+__device__ __forceinline__ float nan_of(float x) {
+  float r = is_nan(x) ? __uint_as_float(0x7fc00000u) : 0.f;
+  asm("" : "+v"(r));
+  return r;
+}
+// jnp.clip (`minimum(maximum(x, lo), hi)`): NaN for NaN (the finite-math
+// clampf's min / max return the bound)
+__device__ __forceinline__ float clampn(float x, float lo, float hi) {
+  return is_nan(x) ? x : clampf(x, lo, hi);
+}
+// jp.where(x < lo, 0, 1) then jp.where(x > hi, 0, that): 1 for NaN (both
+// compares false), whatever way the build rewrites the compares
+__device__ __forceinline__ bool in_range_or_nan(float x, float lo, float hi) {
+  return is_nan(x) || !(x < lo || x > hi);
+}
 __device__ __forceinline__ float signf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
 
 // q / |q| with the bare v_sqrt_f32 (the Ant env kernel's integrator only)

@@ -652,6 +652,151 @@ def gym_ant(n_envs=8, n_steps=6, episode_length=3):
   return out
 
 
+# NaN / Inf poisoning (`step` never raises, NaN/Inf propagate):
+# (env, what, where, value). 'qp' entries poison the state the rollout starts
+# from (field slice start, body, component); 'act' entries poison one action
+# element at one step (step, index). The other envs stay clean, so a test can
+# also hold them to the bits of an unpoisoned run (batch isolation).
+NAN_PLAN = {
+    'ant': [(1, 'qp', (7, 0, 0), np.nan),      # torso vel x
+            (2, 'act', (1, 3), np.nan),        # one action element at step 1
+            (4, 'act', (0, 0), np.inf),        # +Inf action at step 0
+            (6, 'qp', (0, 3, 2), -np.inf)],    # a leg's pos z = -Inf
+    'humanoid': [(1, 'qp', (7, 0, 0), np.nan),
+                 (2, 'act', (1, 5), np.nan),
+                 (4, 'act', (0, 0), np.inf),
+                 (6, 'qp', (0, 0, 2), np.inf)],  # torso pos z = +Inf
+}
+
+
+def _poison_qp(a, plan):
+  a = np.array(a, np.float64, copy=True)
+  for b, what, loc, v in plan:
+    if what == 'qp':
+      f, body, k = loc
+      a[b, body, f + k] = v
+  return a
+
+
+def _poison_act(acts, plan):
+  acts = np.array(acts, np.float64, copy=True)
+  for b, what, loc, v in plan:
+    if what == 'act':
+      t, i = loc
+      acts[t, b, i] = v
+  return acts
+
+
+def nan_env(kind, n_envs=8, n_steps=6, episode_length=4):
+  """The reference's Episode+AutoReset wrapped `kind` (`envs/__init__.py:74-92`)
+  stepped from its reset with NaN / Inf put into some envs' state or actions
+  (NAN_PLAN). Records the poisoned start state, the actions and every step's
+  qp / obs / reward / done / steps / truncation / metrics. The episode ends
+  inside the run, so a poisoned env that the reference keeps (done = 0:
+  `jp.where(z < min_z, 0, 1)` is 1 for NaN, `ant.py:229-231`) is reset at the
+  truncation step (`wrappers.py:138-148`)."""
+  from brax import envs
+  from brax.physics.base import QP
+  plan = NAN_PLAN[kind]
+  from brax.envs import wrappers
+  # the registry's 'humanoid' is the fork's humanoid_new; the kernel's Humanoid
+  # kind is `brax/envs/humanoid.py` (as traj_humanoid): the create() chain
+  # (`envs/__init__.py:74-92`) built around that class
+  base = (importlib.import_module('brax.envs.humanoid').Humanoid() if kind == 'humanoid'
+          else envs.get_environment(kind))
+  env = wrappers.AutoResetWrapper(wrappers.VectorWrapper(
+      wrappers.EpisodeWrapper(base, episode_length, 1), n_envs))
+  st = env.reset(np.array([11, 0], np.uint32))
+  qp0 = _poison_qp(qp_pack(st.qp), plan)
+  st = st.replace(qp=qp_unpack(qp0))
+  out = {k: [] for k in ('qp', 'obs', 'reward', 'done', 'steps', 'truncation', 'metrics')}
+  out['first_qp'] = qp_pack(st.info['first_qp'])
+  out['first_obs'] = np.asarray(st.info['first_obs'])
+  keys = sorted(st.metrics)
+  def rec(s):
+    out['qp'].append(qp_pack(s.qp))
+    out['obs'].append(np.asarray(s.obs))
+    out['reward'].append(np.asarray(s.reward, np.float64))
+    out['done'].append(np.asarray(s.done, np.float64))
+    out['steps'].append(np.asarray(s.info['steps'], np.float64))
+    out['truncation'].append(np.asarray(s.info['truncation'], np.float64))
+    out['metrics'].append(np.stack([np.asarray(s.metrics[k], np.float64) for k in keys], -1))
+  rec(st)
+  A = env.action_size
+  acts = _poison_act(np.stack([np.random.default_rng(50_000 + t).uniform(-1, 1, (n_envs, A))
+                               for t in range(n_steps)]), plan)
+  with np.errstate(all='ignore'):
+    for t in range(n_steps):
+      st = env.step(st, acts[t])
+      rec(st)
+      print(f'  nan_{kind}: step {t + 1}/{n_steps}', flush=True)
+  r = {k: (np.stack(v) if isinstance(v, list) else v) for k, v in out.items()}
+  r['action'] = acts
+  r['metric_keys'] = np.array(keys)
+  r['episode_length'] = np.int32(episode_length)
+  r['poisoned'] = np.array(sorted({p[0] for p in plan}), np.int32)
+  return r
+
+
+def nan_mountain(n_steps=2):
+  """Ant Mountain(4), all pairs (the MULTI kernel's scene): `System.step`
+  from default_qp with env 1's first ant's torso velocity NaN and env 2's
+  last ant's torso pos z +Inf; env 0 clean. The reference's capsule-capsule
+  rows multiply their impulses by masks (`p = dlambda * n * coll_mask`,
+  colliders.py:332-333), so a NaN pair's impulse is NaN even where the mask
+  is 0 and reaches the other body of the pair."""
+  s = ant_mountain_sys(4)
+  q0 = qp_pack(s.default_qp())
+  qs = np.stack([q0, q0, q0])
+  qs[1, 0, 7] = np.nan
+  qs[2, s.body.index['$ Torso_2'], 2] = np.inf  # the last ant's torso
+  with np.errstate(all='ignore'):
+    r = sys_traj(s, 'nan_mountain4', [qp_unpack(q) for q in qs], 3, n_steps, 1.0, 32)
+  return r
+
+
+def eval_ant(n_envs=8, n_steps=7, episode_length=3):
+  """The reference's `envs.create('ant', ..., eval_metrics=True)` chain
+  (`envs/__init__.py:74-92`: Episode, Vector, AutoReset, then EvalWrapper,
+  `wrappers.py:168-202`) stepped from its reset: every step's state and
+  `eval_metrics` (episode_metrics per key, active_episodes, episode_steps).
+  The episode ends inside the run, so the metrics stop accumulating for every
+  env at the truncation step and active_episodes drops to 0 there; env 3's
+  torso is lifted above the healthy range at the start, so it terminates
+  (done from `is_healthy`, `ant.py:229-241`) on the first step."""
+  from brax import envs
+  env = envs.create('ant', episode_length=episode_length, batch_size=n_envs, eval_metrics=True)
+  st = env.reset(np.array([9, 0], np.uint32))
+  q = qp_pack(st.qp)
+  q[3, :, 2] += 2.0  # env 3 above max_z = 1.0: unhealthy after one step
+  st = st.replace(qp=qp_unpack(q))
+  em = st.info['eval_metrics']
+  keys = sorted(em.episode_metrics)
+  out = {'qp0': qp_pack(st.qp), 'obs0': np.asarray(st.obs),
+         'first_qp': qp_pack(st.info['first_qp']), 'first_obs': np.asarray(st.info['first_obs']),
+         'reset_metrics': np.stack([np.asarray(st.metrics[k], np.float64) for k in keys], -1)}
+  acts = np.stack([np.random.default_rng(60_000 + t).uniform(-1, 1, (n_envs, 8))
+                   for t in range(n_steps)])
+  rec = {}
+  for t in range(n_steps):
+    st = env.step(st, acts[t])
+    em = st.info['eval_metrics']
+    for k, v in (('qp', qp_pack(st.qp)), ('obs', np.asarray(st.obs)),
+                 ('reward', np.asarray(st.reward, np.float64)),
+                 ('done', np.asarray(st.done, np.float64)),
+                 ('steps', np.asarray(st.info['steps'], np.float64)),
+                 ('episode_metrics', np.stack([np.asarray(em.episode_metrics[k], np.float64)
+                                               for k in keys], -1)),
+                 ('active_episodes', np.asarray(em.active_episodes, np.float64)),
+                 ('episode_steps', np.asarray(em.episode_steps, np.float64))):
+      rec.setdefault(k, []).append(v)
+  out.update({k: np.stack(v) for k, v in rec.items()})
+  out['action'] = acts
+  out['metric_keys'] = np.array(keys)
+  out['episode_length'] = np.int32(episode_length)
+  return out
+
+
 def kats():
   """Known answers: the reference's own geometry/math functions."""
   from brax import math as bm
@@ -823,6 +968,13 @@ def main():
     save('wrap_ant_ar2', wrapped_ant(n_steps=6, episode_length=5, action_repeat=2))
   if want('gym_ant'):
     save('gym_ant', gym_ant())
+  if want('eval_ant'):
+    save('eval_ant', eval_ant())
+  for kind in NAN_PLAN:
+    if want('nan_' + kind):
+      save('nan_' + kind, nan_env(kind))
+  if want('nan_mountain4'):
+    save('nan_mountain4', nan_mountain())
   # physics-only rollouts of the other registered envs' systems (their pbd
   # configs): Thruster/Twister forces, frozen bodies, systems without contacts
   for mod, (B, T, aw) in ROBOTS.items():

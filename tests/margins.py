@@ -9,6 +9,7 @@ import os
 
 _MARGINS = []
 _RATIOS = {}
+_XRATIOS = {}
 
 
 def record_margin(field, measured, tol, ratios=None, **extra):
@@ -22,12 +23,21 @@ def record_margin(field, measured, tol, ratios=None, **extra):
     _RATIOS.setdefault((test, field), []).extend(ratios)
 
 
-def ratio_table():
+def record_exact(field, ratios):
+  """Beside a per-env gate: each env's HIP_i / max(1e-5, 2 E32x_i), E32x_i
+  the error of Brax's fp32 on that env's EXACT input only (the two oracle
+  builds, no perturbed copies): SURVEY §8(c)'s literal wording. Recorded, not
+  asserted (the gate's E32_i is the max over all 66 realisations)."""
+  test = os.environ.get('PYTEST_CURRENT_TEST', '?').split(' ')[0]
+  _XRATIOS.setdefault((test, field), []).extend(ratios)
+
+
+def ratio_table(src=None):
   """Per (test, field): the per-env ratios HIP_i / max(1e-5, 2 E32_i) pooled
   over the test's steps: n, p50, p99, max, and how many exceed 1 / 0.9."""
   import numpy as np
   rows = []
-  for (test, field), r in _RATIOS.items():
+  for (test, field), r in (_RATIOS if src is None else src).items():
     a = np.asarray(r, np.float64)
     rows.append({'test': test, 'field': field, 'n': int(a.size),
                  'p50': float(np.percentile(a, 50)), 'p99': float(np.percentile(a, 99)),
@@ -54,11 +64,14 @@ def write(path):
     wide = [m for m in rows if m['tol'] > 1e-2 and m.get('role') != 'envelope']
     env = [m for m in rows if m.get('role') == 'envelope']
     table = ratio_table()
+    xt = ratio_table(_XRATIOS)
     json.dump({'n_gates': len(_MARGINS), 'n_wide_gates': len(wide), 'wide_gates': wide,
                'envelope_gates': env,
                'per_env_ratio_table': table,
                'per_env_over_1': sum(t['over_1'] for t in table),
                'per_env_over_0.9': sum(t['over_0.9'] for t in table),
+               'per_env_exact_input_ratio_table': xt,
+               'per_env_exact_input_over_1': sum(t['over_1'] for t in xt),
                'envelope_realisations_per_env': 2 * (1 + int(os.environ.get('BX_ENVELOPE_N', '32'))),
                'worst_per_test_field': [{k: v for k, v in m.items() if k != 'ratios'}
                                         for m in rows]}, f, indent=1)

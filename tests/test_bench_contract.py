@@ -85,6 +85,51 @@ def test_spawn_ranks_fails_when_a_rank_fails(tmp_path, monkeypatch):
 
 
 def test_spawn_ranks_refuses_more_rccl_ranks_than_gpus(monkeypatch):
+  """The RCCL parent counts GPUs from the environment (or the KFD
+  topology), never through HIP: device_count() here would be a HIP call."""
   monkeypatch.delenv('BX_DIST_BACKEND', raising=False)
-  monkeypatch.setattr(bench.torch.cuda, 'device_count', lambda: 1)
+  monkeypatch.setenv('HIP_VISIBLE_DEVICES', '0')
+
+  def no_hip():
+    raise AssertionError('the parent must not call into HIP')
+  monkeypatch.setattr(bench.torch.cuda, 'device_count', no_hip)
   assert bench.spawn_ranks(8, []) == 2
+
+
+def test_visible_gpus_without_hip(tmp_path):
+  assert bench.visible_gpus({'HIP_VISIBLE_DEVICES': '0,1,2'}) == 3
+  assert bench.visible_gpus({'CUDA_VISIBLE_DEVICES': '3'}) == 1
+  assert bench.visible_gpus({'ROCR_VISIBLE_DEVICES': '0,1,2,3'}) == 4
+  # HIP's list indexes into what ROCR leaves
+  assert bench.visible_gpus({'ROCR_VISIBLE_DEVICES': '2', 'HIP_VISIBLE_DEVICES': '0,1'}) == 1
+  assert bench.visible_gpus({'HIP_VISIBLE_DEVICES': ''}) == 0
+  # the KFD topology: CPU nodes have no SIMDs
+  for i, simds in enumerate((0, 1024, 1024)):
+    d = tmp_path / str(i)
+    d.mkdir()
+    (d / 'properties').write_text(f'cpu_cores_count 8\nsimd_count {simds}\ngfx_target_version 0\n')
+  assert bench.visible_gpus({}, topology=str(tmp_path)) == 2
+  assert bench.visible_gpus({}, topology=str(tmp_path / 'absent')) is None
+
+
+def test_spawn_ranks_stops_ranks_when_the_parent_is_interrupted(tmp_path, monkeypatch):
+  """An exception while waiting (e.g. KeyboardInterrupt) leaves no rank
+  running."""
+  monkeypatch.setenv('BX_DIST_BACKEND', 'gloo')
+  s = _script(tmp_path, "time.sleep(600)\n")
+  started = []
+  real_popen = __import__('subprocess').Popen
+
+  def popen(*a, **k):
+    p = real_popen(*a, **k)
+    started.append(p)
+    return p
+  monkeypatch.setattr('subprocess.Popen', popen)
+
+  def interrupted(procs, stop):
+    raise KeyboardInterrupt
+  monkeypatch.setattr(bench, '_wait_ranks', interrupted)
+  import pytest
+  with pytest.raises(KeyboardInterrupt):
+    bench.spawn_ranks(2, [], script=s)
+  assert len(started) == 2 and all(p.poll() is not None for p in started)

@@ -23,7 +23,7 @@ import pytest
 import torch
 
 from tests.conftest import golden
-from tests.margins import record_margin
+from tests.margins import record_exact, record_margin
 from tests.helpers import (CAPSULES, NN_MASKED, SHORT_SCENES, ENVTRAJ_KERNEL, POINTS, QP_FIELDS, ROBOTS, SPRING_ENVS,
                            SPRING_ROBOTS, XCOL, XY_ENVS, compiled, env_golden, env_kind,
                            golden_reset_qp, normwise, obs_flags, prep_oracle, reset_bodies)
@@ -116,6 +116,12 @@ def _gate(got, ref, e32, field, split=True):
     record_margin(field, m, tol, n=int(well.sum()), ratios=r[well].ravel().tolist(),
                   gate='per_env' if split else 'group', group_tol=group_tol,
                   group_ratio=float(nw[well].max()) / group_tol)
+    if split and samples is not None and len(samples) % 2 == 0:
+      # the exact-input realisations: the first of each build's run list
+      h = len(samples) // 2
+      ex = np.broadcast_to(np.maximum(normwise(samples[0], ref), normwise(samples[h], ref)),
+                           nw.shape)
+      record_exact(field, (nw / np.maximum(POS_TOL, 2.0 * ex))[well].ravel().tolist())
     assert float(nw[well].max()) <= group_tol, f'{field}: group bound'
     if m > tol:
       _dump_failure(field, got, ref, samples)

@@ -170,3 +170,58 @@ def test_mountain4_full_batch(dev, oracle_lib, cutoff, variant):
   got = a.numpy()[idx]
   for f, sl in QP_FIELDS.items():
     _gate(got[..., sl], ref[..., sl], _env_err([o[0][..., sl] for o in outs], ref[..., sl]), f)
+
+
+@pytest.mark.parametrize('cutoff', [0, 36])
+def test_mountain4_multi_vs_item_loops(dev, oracle_lib, cutoff):
+  """The two large-scene kernels round differently: the MULTI kernel's body
+  integration keeps the build's fast quotients (`qnormalize(r, true)`: v_rcp
+  + multiply, ~1.5 ulp), the item loops take Newton-corrected ones (`ndiv`,
+  correctly rounded but for ties); a scene whose MULTI tables do not fit runs
+  the item loops, so a system's rounding can change with its size. Recorded
+  here: on the same 2,048 diverged envs, each env's normwise distance between
+  the two kernels' states, against the sum of their two parity bounds
+  (2 x max(1e-5, 2 x E32_i): each kernel within its own bound of the float64
+  reference, sampled envs), and the distances themselves in the margins file
+  (`multi_vs_items:<field>`)."""
+  import brax_amd
+  from brax_amd import _native
+  from tests.margins import record_margin
+  from tests.test_gpu_parity import Envelope, _env_err
+  from tests.helpers import normwise
+  cfg = config_for('mountain4')
+  cfg.collider_cutoff = cutoff
+  sys_ = brax_amd.System(cfg, device=dev)
+  B = 2048
+  q0 = sys_.default_qp()
+  qp = brax_amd.QP(*(t.unsqueeze(0).expand((B,) + t.shape).contiguous()
+                     for t in (q0.pos, q0.rot, q0.vel, q0.ang)))
+  A = sys_.action_size
+  for t in range(2):  # diverge the envs first (on the default kernel)
+    qp, _ = sys_.step(qp, _actions(B, A, t, 3, dev))
+  act = _actions(B, A, 2, 3, dev)
+  out = {}
+  for variant, mode in (('multi', 3), ('items', 0)):
+    _native.check(_native.lib().bx_system_set_variant(sys_._h, 256, mode))
+    out[variant] = sys_.step(qp, act, info=False)[0].numpy()
+  from brax_amd.compiler import compile_reset
+  vc, d, meta = brax_amd.compiler.compile_system(cfg)
+  rd = compile_reset(vc, meta['body_index'])
+  o64 = oracle_lib.Oracle(d, rd, np.float64, safe_guard=True)
+  env32 = Envelope(oracle_lib, None, desc=(d, rd))
+  idx = np.random.default_rng(12).choice(B, 8, replace=False)
+  qp_in = qp.numpy()[idx]
+  an = act.cpu().numpy()[idx].astype(np.float64)
+  ref, _ = o64.system_step(qp_in, an)
+  outs = env32.system(qp_in, an)
+  for f, sl in QP_FIELDS.items():
+    dist = normwise(out['multi'][..., sl], out['items'][..., sl])
+    e32 = np.asarray(_env_err([o[0][..., sl] for o in outs], ref[..., sl]))
+    bound = 2 * np.maximum(1e-5, 2 * e32)
+    ds = dist[idx]
+    k = int(np.argmax(ds / bound))
+    record_margin(f'multi_vs_items:{f}', float(ds[k]), float(bound[k]), n=len(idx),
+                  pair_ratios=(ds / bound).tolist(), role='record', full_batch_max=float(dist.max()),
+                  full_batch_p50=float(np.median(dist)))
+    assert (ds <= bound).all(), (f, ds, bound)
+    assert np.isfinite(dist).all()
