@@ -1,3 +1,4 @@
+#include <cstdio>
 // bx_capi.cpp — the C ABI (include/brax_amd.h): descriptor -> device blob,
 // argument validation, and stream-ordered kernel launches.
 #include <hip/hip_runtime.h>
@@ -603,6 +604,13 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.l_bimg = carve(BI_WORDS * R);
   H.l_cen = carve(4 * (3 * H.n_cen + H.n_mat + N));
   H.env_words_m = (off + 63) & ~63;
+  if (getenv("BX_PLAN_DEBUG"))
+    fprintf(stderr,
+            "bx plan (words): qp..red %d  mslot %d  tslot %d (T=%d)  near %d  bimg %d  cen %d "
+            "(n_cen=%d n_mat=%d)  ract %d  alist %d  nnl %d  m_zero %d  env_words_m %d\n",
+            H.l_red + 64, (H.m_zero + 1) * MSLOT_STRIDE, (H.T + 1) * TSLOT_STRIDE, H.T,
+            H.l_bimg - H.l_near, BI_WORDS * R, 4 * (3 * H.n_cen + H.n_mat + N), H.n_cen, H.n_mat,
+            H.n_nn ? R : 0, H.n_nn ? H.info_rows : 0, H.nnl_words, H.m_zero, H.env_words_m);
   off = tail;
   H.l_rowd = carve(R * ROWD_STRIDE);
   H.l_cslot = carve((2 * R + 1) * SLOT_STRIDE);
