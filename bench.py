@@ -441,7 +441,7 @@ def secondary_configs(dev, steps=50):
         'envs_per_cu_by_lds': (160 * 1024) // max(sys_.lds_bytes, 1),
         # the MULTI kernel holds 256 registers (two waves per SIMD): two
         # 4-wave workgroups per CU run, whatever the LDS would admit
-        'envs_per_cu_by_registers': 2 if sys_.lanes == 256 else None}
+        'envs_per_cu_by_registers': 8 // (sys_.lanes // 64) if sys_.lanes >= 128 else None}
     # the same steps without Info (System.step(..., info=False): the state
     # only, as jit drops the Info a caller ignores)
     wall, gpu = _time(mstep_noinfo, n, 2)

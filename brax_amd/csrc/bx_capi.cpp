@@ -69,7 +69,9 @@ struct bx_system {
   int gw = 8;       // gather width (max per-body list length, 4 or 8)
   int tpb = 64;     // threads per workgroup of the step kernels (multiple of L)
   bool single_ok = false;
-  bool multi_ok = false;  // MODE_MULTI (3): large pbd scenes, 256 threads per env
+  bool multi_ok = false;  // MODE_MULTI (3): large pbd scenes, 128 or 256 threads per env
+  float* movf = nullptr;  // MULTI: the penetrating contacts past MCBUF, per env (grown on demand)
+  int64_t movf_envs = 0;
   int fold = 0;     // every joint j has torque actuator j (the Ant / Humanoid env kernels)
   int jb = 0;       // the joint-halves env kernels may own body copies (JB, build_blob)
   size_t lds_env = 0;    // bytes per block for the per-env kernels
@@ -383,18 +385,13 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   put_lists(al, H.o_al_off, H.o_al);
   put_lists(cl, H.o_cl_off, H.o_cl);
   // MULTI-mode gather tasks: each body's contact list cut, per collider group,
-  // into runs of <= TASK_W slots (same order); a body's tasks in list order.
-  // MULTI slots: row x's a side is slot x, a two-way row's b side slot R +
-  // its two-way rank (one-way rows have none), then the zero slot
-  std::vector<int> mb(R, -1);
-  int n_tw = 0;
-  for (int x = 0; x < R; x++)
-    if (!d->col_oneway[d->row_group[x]]) mb[x] = R + n_tw++;
-  H.m_zero = R + n_tw;
-  for (int x = 0; x < R; x++)
-    if (mb[x] < 0) mb[x] = H.m_zero;
-  auto mslot_of = [&](int s) { return s < R ? s : mb[s - R]; };
-  std::vector<std::vector<int>> task_e;  // slot indices
+  // into runs of <= TASK_W entries (same order); a body's tasks in list order.
+  // An entry names a row and side (row | side << 15, pbd_layout.h MCAP):
+  // the kernel finds the side's slot through the row's compact index; the
+  // padding entry is row R (never indexed); the zero slot is 2 MCAP
+  H.m_zero = 2 * MCAP;
+  auto mslot_of = [&](int s) { return s < R ? s : ((s - R) | 0x8000); };
+  std::vector<std::vector<int>> task_e;  // row | side << 15
   std::vector<std::vector<int>> btask(N);  // task | group << 24
   int max_btask = 0;
   for (int b = 0; b < N; b++) {
@@ -413,7 +410,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.o_task = B.alloc(H.T * TASK_W);
   for (int t = 0; t < H.T; t++)
     for (int k = 0; k < TASK_W; k++)
-      B.i(H.o_task + t * TASK_W + k, k < (int)task_e[t].size() ? task_e[t][k] : H.m_zero);
+      B.i(H.o_task + t * TASK_W + k, k < (int)task_e[t].size() ? task_e[t][k] : R);
   H.o_btask = B.alloc(N * BTASK_W);
   for (int b = 0; b < N; b++) {
     // padding: the zero task (index T, a zero partial) in the last group
@@ -522,19 +519,17 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // slot regions end with one zero slot (padding target of the gather lists)
   H.l_jslot = carve((2 * J + 1) * SLOT_STRIDE);
   H.l_aslot = carve((2 * K + 1) * ASLOT_STRIDE);
-  H.l_acc = carve(N * ACC_STRIDE);
-  // NearNeighbors ranks and the active-row list: culled scenes only (the
-  // SINGLE kernels never cull; MULTI's all-pairs scenes need the room)
-  H.l_ract = carve(H.n_nn ? R : 0);
+  // the active-row list: culled scenes only (the SINGLE kernels never cull;
+  // MULTI's all-pairs scenes need the room)
   H.l_alist = carve(H.n_nn ? H.info_rows : 0);
   H.l_red = carve(64);
   // NearNeighbors: each wave's sorted picks (64-bit keys) when an env spans
-  // up to 4 waves
+  // up to 4 waves (carved with the env-step regions below; the MULTI kernel
+  // keeps them in its task-partials region)
   {
     int max_cut = 0;
     for (int g = 0; g < G; g++) max_cut = std::max(max_cut, d->col_cutoff[g]);
     H.nnl_words = 2 * 4 * max_cut;
-    H.l_nnl = carve(H.nnl_words);
   }
   // the MULTI kernel's row tables: the rows' collidables as the distinct
   // (body, offset, end, radius) records, whose centres the broad phase and
@@ -581,6 +576,11 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // (swimmer: + drag, grasp: 3 palm actions), the staged action row (every
   // index an actuator or force reads: jp.take clips into the row, so no read
   // lands past these words)
+  // (the Info accumulators and the NearNeighbors ranks: the MULTI kernel
+  // keeps them in its contact slots / contact buffer, dead when these live)
+  H.l_acc = carve(N * ACC_STRIDE);
+  H.l_ract = carve(H.n_nn ? R : 0);
+  H.l_nnl = carve(H.nnl_words);
   H.l_ang = carve(2 * D);
   H.xact_words = std::max(16, (d->action_size + 12 + 3) & ~3);
   H.l_xact = carve(H.xact_words);
@@ -593,12 +593,20 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // in registers and needs 6-word slots plus the task partials
   const int tail = off;
   off = tail_m;
-  H.l_mslot = carve((H.m_zero + 1) * MSLOT_STRIDE);
-  H.l_tslot = carve((H.T + 1) * TSLOT_STRIDE);
-  // the broad phase's near-row list (16-bit) and per-wave counts: all-pairs
-  // scenes only (culled scenes skip the broad phase)
-  H.l_near = carve(H.n_nn ? 0 : (R + 1) / 2);
-  H.l_nearc = carve(H.n_nn ? 0 : 16);
+  // the chunk's contact slots (2 MCAP + the zero slot; the Info accumulators
+  // alias them after the substeps)
+  H.l_mslot = carve(std::max((2 * MCAP + 1) * MSLOT_STRIDE, N * ACC_STRIDE));
+  // the task partials; before the passes read them the same words hold the
+  // broad phase's near-row list (16-bit), the NearNeighbors pick lists and the
+  // serial picks' distances
+  H.l_tslot = carve(std::max({(H.T + 1) * TSLOT_STRIDE, (R + 1) / 2, H.nnl_words, H.n_nn ? R : 0}));
+  H.l_near = H.l_tslot;
+  H.l_cnt = carve(32);
+  H.l_nearc = H.l_cnt;
+  // the rows' compact contact indices (16-bit, R + 1: the padding row R)
+  H.l_sidx = carve((R + 2) / 2);
+  // the penetrating rows' contacts, then their rows (16-bit)
+  H.l_cbuf = carve(std::max(MCBUF * MCB_W + MCBUF / 2, H.n_nn ? R : 0));
   // the broad phase's row bounds and centres (constants, then world), staged
   // once per launch
   H.l_bimg = carve(BI_WORDS * R);
@@ -606,11 +614,11 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   H.env_words_m = (off + 63) & ~63;
   if (getenv("BX_PLAN_DEBUG"))
     fprintf(stderr,
-            "bx plan (words): qp..red %d  mslot %d  tslot %d (T=%d)  near %d  bimg %d  cen %d "
-            "(n_cen=%d n_mat=%d)  ract %d  alist %d  nnl %d  m_zero %d  env_words_m %d\n",
-            H.l_red + 64, (H.m_zero + 1) * MSLOT_STRIDE, (H.T + 1) * TSLOT_STRIDE, H.T,
-            H.l_bimg - H.l_near, BI_WORDS * R, 4 * (3 * H.n_cen + H.n_mat + N), H.n_cen, H.n_mat,
-            H.n_nn ? R : 0, H.n_nn ? H.info_rows : 0, H.nnl_words, H.m_zero, H.env_words_m);
+            "bx plan (words): qp..red %d  mslot %d  tslot %d (T=%d)  cnt+sidx+cbuf %d  bimg %d  "
+            "cen %d (n_cen=%d n_mat=%d)  ract %d  alist %d  nnl %d  env_words_m %d (%d B)\n",
+            H.l_red + 64, H.l_tslot - H.l_mslot, H.l_cnt - H.l_tslot, H.T, H.l_bimg - H.l_cnt,
+            H.l_cen - H.l_bimg, 4 * (3 * H.n_cen + H.n_mat + N), H.n_cen, H.n_mat,
+            H.n_nn ? R : 0, H.n_nn ? H.info_rows : 0, H.nnl_words, H.env_words_m, 4 * H.env_words_m);
   off = tail;
   H.l_rowd = carve(R * ROWD_STRIDE);
   H.l_cslot = carve((2 * R + 1) * SLOT_STRIDE);
@@ -635,7 +643,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     for (int b = 0; b < N; b++) mxja = std::max({mxja, jl[b].size(), al[b].size()});
     // (and its LDS tail within one workgroup's 160 KB)
     H.multi = (!H.single && L > 64 && !H.spring && !xcol && N <= 256 && J <= 256 && K <= 256 &&
-               H.T <= 256 && R <= MULTI_MR * 256 && mxja <= 8 && max_btask <= BTASK_W && mtab_ok &&
+               H.T <= 2 * 256 && G < 64 && R < 0x7FFF && mxja <= 8 && max_btask <= BTASK_W && mtab_ok &&
                (size_t)H.env_words_m * 4 <= 160 * 1024) ? 1 : 0;
     H.act_same = 1;
     for (int a = 0; a < K; a++)
@@ -716,10 +724,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         fl |= (uint32_t)((int)B.w[og + G_INFO] + x - (int)B.w[og + G_R0]) << BIF_INFO_SHIFT;
       }
       bw[BI_FLAGS] = fl;
-      bw[BI_BSLOT] = (uint32_t)mb[x];
     }
     H.o_bimg = B.alloc(BI_WORDS * R);
     for (int k = 0; k < BI_WORDS * R; k++) B.w[H.o_bimg + k] = bimg[k];
+    B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
     H.o_cen = B.alloc(8 * H.n_cen + 4 * H.n_mat + 4 * N);
     for (int k = 0; k < H.n_cen; k++)
       for (int i = 0; i < 8; i++) B.w[H.o_cen + 8 * k + i] = cens[k][i];
@@ -828,6 +836,10 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     const bool off = getenv("BX_NO_MULTI_JH") && atoi(getenv("BX_NO_MULTI_JH"));
     mjh = ok && !off;
   }
+  // MULTI threads per env: 128 when the bodies, joints (joint halves: two
+  // lanes each), actuators and gather tasks (two per lane) fit, so four envs
+  // share a CU (two waves each, 256 registers, <= 40 KB of LDS); else 256
+  H.multi_L = (N <= 128 && K <= 128 && (mjh ? 2 * J <= 128 : J <= 128) && H.T <= 2 * 128) ? 128 : 256;
   if (mjh) {
     B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
     H.o_mjh = B.alloc(MJ_W * MJ_LANES);
@@ -971,7 +983,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   S->multi_ok = H.multi != 0 && (S->feat & (1 | 2 | 16 | 64)) == 0;
   S->mode = S->single_ok ? 1 : (S->multi_ok ? 3 : 0);
   S->host = std::move(B.w);
-  S->L = S->multi_ok ? 256 : L;
+  S->L = S->multi_ok ? H.multi_L : L;
   S->tpb = S->L > 64 ? S->L : 64;
   S->lds_env = (size_t)(L > 64 ? 1 : 64 / L) * H.env_words * 4;
   S->lds_reset = (size_t)64 * N * 13 * 4;
@@ -1147,9 +1159,10 @@ int bx_system_create(const bx_desc* desc, const bx_reset_desc* reset, int device
 
 int bx_system_destroy(bx_system* S) {
   if (!S) return 0;
-  if (S->blob) {
+  if (S->blob || S->movf) {
     DEVICE_SCOPE(S);
-    HIP_OK(hipFree(S->blob));
+    if (S->movf) HIP_OK(hipFree(S->movf));
+    if (S->blob) HIP_OK(hipFree(S->blob));
   }
   delete S;
   return 0;
@@ -1187,8 +1200,8 @@ int bx_system_set_variant(bx_system* S, int lanes, int mode) {
   if (mode < 0 || mode > 3) return fail("mode must be 0 (global), 1 (single), 2 (lds) or 3 (multi)");
   if (mode == 1 && (!S->single_ok || lanes < S->min_L || lanes > 64 || lanes > S->hdr.L))
     return fail("system does not fit the single-item-per-lane kernel at that width");
-  if (mode == 3 && (!S->multi_ok || lanes != 256))
-    return fail("system does not fit the MULTI-mode kernel (256 lanes)");
+  if (mode == 3 && (!S->multi_ok || (lanes != 256 && !(lanes == 128 && S->hdr.multi_L == 128))))
+    return fail("system does not fit the MULTI-mode kernel at that width (128 or 256 lanes)");
   int old_L = S->L, old_m = S->mode, old_t = S->tpb;
   S->L = lanes;
   S->mode = mode;
@@ -1243,11 +1256,25 @@ int bx_system_step(bx_system* S, int64_t n_envs, const bx_qp* qin, const float* 
   a.act_stride = act_stride;
   a.act_width = act_width;
   if (info) a.info = *info;
+  if (S->mode == 3 && S->hdr.R > MCBUF && S->movf_envs < n_envs) {
+    // the overflow contacts (a pass with more than MCBUF penetrating rows):
+    // grown to this batch once; a capture cannot allocate
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_OK(hipStreamIsCapturing(as_stream(stream), &cs));
+    if (cs != hipStreamCaptureStatusNone)
+      return fail("MULTI overflow buffer: step the batch once before capturing it");
+    HIP_OK(hipStreamSynchronize(as_stream(stream)));
+    if (S->movf) HIP_OK(hipFree(S->movf));
+    S->movf = nullptr;
+    S->movf_envs = 0;
+    HIP_OK(hipMalloc(&S->movf, (size_t)n_envs * (S->hdr.R - MCBUF) * MOVF_W * 4));
+    S->movf_envs = n_envs;
+  }
+  a.movf = S->movf;
   if (S->mode == 1)
     HIP_OK(launch_system_step_single(S->L, S->feat, S->gw, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   else if (S->mode == 3)
-    HIP_OK(launch_system_step_multi(S->feat | (S->hdr.o_mjh ? 128 : 0), (S->hdr.R + 255) / 256, n_envs,
-                                    step_lds(S), as_stream(stream), a));
+    HIP_OK(launch_system_step_multi(S->L, S->hdr.o_mjh ? 1 : 0, n_envs, step_lds(S), as_stream(stream), a));
   else
     HIP_OK(launch_system_step_generic(S->L, S->mode, S->feat, S->tpb, n_envs, step_lds(S), as_stream(stream), a));
   return 0;

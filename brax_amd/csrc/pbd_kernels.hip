@@ -86,9 +86,11 @@ struct Env {
   float* xact;   // the action an env program hands System.step (xact_words)
   float* arow;   // the env's action row, its first act_read words (env step)
   float* nnl;    // NearNeighbors per-wave pick lists (nnl_words)
-  uint16_t* nearl;  // MULTI: the pass's near rows
-  int* nearc;       // MULTI: the broad phase's per-wave counts
-  uint4* bimg;      // MULTI: the rows' bounds / flags (BI_*), staged per launch
+  uint16_t* nearl;  // MULTI: the pass's near rows (in the task partials' words)
+  int* nearc;       // MULTI: per-wave ballot counts (broad phase 0..15, listing 16..)
+  uint32_t* bimg;   // MULTI: the rows' bounds / flags (BI_WORDS each), staged per launch
+  uint16_t* sidx;   // MULTI: each row's compact contact index this pass (0xFFFF: none)
+  float* cbuf;      // MULTI: the listed rows' contacts (MCBUF x MCB_W), then their rows
   uint4* cen;       // MULTI: the collidables (2 groups each)
   uint4* mat;       // MULTI: the materials (fric, elas, scale, thr)
   uint4* bod;       // MULTI: the bodies' (mass, inverse inertia), then the placed centres
@@ -1517,10 +1519,15 @@ __device__ __forceinline__ Env carve(float* base, const BlobHdr& H, bool multi =
     // as NearNeighbors scratch before the substeps
     E.rowd = nullptr;
     E.cslot = al16(base + H.l_mslot);
+    E.acc = E.cslot;  // the Info accumulators, written after the last pass
     E.tslot = al16(base + H.l_tslot);
     E.nearl = reinterpret_cast<uint16_t*>(base + H.l_near);
-    E.nearc = reinterpret_cast<int*>(base + H.l_nearc);
-    E.bimg = reinterpret_cast<uint4*>(al16(base + H.l_bimg));
+    E.nnl = E.tslot;  // NearNeighbors' lists, before the first task phase
+    E.nearc = reinterpret_cast<int*>(base + H.l_cnt);
+    E.sidx = reinterpret_cast<uint16_t*>(base + H.l_sidx);
+    E.cbuf = al16(base + H.l_cbuf);
+    E.ract = reinterpret_cast<int*>(E.cbuf);  // NearNeighbors' ranks, before the first pass
+    E.bimg = reinterpret_cast<uint32_t*>(base + H.l_bimg);
     E.cen = reinterpret_cast<uint4*>(al16(base + H.l_cen));
     E.mat = E.cen + 2 * H.n_cen;
     E.bod = E.mat + H.n_mat;
@@ -1678,7 +1685,8 @@ __device__ __forceinline__ float centre_dist(const Env& E, const BlobHdr& H, uns
 // two collidables, their bodies' masses and inverse inertias, its
 // material): the words the row image held, with no L2 read
 __device__ __forceinline__ RowC row_from_lds(const Env& E, int r) {
-  const uint4 g0 = E.bimg[r];
+  const uint32_t* g = E.bimg + r * BI_WORDS;
+  const uint4 g0 = make_uint4(g[BI_CEN], g[BI_REACH], g[BI_FLAGS], 0u);
   const uint4 a0 = E.cen[2 * (g0.x & 0xFFFFu)], a1 = E.cen[2 * (g0.x & 0xFFFFu) + 1];
   const uint4 b0 = E.cen[2 * (g0.x >> 16)], b1 = E.cen[2 * (g0.x >> 16) + 1];
   const uint4 mt = E.mat[(g0.z >> BIF_MAT_SHIFT) & 0xFFu];
@@ -1688,7 +1696,6 @@ __device__ __forceinline__ RowC row_from_lds(const Env& E, int r) {
   x.b = (int)b0.x;
   x.fn = (int)((g0.z >> BIF_FN_SHIFT) & 0xFu);
   x.oneway = (g0.z & BIF_OW) ? 1 : 0;
-  x.bslot = (int)g0.w;
   x.a_pos = mk(__uint_as_float(a0.y), __uint_as_float(a0.z), __uint_as_float(a0.w));
   x.a_end = mk(__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z));
   x.a_rad = __uint_as_float(a1.w);
@@ -1729,22 +1736,21 @@ __device__ __forceinline__ RowC row_from_lds(const Env& E, int r) {
 // placed this step (place_centres, before the call): no dependent L2 reads
 // (always inlined: a call would take the caller's header by reference and
 // put the whole struct in scratch, reloaded in every phase of the MULTI loop)
-template <int L, bool MT = false>
+template <int L, bool MT = false, int NK = 4>
 __device__ __forceinline__ void nn_select(const Cst& c, const BlobHdr& H, const Env& E, int lane,
                           unsigned long long* nsa = nullptr, unsigned long long* nsl = nullptr) {
   // Pairs rows are always active (rank 0) at their fixed Info index; culled
   // rows start unselected with empty (zero, uncounted) slots
   if constexpr (MT) {
+    // (the MULTI kernel: a culled row gets no compact index, so its slots
+    // are never read)
     for (int r = lane; r < H.R; r += L) {
-      const uint4 g0 = E.bimg[r];
-      if (g0.z & BIF_CULL) {
+      const uint32_t fl = E.bimg[r * BI_WORDS + BI_FLAGS];
+      if (fl & BIF_CULL) {
         E.ract[r] = -1;
-        const v3 z = mk(0.f, 0.f, 0.f);
-        st_mslot(E.cslot + r * MSLOT_STRIDE, z, z);
-        st_mslot(E.cslot + (int)g0.w * MSLOT_STRIDE, z, z);
       } else {
         E.ract[r] = 0;
-        E.alist[g0.z >> BIF_INFO_SHIFT] = r;
+        E.alist[fl >> BIF_INFO_SHIFT] = r;
       }
     }
   } else
@@ -1762,7 +1768,9 @@ __device__ __forceinline__ void nn_select(const Cst& c, const BlobHdr& H, const 
   BX_NSTAMP(14);
   constexpr int W = L < 64 ? L : 64;  // the env's lanes in one wave
   constexpr int NW = L / W;           // the env's waves
-  constexpr int NK = 4;               // candidates per lane held in registers
+  // NK: candidates per lane held in registers (4; the 128-thread MULTI
+  // kernel 8, so a wave still holds a culled group of up to 8 x 128 rows)
+  static_assert(NK == 4 || NK == 8, "4 or 8 keys per lane");
   const int wl = lane % W;            // lane within the env's part of its wave
   const int wv = lane / W;            // the env's wave
   for (int g = 0; g < H.G; g++) {
@@ -1777,8 +1785,9 @@ __device__ __forceinline__ void nn_select(const Cst& c, const BlobHdr& H, const 
         const int r = r0 + lane + i * L;
         if constexpr (MT) {
           if (r < r1) {
-            const uint4 g0 = E.bimg[r];
-            const unsigned d = (g0.z & BIF_MASK) ? 0x7F800000u : __float_as_uint(centre_dist(E, H, g0.x));
+            const uint32_t* g0 = E.bimg + r * BI_WORDS;
+            const unsigned d = (g0[BI_FLAGS] & BIF_MASK) ? 0x7F800000u
+                                                         : __float_as_uint(centre_dist(E, H, g0[BI_CEN]));
             k[i] = ((unsigned long long)d << 32) | (unsigned)r;
           } else {
             k[i] = ~0ull;
@@ -1793,21 +1802,35 @@ __device__ __forceinline__ void nn_select(const Cst& c, const BlobHdr& H, const 
         a = lo;
         b = hi;
       };
-      cs(k[0], k[1]); cs(k[2], k[3]); cs(k[0], k[2]); cs(k[1], k[3]); cs(k[1], k[2]);
+      if constexpr (NK == 4) {
+        cs(k[0], k[1]); cs(k[2], k[3]); cs(k[0], k[2]); cs(k[1], k[3]); cs(k[1], k[2]);
+      } else {
+        // Batcher's odd-even merge sort of 8 (19 compare-exchanges)
+        cs(k[0], k[1]); cs(k[2], k[3]); cs(k[4], k[5]); cs(k[6], k[7]);
+        cs(k[0], k[2]); cs(k[1], k[3]); cs(k[4], k[6]); cs(k[5], k[7]);
+        cs(k[1], k[2]); cs(k[5], k[6]);
+        cs(k[0], k[4]); cs(k[1], k[5]); cs(k[2], k[6]); cs(k[3], k[7]);
+        cs(k[2], k[4]); cs(k[3], k[5]);
+        cs(k[1], k[2]); cs(k[3], k[4]); cs(k[5], k[6]);
+      }
       BX_NSTAMP(12);
       unsigned long long* lst = reinterpret_cast<unsigned long long*>(E.nnl);
       if constexpr (NW > 1) {
-        // each wave's 4 x 64 keys sorted ascending by a bitonic network
-        // (element 4 wl + q in lane wl's k[q]): the lane's sorted four are
-        // the size-4 blocks (odd lanes' reversed: descending), then per block
-        // size the lane-exchange strides (>= 4 elements: lane ^ stride / 4,
-        // two 32-bit lane swizzles per key) and the in-lane strides 2, 1.
-        // The union's order is the picks' (distance, then row: the 64-bit
+        // each wave's NK x 64 keys sorted ascending by a bitonic network
+        // (element NK wl + q in lane wl's k[q]): the lane's sorted NK are
+        // the size-NK blocks (odd lanes' reversed: descending), then per block
+        // size the lane-exchange strides (>= NK elements: lane ^ stride / NK,
+        // two 32-bit lane swizzles per key) and the in-lane strides NK / 2 ..
+        // 1. The union's order is the picks' (distance, then row: the 64-bit
         // key); its first `cut` keys are the wave's list.
-        static_assert(NW == 1 || (W == 64 && NK == 4), "bitonic lists: 4 keys x 64 lanes");
+        static_assert(NW == 1 || W == 64, "bitonic lists: NK keys x 64 lanes");
         if (wl & 1) {
-          const unsigned long long t0 = k[0], t1 = k[1];
-          k[0] = k[3]; k[1] = k[2]; k[2] = t1; k[3] = t0;
+#pragma unroll
+          for (int q = 0; q < NK / 2; q++) {
+            const unsigned long long t = k[q];
+            k[q] = k[NK - 1 - q];
+            k[NK - 1 - q] = t;
+          }
         }
         auto ced = [](unsigned long long& a, unsigned long long& b, bool up) {
           const bool sw = up ? (b < a) : (a < b);
@@ -1816,10 +1839,10 @@ __device__ __forceinline__ void nn_select(const Cst& c, const BlobHdr& H, const 
           b = sw ? x : b;
         };
 #pragma unroll
-        for (int size = 8; size <= 256; size <<= 1) {
-          const bool up = ((wl * 4) & size) == 0;
+        for (int size = 2 * NK; size <= 64 * NK; size <<= 1) {
+          const bool up = ((wl * NK) & size) == 0;
 #pragma unroll
-          for (int d = size >> 3; d >= 1; d >>= 1) {
+          for (int d = size / (2 * NK); d >= 1; d >>= 1) {
             const bool keep_min = ((wl & d) == 0) == up;
 #pragma unroll
             for (int q = 0; q < NK; q++) {
@@ -1829,13 +1852,16 @@ __device__ __forceinline__ void nn_select(const Cst& c, const BlobHdr& H, const 
               k[q] = keep_min ? (o < k[q] ? o : k[q]) : (o < k[q] ? k[q] : o);
             }
           }
-          ced(k[0], k[2], up); ced(k[1], k[3], up);
-          ced(k[0], k[1], up); ced(k[2], k[3], up);
+#pragma unroll
+          for (int st = NK / 2; st >= 1; st >>= 1)
+#pragma unroll
+            for (int q = 0; q < NK; q++)
+              if ((q & st) == 0) ced(k[q], k[q + st], up);
         }
 #pragma unroll
         for (int q = 0; q < NK; q++)
-          if (4 * wl + q < cut) lst[wv * cut + 4 * wl + q] = k[q];
-        // (a cut past the wave's 256 keys: the rest of its list is empty)
+          if (NK * wl + q < cut) lst[wv * cut + NK * wl + q] = k[q];
+        // (a cut past the wave's NK x 64 keys: the rest of its list is empty)
         for (int i = NK * W + wl; i < cut; i += W) lst[wv * cut + i] = ~0ull;
       } else
       for (int kk = 0; kk < cut; kk++) {
@@ -1847,7 +1873,9 @@ __device__ __forceinline__ void nn_select(const Cst& c, const BlobHdr& H, const 
         const bool own = cur != ~0ull && hi == dmin && lo == rmin;
         if (own) {
           // the picked key leaves the lane's sorted registers
-          k[0] = k[1]; k[1] = k[2]; k[2] = k[3]; k[3] = ~0ull;
+#pragma unroll
+          for (int q = 0; q + 1 < NK; q++) k[q] = k[q + 1];
+          k[NK - 1] = ~0ull;
           if constexpr (NW == 1) {
             E.ract[(int)lo] = kk;
             E.alist[info + kk] = (int)lo;
@@ -3096,7 +3124,6 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
 // collider group into a partial, then each body adds its <= BTASK_W partials
 // group by group, each group divided by (eps + count) (colliders.py:198-240).
 // ---------------------------------------------------------------------------
-template <int MR>
 struct HoistM {
   bool hasB, hasJ, hasA;
   BodyC B;
@@ -3104,14 +3131,29 @@ struct HoistM {
   ActC A;
   JSide S;   // MJH: the lane's side, its joint's first limit row
   JLim JL;
-  GList<MAXG> jl, al;
-  int te[TASK_W];   // the lane's task: contact slot indices (padding: the zero slot)
-  int bt[BTASK_W];  // the lane's body: task | group << 24 (padding: the zero task)
+  // the body's joint / actuator slot lists (padding: the zero slots), two
+  // 16-bit entries per word (registers are the MULTI kernel's limit: 256 at
+  // two waves per SIMD)
+  uint32_t jl[MAXG / 2], al[MAXG / 2];
+  // the lane's two tasks (lane, lane + L): TASK_W entries each (row | side
+  // << 15; padding: row R), two 16-bit entries per word
+  uint32_t te[2][TASK_W / 2];
+  // the lane's body: task | group << 10 (padding: the zero task), 16-bit pairs
+  uint32_t bt[BTASK_W / 2];
 };
+__device__ __forceinline__ int ent16(const uint32_t* p, int k) {
+  return (int)((p[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+}
+template <int M>
+__device__ __forceinline__ v3 gsum3p(const uint32_t* g, const float* base, int stride) {
+  v3 s = mk(0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < M; k++) s = s + ld_v3a(base + ent16(g, k) * stride);
+  return s;
+}
 // MJH: the lane's joint side from the MULTI joint-halves image (MJ_*, 20
 // independent 16-byte loads), parsed as the SINGLE lane image's records
-template <int MR>
-__device__ __forceinline__ void load_mjh(const Cst& c, const BlobHdr& H, int lane, HoistM<MR>& X) {
+__device__ __forceinline__ void load_mjh(const Cst& c, const BlobHdr& H, int lane, HoistM& X) {
   const int jx = ((lane >> 4) << 3) + (lane & 7);
   X.hasJ = jx < H.J;
   X.hasA = jx < H.K;
@@ -3167,39 +3209,81 @@ __device__ __forceinline__ void load_mjh(const Cst& c, const BlobHdr& H, int lan
   X.S.body = n(MJ_SIDE + LS_BODY);
 }
 
-template <int L, int MR, bool MJH = false>
+template <int L, bool MJH = false>
 __device__ __forceinline__ void load_hoist_multi(const Cst& c, const BlobHdr& H, int lane,
-                                                 HoistM<MR>& X) {
+                                                 HoistM& X) {
   X.hasB = lane < H.N;
   X.hasJ = lane < H.J;
   X.hasA = lane < H.K;
   const int b = X.hasB ? lane : 0;
   X.B = load_body(c, H, b);
-  X.jl = load_glist<MAXG>(c, H.o_jl_off, H.o_jl, b, X.hasB, 2 * H.J);
-  X.al = load_glist<MAXG>(c, H.o_al_off, H.o_al, b, X.hasB, 2 * H.K);
-  const bool hasT = lane < H.T;
+  {
+    const GList<MAXG> jl = load_glist<MAXG>(c, H.o_jl_off, H.o_jl, b, X.hasB, 2 * H.J);
+    const GList<MAXG> al = load_glist<MAXG>(c, H.o_al_off, H.o_al, b, X.hasB, 2 * H.K);
 #pragma unroll
-  for (int k = 0; k < TASK_W; k++) X.te[k] = hasT ? c.i(H.o_task + lane * TASK_W + k) : H.m_zero;
+    for (int k = 0; k < MAXG / 2; k++) {
+      X.jl[k] = (uint32_t)jl.e[2 * k] | ((uint32_t)jl.e[2 * k + 1] << 16);
+      X.al[k] = (uint32_t)al.e[2 * k] | ((uint32_t)al.e[2 * k + 1] << 16);
+    }
+  }
 #pragma unroll
-  for (int k = 0; k < BTASK_W; k++) X.bt[k] = X.hasB ? c.i(H.o_btask + b * BTASK_W + k) : H.T;
+  for (int q = 0; q < 2; q++) {
+    const int t = lane + q * L;
+    const bool hasT = t < H.T;
+#pragma unroll
+    for (int k = 0; k < TASK_W / 2; k++) {
+      const uint32_t lo = hasT ? (uint32_t)c.i(H.o_task + t * TASK_W + 2 * k) : (uint32_t)H.R;
+      const uint32_t hi = hasT ? (uint32_t)c.i(H.o_task + t * TASK_W + 2 * k + 1) : (uint32_t)H.R;
+      X.te[q][k] = lo | (hi << 16);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < BTASK_W / 2; k++) {
+    uint32_t w[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const uint32_t v = X.hasB ? (uint32_t)c.i(H.o_btask + b * BTASK_W + 2 * k + i) : (uint32_t)H.T;
+      w[i] = (v & 0x3FFu) | ((v >> 24) << 10);
+    }
+    X.bt[k] = w[0] | (w[1] << 16);
+  }
   if constexpr (MJH) {
-    load_mjh<MR>(c, H, lane, X);
+    load_mjh(c, H, lane, X);
   } else {
     if (H.J > 0) X.J = load_joint(c, H, X.hasJ ? lane : 0);
     if (H.K > 0) X.A = load_act(c, H, X.hasA ? lane : 0);
   }
 }
 
-// phase 1: the lane's task partial, its slots summed in list order; a slot
+// phase 1: a task's partial, its entries summed in list order; an entry
 // counts when its linear part is nonzero (the reference's any(dq_pos) /
-// any(dp_vel) per row, colliders.py:187-195,231-239)
-__device__ __forceinline__ void task_sum(const int* te, const float* ms, float* out) {
+// any(dp_vel) per row, colliders.py:187-195,231-239). An entry is a row and
+// side: its slot in chunk ch is the row's compact index less the chunk's
+// first, on the side's half, when the row is listed in this chunk, else the
+// zero slot (the rows without an update). Chunks after the first add to
+// the partial (one chunk: the sum of every entry's slot in list order, as
+// when every row had a slot)
+__device__ __forceinline__ void task_sum(const uint32_t* te, const uint16_t* sidx, const float* ms,
+                                         float* out, int ch) {
   v3 a = mk(0.f, 0.f, 0.f), l = mk(0.f, 0.f, 0.f);
   float n = 0.f;
+  if (ch > 0) {
+    const f32x4 t0 = ld4a(out), t1 = ld4a(out + 4);
+    a = mk(t0[0], t0[1], t0[2]);
+    l = mk(t0[3], t1[0], t1[1]);
+    n = t1[2];
+  }
+  int slot[TASK_W];
+#pragma unroll
+  for (int k = 0; k < TASK_W; k++) {
+    const uint32_t e = (te[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+    const uint32_t rel = (uint32_t)sidx[e & 0x7FFFu] - (uint32_t)(ch * MCAP);
+    slot[k] = rel < (uint32_t)MCAP ? (int)rel + (int)(e >> 15) * MCAP : 2 * MCAP;
+  }
 #pragma unroll
   for (int k = 0; k < TASK_W; k++) {
     v3 v, w;
-    ld_mslot(ms + te[k] * MSLOT_STRIDE, v, w);
+    ld_mslot(ms + slot[k] * MSLOT_STRIDE, v, w);
     a = a + v;
     l = l + w;
     n += nonzero3(v);
@@ -3210,18 +3294,19 @@ __device__ __forceinline__ void task_sum(const int* te, const float* ms, float* 
 
 // phase 2: sum over the body's groups of (group's partials) / (eps + count):
 // the linear part a and the angular part l
-__device__ __forceinline__ void body_combine(const int* bt, const float* ts, float eps, v3& a,
+__device__ __forceinline__ void body_combine(const uint32_t* bt, const float* ts, float eps, v3& a,
                                              v3& l) {
   a = mk(0.f, 0.f, 0.f);
   l = mk(0.f, 0.f, 0.f);
   v3 ga = mk(0.f, 0.f, 0.f), gl = mk(0.f, 0.f, 0.f);
   float gn = 0.f;
-  int g = bt[0] >> 24;
+  int g = ent16(bt, 0) >> 10;
 #pragma unroll
   for (int k = 0; k < BTASK_W; k++) {
-    const float* t = ts + (bt[k] & 0xFFFFFF) * TSLOT_STRIDE;
+    const int e = ent16(bt, k);
+    const float* t = ts + (e & 0x3FF) * TSLOT_STRIDE;
     const f32x4 t0 = ld4a(t), t1 = ld4a(t + 4);
-    const int gk = bt[k] >> 24;
+    const int gk = e >> 10;
     if (gk != g) {
       const float d = eps + gn;
       a = a + ga / d;
@@ -3265,9 +3350,10 @@ __device__ unsigned long long bx_mstamp_wave[4096][16];
 #define BX_MSTAMP(k) do {} while (0)
 #endif
 
-template <int L, int F, int MR>
+template <int L, int F>
 __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int lane, bool valid,
-                               const float* act, int aw, const HoistM<MR>& X, RowInfoOut io) {
+                               const float* act, int aw, const HoistM& X, RowInfoOut io,
+                               float* ovf) {
 #ifdef BX_MSTAMPS
   unsigned long long ms_acc[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long ms_last;
@@ -3277,6 +3363,8 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
   const v3 g = mk(H.gx, H.gy, H.gz);
   // MJH (the joint halves, F_JH): the lane's joint jx and side
   constexpr bool MJH = (F & F_JH) != 0;
+  constexpr int NWV = L / 64;
+  const int wv = lane >> 6;
   const int mjx = ((lane >> 4) << 3) + (lane & 7);
   const bool mchild = (lane & 8) != 0;
   const bool info_rows = io.pos || io.normal || io.pen || io.cell;
@@ -3296,37 +3384,41 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
   if constexpr ((F & F_FORCE) != 0) {
     if (X.hasB) body_forces(c, H, lane, act, aw, valid, fv, fa);
   }
-  // NearNeighbors.update once per step (system.py:320-321): ranks in E.ract,
-  // culled rows' slots zeroed (their lanes skip them below)
+  // NearNeighbors.update once per step (system.py:320-321): the selected
+  // rows' ranks in E.ract, in Info order in E.alist (the culled rows have no
+  // contact index, so their slots are never read)
   if (H.n_nn) {
     place_centres<L>(H, E, lane);
     esync<L>();
 #ifdef BX_MSTAMPS
-    nn_select<L, true>(c, H, E, lane, ms_acc, &ms_last);
+    nn_select<L, true, (L >= 256 ? 4 : 8)>(c, H, E, lane, ms_acc, &ms_last);
 #else
-    nn_select<L, true>(c, H, E, lane);
+    nn_select<L, true, (L >= 256 ? 4 : 8)>(c, H, E, lane);
 #endif
   }
   BX_MSTAMP(9);
-  // the lane's rows: the m-th is active row x = lane + m * L in Info order
-  // (the culled scenes' selected rows compacted: E.alist), so lanes past
-  // the active count, and whole waves, skip the contact passes
+  // the step's work rows: row x of the culled scenes' active rows in Info
+  // order (E.alist), else row x
   const int nact = H.n_nn ? H.info_rows : H.R;
 #define BX_MULTI_RX(x) (H.n_nn ? E.alist[x] : (x))
-#define BX_MULTI_SKIP(x, r) ((x) >= nact)
-  // the row's contact between the position and velocity passes, and its
-  // slot word (one-way flag, b-side slot) for the velocity pass's stores
-  v3 cpos[MR], cn[MR];
-  float pen[MR], dl[MR];
-  int meta[MR];
+  // a penetrating row's contact (compact index y): LDS below MCBUF, the env's
+  // overflow slice past it
+  auto cb_at = [&](int y) -> float* {
+    return y < MCBUF ? E.cbuf + y * MCB_W : ovf + (int64_t)(y - MCBUF) * MOVF_W;
+  };
+  uint16_t* cbrow = reinterpret_cast<uint16_t*>(E.cbuf + MCBUF * MCB_W);
+  auto cb_row = [&](int y) -> int {
+    return y < MCBUF ? (int)cbrow[y] : __float_as_int(ovf[(int64_t)(y - MCBUF) * MOVF_W + 8]);
+  };
+  // the tasks' sums of chunk ch (TASK_W entries each, in list order; a partial
+  // carried over from the chunk before)
+  auto tasks = [&](int ch) {
 #pragma unroll
-  for (int m = 0; m < MR; m++) {
-    cpos[m] = mk(0.f, 0.f, 0.f);
-    cn[m] = mk(0.f, 0.f, 0.f);
-    pen[m] = 0.f;
-    dl[m] = 0.f;
-    meta[m] = 0;
-  }
+    for (int k = 0; k < 2; k++) {
+      const int t = lane + k * L;
+      if (t < H.T) task_sum(X.te[k], E.sidx, E.cslot, E.tslot + t * TSLOT_STRIDE, ch);
+    }
+  };
   for (int it = 0; it < H.substeps / 2; it++) {
     v3 ppos = q.pos;
     q4 prot = q.rot;
@@ -3368,8 +3460,8 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       BX_MSTAMP(0);
       // Euler.update(acc) + Euler.kinetic (integrators.py:50-93)
       if (X.hasB) {
-        v3 dpa = gsum3(X.al, E.aslot, ASLOT_STRIDE);
-        v3 dpj = gsum3(X.jl, E.jslot, SLOT_STRIDE);
+        v3 dpa = gsum3p<MAXG>(X.al, E.aslot, ASLOT_STRIDE);
+        v3 dpj = gsum3p<MAXG>(X.jl, E.jslot, SLOT_STRIDE);
         v3 vel = H.vexp * q.vel;
         vel = vel + (fv + g) * h;
         q.vel = mul(vel, X.B.pm);
@@ -3415,7 +3507,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
           v3 v;
           q4 r;
           float f;
-          ld_slot(E.jslot + X.jl.e[k] * SLOT_STRIDE, v, r, f);
+          ld_slot(E.jslot + ent16(X.jl, k) * SLOT_STRIDE, v, r, f);
           dp = dp + v;
           dr = dr + r;
         }
@@ -3432,62 +3524,55 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
     // Broad phase, on every pass but the step's last (whose contacts are the
     // step's Info): a capsule pair whose centres lie farther apart than its
     // reach cannot penetrate, so both its passes' updates are exact zeros;
-    // its slots are zeroed here and the pair left out of both passes. The
-    // near rows are listed in (m, wave, lane) order (E.nearl).
+    // the near rows are listed in (m, wave, lane) order (E.nearl) for the
+    // contact pass, the far rows sit it out (no slot: no update, no count).
     // (culled scenes skip it: NearNeighbors already keeps only near cells).
     // Without contact-row Info (System.step(..., info=False): no caller
     // reads the rows) the last pass takes it too: its far rows' Info is never
     // written
-    const bool bph = H.o_bimg != 0 && H.n_nn == 0 && (it + 1 < H.substeps / 2 || !info_rows);
+    const bool last = it + 1 == H.substeps / 2;
+    const bool bph = H.o_bimg != 0 && H.n_nn == 0 && (!last || !info_rows);
     int nwork = nact;
     if (bph) {
-      constexpr int NWV = L / 64;
-      const int wv = lane >> 6;
       int* cnt = E.nearc;
       // the capsule centres in the world, once for every row naming them
       place_centres<L>(H, E, lane);
       esync<L>();
-      bool nr[MR];
-      int rr[MR], rk[MR];
-#pragma unroll
-      for (int m = 0; m < MR; m++) {
-        const int x = lane + m * L;
-        const int r = x < nact ? BX_MULTI_RX(x) : -1;
+      // the lane's rows r = lane + m L: near bits, per (m, wave) counts
+      unsigned nmask = 0u;
+      const int nm = (H.R + L - 1) / L;
+      for (int m = 0; m < nm; m++) {
+        const int r = lane + m * L;
         bool near = false;
-        if (r >= 0) {
-          const uint4 g0 = E.bimg[r];
-          near = (g0.z & BIF_SKIP) == 0u;
+        if (r < H.R) {
+          const uint32_t* g0 = E.bimg + r * BI_WORDS;
+          near = (g0[BI_FLAGS] & BIF_SKIP) == 0u;
           if (!near) {
-            // + 1e-4: far above the fp32 error of the centres
-            const float cd = centre_dist(E, H, g0.x);
-            near = !(cd > __uint_as_float(g0.y) + 1e-4f) || is_nan(cd);
-          }
-          if (!near) {
-            // (a one-way row's b slot is the zero slot: zeros again)
-            const v3 z = mk(0.f, 0.f, 0.f);
-            st_mslot(E.cslot + r * MSLOT_STRIDE, z, z);
-            st_mslot(E.cslot + (int)g0.w * MSLOT_STRIDE, z, z);
+            // + 1e-4: far above the fp32 error of the centres; a NaN
+            // distance is near (a NaN row's impulses are NaN)
+            const float cd = centre_dist(E, H, g0[BI_CEN]);
+            near = !(cd > __uint_as_float(g0[BI_REACH]) + 1e-4f) || is_nan(cd);
           }
         }
-        nr[m] = near;
-        rr[m] = r;
+        nmask |= near ? (1u << m) : 0u;
         const unsigned long long bal = __ballot(near);
-        rk[m] = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-        if ((lane & 63) == 0) cnt[wv * MR + m] = __popcll(bal);
+        if ((lane & 63) == 0) cnt[m * NWV + wv] = __popcll(bal);
       }
       esync<L>();
       int total = 0;
-#pragma unroll
-      for (int m = 0; m < MR; m++) {
+      for (int m = 0; m < nm; m++) {
+        const bool near = (nmask >> m) & 1u;
+        const unsigned long long bal = __ballot(near);
+        const int rk = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
         int before = 0, mt = 0;
 #pragma unroll
         for (int w2 = 0; w2 < NWV; w2++) {
-          const int k = cnt[w2 * MR + m];
+          const int k = cnt[m * NWV + w2];
           before += w2 < wv ? k : 0;
           mt += k;
         }
-        if (nr[m]) E.nearl[total + before + rk[m]] = (uint16_t)rr[m];
+        if (near) E.nearl[total + before + rk] = (uint16_t)(lane + m * L);
         total += mt;
       }
       nwork = total;
@@ -3498,51 +3583,113 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
 #endif
     }
     BX_MSTAMP(11);
-    // Collider.position_apply (colliders.py:198-240): the lane's rows
-#pragma unroll
-    for (int m = 0; m < MR; m++) {
-      const int x = lane + m * L;
-      const int r = x < nwork ? (bph ? E.nearl[x] : BX_MULTI_RX(x)) : 0;
-      if (bph ? x >= nwork : BX_MULTI_SKIP(x, r)) continue;
-      RowC R = row_from_lds(E, r);
-      QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
-      v3 cvel;
-      contact_gen<F>(R, a, b, cpos[m], cvel, cn[m], pen[m]);
-      meta[m] = (R.oneway & 0xFF) | (R.bslot << 16);
-      v3 pap, pbp;
-      q4 par, pbr;
-      float unused;
-      ld_slot(E.prev + R.a * PREV_STRIDE, pap, par, unused);
-      ld_slot(E.prev + R.b * PREV_STRIDE, pbp, pbr, unused);
-      // a row that does not penetrate has exact-zero impulses in both passes
-      // (cm = 0, sm = 0): its math is skipped, by the whole wave when none of
-      // its rows of this iteration penetrates (most near capsule pairs)
-      v3 oap = mk(0.f, 0.f, 0.f), obp = mk(0.f, 0.f, 0.f);
-      q4 oar{0.f, 0.f, 0.f, 0.f}, obr{0.f, 0.f, 0.f, 0.f};
-      dl[m] = 0.f;
-      if (is_nan(pen[m])) {
-        // a NaN contact's impulses are NaN on both sides (the reference's
-        // masked products, colliders.py:332-333: NaN * 0)
-        const float pz = nan_of(pen[m]);
-        oap = obp = mk(pz, pz, pz);
-        oar = obr = q4{pz, pz, pz, pz};
-        dl[m] = pz;
-      } else if (pen[m] > 0.f) {
-        dl[m] = position_contact<F, true>(R, a, b, pap, par, pbp, pbr, cpos[m], cn[m], pen[m], oap,
-                                          oar, obp, obr);
+    // Collider.position_apply (colliders.py:198-240), first the contacts of
+    // the work rows (contact_gen); the pass's Info rows are written here. A
+    // row that does not penetrate has exact-zero impulses in both passes (its
+    // `c < 0` / `penetration > 0` masks, colliders.py:332, 437): only the
+    // penetrating (or NaN) rows are listed, in (m, wave, lane) order, with
+    // their contacts (E.cbuf / the overflow slice) and their compact index in
+    // E.sidx
+    int nstore = 0;
+    for (int m0 = 0, par = 0; m0 < nwork; m0 += L, par ^= 1) {
+      const int x = m0 + lane;
+      const bool has = x < nwork;
+      const int r = has ? (bph ? (int)E.nearl[x] : BX_MULTI_RX(x)) : 0;
+      v3 cp = mk(0.f, 0.f, 0.f), cn = mk(0.f, 0.f, 0.f);
+      float pen = 0.f;
+      bool st = false;
+      if (has) {
+        RowC R = row_from_lds(E, r);
+        QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+        v3 cvel;
+        contact_gen<F>(R, a, b, cp, cvel, cn, pen);
+        st = pen > 0.f || is_nan(pen);
+        // Info contact rows of the last position pass (system.py:36-43)
+        if (last && valid && info_rows) {
+          if (io.pos) st3(io.pos + x * 3, cp);
+          if (io.normal) st3(io.normal + x * 3, cn);
+          if (io.pen) io.pen[x] = pen;
+          if (io.cell) io.cell[x] = c.i(H.o_row + r * ROW_STRIDE + R_FLAT);
+        }
       }
-      st_mslot(E.cslot + r * MSLOT_STRIDE, oap, mk(oar.x, oar.y, oar.z));
-      if (!is_oneway<F>(R.oneway))
-        st_mslot(E.cslot + R.bslot * MSLOT_STRIDE, obp, mk(obr.x, obr.y, obr.z));
+      const unsigned long long bal = __ballot(st);
+      const int rk = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+      // (two count buffers: a wave may write the next iteration's counts
+      // while another still reads these)
+      int* cnt = E.nearc + 16 + par * NWV;
+      if ((lane & 63) == 0) cnt[wv] = __popcll(bal);
+      esync<L>();
+      int before = 0, tot = 0;
+#pragma unroll
+      for (int w2 = 0; w2 < NWV; w2++) {
+        const int k = cnt[w2];
+        before += w2 < wv ? k : 0;
+        tot += k;
+      }
+      if (st) {
+        const int y = nstore + before + rk;
+        float* d = cb_at(y);
+        if (y < MCBUF) {
+          st4a(d, f32x4{cp.x, cp.y, cp.z, cn.x});
+          st4a(d + 4, f32x4{cn.y, cn.z, pen, 0.f});
+          cbrow[y] = (uint16_t)r;
+        } else {
+          d[0] = cp.x; d[1] = cp.y; d[2] = cp.z; d[3] = cn.x;
+          d[4] = cn.y; d[5] = cn.z; d[6] = pen; d[8] = __int_as_float(r);
+        }
+        E.sidx[r] = (uint16_t)y;
+      }
+      nstore += tot;
     }
     esync<L>();
     BX_MSTAMP(4);
-    if (lane < H.T) task_sum(X.te, E.cslot, E.tslot + lane * TSLOT_STRIDE);
-    esync<L>();
+    // the position impulses of the listed rows, MCAP at a time: row y's sides
+    // into the chunk's slots, then the tasks add the chunk
+    const int nch = (nstore + MCAP - 1) / MCAP;
+    for (int ch = 0; ch < nch; ch++) {
+      const int y = ch * MCAP + lane;
+      if (lane < MCAP && y < nstore) {
+        float* d = cb_at(y);
+        const v3 cp = mk(d[0], d[1], d[2]), cn = mk(d[3], d[4], d[5]);
+        const float pen = d[6];
+        const int r = cb_row(y);
+        RowC R = row_from_lds(E, r);
+        v3 oap, obp;
+        q4 oar, obr;
+        float dl;
+        if (is_nan(pen)) {
+          // a NaN contact's impulses are NaN on both sides (the reference's
+          // masked products, colliders.py:332-333: NaN * 0)
+          const float pz = nan_of(pen);
+          oap = obp = mk(pz, pz, pz);
+          oar = obr = q4{pz, pz, pz, pz};
+          dl = pz;
+        } else {
+          QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+          v3 pap, pbp;
+          q4 par, pbr;
+          float unused;
+          ld_slot(E.prev + R.a * PREV_STRIDE, pap, par, unused);
+          ld_slot(E.prev + R.b * PREV_STRIDE, pbp, pbr, unused);
+          dl = position_contact<F, true>(R, a, b, pap, par, pbp, pbr, cp, cn, pen, oap, oar, obp, obr);
+        }
+        d[7] = dl;
+        st_mslot(E.cslot + lane * MSLOT_STRIDE, oap, mk(oar.x, oar.y, oar.z));
+        if (!is_oneway<F>(R.oneway)) st_mslot(E.cslot + (MCAP + lane) * MSLOT_STRIDE, obp, mk(obr.x, obr.y, obr.z));
+      }
+      // the zero task partial (the bodies' padding; the near list and the
+      // NearNeighbors scratch share these words)
+      if (ch == 0 && lane < TSLOT_STRIDE) E.tslot[H.T * TSLOT_STRIDE + lane] = 0.f;
+      esync<L>();
+      tasks(ch);
+      esync<L>();
+    }
     BX_MSTAMP(5);
     if (X.hasB) {
-      v3 dp, dl;
-      body_combine(X.bt, E.tslot, 1e-6f, dp, dl);
+      v3 dp = mk(0.f, 0.f, 0.f), dl = mk(0.f, 0.f, 0.f);
+      // (no listed row: every partial is zero, and 0 / (eps + 0) adds zeros)
+      if (nstore > 0) body_combine(X.bt, E.tslot, 1e-6f, dp, dl);
       // the body's one quaternion product of its summed angular impulses
       const q4 dr = 0.5f * vec_quat_mul(mul(X.B.I, dl), q.rot);
       q.pos = q.pos + mul(dp, X.B.pm);
@@ -3554,37 +3701,38 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
     }
     esync<L>();
     BX_MSTAMP(6);
-    // Collider.velocity_apply (colliders.py:155-196): the position pass's rows
-#pragma unroll
-    for (int m = 0; m < MR; m++) {
-      const int x = lane + m * L;
-      const int r = x < nwork ? (bph ? E.nearl[x] : BX_MULTI_RX(x)) : 0;
-      if (bph ? x >= nwork : BX_MULTI_SKIP(x, r)) continue;
-      // a row that does not penetrate stores exact zeros (sm = 0,
-      // colliders.py:584-658): no constants read, no state gathered
-      v3 oav = mk(0.f, 0.f, 0.f), oaa = oav, obv = oav, oba = oav;
-      if (is_nan(pen[m])) {
-        const float pz = nan_of(pen[m]);
-        oav = oaa = obv = oba = mk(pz, pz, pz);
-      } else if (pen[m] > 0.f) {
+    // Collider.velocity_apply (colliders.py:155-196): the listed rows
+    for (int ch = 0; ch < nch; ch++) {
+      const int y = ch * MCAP + lane;
+      if (lane < MCAP && y < nstore) {
+        const float* d = cb_at(y);
+        const v3 cp = mk(d[0], d[1], d[2]), cn = mk(d[3], d[4], d[5]);
+        const float pen = d[6], dl = d[7];
+        const int r = cb_row(y);
         RowC R = row_from_lds(E, r);
-        QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
-        v3 rap, rav, raa, rbp, rbv, rba;
-        ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
-        ld_rb(E.rb + R.b * RB_STRIDE, rbp, rbv, rba);
-        velocity_contact<F>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cpos[m], cn[m], pen[m], dl[m],
-                            oav, oaa, obv, oba);
+        v3 oav, oaa, obv, oba;
+        if (is_nan(pen)) {
+          const float pz = nan_of(pen);
+          oav = oaa = obv = oba = mk(pz, pz, pz);
+        } else {
+          QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
+          v3 rap, rav, raa, rbp, rbv, rba;
+          ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
+          ld_rb(E.rb + R.b * RB_STRIDE, rbp, rbv, rba);
+          velocity_contact<F>(R, h, a, b, rap, rav, raa, rbp, rbv, rba, cp, cn, pen, dl, oav, oaa, obv,
+                              oba);
+        }
+        st_mslot(E.cslot + lane * MSLOT_STRIDE, oav, oaa);
+        if (!is_oneway<F>(R.oneway)) st_mslot(E.cslot + (MCAP + lane) * MSLOT_STRIDE, obv, oba);
       }
-      st_mslot(E.cslot + r * MSLOT_STRIDE, oav, oaa);
-      if (!is_oneway<F>(meta[m] & 0xFF)) st_mslot(E.cslot + (meta[m] >> 16) * MSLOT_STRIDE, obv, oba);
+      esync<L>();
+      tasks(ch);
+      esync<L>();
     }
-    esync<L>();
     BX_MSTAMP(7);
-    if (lane < H.T) task_sum(X.te, E.cslot, E.tslot + lane * TSLOT_STRIDE);
-    esync<L>();
     if (X.hasB) {
-      v3 dv, dav;
-      body_combine(X.bt, E.tslot, 1e-6f, dv, dav);
+      v3 dv = mk(0.f, 0.f, 0.f), dav = mk(0.f, 0.f, 0.f);
+      if (nstore > 0) body_combine(X.bt, E.tslot, 1e-6f, dv, dav);
       q.vel = mul(q.vel + dv, X.B.pm);
       q.ang = mul(q.ang + dav, X.B.rm);
       stqp(myqp, q);
@@ -3592,22 +3740,13 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       ica = ica + dav;
       iaa = iaa + dpa_last;
     }
+    // the listed rows leave the index (the next pass's listing writes it
+    // after its barriers)
+    for (int y = lane; y < nstore; y += L) E.sidx[cb_row(y)] = (uint16_t)0xFFFFu;
     esync<L>();
     BX_MSTAMP(8);
   }
-  // Info contact rows of the last position pass (system.py:36-43)
-  if (valid && info_rows) {
-#pragma unroll
-    for (int m = 0; m < MR; m++) {
-      const int x = lane + m * L;
-      if (x >= nact) continue;
-      const int r = BX_MULTI_RX(x);
-      if (io.pos) st3(io.pos + x * 3, cpos[m]);
-      if (io.normal) st3(io.normal + x * 3, cn[m]);
-      if (io.pen) io.pen[x] = pen[m];
-      if (io.cell) io.cell[x] = c.i(H.o_row + r * ROW_STRIDE + R_FLAT);
-    }
-  }
+  // (the Info accumulators alias the contact slots, dead from here)
   if (X.hasB) {
     float* acc = E.acc + lane * ACC_STRIDE;
     st3(acc + ACC_ICV, icv);
@@ -3617,7 +3756,6 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
   esync<L>();
   BX_MSTAMP(10);
 #undef BX_MULTI_RX
-#undef BX_MULTI_SKIP
 #ifdef BX_MSTAMPS
   if (threadIdx.x == 0) {
 #pragma unroll
@@ -4233,26 +4371,28 @@ __device__ __forceinline__ void system_step_body(const StepArgs& A) {
   }
   esync<L>();
   if constexpr (MU) {
-    // M = contact rows per lane
-    HoistM<M> X;
-    load_hoist_multi<L, M, (F & F_JH) != 0>(c, H, lane, X);
+    HoistM X;
+    load_hoist_multi<L, (F & F_JH) != 0>(c, H, lane, X);
     // the broad phase's / NearNeighbors' constants into LDS, read by every pass
     if (H.o_bimg != 0) {
-      const uint4* bg = reinterpret_cast<const uint4*>(c.w + H.o_bimg);
-      for (int r = lane; r < H.R; r += L) E.bimg[r] = bg[r];
+      const uint32_t* bg = c.w + H.o_bimg;
+      for (int k = lane; k < BI_WORDS * H.R; k += L) E.bimg[k] = bg[k];
       const uint4* cg = reinterpret_cast<const uint4*>(c.w + H.o_cen);
       for (int k = lane; k < 2 * H.n_cen + H.n_mat + H.N; k += L) E.cen[k] = cg[k];
-      // lane k's first read (place_centres: E.cen[2k]) is another wave's
-      // write: no pass reads the tables before every wave has staged them
-      esync<L>();
     }
+    // no row has a compact contact index yet (row R: the tasks' padding)
+    for (int r = lane; r <= H.R; r += L) E.sidx[r] = (uint16_t)0xFFFFu;
+    // lane k's first read (place_centres: E.cen[2k]) is another wave's
+    // write: no pass reads the tables before every wave has staged them
+    esync<L>();
     const int64_t ro = valid ? e * H.info_rows : 0;
     RowInfoOut io{A.info.contact_pos ? A.info.contact_pos + ro * 3 : nullptr,
                   A.info.contact_normal ? A.info.contact_normal + ro * 3 : nullptr,
                   A.info.contact_penetration ? A.info.contact_penetration + ro : nullptr,
                   A.info.contact_cell ? A.info.contact_cell + ro : nullptr};
-    pbd_step_multi<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr,
-                            (int)A.act_width, X, io);
+    pbd_step_multi<L, F>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr,
+                         (int)A.act_width, X, io,
+                         A.movf ? A.movf + (valid ? e : 0) * (int64_t)(H.R - MCBUF) * MOVF_W : nullptr);
   } else if constexpr (S) {
     v3 icv, ica, iaa;
     pbd_step_single<L, F, M>(c, H, E, lane, valid, valid ? A.act + e * A.act_stride : nullptr,
@@ -4312,16 +4452,15 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR system_step_kern
   system_step_body<L, MODE, F, M>(A);
 }
 // the MULTI kernel held to 256 registers per lane (VGPRs + AGPRs): two waves
-// per SIMD, so two of its 4-wave workgroups per CU. Past 256 (the row image's
-// b-slot index took it to 256 + 4) one wave per SIMD fits and the CU holds
-// ONE workgroup: Ant Mountain(4) at 2,048 envs ran 1.8x slower
-// (tools/multi_occ.py: the step time grew with the batch from 256 envs on).
-// A/B knob BX_MULTI_WPE=3 / 4: held to 168 / 128 (three / four waves per
-// SIMD: the LDS then admits three workgroups per CU; both spill)
-template <int M, int W, int JH = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W)))
+// per SIMD. Past 256 (round 4: the row image's b-slot index took it to
+// 256 + 4) one wave per SIMD fits and the CU holds half the envs: Ant
+// Mountain(4) at 2,048 envs ran 1.8x slower (tools/multi_occ.py). At L = 128
+// threads per env (two waves) four envs share a CU, when their LDS tail
+// fits 40 KB (the compact contact slots, bx_capi.cpp)
+template <int L, int JH = 0>
+__global__ void __launch_bounds__(L) __attribute__((amdgpu_waves_per_eu(2)))
 system_step_multi_kernel(StepArgs A) {
-  system_step_body<256, MODE_MULTI, F_CC | F_TW | JH, M>(A);
+  system_step_body<L, MODE_MULTI, F_CC | F_TW | JH, 1>(A);
 }
 
 
@@ -5358,41 +5497,14 @@ hipError_t launch_env_step_generic(int L, int mode, int feat, int tpb, int64_t n
   BX_DISPATCH_GENERIC(env_step_kernel, EnvArgs)
   return hipGetLastError();
 }
-hipError_t launch_system_step_multi(int feat, int mr, int64_t n_envs, size_t lds, hipStream_t s,
+hipError_t launch_system_step_multi(int L, int jh, int64_t n_envs, size_t lds, hipStream_t s,
                                     const StepArgs& a) {
-  if ((feat & (F_SPH | F_ANGLE | F_FORCE | F_X)) != 0) return hipErrorInvalidValue;
   dim3 grid((unsigned)n_envs);
-  static const int wpe = getenv("BX_MULTI_WPE") ? atoi(getenv("BX_MULTI_WPE")) : 2;
-  if (wpe == 3 || wpe == 4) {
-    switch (mr * 8 + wpe) {
-      case 1 * 8 + 3: launch_one<StepArgs>(system_step_multi_kernel<1, 3>, grid, 256, lds, s, a); break;
-      case 2 * 8 + 3: launch_one<StepArgs>(system_step_multi_kernel<2, 3>, grid, 256, lds, s, a); break;
-      case 3 * 8 + 3: launch_one<StepArgs>(system_step_multi_kernel<3, 3>, grid, 256, lds, s, a); break;
-      case 4 * 8 + 3: launch_one<StepArgs>(system_step_multi_kernel<4, 3>, grid, 256, lds, s, a); break;
-      case 1 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<1, 4>, grid, 256, lds, s, a); break;
-      case 2 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<2, 4>, grid, 256, lds, s, a); break;
-      case 3 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<3, 4>, grid, 256, lds, s, a); break;
-      case 4 * 8 + 4: launch_one<StepArgs>(system_step_multi_kernel<4, 4>, grid, 256, lds, s, a); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
-  if ((feat & F_JH) != 0) {
-    // the joint halves (H.mjh: revolute joints, torque actuators of the same index)
-    switch (mr) {
-      case 1: launch_one<StepArgs>(system_step_multi_kernel<1, 2, F_JH>, grid, 256, lds, s, a); break;
-      case 2: launch_one<StepArgs>(system_step_multi_kernel<2, 2, F_JH>, grid, 256, lds, s, a); break;
-      case 3: launch_one<StepArgs>(system_step_multi_kernel<3, 2, F_JH>, grid, 256, lds, s, a); break;
-      case 4: launch_one<StepArgs>(system_step_multi_kernel<4, 2, F_JH>, grid, 256, lds, s, a); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
-  switch (mr) {
-    case 1: launch_one<StepArgs>(system_step_multi_kernel<1, 2>, grid, 256, lds, s, a); break;
-    case 2: launch_one<StepArgs>(system_step_multi_kernel<2, 2>, grid, 256, lds, s, a); break;
-    case 3: launch_one<StepArgs>(system_step_multi_kernel<3, 2>, grid, 256, lds, s, a); break;
-    case 4: launch_one<StepArgs>(system_step_multi_kernel<4, 2>, grid, 256, lds, s, a); break;
+  switch (L * 2 + (jh ? 1 : 0)) {
+    case 128 * 2: launch_one<StepArgs>(system_step_multi_kernel<128>, grid, 128, lds, s, a); break;
+    case 128 * 2 + 1: launch_one<StepArgs>(system_step_multi_kernel<128, F_JH>, grid, 128, lds, s, a); break;
+    case 256 * 2: launch_one<StepArgs>(system_step_multi_kernel<256>, grid, 256, lds, s, a); break;
+    case 256 * 2 + 1: launch_one<StepArgs>(system_step_multi_kernel<256, F_JH>, grid, 256, lds, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -14,6 +14,9 @@ struct StepArgs {
   const float* act;
   int64_t act_stride, act_width;
   bx_info info;
+  // MULTI: the contacts of a pass's penetrating rows past MCBUF (env e's at
+  // movf + e * (R - MCBUF) * MOVF_W; null when R <= MCBUF)
+  float* movf;
 };
 struct EnvArgs {
   const uint32_t* blob;
@@ -82,8 +85,9 @@ hipError_t launch_system_step_single(int L, int feat, int gw, int tpb, int64_t n
                                      hipStream_t s, const StepArgs& a);
 hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_envs, size_t lds,
                                   hipStream_t s, const EnvArgs& a, int fold);
-// MULTI-mode step kernel (large pbd scenes, 256 threads per env; mr = rows per lane)
-hipError_t launch_system_step_multi(int feat, int mr, int64_t n_envs, size_t lds, hipStream_t s,
+// MULTI-mode step kernel (large pbd scenes, L = 128 or 256 threads per env;
+// jh: the joint halves)
+hipError_t launch_system_step_multi(int L, int jh, int64_t n_envs, size_t lds, hipStream_t s,
                                     const StepArgs& a);
 // item-loop step kernels (generic translation unit)
 hipError_t launch_system_step_generic(int L, int mode, int feat, int tpb, int64_t n_envs, size_t lds,

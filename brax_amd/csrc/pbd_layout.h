@@ -110,6 +110,10 @@ struct BlobHdr {
   int32_t l_bimg, l_cen;             // LDS (MULTI broad phase): the rows' bounds, the centres
   int32_t o_mjh;                     // MULTI joint halves: the image (MJ_*) of lane l's joint side, 0 = none
   int32_t n_mat;                     // MULTI row tables: materials (after the collidables, o_cen / l_cen)
+  int32_t l_sidx;                    // LDS (MULTI): per row its compact contact index this pass (u16, R + 1)
+  int32_t l_cbuf;                    // LDS (MULTI): the penetrating rows' contacts (MCBUF x MCB_W), then their rows (u16)
+  int32_t l_cnt;                     // LDS (MULTI): per-wave ballot counts (2 x 16 ints)
+  int32_t multi_L;                   // MULTI: threads per env (128: four envs per CU; 256)
 };
 
 // SINGLE-mode lane image: for each of 64 lanes, every constant the
@@ -178,20 +182,30 @@ enum {
 // change, 3) and the angular part (3: the position pass's angular impulse
 // before the body's one quaternion product, the velocity pass's angular
 // velocity change); the count is the linear part's any-nonzero, formed where
-// the task sums. Slot r is row r's a side; a two-way row's b side is slot R +
-// its two-way rank (LR_MBSLOT / BI_BSLOT), then one zero slot (m_zero). Task
+// the task sums (slots: the compact layout below; m_zero = 2 MCAP). Task
 // partials: 8 words (the two sums, the count).
-enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 6, TSLOT_STRIDE = 8, MULTI_MR = 4 };
-// MULTI-mode broad phase: per row one 16-byte group at o_bimg + 4 r (staged
+enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 6, TSLOT_STRIDE = 8 };
+// MULTI compact contacts (round 6). Only a penetrating row (pen > 0, or NaN)
+// has a nonzero impulse (`c < 0` / `penetration > 0` masks,
+// colliders.py:306-377, 584-658), so only those get contact slots: each
+// pass lists them in (m, wave, lane) order (compact index y), keeps their
+// contacts (cpos 3, normal 3, penetration, dlambda) in LDS (y < MCBUF) or in
+// the env's slice of a global overflow buffer (MOVF_W words each), and
+// writes y into the row's index word (l_sidx; 0xFFFF: no slot). The impulse
+// passes run in chunks of MCAP rows: row y's a side in slot y - chunk, its b
+// side in slot MCAP + y - chunk, the zero slot at 2 MCAP. A task entry is a
+// row and side (row | side << 15; padding: row R, whose index stays 0xFFFF),
+// resolved through l_sidx; its partial accumulates over the chunks.
+enum { MCAP = 64, MCBUF = 128, MCB_W = 8, MOVF_W = 12 };
+// MULTI-mode broad phase: per row three words at o_bimg + 3 r (staged
 // in LDS at l_bimg once per launch): (centre a | centre b << 16, reach,
-// flags, b slot). A capsule-capsule row whose capsule centres lie farther
+// flags). A capsule-capsule row whose capsule centres lie farther
 // apart than reach (half segments + radii, rounded up) cannot penetrate, and
 // its position / velocity updates are exact zeros. The centres are the
 // distinct (body, offset) pairs of the rows' capsules, 16 bytes each at
 // o_cen + 4 k: (body, offset xyz), staged at l_cen; each broad-phase pass
 // places them in the world once (l_cen + 4 n_cen + 4 k) for every row that
-// names them. BI_BSLOT: the row's b-side slot (two-way rows; one-way rows:
-// the zero slot).
+// names them.
 // BI_FLAGS: bit 0 may_skip (capsule-capsule), bit 1 the row's group is
 // culled (NearNeighbors), bit 2 a masked cell (R_NNMASK), bit 3 one-way,
 // bits 4-7 the contact function, 8-15 the material, 16.. a row of an
@@ -203,7 +217,7 @@ enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 6, TSLOT_STRIDE = 8, MULTI_MR = 4
 // assembles its rows' records from them (row_from_lds), the broad phase and
 // the NearNeighbors keys take the placed centres (culled scenes, which have
 // no broad phase, stage the same tables).
-enum { BI_CEN = 0, BI_REACH = 1, BI_FLAGS = 2, BI_BSLOT = 3, BI_WORDS = 4 };
+enum { BI_CEN = 0, BI_REACH = 1, BI_FLAGS = 2, BI_WORDS = 3 };
 enum { BIF_SKIP = 1, BIF_CULL = 2, BIF_MASK = 4, BIF_OW = 8, BIF_FN_SHIFT = 4, BIF_MAT_SHIFT = 8,
        BIF_INFO_SHIFT = 16 };
 enum { HULL_STRIDE = 114, HULL_V = 0, HULL_F = 24, HULL_N = 96 };

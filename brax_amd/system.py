@@ -164,8 +164,9 @@ class System:
     threads per env, 'lds_bytes': the System.step kernel's LDS per workgroup,
     'envs_per_cu_by_lds': what 160 KB of LDS holds, 'envs_per_cu_by_registers':
     what the register file holds (MULTI: the kernel is built for two waves per
-    SIMD, 256 registers, so two 4-wave workgroups; None where not fixed by the
-    build), 'envs_per_cu': the smaller of the two, i.e. what runs}."""
+    SIMD, 256 registers, so eight waves per CU: four 128-thread envs or two
+    256-thread ones; None where not fixed by the build), 'envs_per_cu': the
+    smaller of the two, i.e. what runs}."""
     vc, desc, meta = compiler.compile_system(config)
     rdesc = compiler.compile_reset(vc, meta['body_index'])
     cd, keep = abi.make_desc(desc)
@@ -177,8 +178,9 @@ class System:
     per_wg = lds.value
     envs_per_wg = max(64 // lanes.value, 1)
     by_lds = (160 * 1024 // per_wg) * envs_per_wg if per_wg else None
-    # system_step_multi_kernel<M, 2>: amdgpu_waves_per_eu(2) (pbd_kernels.hip)
-    by_regs = 2 if mode.value == 3 else None
+    # system_step_multi_kernel<L>: amdgpu_waves_per_eu(2) (pbd_kernels.hip):
+    # 256 registers, two waves per SIMD, eight per CU, L / 64 per env
+    by_regs = 8 // (lanes.value // 64) if mode.value == 3 else None
     runs = min(x for x in (by_lds, by_regs) if x is not None) if (by_lds or by_regs) else None
     return {'mode': mode.value, 'lanes': lanes.value, 'lds_bytes': per_wg,
             'envs_per_cu_by_lds': by_lds, 'envs_per_cu_by_registers': by_regs,

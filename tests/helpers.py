@@ -183,6 +183,21 @@ def compiled(name):
   return vc, d, rd, meta
 
 
+def set_variant(sys_, variant):
+  """Put a System on one large-scene kernel: 'multi' (the MULTI kernel at its
+  own width: 128 threads per env where the scene fits, else 256), 'multi256'
+  (the MULTI kernel at 256 threads per env), 'itemloop' / 'items' (the item
+  loops at 256 threads per env). Returns bx_system_set_variant's status."""
+  from brax_amd import _native
+  lib = _native.lib()
+  if variant == 'multi':
+    rc = lib.bx_system_set_variant(sys_._h, 128, 3)
+    return rc if rc == 0 else lib.bx_system_set_variant(sys_._h, 256, 3)
+  if variant == 'multi256':
+    return lib.bx_system_set_variant(sys_._h, 256, 3)
+  return lib.bx_system_set_variant(sys_._h, 256, 0)
+
+
 def normwise(a, b):
   """Per-env normwise error max|a-b| / max(1, max|b|) over trailing axes."""
   a = np.asarray(a, np.float64)

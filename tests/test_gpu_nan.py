@@ -152,7 +152,8 @@ def _mountain(dev, variant, cutoff=0):
   cfg = config_for('mountain4')
   cfg.collider_cutoff = cutoff
   s = brax_amd.System(cfg, device=dev)
-  _native.check(_native.lib().bx_system_set_variant(s._h, 256, 3 if variant == 'multi' else 0))
+  from tests.helpers import set_variant
+  _native.check(set_variant(s, variant))
   return s
 
 
@@ -170,7 +171,7 @@ def _sys_steps(s, qp, acts, dev, info=True):
   return outs
 
 
-@pytest.mark.parametrize('variant', ['multi', 'items'])
+@pytest.mark.parametrize('variant', ['multi', 'multi256', 'items'])
 @pytest.mark.parametrize('info', [True, False], ids=['info', 'noinfo'])
 def test_mountain4_nan_vs_reference(dev, variant, info):
   """Ant Mountain(4) all pairs on the MULTI kernel and the item loops, with and
@@ -190,7 +191,7 @@ def test_mountain4_nan_vs_reference(dev, variant, info):
       assert np.array_equal(v[0], clean[t][k][0]), f'step {t + 1} {k}: the clean env moved'
 
 
-@pytest.mark.parametrize('variant', ['multi', 'items'])
+@pytest.mark.parametrize('variant', ['multi', 'multi256', 'items'])
 def test_mountain4nn_nan_isolation(dev, variant):
   """The culled scene (NearNeighbors cutoff 36, BASELINE configs[4]): the
   reference's top_k over NaN distances is not pinned here (its order for NaN

@@ -557,7 +557,8 @@ def nn_cells_check(cells, ref_sel, sim, tol_rel=1e-5):
 
 @pytest.mark.parametrize('name,variant', [('mountain1nn', None), ('mountain1nn', 'itemloop'),
                                           ('mountain1nn', 'multi'), ('mountain4nn', None),
-                                          ('mountain4nn', 'multi'), ('mountain4nn', 'itemloop'),
+                                          ('mountain4nn', 'multi'), ('mountain4nn', 'multi256'),
+                                          ('mountain4nn', 'itemloop'),
                                           ('capsule_cull_s', None),
                                           ('twin_cull', None), ('twin_cull', 'multi')])
 def test_near_neighbors_cells_vs_reference(dev, name, variant):
@@ -566,11 +567,10 @@ def test_near_neighbors_cells_vs_reference(dev, name, variant):
   Info rows in top_k order) against the reference's own top_k indices
   recorded per step and env by oracle/gen_golden.py (`nn_cell`, `nn_sim`),
   on the kernel variants that cull (item loops, MULTI)."""
-  from brax_amd import _native
+  from tests.helpers import set_variant
   sys_ = _system(name, dev)
   if variant is not None:
-    lanes = 256 if variant == 'multi' else sys_.lanes
-    rc = _native.lib().bx_system_set_variant(sys_._h, lanes, 3 if variant == 'multi' else 0)
+    rc = set_variant(sys_, variant)
     if rc != 0:
       pytest.skip(f'{name} does not fit the {variant} kernel')
   T = golden('traj_' + name)

@@ -120,15 +120,16 @@ def test_ant_32768_shards_reproduce_one_batch(dev, oracle_lib):
           _env_err([o[0][keep][..., sl] for o in outs], ref[keep][..., sl]), f)
 
 
-@pytest.mark.parametrize('variant', ['multi', 'itemloop'])
+@pytest.mark.parametrize('variant', ['multi', 'multi256', 'itemloop'])
 @pytest.mark.parametrize('cutoff', [0, 36, 300])
 def test_mountain4_full_batch(dev, oracle_lib, cutoff, variant):
   """BASELINE configs[4]: Ant Mountain(4) System.step at 2,048 envs
   (37 bodies, 630 capsule-capsule + 72 capsule-plane rows; NearNeighbors
   cutoff 36 as published): determinism, batch independence, unit
   quaternions and parity with the fp64 oracle on sampled envs. Both large-
-  scene kernels: MULTI (the default: 256 threads per env, gather tasks) and
-  the item loops at 256 threads per env. Cutoff 300 keeps more cells than
+  scene kernels: MULTI (the default: 128 threads per env, four envs per CU,
+  gather tasks; and the same at 256 threads per env) and the item loops at
+  256 threads per env. Cutoff 300 keeps more cells than
   one wave's 256 candidate keys: the NearNeighbors lists past a wave's
   sorted keys are empty (the bitonic lists' padding)."""
   import brax_amd
@@ -137,8 +138,9 @@ def test_mountain4_full_batch(dev, oracle_lib, cutoff, variant):
   cfg = config_for('mountain4')
   cfg.collider_cutoff = cutoff
   sys_ = brax_amd.System(cfg, device=dev)
-  assert sys_.lanes == 256
-  _native.check(_native.lib().bx_system_set_variant(sys_._h, 256, 3 if variant == 'multi' else 0))
+  assert sys_.lanes == 128  # the MULTI kernel's default width here: four envs per CU
+  from tests.helpers import set_variant
+  _native.check(set_variant(sys_, variant))
   B = 2048
   q0 = sys_.default_qp()
   qp = brax_amd.QP(*(t.unsqueeze(0).expand((B,) + t.shape).contiguous()
@@ -201,8 +203,9 @@ def test_mountain4_multi_vs_item_loops(dev, oracle_lib, cutoff):
     qp, _ = sys_.step(qp, _actions(B, A, t, 3, dev))
   act = _actions(B, A, 2, 3, dev)
   out = {}
-  for variant, mode in (('multi', 3), ('items', 0)):
-    _native.check(_native.lib().bx_system_set_variant(sys_._h, 256, mode))
+  from tests.helpers import set_variant
+  for variant in ('multi', 'items'):
+    _native.check(set_variant(sys_, variant))
     out[variant] = sys_.step(qp, act, info=False)[0].numpy()
   from brax_amd.compiler import compile_reset
   vc, d, meta = brax_amd.compiler.compile_system(cfg)

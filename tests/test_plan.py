@@ -18,23 +18,22 @@ def test_env_systems_run_the_register_hoisted_kernel(name):
 
 
 @pytest.mark.parametrize('cutoff', [0, 36])
-def test_ant_mountain4_runs_two_envs_per_cu(cutoff):
-  """BASELINE configs[4]: Ant Mountain(4) runs the large-scene kernel (one env
-  per 256-thread workgroup) with 6-word contact slots and b slots for the
-  630 two-way rows only. The kernel is built for two waves per SIMD (256
-  registers: a third workgroup's registers spill), so two envs run per CU:
-  the register file sets the residency. With all pairs (cutoff 0) the broad
-  phase's row bounds and capsule centres sit in LDS too (round 5: 16 bytes per
-  row, staged once per launch), which the second workgroup's share still
-  holds; the culled scene (cutoff 36) stages the same image for its
-  NearNeighbors keys (two by either count too)."""
+def test_ant_mountain4_runs_four_envs_per_cu(cutoff):
+  """BASELINE configs[4]: Ant Mountain(4) runs the large-scene kernel at 128
+  threads per env (two waves). The kernel is built for two waves per SIMD
+  (256 registers), so the register file holds four such envs per CU, and
+  since round 6 the LDS does too: only the penetrating rows get contact
+  slots (64 per chunk) and a contact record (128 in LDS), the rows' bounds
+  are 12 bytes, and the Info accumulators, the NearNeighbors ranks / lists
+  and the near-row list share words that are dead while they live, so an
+  env's tail fits 40 KB with all pairs (cutoff 0) and culled (cutoff 36)."""
   cfg = config_for('mountain4')
   cfg.collider_cutoff = cutoff
   p = System.plan(cfg)
-  assert p['mode'] == 3 and p['lanes'] == 256, p
-  assert p['lds_bytes'] * 2 <= LDS_CU, p
-  assert p['envs_per_cu_by_lds'] == 2, p
-  assert p['envs_per_cu_by_registers'] == 2 and p['envs_per_cu'] == 2, p
+  assert p['mode'] == 3 and p['lanes'] == 128, p
+  assert p['lds_bytes'] * 4 <= LDS_CU, p
+  assert p['envs_per_cu_by_lds'] == 4, p
+  assert p['envs_per_cu_by_registers'] == 4 and p['envs_per_cu'] == 4, p
 
 
 def test_plan_refuses_a_null_descriptor():

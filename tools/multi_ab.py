@@ -17,11 +17,15 @@ from brax_amd.envs.mountain import ant_mountain_config  # noqa: E402
 def main():
   dev = torch.device('cuda', 0)
   B, n = 2048, 30
-  out = {'lib': os.environ.get('BRAX_AMD_LIB', 'brax_amd/_lib')}
+  out = {'lib': os.environ.get('BRAX_AMD_LIB', 'brax_amd/_lib'),
+         'lanes': os.environ.get('BX_MULTI_LANES', 'default')}
   for cutoff in (0, 36):
     cfg = ant_mountain_config(4)
     cfg.collider_cutoff = cutoff
     sys_ = brax_amd.System(cfg, device=dev)
+    if os.environ.get('BX_MULTI_LANES'):
+      from brax_amd import _native
+      _native.check(_native.lib().bx_system_set_variant(sys_._h, int(os.environ['BX_MULTI_LANES']), 3))
     qp0 = sys_.default_qp()
     qp = brax_amd.QP(*(t.unsqueeze(0).expand((B,) + t.shape).contiguous()
                        for t in (qp0.pos, qp0.rot, qp0.vel, qp0.ang)))

@@ -2,7 +2,7 @@
 cutoff 0 and 36, Info on) on the library / knobs of this process, saved for a
 bitwise comparison between MULTI-kernel variants.
 
-  BRAX_AMD_LIB=<lib> [BX_MULTI_L=128] python tools/multi_bitcmp.py save <out.npz>
+  BRAX_AMD_LIB=<lib> [BX_MULTI_LANES=128|256] python tools/multi_bitcmp.py save <out.npz>
   python tools/multi_bitcmp.py cmp <a.npz> <b.npz>
 """
 import os
@@ -24,6 +24,9 @@ def save(path):
     cfg = ant_mountain_config(4)
     cfg.collider_cutoff = cut
     s = brax_amd.System(cfg, device=dev)
+    if os.environ.get('BX_MULTI_LANES'):
+      from brax_amd import _native
+      _native.check(_native.lib().bx_system_set_variant(s._h, int(os.environ['BX_MULTI_LANES']), 3))
     qp0 = s.default_qp()
     qp = brax_amd.QP(*(t.unsqueeze(0).expand((B,) + t.shape).contiguous()
                        for t in (qp0.pos, qp0.rot, qp0.vel, qp0.ang)))
@@ -36,6 +39,14 @@ def save(path):
     for f in ('pos', 'rot', 'vel', 'ang'):
       out[f'c{cut}_{f}'] = getattr(qp, f).cpu().numpy()
     out[f'c{cut}_pen'] = info.contact_penetration.cpu().numpy()
+    # Info off: the broad phase on the last pass too
+    q2 = qp
+    for _ in range(3):
+      a = torch.rand((B, s.action_size), device=dev, generator=g) * 2 - 1
+      q2, _ = s.step(q2, a, info=False)
+    torch.cuda.synchronize()
+    for f in ('pos', 'vel'):
+      out[f'c{cut}_noinfo_{f}'] = getattr(q2, f).cpu().numpy()
   np.savez(path, **out)
 
 
