@@ -601,7 +601,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // serial picks' distances
   H.l_tslot = carve(std::max({(H.T + 1) * TSLOT_STRIDE, (R + 1) / 2, H.nnl_words, H.n_nn ? R : 0}));
   H.l_near = H.l_tslot;
-  H.l_cnt = carve(32);
+  H.l_cnt = carve(48);
   H.l_nearc = H.l_cnt;
   // the rows' compact contact indices (16-bit, R + 1: the padding row R)
   H.l_sidx = carve((R + 2) / 2);
@@ -643,7 +643,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     for (int b = 0; b < N; b++) mxja = std::max({mxja, jl[b].size(), al[b].size()});
     // (and its LDS tail within one workgroup's 160 KB)
     H.multi = (!H.single && L > 64 && !H.spring && !xcol && N <= 256 && J <= 256 && K <= 256 &&
-               H.T <= 2 * 256 && G < 64 && R < 0x7FFF && mxja <= 8 && max_btask <= BTASK_W && mtab_ok &&
+               H.T <= 2 * 256 && G < 64 && R <= 8 * 256 && mxja <= 8 && max_btask <= BTASK_W && mtab_ok &&
                (size_t)H.env_words_m * 4 <= 160 * 1024) ? 1 : 0;
     H.act_same = 1;
     for (int a = 0; a < K; a++)
@@ -708,7 +708,11 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
         eb += d->row_b_end[3 * x + k] * d->row_b_end[3 * x + k];
       }
       reach += std::sqrt(ea) + std::sqrt(eb);
-      const float rf = std::nextafter((float)reach, 3.0e38f);
+      // the broad phase compares squared centre distances with (reach +
+      // 1e-4)^2, rounded up (the margin far above the fp32 error of the
+      // centres; a row it keeps that cannot touch only costs its test)
+      const double r2 = (reach + 1e-4) * (reach + 1e-4);
+      const float rf = std::nextafter((float)r2, 3.0e38f);
       uint32_t* bw = &bimg[BI_WORDS * x];
       const bool skip = d->col_fn[g] == BX_COL_CAPSULE_CAPSULE;
       const bool cull = d->col_cutoff[g] != 0;
@@ -839,7 +843,8 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
   // MULTI threads per env: 128 when the bodies, joints (joint halves: two
   // lanes each), actuators and gather tasks (two per lane) fit, so four envs
   // share a CU (two waves each, 256 registers, <= 40 KB of LDS); else 256
-  H.multi_L = (N <= 128 && K <= 128 && (mjh ? 2 * J <= 128 : J <= 128) && H.T <= 2 * 128) ? 128 : 256;
+  H.multi_L = (N <= 128 && K <= 128 && (mjh ? 2 * J <= 128 : J <= 128) && H.T <= 2 * 128 &&
+               R <= 8 * 128) ? 128 : 256;
   if (mjh) {
     B.alloc((4 - (int)B.w.size() % 4) % 4);  // 16-byte aligned groups
     H.o_mjh = B.alloc(MJ_W * MJ_LANES);

@@ -1681,6 +1681,15 @@ __device__ __forceinline__ float centre_dist(const Env& E, const BlobHdr& H, uns
   return norm(cb - ca);
 }
 
+// the same squared (the broad phase compares it with its squared reach)
+__device__ __forceinline__ float centre_dist2(const Env& E, const BlobHdr& H, unsigned pair) {
+  const uint4* cw = E.bod + H.N;
+  const uint4 a4 = cw[pair & 0xFFFFu], b4 = cw[pair >> 16];
+  const v3 d = mk(__uint_as_float(b4.x), __uint_as_float(b4.y), __uint_as_float(b4.z)) -
+               mk(__uint_as_float(a4.x), __uint_as_float(a4.y), __uint_as_float(a4.z));
+  return dot(d, d);
+}
+
 // MULTI: contact row r's record from the LDS tables (its flags / b slot, its
 // two collidables, their bodies' masses and inverse inertias, its
 // material): the words the row image held, with no L2 read
@@ -3538,20 +3547,24 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       // the capsule centres in the world, once for every row naming them
       place_centres<L>(H, E, lane);
       esync<L>();
-      // the lane's rows r = lane + m L: near bits, per (m, wave) counts
+      // the lane's rows r = lane + m L (m < 8: the host keeps R <= 8 L):
+      // near bits, per (m, wave) counts; unrolled, so every row's loads issue
+      // together
       unsigned nmask = 0u;
       const int nm = (H.R + L - 1) / L;
-      for (int m = 0; m < nm; m++) {
+#pragma unroll
+      for (int m = 0; m < 8; m++) {
+        if (m >= nm) break;
         const int r = lane + m * L;
         bool near = false;
         if (r < H.R) {
           const uint32_t* g0 = E.bimg + r * BI_WORDS;
           near = (g0[BI_FLAGS] & BIF_SKIP) == 0u;
           if (!near) {
-            // + 1e-4: far above the fp32 error of the centres; a NaN
+            // squared distance against (reach + 1e-4)^2 (bx_capi.cpp); a NaN
             // distance is near (a NaN row's impulses are NaN)
-            const float cd = centre_dist(E, H, g0[BI_CEN]);
-            near = !(cd > __uint_as_float(g0[BI_REACH]) + 1e-4f) || is_nan(cd);
+            const float cd2 = centre_dist2(E, H, g0[BI_CEN]);
+            near = !(cd2 > __uint_as_float(g0[BI_REACH])) || is_nan(cd2);
           }
         }
         nmask |= near ? (1u << m) : 0u;
@@ -3560,7 +3573,9 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       }
       esync<L>();
       int total = 0;
-      for (int m = 0; m < nm; m++) {
+#pragma unroll
+      for (int m = 0; m < 8; m++) {
+        if (m >= nm) break;
         const bool near = (nmask >> m) & 1u;
         const unsigned long long bal = __ballot(near);
         const int rk = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
@@ -3617,7 +3632,7 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
                                                __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
       // (two count buffers: a wave may write the next iteration's counts
       // while another still reads these)
-      int* cnt = E.nearc + 16 + par * NWV;
+      int* cnt = E.nearc + 32 + par * NWV;
       if ((lane & 63) == 0) cnt[wv] = __popcll(bal);
       esync<L>();
       int before = 0, tot = 0;
@@ -3643,6 +3658,9 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
       nstore += tot;
     }
     esync<L>();
+#ifdef BX_MSTAMPS
+    if (H.n_nn == 0) ms_acc[14] += (unsigned long long)nstore;
+#endif
     BX_MSTAMP(4);
     // the position impulses of the listed rows, MCAP at a time: row y's sides
     // into the chunk's slots, then the tasks add the chunk

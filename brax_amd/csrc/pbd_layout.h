@@ -112,7 +112,7 @@ struct BlobHdr {
   int32_t n_mat;                     // MULTI row tables: materials (after the collidables, o_cen / l_cen)
   int32_t l_sidx;                    // LDS (MULTI): per row its compact contact index this pass (u16, R + 1)
   int32_t l_cbuf;                    // LDS (MULTI): the penetrating rows' contacts (MCBUF x MCB_W), then their rows (u16)
-  int32_t l_cnt;                     // LDS (MULTI): per-wave ballot counts (2 x 16 ints)
+  int32_t l_cnt;                     // LDS (MULTI): per-wave ballot counts (broad phase 32, listing 2 x 8)
   int32_t multi_L;                   // MULTI: threads per env (128: four envs per CU; 256)
 };
 
@@ -198,8 +198,8 @@ enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 6, TSLOT_STRIDE = 8 };
 // resolved through l_sidx; its partial accumulates over the chunks.
 enum { MCAP = 64, MCBUF = 128, MCB_W = 8, MOVF_W = 12 };
 // MULTI-mode broad phase: per row three words at o_bimg + 3 r (staged
-// in LDS at l_bimg once per launch): (centre a | centre b << 16, reach,
-// flags). A capsule-capsule row whose capsule centres lie farther
+// in LDS at l_bimg once per launch): (centre a | centre b << 16, (reach +
+// 1e-4)^2 rounded up, flags). A capsule-capsule row whose capsule centres lie farther
 // apart than reach (half segments + radii, rounded up) cannot penetrate, and
 // its position / velocity updates are exact zeros. The centres are the
 // distinct (body, offset) pairs of the rows' capsules, 16 bytes each at

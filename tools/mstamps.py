@@ -33,15 +33,16 @@ torch.cuda.synchronize()
 _native.check(lib.bx_debug_stamps(buf, 2))
 v = np.array(buf[:12], dtype=np.float64)
 n = max(buf[15], 1)
-names = ['act+damp', 'body acc', 'joint', 'body pos(+vproj)', 'contact pos rows', 'task sum (pos)',
-         'body combine pos', 'contact vel rows', 'task sum + body (vel)', 'nn select', 'tail',
-         'broad phase']
+names = ['act+damp', 'body acc', 'joint', 'body pos(+vproj)', 'contacts + listing',
+         'pos impulses + tasks', 'body combine pos', 'vel impulses + tasks', 'body combine vel',
+         'nn select', 'tail', 'broad phase']
 if cut:
   # (culled scenes: slots 12-14 split the NearNeighbors picks)
   print('nn: init loop', buf[14] / n, 'keys + sort', buf[12] / n, 'wave picks', buf[13] / n,
         'merge (rest of nn select)', buf[9] / n)
 else:
-  print('near rows per broad-phase pass', buf[12] / max(buf[13], 1), 'passes/wg-step', buf[13] / n)
+  print('near rows per broad-phase pass', buf[12] / max(buf[13], 1), 'passes/wg-step', buf[13] / n,
+        'listed (penetrating) rows per pass', buf[14] / (n * (sys_.config.substeps // 2)))
 tot = v.sum()
 print('cutoff', cut, 'samples', n, 'cycles/wave0/step', tot / n)
 for i, nm in enumerate(names):
