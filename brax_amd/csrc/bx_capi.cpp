@@ -567,7 +567,7 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
     row_mat[x] = it->second;
   }
   // (past these sizes the scene takes the item-loop kernels: no MULTI tables)
-  const bool mtab_ok = cens.size() <= 0xFFFF && mats.size() <= 0xFF && R <= 0xFFFF;
+  const bool mtab_ok = cens.size() <= 256 && mats.size() <= 0xFF && R <= 0xFFFF;
   H.n_cen = mtab_ok ? (int)cens.size() : 0;
   H.n_mat = mtab_ok ? (int)mats.size() : 0;
   // the MULTI (System.step only) tail starts here, over the env step's regions
@@ -712,22 +712,27 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       // 1e-4)^2, rounded up (the margin far above the fp32 error of the
       // centres; a row it keeps that cannot touch only costs its test)
       const double r2 = (reach + 1e-4) * (reach + 1e-4);
-      const float rf = std::nextafter((float)r2, 3.0e38f);
+      // as a half float rounded up (+inf past 65504: always near)
+      uint16_t hb = 0x7C00u;
+      if (r2 <= 65504.0) {
+        hb = __builtin_bit_cast(uint16_t, (_Float16)r2);
+        if ((double)__builtin_bit_cast(_Float16, hb) < r2) hb++;
+      }
       uint32_t* bw = &bimg[BI_WORDS * x];
       const bool skip = d->col_fn[g] == BX_COL_CAPSULE_CAPSULE;
       const bool cull = d->col_cutoff[g] != 0;
-      bw[BI_CEN] = (uint32_t)row_cen[2 * x] | ((uint32_t)row_cen[2 * x + 1] << 16);
-      std::memcpy(&bw[BI_REACH], &rf, 4);
       uint32_t fl = (skip ? BIF_SKIP : 0u) | (cull ? BIF_CULL : 0u) |
                     (d->row_nn_masked && d->row_nn_masked[x] ? BIF_MASK : 0u) |
                     (d->col_oneway[g] ? BIF_OW : 0u) | ((uint32_t)d->col_fn[g] << BIF_FN_SHIFT) |
                     ((uint32_t)row_mat[x] << BIF_MAT_SHIFT);
+      uint32_t info = 0u;
       if (!cull) {
         // the unculled row's Info index (its group's first Info row + its offset)
         const int og = H.o_group + g * GROUP_STRIDE;
-        fl |= (uint32_t)((int)B.w[og + G_INFO] + x - (int)B.w[og + G_R0]) << BIF_INFO_SHIFT;
+        info = (uint32_t)((int)B.w[og + G_INFO] + x - (int)B.w[og + G_R0]);
       }
-      bw[BI_FLAGS] = fl;
+      bw[BI_W0] = (uint32_t)row_cen[2 * x] | ((uint32_t)row_cen[2 * x + 1] << 8) | (fl << 16);
+      bw[BI_W1] = (uint32_t)hb | (info << 16);
     }
     H.o_bimg = B.alloc(BI_WORDS * R);
     for (int k = 0; k < BI_WORDS * R; k++) B.w[H.o_bimg + k] = bimg[k];

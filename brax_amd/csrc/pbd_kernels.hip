@@ -1690,12 +1690,22 @@ __device__ __forceinline__ float centre_dist2(const Env& E, const BlobHdr& H, un
   return dot(d, d);
 }
 
+// MULTI: a row's bounds words (BI_*): its collidable pair as centre_dist
+// takes it, its flags (BIF_*), its squared reach, its Info index
+__device__ __forceinline__ unsigned bi_pair(uint32_t w0) {
+  return (w0 & 0xFFu) | ((w0 & 0xFF00u) << 8);
+}
+__device__ __forceinline__ uint32_t bi_flags(uint32_t w0) { return w0 >> 16; }
+__device__ __forceinline__ float bi_reach2(uint32_t w1) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)(w1 & 0xFFFFu));
+}
+
 // MULTI: contact row r's record from the LDS tables (its flags / b slot, its
 // two collidables, their bodies' masses and inverse inertias, its
 // material): the words the row image held, with no L2 read
 __device__ __forceinline__ RowC row_from_lds(const Env& E, int r) {
-  const uint32_t* g = E.bimg + r * BI_WORDS;
-  const uint4 g0 = make_uint4(g[BI_CEN], g[BI_REACH], g[BI_FLAGS], 0u);
+  const uint32_t w0 = E.bimg[r * BI_WORDS + BI_W0];
+  const uint4 g0 = make_uint4(bi_pair(w0), 0u, bi_flags(w0), 0u);
   const uint4 a0 = E.cen[2 * (g0.x & 0xFFFFu)], a1 = E.cen[2 * (g0.x & 0xFFFFu) + 1];
   const uint4 b0 = E.cen[2 * (g0.x >> 16)], b1 = E.cen[2 * (g0.x >> 16) + 1];
   const uint4 mt = E.mat[(g0.z >> BIF_MAT_SHIFT) & 0xFFu];
@@ -1754,12 +1764,12 @@ __device__ __forceinline__ void nn_select(const Cst& c, const BlobHdr& H, const 
     // (the MULTI kernel: a culled row gets no compact index, so its slots
     // are never read)
     for (int r = lane; r < H.R; r += L) {
-      const uint32_t fl = E.bimg[r * BI_WORDS + BI_FLAGS];
+      const uint32_t fl = bi_flags(E.bimg[r * BI_WORDS + BI_W0]);
       if (fl & BIF_CULL) {
         E.ract[r] = -1;
       } else {
         E.ract[r] = 0;
-        E.alist[fl >> BIF_INFO_SHIFT] = r;
+        E.alist[E.bimg[r * BI_WORDS + BI_W1] >> 16] = r;
       }
     }
   } else
@@ -1794,9 +1804,9 @@ __device__ __forceinline__ void nn_select(const Cst& c, const BlobHdr& H, const 
         const int r = r0 + lane + i * L;
         if constexpr (MT) {
           if (r < r1) {
-            const uint32_t* g0 = E.bimg + r * BI_WORDS;
-            const unsigned d = (g0[BI_FLAGS] & BIF_MASK) ? 0x7F800000u
-                                                         : __float_as_uint(centre_dist(E, H, g0[BI_CEN]));
+            const uint32_t w0 = E.bimg[r * BI_WORDS + BI_W0];
+            const unsigned d = (bi_flags(w0) & BIF_MASK) ? 0x7F800000u
+                                                         : __float_as_uint(centre_dist(E, H, bi_pair(w0)));
             k[i] = ((unsigned long long)d << 32) | (unsigned)r;
           } else {
             k[i] = ~0ull;
@@ -3558,13 +3568,13 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
         const int r = lane + m * L;
         bool near = false;
         if (r < H.R) {
-          const uint32_t* g0 = E.bimg + r * BI_WORDS;
-          near = (g0[BI_FLAGS] & BIF_SKIP) == 0u;
+          const uint2 g0 = *reinterpret_cast<const uint2*>(E.bimg + r * BI_WORDS);
+          near = (bi_flags(g0.x) & BIF_SKIP) == 0u;
           if (!near) {
             // squared distance against (reach + 1e-4)^2 (bx_capi.cpp); a NaN
             // distance is near (a NaN row's impulses are NaN)
-            const float cd2 = centre_dist2(E, H, g0[BI_CEN]);
-            near = !(cd2 > __uint_as_float(g0[BI_REACH])) || is_nan(cd2);
+            const float cd2 = centre_dist2(E, H, bi_pair(g0.x));
+            near = !(cd2 > bi_reach2(g0.y)) || is_nan(cd2);
           }
         }
         nmask |= near ? (1u << m) : 0u;

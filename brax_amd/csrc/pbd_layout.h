@@ -196,20 +196,21 @@ enum { TASK_W = 8, BTASK_W = 8, MSLOT_STRIDE = 6, TSLOT_STRIDE = 8 };
 // side in slot MCAP + y - chunk, the zero slot at 2 MCAP. A task entry is a
 // row and side (row | side << 15; padding: row R, whose index stays 0xFFFF),
 // resolved through l_sidx; its partial accumulates over the chunks.
-enum { MCAP = 64, MCBUF = 128, MCB_W = 8, MOVF_W = 12 };
-// MULTI-mode broad phase: per row three words at o_bimg + 3 r (staged
-// in LDS at l_bimg once per launch): (centre a | centre b << 16, (reach +
-// 1e-4)^2 rounded up, flags). A capsule-capsule row whose capsule centres lie farther
+enum { MCAP = 128, MCBUF = 128, MCB_W = 8, MOVF_W = 12 };
+// MULTI-mode broad phase: per row two words at o_bimg + 2 r (staged in LDS
+// at l_bimg once per launch): BI_W0 = centre a | centre b << 8 | flags << 16
+// (<= 256 collidables), BI_W1 = (reach + 1e-4)^2 as a half float rounded up
+// | Info index << 16. A capsule-capsule row whose capsule centres lie farther
 // apart than reach (half segments + radii, rounded up) cannot penetrate, and
 // its position / velocity updates are exact zeros. The centres are the
 // distinct (body, offset) pairs of the rows' capsules, 16 bytes each at
 // o_cen + 4 k: (body, offset xyz), staged at l_cen; each broad-phase pass
 // places them in the world once (l_cen + 4 n_cen + 4 k) for every row that
 // names them.
-// BI_FLAGS: bit 0 may_skip (capsule-capsule), bit 1 the row's group is
+// The flags: bit 0 may_skip (capsule-capsule), bit 1 the row's group is
 // culled (NearNeighbors), bit 2 a masked cell (R_NNMASK), bit 3 one-way,
-// bits 4-7 the contact function, 8-15 the material, 16.. a row of an
-// unculled group: its Info index. BI_CEN names the row's two collidables.
+// bits 4-7 the contact function, 8-15 the material. The Info index: a row
+// of an unculled group's.
 // The row tables at o_cen (uint4 units, staged at l_cen once per launch):
 // 2 n_cen collidable groups ((body, offset), (end, radius)), n_mat materials
 // (friction, elasticity, scale, velocity threshold), N bodies (mass, inverse
@@ -217,9 +218,8 @@ enum { MCAP = 64, MCBUF = 128, MCB_W = 8, MOVF_W = 12 };
 // assembles its rows' records from them (row_from_lds), the broad phase and
 // the NearNeighbors keys take the placed centres (culled scenes, which have
 // no broad phase, stage the same tables).
-enum { BI_CEN = 0, BI_REACH = 1, BI_FLAGS = 2, BI_WORDS = 3 };
-enum { BIF_SKIP = 1, BIF_CULL = 2, BIF_MASK = 4, BIF_OW = 8, BIF_FN_SHIFT = 4, BIF_MAT_SHIFT = 8,
-       BIF_INFO_SHIFT = 16 };
+enum { BI_W0 = 0, BI_W1 = 1, BI_WORDS = 2 };
+enum { BIF_SKIP = 1, BIF_CULL = 2, BIF_MASK = 4, BIF_OW = 8, BIF_FN_SHIFT = 4, BIF_MAT_SHIFT = 8 };
 enum { HULL_STRIDE = 114, HULL_V = 0, HULL_F = 24, HULL_N = 96 };
 
 }  // namespace bx

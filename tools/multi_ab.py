@@ -18,6 +18,7 @@ def main():
   dev = torch.device('cuda', 0)
   B, n = 2048, 30
   out = {'lib': os.environ.get('BRAX_AMD_LIB', 'brax_amd/_lib'),
+         'warm_steps': int(os.environ.get('BX_MULTI_WARM', '10')),
          'lanes': os.environ.get('BX_MULTI_LANES', 'default')}
   for cutoff in (0, 36):
     cfg = ant_mountain_config(4)
@@ -33,7 +34,7 @@ def main():
     act = torch.rand((B, sys_.action_size), device=dev, generator=g) * 2 - 1
     for info in (True, False):
       q = qp
-      for _ in range(10):
+      for _ in range(int(os.environ.get('BX_MULTI_WARM', '10'))):
         q, _ = sys_.step(q, act, info=info)
       torch.cuda.synchronize()
       a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
