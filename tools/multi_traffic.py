@@ -31,10 +31,24 @@ def main():
   qp = brax_amd.QP(*(t.unsqueeze(0).expand((B,) + t.shape).contiguous()
                      for t in (qp0.pos, qp0.rot, qp0.vel, qp0.ang)))
   act = torch.rand((B, sys_.action_size), device=dev, generator=torch.Generator(dev).manual_seed(0)) * 2 - 1
+  qp_bytes = 0
   for _ in range(30):
-    qp = sys_.step(qp, act, info=info)[0]
+    qp, inf = sys_.step(qp, act, info=info)
   torch.cuda.synchronize()
-  print('mode', 'info' if info else 'noinfo', 'cutoff', cutoff, 'envs', B, 'rows', sys_.num_rows, flush=True)
+  # algorithmic bytes per env-step: the QP in and out (13
+  # floats per body), the action row and, with Info, every Info tensor
+  qp_bytes = 2 * 13 * 4 * sys_.num_bodies + 4 * sys_.action_size
+  info_bytes = 0
+  if info:
+    def leaves(x):
+      if isinstance(x, torch.Tensor):
+        yield x
+      elif x is not None and hasattr(x, '__dataclass_fields__'):
+        for f in x.__dataclass_fields__:
+          yield from leaves(getattr(x, f))
+    info_bytes = sum(t.numel() * t.element_size() for t in leaves(inf)) // B
+  print('mode', 'info' if info else 'noinfo', 'cutoff', cutoff, 'envs', B, 'rows', sys_.num_rows,
+        'algorithmic_bytes_per_env_step', qp_bytes + info_bytes, 'info_bytes', info_bytes, flush=True)
   if len(sys.argv) > 3:
     np.savez(sys.argv[3], **{k: getattr(qp, k).cpu().numpy() for k in ('pos', 'rot', 'vel', 'ang')})
 
