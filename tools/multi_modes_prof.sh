@@ -9,6 +9,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r06}
 OUT=gpurun_out/mmodes_$TAG
+mkdir -p $OUT
 for mode in noinfo info; do
   for cut in 0 36; do
     M=$OUT/${mode}_$cut
