@@ -3550,10 +3550,16 @@ __device__ void pbd_step_multi(const Cst& c, const BlobHdr& H, const Env& E, int
     // reads the rows) the last pass takes it too: its far rows' Info is never
     // written
     const bool last = it + 1 == H.substeps / 2;
+    const int lane0 = lane;
     const bool bph = H.o_bimg != 0 && H.n_nn == 0 && (!last || !info_rows);
     int nwork = nact;
     if (bph) {
       int* cnt = E.nearc;
+      // (the lane index made opaque per pass: its row addresses and masks are
+      // recomputed here instead of hoisted out of the substep loop, where
+      // they had no registers left and went to scratch)
+      int lane = lane0;
+      asm volatile("" : "+v"(lane));
       // the capsule centres in the world, once for every row naming them
       place_centres<L>(H, E, lane);
       esync<L>();
@@ -4376,11 +4382,13 @@ __device__ __forceinline__ void system_step_body(const StepArgs& A) {
   Cst c{A.blob};
   float* ebase = stage_constants<MODE>(A.blob, H, smem, c);
   constexpr bool S = MODE == MODE_SINGLE;
-  const int lane = threadIdx.x % L;
-  const int le = threadIdx.x / L;
-  const int64_t e = (int64_t)blockIdx.x * (blockDim.x / L) + le;
-  const bool valid = e < A.n_envs;
   constexpr bool MU = MODE == MODE_MULTI;
+  // (MULTI: one env per workgroup of L threads, so the env's LDS base is
+  // uniform by construction)
+  const int lane = MU ? (int)threadIdx.x : (int)(threadIdx.x % L);
+  const int le = MU ? 0 : (int)(threadIdx.x / L);
+  const int64_t e = (int64_t)blockIdx.x * (MU ? 1 : (blockDim.x / L)) + le;
+  const bool valid = e < A.n_envs;
   Env E = carve(ebase + le * H.env_words, H, MU);
   zero_slots(E, H, lane);
   // SINGLE: the lane image's loads go out before the state's
