@@ -1335,6 +1335,7 @@ static int env_step_impl(bx_system* S, const bx_env_params* env, int64_t n_envs,
     return fail("episode wrapper needs steps and truncation buffers");
   EnvArgs a{};
   a.blob = S->blob;
+  a.lane_img = S->blob + S->hdr.o_lane;
   a.n_envs = n_envs;
   a.P = *env;
   a.in = *in;

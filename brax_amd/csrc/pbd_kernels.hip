@@ -2484,7 +2484,7 @@ struct Hoist {
 // its side's (parent of joint j on lane j, child on lane j + 8), a copy per
 // side lane
 template <int M, bool JH, bool R2 = false, int MC = M, bool JB = false>
-__device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& H, int lane,
+__device__ __forceinline__ void load_hoist(const uint32_t* img, const BlobHdr& H, int lane,
                                            Hoist<M, MC>& X) {
   static_assert(!JB || (JH && MC <= 8), "JB: joint halves, <= 8 contact entries");
   const int jx = JH ? (lane & 7) : lane;
@@ -2495,7 +2495,9 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
   X.hasR2 = false;
   X.r1 = lane;
   X.r2 = -1;
-  const uint4* im = reinterpret_cast<const uint4*>(blob + H.o_lane) + lane;
+  // (img: the lane image, blob + H.o_lane; the env kernels take it from
+  // their arguments, so these loads need not wait for the header)
+  const uint4* im = reinterpret_cast<const uint4*>(img) + lane;
   uint32_t w[LANE_W];
   auto grab = [&](int o, int n) {
 #pragma unroll
@@ -2613,10 +2615,10 @@ __device__ __forceinline__ void load_hoist(const uint32_t* blob, const BlobHdr& 
 // the spherical SINGLE kernels' limit rows into LDS, once per launch (see
 // ld_lim): 6 independent 16-byte loads per lane from the lane image
 template <int L, int F>
-__device__ __forceinline__ void stage_lim(const uint32_t* blob, const BlobHdr& H, const Env& E,
+__device__ __forceinline__ void stage_lim(const uint32_t* img, const BlobHdr& H, const Env& E,
                                           int lane) {
   if constexpr ((F & F_SPH) != 0) {
-    const uint4* im = reinterpret_cast<const uint4*>(blob + H.o_lane) + lane;
+    const uint4* im = reinterpret_cast<const uint4*>(img) + lane;
     constexpr int G[LIM_SLOTS] = {LI_JLIM / 4, LI_JLIM / 4 + 1, LI_JLIM12 / 4, LI_JLIM12 / 4 + 1,
                                   LI_JLIM12 / 4 + 2, LI_JLIM12 / 4 + 3};
 #pragma unroll
@@ -4394,8 +4396,8 @@ __device__ __forceinline__ void system_step_body(const StepArgs& A) {
   // SINGLE: the lane image's loads go out before the state's
   Hoist<M, cl_width<F, M>()> X;
   if constexpr (S) {
-    load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>()>(A.blob, H, lane, X);
-    stage_lim<L, F>(A.blob, H, E, lane);
+    load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>()>(A.blob + H.o_lane, H, lane, X);
+    stage_lim<L, F>(A.blob + H.o_lane, H, E, lane);
   }
   for (int b = lane; b < H.N; b += L) {
     if (valid) {
@@ -4514,10 +4516,43 @@ system_step_multi_kernel(StepArgs A) {
 // steps, truncation (4, B) | metrics (B, M)), so the step derives every
 // output pointer from that base instead of carrying eleven strided fields
 // across the step loop (uniform registers the kernel otherwise spills)
-template <int L, int MODE, int F, int M, int EK = EK_ANY, bool PK = false>
+// ONE (env_step_packed_kernel, launched for n_steps <= 1 only): one step,
+// its first loads issued from the kernel arguments (EARLY below)
+template <int L, int MODE, int F, int M, int EK = EK_ANY, bool PK = false, bool ONE = false>
 __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   BX_KSTAMP_DECL
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  // the packed SINGLE-mode kernels (Env.step's bx_env_step_packed, the
+  // rollouts) load the lane's state record first, from the kernel arguments
+  // alone (the packed (B, N, 16) layout: in.qp.pos.env_stride = 16 N, no
+  // blob header needed), so its HBM latency runs under the header / lane
+  // image chain instead of after it
+  constexpr bool EARLY = PK && ONE && MODE == MODE_SINGLE;
+  f32x4 eq0 = {0.f, 0.f, 0.f, 0.f}, eq1 = eq0, eq2 = eq0;
+  float eq3 = 0.f;
+  if constexpr (EARLY) {
+    const int64_t es = A.in.qp.pos.env_stride;
+    const int nb = (int)(es >> 4);
+    const int ln = (int)(threadIdx.x % L);
+    const int64_t ee = (int64_t)blockIdx.x * (blockDim.x / L) + threadIdx.x / L;
+    const float* qs = A.in.qp.pos.ptr + (ee < A.n_envs ? ee : 0) * es + (int64_t)(ln < nb ? ln : 0) * 16;
+    eq0 = ld4a(qs);
+    eq1 = ld4a(qs + 4);
+    eq2 = ld4a(qs + 8);
+    eq3 = qs[12];
+  }
+  // and the env's done / steps and the first action chunk (one element per
+  // lane), likewise from the arguments alone
+  float ed = 0.f, est = 0.f, ea0 = 0.f;
+  if constexpr (EARLY) {
+    const int ln = (int)(threadIdx.x % L);
+    const int64_t ee = (int64_t)blockIdx.x * (blockDim.x / L) + threadIdx.x / L;
+    const int64_t eel = ee < A.n_envs ? ee : 0;
+    ed = A.in.done[eel];
+    if (A.in.steps) est = A.in.steps[eel];
+    const int aw0 = (int)A.act_width;
+    if (!A.draw && aw0 > 0 && ln < (L < 64 ? L : 64)) ea0 = A.act[eel * A.act_stride + (ln < aw0 ? ln : aw0 - 1)];
+  }
   BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
   Cst c{A.blob};
   float* ebase = stage_constants<MODE>(A.blob, H, smem, c);
@@ -4526,28 +4561,33 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   const int le = threadIdx.x / L;
   const int64_t e = (int64_t)blockIdx.x * (blockDim.x / L) + le;
   const bool valid = e < A.n_envs;
+  // every load first, with clamped (unconditional) addresses so their
+  // latencies overlap: the lane image (its address from the arguments, so
+  // before the LDS setup that waits for the header), the per-env scalars,
+  // the state and the first chunk of the action row; an invalid env's lanes
+  // read env 0's (never stored)
+  // (ONE: before the LDS setup, which waits for the header; the rollout
+  // kernels keep the order their main loop was tuned with)
+  Hoist<M, cl_width<F, M>()> X;
+  // JB: the env-program kernels with joint halves (pbd_step_single's FOLD && JH)
+  if constexpr (S && ONE)
+    load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>(),
+               (F & F_JH) != 0 && EK != EK_ANY>(A.lane_img, H, lane, X);
   Env E = carve(ebase + le * H.env_words, H);
   zero_slots(E, H, lane);
   BX_PSTAMP(5);
   const bx_env_params& P = A.P;
   const int kind = P.kind;
   const int aw = (int)A.act_width;
-  // every load first, with clamped (unconditional) addresses so their
-  // latencies overlap: the lane image, the per-env scalars, the state and the
-  // first chunk of the action row; an invalid env's lanes read env 0's
-  // (never stored)
   const int64_t el = valid ? e : 0;
-  Hoist<M, cl_width<F, M>()> X;
-  if constexpr (S) {
-    // JB: the env-program kernels with joint halves (pbd_step_single's FOLD && JH)
+  if constexpr (S && !ONE)
     load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>(),
-               (F & F_JH) != 0 && EK != EK_ANY>(A.blob, H, lane, X);
-    stage_lim<L, F>(A.blob, H, E, lane);
-  }
+               (F & F_JH) != 0 && EK != EK_ANY>(A.blob + H.o_lane, H, lane, X);
+  if constexpr (S) stage_lim<L, F>(ONE ? A.lane_img : A.blob + H.o_lane, H, E, lane);
   BX_PSTAMP(6);
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
-  float done_in = A.in.done[el];
-  float steps_in = A.in.steps ? A.in.steps[el] : 0.f;
+  float done_in = EARLY ? ed : A.in.done[el];
+  float steps_in = EARLY ? est : (A.in.steps ? A.in.steps[el] : 0.f);
   if (!valid) done_in = steps_in = 0.f;
   // the target envs' per-env stream (advanced by one per env step)
   uint32_t rng_c = (A.in.rng && valid) ? A.in.rng[e] : 0u;
@@ -4562,12 +4602,22 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   };
   const float* arow_g = drw ? nullptr : A.act + el * A.act_stride;
   float a0 = 0.f;
-  if (aw > 0 && lane < C) a0 = drw ? draw_at(0, lane < aw ? lane : aw - 1) : arow_g[lane < aw ? lane : aw - 1];
+  if (aw > 0 && lane < C) a0 = drw ? draw_at(0, lane < aw ? lane : aw - 1) : (EARLY ? ea0 : arow_g[lane < aw ? lane : aw - 1]);
   BX_PSTAMP(7);
   if constexpr (S) {
     // N <= L: the lane's body
     float qv[13];
-    load_qp_regs(A.in.qp, el, lane < H.N ? lane : 0, qv);
+    if constexpr (EARLY) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        qv[k] = eq0[k];
+        qv[4 + k] = eq1[k];
+        qv[8 + k] = eq2[k];
+      }
+      qv[12] = eq3;
+    } else {
+      load_qp_regs(A.in.qp, el, lane < H.N ? lane : 0, qv);
+    }
     if (lane < H.N) {
       float* s = E.qp + lane * QP_STRIDE;
 #pragma unroll
@@ -4584,7 +4634,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     }
   }
   BX_PSTAMP(8);
-  const int nst = A.n_steps > 1 ? A.n_steps : 1;
+  const int nst = ONE ? 1 : (A.n_steps > 1 ? A.n_steps : 1);
   for (int t = 0; t < nst; t++) {
   // (draw mode: the env programs that read the raw row are refused on the
   // host; physics reads the staged row)
@@ -5030,7 +5080,7 @@ __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_kernel(
 // through the PK body, under its own name (the benchmarked envs' kernels)
 template <int L, int MODE, int F, int M, int EK = EK_ANY>
 __global__ void __launch_bounds__(L > 64 ? L : 64) BX_STEP_ATTR env_step_packed_kernel(EnvArgs A) {
-  env_step_body<L, MODE, F, M, EK, true>(A);
+  env_step_body<L, MODE, F, M, EK, true, true>(A);
 }
 // the Ant step kernel held to 256 registers (2 waves per SIMD) for batches
 // past one wave per SIMD: at 4,096 envs the unbounded kernel's single wave

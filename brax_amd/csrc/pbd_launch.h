@@ -39,6 +39,10 @@ struct EnvArgs {
   uint64_t draw_seed, draw_offset, draw_step;
   float draw_lo, draw_hi;
   float* act_out;
+  // SINGLE mode: blob + o_lane (the lane image), so the one-step kernels
+  // issue its loads before the header arrives (last: the other kernels'
+  // argument offsets stay as they were)
+  const uint32_t* lane_img;
 };
 struct InfoArgs {
   const uint32_t* blob;
