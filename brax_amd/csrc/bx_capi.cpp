@@ -1336,6 +1336,7 @@ static int env_step_impl(bx_system* S, const bx_env_params* env, int64_t n_envs,
   EnvArgs a{};
   a.blob = S->blob;
   a.lane_img = S->blob + S->hdr.o_lane;
+  a.hdr = S->hdr;
   a.n_envs = n_envs;
   a.P = *env;
   a.in = *in;

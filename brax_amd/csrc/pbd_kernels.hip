@@ -4553,7 +4553,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     const int aw0 = (int)A.act_width;
     if (!A.draw && aw0 > 0 && ln < (L < 64 ? L : 64)) ea0 = A.act[eel * A.act_stride + (ln < aw0 ? ln : aw0 - 1)];
   }
-  BlobHdr H = *reinterpret_cast<const BlobHdr*>(A.blob);
+  BlobHdr H = ONE ? A.hdr : *reinterpret_cast<const BlobHdr*>(A.blob);
   Cst c{A.blob};
   float* ebase = stage_constants<MODE>(A.blob, H, smem, c);
   constexpr bool S = MODE == MODE_SINGLE;

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../include/brax_amd.h"
+#include "pbd_layout.h"
 
 namespace bx {
 
@@ -43,6 +44,10 @@ struct EnvArgs {
   // issue its loads before the header arrives (last: the other kernels'
   // argument offsets stay as they were)
   const uint32_t* lane_img;
+  // the blob's header, for the one-step kernels: read from the arguments,
+  // which the kernel holds at its start, instead of one more dependent load
+  // from the blob
+  BlobHdr hdr;
 };
 struct InfoArgs {
   const uint32_t* blob;
