@@ -768,8 +768,14 @@ int build_blob(const bx_desc* d, const bx_reset_desc* r, bx_system* S) {
       for (int x : pl) r2g &= d->col_oneway[d->row_group[x]] != 0;
       for (int x : other)
         r2g &= d->col_fn[d->row_group[x]] == BX_COL_CAPSULE_CAPSULE && !d->col_oneway[d->row_group[x]];
+      // F_R2G's two-way slot runs as contact halves: row k's a side on lane
+      // k, its b side on lane k + 8 (pbd_kernels.hip position_contact_half)
+      r2g &= other.size() <= 8;
       for (size_t i = 0; i < pl.size(); i++) slot1[i] = pl[i];
-      for (size_t i = 0; i < other.size(); i++) slot2[i] = other[i];
+      for (size_t i = 0; i < other.size(); i++) {
+        slot2[i] = other[i];
+        if (r2g) slot2[i + 8] = other[i];
+      }
     } else {
       for (int l = 0; l < 16; l++) {
         slot1[l] = l < R ? l : -1;

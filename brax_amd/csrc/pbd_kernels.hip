@@ -275,6 +275,11 @@ template <int F> __device__ __forceinline__ bool is_plane(int fn) {
   if constexpr ((F & F_CCO) != 0) return false;
   else if constexpr ((F & F_CC) == 0) return true; else return fn == 0;
 }
+// the F_R2G kernels' two-way slot runs as contact halves (HALF: a row's a
+// side on lane k, its b side on lane k + 8; the host places them so)
+template <int F> __device__ __forceinline__ constexpr bool HALF() {
+  return (F & F_CCO) != 0 && (F & F_R2G) != 0;
+}
 template <int F> __device__ __forceinline__ bool is_oneway(int ow) {
   if constexpr ((F & F_CCO) != 0) return false;
   else if constexpr ((F & F_TW) == 0) return true; else return ow != 0;
@@ -1406,6 +1411,101 @@ __device__ __forceinline__ v3 xh3(v3 v) { return mk(xh(v.x), xh(v.y), xh(v.z)); 
 __device__ __forceinline__ v3 sel3(bool s, v3 a, v3 b) {
   return mk(s ? a.x : b.x, s ? a.y : b.y, s ? a.z : b.z);
 }
+
+// Contact halves (SINGLE mode, F_R2G's two-way capsule-capsule slot): row k's
+// a side on lane k, its b side on lane k + 8 of the env's 16 (partner xh,
+// lane ^ 8). Both lanes hold the row's contact (contact_gen of the same words:
+// the same bits); each forms its own body's terms of TwoWay._position_contact
+// / _velocity_contact and trades them with the partner, so the shared values
+// (the effective-mass sums, the rest-pose drift, the relative velocities)
+// come out as the one-lane functions above form them, bit for bit, and each
+// lane returns only its own side's impulse. The two lanes run at once where
+// one lane ran both sides in turn.
+__device__ __forceinline__ float pick_a(bool sb, float own, float other) { return sb ? other : own; }
+__device__ __forceinline__ float pick_b(bool sb, float own, float other) { return sb ? own : other; }
+
+template <int F>
+__device__ __forceinline__ float position_contact_half(const RowC& R, const QP& o, const v3& oo_pos,
+                                                       const q4& oo_rot, v3 cpos, v3 n, float cpen,
+                                                       bool sb, v3& op, q4& orr) {
+  BX_IEEE_IN_CONTACT
+  const float sc = R.scale;
+  const float m = sb ? R.mb : R.ma;
+  const v3 I = sb ? R.Ib : R.Ia;
+  const v3 hn = n * cpen / 2.f;
+  const v3 pq = (sb ? cpos + hn : cpos - hn) - o.pos;  // a: pp, b: pc
+  const float c = -cpen;
+  v3 cr = cross(pq, n);
+  float w = 1.f / m + dot(cr, mul(I, cr));
+  float wp = xh(w);
+  const float dl = -c / (pick_a(sb, w, wp) + pick_b(sb, w, wp) + 1e-6f);
+  const float cm = c < 0.f ? 1.f : 0.f;
+  const v3 pv = dl * n * cm;
+  const v3 l0 = cross(pq, pv);  // a: la, b: lb
+  const v3 r = rotate(cpos - o.pos, quat_inv(o.rot));
+  const v3 pbar = oo_pos + rotate(r, oo_rot);
+  const v3 pbp = xh3(pbar);
+  const v3 p1bar = sel3(sb, pbp, pbar), p2bar = sel3(sb, pbar, pbp);
+  const v3 dp = (cpos - p1bar) - (cpos - p2bar);
+  const v3 dt = dp - dot(dp, n) * n;
+  const v3 pr = cpos - o.pos;  // a: pp, b: pc (the friction lever)
+  const float c2 = cancel_norm(dt);
+  const v3 n2 = dt / (c2 + 1e-6f);
+  cr = cross(pr, n2);
+  w = 1.f / m + dot(cr, mul(I, cr));
+  wp = xh(w);
+  const float dlt = -c2 / (pick_a(sb, w, wp) + pick_b(sb, w, wp));
+  const float sm = fabsf(dlt) < fabsf(dl) ? 1.f : 0.f;
+  const v3 pt = dlt * n2 * sm * cm;
+  const v3 ps = pv + pt;
+  op = sb ? sc * (-ps / m) : sc * (ps / m);
+  orr = sb ? sc * (-0.5f * vec_quat_mul(mul(I, l0 + cross(pr, pt)), o.rot))
+           : sc * (0.5f * vec_quat_mul(mul(I, l0 + cross(pr, pt)), o.rot));
+  return dl;
+}
+
+template <int F>
+__device__ __forceinline__ void velocity_contact_half(const RowC& R, float h, const QP& o, v3 oop, v3 oov,
+                                                      v3 ooa, v3 cpos, v3 n, float cpen, float dlam,
+                                                      bool sb, v3& ov, v3& oa) {
+  BX_IEEE_IN_CONTACT
+  const float m = sb ? R.mb : R.ma;
+  const v3 I = sb ? R.Ib : R.Ia;
+  const v3 ro = cpos - o.pos;  // a: ra, b: rb
+  const v3 t = o.vel + cross(o.ang, ro);
+  const v3 tp = xh3(t);
+  const v3 rv = sel3(sb, tp, t) - sel3(sb, t, tp);
+  float vn = dot(rv, n);
+  v3 vt = rv - n * vn;
+  float vtn = cancel_norm(vt);
+  v3 vtd = vt / (1e-6f + vtn);
+  float lim = R.fric * fabsf(dlam) / (2.f * h);
+  float mag = fminf(lim, vtn);
+  v3 dvel = -vtd * mag;
+  const v3 a1 = cross(ro, vtd);
+  float w = 1.f / m + dot(a1, mul(I, a1));
+  float wp = xh(w);
+  const v3 pdyn = dvel / (pick_a(sb, w, wp) + pick_b(sb, w, wp) + 1e-6f);
+  const v3 to = oov + cross(ooa, cpos - oop);
+  const v3 top = xh3(to);
+  const v3 rvo = sel3(sb, top, to) - sel3(sb, to, top);
+  float vno = dot(rvo, n);
+  float mn = fminf(R.elas * vno, 0.f);
+  v3 dvr = n * (-vn - mn);
+  const v3 pq = (sb ? cpos + n * cpen : cpos) - o.pos;  // a: pp, b: pc
+  float c = cancel_norm(dvr);
+  v3 n2 = dvr / (c + 1e-6f);
+  const v3 cr = cross(pq, n2);
+  w = 1.f / m + dot(cr, mul(I, cr));
+  wp = xh(w);
+  const float dlr = c / (pick_a(sb, w, wp) + pick_b(sb, w, wp) + 1e-6f);
+  float smk = cpen > 0.f ? 1.f : 0.f;
+  float sink = vno <= 0.f ? 1.f : 0.f;
+  v3 pv = (dlr * n2 * sink + pdyn) * smk;
+  ov = sb ? -pv / m : pv / m;
+  oa = cross(mul(I, ro), sb ? -pv : pv);
+}
+
 
 
 // Revolute.apply_reduced (joints.py:79-100, 154-195, 270-309), one side: o is
@@ -3015,6 +3115,31 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
       } else {
         contact_gen<FS>(R, a, b, cpos, cvel, cn, pen);
       }
+      if constexpr (HALF<FS>()) {
+        // contact halves: this lane's side only (a on lanes 0-7, b on 8-15)
+        const bool sb = (lane & 8) != 0;
+        v3 pop, op = z3;
+        q4 por, orr = z4;
+        float unused;
+        ld_slot(E.prev + (sb ? R.b : R.a) * PREV_STRIDE, pop, por, unused);
+        if (is_nan(pen)) {
+          const float pz = nan_of(pen);
+          op = mk(pz, pz, pz);
+          orr = q4{pz, pz, pz, pz};
+          dl = pz;
+        } else if (pen > 0.f) {
+          dl = position_contact_half<FS>(R, sb ? b : a, pop, por, cpos, cn, pen, sb, op, orr);
+        } else {
+          dl = 0.f;
+        }
+        if (!sb) {
+          float* rd = E.rowd + r * ROWD_STRIDE;
+          st4a(rd, f32x4{cpos.x, cpos.y, cpos.z, cn.x});
+          st4a(rd + 4, f32x4{cn.y, cn.z, pen, dl});
+        }
+        st_slot(E.cslot + (sb ? E.nR + r : r) * SLOT_STRIDE, op, orr, nonzero3(op));
+        return;
+      }
       v3 pap, pbp;
       q4 par, pbr;
       float unused;
@@ -3063,6 +3188,20 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
     BX_STAMP(5);
     auto vel_pass = [&](auto fc, const RowC& R, int r, v3 cpos, v3 cn, float pen, float dl) {
       constexpr int FS = decltype(fc)::value;
+      if constexpr (HALF<FS>()) {
+        const bool sb = (lane & 8) != 0;
+        const QP o = ldqp(E.qp + (sb ? R.b : R.a) * QP_STRIDE);
+        v3 rop, rov, roa, ov = z3, oa = z3;
+        ld_rb(E.rb + (sb ? R.b : R.a) * RB_STRIDE, rop, rov, roa);
+        if (is_nan(pen)) {
+          const float pz = nan_of(pen);
+          ov = oa = mk(pz, pz, pz);
+        } else if (pen > 0.f) {
+          velocity_contact_half<FS>(R, h, o, rop, rov, roa, cpos, cn, pen, dl, sb, ov, oa);
+        }
+        st_slot(E.cslot + (sb ? E.nR + r : r) * SLOT_STRIDE, ov, q4{oa.x, oa.y, oa.z, 0.f}, nonzero3(ov));
+        return;
+      }
       QP a = ldqp(E.qp + R.a * QP_STRIDE), b = ldqp(E.qp + R.b * QP_STRIDE);
       v3 rap, rav, raa, rbp, rbv, rba;
       ld_rb(E.rb + R.a * RB_STRIDE, rap, rav, raa);
@@ -4543,7 +4682,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   }
   // and the env's done / steps and the first action chunk (one element per
   // lane), likewise from the arguments alone
-  float ed = 0.f, est = 0.f, ea0 = 0.f;
+  float ed = 0.f, est = 0.f, ea0 = 0.f, ea1 = 0.f;
   if constexpr (EARLY) {
     const int ln = (int)(threadIdx.x % L);
     const int64_t ee = (int64_t)blockIdx.x * (blockDim.x / L) + threadIdx.x / L;
@@ -4551,7 +4690,13 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     ed = A.in.done[eel];
     if (A.in.steps) est = A.in.steps[eel];
     const int aw0 = (int)A.act_width;
-    if (!A.draw && aw0 > 0 && ln < (L < 64 ? L : 64)) ea0 = A.act[eel * A.act_stride + (ln < aw0 ? ln : aw0 - 1)];
+    constexpr int C0 = L < 64 ? L : 64;
+    if (!A.draw && aw0 > 0 && ln < C0) {
+      const float* ar = A.act + eel * A.act_stride;
+      ea0 = ar[ln < aw0 ? ln : aw0 - 1];
+      // (the second chunk too: Humanoid's 17-wide row)
+      if (aw0 > C0) ea1 = ar[C0 + ln < aw0 ? C0 + ln : aw0 - 1];
+    }
   }
   BlobHdr H = ONE ? A.hdr : *reinterpret_cast<const BlobHdr*>(A.blob);
   Cst c{A.blob};
@@ -4692,7 +4837,8 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   for (int i0 = 0; i0 < aw; i0 += C) {
     const int i = i0 + lane;
     float v = a0;
-    if (i0 > 0 && lane < C) v = drw ? draw_at(t, i < aw ? i : aw - 1) : arow_g[i < aw ? i : aw - 1];
+    if (i0 > 0 && lane < C)
+      v = drw ? draw_at(t, i < aw ? i : aw - 1) : ((EARLY && i0 == C) ? ea1 : arow_g[i < aw ? i : aw - 1]);
     if (i >= aw || !valid) v = 0.f;
     if (drw && A.act_out && valid && lane < C && i < aw) A.act_out[((int64_t)t * A.n_envs + e) * aw + i] = v;
     if constexpr (EK == EK_ANT && L == 16) {
