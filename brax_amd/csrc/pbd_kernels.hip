@@ -5676,7 +5676,16 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
   // HumanoidStandup: the Humanoid system lying down, 22 ground rows (F_R2)
   if (fold && L == 16 && (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP) &&
       feat == (F_SPH | F_G1 | F_R2)) {
-    launch_one<EnvArgs>(env_step_kernel<16, 1, F_SPH | F_G1 | F_R2, 8, EK_HUM>, grid, tpb, lds, s, a);
+    if (a.packed && a.n_steps <= 1)
+      launch_one<EnvArgs>(env_step_packed_kernel<16, 1, F_SPH | F_G1 | F_R2, 8, EK_HUM>, grid, tpb, lds, s, a);
+    else
+      launch_one<EnvArgs>(env_step_kernel<16, 1, F_SPH | F_G1 | F_R2, 8, EK_HUM>, grid, tpb, lds, s, a);
+    return hipGetLastError();
+  }
+  // every other env's Env.step (one packed step): the one-step kernels, whose
+  // first loads need no header
+  if (a.packed && a.n_steps <= 1) {
+    BX_DISPATCH_SINGLE(env_step_packed_kernel, EnvArgs)
     return hipGetLastError();
   }
   BX_DISPATCH_SINGLE(env_step_kernel, EnvArgs)
