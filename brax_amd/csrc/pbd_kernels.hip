@@ -2915,7 +2915,8 @@ __device__ void pbd_step_single(const Cst& c, const BlobHdr& H, const Env& E, in
   // writes of equal values; one writing copy per body measured slower).
   // Bodies on no joint side are frozen (checked on the host) and keep their
   // loaded record
-  constexpr bool JB = FOLD && JH;
+  // (no body copies with 16-entry contact lists: Pusher folds only)
+  constexpr bool JB = FOLD && JH && (F & F_C16) == 0;
   const int bi = JB ? X.S.body : lane;  // the lane's body
   float* myqp = E.qp + bi * QP_STRIDE;
   QP q;
@@ -4070,12 +4071,13 @@ __device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3
 // env-program specialisation: the hot env kinds get step kernels holding
 // only their own env code (EK_ANT, EK_HUM: Humanoid and HumanoidStandup,
 // EK_CHEETAH: HalfCheetah); EK_ANY carries every kind, chosen at run time
-enum { EK_ANY = 0, EK_ANT = 1, EK_HUM = 2, EK_CHEETAH = 3 };
+// (EK_PUSHER: Pusher, round 6: its 50 substeps with the damping folded)
+enum { EK_ANY = 0, EK_ANT = 1, EK_HUM = 2, EK_CHEETAH = 3, EK_PUSHER = 4 };
 template <int EK>
 __device__ __forceinline__ constexpr bool ek_has(int k) {
   return EK == EK_ANY || (EK == EK_ANT && k == BX_ENV_ANT) ||
          (EK == EK_HUM && (k == BX_ENV_HUMANOID || k == BX_ENV_HUMANOID_STANDUP)) ||
-         (EK == EK_CHEETAH && k == BX_ENV_HALFCHEETAH);
+         (EK == EK_CHEETAH && k == BX_ENV_HALFCHEETAH) || (EK == EK_PUSHER && k == BX_ENV_PUSHER);
 }
 #define KIND_IS(k) (ek_has<EK>(k) && kind == (k))
 
@@ -4717,7 +4719,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   // JB: the env-program kernels with joint halves (pbd_step_single's FOLD && JH)
   if constexpr (S && ONE)
     load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>(),
-               (F & F_JH) != 0 && EK != EK_ANY>(A.lane_img, H, lane, X);
+               (F & F_JH) != 0 && EK != EK_ANY && (F & F_C16) == 0>(A.lane_img, H, lane, X);
   Env E = carve(ebase + le * H.env_words, H);
   zero_slots(E, H, lane);
   BX_PSTAMP(5);
@@ -4727,7 +4729,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
   const int64_t el = valid ? e : 0;
   if constexpr (S && !ONE)
     load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>(),
-               (F & F_JH) != 0 && EK != EK_ANY>(A.blob + H.o_lane, H, lane, X);
+               (F & F_JH) != 0 && EK != EK_ANY && (F & F_C16) == 0>(A.blob + H.o_lane, H, lane, X);
   if constexpr (S) stage_lim<L, F>(ONE ? A.lane_img : A.blob + H.o_lane, H, E, lane);
   BX_PSTAMP(6);
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
@@ -4951,7 +4953,7 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     // (its launch requires fold), so its observation takes the lane's
     // hoisted body, joint and actuator
     // (JB: the lane's hoisted body is its joint side's, not body lane)
-    constexpr bool JBK = S && (F & F_JH) != 0 && EK != EK_ANY;
+    constexpr bool JBK = S && (F & F_JH) != 0 && EK != EK_ANY && (F & F_C16) == 0;
     env_observe<L, EK>(c, H, E, lane, kind, P.obs_flags, P.obs_size, act, aw,
                    valid ? O.obs + e * P.obs_size : nullptr, P.coef, S ? &X.J : nullptr,
                    (S && !JBK) ? &X.B : nullptr, (S && EK == EK_HUM) ? &X.A : nullptr);
@@ -5671,6 +5673,22 @@ hipError_t launch_env_step_single(int L, int feat, int gw, int tpb, int64_t n_en
       launch_one<EnvArgs>(env_step_packed_kernel<16, 1, F_CHEETAH, 4, EK_CHEETAH>, grid, tpb, lds, s, a);
     else
       launch_one<EnvArgs>(env_step_kernel<16, 1, F_CHEETAH, 4, EK_CHEETAH>, grid, tpb, lds, s, a);
+    return hipGetLastError();
+  }
+  // Pusher: 16 one-way plane rows in slot 1, 7 two-way capsule-capsule rows
+  // as contact halves in slot 2, 16-entry contact lists, joint halves, the
+  // damping folded (no body copies: F_C16)
+  constexpr int F_PUSHER = F_CC | F_TW | F_JH | F_R2 | F_C16 | F_R2G;
+  if (fold && L == 16 && k == BX_ENV_PUSHER && (feat & ~F_G1) == F_PUSHER) {
+#define BX_PUSHER_LAUNCH(MW)                                                                        \
+    if (a.n_steps > 1)                                                                              \
+      launch_one<EnvArgs>(env_rollout_kernel<16, 1, F_PUSHER, MW, EK_PUSHER>, grid, tpb, lds, s, a); \
+    else if (a.packed)                                                                              \
+      launch_one<EnvArgs>(env_step_packed_kernel<16, 1, F_PUSHER, MW, EK_PUSHER>, grid, tpb, lds, s, a); \
+    else                                                                                            \
+      launch_one<EnvArgs>(env_step_kernel<16, 1, F_PUSHER, MW, EK_PUSHER>, grid, tpb, lds, s, a);
+    if (gw <= 4) { BX_PUSHER_LAUNCH(4) } else { BX_PUSHER_LAUNCH(8) }
+#undef BX_PUSHER_LAUNCH
     return hipGetLastError();
   }
   // HumanoidStandup: the Humanoid system lying down, 22 ground rows (F_R2)
