@@ -187,12 +187,26 @@ def main():
                         ('wait_inst_lds_frac', 'SQ_WAIT_INST_LDS')):
         if ctr in c:
           stats[k]['sq'][name] = c[ctr]['mean'] / wc
+  # the MULTI kernel's bench launches mix four modes (Info on / off x cutoff
+  # 0 / 36): its per-mode record (tools/multi_modes_prof.sh), when present,
+  # keyed beside the mixed average
+  mm = None
+  mp = os.path.join(prof, f'{tag}_multi_modes.json')
+  if os.path.exists(mp):
+    with open(mp) as f:
+      mm = json.load(f)
+    for k in stats:
+      if 'system_step_multi_kernel' in k:
+        stats[k]['note'] = ('averages the bench\'s four MULTI modes; per mode: '
+                            f'profiles/{tag}_multi_modes.json (multi_modes below)')
   with open(os.path.join(prof, 'rocprof_latest.json'), 'w') as f:
     sys.path.insert(0, ROOT)
     from bench import src_sha1
-    json.dump({'round': tag, 'source': f'profiles/{tag}_kernel_stats.csv', 'lib_sha1': sha,
-               'src_sha1': src_sha1(),
-               'kernels': stats}, f, indent=1)
+    out = {'round': tag, 'source': f'profiles/{tag}_kernel_stats.csv', 'lib_sha1': sha,
+           'src_sha1': src_sha1(), 'kernels': stats}
+    if mm is not None:
+      out['multi_modes'] = mm
+    json.dump(out, f, indent=1)
   print(json.dumps(traffic, indent=1))
 
 
