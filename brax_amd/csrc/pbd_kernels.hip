@@ -4041,8 +4041,11 @@ __device__ __forceinline__ float euler_y(const float* q) {
 // which leaves acc and m unchanged. (Not the lanes' hoisted masses through
 // readlane: the call sits in a lane-0 branch, where a spilled mass is
 // restored for the active lanes only.)
+// lmass (the SINGLE kernels at 16 lanes): the bodies' masses staged in LDS
+// once per launch (E.red + 16, from the lanes' hoisted records: the same
+// bits), read there instead of from the blob
 __device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3& com, float& msum,
-                             bool n16 = false) {
+                             bool n16 = false, const float* lmass = nullptr) {
   v3 acc = mk(0.f, 0.f, 0.f);
   float m = 0.f;
   if (n16) {
@@ -4050,7 +4053,7 @@ __device__ void humanoid_com(const Cst& c, const BlobHdr& H, const float* qp, v3
     for (int b = 0; b < 16; b++) {
       const bool in = b < H.N - 1;
       const int bb = in ? b : 0;
-      const float w = in ? c.f(H.o_body + bb * BODY_STRIDE + BODY_MASS) : 0.f;
+      const float w = in ? (lmass ? lmass[bb] : c.f(H.o_body + bb * BODY_STRIDE + BODY_MASS)) : 0.f;
       acc = acc + w * ld3(qp + bb * QP_STRIDE);
       m += w;
     }
@@ -4363,15 +4366,34 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
                             int flags, int obs_size, const float* act, int aw, float* obs_out,
                             const float* coef, const JointC* hj = nullptr,
                             const BodyC* hbody = nullptr, const ActC* hact = nullptr) {
+#if defined(BX_OSTAMPS) && defined(BX_TU_FAST)
+  // (diagnostic: the observation's parts into stamp slots 5..9)
+  unsigned long long ost_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ost_last)::"memory");
+#define BX_OST(k)                                                                  \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long _t;                                                         \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");     \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    if (threadIdx.x == 0) bx_stamp_wave[blockIdx.x & 4095][k] += _t - ost_last;    \
+    ost_last = _t;                                                                 \
+  } while (0)
+#else
+#define BX_OST(k) do {} while (0)
+#endif
   joint_angles<L>(c, H, E, lane, hj);
+  BX_OST(0);
   if ((KIND_IS(BX_ENV_HUMANOID) || KIND_IS(BX_ENV_HUMANOID_STANDUP)) && lane == 0) {
     v3 com;
     float msum;
-    humanoid_com(c, H, E.qp, com, msum, L == 16 && hbody != nullptr);
+    humanoid_com(c, H, E.qp, com, msum, L == 16 && hbody != nullptr,
+                 L == 16 && hbody != nullptr ? E.red + 16 : nullptr);
     st3(E.red + 32, com);
     E.red[35] = msum;
   }
   esync<L>();
+  BX_OST(1);
   if (!obs_out) return;
   if constexpr (EK == EK_ANT) {
     // the Ant observation (ant.py:257-282) written lane by lane without the
@@ -4422,6 +4444,7 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
     const int base = x + 11 + 2 * D;
     const v3 com = ld3(E.red + 32);
     const float msum = E.red[35];
+    BX_OST(2);
     for (int b = lane; b < M; b += L) {
       // SINGLE mode: body b is the lane's, its constants hoisted (hbody)
       const int ob = H.o_body + b * BODY_STRIDE;
@@ -4453,6 +4476,7 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
       oa[1] = cr.y / den;
       oa[2] = cr.z / den;
     }
+    BX_OST(3);
     // qfrc_actuator: unmasked take (index -1 clips to 0), times strength
     const bool ha = lane < H.K;
     ActC A{};
@@ -4477,7 +4501,10 @@ __device__ void env_observe(const Cst& c, const BlobHdr& H, const Env& E, int la
     // constant indices into A.idx (a dynamic one would put A on the stack)
 #pragma unroll
     for (int i = 0; i < 3; i++)
-      if (i < dof) oq[i] = (act ? act[take_idx(A.idx[i], aw)] : 0.f) * A.strength;
+      // (the row as staged in LDS for the physics: the same words, no second
+      // read of the action row from HBM)
+      if (i < dof) oq[i] = (act ? E.arow[take_idx(A.idx[i], aw)] : 0.f) * A.strength;
+    BX_OST(4);
     return;
   }
   for (int i = lane; i < obs_size; i += L)
@@ -4731,6 +4758,10 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     load_hoist<M, (F & F_JH) != 0, (F & F_R2) != 0, cl_width<F, M>(),
                (F & F_JH) != 0 && EK != EK_ANY && (F & F_C16) == 0>(A.blob + H.o_lane, H, lane, X);
   if constexpr (S) stage_lim<L, F>(ONE ? A.lane_img : A.blob + H.o_lane, H, E, lane);
+  // the bodies' masses for humanoid_com (its lmass): lane b's hoisted body b
+  // (the SINGLE kernels without body copies), into E.red + 16 once per launch
+  if constexpr (S && L == 16 && !((F & F_JH) != 0 && EK != EK_ANY && (F & F_C16) == 0))
+    E.red[16 + lane] = X.B.mass;
   BX_PSTAMP(6);
   // AutoResetWrapper.step: steps zeroed where the incoming done is set; done := 0
   float done_in = EARLY ? ed : A.in.done[el];
@@ -4874,7 +4905,8 @@ __device__ __forceinline__ void env_step_body(const EnvArgs& A) {
     v3 com0 = mk(0.f, 0.f, 0.f);
     float msum = 0.f;
     if (KIND_IS(BX_ENV_HUMANOID) || KIND_IS(BX_ENV_SWIMMER))
-      humanoid_com(c, H, E.qp, com0, msum, S && EK == EK_HUM && (F & F_JH) == 0);
+      humanoid_com(c, H, E.qp, com0, msum, S && EK == EK_HUM && (F & F_JH) == 0,
+                   S && L == 16 && EK == EK_HUM && (F & F_JH) == 0 ? E.red + 16 : nullptr);
     // the target envs' torso before the step (red words 36..38)
     if ((KIND_IS(BX_ENV_UR5E) || KIND_IS(BX_ENV_FETCH)) && lane == 0)
       st3(E.red + 36, ld3(E.qp + (int)P.coef[0] * QP_STRIDE));

@@ -39,3 +39,9 @@ print('samples', n, 'cycles/wave/step', tot)
 for k, nm in names.items():
   if v[k]:
     print(f'{nm:28s} {100 * v[k] / tot:5.1f}%  {v[k]:9.0f} cyc')
+# a -DBX_OSTAMPS build: the observation's parts (slots 0..4, inside slot 12)
+sub = {0: 'obs: joint angles', 1: 'obs: centre of mass + sync', 2: 'obs: torso / joint words',
+       3: 'obs: per-body loop', 4: 'obs: actuator words'}
+for k, nm in sub.items():
+  if buf[k]:
+    print(f'  {nm:26s} {buf[k] / n:9.0f} cyc')
